@@ -1,0 +1,346 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident batched CRC32C over sstable blocks on MI355X.
+
+Metric (BASELINE.json): "GiB/s CRC32C over batched 4 KiB sstable blocks (device-resident);
+% HBM peak".  Default workload = BASELINE configs[1]: 1,048,576 x 4 KiB synthetic blocks
+(splitmix64 seed 301), one GPU.  One *step* = one batch CRC over every block of the rank's
+shard (one kernel launch through the C-ABI, pdb_crc32c_batch_device_fixed).
+
+Multi-GPU (torchrun, one process per GPU): every rank owns an independent shard of the same
+per-GPU size (weak scaling).  RCCL is used only to scatter each rank's block-range index from
+rank 0 and, outside the timed region, to gather a checksum-of-checksums.  No data-path
+collective: blocks are independent.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+GIB = float(1 << 30)
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+METRIC = "GiB/s CRC32C over batched 4 KiB sstable blocks (device-resident); % HBM peak"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "sstable"])
+    ap.add_argument("--nblk", type=int, default=1 << 20, help="blocks per GPU (c2/sstable)")
+    ap.add_argument("--c3-bytes", type=int, default=16 << 30, help="bytes per GPU for c3 (Zipf)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-copy-inclusive", action="store_true")
+    ap.add_argument("--diag", action="store_true", help="also time the read-stream calibration kernels")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    return ap.parse_args()
+
+
+def zipf_kib_sizes(n: int, seed: int, kmax: int = 64) -> np.ndarray:
+    rng = np.random.Generator(np.random.PCG64(seed))
+    k = np.arange(1, kmax + 1)
+    p = (1.0 / k) / np.sum(1.0 / k)
+    return (rng.choice(k, size=n, p=p) * 1024).astype(np.int64)
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from pebblesdb_amd import crc32c
+    from pebblesdb_amd.shard import block_range
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    distributed = world > 1
+    if distributed:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    crc32c.init_device(local)
+    dev = torch.device("cuda", local)
+    stream = torch.cuda.current_stream()
+
+    # ---- the rank's shard index: scattered from rank 0 over RCCL (the only collective) -------
+    if args.workload == "c3":
+        n_total = 0
+    else:
+        n_total = args.nblk * world
+    idx = torch.zeros(world, 2, dtype=torch.int64, device=dev)
+    if rank == 0:
+        for r in range(world):
+            lo, hi = block_range(n_total, world, r) if args.workload != "c3" else (r, r + 1)
+            idx[r, 0], idx[r, 1] = lo, hi
+    if distributed:
+        dist.broadcast(idx, src=0)
+    lo, hi = int(idx[rank, 0]), int(idx[rank, 1])
+
+    # ---- synthetic, device-resident input ---------------------------------------------------
+    if args.workload == "c2":
+        L = stride = 4096
+        nblk = hi - lo
+        data = torch.empty(nblk * stride, dtype=torch.uint8, device=dev)
+        crc32c.fill_splitmix(data, 301, byte_offset=lo * stride)
+        algo_bytes_per_blk = L + 4  # L read + 4 B CRC written
+        hashed = nblk * L
+        out = torch.empty(nblk, dtype=torch.int32, device=dev)
+
+        def step():
+            crc32c.batch_fixed(data, stride, L, nblk, out=out)
+
+        workload = {"workload": "c2: 1M x 4 KiB blocks per GPU, stride 4096, device-resident",
+                    "block_bytes": L, "blocks_per_gpu": nblk, "bytes_per_gpu": hashed}
+    elif args.workload == "sstable":
+        # sstable layout: contents 4096 B + type byte under the CRC, trailer 5 B -> stride 4101
+        L, stride = 4097, 4101
+        nblk = hi - lo
+        data = torch.empty(nblk * stride, dtype=torch.uint8, device=dev)
+        crc32c.fill_splitmix(data, 301, byte_offset=lo * stride)
+        algo_bytes_per_blk = L + 4
+        hashed = nblk * L
+        out = torch.empty(nblk, dtype=torch.int32, device=dev)
+
+        def step():
+            crc32c.batch_fixed(data, stride, L, nblk, out=out)
+
+        workload = {"workload": "sstable layout: 4096 B contents + type byte, stride 4101 (unaligned)",
+                    "block_bytes": L, "blocks_per_gpu": nblk, "bytes_per_gpu": hashed}
+    else:
+        # c3: Zipf 1..64 KiB blocks packed back to back, args.c3_bytes per GPU
+        sizes = zipf_kib_sizes(int(args.c3_bytes / (13.5 * 1024) * 1.1) + 16, 301 + rank)
+        cs = np.cumsum(sizes)
+        n = int(np.searchsorted(cs, args.c3_bytes, side="right"))
+        sizes = sizes[:n]
+        offs = np.concatenate([[0], np.cumsum(sizes)[:-1]])
+        total = int(sizes.sum())
+        data = torch.empty(total, dtype=torch.uint8, device=dev)
+        crc32c.fill_splitmix(data, 303 + rank)
+        d_blk = crc32c.blocks_to_device(crc32c.make_blocks(offs, sizes), dev)
+        nblk = n
+        algo_bytes_per_blk = None
+        hashed = total
+        out = torch.empty(nblk, dtype=torch.int32, device=dev)
+
+        def step():
+            crc32c.batch(data, d_blk, out=out)
+
+        workload = {"workload": "c3: Zipf 1-64 KiB blocks, packed, descriptor list",
+                    "blocks_per_gpu": nblk, "bytes_per_gpu": hashed}
+    algo_bytes = hashed + 4 * nblk + (16 * nblk if args.workload == "c3" else 0)
+
+    # ---- warmup + timed region -------------------------------------------------------------
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for s, e in ev:
+        s.record(stream)
+        step()
+        e.record(stream)
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    kern_ms = [s.elapsed_time(e) for s, e in ev]
+    kern_avg_ms = float(np.mean(kern_ms))
+
+    t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    if distributed:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall_max = float(t.item())
+
+    # checksum of checksums (outside the timed region) gathered to rank 0
+    xs = torch.tensor([int(np.bitwise_xor.reduce(out.cpu().numpy().view(np.uint32)))], dtype=torch.int64,
+                      device=dev)
+    if distributed:
+        allx = [torch.zeros_like(xs) for _ in range(world)]
+        dist.all_gather(allx, xs)
+        xor_all = 0
+        for v in allx:
+            xor_all ^= int(v.item())
+    else:
+        xor_all = int(xs.item())
+
+    total_bytes = hashed * world * args.steps  # weak scaling: every rank hashes its own shard
+    value = total_bytes / wall_max / GIB
+    ms_per_step = wall_max / args.steps * 1e3
+    achieved_gbs = algo_bytes / (kern_avg_ms * 1e-3) / 1e9
+
+    extra = {}
+    if rank == 0:
+        if args.diag:
+            extra["diag"] = diag(crc32c, torch, dev, data, stream)
+        if not args.no_copy_inclusive and args.workload != "c3":
+            extra["copy_inclusive"] = copy_inclusive(crc32c, data, L, stride, min(nblk, 1 << 18))
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline(data, L, stride, nblk, args, d_blk if args.workload == "c3" else None)
+
+    if rank == 0:
+        traffic = pmc_traffic(args.workload)
+        line = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (splitmix64 seed 301, generated on device)",
+            "config": dict(workload, parallelism=f"block-range shards x{world}"),
+            "hbm_frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved_gbs, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "kernel": "crc_fixed_kernel<true>" if args.workload == "c2" else
+                          ("crc_fixed_kernel<false>" if args.workload == "sstable" else "crc_desc_kernel<0>"),
+                "algorithmic_bytes_per_launch": algo_bytes,
+                "kernel_avg_ms": round(kern_avg_ms, 4),
+                "kernel_min_ms": round(float(np.min(kern_ms)), 4),
+            },
+            "cpu_baseline": cpu,
+            "xor_of_crcs": f"{xor_all:08x}",
+        }
+        line.update(extra)
+        print(json.dumps(line), flush=True)
+    if distributed:
+        dist.destroy_process_group()
+
+
+def diag(crc32c, torch, dev, data, stream):
+    """Achievable read bandwidth on this box: a coalesced 16-B/lane stream and the exact load
+    pattern of the 4-KiB fast path with no CRC work."""
+    from pebblesdb_amd._native import check, lib
+
+    nbytes = data.numel()
+    o = torch.zeros(1, dtype=torch.int32, device=dev)
+    res = {}
+    for name, fn in (
+        ("read_stream", lambda: check(lib().pdb_diag_read_stream(data.data_ptr(), nbytes, o.data_ptr(), stream.cuda_stream))),
+        ("read_pattern4k", lambda: check(lib().pdb_diag_read_pattern4k(data.data_ptr(), nbytes // 4096, o.data_ptr(), stream.cuda_stream))),
+    ):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record(stream)
+        for _ in range(10):
+            fn()
+        e.record(stream)
+        torch.cuda.synchronize()
+        ms = s.elapsed_time(e) / 10
+        res[name] = {"GB/s": round(nbytes / (ms * 1e-3) / 1e9, 1), "ms": round(ms, 4)}
+    return res
+
+
+def copy_inclusive(crc32c, data, L, stride, nblk):
+    """Host-resident blocks -> pdb_crc32c_batch_host (H2D + kernel + D2H), pageable memory."""
+    host = data[: nblk * stride].cpu().numpy()
+    blk = crc32c.make_blocks(np.arange(nblk) * stride, np.full(nblk, L))
+    crc32c.batch_host(host, blk)  # warm (workspace growth)
+    reps = 3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        crc32c.batch_host(host, blk)
+    dt = (time.perf_counter() - t0) / reps
+    return {"GiB/s": round(nblk * L / dt / GIB, 3), "blocks": nblk, "host_memory": "pageable",
+            "entry": "pdb_crc32c_batch_host"}
+
+
+def cpu_baseline(data, L, stride, nblk, args, d_blk):
+    """The reference's own CRC32C (oracle/_ref, compiled from src/util/crc32c.cc) on this box's
+    host cores over a bounded sample of the same blocks; falls back to the C restatement
+    (kind "port") only if the reference .so did not travel."""
+    import oracle
+
+    try:
+        lib, kind = oracle.Reference(), "reference"
+    except (FileNotFoundError, OSError):
+        if not os.path.exists(oracle.ORACLE_SO):
+            oracle.build()
+        lib, kind = oracle.Oracle(), "port"
+    threads = args.cpu_threads or min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
+    if d_blk is None:
+        ns = min(nblk, 1 << 18)  # 256 Ki blocks = 1 GiB sample of the same workload
+        host = data[: ns * stride].cpu().numpy()
+        blk = np.zeros(ns, dtype=oracle.BLK_DTYPE)
+        blk["off"] = np.arange(ns) * stride
+        blk["len"] = L
+    else:
+        b = d_blk.cpu().numpy().view(oracle.BLK_DTYPE)
+        end = np.cumsum(b["len"].astype(np.int64))
+        ns = int(np.searchsorted(end, 1 << 30, side="right")) or 1
+        blk = b[:ns].copy()
+        hi = int(blk["off"][-1] + blk["len"][-1])
+        host = data[:hi].cpu().numpy()
+    sample_bytes = int(blk["len"].astype(np.int64).sum())
+    res = {}
+    for nt in sorted({1, threads}):
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            lib.batch(host, blk, flags=0, nthreads=nt)
+            reps += 1
+            dt = time.perf_counter() - t0
+            if dt > (6.0 if nt == 1 else 4.0) or reps >= 50:
+                break
+        res[nt] = sample_bytes * reps / dt / GIB
+    cpu_model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    cpu_model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {
+        "value": round(res[threads], 3),
+        "unit": "GiB/s",
+        "cores": threads,
+        "kind": kind,
+        "sample": f"{ns} blocks ({sample_bytes / GIB:.2f} GiB) of the same workload, repeated ~4-6 s",
+        "single_thread_GiB/s": round(res[1], 3),
+        "cpu_model": cpu_model,
+        "nproc": os.cpu_count(),
+    }
+
+
+def pmc_traffic(workload: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_traffic.py),
+    FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM; None when not collected."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        return d.get(workload, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+if __name__ == "__main__":
+    main()

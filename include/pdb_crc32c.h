@@ -1,0 +1,130 @@
+/*
+ * pdb_crc32c.h -- C-ABI drop-in boundary for PebblesDB's sstable block checksum path,
+ * served by hand-written HIP kernels for MI355X (gfx950).
+ *
+ * Reference interfaces this replaces (paths under utsaslab/pebblesdb src/):
+ *   util/crc32c.h:17      uint32_t crc32c::Extend(uint32_t init_crc, const char* data, size_t n)
+ *   util/crc32c.h:20-22   uint32_t crc32c::Value(const char* data, size_t n)
+ *   util/crc32c.h:29-32   uint32_t crc32c::Mask(uint32_t crc)    (ror32(crc,15) + 0xa282ead8)
+ *   util/crc32c.h:35-40   uint32_t crc32c::Unmask(uint32_t masked)
+ *   util/crc32c.cc:65,99  the file-static crc32c_func pointer = the reference's only swap point
+ *   table/table_builder.cc:187-205  TableBuilder::WriteRawBlock: trailer [type][Mask(crc(contents||type))]
+ *   table/format.cc:66-104          ReadBlock: Unmask(DecodeFixed32(data+n+1)) == Value(data, n+1)
+ *                                   else Status::Corruption("block checksum mismatch")
+ *   table/format.h:87               kBlockTrailerSize = 5
+ *
+ * Conventions
+ *   - Plain C types only; device pointers are `const void*`, streams are `void*` (a hipStream_t;
+ *     NULL = the HIP default stream, as for hipLaunchKernel).  Host entry points use a
+ *     per-device internal stream and return after the results are in host memory.
+ *   - Every batch entry returns 0 or a negative PDB_E* code.  There is NO CPU fallback: with no
+ *     usable device the call fails (PDB_ENODEV) and pdb_last_error() says why.
+ *   - Scalar Extend/Value cannot report errors (the reference contract, util/crc32c.h:17); on a
+ *     device failure they abort() with a message instead of returning a wrong value.
+ *   - Caller owns every buffer.  Device-resident entry points allocate nothing and are
+ *     stream-ordered (capturable into a hipGraph).  Host entry points stage through a cached
+ *     per-device workspace that only grows.
+ *   - Per-block length is < 2^32 bytes (the reference narrows to uint32_t: util/crc32c.cc:19-23,589).
+ *   - Thread-safe: host entry points serialise per device; device entry points are pure launches.
+ */
+#ifndef PDB_CRC32C_H_
+#define PDB_CRC32C_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PDB_CRC32C_ABI_VERSION 1
+
+/* One block of a batch: bytes [base+off, base+off+len), optional Extend seed. 16 bytes. */
+typedef struct pdb_blk {
+  uint64_t off;  /* byte offset from the batch base (any alignment) */
+  uint32_t len;  /* bytes under the CRC */
+  uint32_t init; /* Extend() init crc; used only with PDB_CRC_USE_INIT */
+} pdb_blk;
+
+/* An sstable BlockHandle (table/format.h:22-45): block contents at [offset, offset+size),
+ * followed by the 5-byte trailer [type][masked crc LE32] at offset+size. */
+typedef struct pdb_block_handle {
+  uint64_t offset;
+  uint64_t size;
+} pdb_block_handle;
+
+/* flags */
+#define PDB_CRC_MASK_OUTPUT 0x1u /* out[i] = Mask(crc) (util/crc32c.h:29-32) */
+#define PDB_CRC_USE_INIT 0x2u    /* crc = Extend(blk.init, ...) instead of Value(...) */
+
+/* error codes */
+#define PDB_OK 0
+#define PDB_ENODEV (-1)  /* no HIP device / extension unusable */
+#define PDB_EHIP (-2)    /* HIP runtime error (see pdb_last_error) */
+#define PDB_EINVAL (-3)  /* bad argument */
+#define PDB_ERANGE (-4)  /* a block or buffer exceeds a limit */
+#define PDB_ENOMEM (-5)  /* device workspace allocation failed */
+
+/* ---- library / device ---------------------------------------------------------------------- */
+int pdb_crc32c_abi_version(void);
+/* Create the per-device state: upload the CRC tables, query CU count, create the internal
+ * stream.  Called implicitly by every entry point; explicit calls are idempotent. */
+int pdb_crc32c_init(int device);
+const char* pdb_last_error(void); /* thread-local message of the last failure */
+/* Device the calling thread uses (HIP current device). */
+int pdb_crc32c_current_device(void);
+
+/* ---- scalar, LevelDB-compatible (util/crc32c.h:17-40) ---------------------------------------- */
+uint32_t pdb_crc32c_extend(uint32_t init_crc, const void* data, size_t n); /* host data */
+uint32_t pdb_crc32c_value(const void* data, size_t n);                     /* host data */
+uint32_t pdb_crc32c_mask(uint32_t crc);
+uint32_t pdb_crc32c_unmask(uint32_t masked_crc);
+
+/* ---- device-resident batches (the hot path) ------------------------------------------------ */
+/* Blocks i in [0,nblk): bytes [d_base + i*stride, +len).  Seed `init` applies to every block when
+ * PDB_CRC_USE_INIT is set.  d_out[i] = crc (masked with PDB_CRC_MASK_OUTPUT). */
+int pdb_crc32c_batch_device_fixed(const void* d_base, uint64_t stride, uint32_t len, uint64_t nblk,
+                                  uint32_t flags, uint32_t init, uint32_t* d_out, void* stream);
+/* Blocks from a device-resident descriptor array. */
+int pdb_crc32c_batch_device(const void* d_base, const pdb_blk* d_blk, uint64_t nblk, uint32_t flags,
+                            uint32_t* d_out, void* stream);
+/* Verify: d_ok[i] = (crc_i == expected_i), where expected is masked iff PDB_CRC_MASK_OUTPUT.
+ * *d_nbad (device u32, caller-zeroed) is atomically incremented per mismatch; may be NULL. */
+int pdb_crc32c_verify_device(const void* d_base, const pdb_blk* d_blk, uint64_t nblk, uint32_t flags,
+                             const uint32_t* d_expected, uint8_t* d_ok, uint32_t* d_nbad,
+                             void* stream);
+
+/* ---- host batches (copy-inclusive: H2D + kernel + D2H on the internal stream) --------------- */
+int pdb_crc32c_batch_host(const void* base, uint64_t base_len, const pdb_blk* blk, uint64_t nblk,
+                          uint32_t flags, uint32_t* out);
+
+/* ---- sstable block trailers (table/table_builder.cc:187-205, table/format.cc:66-104) ---------
+ * `buf` holds an sstable image (or any span of one) in which each handle's block is followed by
+ * its trailer at buf[offset+size .. offset+size+5).  The type byte buf[offset+size] is input. */
+/* Seal: write Mask(crc32c(contents||type)) little-endian at buf[offset+size+1]. */
+int pdb_sst_seal_device(void* d_buf, uint64_t buf_len, const pdb_block_handle* d_h, uint64_t n,
+                        void* stream);
+int pdb_sst_seal_host(void* buf, uint64_t buf_len, const pdb_block_handle* h, uint64_t n);
+/* Verify: ok[i] = 1 iff Unmask(DecodeFixed32(trailer+1)) == crc32c(contents||type).
+ * Returns the number of mismatching blocks (>= 0) or a negative error. */
+int64_t pdb_sst_verify_host(const void* buf, uint64_t buf_len, const pdb_block_handle* h, uint64_t n,
+                            uint8_t* ok);
+int pdb_sst_verify_device(const void* d_buf, uint64_t buf_len, const pdb_block_handle* d_h,
+                          uint64_t n, uint8_t* d_ok, uint32_t* d_nbad, void* stream);
+
+/* ---- diagnostics (roofline calibration; not part of the reference interface) ---------------- */
+/* Streams nbytes from d_base with coalesced 16-B loads and XOR-folds them into d_out[0..grid). */
+int pdb_diag_read_stream(const void* d_base, uint64_t nbytes, uint32_t* d_out, void* stream);
+/* Same loads as the 4-KiB fast path (64 B contiguous per lane) with trivial compute. */
+int pdb_diag_read_pattern4k(const void* d_base, uint64_t nblk, uint32_t* d_out, void* stream);
+/* Fill d_dst[0..nbytes) with the splitmix64 synthetic stream (seed, byte_offset). */
+int pdb_fill_splitmix_device(void* d_dst, uint64_t nbytes, uint64_t seed, uint64_t byte_offset,
+                             void* stream);
+/* Launch geometry actually used (for bench reporting): workgroups and threads per workgroup. */
+int pdb_crc32c_launch_geometry(int device, uint32_t* grid, uint32_t* block, uint32_t* lds_bytes);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* PDB_CRC32C_H_ */

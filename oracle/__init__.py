@@ -1,0 +1,144 @@
+"""oracle -- TEST INFRASTRUCTURE ONLY (the checker, never the thing measured or shipped).
+
+ctypes bindings for
+  * ``_build/liboracle.so``  -- the C restatement of the reference CRC32C
+    (oracle/crc32c_oracle.c; cites /root/reference/src/util/crc32c.cc:25-32,585-625)
+  * ``_ref/libpdbref.so``    -- the reference's own util/crc32c.cc compiled in place by
+    oracle/build_ref.sh (only present where /root/reference was available at build time;
+    the .so travels to the GPU box, the reference sources do not)
+plus the numpy twin of the splitmix64 synthetic-data generator.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ORACLE_SO = os.path.join(HERE, "_build", "liboracle.so")
+REF_SO = os.path.join(HERE, "_ref", "libpdbref.so")
+
+BLK_DTYPE = np.dtype([("off", "<u8"), ("len", "<u4"), ("init", "<u4")])  # == pdb_blk / oracle_blk
+
+_u8p = ctypes.c_void_p
+
+
+def build() -> None:
+    """Compile the C restatement (and the reference shim when the reference is present)."""
+    subprocess.check_call([os.path.join(HERE, "build_oracle.sh")])
+    subprocess.check_call([os.path.join(HERE, "build_ref.sh")])
+
+
+def _bind(lib, prefix: str) -> None:
+    lib_ext = getattr(lib, f"{prefix}_crc32c_extend")
+    lib_ext.restype = ctypes.c_uint32
+    lib_ext.argtypes = [ctypes.c_uint32, _u8p, ctypes.c_size_t]
+    for nm in ("mask", "unmask"):
+        f = getattr(lib, f"{prefix}_crc32c_{nm}")
+        f.restype = ctypes.c_uint32
+        f.argtypes = [ctypes.c_uint32]
+    b = getattr(lib, f"{prefix}_crc32c_batch")
+    b.restype = ctypes.c_int
+    b.argtypes = [_u8p, _u8p, ctypes.c_size_t, ctypes.c_uint32, _u8p, ctypes.c_int]
+
+
+class _CrcLib:
+    def __init__(self, path: str, prefix: str):
+        if not os.path.exists(path):
+            raise FileNotFoundError(path)
+        self.path = path
+        self.prefix = prefix
+        self.lib = ctypes.CDLL(path)
+        _bind(self.lib, prefix)
+        self._extend = getattr(self.lib, f"{prefix}_crc32c_extend")
+        self._mask = getattr(self.lib, f"{prefix}_crc32c_mask")
+        self._unmask = getattr(self.lib, f"{prefix}_crc32c_unmask")
+        self._batch = getattr(self.lib, f"{prefix}_crc32c_batch")
+
+    def extend(self, init: int, data) -> int:
+        buf = _as_u8(data)
+        return int(self._extend(init & 0xFFFFFFFF, buf.ctypes.data, buf.size))
+
+    def value(self, data) -> int:
+        return self.extend(0, data)
+
+    def mask(self, c: int) -> int:
+        return int(self._mask(c & 0xFFFFFFFF))
+
+    def unmask(self, c: int) -> int:
+        return int(self._unmask(c & 0xFFFFFFFF))
+
+    def batch(self, base: np.ndarray, blk: np.ndarray, flags: int = 0, nthreads: int = 1) -> np.ndarray:
+        base = _as_u8(base)
+        blk = np.ascontiguousarray(blk, dtype=BLK_DTYPE)
+        out = np.zeros(len(blk), dtype=np.uint32)
+        rc = self._batch(base.ctypes.data, blk.ctypes.data, len(blk), flags, out.ctypes.data, nthreads)
+        if rc != 0:
+            raise RuntimeError(f"{self.prefix} batch rc={rc}")
+        return out
+
+
+class Oracle(_CrcLib):
+    """The C restatement (always available: built from repo sources)."""
+
+    def __init__(self, path: str = ORACLE_SO):
+        super().__init__(path, "oracle")
+        self._bitwise = self.lib.oracle_crc32c_extend_bitwise
+        self._bitwise.restype = ctypes.c_uint32
+        self._bitwise.argtypes = [ctypes.c_uint32, _u8p, ctypes.c_size_t]
+        self._fill = self.lib.oracle_fill_splitmix
+        self._fill.restype = None
+        self._fill.argtypes = [_u8p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64]
+
+    def extend_bitwise(self, init: int, data) -> int:
+        buf = _as_u8(data)
+        return int(self._bitwise(init & 0xFFFFFFFF, buf.ctypes.data, buf.size))
+
+    def fill(self, nbytes: int, seed: int, byte_offset: int = 0) -> np.ndarray:
+        out = np.empty(nbytes, dtype=np.uint8)
+        self._fill(out.ctypes.data, nbytes, seed & 0xFFFFFFFFFFFFFFFF, byte_offset)
+        return out
+
+
+class Reference(_CrcLib):
+    """The reference's own util/crc32c.cc, compiled in place (oracle/_ref)."""
+
+    def __init__(self, path: str = REF_SO):
+        super().__init__(path, "ref")
+
+
+def reference_available() -> bool:
+    return os.path.exists(REF_SO)
+
+
+def _as_u8(data) -> np.ndarray:
+    if isinstance(data, (bytes, bytearray, memoryview)):
+        return np.frombuffer(bytes(data), dtype=np.uint8)
+    a = np.ascontiguousarray(data)
+    if a.dtype != np.uint8:
+        a = a.view(np.uint8).reshape(-1)
+    return a.reshape(-1)
+
+
+_M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def splitmix_bytes(nbytes: int, seed: int, byte_offset: int = 0) -> np.ndarray:
+    """numpy twin of oracle_fill_splitmix / the device fill kernel."""
+    if nbytes == 0:
+        return np.zeros(0, dtype=np.uint8)
+    w0 = byte_offset >> 3
+    w1 = (byte_offset + nbytes + 7) >> 3
+    with np.errstate(over="ignore"):
+        i = np.arange(w0, w1, dtype=np.uint64)
+        z = np.uint64(seed & 0xFFFFFFFFFFFFFFFF) + (i + np.uint64(1)) * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    b = z.astype("<u8").view(np.uint8)
+    s = byte_offset - (w0 << 3)
+    return b[s : s + nbytes].copy()

@@ -1,0 +1,192 @@
+"""LevelDB-compatible CRC32C API over the MI355X kernels.
+
+Mirrors ``leveldb::crc32c`` (reference src/util/crc32c.h:14-40):
+
+    extend(init_crc, data) -> int   # util/crc32c.h:17  (crc of A||data given init_crc = crc(A))
+    value(data) -> int              # util/crc32c.h:20-22
+    mask(crc) / unmask(masked)      # util/crc32c.h:29-40  (ror 15 + 0xa282ead8)
+
+plus the batch entry points the reference lacks (one call per many independent blocks):
+
+    batch_fixed(d_base, stride, length, nblk)     device-resident fixed-stride blocks
+    batch(d_base, d_blocks)                       device-resident descriptor list
+    verify(d_base, d_blocks, d_expected)          device-resident verify (ReadBlock's check)
+    batch_host(base, blocks)                      host buffers, H2D + kernel + D2H
+
+Every checksum comes from the HIP library; nothing here computes a CRC on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _native
+from ._native import PdbError, check, lib
+
+MASK_OUTPUT = 0x1  # PDB_CRC_MASK_OUTPUT
+USE_INIT = 0x2  # PDB_CRC_USE_INIT
+K_MASK_DELTA = 0xA282EAD8  # util/crc32c.h:24
+
+BLK_DTYPE = np.dtype([("off", "<u8"), ("len", "<u4"), ("init", "<u4")])  # == pdb_blk (16 B)
+HANDLE_DTYPE = np.dtype([("offset", "<u8"), ("size", "<u8")])  # == pdb_block_handle
+
+__all__ = [
+    "extend", "value", "mask", "unmask", "batch_fixed", "batch", "verify", "batch_host",
+    "make_blocks", "blocks_to_device", "PdbError", "MASK_OUTPUT", "USE_INIT", "BLK_DTYPE",
+    "HANDLE_DTYPE", "init_device", "launch_geometry", "fill_splitmix",
+]
+
+
+def _buf(data):
+    """(pointer, nbytes, keepalive) for bytes-like / numpy input on the host."""
+    if isinstance(data, (bytes, bytearray)):
+        a = np.frombuffer(bytes(data), dtype=np.uint8)
+    elif isinstance(data, memoryview):
+        a = np.frombuffer(data.tobytes(), dtype=np.uint8)
+    else:
+        a = np.ascontiguousarray(data)
+        if a.dtype != np.uint8:
+            a = a.view(np.uint8)
+        a = a.reshape(-1)
+    return a.ctypes.data, a.size, a
+
+
+def init_device(device: int = -1) -> None:
+    check(lib().pdb_crc32c_init(device))
+
+
+def extend(init_crc: int, data) -> int:
+    """crc32c of A||data where init_crc = crc32c(A)  (util/crc32c.h:17)."""
+    p, n, _keep = _buf(data)
+    if n and lib().pdb_crc32c_init(-1) < 0:  # surface the error instead of the C abort()
+        check(-1)
+    return int(lib().pdb_crc32c_extend(init_crc & 0xFFFFFFFF, p, n))
+
+
+def value(data) -> int:
+    """crc32c of data  (util/crc32c.h:20-22)."""
+    return extend(0, data)
+
+
+def mask(crc: int) -> int:
+    """util/crc32c.h:29-32 (pure integer op, exported by the library)."""
+    return int(lib().pdb_crc32c_mask(crc & 0xFFFFFFFF))
+
+
+def unmask(masked_crc: int) -> int:
+    """util/crc32c.h:35-40."""
+    return int(lib().pdb_crc32c_unmask(masked_crc & 0xFFFFFFFF))
+
+
+def make_blocks(offs, lens, inits=None) -> np.ndarray:
+    """Host descriptor array (pdb_blk layout)."""
+    offs = np.asarray(offs, dtype=np.uint64).reshape(-1)
+    lens = np.asarray(lens, dtype=np.uint64).reshape(-1)
+    if offs.shape != lens.shape:
+        raise ValueError("offs/lens shape mismatch")
+    if lens.size and int(lens.max()) > 0xFFFFFFFF:
+        raise ValueError("per-block length must be < 4 GiB (util/crc32c.cc:589 narrows to uint32)")
+    b = np.zeros(offs.size, dtype=BLK_DTYPE)
+    b["off"] = offs
+    b["len"] = lens
+    if inits is not None:
+        b["init"] = np.asarray(inits, dtype=np.uint64).reshape(-1) & 0xFFFFFFFF
+    return b
+
+
+def _torch():
+    import torch
+
+    return torch
+
+
+def blocks_to_device(blocks: np.ndarray, device=None):
+    """Copy a pdb_blk array to the GPU as a uint8 tensor (16 B per block)."""
+    torch = _torch()
+    raw = np.ascontiguousarray(blocks, dtype=BLK_DTYPE).view(np.uint8)
+    return torch.from_numpy(raw.copy()).to(device or "cuda")
+
+
+def _stream_ptr(stream) -> int:
+    torch = _torch()
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return int(s.cuda_stream)
+
+
+def _dev_ptr(t) -> int:
+    if not t.is_cuda:
+        raise ValueError("expected a device (cuda) tensor")
+    if not t.is_contiguous():
+        raise ValueError("expected a contiguous tensor")
+    return int(t.data_ptr())
+
+
+def _out_tensor(n: int, like, out):
+    torch = _torch()
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=like.device)
+    elif out.numel() < n or out.dtype != torch.int32:
+        raise ValueError("out must be an int32 tensor with >= nblk elements")
+    return out
+
+
+def batch_fixed(d_base, stride: int, length: int, nblk: int, *, masked: bool = False,
+                init: int | None = None, out=None, stream=None):
+    """CRC of blocks i at d_base[i*stride : i*stride+length] -> int32 tensor (bit pattern = u32)."""
+    if nblk and (nblk - 1) * stride + length > d_base.numel() * d_base.element_size():
+        raise ValueError("blocks exceed the base tensor")
+    out = _out_tensor(nblk, d_base, out)
+    flags = (MASK_OUTPUT if masked else 0) | (USE_INIT if init is not None else 0)
+    check(lib().pdb_crc32c_batch_device_fixed(
+        _dev_ptr(d_base), stride, length, nblk, flags, (init or 0) & 0xFFFFFFFF,
+        _dev_ptr(out), _stream_ptr(stream)))
+    return out
+
+
+def batch(d_base, d_blocks, *, masked: bool = False, use_init: bool = False, out=None, stream=None):
+    """CRC of each descriptor (pdb_blk, 16 B each, device tensor) -> int32 tensor."""
+    n = d_blocks.numel() * d_blocks.element_size() // 16
+    out = _out_tensor(n, d_base, out)
+    flags = (MASK_OUTPUT if masked else 0) | (USE_INIT if use_init else 0)
+    check(lib().pdb_crc32c_batch_device(
+        _dev_ptr(d_base), _dev_ptr(d_blocks), n, flags, _dev_ptr(out), _stream_ptr(stream)))
+    return out
+
+
+def verify(d_base, d_blocks, d_expected, *, masked: bool = True, use_init: bool = False,
+           stream=None):
+    """(ok uint8 tensor, nbad int32 tensor[1]) -- ReadBlock's check for many blocks at once."""
+    torch = _torch()
+    n = d_blocks.numel() * d_blocks.element_size() // 16
+    ok = torch.empty(n, dtype=torch.uint8, device=d_base.device)
+    nbad = torch.zeros(1, dtype=torch.int32, device=d_base.device)
+    flags = (MASK_OUTPUT if masked else 0) | (USE_INIT if use_init else 0)
+    check(lib().pdb_crc32c_verify_device(
+        _dev_ptr(d_base), _dev_ptr(d_blocks), n, flags, _dev_ptr(d_expected), _dev_ptr(ok),
+        _dev_ptr(nbad), _stream_ptr(stream)))
+    return ok, nbad
+
+
+def batch_host(base, blocks: np.ndarray, *, masked: bool = False, use_init: bool = False) -> np.ndarray:
+    """Host buffers in, host CRCs out (copy-inclusive path)."""
+    p, n, _keep = _buf(base)
+    blocks = np.ascontiguousarray(blocks, dtype=BLK_DTYPE)
+    out = np.zeros(len(blocks), dtype=np.uint32)
+    flags = (MASK_OUTPUT if masked else 0) | (USE_INIT if use_init else 0)
+    check(lib().pdb_crc32c_batch_host(p, n, blocks.ctypes.data, len(blocks), flags, out.ctypes.data))
+    return out
+
+
+def launch_geometry(device: int = -1):
+    g, b, l = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+    check(lib().pdb_crc32c_launch_geometry(device, ctypes.byref(g), ctypes.byref(b), ctypes.byref(l)))
+    return g.value, b.value, l.value
+
+
+def fill_splitmix(d_dst, seed: int, byte_offset: int = 0, nbytes: int | None = None, stream=None):
+    """Fill a device tensor with the splitmix64 synthetic byte stream (same as the oracle's)."""
+    nb = d_dst.numel() * d_dst.element_size() if nbytes is None else nbytes
+    check(lib().pdb_fill_splitmix_device(_dev_ptr(d_dst), nb, seed & 0xFFFFFFFFFFFFFFFF,
+                                         byte_offset, _stream_ptr(stream)))
+    return d_dst

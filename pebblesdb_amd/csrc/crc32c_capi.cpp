@@ -1,0 +1,419 @@
+// crc32c_capi.cpp -- the C-ABI boundary (include/pdb_crc32c.h) over the HIP kernels.
+//
+// Replaces leveldb::crc32c::{Extend,Value,Mask,Unmask} (reference util/crc32c.h:14-40) and the
+// trailer math inside TableBuilder::WriteRawBlock / ReadBlock (table/table_builder.cc:187-205,
+// table/format.cc:96-104).  There is deliberately no CPU implementation of the CRC here: every
+// checksum is computed by the gfx950 kernels, and a missing device is an error.
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "crc32c_internal.h"
+#include "crc32c_math.h"
+
+namespace pdb {
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+  return fail(PDB_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+struct DevState {
+  int device = -1;
+  uint32_t* d_tables = nullptr;
+  LaunchGeom geom{256, 1024};
+  hipStream_t stream = nullptr;
+  std::mutex mu;  // guards the host-staging workspace below
+  uint8_t* d_ws = nullptr;
+  size_t ws_cap = 0;
+};
+
+constexpr int kMaxDev = 64;
+std::mutex g_init_mu;
+DevState* g_dev[kMaxDev] = {};
+
+int get_state(DevState** out) {
+  int dev = 0;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n <= 0)
+    return fail(PDB_ENODEV, "no HIP device visible (pdb_crc32c has no CPU fallback)");
+  e = hipGetDevice(&dev);
+  if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+  if (dev < 0 || dev >= kMaxDev) return fail(PDB_ENODEV, "device index out of range");
+  DevState* st = __atomic_load_n(&g_dev[dev], __ATOMIC_ACQUIRE);
+  if (st) {
+    *out = st;
+    return PDB_OK;
+  }
+  std::lock_guard<std::mutex> lk(g_init_mu);
+  if (g_dev[dev]) {
+    *out = g_dev[dev];
+    return PDB_OK;
+  }
+  std::unique_ptr<DevState> s(new DevState);
+  s->device = dev;
+  hipDeviceProp_t prop;
+  e = hipGetDeviceProperties(&prop, dev);
+  if (e != hipSuccess) return hip_fail(e, "hipGetDeviceProperties");
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(PDB_ENODEV, std::string("pdb_crc32c is built for gfx950; device is ") +
+                                prop.gcnArchName);
+  s->geom.grid = prop.multiProcessorCount > 0 ? static_cast<uint32_t>(prop.multiProcessorCount) : 256;
+  s->geom.block = 1024;
+  std::vector<uint32_t> tabs(PDB_TABLE_WORDS);
+  build_device_tables(tabs.data());
+  e = hipMalloc(&s->d_tables, tabs.size() * sizeof(uint32_t));
+  if (e != hipSuccess) return hip_fail(e, "hipMalloc(tables)");
+  e = hipMemcpy(s->d_tables, tabs.data(), tabs.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+  if (e != hipSuccess) return hip_fail(e, "hipMemcpy(tables)");
+  e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) return hip_fail(e, "hipStreamCreate");
+  __atomic_store_n(&g_dev[dev], s.get(), __ATOMIC_RELEASE);
+  *out = s.release();
+  return PDB_OK;
+}
+
+// Device entry points launch on the caller's stream; NULL is the HIP default (null) stream,
+// exactly as for hipMemcpyAsync/hipLaunchKernel (torch's default stream is that stream).
+hipStream_t pick_stream(DevState* st, void* stream) {
+  (void)st;
+  return static_cast<hipStream_t>(stream);
+}
+
+int ensure_ws(DevState* st, size_t bytes) {
+  if (bytes <= st->ws_cap) return PDB_OK;
+  if (st->d_ws) {
+    (void)hipStreamSynchronize(st->stream);
+    (void)hipFree(st->d_ws);
+    st->d_ws = nullptr;
+    st->ws_cap = 0;
+  }
+  size_t cap = std::max<size_t>(bytes, 1 << 20);
+  hipError_t e = hipMalloc(&st->d_ws, cap);
+  if (e != hipSuccess) return fail(PDB_ENOMEM, std::string("hipMalloc(workspace): ") + hipGetErrorString(e));
+  st->ws_cap = cap;
+  return PDB_OK;
+}
+
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// Host batch over descriptors: stage [lo, hi) of the host span, the rebased descriptors and the
+// outputs in one workspace; one H2D span copy, one H2D descriptor copy, kernel, one D2H.
+int host_desc(const uint8_t* base, uint64_t base_len, const pdb_blk* blk, uint64_t nblk,
+              uint32_t flags, int mode, const uint32_t* expected, uint32_t* out, uint8_t* ok,
+              uint64_t* nbad_out) {
+  if (nblk == 0) {
+    if (nbad_out) *nbad_out = 0;
+    return PDB_OK;
+  }
+  if (!base || !blk) return fail(PDB_EINVAL, "null argument");
+  uint64_t lo = UINT64_MAX, hi = 0;
+  for (uint64_t i = 0; i < nblk; ++i) {
+    if (blk[i].off > base_len || blk[i].len > base_len - blk[i].off)
+      return fail(PDB_ERANGE, "block " + std::to_string(i) + " exceeds base_len");
+    if (blk[i].len == 0) continue;
+    lo = std::min(lo, blk[i].off);
+    hi = std::max(hi, blk[i].off + blk[i].len);
+  }
+  if (lo == UINT64_MAX) lo = hi = 0;
+  lo &= ~static_cast<uint64_t>(15);  // keep the source's 16-B phase so fast loads stay aligned
+  DevState* st;
+  int rc = get_state(&st);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(st->mu);
+  hipError_t e = hipSetDevice(st->device);
+  if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+  const size_t span = hi - lo;
+  const size_t off_desc = align_up(span + 16, 256);
+  const size_t off_out = align_up(off_desc + nblk * sizeof(pdb_blk), 256);
+  const size_t off_exp = align_up(off_out + nblk * sizeof(uint32_t), 256);
+  const size_t off_ok = align_up(off_exp + (mode == kModeVerify ? nblk * 4 : 0), 256);
+  const size_t off_nbad = align_up(off_ok + (mode == kModeVerify ? nblk : 0), 256);
+  rc = ensure_ws(st, off_nbad + 256);
+  if (rc) return rc;
+  std::vector<pdb_blk> rb(blk, blk + nblk);
+  for (auto& b : rb) b.off = b.len ? b.off - lo : 0;
+  hipStream_t s = st->stream;
+  uint8_t* ws = st->d_ws;
+  if (span && (e = hipMemcpyAsync(ws, base + lo, span, hipMemcpyHostToDevice, s)) != hipSuccess)
+    return hip_fail(e, "hipMemcpyAsync(span)");
+  if ((e = hipMemcpyAsync(ws + off_desc, rb.data(), nblk * sizeof(pdb_blk), hipMemcpyHostToDevice,
+                          s)) != hipSuccess)
+    return hip_fail(e, "hipMemcpyAsync(desc)");
+  uint32_t* d_nbad = reinterpret_cast<uint32_t*>(ws + off_nbad);
+  if (mode == kModeVerify) {
+    if ((e = hipMemcpyAsync(ws + off_exp, expected, nblk * 4, hipMemcpyHostToDevice, s)) != hipSuccess)
+      return hip_fail(e, "hipMemcpyAsync(expected)");
+    if ((e = hipMemsetAsync(d_nbad, 0, 4, s)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
+  }
+  e = launch_desc(st->geom, st->d_tables, ws, reinterpret_cast<const pdb_blk*>(ws + off_desc), nblk,
+                  flags, mode, reinterpret_cast<const uint32_t*>(ws + off_exp),
+                  reinterpret_cast<uint32_t*>(ws + off_out), ws + off_ok, d_nbad, s);
+  if (e != hipSuccess) return hip_fail(e, "launch_desc");
+  if (mode == kModeOut) {
+    if ((e = hipMemcpyAsync(out, ws + off_out, nblk * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
+      return hip_fail(e, "hipMemcpyAsync(out)");
+  } else {
+    uint32_t nb = 0;
+    if (ok && (e = hipMemcpyAsync(ok, ws + off_ok, nblk, hipMemcpyDeviceToHost, s)) != hipSuccess)
+      return hip_fail(e, "hipMemcpyAsync(ok)");
+    if ((e = hipMemcpyAsync(&nb, d_nbad, 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
+      return hip_fail(e, "hipMemcpyAsync(nbad)");
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+    if (nbad_out) *nbad_out = nb;
+    return PDB_OK;
+  }
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+  return PDB_OK;
+}
+
+int host_sst(uint8_t* buf, uint64_t buf_len, const pdb_block_handle* h, uint64_t n, bool seal,
+             uint8_t* ok, int64_t* nbad_out) {
+  if (n == 0) {
+    if (nbad_out) *nbad_out = 0;
+    return PDB_OK;
+  }
+  if (!buf || !h) return fail(PDB_EINVAL, "null argument");
+  uint64_t lo = UINT64_MAX, hi = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    // block + 5-byte trailer must lie inside the buffer (table/format.cc:84-87 "truncated")
+    if (h[i].offset > buf_len || h[i].size > buf_len - h[i].offset ||
+        buf_len - h[i].offset - h[i].size < 5)
+      return fail(PDB_ERANGE, "block handle " + std::to_string(i) + " (+trailer) exceeds buffer");
+    if (h[i].size + 1 > 0xFFFFFFFFull) return fail(PDB_ERANGE, "block larger than 4 GiB");
+    lo = std::min(lo, h[i].offset);
+    hi = std::max(hi, h[i].offset + h[i].size + 5);
+  }
+  lo &= ~static_cast<uint64_t>(15);
+  DevState* st;
+  int rc = get_state(&st);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(st->mu);
+  hipError_t e = hipSetDevice(st->device);
+  if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+  const size_t span = hi - lo;
+  const size_t off_h = align_up(span + 16, 256);
+  const size_t off_ok = align_up(off_h + n * sizeof(pdb_block_handle), 256);
+  const size_t off_nbad = align_up(off_ok + n, 256);
+  rc = ensure_ws(st, off_nbad + 256);
+  if (rc) return rc;
+  std::vector<pdb_block_handle> rh(h, h + n);
+  for (auto& x : rh) x.offset -= lo;
+  hipStream_t s = st->stream;
+  uint8_t* ws = st->d_ws;
+  uint32_t* d_nbad = reinterpret_cast<uint32_t*>(ws + off_nbad);
+  if ((e = hipMemcpyAsync(ws, buf + lo, span, hipMemcpyHostToDevice, s)) != hipSuccess)
+    return hip_fail(e, "hipMemcpyAsync(span)");
+  if ((e = hipMemcpyAsync(ws + off_h, rh.data(), n * sizeof(pdb_block_handle), hipMemcpyHostToDevice,
+                          s)) != hipSuccess)
+    return hip_fail(e, "hipMemcpyAsync(handles)");
+  if ((e = hipMemsetAsync(d_nbad, 0, 4, s)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
+  e = launch_sst(st->geom, st->d_tables, ws, span, reinterpret_cast<const pdb_block_handle*>(ws + off_h),
+                 n, seal, ws + off_ok, d_nbad, s);
+  if (e != hipSuccess) return hip_fail(e, "launch_sst");
+  if (seal) {
+    // Copy back only the 4 CRC bytes of every trailer (the rest of the image is unchanged).
+    // Done as one span copy into a host temp, then scattered, to keep it to one D2H.
+    std::vector<uint8_t> tmp(span);
+    if ((e = hipMemcpyAsync(tmp.data(), ws, span, hipMemcpyDeviceToHost, s)) != hipSuccess)
+      return hip_fail(e, "hipMemcpyAsync(span back)");
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+    for (uint64_t i = 0; i < n; ++i) memcpy(buf + h[i].offset + h[i].size + 1, tmp.data() + rh[i].offset + h[i].size + 1, 4);
+    if (nbad_out) *nbad_out = 0;
+    return PDB_OK;
+  }
+  uint32_t nb = 0;
+  if (ok && (e = hipMemcpyAsync(ok, ws + off_ok, n, hipMemcpyDeviceToHost, s)) != hipSuccess)
+    return hip_fail(e, "hipMemcpyAsync(ok)");
+  if ((e = hipMemcpyAsync(&nb, d_nbad, 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
+    return hip_fail(e, "hipMemcpyAsync(nbad)");
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+  if (nbad_out) *nbad_out = nb;
+  return PDB_OK;
+}
+
+}  // namespace
+}  // namespace pdb
+
+using namespace pdb;
+
+extern "C" {
+
+int pdb_crc32c_abi_version(void) { return PDB_CRC32C_ABI_VERSION; }
+
+int pdb_crc32c_init(int device) {
+  if (device >= 0) {
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+  }
+  DevState* st;
+  return get_state(&st);
+}
+
+const char* pdb_last_error(void) { return g_err.c_str(); }
+
+int pdb_crc32c_current_device(void) {
+  int d = -1;
+  if (hipGetDevice(&d) != hipSuccess) return -1;
+  return d;
+}
+
+uint32_t pdb_crc32c_mask(uint32_t crc) { return pdb_mask(crc); }
+uint32_t pdb_crc32c_unmask(uint32_t m) { return pdb_unmask(m); }
+
+uint32_t pdb_crc32c_extend(uint32_t init_crc, const void* data, size_t n) {
+  if (n == 0) return init_crc;  // Extend over nothing is the identity (util/crc32c.cc:25-32)
+  if (n > 0xFFFFFFFFull) {
+    fprintf(stderr, "pdb_crc32c_extend: span >= 4 GiB is not supported\n");
+    abort();
+  }
+  pdb_blk b{0, static_cast<uint32_t>(n), init_crc};
+  uint32_t out = 0;
+  int rc = host_desc(static_cast<const uint8_t*>(data), n, &b, 1, PDB_CRC_USE_INIT, kModeOut, nullptr,
+                     &out, nullptr, nullptr);
+  if (rc) {
+    fprintf(stderr, "pdb_crc32c_extend: device CRC failed (%d): %s\n", rc, g_err.c_str());
+    abort();
+  }
+  return out;
+}
+
+uint32_t pdb_crc32c_value(const void* data, size_t n) { return pdb_crc32c_extend(0, data, n); }
+
+int pdb_crc32c_batch_device_fixed(const void* d_base, uint64_t stride, uint32_t len, uint64_t nblk,
+                                  uint32_t flags, uint32_t init, uint32_t* d_out, void* stream) {
+  if (nblk == 0) return PDB_OK;
+  if (!d_base || !d_out) return fail(PDB_EINVAL, "null argument");
+  DevState* st;
+  int rc = get_state(&st);
+  if (rc) return rc;
+  hipError_t e = launch_fixed(st->geom, st->d_tables, static_cast<const uint8_t*>(d_base), stride, len,
+                              nblk, flags, init, d_out, pick_stream(st, stream));
+  return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_fixed");
+}
+
+int pdb_crc32c_batch_device(const void* d_base, const pdb_blk* d_blk, uint64_t nblk, uint32_t flags,
+                            uint32_t* d_out, void* stream) {
+  if (nblk == 0) return PDB_OK;
+  if (!d_base || !d_blk || !d_out) return fail(PDB_EINVAL, "null argument");
+  DevState* st;
+  int rc = get_state(&st);
+  if (rc) return rc;
+  hipError_t e = launch_desc(st->geom, st->d_tables, static_cast<const uint8_t*>(d_base), d_blk, nblk,
+                             flags, kModeOut, nullptr, d_out, nullptr, nullptr, pick_stream(st, stream));
+  return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_desc");
+}
+
+int pdb_crc32c_verify_device(const void* d_base, const pdb_blk* d_blk, uint64_t nblk, uint32_t flags,
+                             const uint32_t* d_expected, uint8_t* d_ok, uint32_t* d_nbad,
+                             void* stream) {
+  if (nblk == 0) return PDB_OK;
+  if (!d_base || !d_blk || !d_expected) return fail(PDB_EINVAL, "null argument");
+  DevState* st;
+  int rc = get_state(&st);
+  if (rc) return rc;
+  hipError_t e = launch_desc(st->geom, st->d_tables, static_cast<const uint8_t*>(d_base), d_blk, nblk,
+                             flags, kModeVerify, d_expected, nullptr, d_ok, d_nbad,
+                             pick_stream(st, stream));
+  return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_desc(verify)");
+}
+
+int pdb_crc32c_batch_host(const void* base, uint64_t base_len, const pdb_blk* blk, uint64_t nblk,
+                          uint32_t flags, uint32_t* out) {
+  if (nblk && !out) return fail(PDB_EINVAL, "null out");
+  return host_desc(static_cast<const uint8_t*>(base), base_len, blk, nblk, flags, kModeOut, nullptr,
+                   out, nullptr, nullptr);
+}
+
+int pdb_sst_seal_device(void* d_buf, uint64_t buf_len, const pdb_block_handle* d_h, uint64_t n,
+                        void* stream) {
+  if (n == 0) return PDB_OK;
+  if (!d_buf || !d_h) return fail(PDB_EINVAL, "null argument");
+  DevState* st;
+  int rc = get_state(&st);
+  if (rc) return rc;
+  hipError_t e = launch_sst(st->geom, st->d_tables, static_cast<uint8_t*>(d_buf), buf_len, d_h, n, true,
+                            nullptr, nullptr, pick_stream(st, stream));
+  return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_sst(seal)");
+}
+
+int pdb_sst_verify_device(const void* d_buf, uint64_t buf_len, const pdb_block_handle* d_h,
+                          uint64_t n, uint8_t* d_ok, uint32_t* d_nbad, void* stream) {
+  if (n == 0) return PDB_OK;
+  if (!d_buf || !d_h) return fail(PDB_EINVAL, "null argument");
+  DevState* st;
+  int rc = get_state(&st);
+  if (rc) return rc;
+  hipError_t e = launch_sst(st->geom, st->d_tables, static_cast<uint8_t*>(const_cast<void*>(d_buf)),
+                            buf_len, d_h, n, false, d_ok, d_nbad, pick_stream(st, stream));
+  return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_sst(verify)");
+}
+
+int pdb_sst_seal_host(void* buf, uint64_t buf_len, const pdb_block_handle* h, uint64_t n) {
+  return host_sst(static_cast<uint8_t*>(buf), buf_len, h, n, true, nullptr, nullptr);
+}
+
+int64_t pdb_sst_verify_host(const void* buf, uint64_t buf_len, const pdb_block_handle* h, uint64_t n,
+                            uint8_t* ok) {
+  int64_t nbad = 0;
+  int rc = host_sst(static_cast<uint8_t*>(const_cast<void*>(buf)), buf_len, h, n, false, ok, &nbad);
+  return rc ? rc : nbad;
+}
+
+int pdb_diag_read_stream(const void* d_base, uint64_t nbytes, uint32_t* d_out, void* stream) {
+  DevState* st;
+  int rc = get_state(&st);
+  if (rc) return rc;
+  hipError_t e = launch_read_stream(static_cast<const uint8_t*>(d_base), nbytes, d_out,
+                                    pick_stream(st, stream));
+  return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_read_stream");
+}
+
+int pdb_diag_read_pattern4k(const void* d_base, uint64_t nblk, uint32_t* d_out, void* stream) {
+  DevState* st;
+  int rc = get_state(&st);
+  if (rc) return rc;
+  hipError_t e = launch_read_pattern4k(st->geom, static_cast<const uint8_t*>(d_base), nblk, d_out,
+                                       pick_stream(st, stream));
+  return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_read_pattern4k");
+}
+
+int pdb_fill_splitmix_device(void* d_dst, uint64_t nbytes, uint64_t seed, uint64_t byte_offset,
+                             void* stream) {
+  DevState* st;
+  int rc = get_state(&st);
+  if (rc) return rc;
+  hipError_t e = launch_fill_splitmix(static_cast<uint8_t*>(d_dst), nbytes, seed, byte_offset,
+                                      pick_stream(st, stream));
+  return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_fill_splitmix");
+}
+
+int pdb_crc32c_launch_geometry(int device, uint32_t* grid, uint32_t* block, uint32_t* lds_bytes) {
+  if (device >= 0) {
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+  }
+  DevState* st;
+  int rc = get_state(&st);
+  if (rc) return rc;
+  if (grid) *grid = st->geom.grid;
+  if (block) *block = st->geom.block;
+  if (lds_bytes) *lds_bytes = PDB_LDS_BYTES;
+  return PDB_OK;
+}
+
+}  // extern "C"

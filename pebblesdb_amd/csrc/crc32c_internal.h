@@ -1,0 +1,45 @@
+// crc32c_internal.h -- declarations shared between the C-ABI layer and the HIP kernel TU.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#include <hip/hip_runtime.h>
+
+#include "../../include/pdb_crc32c.h"
+
+namespace pdb {
+
+// crc32c_tables.cpp
+void build_byte_table(uint32_t t0[256]);
+void build_device_tables(uint32_t* out);  // PDB_TABLE_WORDS
+uint32_t host_shift(uint32_t c, uint64_t nbytes);
+
+// Kernel launch modes for the descriptor kernel.
+enum DescMode : int {
+  kModeOut = 0,     // out[i] = crc
+  kModeVerify = 1,  // ok[i] = (crc == expected[i])
+};
+
+struct LaunchGeom {
+  uint32_t grid;   // workgroups (one per CU: the LDS image is ~156 KiB)
+  uint32_t block;  // threads per workgroup
+};
+
+// crc32c_kernels.hip -- all launches are asynchronous on `s`.
+hipError_t launch_fixed(const LaunchGeom& g, const uint32_t* d_tables, const uint8_t* base,
+                        uint64_t stride, uint32_t len, uint64_t nblk, uint32_t flags, uint32_t init,
+                        uint32_t* out, hipStream_t s);
+hipError_t launch_desc(const LaunchGeom& g, const uint32_t* d_tables, const uint8_t* base,
+                       const pdb_blk* blk, uint64_t nblk, uint32_t flags, int mode,
+                       const uint32_t* expected, uint32_t* out, uint8_t* ok, uint32_t* nbad,
+                       hipStream_t s);
+hipError_t launch_sst(const LaunchGeom& g, const uint32_t* d_tables, uint8_t* buf, uint64_t buf_len,
+                      const pdb_block_handle* h, uint64_t n, bool seal, uint8_t* ok, uint32_t* nbad,
+                      hipStream_t s);
+hipError_t launch_read_stream(const uint8_t* base, uint64_t nbytes, uint32_t* out, hipStream_t s);
+hipError_t launch_read_pattern4k(const LaunchGeom& g, const uint8_t* base, uint64_t nblk,
+                                 uint32_t* out, hipStream_t s);
+hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed, uint64_t byte_offset,
+                                hipStream_t s);
+
+}  // namespace pdb

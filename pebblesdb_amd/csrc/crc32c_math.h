@@ -1,0 +1,55 @@
+// crc32c_math.h -- GF(2) algebra of CRC32C (Castagnoli, reflected) shared by the host table
+// builder and the HIP kernels.
+//
+// Conventions ("raw state" = the register the reference's crc32c_sb8_64_bit carries between
+// calls, i.e. crc ^ 0xFFFFFFFF; util/crc32c.cc:27,31):
+//   byte step      c' = T0[(c ^ b) & 0xff] ^ (c >> 8)          (util/crc32c.cc:601,623)
+//   shift(c, D)    = raw state after D zero bytes from state c; linear in c.
+//   Tk[b]          = shift(b, k+1);  T0 is the byte table, T1..T7 = the reference's
+//                    o40..o88 slices (util/crc32c.cc:130-556, generated here, not copied).
+//   word step      x = c ^ LE32(w); c' = T3[x0] ^ T2[x1] ^ T1[x2] ^ T0[x3]  (= shift(x, 4))
+//   injection      processing M from state c == processing (M with its first 4 bytes XORed
+//                  with LE32(c)) from state 0, for |M| >= 4.
+//   concatenation  R(A||B) = shift(R(A), |B|) ^ R(B), with R the raw CRC from state 0.
+//   Extend(init,M) = ~S(~init, M)   (util/crc32c.cc:25-32)
+//   Mask(c)        = ror32(c,15) + 0xa282ead8 (util/crc32c.h:29-32)
+#pragma once
+#include <stdint.h>
+
+#define PDB_CRC32C_POLY_REFLECTED 0x82F63B78u /* 0x1EDC6F41 reflected (util/crc32c.cc:116-128) */
+#define PDB_CRC32C_MASK_DELTA 0xa282ead8u     /* util/crc32c.h:24 */
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define PDB_HD __host__ __device__ __forceinline__
+#else
+#define PDB_HD static inline
+#endif
+
+PDB_HD uint32_t pdb_mask(uint32_t crc) { return ((crc >> 15) | (crc << 17)) + PDB_CRC32C_MASK_DELTA; }
+PDB_HD uint32_t pdb_unmask(uint32_t m) {
+  uint32_t rot = m - PDB_CRC32C_MASK_DELTA;
+  return (rot >> 17) | (rot << 15);
+}
+
+// ---- LDS image geometry (shared by host table packer and kernels) -----------------------------
+//
+// MAIN region [0, 0x20000): the four slice-by-4 tables T0..T3, each replicated 32x so that lane
+// l reads replica (l & 31) -> LDS bank (l & 31) for every ds_read_b32: conflict-free random
+// lookups.  Entry b of table k, replica r lives at byte
+//     ((k >> 1) << 16) | (b << 8) | ((k & 1) << 7) | (r << 2)
+// i.e. the data byte lands in address bits 8..15, so one v_perm_b32 builds the address.
+//
+// OPS region [0x20000, 0x20000 + PDB_NOPS*4096): shift operators (4 x 256 u32 each, one copy).
+//   op k (k = 0..5): shift by 64 << k bytes (wave tree combine: 64, 128, ..., 2048)
+//   op 6:            shift by 63*64 = 4032 bytes (per-lane Horner step between rounds)
+#define PDB_LANES 64
+#define PDB_CHUNK 64 /* bytes per lane per round */
+#define PDB_MAIN_BYTES 0x20000u
+#define PDB_NOPS 7
+#define PDB_OP_TREE0 0
+#define PDB_OP_HORNER 6
+#define PDB_OPS_BYTES (PDB_NOPS * 4096u)
+#define PDB_LDS_BYTES (PDB_MAIN_BYTES + PDB_OPS_BYTES) /* 159744 <= 163840 */
+/* Device table source: T0..T3 (1024 u32) then ops (PDB_NOPS * 1024 u32). */
+#define PDB_TABLE_WORDS (1024u + PDB_NOPS * 1024u)

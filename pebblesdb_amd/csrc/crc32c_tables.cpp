@@ -1,0 +1,88 @@
+// crc32c_tables.cpp -- host-side generation of the slice-by-4 tables and the GF(2) shift
+// operators the kernels stage into LDS.  Everything is generated from the reflected polynomial;
+// no table literal is copied from the reference (util/crc32c.cc:130-556).
+#include <string.h>
+
+#include "crc32c_math.h"
+#include "crc32c_internal.h"
+
+namespace pdb {
+namespace {
+
+// 32x32 GF(2) matrix as 32 column vectors: M * v = XOR of cols[i] for set bits i of v.
+struct Gf2Mat {
+  uint32_t col[32];
+};
+
+uint32_t mat_vec(const Gf2Mat& m, uint32_t v) {
+  uint32_t r = 0;
+  for (int i = 0; v; ++i, v >>= 1)
+    if (v & 1u) r ^= m.col[i];
+  return r;
+}
+
+Gf2Mat mat_mul(const Gf2Mat& a, const Gf2Mat& b) {  // (a*b)v = a(b v)
+  Gf2Mat r;
+  for (int i = 0; i < 32; ++i) r.col[i] = mat_vec(a, b.col[i]);
+  return r;
+}
+
+// Operator for one zero byte: c' = T0[c & 0xff] ^ (c >> 8).
+Gf2Mat one_zero_byte(const uint32_t* t0) {
+  Gf2Mat m;
+  for (int i = 0; i < 32; ++i) {
+    uint32_t c = 1u << i;
+    m.col[i] = t0[c & 0xffu] ^ (c >> 8);
+  }
+  return m;
+}
+
+Gf2Mat mat_pow(Gf2Mat base, uint64_t e) {
+  Gf2Mat r;
+  for (int i = 0; i < 32; ++i) r.col[i] = 1u << i;
+  while (e) {
+    if (e & 1) r = mat_mul(base, r);
+    base = mat_mul(base, base);
+    e >>= 1;
+  }
+  return r;
+}
+
+}  // namespace
+
+void build_byte_table(uint32_t t0[256]) {
+  for (uint32_t b = 0; b < 256; ++b) {
+    uint32_t c = b;
+    for (int k = 0; k < 8; ++k) c = (c & 1u) ? (c >> 1) ^ PDB_CRC32C_POLY_REFLECTED : (c >> 1);
+    t0[b] = c;
+  }
+}
+
+uint32_t host_shift(uint32_t c, uint64_t nbytes) {
+  uint32_t t0[256];
+  build_byte_table(t0);
+  return mat_vec(mat_pow(one_zero_byte(t0), nbytes), c);
+}
+
+// Fills `out` (PDB_TABLE_WORDS u32): [T0|T1|T2|T3] then PDB_NOPS operators, each laid out as
+// 4 sub-tables j=0..3 of 256 entries: op[j][b] = shift(b << 8j, D).
+void build_device_tables(uint32_t* out) {
+  uint32_t t[4][256];
+  build_byte_table(t[0]);
+  for (int k = 1; k < 4; ++k)
+    for (int b = 0; b < 256; ++b) t[k][b] = (t[k - 1][b] >> 8) ^ t[0][t[k - 1][b] & 0xffu];
+  memcpy(out, t, sizeof(t));
+
+  const Gf2Mat z1 = one_zero_byte(t[0]);
+  uint64_t dist[PDB_NOPS];
+  for (int k = 0; k < 6; ++k) dist[PDB_OP_TREE0 + k] = (uint64_t)PDB_CHUNK << k;
+  dist[PDB_OP_HORNER] = (uint64_t)(PDB_LANES - 1) * PDB_CHUNK;
+  for (int o = 0; o < PDB_NOPS; ++o) {
+    Gf2Mat m = mat_pow(z1, dist[o]);
+    uint32_t* op = out + 1024 + o * 1024;
+    for (int j = 0; j < 4; ++j)
+      for (uint32_t b = 0; b < 256; ++b) op[j * 256 + b] = mat_vec(m, b << (8 * j));
+  }
+}
+
+}  // namespace pdb

@@ -1,0 +1,33 @@
+"""Block-range sharding across ranks.
+
+Blocks are independent, so N GPUs = N disjoint shards and no data-path collective.  Fixed-size
+blocks split by count; variable-size blocks split by bytes (prefix sum over lengths) so each
+rank hashes about the same number of bytes.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def block_range(nblk: int, world: int, rank: int) -> tuple[int, int]:
+    """Contiguous [lo, hi) of `nblk` fixed-size blocks owned by `rank` ([r*N/G, (r+1)*N/G))."""
+    if world < 1 or not (0 <= rank < world):
+        raise ValueError("bad world/rank")
+    return nblk * rank // world, nblk * (rank + 1) // world
+
+
+def byte_balanced_ranges(lens, world: int) -> list[tuple[int, int]]:
+    """Split a descriptor list into `world` contiguous ranges with ~equal byte totals."""
+    lens = np.asarray(lens, dtype=np.int64)
+    if world < 1:
+        raise ValueError("bad world")
+    if lens.size == 0:
+        return [(0, 0)] * world
+    cs = np.cumsum(lens)
+    total = int(cs[-1])
+    cuts = [0]
+    for r in range(1, world):
+        cuts.append(int(np.searchsorted(cs, total * r / world, side="left")) + 1)
+    cuts.append(lens.size)
+    cuts = np.maximum.accumulate(np.minimum(np.array(cuts), lens.size))
+    return [(int(cuts[r]), int(cuts[r + 1])) for r in range(world)]

@@ -1,0 +1,199 @@
+#!/usr/bin/env python3
+"""Generate tests/golden/crc32c_golden.json from the REFERENCE CRC32C.
+
+Run in the build container (where /root/reference exists):
+    oracle/build_ref.sh && python tests/golden/gen_golden.py
+
+Every expected value below comes from ``oracle/_ref/libpdbref.so`` -- the reference's
+own src/util/crc32c.cc compiled in place -- not from this repo's code.  Inputs are stored
+generatively (fill byte / iota / hex / splitmix64 seed), so the fixture is small data.
+
+Sections
+  known_answers : the reference's unit-test vectors (util/crc32c_test.cc:13-60), the
+                  db_bench crc32c probe (db/db_bench.cc:1112-1129) and SURVEY §8(c) edges
+  sweep         : offsets 0..15 x lengths 0..300 over one splitmix buffer (alignment prefix
+                  and tail paths of util/crc32c.cc:25-32,600-623)
+  extend        : Extend(init, data) with random init (util/crc32c.h:14-17)
+  batches       : seeded random block batches {off,len,init} + expected crc and Mask(crc)
+  trailers      : sstable block trailers [type][Mask(crc(contents||type))]
+                  (table/table_builder.cc:187-205)
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+import oracle  # noqa: E402
+
+OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "crc32c_golden.json")
+
+
+def materialize(spec: dict) -> np.ndarray:
+    k = spec["kind"]
+    if k == "fill":
+        return np.full(spec["len"], spec["byte"], dtype=np.uint8)
+    if k == "iota":
+        return (np.arange(spec["len"]) & 0xFF).astype(np.uint8)
+    if k == "riota":
+        return ((spec["len"] - 1 - np.arange(spec["len"])) & 0xFF).astype(np.uint8)
+    if k == "hex":
+        return np.frombuffer(bytes.fromhex(spec["hex"]), dtype=np.uint8).copy()
+    if k == "ascii":
+        return np.frombuffer(spec["text"].encode(), dtype=np.uint8).copy()
+    if k == "splitmix":
+        return oracle.splitmix_bytes(spec["len"], spec["seed"], spec.get("byte_offset", 0))
+    raise ValueError(k)
+
+
+def zipf_kib_sizes(n: int, seed: int, kmax: int = 64) -> np.ndarray:
+    """Block sizes k KiB, k in 1..kmax, p(k) ~ 1/k."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    k = np.arange(1, kmax + 1)
+    p = (1.0 / k) / np.sum(1.0 / k)
+    return (rng.choice(k, size=n, p=p) * 1024).astype(np.int64)
+
+
+def main() -> None:
+    if not oracle.reference_available():
+        sys.exit("oracle/_ref/libpdbref.so missing: run oracle/build_ref.sh first")
+    ref = oracle.Reference()
+    out: dict = {
+        "generator": "tests/golden/gen_golden.py via oracle/_ref/libpdbref.so "
+        "(reference src/util/crc32c.cc compiled in place)",
+        "splitmix64": "byte j = byte (j%8) of splitmix64(seed + (j//8 + 1)*0x9E3779B97F4A7C15), LE",
+    }
+
+    # ---- known answers -------------------------------------------------------------------
+    iscsi = (
+        "01c00000000000000000000000000000"
+        "14000000000004000000001400000018"
+        "28000000000000000200000000000000"
+    )
+    ka_specs = [
+        ("rfc3720 32x00", {"kind": "fill", "byte": 0, "len": 32}, 0x8A9136AA),
+        ("rfc3720 32xff", {"kind": "fill", "byte": 255, "len": 32}, 0x62A8AB43),
+        ("rfc3720 0..31", {"kind": "iota", "len": 32}, 0x46DD794E),
+        ("rfc3720 31..0", {"kind": "riota", "len": 32}, 0x113FDB5C),
+        ("rfc3720 iscsi pdu", {"kind": "hex", "hex": iscsi}, 0xD9963A56),
+        ("LargeBuffer A x64", {"kind": "fill", "byte": 0x41, "len": 64}, 0x3C36F666),
+        ("LargeBuffer A x1024", {"kind": "fill", "byte": 0x41, "len": 1024}, 0xF6607A92),
+        ("LargeBuffer A x1111", {"kind": "fill", "byte": 0x41, "len": 1111}, 0xA9BC21EF),
+        ("LargeBuffer A x2048", {"kind": "fill", "byte": 0x41, "len": 2048}, 0x88DDB66B),
+        ("LargeBuffer A x4096", {"kind": "fill", "byte": 0x41, "len": 4096}, 0x057251E9),
+        ("db_bench crc32c x x4096", {"kind": "fill", "byte": 0x78, "len": 4096}, 0xA46AB21F),
+        ("4096 x 00", {"kind": "fill", "byte": 0, "len": 4096}, 0x98F94189),
+        ("4097 x 00 (block+type 0)", {"kind": "fill", "byte": 0, "len": 4097}, 0xA8A14AA4),
+        ("empty", {"kind": "fill", "byte": 0, "len": 0}, 0x00000000),
+        ("a", {"kind": "ascii", "text": "a"}, 0xC1D04330),
+        ("hello world", {"kind": "ascii", "text": "hello world"}, None),
+        ("foo", {"kind": "ascii", "text": "foo"}, None),
+    ]
+    kas = []
+    for name, spec, published in ka_specs:
+        v = ref.value(materialize(spec))
+        if published is not None and v != published:
+            raise SystemExit(f"reference disagrees with its own known answer {name}: {v:#x}")
+        kas.append({"name": name, "input": spec, "crc": v, "masked": ref.mask(v)})
+    out["known_answers"] = kas
+    out["mask_of_zero"] = ref.mask(0)
+
+    # ---- sweep: every offset 0..15 x length 0..300 over one buffer ------------------------
+    sweep_seed = 0x5EED
+    buf = oracle.splitmix_bytes(16 + 300 + 64, sweep_seed)
+    crcs = []
+    for off in range(16):
+        row = []
+        for n in range(301):
+            row.append(ref.value(buf[off : off + n]))
+        crcs.append(row)
+    out["sweep"] = {
+        "input": {"kind": "splitmix", "seed": sweep_seed, "len": len(buf)},
+        "offsets": 16,
+        "max_len": 300,
+        "crc": crcs,
+    }
+
+    # ---- extend ---------------------------------------------------------------------------
+    rng = np.random.Generator(np.random.PCG64(11))
+    ext = []
+    for i in range(40):
+        n = int(rng.integers(0, 9000))
+        init = int(rng.integers(0, 2**32))
+        spec = {"kind": "splitmix", "seed": 1000 + i, "len": n}
+        ext.append({"init": init, "input": spec, "crc": ref.extend(init, materialize(spec))})
+    out["extend"] = ext
+
+    # ---- batches --------------------------------------------------------------------------
+    batches = []
+
+    def add_batch(name, seed, total, offs, lens, inits=None, flags=0):
+        data = oracle.splitmix_bytes(total, seed)
+        blk = np.zeros(len(offs), dtype=oracle.BLK_DTYPE)
+        blk["off"] = offs
+        blk["len"] = lens
+        blk["init"] = 0 if inits is None else inits
+        f = 2 if inits is not None else 0
+        crc = ref.batch(data, blk, flags=f)
+        masked = ref.batch(data, blk, flags=f | 1)
+        batches.append(
+            {
+                "name": name,
+                "seed": seed,
+                "total_bytes": int(total),
+                "use_init": inits is not None,
+                "off": [int(x) for x in offs],
+                "len": [int(x) for x in lens],
+                "init": [int(x) for x in (blk["init"])],
+                "crc": [int(x) for x in crc],
+                "masked": [int(x) for x in masked],
+            }
+        )
+
+    # (1) fixed stride 4 KiB, like config 2 (scaled down)
+    nb = 512
+    add_batch("fixed4k", 301, nb * 4096, np.arange(nb) * 4096, np.full(nb, 4096))
+    # (2) sstable layout: contents n (+1 type byte under the CRC) packed at stride n+5
+    rs = np.random.Generator(np.random.PCG64(302))
+    ns = rs.integers(4090, 4200, size=300)
+    offs = np.concatenate([[0], np.cumsum(ns + 5)[:-1]])
+    add_batch("sstable_layout", 302, int(offs[-1] + ns[-1] + 5), offs, ns + 1)
+    # (3) Zipf 1..64 KiB, packed back-to-back
+    zs = zipf_kib_sizes(120, 303)
+    offs = np.concatenate([[0], np.cumsum(zs)[:-1]])
+    add_batch("zipf_1_64k", 303, int(zs.sum()), offs, zs)
+    # (4) ragged: tiny and odd lengths at random byte offsets (incl. 0-length)
+    rr = np.random.Generator(np.random.PCG64(304))
+    lens = np.concatenate([np.arange(0, 80), rr.integers(0, 20000, size=120)])
+    offs = rr.integers(0, 1 << 20, size=len(lens))
+    add_batch("ragged", 304, (1 << 20) + 20000, offs, lens)
+    # (5) Extend semantics per block (random init) over ragged blocks
+    inits = rr.integers(0, 2**32, size=len(lens), dtype=np.uint64)
+    add_batch("ragged_init", 305, (1 << 20) + 20000, offs, lens, inits=inits)
+    # (6) large single blocks (>= several rounds of any GPU chunking)
+    lens = np.array([1 << 20, 3 * (1 << 20) + 7, 213 * 1024 + 13, 65536, 65537])
+    offs = np.array([0, (1 << 20) + 3, 5 * (1 << 20) + 1, 6 * (1 << 20), 6 * (1 << 20) + 65536 + 9])
+    add_batch("large", 306, 7 * (1 << 20), offs, lens)
+    out["batches"] = batches
+
+    # ---- sstable trailers -----------------------------------------------------------------
+    trailers = []
+    for i, (n, t) in enumerate([(4091, 0), (4171, 0), (51, 0), (0, 0), (4096, 1), (213 * 1024, 0), (17, 1)]):
+        spec = {"kind": "splitmix", "seed": 400 + i, "len": n}
+        contents = materialize(spec)
+        crc = ref.extend(ref.value(contents), np.array([t], dtype=np.uint8))
+        trailer = bytes([t]) + int(ref.mask(crc)).to_bytes(4, "little")
+        trailers.append({"input": spec, "type": t, "trailer_hex": trailer.hex(), "crc": crc})
+    out["trailers"] = trailers
+
+    with open(OUT, "w") as f:
+        json.dump(out, f, separators=(",", ":"))
+    print(f"wrote {OUT} ({os.path.getsize(OUT)} bytes)")
+
+
+if __name__ == "__main__":
+    main()

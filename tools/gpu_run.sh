@@ -1,0 +1,29 @@
+#!/usr/bin/env bash
+# tools/gpu_run.sh -- run on the GPU box via gpurun: GPU tests, then a bench line.
+# Each GPU step has its own time limit; a fault / abort / timeout (rc >= 124 or signal)
+# stops the script before any further GPU work.  A plain test failure (rc 1) does not.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+TAG="${1:-run}"
+shift || true
+step() {  # step <name> <timeout> <cmd...>
+  local name=$1 to=$2; shift 2
+  echo "== $name: $*" | tee -a gpurun_out/${TAG}_steps.log
+  timeout -k 10 "$to" "$@" > "gpurun_out/${TAG}_${name}.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc" | tee -a gpurun_out/${TAG}_steps.log
+  tail -5 "gpurun_out/${TAG}_${name}.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "fatal rc=$rc in $name; stopping"; exit $rc; fi
+  return 0
+}
+for s in "$@"; do
+  case "$s" in
+    tests) step tests 900 python -m pytest tests -m gpu -x -q ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench 600 python bench.py --diag ;;
+    bench_sst) step bench_sst 600 python bench.py --workload sstable --no-cpu-baseline --no-copy-inclusive ;;
+    bench_c3) step bench_c3 600 python bench.py --workload c3 --no-copy-inclusive --steps 10 ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
