@@ -59,7 +59,7 @@ def main():
     import torch.distributed as dist
 
     from pebblesdb_amd import crc32c
-    from pebblesdb_amd.shard import block_range
+    from pebblesdb_amd.shard import scatter_block_ranges
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -77,14 +77,7 @@ def main():
         n_total = 0
     else:
         n_total = args.nblk * world
-    idx = torch.zeros(world, 2, dtype=torch.int64, device=dev)
-    if rank == 0:
-        for r in range(world):
-            lo, hi = block_range(n_total, world, r) if args.workload != "c3" else (r, r + 1)
-            idx[r, 0], idx[r, 1] = lo, hi
-    if distributed:
-        dist.broadcast(idx, src=0)
-    lo, hi = int(idx[rank, 0]), int(idx[rank, 1])
+    lo, hi = scatter_block_ranges(n_total, world, rank, dev, dist if distributed else None)
 
     # ---- synthetic, device-resident input ---------------------------------------------------
     if args.workload == "c2":
@@ -217,8 +210,8 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": "crc_fixed_kernel<true>" if args.workload == "c2" else
-                          ("crc_fixed_kernel<false>" if args.workload == "sstable" else "crc_desc_kernel<0>"),
+                "kernel": {"c2": "crc_fast4k_kernel<2,1>", "sstable": "crc_fixed_kernel",
+                           "c3": "crc_desc_kernel<0>"}[args.workload],
                 "algorithmic_bytes_per_launch": algo_bytes,
                 "kernel_avg_ms": round(kern_avg_ms, 4),
                 "kernel_min_ms": round(float(np.min(kern_ms)), 4),
@@ -242,7 +235,7 @@ def diag(crc32c, torch, dev, data, stream):
     res = {}
     for name, fn in (
         ("read_stream", lambda: check(lib().pdb_diag_read_stream(data.data_ptr(), nbytes, o.data_ptr(), stream.cuda_stream))),
-        ("read_pattern4k", lambda: check(lib().pdb_diag_read_pattern4k(data.data_ptr(), nbytes // 4096, o.data_ptr(), stream.cuda_stream))),
+        ("read_pattern4k", lambda: check(lib().pdb_diag_read_pattern4k(data.data_ptr(), nbytes // 4096, 0, o.data_ptr(), stream.cuda_stream))),
     ):
         for _ in range(3):
             fn()

@@ -115,11 +115,16 @@ int pdb_sst_verify_device(const void* d_buf, uint64_t buf_len, const pdb_block_h
 /* ---- diagnostics (roofline calibration; not part of the reference interface) ---------------- */
 /* Streams nbytes from d_base with coalesced 16-B loads and XOR-folds them into d_out[0..grid). */
 int pdb_diag_read_stream(const void* d_base, uint64_t nbytes, uint32_t* d_out, void* stream);
-/* Same loads as the 4-KiB fast path (64 B contiguous per lane) with trivial compute. */
-int pdb_diag_read_pattern4k(const void* d_base, uint64_t nblk, uint32_t* d_out, void* stream);
+/* 4-KiB block load patterns with trivial compute (variant 0 = the fast path's loads: 64 B
+ * contiguous per lane, one block in flight per wave; other variants: see crc32c_kernels.hip). */
+int pdb_diag_read_pattern4k(const void* d_base, uint64_t nblk, int variant, uint32_t* d_out,
+                            void* stream);
 /* Fill d_dst[0..nbytes) with the splitmix64 synthetic stream (seed, byte_offset). */
 int pdb_fill_splitmix_device(void* d_dst, uint64_t nbytes, uint64_t seed, uint64_t byte_offset,
                              void* stream);
+/* Select a 4-KiB fast-path kernel variant (A/B experiments only; 0 = shipped default).
+ * Returns the previous selection. */
+int pdb_diag_set_variant(int v);
 /* Launch geometry actually used (for bench reporting): workgroups and threads per workgroup. */
 int pdb_crc32c_launch_geometry(int device, uint32_t* grid, uint32_t* block, uint32_t* lds_bytes);
 

@@ -383,11 +383,12 @@ int pdb_diag_read_stream(const void* d_base, uint64_t nbytes, uint32_t* d_out, v
   return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_read_stream");
 }
 
-int pdb_diag_read_pattern4k(const void* d_base, uint64_t nblk, uint32_t* d_out, void* stream) {
+int pdb_diag_read_pattern4k(const void* d_base, uint64_t nblk, int variant, uint32_t* d_out,
+                            void* stream) {
   DevState* st;
   int rc = get_state(&st);
   if (rc) return rc;
-  hipError_t e = launch_read_pattern4k(st->geom, static_cast<const uint8_t*>(d_base), nblk, d_out,
+  hipError_t e = launch_read_pattern4k(st->geom, static_cast<const uint8_t*>(d_base), nblk, variant, d_out,
                                        pick_stream(st, stream));
   return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_read_pattern4k");
 }
@@ -400,6 +401,12 @@ int pdb_fill_splitmix_device(void* d_dst, uint64_t nbytes, uint64_t seed, uint64
   hipError_t e = launch_fill_splitmix(static_cast<uint8_t*>(d_dst), nbytes, seed, byte_offset,
                                       pick_stream(st, stream));
   return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_fill_splitmix");
+}
+
+int pdb_diag_set_variant(int v) {
+  const int old = g_fast_variant;
+  g_fast_variant = v;
+  return old;
 }
 
 int pdb_crc32c_launch_geometry(int device, uint32_t* grid, uint32_t* block, uint32_t* lds_bytes) {

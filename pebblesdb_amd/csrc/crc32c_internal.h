@@ -25,6 +25,8 @@ struct LaunchGeom {
   uint32_t block;  // threads per workgroup
 };
 
+extern int g_fast_variant;  // diagnostics only: selects a 4-KiB fast-path variant
+
 // crc32c_kernels.hip -- all launches are asynchronous on `s`.
 hipError_t launch_fixed(const LaunchGeom& g, const uint32_t* d_tables, const uint8_t* base,
                         uint64_t stride, uint32_t len, uint64_t nblk, uint32_t flags, uint32_t init,
@@ -38,7 +40,7 @@ hipError_t launch_sst(const LaunchGeom& g, const uint32_t* d_tables, uint8_t* bu
                       hipStream_t s);
 hipError_t launch_read_stream(const uint8_t* base, uint64_t nbytes, uint32_t* out, hipStream_t s);
 hipError_t launch_read_pattern4k(const LaunchGeom& g, const uint8_t* base, uint64_t nblk,
-                                 uint32_t* out, hipStream_t s);
+                                 int variant, uint32_t* out, hipStream_t s);
 hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed, uint64_t byte_offset,
                                 hipStream_t s);
 

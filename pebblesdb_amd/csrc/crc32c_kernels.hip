@@ -77,13 +77,13 @@ __device__ __forceinline__ uint32_t shift_op(const char* lds, uint32_t op, uint3
   return (v0 ^ v1) ^ (v2 ^ v3);
 }
 
-// Fold the 64 lane partials (lane v's partial ends 64*(63-v) bytes before the region end).
-// Result valid in lane 0.
+// Fold the 64 lane partials (lane v's partial ends P*(63-v) bytes before the region end, where
+// slots 0..5 hold "shift by P << k").  Result valid in lane 0.
 __device__ __forceinline__ uint32_t wave_tree(const char* lds, uint32_t lane, uint32_t c) {
 #pragma unroll
   for (uint32_t k = 0; k < 6; ++k) {
     const uint32_t y = __shfl_down(c, 1u << k, 64);
-    if ((lane & ((2u << k) - 1u)) == 0) c = shift_op(lds, PDB_OP_TREE0 + k, c) ^ y;
+    if ((lane & ((2u << k) - 1u)) == 0) c = shift_op(lds, k, c) ^ y;
   }
   return c;
 }
@@ -104,7 +104,9 @@ __device__ __forceinline__ uint32_t ld32u(const uint8_t* q) {
   return __builtin_amdgcn_alignbyte(w[1], lo, s);
 }
 
-// Stage the table image into LDS: T0..T3 written 32x (8 x 16-B stores per entry), ops copied.
+// Stage the table image into LDS: T0..T3 written 32x (8 x 16-B stores per entry); tree
+// operators catalog[kTree .. kTree+5] -> slots 0..5; catalog[kHorner] -> slot 6 (if >= 0).
+template <int kTree, int kHorner>
 __device__ __forceinline__ void stage_tables(char* lds, const uint32_t* __restrict__ tabs) {
   for (uint32_t i = threadIdx.x; i < 4u * 256u * 8u; i += blockDim.x) {
     const uint32_t k = i >> 11, b = (i >> 3) & 255u, part = i & 7u;
@@ -112,9 +114,13 @@ __device__ __forceinline__ void stage_tables(char* lds, const uint32_t* __restri
     const uint32_t addr = ((k >> 1) << 16) | (b << 8) | ((k & 1u) << 7) | (part << 4);
     *reinterpret_cast<u32x4*>(lds + addr) = u32x4{v, v, v, v};
   }
-  const u32x4* ops = reinterpret_cast<const u32x4*>(tabs + 1024);
-  for (uint32_t i = threadIdx.x; i < PDB_NOPS * 256u; i += blockDim.x)
-    *reinterpret_cast<u32x4*>(lds + PDB_MAIN_BYTES + i * 16u) = ops[i];
+  const u32x4* cat = reinterpret_cast<const u32x4*>(tabs + 1024);
+  constexpr uint32_t nslots = kHorner >= 0 ? 7u : 6u;
+  for (uint32_t i = threadIdx.x; i < nslots * 256u; i += blockDim.x) {
+    const uint32_t slot = i >> 8;
+    const uint32_t src = slot < 6 ? kTree + slot : static_cast<uint32_t>(kHorner);
+    *reinterpret_cast<u32x4*>(lds + PDB_MAIN_BYTES + i * 16u) = cat[src * 256u + (i & 255u)];
+  }
 }
 
 // 16 dwords of the 64-B chunk at q.  `s` = q & 3 (uniform across the wave for one block).
@@ -173,7 +179,7 @@ __device__ uint32_t crc_block(const char* lds, const LaneTabs& lt, uint32_t lane
   for (uint32_t r = 0; r < R; ++r) {
     const uint32_t ch = lane + (r << 6);
     if (ch < K) {
-      if (r) c = shift_op(lds, PDB_OP_HORNER, c);
+      if (r) c = shift_op(lds, PDB_SLOT_HORNER, c);
       uint32_t d[16];
       load_chunk(d, q0 + static_cast<uint64_t>(ch) * 64u, s);
       c = chain16(lds, lt, c, d);
@@ -189,47 +195,89 @@ __device__ __forceinline__ uint64_t wave_id_uniform() {
   return static_cast<uint64_t>(blockIdx.x) * kWavesPerWg + w;
 }
 
-// ---- fixed-stride batch: the 4-KiB fast path and the generic strided path --------------------
-template <bool kFast4K>
+// ---- fixed-stride batch, 4-KiB fast path ------------------------------------------------------
+// len == 4096, base and stride 16-B aligned, one round, no head.  Lane l owns kNP pieces of
+// P = 64/kNP contiguous bytes: piece p at p*(4096/kNP) + l*P.  kNP = 1 is the lane-contiguous
+// layout (each 16-B load instruction spans 4 KiB); kNP = 4 makes every load instruction read
+// 1 KiB contiguous (coalesced) at the price of a Horner shift over the (4096/kNP - P)-byte gap
+// between a lane's pieces (LDS slot 6).  Each wave walks blocks b, b+W, ... (W = waves in the
+// grid) with kDepth blocks of loads in flight ahead of the one it hashes.
+template <int kNP>
+__device__ __forceinline__ void load4k(u32x4 (&v)[4], const uint8_t* base, uint64_t stride, uint64_t b,
+                                       uint32_t lane) {
+  constexpr uint32_t P = 64u / kNP, gap = 4096u / kNP, per = 4u / kNP;
+  const uint8_t* blk = base + b * stride + lane * P;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    v[i] = *reinterpret_cast<const u32x4*>(blk + (i / per) * gap + (i % per) * 16u);
+}
+
+template <int kNP>
+__device__ __forceinline__ uint32_t hash4k(const char* lds, const LaneTabs& lt, uint32_t lane,
+                                           uint32_t c, const u32x4 (&v)[4]) {
+  const uint32_t d[16] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w,
+                          v[2].x, v[2].y, v[2].z, v[2].w, v[3].x, v[3].y, v[3].z, v[3].w};
+  constexpr int per = 16 / kNP;  // dwords per piece
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    if (i && (i % per) == 0) c = shift_op(lds, PDB_SLOT_HORNER, c);
+    c = step4(lds, lt, c, d[i]);
+  }
+  return wave_tree(lds, lane, c);
+}
+
+template <int kNP, int kDepth>
+__global__ __launch_bounds__(kThreads) void crc_fast4k_kernel(
+    const uint32_t* __restrict__ tabs, const uint8_t* __restrict__ base, uint64_t stride,
+    uint64_t nblk, uint32_t flags, uint32_t init, uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
+  char* lds = reinterpret_cast<char*>(lds_words);
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWavesPerWg;
+  const uint64_t b0 = wave_id_uniform();
+  // Issue the first kDepth blocks' loads before staging the tables: the table copy then
+  // overlaps the first HBM round trip.
+  u32x4 buf[kDepth][4];
+#pragma unroll
+  for (int k = 0; k < kDepth; ++k) {
+    const uint64_t b = b0 + k * nw;
+    load4k<kNP>(buf[k], base, stride, b < nblk ? b : (nblk - 1), lane);
+  }
+  constexpr int kTree = kNP == 1 ? PDB_CAT_TREE64 : (kNP == 2 ? PDB_CAT_TREE32 : PDB_CAT_TREE16);
+  constexpr int kHorner = kNP == 1 ? -1 : (kNP == 2 ? PDB_CAT_H2016 : PDB_CAT_H1008);
+  stage_tables<kTree, kHorner>(lds, tabs);
+  __syncthreads();
+  const LaneTabs lt = lane_tabs(lane);
+  const uint32_t init_raw = (flags & PDB_CRC_USE_INIT) ? ~init : 0xFFFFFFFFu;
+  for (uint64_t b = b0; b < nblk; b += kDepth * nw) {
+#pragma unroll
+    for (int k = 0; k < kDepth; ++k) {
+      const uint64_t bk = b + k * nw;
+      if (bk >= nblk) return;  // wave-uniform
+      u32x4 cur[4] = {buf[k][0], buf[k][1], buf[k][2], buf[k][3]};
+      const uint64_t bn = bk + kDepth * nw;
+      load4k<kNP>(buf[k], base, stride, bn < nblk ? bn : bk, lane);  // clamp: valid block
+      const uint32_t c = hash4k<kNP>(lds, lt, lane, lane == 0 ? init_raw : 0u, cur);
+      if (lane == 0) out[bk] = finalize(c, flags);
+    }
+  }
+}
+
+// ---- fixed-stride batch, generic (any length / alignment) ---------------------------------------
 __global__ __launch_bounds__(kThreads) void crc_fixed_kernel(
     const uint32_t* __restrict__ tabs, const uint8_t* __restrict__ base, uint64_t stride,
     uint32_t len, uint64_t nblk, uint32_t flags, uint32_t init, uint32_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
   char* lds = reinterpret_cast<char*>(lds_words);
-  stage_tables(lds, tabs);
+  stage_tables<PDB_CAT_TREE64, PDB_CAT_H4032>(lds, tabs);
   __syncthreads();
-
   const uint32_t lane = threadIdx.x & 63u;
   const LaneTabs lt = lane_tabs(lane);
   const uint64_t nwaves = static_cast<uint64_t>(gridDim.x) * kWavesPerWg;
   const uint32_t init_raw = (flags & PDB_CRC_USE_INIT) ? ~init : 0xFFFFFFFFu;
-
-  if constexpr (kFast4K) {
-    // len == 4096, base and stride 16-B aligned: lane l owns bytes [64l, 64l+64), one round.
-    uint64_t b = wave_id_uniform();
-    if (b >= nblk) return;
-    const u32x4* src = reinterpret_cast<const u32x4*>(base + b * stride + lane * 64u);
-    u32x4 c0 = src[0], c1 = src[1], c2 = src[2], c3 = src[3];
-    for (; b < nblk; b += nwaves) {
-      const uint64_t bn = (b + nwaves < nblk) ? b + nwaves : b;  // clamp: always a valid block
-      const u32x4* nsrc = reinterpret_cast<const u32x4*>(base + bn * stride + lane * 64u);
-      const u32x4 n0 = nsrc[0], n1 = nsrc[1], n2 = nsrc[2], n3 = nsrc[3];
-      uint32_t c = (lane == 0) ? init_raw : 0u;
-      const uint32_t d[16] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w,
-                              c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
-      c = chain16(lds, lt, c, d);
-      c = wave_tree(lds, lane, c);
-      if (lane == 0) out[b] = finalize(c, flags);
-      c0 = n0;
-      c1 = n1;
-      c2 = n2;
-      c3 = n3;
-    }
-  } else {
-    for (uint64_t b = wave_id_uniform(); b < nblk; b += nwaves) {
-      const uint32_t c = crc_block(lds, lt, lane, base + b * stride, len, init_raw);
-      if (lane == 0) out[b] = finalize(c, flags);
-    }
+  for (uint64_t b = wave_id_uniform(); b < nblk; b += nwaves) {
+    const uint32_t c = crc_block(lds, lt, lane, base + b * stride, len, init_raw);
+    if (lane == 0) out[b] = finalize(c, flags);
   }
 }
 
@@ -242,7 +290,7 @@ __global__ __launch_bounds__(kThreads) void crc_desc_kernel(
     uint32_t* __restrict__ nbad) {
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
   char* lds = reinterpret_cast<char*>(lds_words);
-  stage_tables(lds, tabs);
+  stage_tables<PDB_CAT_TREE64, PDB_CAT_H4032>(lds, tabs);
   __syncthreads();
 
   const uint32_t lane = threadIdx.x & 63u;
@@ -274,7 +322,7 @@ __global__ __launch_bounds__(kThreads) void sst_kernel(const uint32_t* __restric
                                                         uint32_t* __restrict__ nbad) {
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
   char* lds = reinterpret_cast<char*>(lds_words);
-  stage_tables(lds, tabs);
+  stage_tables<PDB_CAT_TREE64, PDB_CAT_H4032>(lds, tabs);
   __syncthreads();
 
   const uint32_t lane = threadIdx.x & 63u;
@@ -321,15 +369,45 @@ __global__ __launch_bounds__(256) void read_stream_kernel(const u32x4* __restric
   if ((threadIdx.x & 63) == 0) atomicXor(out, r);
 }
 
+// Load-pattern calibration for 4-KiB blocks, no CRC work.
+//   kPat 0: lane l reads bytes [64l, 64l+64) of the block (the fast path's pattern)
+//   kPat 1: lane l reads 16 B at 16l + 1024j, j = 0..3 (each instruction 1 KiB contiguous)
+//   kDepth: blocks in flight per wave; kAssign 0: wave-interleaved blocks, 1: contiguous per WG
+template <int kPat, int kDepth, int kAssign>
 __global__ __launch_bounds__(kThreads) void read_pattern4k_kernel(const uint8_t* __restrict__ base,
                                                                   uint64_t nblk,
                                                                   uint32_t* __restrict__ out) {
   const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t nwaves = static_cast<uint64_t>(gridDim.x) * kWavesPerWg;
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWavesPerWg;
   uint32_t acc = 0;
-  for (uint64_t b = wave_id_uniform(); b < nblk; b += nwaves) {
-    const u32x4* src = reinterpret_cast<const u32x4*>(base + b * 4096u + lane * 64u);
-    const u32x4 x = src[0] ^ src[1] ^ src[2] ^ src[3];
+  uint64_t first, step, last;
+  if constexpr (kAssign == 0) {
+    first = wave_id_uniform();
+    step = nw;
+    last = nblk;
+  } else {
+    const uint64_t per = (nblk + gridDim.x - 1) / gridDim.x;
+    const uint64_t lo = blockIdx.x * per;
+    first = lo + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    step = kWavesPerWg;
+    last = lo + per < nblk ? lo + per : nblk;
+  }
+  for (uint64_t b = first; b < last; b += step * kDepth) {
+    u32x4 x = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < kDepth; ++k) {
+      const uint64_t bk = b + k * step;
+      if (bk < last) {
+        const uint8_t* blk = base + bk * 4096u;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t off = kPat == 0 ? lane * 64u + j * 16u
+                             : (kPat == 1 ? lane * 16u + j * 1024u
+                                          : lane * 32u + (j >> 1) * 2048u + (j & 1) * 16u);
+          x ^= *reinterpret_cast<const u32x4*>(blk + off);
+        }
+      }
+    }
     acc ^= x.x ^ x.y ^ x.z ^ x.w;
   }
   for (int k = 32; k; k >>= 1) acc ^= __shfl_xor(acc, k, 64);
@@ -374,6 +452,8 @@ uint32_t grid_for(const LaunchGeom& g, uint64_t nblk) {
 
 }  // namespace
 
+int g_fast_variant = 0;  // diagnostics: pdb_diag_set_variant()
+
 hipError_t launch_fixed(const LaunchGeom& g, const uint32_t* d_tables, const uint8_t* base,
                         uint64_t stride, uint32_t len, uint64_t nblk, uint32_t flags, uint32_t init,
                         uint32_t* out, hipStream_t s) {
@@ -381,12 +461,20 @@ hipError_t launch_fixed(const LaunchGeom& g, const uint32_t* d_tables, const uin
   const dim3 grid(grid_for(g, nblk)), block(kThreads);
   const bool fast = len == 4096u && (reinterpret_cast<uintptr_t>(base) & 15u) == 0 &&
                     (stride & 15u) == 0;
-  if (fast)
-    hipLaunchKernelGGL(crc_fixed_kernel<true>, grid, block, 0, s, d_tables, base, stride, len, nblk,
+  if (!fast) {
+    hipLaunchKernelGGL(crc_fixed_kernel, grid, block, 0, s, d_tables, base, stride, len, nblk,
                        flags, init, out);
-  else
-    hipLaunchKernelGGL(crc_fixed_kernel<false>, grid, block, 0, s, d_tables, base, stride, len,
-                       nblk, flags, init, out);
+    return hipGetLastError();
+  }
+#define PDB_FAST(NP, D)                                                                      \
+  hipLaunchKernelGGL((crc_fast4k_kernel<NP, D>), grid, block, 0, s, d_tables, base, stride, nblk, \
+                     flags, init, out)
+  switch (g_fast_variant) {
+    case 1: PDB_FAST(1, 1); break;
+    case 2: PDB_FAST(4, 1); break;
+    default: PDB_FAST(2, 1); break;  // measured best: 2 x 32-B pieces per lane, depth 1
+  }
+#undef PDB_FAST
   return hipGetLastError();
 }
 
@@ -426,8 +514,23 @@ hipError_t launch_read_stream(const uint8_t* base, uint64_t nbytes, uint32_t* ou
 }
 
 hipError_t launch_read_pattern4k(const LaunchGeom& g, const uint8_t* base, uint64_t nblk,
-                                 uint32_t* out, hipStream_t s) {
-  hipLaunchKernelGGL(read_pattern4k_kernel, dim3(g.grid), dim3(kThreads), 0, s, base, nblk, out);
+                                 int variant, uint32_t* out, hipStream_t s) {
+  const dim3 grid(g.grid), block(kThreads);
+#define PDB_RP(P, D, A) \
+  hipLaunchKernelGGL((read_pattern4k_kernel<P, D, A>), grid, block, 0, s, base, nblk, out)
+  switch (variant) {
+    case 1: PDB_RP(1, 1, 0); break;
+    case 2: PDB_RP(0, 2, 0); break;
+    case 3: PDB_RP(1, 2, 0); break;
+    case 4: PDB_RP(0, 1, 1); break;
+    case 5: PDB_RP(1, 1, 1); break;
+    case 6: PDB_RP(1, 4, 0); break;
+    case 7: PDB_RP(0, 4, 0); break;
+    case 8: PDB_RP(2, 1, 0); break;
+    case 9: PDB_RP(2, 2, 0); break;
+    default: PDB_RP(0, 1, 0); break;
+  }
+#undef PDB_RP
   return hipGetLastError();
 }
 

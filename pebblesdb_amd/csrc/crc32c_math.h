@@ -40,16 +40,27 @@ PDB_HD uint32_t pdb_unmask(uint32_t m) {
 //     ((k >> 1) << 16) | (b << 8) | ((k & 1) << 7) | (r << 2)
 // i.e. the data byte lands in address bits 8..15, so one v_perm_b32 builds the address.
 //
-// OPS region [0x20000, 0x20000 + PDB_NOPS*4096): shift operators (4 x 256 u32 each, one copy).
-//   op k (k = 0..5): shift by 64 << k bytes (wave tree combine: 64, 128, ..., 2048)
-//   op 6:            shift by 63*64 = 4032 bytes (per-lane Horner step between rounds)
+// OPS region [0x20000, 0x20000 + PDB_NOPS*4096): PDB_NOPS = 7 operator slots (4 x 256 u32
+// each, one copy).  Slots 0..5 hold the wave-tree operators "shift by P << k bytes" (P = bytes a
+// lane owns contiguously: 64, 32 or 16 depending on the kernel's load pattern); slot 6 holds the
+// per-lane Horner operator (the gap between two pieces a lane owns).  Each kernel stages the
+// operators it needs from the catalog below.
 #define PDB_LANES 64
-#define PDB_CHUNK 64 /* bytes per lane per round */
+#define PDB_CHUNK 64 /* bytes per lane per round in the generic kernel */
 #define PDB_MAIN_BYTES 0x20000u
 #define PDB_NOPS 7
-#define PDB_OP_TREE0 0
-#define PDB_OP_HORNER 6
+#define PDB_SLOT_HORNER 6
 #define PDB_OPS_BYTES (PDB_NOPS * 4096u)
 #define PDB_LDS_BYTES (PDB_MAIN_BYTES + PDB_OPS_BYTES) /* 159744 <= 163840 */
-/* Device table source: T0..T3 (1024 u32) then ops (PDB_NOPS * 1024 u32). */
-#define PDB_TABLE_WORDS (1024u + PDB_NOPS * 1024u)
+/* Operator catalog (device table source): distance in bytes of catalog entry i. */
+#define PDB_NCAT 11
+#define PDB_CAT_TREE16 0   /* 16, 32, ..., 512   (entries 0..5) */
+#define PDB_CAT_TREE32 1   /* 32, ..., 1024      (entries 1..6) */
+#define PDB_CAT_TREE64 2   /* 64, ..., 2048      (entries 2..7) */
+#define PDB_CAT_H1008 8    /* 1024 - 16: 4 x 16-B pieces per lane per 4 KiB */
+#define PDB_CAT_H2016 9    /* 2048 - 32: 2 x 32-B pieces per lane per 4 KiB */
+#define PDB_CAT_H4032 10   /* 4096 - 64: generic kernel, rounds of 64 x 64 B */
+static const unsigned long long kPdbCatDist[PDB_NCAT] = {16,   32,   64,   128,  256, 512,
+                                                           1024, 2048, 1008, 2016, 4032};
+/* Device table source: T0..T3 (1024 u32) then the catalog (PDB_NCAT * 1024 u32). */
+#define PDB_TABLE_WORDS (1024u + PDB_NCAT * 1024u)

@@ -64,7 +64,7 @@ uint32_t host_shift(uint32_t c, uint64_t nbytes) {
   return mat_vec(mat_pow(one_zero_byte(t0), nbytes), c);
 }
 
-// Fills `out` (PDB_TABLE_WORDS u32): [T0|T1|T2|T3] then PDB_NOPS operators, each laid out as
+// Fills `out` (PDB_TABLE_WORDS u32): [T0|T1|T2|T3] then the PDB_NCAT catalog operators, each as
 // 4 sub-tables j=0..3 of 256 entries: op[j][b] = shift(b << 8j, D).
 void build_device_tables(uint32_t* out) {
   uint32_t t[4][256];
@@ -74,11 +74,8 @@ void build_device_tables(uint32_t* out) {
   memcpy(out, t, sizeof(t));
 
   const Gf2Mat z1 = one_zero_byte(t[0]);
-  uint64_t dist[PDB_NOPS];
-  for (int k = 0; k < 6; ++k) dist[PDB_OP_TREE0 + k] = (uint64_t)PDB_CHUNK << k;
-  dist[PDB_OP_HORNER] = (uint64_t)(PDB_LANES - 1) * PDB_CHUNK;
-  for (int o = 0; o < PDB_NOPS; ++o) {
-    Gf2Mat m = mat_pow(z1, dist[o]);
+  for (int o = 0; o < PDB_NCAT; ++o) {
+    Gf2Mat m = mat_pow(z1, kPdbCatDist[o]);
     uint32_t* op = out + 1024 + o * 1024;
     for (int j = 0; j < 4; ++j)
       for (uint32_t b = 0; b < 256; ++b) op[j * 256 + b] = mat_vec(m, b << (8 * j));

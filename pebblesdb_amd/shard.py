@@ -31,3 +31,20 @@ def byte_balanced_ranges(lens, world: int) -> list[tuple[int, int]]:
     cuts.append(lens.size)
     cuts = np.maximum.accumulate(np.minimum(np.array(cuts), lens.size))
     return [(int(cuts[r]), int(cuts[r + 1])) for r in range(world)]
+
+
+def scatter_block_ranges(n_total: int, world: int, rank: int, device, dist=None,
+                         lens=None) -> tuple[int, int]:
+    """Rank 0 computes every rank's [lo, hi) (by count, or by bytes when `lens` is given) and
+    broadcasts the small index over the process group -- the only collective on this path
+    (RCCL over xGMI on GPUs, gloo in the CPU tests).  Returns this rank's range."""
+    import torch
+
+    idx = torch.zeros(world, 2, dtype=torch.int64, device=device)
+    if rank == 0:
+        rngs = (byte_balanced_ranges(lens, world) if lens is not None
+                else [block_range(n_total, world, r) for r in range(world)])
+        idx.copy_(torch.tensor(rngs, dtype=torch.int64))
+    if dist is not None and world > 1:
+        dist.broadcast(idx, src=0)
+    return int(idx[rank, 0]), int(idx[rank, 1])

@@ -1,0 +1,92 @@
+"""CPU: block-range sharding and the multi-rank index scatter, world_size 2 over
+gloo (the GPU run uses the same code over RCCL).  The per-rank CRC here is the oracle -- these
+tests check the partitioning and the checksum-of-checksums, not the kernel."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from pebblesdb_amd.shard import block_range, byte_balanced_ranges, scatter_block_ranges
+
+
+@pytest.mark.parametrize("n,world", [(0, 1), (1, 2), (7, 8), (1 << 20, 8), (33554432, 8), (1000, 3)])
+def test_block_range_partitions(n, world):
+    rs = [block_range(n, world, r) for r in range(world)]
+    assert rs[0][0] == 0 and rs[-1][1] == n
+    for (a, b), (c, d) in zip(rs, rs[1:]):
+        assert b == c and a <= b
+    sizes = [b - a for a, b in rs]
+    assert max(sizes) - min(sizes) <= 1
+
+
+def test_byte_balanced_ranges():
+    rng = np.random.Generator(np.random.PCG64(1))
+    lens = (rng.choice(np.arange(1, 65), size=5000, p=(1 / np.arange(1, 65)) / np.sum(1 / np.arange(1, 65))) * 1024)
+    for world in (1, 2, 4, 8):
+        rs = byte_balanced_ranges(lens, world)
+        assert rs[0][0] == 0 and rs[-1][1] == len(lens)
+        for (a, b), (c, d) in zip(rs, rs[1:]):
+            assert b == c
+        tot = [int(lens[a:b].sum()) for a, b in rs]
+        assert max(tot) - min(tot) <= 2 * int(lens.max())
+    assert byte_balanced_ranges([], 4) == [(0, 0)] * 4
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, n_total, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import oracle
+
+    lo, hi = scatter_block_ranges(n_total, world, rank, torch.device("cpu"), dist)
+    L = 4096
+    data = oracle.splitmix_bytes((hi - lo) * L, 301, lo * L)
+    blk = np.zeros(hi - lo, dtype=oracle.BLK_DTYPE)
+    blk["off"] = np.arange(hi - lo) * L
+    blk["len"] = L
+    crcs = oracle.Oracle().batch(data, blk)
+    x = torch.tensor([int(np.bitwise_xor.reduce(crcs)) if len(crcs) else 0], dtype=torch.int64)
+    allx = [torch.zeros_like(x) for _ in range(world)]
+    dist.all_gather(allx, x)
+    if rank == 0:
+        v = 0
+        for t in allx:
+            v ^= int(t.item())
+        q.put(("xor", v))
+    q.put(("range", rank, lo, hi))
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_shards_cover_and_checksum_matches(oracle_lib):
+    n_total, world = 3000, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, n_total, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(120)
+        assert p.exitcode == 0
+    msgs = [q.get(timeout=10) for _ in range(world + 1)]
+    ranges = sorted((m[1], m[2], m[3]) for m in msgs if m[0] == "range")
+    assert ranges == [(0, 0, 1500), (1, 1500, 3000)]
+    xor = next(m[1] for m in msgs if m[0] == "xor")
+    import oracle
+
+    data = oracle.splitmix_bytes(n_total * 4096, 301)
+    blk = np.zeros(n_total, dtype=oracle.BLK_DTYPE)
+    blk["off"] = np.arange(n_total) * 4096
+    blk["len"] = 4096
+    assert xor == int(np.bitwise_xor.reduce(oracle_lib.batch(data, blk, nthreads=4)))

@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""Summarise tools/profile.sh output: per-kernel average duration (kernel-trace) and HBM bytes
+per launch from FETCH_SIZE / WRITE_SIZE (rocprofv3 PMC, KB units).
+
+gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE reports 1/2 of the bytes of a wide
+16-B/lane streaming read.  We calibrate the factor on the diag kernel read_pattern4k, which
+issues exactly the fast path's loads over a known byte count, and apply it to the CRC kernel.
+"""
+import csv
+import glob
+import json
+import os
+import statistics
+import sys
+
+out_dir, workload = sys.argv[1], (sys.argv[2] if len(sys.argv) > 2 else "c2")
+KERNELS = {"c2": "crc_fast4k_kernel", "sstable": "crc_fixed_kernel", "c3": "crc_desc_kernel"}
+target = KERNELS[workload]
+
+
+def rows(pattern):
+    for f in glob.glob(os.path.join(out_dir, pattern), recursive=True):
+        with open(f) as fh:
+            yield from csv.DictReader(fh)
+
+
+def kname(r):
+    return r.get("Kernel_Name") or r.get("KernelName") or r.get("Name") or ""
+
+
+def durations(sub):
+    d = []
+    for r in rows("trace/**/*kernel_trace.csv"):
+        if sub in kname(r):
+            d.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)  # ns -> ms
+    return d
+
+
+def counter(name, sub):
+    v = []
+    for r in rows(f"pmc_*/**/*counter_collection.csv"):
+        if r.get("Counter_Name") == name and sub in kname(r):
+            v.append(float(r["Counter_Value"]))
+    return v
+
+
+res = {}
+dur = durations(target)
+fetch = counter("FETCH_SIZE", target)
+write = counter("WRITE_SIZE", target)
+cal_fetch = counter("FETCH_SIZE", "read_pattern4k_kernel")
+# known bytes for the calibration kernel: the whole buffer (bench allocs it; read from its log)
+known = None
+try:
+    with open(os.path.join(out_dir, "trace.log")) as fh:
+        for ln in fh:
+            if ln.startswith("{"):
+                known = json.loads(ln)["config"]["bytes_per_gpu"]
+except (OSError, ValueError, KeyError):
+    pass
+factor = 2.0
+if cal_fetch and known:
+    factor = known / (statistics.median(cal_fetch) * 1024.0)
+entry = {
+    "kernel": target,
+    "launches_traced": len(dur),
+    "avg_ms": round(statistics.mean(dur), 4) if dur else None,
+    "median_ms": round(statistics.median(dur), 4) if dur else None,
+    "fetch_size_kb_median": statistics.median(fetch) if fetch else None,
+    "write_size_kb_median": statistics.median(write) if write else None,
+    "fetch_correction_factor": round(factor, 4),
+    "fetch_calibration": "read_pattern4k_kernel (same loads, known bytes)" if cal_fetch and known else
+                         "MI355X_MICROARCH.md §HBM x2",
+}
+if fetch and write:
+    entry["hbm_bytes_per_launch"] = int(statistics.median(fetch) * 1024 * factor + statistics.median(write) * 1024)
+res[workload] = entry
+print(json.dumps(res, indent=1))
