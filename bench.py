@@ -121,6 +121,7 @@ def main():
         crc32c.fill_splitmix(data, 303 + rank)
         d_blk = crc32c.blocks_to_device(crc32c.make_blocks(offs, sizes), dev)
         nblk = n
+        L = stride = None
         algo_bytes_per_blk = None
         hashed = total
         out = torch.empty(nblk, dtype=torch.int32, device=dev)

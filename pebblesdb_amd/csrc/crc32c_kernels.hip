@@ -61,6 +61,21 @@ __device__ __forceinline__ uint32_t step4(const char* lds, const LaneTabs& lt, u
   return (lds_u32(lds, a3) ^ lds_u32(lds, a2)) ^ (lds_u32(lds, a1) ^ lds_u32(lds, a0));
 }
 
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // gfx950 v_bitop3_b32: a ^ b ^ c
+}
+
+// x' = shift(x, 4 bytes) ^ w_next: one slice-by-4 step whose input is already crc ^ word, with
+// the next word folded in (chains carry x = state ^ next data word).
+__device__ __forceinline__ uint32_t step4x(const char* lds, const LaneTabs& lt, uint32_t x,
+                                           uint32_t wnext) {
+  const uint32_t a3 = __builtin_amdgcn_perm(lt.t3, x, sel_byte(0));
+  const uint32_t a2 = __builtin_amdgcn_perm(lt.t2, x, sel_byte(1));
+  const uint32_t a1 = __builtin_amdgcn_perm(lt.t1, x, sel_byte(2));
+  const uint32_t a0 = __builtin_amdgcn_perm(lt.t0, x, sel_byte(3));
+  return xor3(xor3(lds_u32(lds, a3), lds_u32(lds, a2), lds_u32(lds, a1)), lds_u32(lds, a0), wnext);
+}
+
 // Byte step (util/crc32c.cc:601): c' = T0[(c ^ b) & 0xff] ^ (c >> 8).
 __device__ __forceinline__ uint32_t step1(const char* lds, const LaneTabs& lt, uint32_t c,
                                           uint32_t b) {
@@ -77,14 +92,33 @@ __device__ __forceinline__ uint32_t shift_op(const char* lds, uint32_t op, uint3
   return (v0 ^ v1) ^ (v2 ^ v3);
 }
 
-// Fold the 64 lane partials (lane v's partial ends P*(63-v) bytes before the region end, where
-// slots 0..5 hold "shift by P << k").  Result valid in lane 0.
-__device__ __forceinline__ uint32_t wave_tree(const char* lds, uint32_t lane, uint32_t c) {
-#pragma unroll
-  for (uint32_t k = 0; k < 6; ++k) {
-    const uint32_t y = __shfl_down(c, 1u << k, 64);
-    if ((lane & ((2u << k) - 1u)) == 0) c = shift_op(lds, k, c) ^ y;
-  }
+// shift(c, D_op) ^ y
+__device__ __forceinline__ uint32_t shift_op_x(const char* lds, uint32_t op, uint32_t c, uint32_t y) {
+  const uint32_t base = PDB_MAIN_BYTES + op * 4096u;
+  const uint32_t v0 = lds_u32(lds, base + ((c & 0xffu) << 2));
+  const uint32_t v1 = lds_u32(lds, base + 1024u + (((c >> 8) & 0xffu) << 2));
+  const uint32_t v2 = lds_u32(lds, base + 2048u + (((c >> 16) & 0xffu) << 2));
+  const uint32_t v3 = lds_u32(lds, base + 3072u + ((c >> 24) << 2));
+  return xor3(xor3(v0, v1, v2), v3, y);
+}
+
+// Same fold with the partner values moved by DPP (levels 0-3, row_shl), ds_swizzle (level 4,
+// xor 16 within 32-lane halves) and readlane (level 5): one LDS round trip fewer per level
+// than ds_bpermute.  Result valid in lane 0.
+__device__ __forceinline__ uint32_t wave_tree_dpp(const char* lds, uint32_t lane, uint32_t c) {
+  uint32_t y;
+  y = __builtin_amdgcn_update_dpp(0u, c, 0x101, 0xF, 0xF, false);  // row_shl:1
+  if ((lane & 1u) == 0) c = shift_op_x(lds, 0, c, y);
+  y = __builtin_amdgcn_update_dpp(0u, c, 0x102, 0xF, 0xF, false);  // row_shl:2
+  if ((lane & 3u) == 0) c = shift_op_x(lds, 1, c, y);
+  y = __builtin_amdgcn_update_dpp(0u, c, 0x104, 0xF, 0xF, false);  // row_shl:4
+  if ((lane & 7u) == 0) c = shift_op_x(lds, 2, c, y);
+  y = __builtin_amdgcn_update_dpp(0u, c, 0x108, 0xF, 0xF, false);  // row_shl:8
+  if ((lane & 15u) == 0) c = shift_op_x(lds, 3, c, y);
+  y = __builtin_amdgcn_ds_swizzle(c, 0x401F);  // bitmask mode: lane ^ 16 within 32
+  if ((lane & 31u) == 0) c = shift_op_x(lds, 4, c, y);
+  y = __builtin_amdgcn_readlane(c, 32);
+  if (lane == 0) c = shift_op_x(lds, 5, c, y);
   return c;
 }
 
@@ -106,7 +140,7 @@ __device__ __forceinline__ uint32_t ld32u(const uint8_t* q) {
 
 // Stage the table image into LDS: T0..T3 written 32x (8 x 16-B stores per entry); tree
 // operators catalog[kTree .. kTree+5] -> slots 0..5; catalog[kHorner] -> slot 6 (if >= 0).
-template <int kTree, int kHorner>
+template <int kTree, int kHorner, int kSlot7 = -1>
 __device__ __forceinline__ void stage_tables(char* lds, const uint32_t* __restrict__ tabs) {
   for (uint32_t i = threadIdx.x; i < 4u * 256u * 8u; i += blockDim.x) {
     const uint32_t k = i >> 11, b = (i >> 3) & 255u, part = i & 7u;
@@ -115,79 +149,13 @@ __device__ __forceinline__ void stage_tables(char* lds, const uint32_t* __restri
     *reinterpret_cast<u32x4*>(lds + addr) = u32x4{v, v, v, v};
   }
   const u32x4* cat = reinterpret_cast<const u32x4*>(tabs + 1024);
-  constexpr uint32_t nslots = kHorner >= 0 ? 7u : 6u;
+  constexpr uint32_t nslots = kSlot7 >= 0 ? 8u : (kHorner >= 0 ? 7u : 6u);
   for (uint32_t i = threadIdx.x; i < nslots * 256u; i += blockDim.x) {
     const uint32_t slot = i >> 8;
-    const uint32_t src = slot < 6 ? kTree + slot : static_cast<uint32_t>(kHorner);
+    const uint32_t src = slot < 6 ? kTree + slot
+                                  : (slot == 6 ? static_cast<uint32_t>(kHorner) : static_cast<uint32_t>(kSlot7));
     *reinterpret_cast<u32x4*>(lds + PDB_MAIN_BYTES + i * 16u) = cat[src * 256u + (i & 255u)];
   }
-}
-
-// 16 dwords of the 64-B chunk at q.  `s` = q & 3 (uniform across the wave for one block).
-__device__ __forceinline__ void load_chunk(uint32_t d[16], const uint8_t* q, uint32_t s) {
-  if (s == 0) {
-    const u32x4a4* v = reinterpret_cast<const u32x4a4*>(q);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const u32x4a4 x = v[i];
-      d[4 * i + 0] = x.x;
-      d[4 * i + 1] = x.y;
-      d[4 * i + 2] = x.z;
-      d[4 * i + 3] = x.w;
-    }
-  } else {
-    const uint8_t* a = q - s;
-    const u32x4a4* v = reinterpret_cast<const u32x4a4*>(a);
-    uint32_t e[17];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const u32x4a4 x = v[i];
-      e[4 * i + 0] = x.x;
-      e[4 * i + 1] = x.y;
-      e[4 * i + 2] = x.z;
-      e[4 * i + 3] = x.w;
-    }
-    e[16] = *reinterpret_cast<const uint32_t*>(a + 64);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) d[i] = __builtin_amdgcn_alignbyte(e[i + 1], e[i], s);
-  }
-}
-
-__device__ __forceinline__ uint32_t chain16(const char* lds, const LaneTabs& lt, uint32_t c,
-                                            const uint32_t d[16]) {
-#pragma unroll
-  for (int i = 0; i < 16; ++i) c = step4(lds, lt, c, d[i]);
-  return c;
-}
-
-// Raw state S(init_raw, p[0..n)) in lane 0 for one block of any length/alignment.
-__device__ uint32_t crc_block(const char* lds, const LaneTabs& lt, uint32_t lane, const uint8_t* p,
-                              uint32_t n, uint32_t init_raw) {
-  const uint32_t t = n & 63u;
-  const uint32_t K = n >> 6;
-  uint32_t c = 0;
-  if (lane == 0) {
-    c = init_raw;
-    uint32_t i = 0;
-    for (; i < (t & 3u); ++i) c = step1(lds, lt, c, p[i]);
-    for (; i < t; i += 4) c = step4(lds, lt, c, ld32u(p + i));
-  }
-  if (K == 0) return c;
-  const uint8_t* q0 = p + t;
-  const uint32_t s = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(q0) & 3u);
-  const uint32_t R = (K + 63u) >> 6;
-  for (uint32_t r = 0; r < R; ++r) {
-    const uint32_t ch = lane + (r << 6);
-    if (ch < K) {
-      if (r) c = shift_op(lds, PDB_SLOT_HORNER, c);
-      uint32_t d[16];
-      load_chunk(d, q0 + static_cast<uint64_t>(ch) * 64u, s);
-      c = chain16(lds, lt, c, d);
-    }
-  }
-  const uint32_t q = K & 63u;
-  if (q) c = __shfl(c, (lane + q) & 63u, 64);
-  return wave_tree(lds, lane, c);
 }
 
 __device__ __forceinline__ uint64_t wave_id_uniform() {
@@ -212,18 +180,27 @@ __device__ __forceinline__ void load4k(u32x4 (&v)[4], const uint8_t* base, uint6
     v[i] = *reinterpret_cast<const u32x4*>(blk + (i / per) * gap + (i % per) * 16u);
 }
 
+// The lane's 16 dwords are hashed as NCH independent slice-by-4 chains (ILP: half or a quarter
+// of the serial LDS round trips), then folded with the slot-6 operator "shift by the distance
+// between consecutive chain ends" (32 B for kNP=1, 2048 B for kNP=2, 1024 B for kNP=4).
 template <int kNP>
 __device__ __forceinline__ uint32_t hash4k(const char* lds, const LaneTabs& lt, uint32_t lane,
-                                           uint32_t c, const u32x4 (&v)[4]) {
+                                           uint32_t c0, const u32x4 (&v)[4]) {
   const uint32_t d[16] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w,
                           v[2].x, v[2].y, v[2].z, v[2].w, v[3].x, v[3].y, v[3].z, v[3].w};
-  constexpr int per = 16 / kNP;  // dwords per piece
+  constexpr int NCH = kNP == 1 ? 2 : kNP;
+  constexpr int per = 16 / NCH;
+  uint32_t x[NCH];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    if (i && (i % per) == 0) c = shift_op(lds, PDB_SLOT_HORNER, c);
-    c = step4(lds, lt, c, d[i]);
-  }
-  return wave_tree(lds, lane, c);
+  for (int ch = 0; ch < NCH; ++ch) x[ch] = (ch == 0 ? c0 : 0u) ^ d[ch * per];
+#pragma unroll
+  for (int i = 1; i <= per; ++i)
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) x[ch] = step4x(lds, lt, x[ch], i < per ? d[ch * per + i] : 0u);
+  uint32_t c = x[0];
+#pragma unroll
+  for (int ch = 1; ch < NCH; ++ch) c = shift_op_x(lds, PDB_SLOT_HORNER, c, x[ch]);
+  return wave_tree_dpp(lds, lane, c);
 }
 
 template <int kNP, int kDepth>
@@ -244,7 +221,7 @@ __global__ __launch_bounds__(kThreads) void crc_fast4k_kernel(
     load4k<kNP>(buf[k], base, stride, b < nblk ? b : (nblk - 1), lane);
   }
   constexpr int kTree = kNP == 1 ? PDB_CAT_TREE64 : (kNP == 2 ? PDB_CAT_TREE32 : PDB_CAT_TREE16);
-  constexpr int kHorner = kNP == 1 ? -1 : (kNP == 2 ? PDB_CAT_H2016 : PDB_CAT_H1008);
+  constexpr int kHorner = kNP == 1 ? PDB_CAT_TREE32 : (kNP == 2 ? PDB_CAT_S2048 : PDB_CAT_S1024);
   stage_tables<kTree, kHorner>(lds, tabs);
   __syncthreads();
   const LaneTabs lt = lane_tabs(lane);
@@ -263,92 +240,300 @@ __global__ __launch_bounds__(kThreads) void crc_fast4k_kernel(
   }
 }
 
-// ---- fixed-stride batch, generic (any length / alignment) ---------------------------------------
-__global__ __launch_bounds__(kThreads) void crc_fixed_kernel(
-    const uint32_t* __restrict__ tabs, const uint8_t* __restrict__ base, uint64_t stride,
-    uint32_t len, uint64_t nblk, uint32_t flags, uint32_t init, uint32_t* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
-  char* lds = reinterpret_cast<char*>(lds_words);
-  stage_tables<PDB_CAT_TREE64, PDB_CAT_H4032>(lds, tabs);
-  __syncthreads();
-  const uint32_t lane = threadIdx.x & 63u;
-  const LaneTabs lt = lane_tabs(lane);
-  const uint64_t nwaves = static_cast<uint64_t>(gridDim.x) * kWavesPerWg;
-  const uint32_t init_raw = (flags & PDB_CRC_USE_INIT) ? ~init : 0xFFFFFFFFu;
-  for (uint64_t b = wave_id_uniform(); b < nblk; b += nwaves) {
-    const uint32_t c = crc_block(lds, lt, lane, base + b * stride, len, init_raw);
-    if (lane == 0) out[b] = finalize(c, flags);
+// ---- fixed-stride batch, 4-KiB team path ----------------------------------------------------
+// A wave hashes T = 64/kG consecutive 4-KiB blocks at once: team t (lanes [t*kG, (t+1)*kG))
+// owns block t.  Within a team, lane u owns R = 4096/(32*kG) pieces of 32 B, piece r at
+// r*32*kG + 32*u, so every 16-B load instruction covers T blocks x kG lanes at a 32-B lane
+// stride.  Each piece is an independent 8-step chain; the R chains fold with "shift by
+// 32*kG bytes" (slot 6), then a log2(kG)-level team tree (slots 0.., shift by 32 << k) whose
+// VALU/LDS instructions serve all T blocks at once -- the per-block tree cost drops by T.
+template <int kG>
+__device__ __forceinline__ uint32_t team_tree(const char* lds, uint32_t u, uint32_t c) {
+  uint32_t y;
+  y = __builtin_amdgcn_update_dpp(0u, c, 0x101, 0xF, 0xF, false);
+  if ((u & 1u) == 0) c = shift_op_x(lds, 0, c, y);
+  y = __builtin_amdgcn_update_dpp(0u, c, 0x102, 0xF, 0xF, false);
+  if ((u & 3u) == 0) c = shift_op_x(lds, 1, c, y);
+  y = __builtin_amdgcn_update_dpp(0u, c, 0x104, 0xF, 0xF, false);
+  if ((u & 7u) == 0) c = shift_op_x(lds, 2, c, y);
+  y = __builtin_amdgcn_update_dpp(0u, c, 0x108, 0xF, 0xF, false);
+  if ((u & 15u) == 0) c = shift_op_x(lds, 3, c, y);
+  if constexpr (kG >= 32) {
+    y = __builtin_amdgcn_ds_swizzle(c, 0x401F);
+    if ((u & 31u) == 0) c = shift_op_x(lds, 4, c, y);
   }
+  if constexpr (kG >= 64) {
+    y = __builtin_amdgcn_readlane(c, 32);
+    if (u == 0) c = shift_op_x(lds, 5, c, y);
+  }
+  return c;
 }
 
-// ---- descriptor batch (variable length, any alignment); optional verify ---------------------
-template <int kMode>
-__global__ __launch_bounds__(kThreads) void crc_desc_kernel(
-    const uint32_t* __restrict__ tabs, const uint8_t* __restrict__ base,
-    const pdb_blk* __restrict__ blk, uint64_t nblk, uint32_t flags,
-    const uint32_t* __restrict__ expected, uint32_t* __restrict__ out, uint8_t* __restrict__ ok,
-    uint32_t* __restrict__ nbad) {
+template <int kG, int kDepth>
+__global__ __launch_bounds__(kThreads) void crc_team4k_kernel(
+    const uint32_t* __restrict__ tabs, const uint8_t* __restrict__ base, uint64_t stride,
+    uint64_t nblk, uint32_t flags, uint32_t init, uint32_t* __restrict__ out) {
+  constexpr uint32_t T = 64 / kG;             // blocks per wave-iteration
+  constexpr uint32_t R = 4096 / (32 * kG);    // 32-B pieces per lane per block
+  constexpr uint32_t ROW = 32 * kG;           // bytes between a lane's pieces
+  constexpr int kFold = kG == 32 ? PDB_CAT_S1024 : (kG == 16 ? 5 /* 512 */ : PDB_CAT_S2048);
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
   char* lds = reinterpret_cast<char*>(lds_words);
-  stage_tables<PDB_CAT_TREE64, PDB_CAT_H4032>(lds, tabs);
-  __syncthreads();
-
   const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t t = lane / kG, u = lane % kG;
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWavesPerWg;
+  const uint64_t ngroups = (nblk + T - 1) / T;  // wave-iterations needed in total
+  const uint64_t g0 = wave_id_uniform();
+
+  auto load = [&](u32x4 (&v)[2 * R], uint64_t g) {
+    uint64_t b = g * T + t;
+    if (b >= nblk) b = nblk - 1;  // clamp: a valid block (result discarded)
+    const uint8_t* p = base + b * stride + u * 32u;
+#pragma unroll
+    for (uint32_t r = 0; r < R; ++r) {
+      v[2 * r] = *reinterpret_cast<const u32x4*>(p + r * ROW);
+      v[2 * r + 1] = *reinterpret_cast<const u32x4*>(p + r * ROW + 16u);
+    }
+  };
+
+  u32x4 nxt[2 * R];
+  if constexpr (kDepth > 0) load(nxt, g0 < ngroups ? g0 : 0);
+  stage_tables<PDB_CAT_TREE32, kFold>(lds, tabs);
+  __syncthreads();
   const LaneTabs lt = lane_tabs(lane);
-  const uint64_t nwaves = static_cast<uint64_t>(gridDim.x) * kWavesPerWg;
-  for (uint64_t i = wave_id_uniform(); i < nblk; i += nwaves) {
-    const pdb_blk d = blk[i];
-    const uint32_t init_raw = (flags & PDB_CRC_USE_INIT) ? ~d.init : 0xFFFFFFFFu;
-    const uint32_t c = crc_block(lds, lt, lane, base + d.off, d.len, init_raw);
-    if (lane == 0) {
-      const uint32_t v = finalize(c, flags);
-      if constexpr (kMode == kModeOut) {
-        out[i] = v;
-      } else {
-        const bool good = (v == expected[i]);
-        if (ok) ok[i] = good ? 1 : 0;
-        if (!good && nbad) atomicAdd(nbad, 1u);
+  const uint32_t init_raw = (flags & PDB_CRC_USE_INIT) ? ~init : 0xFFFFFFFFu;
+  for (uint64_t g = g0; g < ngroups; g += nw) {
+    u32x4 cur[2 * R];
+    if constexpr (kDepth > 0) {
+#pragma unroll
+      for (uint32_t i = 0; i < 2 * R; ++i) cur[i] = nxt[i];
+      const uint64_t gn = g + nw;
+      load(nxt, gn < ngroups ? gn : g);
+    } else {
+      load(cur, g);
+    }
+    uint32_t x[R];
+#pragma unroll
+    for (uint32_t r = 0; r < R; ++r) x[r] = cur[2 * r].x ^ ((r == 0 && u == 0) ? init_raw : 0u);
+#pragma unroll
+    for (int i = 1; i <= 8; ++i) {
+#pragma unroll
+      for (uint32_t r = 0; r < R; ++r) {
+        const u32x4& a = cur[2 * r];
+        const u32x4& bq = cur[2 * r + 1];
+        const uint32_t w = i == 1 ? a.y : i == 2 ? a.z : i == 3 ? a.w : i == 4 ? bq.x
+                         : i == 5 ? bq.y : i == 6 ? bq.z : i == 7 ? bq.w : 0u;
+        x[r] = step4x(lds, lt, x[r], w);
       }
     }
+    uint32_t c = x[0];
+#pragma unroll
+    for (uint32_t r = 1; r < R; ++r) c = shift_op_x(lds, PDB_SLOT_HORNER, c, x[r]);
+    c = team_tree<kG>(lds, u, c);
+    const uint64_t b = g * T + t;
+    if (u == 0 && b < nblk) out[b] = finalize(c, flags);
   }
 }
 
-// ---- sstable trailers: seal (write) or verify (read) ----------------------------------------
-template <bool kSeal>
-__global__ __launch_bounds__(kThreads) void sst_kernel(const uint32_t* __restrict__ tabs,
-                                                        uint8_t* __restrict__ buf,
-                                                        const pdb_block_handle* __restrict__ h,
-                                                        uint64_t n, uint8_t* __restrict__ ok,
-                                                        uint32_t* __restrict__ nbad) {
+// ---- generic stream kernel: any length, any alignment, fixed-stride / descriptors / sstable --
+// One wave per block; the wave walks its blocks (i, i+W, ...) and each block's rounds as one
+// software-pipelined stream of items: while item (i, r) is hashed, item (i, r+1) -- or round 0
+// of the next block, with its descriptor and head words -- is already loading.
+//   block of n bytes = head (t = n % 32 bytes) + K = n / 32 pieces of 32 B at p + t + 32c;
+//   piece c -> lane c % 64, j = c / 64; a round is 4 KiB: lane u hashes pieces j = 2r (at
+//   4096r + 32u) and 2r+1 (2048 higher) as two independent chains, folded with "shift 2048"
+//   (slot 7); rounds chain per lane with "shift 2016" (slot 6) -- the 4-KiB fast path's
+//   geometry generalised.  The head is hashed by every lane (broadcast words) from the Extend
+//   seed and becomes lane 0's starting state; lanes are rotated when K % 64 != 0 so lane v's
+//   partial ends 32*(63-v) bytes before the end; then the 6-level DPP tree (slots 0..5: 32 << k).
+struct BlkDesc {
+  const uint8_t* p;
+  uint32_t n;
+  uint32_t init_raw;  // ~Extend seed
+};
+
+struct FixedSrc {
+  const uint8_t* base;
+  uint64_t stride;
+  uint32_t len;
+  uint32_t init_raw;
+  __device__ __forceinline__ BlkDesc get(uint64_t i) const { return {base + i * stride, len, init_raw}; }
+};
+
+struct DescSrc {
+  const uint8_t* base;
+  const pdb_blk* blk;
+  uint32_t flags;
+  __device__ __forceinline__ BlkDesc get(uint64_t i) const {
+    const pdb_blk d = blk[i];
+    return {base + d.off, d.len, (flags & PDB_CRC_USE_INIT) ? ~d.init : 0xFFFFFFFFu};
+  }
+};
+
+// sstable handle: CRC over contents || type (table/table_builder.cc:197-198; format.cc:98).
+struct SstSrc {
+  uint8_t* buf;
+  const pdb_block_handle* h;
+  __device__ __forceinline__ BlkDesc get(uint64_t i) const {
+    const pdb_block_handle x = h[i];
+    return {buf + x.offset, static_cast<uint32_t>(x.size + 1), 0xFFFFFFFFu};
+  }
+};
+
+struct OutSink {
+  uint32_t* out;
+  uint32_t flags;
+  __device__ __forceinline__ void put(uint64_t i, uint32_t raw, const BlkDesc&) const {
+    out[i] = finalize(raw, flags);
+  }
+};
+
+struct VerifySink {
+  const uint32_t* expected;
+  uint8_t* ok;
+  uint32_t* nbad;
+  uint32_t flags;
+  __device__ __forceinline__ void put(uint64_t i, uint32_t raw, const BlkDesc&) const {
+    const bool good = finalize(raw, flags) == expected[i];
+    if (ok) ok[i] = good ? 1 : 0;
+    if (!good && nbad) atomicAdd(nbad, 1u);
+  }
+};
+
+// Seal: EncodeFixed32(trailer + 1, Mask(crc)) at contents + size + 1 = p + n.
+struct SealSink {
+  __device__ __forceinline__ void put(uint64_t, uint32_t raw, const BlkDesc& d) const {
+    uint8_t* tr = const_cast<uint8_t*>(d.p) + d.n;
+    const uint32_t m = pdb_mask(~raw);
+    tr[0] = static_cast<uint8_t>(m);
+    tr[1] = static_cast<uint8_t>(m >> 8);
+    tr[2] = static_cast<uint8_t>(m >> 16);
+    tr[3] = static_cast<uint8_t>(m >> 24);
+  }
+};
+
+// ReadBlock's check: Unmask(DecodeFixed32(data + n + 1)) == crc (format.cc:96-104).
+struct SstVerifySink {
+  uint8_t* ok;
+  uint32_t* nbad;
+  __device__ __forceinline__ void put(uint64_t i, uint32_t raw, const BlkDesc& d) const {
+    const uint8_t* tr = d.p + d.n;
+    const uint32_t stored = static_cast<uint32_t>(tr[0]) | (static_cast<uint32_t>(tr[1]) << 8) |
+                            (static_cast<uint32_t>(tr[2]) << 16) | (static_cast<uint32_t>(tr[3]) << 24);
+    const bool good = pdb_unmask(stored) == ~raw;
+    if (ok) ok[i] = good ? 1 : 0;
+    if (!good && nbad) atomicAdd(nbad, 1u);
+  }
+};
+
+// Raw (possibly misaligned) 32-B piece: e[0..8] are the aligned dwords covering [q - s, q - s + 36).
+struct RawPiece {
+  uint32_t e[9];
+};
+
+__device__ __forceinline__ void issue_piece(RawPiece& r, const uint8_t* q, uint32_t s) {
+  const u32x4a4* v = reinterpret_cast<const u32x4a4*>(q - s);
+  const u32x4a4 x0 = v[0], x1 = v[1];
+  r.e[0] = x0.x; r.e[1] = x0.y; r.e[2] = x0.z; r.e[3] = x0.w;
+  r.e[4] = x1.x; r.e[5] = x1.y; r.e[6] = x1.z; r.e[7] = x1.w;
+  // the 9th dword holds the piece's last byte(s) only when misaligned (never past the block)
+  r.e[8] = s ? *reinterpret_cast<const uint32_t*>(q - s + 32) : 0u;
+}
+
+// Chain over one 32-B piece: returns shift(x0_state ^ piece ...), i.e. the raw state after the
+// piece starting from `start` (injected into the first word).
+__device__ __forceinline__ uint32_t chain_piece(const char* lds, const LaneTabs& lt, uint32_t start,
+                                                const RawPiece& r, uint32_t s) {
+  uint32_t w[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) w[j] = s ? __builtin_amdgcn_alignbyte(r.e[j + 1], r.e[j], s) : r.e[j];
+  uint32_t x = start ^ w[0];
+#pragma unroll
+  for (int j = 1; j <= 8; ++j) x = step4x(lds, lt, x, j < 8 ? w[j] : 0u);
+  return x;
+}
+
+template <class Src, class Sink>
+__global__ __launch_bounds__(kThreads) void crc_stream_kernel(const uint32_t* __restrict__ tabs,
+                                                               Src src, uint64_t nblk, Sink sink) {
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
   char* lds = reinterpret_cast<char*>(lds_words);
-  stage_tables<PDB_CAT_TREE64, PDB_CAT_H4032>(lds, tabs);
+  stage_tables<PDB_CAT_TREE32, PDB_CAT_H2016, PDB_CAT_S2048>(lds, tabs);
   __syncthreads();
+  const uint32_t u = threadIdx.x & 63u;
+  const LaneTabs lt = lane_tabs(u);
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWavesPerWg;
+  uint64_t i = wave_id_uniform();
+  if (i >= nblk) return;
 
-  const uint32_t lane = threadIdx.x & 63u;
-  const LaneTabs lt = lane_tabs(lane);
-  const uint64_t nwaves = static_cast<uint64_t>(gridDim.x) * kWavesPerWg;
-  for (uint64_t i = wave_id_uniform(); i < n; i += nwaves) {
-    const pdb_block_handle hd = h[i];
-    uint8_t* p = buf + hd.offset;
-    // CRC input = contents || type byte  (table/table_builder.cc:197-198; format.cc:98)
-    const uint32_t c = crc_block(lds, lt, lane, p, static_cast<uint32_t>(hd.size + 1), 0xFFFFFFFFu);
-    if (lane == 0) {
-      uint8_t* tr = p + hd.size + 1;
-      if constexpr (kSeal) {
-        const uint32_t m = pdb_mask(~c);  // EncodeFixed32(trailer+1, Mask(crc))
-        tr[0] = static_cast<uint8_t>(m);
-        tr[1] = static_cast<uint8_t>(m >> 8);
-        tr[2] = static_cast<uint8_t>(m >> 16);
-        tr[3] = static_cast<uint8_t>(m >> 24);
-      } else {
-        const uint32_t stored = static_cast<uint32_t>(tr[0]) | (static_cast<uint32_t>(tr[1]) << 8) |
-                                (static_cast<uint32_t>(tr[2]) << 16) |
-                                (static_cast<uint32_t>(tr[3]) << 24);
-        const bool good = pdb_unmask(stored) == ~c;
-        if (ok) ok[i] = good ? 1 : 0;
-        if (!good && nbad) atomicAdd(nbad, 1u);
+  // the item being loaded: block d, round k
+  BlkDesc d = src.get(i);
+  uint32_t k = 0;
+  RawPiece na, nb;
+  uint32_t nhw = 0, nhb = 0;
+  auto issue = [&](const BlkDesc& bd, uint32_t kk) {
+    const uint32_t t = bd.n & 31u, K = bd.n >> 5;
+    const uint8_t* q0 = bd.p + t;
+    const uint32_t s = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(q0) & 3u);
+    const uint32_t ca = u + (kk << 7), cb = ca + 64u;
+    if (ca < K) issue_piece(na, q0 + static_cast<uint64_t>(ca) * 32u, s);
+    if (cb < K) issue_piece(nb, q0 + static_cast<uint64_t>(cb) * 32u, s);
+    if (kk == 0) {
+      const uint32_t lead = t & 3u, nh = t >> 2;
+      if (u >= 1 && u <= nh) nhw = ld32u(bd.p + lead + 4u * (u - 1));
+      if (u == 0 && lead) {
+        uint32_t v = bd.p[0];
+        if (lead > 1) v |= static_cast<uint32_t>(bd.p[1]) << 8;
+        if (lead > 2) v |= static_cast<uint32_t>(bd.p[2]) << 16;
+        nhb = v;
       }
+    }
+  };
+  issue(d, 0);
+  uint32_t acc = 0;
+  for (;;) {
+    const RawPiece ca_ = na, cb_ = nb;
+    const uint32_t chw = nhw, chb = nhb;
+    const BlkDesc cd = d;
+    const uint32_t ck = k;
+    const uint32_t K = cd.n >> 5;
+    const uint32_t R = K ? (K + 127u) >> 7 : 1u;
+    const bool last_round = ck + 1 >= R;
+    const uint64_t ni = last_round ? i + nw : i;
+    const bool have_next = ni < nblk;
+    if (last_round && have_next) d = src.get(ni);
+    k = last_round ? 0 : ck + 1;
+    if (have_next) issue(d, k);
+
+    if (ck == 0) {  // head: every lane hashes the same (broadcast) head bytes from the seed
+      const uint32_t t = cd.n & 31u, lead = t & 3u, nh = t >> 2;
+      uint32_t h = cd.init_raw;
+      const uint32_t lb = __builtin_amdgcn_readfirstlane(chb);
+      for (uint32_t j = 0; j < lead; ++j) h = step1(lds, lt, h, (lb >> (8 * j)) & 0xffu);
+      for (uint32_t j = 0; j < nh; ++j) h = step4(lds, lt, h, __builtin_amdgcn_readlane(chw, j + 1));
+      acc = (u == 0) ? h : 0u;
+    }
+    const uint32_t s = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(cd.p + (cd.n & 31u)) & 3u);
+    const uint32_t ca = u + (ck << 7), cb = ca + 64u;
+    if (cb < K) {
+      const uint32_t start = ck ? shift_op(lds, PDB_SLOT_HORNER, acc) : acc;
+      const uint32_t xa = chain_piece(lds, lt, start, ca_, s);
+      const uint32_t xb = chain_piece(lds, lt, 0u, cb_, s);
+      acc = shift_op_x(lds, 7, xa, xb);
+    } else if (ca < K) {
+      const uint32_t start = ck ? shift_op(lds, PDB_SLOT_HORNER, acc) : acc;
+      acc = chain_piece(lds, lt, start, ca_, s);
+    }
+    if (last_round) {
+      uint32_t raw = acc;
+      if (K) {
+        const uint32_t q = K & 63u;
+        if (q) acc = __shfl(acc, (u + q) & 63u, 64);
+        raw = wave_tree_dpp(lds, u, acc);
+      }
+      if (u == 0) sink.put(i, raw, cd);
+      i = ni;
+      if (!have_next) break;
     }
   }
 }
@@ -462,19 +647,28 @@ hipError_t launch_fixed(const LaunchGeom& g, const uint32_t* d_tables, const uin
   const bool fast = len == 4096u && (reinterpret_cast<uintptr_t>(base) & 15u) == 0 &&
                     (stride & 15u) == 0;
   if (!fast) {
-    hipLaunchKernelGGL(crc_fixed_kernel, grid, block, 0, s, d_tables, base, stride, len, nblk,
-                       flags, init, out);
+    const FixedSrc src{base, stride, len, (flags & PDB_CRC_USE_INIT) ? ~init : 0xFFFFFFFFu};
+    hipLaunchKernelGGL((crc_stream_kernel<FixedSrc, OutSink>), grid, block, 0, s, d_tables, src, nblk,
+                       OutSink{out, flags});
     return hipGetLastError();
   }
 #define PDB_FAST(NP, D)                                                                      \
   hipLaunchKernelGGL((crc_fast4k_kernel<NP, D>), grid, block, 0, s, d_tables, base, stride, nblk, \
                      flags, init, out)
+#define PDB_TEAM(G, D)                                                                       \
+  hipLaunchKernelGGL((crc_team4k_kernel<G, D>), grid, block, 0, s, d_tables, base, stride, nblk, \
+                     flags, init, out)
   switch (g_fast_variant) {
     case 1: PDB_FAST(1, 1); break;
     case 2: PDB_FAST(4, 1); break;
+    case 3: PDB_TEAM(32, 1); break;
+    case 4: PDB_TEAM(32, 0); break;
+    case 5: PDB_TEAM(16, 0); break;
+    case 6: PDB_TEAM(16, 1); break;
     default: PDB_FAST(2, 1); break;  // measured best: 2 x 32-B pieces per lane, depth 1
   }
 #undef PDB_FAST
+#undef PDB_TEAM
   return hipGetLastError();
 }
 
@@ -484,12 +678,13 @@ hipError_t launch_desc(const LaunchGeom& g, const uint32_t* d_tables, const uint
                        hipStream_t s) {
   if (nblk == 0) return hipSuccess;
   const dim3 grid(grid_for(g, nblk)), block(kThreads);
+  const DescSrc src{base, blk, flags};
   if (mode == kModeOut)
-    hipLaunchKernelGGL(crc_desc_kernel<kModeOut>, grid, block, 0, s, d_tables, base, blk, nblk,
-                       flags, expected, out, ok, nbad);
+    hipLaunchKernelGGL((crc_stream_kernel<DescSrc, OutSink>), grid, block, 0, s, d_tables, src, nblk,
+                       OutSink{out, flags});
   else
-    hipLaunchKernelGGL(crc_desc_kernel<kModeVerify>, grid, block, 0, s, d_tables, base, blk, nblk,
-                       flags, expected, out, ok, nbad);
+    hipLaunchKernelGGL((crc_stream_kernel<DescSrc, VerifySink>), grid, block, 0, s, d_tables, src, nblk,
+                       VerifySink{expected, ok, nbad, flags});
   return hipGetLastError();
 }
 
@@ -499,10 +694,13 @@ hipError_t launch_sst(const LaunchGeom& g, const uint32_t* d_tables, uint8_t* bu
   (void)buf_len;
   if (n == 0) return hipSuccess;
   const dim3 grid(grid_for(g, n)), block(kThreads);
+  const SstSrc src{buf, h};
   if (seal)
-    hipLaunchKernelGGL(sst_kernel<true>, grid, block, 0, s, d_tables, buf, h, n, ok, nbad);
+    hipLaunchKernelGGL((crc_stream_kernel<SstSrc, SealSink>), grid, block, 0, s, d_tables, src, n,
+                       SealSink{});
   else
-    hipLaunchKernelGGL(sst_kernel<false>, grid, block, 0, s, d_tables, buf, h, n, ok, nbad);
+    hipLaunchKernelGGL((crc_stream_kernel<SstSrc, SstVerifySink>), grid, block, 0, s, d_tables, src, n,
+                       SstVerifySink{ok, nbad});
   return hipGetLastError();
 }
 

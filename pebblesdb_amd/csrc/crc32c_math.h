@@ -40,23 +40,26 @@ PDB_HD uint32_t pdb_unmask(uint32_t m) {
 //     ((k >> 1) << 16) | (b << 8) | ((k & 1) << 7) | (r << 2)
 // i.e. the data byte lands in address bits 8..15, so one v_perm_b32 builds the address.
 //
-// OPS region [0x20000, 0x20000 + PDB_NOPS*4096): PDB_NOPS = 7 operator slots (4 x 256 u32
+// OPS region [0x20000, 0x20000 + PDB_NOPS*4096): PDB_NOPS = 8 operator slots (4 x 256 u32
 // each, one copy).  Slots 0..5 hold the wave-tree operators "shift by P << k bytes" (P = bytes a
 // lane owns contiguously: 64, 32 or 16 depending on the kernel's load pattern); slot 6 holds the
-// per-lane Horner operator (the gap between two pieces a lane owns).  Each kernel stages the
+// per-lane Horner operator (the gap between two pieces a lane owns); slot 7 a second fold
+// operator (the generic stream kernel's "shift 32").  Each kernel stages the
 // operators it needs from the catalog below.
 #define PDB_LANES 64
 #define PDB_CHUNK 64 /* bytes per lane per round in the generic kernel */
 #define PDB_MAIN_BYTES 0x20000u
-#define PDB_NOPS 7
+#define PDB_NOPS 8
 #define PDB_SLOT_HORNER 6
 #define PDB_OPS_BYTES (PDB_NOPS * 4096u)
-#define PDB_LDS_BYTES (PDB_MAIN_BYTES + PDB_OPS_BYTES) /* 159744 <= 163840 */
+#define PDB_LDS_BYTES (PDB_MAIN_BYTES + PDB_OPS_BYTES) /* 163840 = the whole 160 KiB LDS of a CU */
 /* Operator catalog (device table source): distance in bytes of catalog entry i. */
 #define PDB_NCAT 11
 #define PDB_CAT_TREE16 0   /* 16, 32, ..., 512   (entries 0..5) */
 #define PDB_CAT_TREE32 1   /* 32, ..., 1024      (entries 1..6) */
 #define PDB_CAT_TREE64 2   /* 64, ..., 2048      (entries 2..7) */
+#define PDB_CAT_S1024 6    /* 1024: chain fold, 4 x 16-B pieces per lane per 4 KiB */
+#define PDB_CAT_S2048 7    /* 2048: chain fold, 2 x 32-B pieces per lane per 4 KiB */
 #define PDB_CAT_H1008 8    /* 1024 - 16: 4 x 16-B pieces per lane per 4 KiB */
 #define PDB_CAT_H2016 9    /* 2048 - 32: 2 x 32-B pieces per lane per 4 KiB */
 #define PDB_CAT_H4032 10   /* 4096 - 64: generic kernel, rounds of 64 x 64 B */

@@ -1,0 +1,188 @@
+"""sstable block emit/verify hooks, batched, over the MI355X CRC32C kernels.
+
+Mirrors the two reference call sites of the block checksum:
+
+* ``TableBuilder::WriteRawBlock`` (src/table/table_builder.cc:187-205): a block is appended as
+  ``[contents n B][type 1 B][Mask(crc32c(contents || type)) LE32]`` and gets the BlockHandle
+  ``{offset, n}``; the next block starts at ``offset + n + kBlockTrailerSize``.
+* ``ReadBlock`` (src/table/format.cc:66-148): with ``verify_checksums`` it compares
+  ``Unmask(DecodeFixed32(data + n + 1))`` with ``Value(data, n + 1)`` and returns
+  ``Status::Corruption("block checksum mismatch")``; a short read is
+  ``Corruption("truncated block read")``.
+
+Here ``TableBlockWriter`` buffers blocks and seals all trailers with one GPU batch
+(``pdb_sst_seal_host``), and ``verify_blocks`` checks many handles in one batch
+(``pdb_sst_verify_host``) -- the scan / paranoid-compaction / leveldb-verify form of ReadBlock.
+The BlockHandle varint codec and the Footer codec (table/format.cc:15-64, table/format.h:47-79)
+are included so real table images can be walked.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from ._native import check, lib
+from .crc32c import HANDLE_DTYPE, _buf
+
+K_BLOCK_TRAILER_SIZE = 5  # table/format.h:87
+K_NO_COMPRESSION = 0  # include/pebblesdb/options.h (CompressionType)
+K_SNAPPY_COMPRESSION = 1
+K_TABLE_MAGIC_NUMBER = 0xDB4775248B80FB57  # table/format.h:84
+K_MAX_ENCODED_HANDLE_LENGTH = 10 + 10  # table/format.h:41
+K_FOOTER_ENCODED_LENGTH = 2 * K_MAX_ENCODED_HANDLE_LENGTH + 8  # table/format.h:71
+
+
+class Corruption(Exception):
+    """The reference's Status::Corruption (include/pebblesdb/status.h)."""
+
+
+@dataclass(frozen=True)
+class BlockHandle:
+    offset: int
+    size: int
+
+    def encode(self) -> bytes:  # table/format.cc:15-21 (two varint64s)
+        return encode_varint64(self.offset) + encode_varint64(self.size)
+
+    @staticmethod
+    def decode(buf: bytes, pos: int = 0) -> tuple["BlockHandle", int]:  # format.cc:23-30
+        off, pos = decode_varint64(buf, pos)
+        size, pos = decode_varint64(buf, pos)
+        return BlockHandle(off, size), pos
+
+
+def encode_varint64(v: int) -> bytes:
+    out = bytearray()
+    while v >= 0x80:
+        out.append((v & 0x7F) | 0x80)
+        v >>= 7
+    out.append(v)
+    return bytes(out)
+
+
+def decode_varint64(buf: bytes, pos: int) -> tuple[int, int]:
+    result, shift = 0, 0
+    while shift <= 63:
+        if pos >= len(buf):
+            raise Corruption("bad block handle")
+        b = buf[pos]
+        pos += 1
+        result |= (b & 0x7F) << shift
+        if not b & 0x80:
+            return result, pos
+        shift += 7
+    raise Corruption("bad block handle")
+
+
+@dataclass(frozen=True)
+class Footer:
+    """table/format.h:47-79: metaindex handle, index handle, padding, 8-byte magic."""
+
+    metaindex: BlockHandle
+    index: BlockHandle
+
+    def encode(self) -> bytes:  # format.cc:32-42
+        b = self.metaindex.encode() + self.index.encode()
+        b = b + b"\x00" * (2 * K_MAX_ENCODED_HANDLE_LENGTH - len(b))
+        m = K_TABLE_MAGIC_NUMBER
+        return b + (m & 0xFFFFFFFF).to_bytes(4, "little") + (m >> 32).to_bytes(4, "little")
+
+    @staticmethod
+    def decode(buf: bytes) -> "Footer":  # format.cc:44-64
+        if len(buf) < K_FOOTER_ENCODED_LENGTH:
+            raise Corruption("file is too short to be an sstable")
+        buf = buf[-K_FOOTER_ENCODED_LENGTH:]
+        lo = int.from_bytes(buf[-8:-4], "little")
+        hi = int.from_bytes(buf[-4:], "little")
+        if (hi << 32) | lo != K_TABLE_MAGIC_NUMBER:
+            raise Corruption("not an sstable (bad magic number)")
+        mi, pos = BlockHandle.decode(buf, 0)
+        ix, _ = BlockHandle.decode(buf, pos)
+        return Footer(mi, ix)
+
+
+class TableBlockWriter:
+    """Buffered WriteRawBlock: ``add`` returns the handle the reference would set; ``seal``
+    computes every trailer in one GPU batch; ``data`` is the byte stream to Append."""
+
+    def __init__(self, base_offset: int = 0):
+        self.base = base_offset
+        self._buf = bytearray()
+        self._rel: list[tuple[int, int]] = []
+        self._sealed = True
+
+    def add(self, contents: bytes, type_: int = K_NO_COMPRESSION) -> BlockHandle:
+        h = BlockHandle(self.base + len(self._buf), len(contents))
+        self._rel.append((len(self._buf), len(contents)))
+        self._buf += contents
+        self._buf.append(type_ & 0xFF)
+        self._buf += b"\x00\x00\x00\x00"
+        self._sealed = False
+        return h
+
+    def seal(self) -> None:
+        if not self._rel:
+            self._sealed = True
+            return
+        h = np.array(self._rel, dtype=np.uint64).view(HANDLE_DTYPE).reshape(-1)
+        h = np.ascontiguousarray(h)
+        arr = np.frombuffer(self._buf, dtype=np.uint8)
+        check(lib().pdb_sst_seal_host(arr.ctypes.data, arr.size, h.ctypes.data, len(h)))
+        self._sealed = True
+
+    @property
+    def data(self) -> bytes:
+        if not self._sealed:
+            raise RuntimeError("seal() before reading the sealed bytes")
+        return bytes(self._buf)
+
+    @property
+    def next_offset(self) -> int:
+        return self.base + len(self._buf)
+
+    def handles(self) -> list[BlockHandle]:
+        return [BlockHandle(self.base + o, n) for o, n in self._rel]
+
+
+def _handles_array(handles) -> np.ndarray:
+    h = np.zeros(len(handles), dtype=HANDLE_DTYPE)
+    for i, x in enumerate(handles):
+        h[i]["offset"], h[i]["size"] = (x.offset, x.size) if isinstance(x, BlockHandle) else x
+    return h
+
+
+def verify_blocks(image, handles) -> np.ndarray:
+    """ok[i] = 1 iff block i's stored trailer matches crc32c(contents||type)."""
+    p, n, _keep = _buf(image)
+    h = _handles_array(handles)
+    for x in h:
+        if int(x["offset"]) + int(x["size"]) + K_BLOCK_TRAILER_SIZE > n:
+            raise Corruption("truncated block read")
+    ok = np.zeros(len(h), dtype=np.uint8)
+    rc = lib().pdb_sst_verify_host(p, n, h.ctypes.data, len(h), ok.ctypes.data)
+    check(int(rc))
+    return ok
+
+
+def read_block(image, handle: BlockHandle, verify_checksums: bool = True) -> tuple[bytes, int]:
+    """ReadBlock (format.cc:66-148) for an in-memory image: returns (contents, type).
+    Compression is left to the caller (Snappy is delegated, out of scope)."""
+    data = bytes(image[handle.offset : handle.offset + handle.size + K_BLOCK_TRAILER_SIZE])
+    if len(data) != handle.size + K_BLOCK_TRAILER_SIZE:
+        raise Corruption("truncated block read")
+    if verify_checksums and not verify_blocks(data, [BlockHandle(0, handle.size)])[0]:
+        raise Corruption("block checksum mismatch")
+    return data[: handle.size], data[handle.size]
+
+
+def read_blocks(image, handles, verify_checksums: bool = True) -> list[tuple[bytes, int]]:
+    """Batch ReadBlock: one GPU verify for all handles, then the per-block slices."""
+    if verify_checksums:
+        ok = verify_blocks(image, handles)
+        bad = np.nonzero(ok == 0)[0]
+        if bad.size:
+            raise Corruption(f"block checksum mismatch (block {int(bad[0])} of {len(handles)})")
+    mv = memoryview(bytes(image))
+    return [(bytes(mv[h.offset : h.offset + h.size]), mv[h.offset + h.size]) for h in handles]

@@ -1,0 +1,126 @@
+// tests/cpp/table_blocks_test.cc -- C++ consumer of the drop-in headers, written the way the
+// reference's own tests are (util/crc32c_test.cc, table/table_test.cc): the LevelDB-compatible
+// leveldb::crc32c API on known answers, then a buffered WriteRawBlock round trip and the
+// ReadBlock checksum check (including a corrupted block).  Built by tests/test_cpp_consumer.py
+// with g++ against include/ and pebblesdb_amd/_lib/libpdb_crc32c.so.
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "pebblesdb_amd/crc32c.h"
+#include "pebblesdb_amd/table_blocks.h"
+
+static int failures = 0;
+#define EXPECT(cond)                                               \
+  do {                                                             \
+    if (!(cond)) {                                                 \
+      fprintf(stderr, "%s:%d: EXPECT(%s) failed\n", __FILE__, __LINE__, #cond); \
+      ++failures;                                                  \
+    }                                                              \
+  } while (0)
+
+using namespace leveldb;
+
+static void StandardResults() {  // util/crc32c_test.cc:13-48
+  char buf[32];
+  memset(buf, 0, sizeof(buf));
+  EXPECT(0x8a9136aa == crc32c::Value(buf, sizeof(buf)));
+  memset(buf, 0xff, sizeof(buf));
+  EXPECT(0x62a8ab43 == crc32c::Value(buf, sizeof(buf)));
+  for (int i = 0; i < 32; i++) buf[i] = i;
+  EXPECT(0x46dd794e == crc32c::Value(buf, sizeof(buf)));
+  for (int i = 0; i < 32; i++) buf[i] = 31 - i;
+  EXPECT(0x113fdb5c == crc32c::Value(buf, sizeof(buf)));
+  unsigned char data[48] = {0x01, 0xc0, 0, 0, 0, 0, 0, 0, 0,    0,    0, 0, 0,    0, 0, 0,
+                            0x14, 0,    0, 0, 0, 0, 4, 0, 0,    0,    0, 0x14, 0, 0, 0, 0x18,
+                            0x28, 0,    0, 0, 0, 0, 0, 0, 0x02, 0,    0, 0, 0,    0, 0, 0};
+  EXPECT(0xd9963a56 == crc32c::Value(reinterpret_cast<char*>(data), sizeof(data)));
+}
+
+static void LargeBuffer() {  // util/crc32c_test.cc:50-60
+  std::string tmp(4096, 'A');
+  EXPECT(0x3c36f666 == crc32c::Value(tmp.data(), 64));
+  EXPECT(0xf6607a92 == crc32c::Value(tmp.data(), 1024));
+  EXPECT(0xa9bc21ef == crc32c::Value(tmp.data(), 1111));
+  EXPECT(0x88ddb66b == crc32c::Value(tmp.data(), 2048));
+  EXPECT(0x057251e9 == crc32c::Value(tmp.data(), 4096));
+}
+
+static void ExtendAndMask() {  // util/crc32c_test.cc:62-77
+  EXPECT(crc32c::Value("a", 1) != crc32c::Value("foo", 3));
+  EXPECT(crc32c::Value("hello world", 11) == crc32c::Extend(crc32c::Value("hello ", 6), "world", 5));
+  uint32_t crc = crc32c::Value("foo", 3);
+  EXPECT(crc != crc32c::Mask(crc));
+  EXPECT(crc != crc32c::Mask(crc32c::Mask(crc)));
+  EXPECT(crc == crc32c::Unmask(crc32c::Mask(crc)));
+  EXPECT(crc == crc32c::Unmask(crc32c::Unmask(crc32c::Mask(crc32c::Mask(crc)))));
+}
+
+static void TrailerRoundTrip() {
+  // Blocks of the sizes a real table has: ~4 KiB data blocks, a tiny metaindex, a large index.
+  std::vector<std::string> blocks;
+  unsigned x = 301;
+  size_t sizes[] = {4171, 4175, 4096, 0, 51, 17, 213 * 1024 + 3, 4091};
+  for (size_t n : sizes) {
+    std::string b(n, '\0');
+    for (size_t i = 0; i < n; ++i) {
+      x = x * 1103515245u + 12345u;
+      b[i] = static_cast<char>(x >> 16);
+    }
+    blocks.push_back(b);
+  }
+  pdb::BlockTrailerBatch batch(1000);
+  std::vector<pdb::BlockHandle> hs;
+  uint64_t expect_off = 1000;
+  for (size_t i = 0; i < blocks.size(); ++i) {
+    pdb::BlockHandle h = batch.Add(blocks[i].data(), blocks[i].size(), i % 2);
+    EXPECT(h.offset == expect_off && h.size == blocks[i].size());  // WriteRawBlock's handle
+    expect_off += blocks[i].size() + pdb::kBlockTrailerSize;
+    hs.push_back(pdb::BlockHandle{h.offset - 1000, h.size});
+  }
+  EXPECT(batch.Seal() == 0);
+  const std::string& img = batch.bytes();
+  // Each trailer equals what WriteRawBlock computes with the scalar API (table_builder.cc:196-199)
+  for (size_t i = 0; i < blocks.size(); ++i) {
+    const char* p = img.data() + hs[i].offset;
+    char type = static_cast<char>(i % 2);
+    uint32_t crc = crc32c::Value(blocks[i].data(), blocks[i].size());
+    crc = crc32c::Extend(crc, &type, 1);
+    uint32_t stored;
+    memcpy(&stored, p + hs[i].size + 1, 4);
+    EXPECT(p[hs[i].size] == type);
+    EXPECT(stored == crc32c::Mask(crc));
+    EXPECT(crc32c::Unmask(stored) == crc32c::Value(p, hs[i].size + 1));  // ReadBlock's check
+  }
+  std::vector<uint8_t> ok;
+  EXPECT(pdb::VerifyBlocks(img.data(), img.size(), hs.data(), hs.size(), &ok) == 0);
+  // Corrupt one byte of block 6 -> exactly that block reports "block checksum mismatch".
+  std::string bad = img;
+  bad[hs[6].offset + 12345] ^= 0x01;
+  EXPECT(pdb::VerifyBlocks(bad.data(), bad.size(), hs.data(), hs.size(), &ok) == 1);
+  for (size_t i = 0; i < hs.size(); ++i) EXPECT(ok[i] == (i == 6 ? 0 : 1));
+  // A corrupted trailer byte is detected too.
+  bad = img;
+  bad[hs[2].offset + hs[2].size + 2] ^= 0x80;
+  EXPECT(pdb::VerifyBlocks(bad.data(), bad.size(), hs.data(), hs.size(), &ok) == 1 && ok[2] == 0);
+}
+
+int main() {
+  if (pdb_crc32c_init(0) != 0) {
+    fprintf(stderr, "no device: %s\n", pdb_last_error());
+    return 2;
+  }
+  StandardResults();
+  LargeBuffer();
+  ExtendAndMask();
+  TrailerRoundTrip();
+  if (failures) {
+    fprintf(stderr, "%d failures\n", failures);
+    return 1;
+  }
+  printf("table_blocks_test: PASS\n");
+  return 0;
+}

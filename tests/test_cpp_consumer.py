@@ -1,0 +1,33 @@
+"""The C++ drop-in headers (include/pebblesdb_amd/{crc32c,table_blocks}.h) compile and link
+against the library with plain g++ (CPU), and the consumer test passes on the GPU."""
+import os
+import subprocess
+
+import pytest
+
+from pebblesdb_amd import build
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "tests", "cpp", "table_blocks_test.cc")
+EXE = os.path.join(ROOT, "tests", "cpp", "table_blocks_test")
+
+
+def _compile():
+    build.build(verbose=False)
+    libdir = os.path.dirname(build.LIB)
+    subprocess.check_call(["g++", "-O2", "-std=c++11", "-Wall", "-Werror", f"-I{ROOT}/include", SRC,
+                           "-o", EXE, f"-L{libdir}", "-lpdb_crc32c", f"-Wl,-rpath,{libdir}"])
+    return EXE
+
+
+def test_cpp_consumer_builds_and_links():
+    exe = _compile()
+    assert os.path.exists(exe)
+
+
+@pytest.mark.gpu
+def test_cpp_consumer_runs_on_gpu():
+    exe = _compile()
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "PASS" in r.stdout

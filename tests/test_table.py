@@ -1,0 +1,100 @@
+"""sstable block hooks (table/table_builder.cc:187-205 WriteRawBlock, table/format.cc:66-148
+ReadBlock) through pebblesdb_amd.table.  CPU: the handle/footer codecs.  GPU: trailers vs the
+reference-generated golden trailers and vs the oracle, corruption detection."""
+import numpy as np
+import pytest
+
+from pebblesdb_amd import table as T
+
+
+def test_varint_handle_roundtrip():
+    for off, size in [(0, 0), (1, 127), (128, 16383), (2**35 + 7, 4171), (2**63 - 1, 2**40)]:
+        h = T.BlockHandle(off, size)
+        enc = h.encode()
+        assert len(enc) <= T.K_MAX_ENCODED_HANDLE_LENGTH
+        d, pos = T.BlockHandle.decode(enc)
+        assert d == h and pos == len(enc)
+    with pytest.raises(T.Corruption):
+        T.BlockHandle.decode(b"\x80\x80")
+
+
+def test_footer_roundtrip_and_magic():
+    f = T.Footer(T.BlockHandle(123456, 51), T.BlockHandle(123512, 3000))
+    enc = f.encode()
+    assert len(enc) == T.K_FOOTER_ENCODED_LENGTH == 48
+    assert T.Footer.decode(b"junk" + enc) == f
+    with pytest.raises(T.Corruption):
+        T.Footer.decode(enc[:-1] + b"\x00")
+    with pytest.raises(T.Corruption):
+        T.Footer.decode(b"short")
+
+
+gpu = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from pebblesdb_amd import crc32c
+
+    crc32c.init_device(0)
+
+
+@gpu
+def test_writer_matches_golden_trailers(dev, golden):
+    import oracle
+
+    w = T.TableBlockWriter(base_offset=777)
+    handles = []
+    for t in golden["trailers"]:
+        contents = oracle.splitmix_bytes(t["input"]["len"], t["input"]["seed"]).tobytes()
+        h = w.add(contents, t["type"])
+        handles.append(h)
+    w.seal()
+    data = w.data
+    off = 777
+    for t, h in zip(golden["trailers"], handles):
+        assert h.offset == off  # WriteRawBlock's handle bookkeeping
+        tr = data[h.offset - 777 + h.size : h.offset - 777 + h.size + 5]
+        assert tr.hex() == t["trailer_hex"]
+        off += h.size + T.K_BLOCK_TRAILER_SIZE
+    assert w.next_offset == off
+
+
+@gpu
+def test_verify_and_read_blocks(dev, oracle_lib):
+    import oracle
+
+    rng = np.random.Generator(np.random.PCG64(9))
+    sizes = [int(x) for x in rng.integers(0, 9000, size=300)] + [4096, 4171, 213 * 1024]
+    w = T.TableBlockWriter()
+    hs = [w.add(oracle.splitmix_bytes(n, 1000 + i).tobytes(), i % 2) for i, n in enumerate(sizes)]
+    w.seal()
+    img = bytearray(w.data)
+    # trailers agree with the oracle (table_builder.cc:197-199 with the restatement)
+    for h in hs[:50]:
+        body = bytes(img[h.offset : h.offset + h.size + 1])
+        stored = int.from_bytes(img[h.offset + h.size + 1 : h.offset + h.size + 5], "little")
+        assert stored == oracle_lib.mask(oracle_lib.value(body))
+    assert T.verify_blocks(img, hs).all()
+    blocks = T.read_blocks(img, hs)
+    assert blocks[5][0] == oracle.splitmix_bytes(sizes[5], 1005).tobytes() and blocks[5][1] == 1
+    # one flipped bit in block 17's contents -> ReadBlock's Corruption("block checksum mismatch")
+    bad = bytearray(img)
+    bad[hs[17].offset + hs[17].size // 2] ^= 0x04
+    ok = T.verify_blocks(bad, hs)
+    assert ok.sum() == len(hs) - 1 and ok[17] == 0
+    with pytest.raises(T.Corruption, match="block checksum mismatch"):
+        T.read_block(bad, hs[17])
+    with pytest.raises(T.Corruption, match="block checksum mismatch"):
+        T.read_blocks(bad, hs)
+    assert T.read_block(bad, hs[17], verify_checksums=False)[0] != blocks[17][0]
+    # a flipped type byte is covered by the CRC too (contents || type)
+    bad = bytearray(img)
+    bad[hs[3].offset + hs[3].size] ^= 0x01
+    assert T.verify_blocks(bad, hs)[3] == 0
+    # truncated read (format.cc:84-87)
+    with pytest.raises(T.Corruption, match="truncated block read"):
+        T.read_block(img[: hs[-1].offset + 10], hs[-1])
