@@ -34,8 +34,8 @@ METRIC = "GiB/s CRC32C over batched 4 KiB sstable blocks (device-resident); % HB
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="c2", choices=["c2", "c3", "sstable"])
     ap.add_argument("--nblk", type=int, default=1 << 20, help="blocks per GPU (c2/sstable)")
     ap.add_argument("--c3-bytes", type=int, default=16 << 30, help="bytes per GPU for c3 (Zipf)")
@@ -211,8 +211,8 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": {"c2": "crc_fast4k_kernel<2,1>", "sstable": "crc_fixed_kernel",
-                           "c3": "crc_desc_kernel<0>"}[args.workload],
+                "kernel": {"c2": "crc_pack4k_kernel", "sstable": "crc_stream_kernel<FixedSrc,OutSink>",
+                           "c3": "crc_stream_kernel<DescSrc,OutSink>"}[args.workload],
                 "algorithmic_bytes_per_launch": algo_bytes,
                 "kernel_avg_ms": round(kern_avg_ms, 4),
                 "kernel_min_ms": round(float(np.min(kern_ms)), 4),

@@ -203,7 +203,7 @@ __device__ __forceinline__ uint32_t hash4k(const char* lds, const LaneTabs& lt, 
   return wave_tree_dpp(lds, lane, c);
 }
 
-template <int kNP, int kDepth>
+template <int kNP, int kDepth, bool kIssueFirst = false>
 __global__ __launch_bounds__(kThreads) void crc_fast4k_kernel(
     const uint32_t* __restrict__ tabs, const uint8_t* __restrict__ base, uint64_t stride,
     uint64_t nblk, uint32_t flags, uint32_t init, uint32_t* __restrict__ out) {
@@ -226,17 +226,168 @@ __global__ __launch_bounds__(kThreads) void crc_fast4k_kernel(
   __syncthreads();
   const LaneTabs lt = lane_tabs(lane);
   const uint32_t init_raw = (flags & PDB_CRC_USE_INIT) ? ~init : 0xFFFFFFFFu;
+  // Results are parked in a register (lane j holds the j-th block's CRC of the current 64-block
+  // window) and flushed with one scattered 64-lane store per window: a per-block store from
+  // lane 0 would sit in vmcnt behind the next block's loads and make every wait drain it.
+  uint32_t res = 0;
+  uint32_t it = 0;
+  uint64_t win0 = b0;  // first block of the current window
   for (uint64_t b = b0; b < nblk; b += kDepth * nw) {
 #pragma unroll
     for (int k = 0; k < kDepth; ++k) {
       const uint64_t bk = b + k * nw;
-      if (bk >= nblk) return;  // wave-uniform
+      if (bk >= nblk) break;  // wave-uniform
       u32x4 cur[4] = {buf[k][0], buf[k][1], buf[k][2], buf[k][3]};
       const uint64_t bn = bk + kDepth * nw;
       load4k<kNP>(buf[k], base, stride, bn < nblk ? bn : bk, lane);  // clamp: valid block
+      if constexpr (kIssueFirst) __builtin_amdgcn_sched_barrier(0);
       const uint32_t c = hash4k<kNP>(lds, lt, lane, lane == 0 ? init_raw : 0u, cur);
-      if (lane == 0) out[bk] = finalize(c, flags);
+      const uint32_t v = finalize(__builtin_amdgcn_readfirstlane(c), flags);
+      if (lane == (it & 63u)) res = v;
+      if ((++it & 63u) == 0) {
+        out[win0 + static_cast<uint64_t>(lane) * nw] = res;
+        win0 += 64 * nw;
+      }
     }
+  }
+  if ((it & 63u) && lane < (it & 63u)) out[win0 + static_cast<uint64_t>(lane) * nw] = res;
+}
+
+// ---- fixed-stride batch, 4-KiB ping-pong path ----------------------------------------------------
+// crc_fast4k_kernel<2,1> with two named load buffers and a scheduling barrier right after each
+// load issue, so the next block's 4 KiB is in flight for the WHOLE hash of the current block
+// (hipcc otherwise sinks the loads a third of the way into the chain to reuse registers).
+__global__ __launch_bounds__(kThreads) void crc_pingpong4k_kernel(
+    const uint32_t* __restrict__ tabs, const uint8_t* __restrict__ base, uint64_t stride,
+    uint64_t nblk, uint32_t flags, uint32_t init, uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
+  char* lds = reinterpret_cast<char*>(lds_words);
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWavesPerWg;
+  const uint64_t b0 = wave_id_uniform();
+  u32x4 A[4], B[4];
+  load4k<2>(A, base, stride, b0 < nblk ? b0 : nblk - 1, lane);
+  stage_tables<PDB_CAT_TREE32, PDB_CAT_S2048>(lds, tabs);
+  __syncthreads();
+  if (b0 >= nblk) return;
+  const LaneTabs lt = lane_tabs(lane);
+  const uint32_t init_raw = (flags & PDB_CRC_USE_INIT) ? ~init : 0xFFFFFFFFu;
+  const uint32_t c0 = lane == 0 ? init_raw : 0u;
+  uint32_t res = 0, it = 0;
+  uint64_t win0 = b0;
+  auto emit = [&](uint32_t c) {
+    const uint32_t v = finalize(__builtin_amdgcn_readfirstlane(c), flags);
+    if (lane == (it & 63u)) res = v;
+    if ((++it & 63u) == 0) {
+      out[win0 + static_cast<uint64_t>(lane) * nw] = res;
+      win0 += 64 * nw;
+    }
+  };
+  for (uint64_t b = b0; b < nblk; b += 2 * nw) {
+    const uint64_t b1 = b + nw, b2 = b + 2 * nw;
+    load4k<2>(B, base, stride, b1 < nblk ? b1 : b, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    emit(hash4k<2>(lds, lt, lane, c0, A));
+    if (b1 >= nblk) break;
+    load4k<2>(A, base, stride, b2 < nblk ? b2 : b1, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    emit(hash4k<2>(lds, lt, lane, c0, B));
+  }
+  if ((it & 63u) && lane < (it & 63u)) out[win0 + static_cast<uint64_t>(lane) * nw] = res;
+}
+
+// ---- fixed-stride batch, 4-KiB packed-tree path ------------------------------------------------
+// Same per-block loads and chains as crc_fast4k_kernel<2,1> (64 lanes per block, two 32-B pieces
+// per lane), but a wave hashes 4 blocks back to back and folds their 4 x 64 lane partials in ONE
+// packed tree: level 0 pairs lanes (2m, 2m+1) of blocks {0,1} and then {2,3} with every lane
+// doing useful work, level 1 pairs quads of all 4 blocks in one full-wave round, levels 2-5 run
+// once for all 4 blocks.  7 shift operations per 4 blocks instead of 24.
+__device__ __forceinline__ uint32_t sel(bool c, uint32_t a, uint32_t b) { return c ? a : b; }
+
+// Returns block (lane & 3)'s raw state in lanes 0..3.
+__device__ __forceinline__ uint32_t tree4_packed(const char* lds, uint32_t u, uint32_t p0, uint32_t p1,
+                                                 uint32_t p2, uint32_t p3) {
+  const bool odd = u & 1u;
+  // level 0 (shift 32): even lane 2m -> block 0/2 pair m, odd lane 2m+1 -> block 1/3 pair m
+  const uint32_t p0n = __builtin_amdgcn_update_dpp(0u, p0, 0x101, 0xF, 0xF, false);  // p0[L+1]
+  const uint32_t p1p = __builtin_amdgcn_update_dpp(0u, p1, 0x111, 0xF, 0xF, false);  // p1[L-1]
+  const uint32_t r0 = shift_op_x(lds, 0, sel(odd, p1p, p0), sel(odd, p1, p0n));
+  const uint32_t p2n = __builtin_amdgcn_update_dpp(0u, p2, 0x101, 0xF, 0xF, false);
+  const uint32_t p3p = __builtin_amdgcn_update_dpp(0u, p3, 0x111, 0xF, 0xF, false);
+  const uint32_t r1 = shift_op_x(lds, 0, sel(odd, p3p, p2), sel(odd, p3, p2n));
+  // level 1 (shift 64): lane 4j+r -> block r pair j.  r<2 reads r0 at L, L+2; r>=2 reads r1 at L-2, L
+  const bool hi = u & 2u;
+  const uint32_t r0n = __builtin_amdgcn_update_dpp(0u, r0, 0x102, 0xF, 0xF, false);  // r0[L+2]
+  const uint32_t r1p = __builtin_amdgcn_update_dpp(0u, r1, 0x112, 0xF, 0xF, false);  // r1[L-2]
+  uint32_t v = shift_op_x(lds, 1, sel(hi, r1p, r0), sel(hi, r1, r0n));
+  // levels 2..5: lane 4j+r holds block r; pair (L, L + 4*2^(k-2))
+  uint32_t y = __builtin_amdgcn_update_dpp(0u, v, 0x104, 0xF, 0xF, false);  // row_shl:4
+  if ((u & 4u) == 0) v = shift_op_x(lds, 2, v, y);
+  y = __builtin_amdgcn_update_dpp(0u, v, 0x108, 0xF, 0xF, false);  // row_shl:8
+  if ((u & 12u) == 0) v = shift_op_x(lds, 3, v, y);
+  y = __builtin_amdgcn_ds_swizzle(v, 0x401F);  // lane ^ 16
+  if ((u & 28u) == 0) v = shift_op_x(lds, 4, v, y);
+  y = __shfl_down(v, 32, 64);
+  if ((u & 60u) == 0) v = shift_op_x(lds, 5, v, y);
+  return v;
+}
+
+__device__ __forceinline__ uint32_t partial4k(const char* lds, const LaneTabs& lt, uint32_t c0,
+                                              const u32x4 (&v)[4]) {
+  uint32_t xa = c0 ^ v[0].x, xb = v[2].x;
+  const uint32_t da[8] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w};
+  const uint32_t db[8] = {v[2].x, v[2].y, v[2].z, v[2].w, v[3].x, v[3].y, v[3].z, v[3].w};
+#pragma unroll
+  for (int i = 1; i <= 8; ++i) {
+    xa = step4x(lds, lt, xa, i < 8 ? da[i] : 0u);
+    xb = step4x(lds, lt, xb, i < 8 ? db[i] : 0u);
+  }
+  return shift_op_x(lds, PDB_SLOT_HORNER, xa, xb);  // shift 2048
+}
+
+__global__ __launch_bounds__(kThreads) void crc_pack4k_kernel(
+    const uint32_t* __restrict__ tabs, const uint8_t* __restrict__ base, uint64_t stride,
+    uint64_t nblk, uint32_t flags, uint32_t init, uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
+  char* lds = reinterpret_cast<char*>(lds_words);
+  const uint32_t u = threadIdx.x & 63u;
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWavesPerWg;
+  const uint64_t w = wave_id_uniform();
+  u32x4 buf[4];
+  load4k<2>(buf, base, stride, w < nblk ? w : nblk - 1, u);
+  stage_tables<PDB_CAT_TREE32, PDB_CAT_S2048>(lds, tabs);
+  __syncthreads();
+  if (w >= nblk) return;
+  const LaneTabs lt = lane_tabs(u);
+  const uint32_t init_raw = (flags & PDB_CRC_USE_INIT) ? ~init : 0xFFFFFFFFu;
+  const uint32_t c0 = u == 0 ? init_raw : 0u;
+  uint32_t res = 0, it = 0;
+  uint64_t win0 = w;
+  for (uint64_t g = w; g < nblk; g += 4 * nw) {  // blocks g, g+nw, g+2nw, g+3nw
+    uint32_t p[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint64_t bk = g + r * nw;
+      u32x4 cur[4] = {buf[0], buf[1], buf[2], buf[3]};
+      const uint64_t bn = bk + nw;
+      if (bn < nblk) load4k<2>(buf, base, stride, bn, u);  // wave-uniform
+      p[r] = bk < nblk ? partial4k(lds, lt, c0, cur) : 0u;
+    }
+    const uint32_t v = tree4_packed(lds, u, p[0], p[1], p[2], p[3]);
+    // lane 4j+r of the 64-block window holds block (window + (4j+r)*nw): move lanes 0..3's
+    // results up by 4*(group mod 16) with one DPP-free bpermute, park, flush every 16 groups.
+    const uint32_t slot = (it & 15u) * 4u;
+    const uint32_t vv = __shfl(v, u & 3u, 64);
+    if ((u & ~3u) == slot) res = finalize(vv, flags);
+    if ((++it & 15u) == 0) {
+      const uint64_t bo = win0 + static_cast<uint64_t>(u) * nw;
+      if (bo < nblk) out[bo] = res;
+      win0 += 64 * nw;
+    }
+  }
+  if (it & 15u) {
+    const uint64_t bo = win0 + static_cast<uint64_t>(u) * nw;
+    if (u < (it & 15u) * 4u && bo < nblk) out[bo] = res;
   }
 }
 
@@ -659,13 +810,17 @@ hipError_t launch_fixed(const LaunchGeom& g, const uint32_t* d_tables, const uin
   hipLaunchKernelGGL((crc_team4k_kernel<G, D>), grid, block, 0, s, d_tables, base, stride, nblk, \
                      flags, init, out)
   switch (g_fast_variant) {
-    case 1: PDB_FAST(1, 1); break;
-    case 2: PDB_FAST(4, 1); break;
-    case 3: PDB_TEAM(32, 1); break;
-    case 4: PDB_TEAM(32, 0); break;
+    // A/B variants (tools/ab_fast.py); 0 = shipped default, measured best or tied on every box
+    case 1: PDB_FAST(2, 1); break;  // 64-lane tree per block
+    case 2: PDB_FAST(1, 1); break;  // 64-B lane pieces
+    case 3: PDB_FAST(4, 1); break;  // coalesced 16-B pieces, 4 chains
+    case 4: PDB_TEAM(32, 1); break;
     case 5: PDB_TEAM(16, 0); break;
-    case 6: PDB_TEAM(16, 1); break;
-    default: PDB_FAST(2, 1); break;  // measured best: 2 x 32-B pieces per lane, depth 1
+    case 6: hipLaunchKernelGGL(crc_pingpong4k_kernel, grid, block, 0, s, d_tables, base, stride, nblk, flags, init, out); break;
+    case 7: hipLaunchKernelGGL((crc_fast4k_kernel<2, 1, true>), grid, block, 0, s, d_tables, base, stride, nblk, flags, init, out); break;
+    default:  // 4 blocks per wave-iteration, one packed tree
+      hipLaunchKernelGGL(crc_pack4k_kernel, grid, block, 0, s, d_tables, base, stride, nblk, flags, init, out);
+      break;
   }
 #undef PDB_FAST
 #undef PDB_TEAM

@@ -165,3 +165,34 @@ def test_full_size_config2_vs_oracle(crc, oracle_lib):
     torch.cuda.empty_cache()
     exp = oracle_lib.batch(host, crc.make_blocks(np.arange(nblk) * L, np.full(nblk, L)), nthreads=16)
     assert (got == exp).all(), int(np.count_nonzero(got != exp))
+
+
+@pytest.mark.parametrize("nblk", [1, 2, 3, 5, 4095, 4096, 4097, 16383, 16384, 16385, 65539])
+def test_fast_path_partial_groups(crc, oracle_lib, nblk):
+    """4-KiB fast path (4 blocks per wave-iteration, 64-block result windows): every count
+    around the wave / group / window boundaries, with seed and mask flags."""
+    d = torch.empty(nblk * 4096, dtype=torch.uint8, device="cuda")
+    crc.fill_splitmix(d, 1000 + nblk)
+    host = d.cpu().numpy()
+    blk = crc.make_blocks(np.arange(nblk) * 4096, np.full(nblk, 4096), np.full(nblk, 0x1234567))
+    got = _u32(crc.batch_fixed(d, 4096, 4096, nblk, masked=True, init=0x1234567))
+    exp = oracle_lib.batch(host, blk, flags=3, nthreads=8)
+    assert (got == exp).all()
+
+
+def test_all_fast_variants_bit_exact(crc, oracle_lib):
+    """The A/B variants selectable through pdb_diag_set_variant are all exact."""
+    from pebblesdb_amd._native import lib
+
+    nblk = 3 * 4096 * 4 + 7
+    d = torch.empty(nblk * 4096, dtype=torch.uint8, device="cuda")
+    crc.fill_splitmix(d, 4242)
+    exp = oracle_lib.batch(d.cpu().numpy(), crc.make_blocks(np.arange(nblk) * 4096, np.full(nblk, 4096)),
+                           nthreads=8)
+    try:
+        for v in range(8):
+            lib().pdb_diag_set_variant(v)
+            got = _u32(crc.batch_fixed(d, 4096, 4096, nblk))
+            assert (got == exp).all(), f"variant {v}"
+    finally:
+        lib().pdb_diag_set_variant(0)
