@@ -18,3 +18,18 @@ g++ -O3 -std=c++11 -fPIC -shared \
   -I"$REF" -I"$REF/include" \
   -o "$HERE/_ref/libpdbref.so" "$HERE/ref_shim.cc" "$REF/util/crc32c.cc" -lpthread
 echo "built $HERE/_ref/libpdbref.so"
+
+# The reference's own sstable writer/reader (table/*, util/*, port/*) + oracle/ref_sstwriter.cc
+# -> oracle/_ref/ref_sstwriter, used only to generate tests/golden/sst fixtures.
+SRCS="table/table_builder.cc table/block_builder.cc table/filter_block.cc table/format.cc
+      table/block.cc table/table.cc table/iterator.cc table/two_level_iterator.cc
+      util/coding.cc util/crc32c.cc util/comparator.cc util/options.cc util/env.cc
+      util/env_posix.cc util/status.cc util/logging.cc util/hash.cc util/bloom.cc
+      util/filter_policy.cc util/arena.cc util/atomic.cc util/cache.cc port/port_posix.cc"
+ABS=""
+for f in $SRCS; do ABS="$ABS $REF/$f"; done
+g++ -O2 -std=c++11 -w \
+  -DLEVELDB_PLATFORM_POSIX -DOS_LINUX -DHAVE_FFLUSH_UNLOCKED -DHAVE_FREAD_UNLOCKED \
+  -DHAVE_FWRITE_UNLOCKED -DHAVE_FDATASYNC -DHAVE_DECL_FDATASYNC=1 \
+  -I"$REF" -I"$REF/include" -o "$HERE/_ref/ref_sstwriter" "$HERE/ref_sstwriter.cc" $ABS -lpthread
+echo "built $HERE/_ref/ref_sstwriter"

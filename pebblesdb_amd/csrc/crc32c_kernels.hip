@@ -105,6 +105,7 @@ __device__ __forceinline__ uint32_t shift_op_x(const char* lds, uint32_t op, uin
 // Same fold with the partner values moved by DPP (levels 0-3, row_shl), ds_swizzle (level 4,
 // xor 16 within 32-lane halves) and readlane (level 5): one LDS round trip fewer per level
 // than ds_bpermute.  Result valid in lane 0.
+template <bool kL5Twice = false>
 __device__ __forceinline__ uint32_t wave_tree_dpp(const char* lds, uint32_t lane, uint32_t c) {
   uint32_t y;
   y = __builtin_amdgcn_update_dpp(0u, c, 0x101, 0xF, 0xF, false);  // row_shl:1
@@ -118,7 +119,12 @@ __device__ __forceinline__ uint32_t wave_tree_dpp(const char* lds, uint32_t lane
   y = __builtin_amdgcn_ds_swizzle(c, 0x401F);  // bitmask mode: lane ^ 16 within 32
   if ((lane & 31u) == 0) c = shift_op_x(lds, 4, c, y);
   y = __builtin_amdgcn_readlane(c, 32);
-  if (lane == 0) c = shift_op_x(lds, 5, c, y);
+  if (lane == 0) {
+    if constexpr (kL5Twice)  // slot 5 left free (LDS scratch): shift 2P = shift P twice
+      c = shift_op_x(lds, 4, shift_op(lds, 4, c), y);
+    else
+      c = shift_op_x(lds, 5, c, y);
+  }
   return c;
 }
 
@@ -140,7 +146,7 @@ __device__ __forceinline__ uint32_t ld32u(const uint8_t* q) {
 
 // Stage the table image into LDS: T0..T3 written 32x (8 x 16-B stores per entry); tree
 // operators catalog[kTree .. kTree+5] -> slots 0..5; catalog[kHorner] -> slot 6 (if >= 0).
-template <int kTree, int kHorner, int kSlot7 = -1>
+template <int kTree, int kHorner, int kSlot7 = -1, bool kSkipSlot5 = false>
 __device__ __forceinline__ void stage_tables(char* lds, const uint32_t* __restrict__ tabs) {
   for (uint32_t i = threadIdx.x; i < 4u * 256u * 8u; i += blockDim.x) {
     const uint32_t k = i >> 11, b = (i >> 3) & 255u, part = i & 7u;
@@ -152,6 +158,7 @@ __device__ __forceinline__ void stage_tables(char* lds, const uint32_t* __restri
   constexpr uint32_t nslots = kSlot7 >= 0 ? 8u : (kHorner >= 0 ? 7u : 6u);
   for (uint32_t i = threadIdx.x; i < nslots * 256u; i += blockDim.x) {
     const uint32_t slot = i >> 8;
+    if (kSkipSlot5 && slot == 5) continue;
     const uint32_t src = slot < 6 ? kTree + slot
                                   : (slot == 6 ? static_cast<uint32_t>(kHorner) : static_cast<uint32_t>(kSlot7));
     *reinterpret_cast<u32x4*>(lds + PDB_MAIN_BYTES + i * 16u) = cat[src * 256u + (i & 255u)];
@@ -400,6 +407,46 @@ __global__ __launch_bounds__(kThreads) void crc_pack4k_kernel(
   }
 }
 
+// Dynamic variant of the packed kernel: workgroup g owns blocks [g*N/G, (g+1)*N/G); each wave
+// takes 4 consecutive blocks at a time from an LDS counter (operator slot 7 is unused here) and
+// writes their 4 CRCs with one 16-B store.
+__global__ __launch_bounds__(kThreads) void crc_pack4k_dyn_kernel(
+    const uint32_t* __restrict__ tabs, const uint8_t* __restrict__ base, uint64_t stride,
+    uint64_t nblk, uint32_t flags, uint32_t init, uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
+  char* lds = reinterpret_cast<char*>(lds_words);
+  uint32_t* ctr = reinterpret_cast<uint32_t*>(lds + PDB_MAIN_BYTES + 7 * 4096u);
+  const uint32_t u = threadIdx.x & 63u;
+  const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t g_lo = nblk * blockIdx.x / gridDim.x, g_hi = nblk * (blockIdx.x + 1) / gridDim.x;
+  uint64_t grp = g_lo + 4u * wid;  // first group of this wave (static), then from the counter
+  u32x4 buf[4];
+  load4k<2>(buf, base, stride, grp < g_hi ? grp : (nblk ? nblk - 1 : 0), u);
+  stage_tables<PDB_CAT_TREE32, PDB_CAT_S2048>(lds, tabs);
+  if (threadIdx.x == 0) *ctr = kWavesPerWg;  // next group, in groups relative to g_lo
+  __syncthreads();
+  const LaneTabs lt = lane_tabs(u);
+  const uint32_t init_raw = (flags & PDB_CRC_USE_INIT) ? ~init : 0xFFFFFFFFu;
+  const uint32_t c0 = u == 0 ? init_raw : 0u;
+  while (grp < g_hi) {
+    uint32_t r0 = 0;
+    if (u == 0) r0 = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const uint64_t ngrp = g_lo + 4u * static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(r0));
+    uint32_t p[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint64_t bk = grp + r;
+      u32x4 cur[4] = {buf[0], buf[1], buf[2], buf[3]};
+      const uint64_t bn = r < 3 ? bk + 1 : ngrp;
+      if (bn < g_hi) load4k<2>(buf, base, stride, bn, u);  // wave-uniform
+      p[r] = bk < g_hi ? partial4k(lds, lt, c0, cur) : 0u;
+    }
+    const uint32_t v = tree4_packed(lds, u, p[0], p[1], p[2], p[3]);
+    if (u < 4 && grp + u < g_hi) out[grp + u] = finalize(v, flags);
+    grp = ngrp;
+  }
+}
+
 // ---- fixed-stride batch, 4-KiB team path ----------------------------------------------------
 // A wave hashes T = 64/kG consecutive 4-KiB blocks at once: team t (lanes [t*kG, (t+1)*kG))
 // owns block t.  Within a team, lane u owns R = 4096/(32*kG) pieces of 32 B, piece r at
@@ -617,18 +664,35 @@ __device__ __forceinline__ uint32_t chain_piece(const char* lds, const LaneTabs&
 // step (one barrier per item), so their outstanding loads stay within one compact span of
 // consecutive blocks -- DRAM row locality that free-running waves lose as they drift apart
 // (measured on the 4-KiB path: +8 %).
-template <class Src, class Sink, int kSync>
+// kDyn (unequal lengths: descriptors, sstable handles): workgroup g owns the contiguous block
+// range [g*N/G, (g+1)*N/G) and its 16 waves take the next block from an LDS counter (LDS slot 5,
+// freed by folding tree level 5 as two "shift 512"s): the CU's work is balanced and its
+// outstanding loads stay on a compact run of consecutive blocks.
+template <class Src, class Sink, int kSync, bool kDyn = false>
 __global__ __launch_bounds__(kThreads) void crc_stream_kernel(const uint32_t* __restrict__ tabs,
                                                                Src src, uint64_t nblk, Sink sink) {
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
   char* lds = reinterpret_cast<char*>(lds_words);
-  stage_tables<PDB_CAT_TREE32, PDB_CAT_H2016, PDB_CAT_S2048>(lds, tabs);
+  stage_tables<PDB_CAT_TREE32, PDB_CAT_H2016, PDB_CAT_S2048, kDyn>(lds, tabs);
+  uint32_t* ctr = reinterpret_cast<uint32_t*>(lds + PDB_MAIN_BYTES + 5 * 4096u);
+  const uint64_t g_lo = nblk * blockIdx.x / gridDim.x, g_hi = nblk * (blockIdx.x + 1) / gridDim.x;
+  if (kDyn && threadIdx.x == 0) *ctr = kWavesPerWg;  // next block, relative to g_lo
   __syncthreads();
   const uint32_t u = threadIdx.x & 63u;
   const LaneTabs lt = lane_tabs(u);
   const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWavesPerWg;
-  uint64_t i = wave_id_uniform();
-  bool active = i < nblk;
+  auto next_block = [&](uint64_t cur) -> uint64_t {
+    if constexpr (kDyn) {
+      uint32_t r = 0;
+      if (u == 0) r = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      return g_lo + __builtin_amdgcn_readfirstlane(r);
+    } else {
+      return cur + nw;
+    }
+  };
+  const uint64_t nend = kDyn ? g_hi : nblk;
+  uint64_t i = kDyn ? g_lo + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : wave_id_uniform();
+  bool active = i < nend;
   if (kSync == 0 && !active) return;
 
   // the item being loaded: block d, round k
@@ -681,8 +745,8 @@ __global__ __launch_bounds__(kThreads) void crc_stream_kernel(const uint32_t* __
     const uint32_t K = cd.n >> 5;
     const uint32_t R = K ? (K + 127u) >> 7 : 1u;
     const bool last_round = ck + 1 >= R;
-    const uint64_t ni = last_round ? i + nw : i;
-    const bool have_next = ni < nblk;
+    const uint64_t ni = last_round ? next_block(i) : i;
+    const bool have_next = ni < nend;
     if (last_round && have_next) d = src.get(ni);
     k = last_round ? 0 : ck + 1;
     if (have_next) issue(d, k);
@@ -711,7 +775,7 @@ __global__ __launch_bounds__(kThreads) void crc_stream_kernel(const uint32_t* __
       if (K) {
         const uint32_t q = K & 63u;
         if (q) acc = __shfl(acc, (u + q) & 63u, 64);
-        raw = wave_tree_dpp(lds, u, acc);
+        raw = wave_tree_dpp<kDyn>(lds, u, acc);
       }
       if (u == 0) sink.put(i, raw, cd);
       i = ni;
@@ -840,7 +904,11 @@ hipError_t launch_fixed(const LaunchGeom& g, const uint32_t* d_tables, const uin
       case 8: PDB_STREAM_FIXED(0); break;
       case 9: PDB_STREAM_FIXED(1); break;
       case 10: PDB_STREAM_FIXED(4); break;
-      default: PDB_STREAM_FIXED(8); break;  // measured best (sstable layout +3 %, 4-B-aligned 4 KiB +5 %)
+      case 11: PDB_STREAM_FIXED(8); break;
+      default:  // workgroup-local dynamic blocks: measured best (sstable layout +4 % over lock-step)
+        hipLaunchKernelGGL((crc_stream_kernel<FixedSrc, OutSink, 0, true>), grid, block, 0, s, d_tables, src,
+                           nblk, OutSink{out, flags});
+        break;
     }
 #undef PDB_STREAM_FIXED
     return hipGetLastError();
@@ -862,6 +930,7 @@ hipError_t launch_fixed(const LaunchGeom& g, const uint32_t* d_tables, const uin
     case 7: hipLaunchKernelGGL((crc_fast4k_kernel<2, 1, true>), grid, block, 0, s, d_tables, base, stride, nblk, flags, init, out); break;
     case 8: hipLaunchKernelGGL(crc_pack4k_kernel<0>, grid, block, 0, s, d_tables, base, stride, nblk, flags, init, out); break;
     case 9: hipLaunchKernelGGL(crc_pack4k_kernel<2>, grid, block, 0, s, d_tables, base, stride, nblk, flags, init, out); break;
+    case 11: hipLaunchKernelGGL(crc_pack4k_dyn_kernel, grid, block, 0, s, d_tables, base, stride, nblk, flags, init, out); break;
     case 10: hipLaunchKernelGGL(crc_pack4k_kernel<4>, grid, block, 0, s, d_tables, base, stride, nblk, flags, init, out); break;
     default:  // 4 blocks per wave-iteration, one packed tree, workgroup lock-step per group
       hipLaunchKernelGGL(crc_pack4k_kernel<1>, grid, block, 0, s, d_tables, base, stride, nblk, flags, init, out);
@@ -879,11 +948,14 @@ hipError_t launch_desc(const LaunchGeom& g, const uint32_t* d_tables, const uint
   if (nblk == 0) return hipSuccess;
   const dim3 grid(grid_for(g, nblk)), block(kThreads);
   const DescSrc src{base, blk, flags};
-  if (mode == kModeOut)
-    hipLaunchKernelGGL((crc_stream_kernel<DescSrc, OutSink, 0>), grid, block, 0, s, d_tables, src, nblk,
+  if (mode == kModeOut && g_fast_variant == 8)  // A/B: static strided assignment
+    hipLaunchKernelGGL((crc_stream_kernel<DescSrc, OutSink, 0, false>), grid, block, 0, s, d_tables, src,
+                       nblk, OutSink{out, flags});
+  else if (mode == kModeOut)
+    hipLaunchKernelGGL((crc_stream_kernel<DescSrc, OutSink, 0, true>), grid, block, 0, s, d_tables, src, nblk,
                        OutSink{out, flags});
   else
-    hipLaunchKernelGGL((crc_stream_kernel<DescSrc, VerifySink, 0>), grid, block, 0, s, d_tables, src, nblk,
+    hipLaunchKernelGGL((crc_stream_kernel<DescSrc, VerifySink, 0, true>), grid, block, 0, s, d_tables, src, nblk,
                        VerifySink{expected, ok, nbad, flags});
   return hipGetLastError();
 }
@@ -896,10 +968,10 @@ hipError_t launch_sst(const LaunchGeom& g, const uint32_t* d_tables, uint8_t* bu
   const dim3 grid(grid_for(g, n)), block(kThreads);
   const SstSrc src{buf, h};
   if (seal)
-    hipLaunchKernelGGL((crc_stream_kernel<SstSrc, SealSink, 0>), grid, block, 0, s, d_tables, src, n,
+    hipLaunchKernelGGL((crc_stream_kernel<SstSrc, SealSink, 0, true>), grid, block, 0, s, d_tables, src, n,
                        SealSink{});
   else
-    hipLaunchKernelGGL((crc_stream_kernel<SstSrc, SstVerifySink, 0>), grid, block, 0, s, d_tables, src, n,
+    hipLaunchKernelGGL((crc_stream_kernel<SstSrc, SstVerifySink, 0, true>), grid, block, 0, s, d_tables, src, n,
                        SstVerifySink{ok, nbad});
   return hipGetLastError();
 }

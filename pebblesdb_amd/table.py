@@ -186,3 +186,67 @@ def read_blocks(image, handles, verify_checksums: bool = True) -> list[tuple[byt
             raise Corruption(f"block checksum mismatch (block {int(bad[0])} of {len(handles)})")
     mv = memoryview(bytes(image))
     return [(bytes(mv[h.offset : h.offset + h.size]), mv[h.offset + h.size]) for h in handles]
+
+
+# ---- whole-table walk: the batched form of leveldb-verify (src/leveldb-verify.cc:120-164) -------
+
+
+def decode_varint32(buf: bytes, pos: int) -> tuple[int, int]:
+    v, pos = decode_varint64(buf, pos)
+    if v > 0xFFFFFFFF:
+        raise Corruption("bad varint32")
+    return v, pos
+
+
+def block_entries(contents: bytes) -> list[tuple[bytes, bytes]]:
+    """Parse a block (table/block_builder.cc: prefix-compressed entries
+    [shared][non_shared][value_len][key_delta][value], then uint32 restarts[], uint32 count)."""
+    n = len(contents)
+    if n < 4:
+        raise Corruption("bad block contents")
+    num_restarts = int.from_bytes(contents[n - 4 :], "little")
+    limit = n - 4 * (num_restarts + 1)
+    if limit < 0:
+        raise Corruption("bad block contents")
+    out, pos, key = [], 0, b""
+    while pos < limit:
+        shared, pos = decode_varint32(contents, pos)
+        non_shared, pos = decode_varint32(contents, pos)
+        vlen, pos = decode_varint32(contents, pos)
+        if shared > len(key) or pos + non_shared + vlen > limit:
+            raise Corruption("bad entry in block")
+        key = key[:shared] + contents[pos : pos + non_shared]
+        pos += non_shared
+        out.append((key, contents[pos : pos + vlen]))
+        pos += vlen
+    return out
+
+
+@dataclass
+class TableLayout:
+    footer: Footer
+    data: list  # BlockHandle of every data block, in file order
+    meta: dict  # metaindex name -> BlockHandle (e.g. "filter.leveldb.BuiltinBloomFilter")
+
+    def all_handles(self) -> list:
+        return list(self.data) + list(self.meta.values()) + [self.footer.metaindex, self.footer.index]
+
+
+def table_layout(image, verify_checksums: bool = True) -> TableLayout:
+    """Footer -> index block -> data-block handles, metaindex block -> meta handles
+    (table/table.cc:70-170 Table::Open / ReadMeta).  Index and metaindex are read through
+    read_block, i.e. checksum-verified on the GPU when verify_checksums is set."""
+    image = bytes(image)
+    f = Footer.decode(image)
+    idx, _ = read_block(image, f.index, verify_checksums)
+    data = [BlockHandle.decode(v)[0] for _, v in block_entries(idx)]
+    mi, _ = read_block(image, f.metaindex, verify_checksums)
+    meta = {k.decode("latin-1"): BlockHandle.decode(v)[0] for k, v in block_entries(mi)}
+    return TableLayout(f, data, meta)
+
+
+def verify_table(image) -> tuple[TableLayout, np.ndarray]:
+    """leveldb-verify for one table image: every block (data, meta, metaindex, index) checked in
+    ONE GPU batch.  Returns (layout, ok flags in all_handles() order)."""
+    lay = table_layout(image, verify_checksums=False)
+    return lay, verify_blocks(image, lay.all_handles())

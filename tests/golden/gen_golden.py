@@ -193,6 +193,39 @@ def main() -> None:
     with open(OUT, "w") as f:
         json.dump(out, f, separators=(",", ":"))
     print(f"wrote {OUT} ({os.path.getsize(OUT)} bytes)")
+    gen_sstables()
+
+
+SST_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "sst")
+WRITER = os.path.join(ROOT, "oracle", "_ref", "ref_sstwriter")
+# (name, nkeys, value_size, seed, block_size, bloom_bits): written by the reference's TableBuilder
+SST_SPECS = [
+    ("small_bloom", 1000, 100, 7, 4096, 10),   # ~4.1 KiB data blocks + bloom filter block
+    ("bigvals", 40, 3000, 8, 4096, 0),         # values near the block size
+    ("tinyblocks", 500, 20, 9, 256, 0),        # table_test's block_size 256 (table_test.cc:452-478)
+    ("empty", 0, 0, 10, 4096, 0),              # no data block: metaindex + index + footer only
+]
+
+
+def gen_sstables() -> None:
+    """sstables written AND re-read with verify_checksums by the reference itself
+    (oracle/_ref/ref_sstwriter: the reference's table/*.cc compiled in place)."""
+    import subprocess
+
+    os.makedirs(SST_DIR, exist_ok=True)
+    manifest = []
+    for name, n, vs, seed, bs, bloom in SST_SPECS:
+        line = subprocess.check_output([WRITER, SST_DIR, name, str(n), str(vs), str(seed), str(bs), str(bloom)],
+                                       text=True)
+        rec = json.loads(line)
+        assert rec["reference_verify_ok"], rec
+        rec.update({"nkeys": n, "value_size": vs, "seed": seed})
+        manifest.append(rec)
+    with open(os.path.join(SST_DIR, "manifest.json"), "w") as f:
+        json.dump({"generator": "tests/golden/gen_golden.py -> oracle/_ref/ref_sstwriter (reference "
+                                "TableBuilder + Table::Open/iterator with verify_checksums)",
+                   "tables": manifest}, f, indent=1)
+    print(f"wrote {len(manifest)} sstables to {SST_DIR}")
 
 
 if __name__ == "__main__":
