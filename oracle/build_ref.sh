@@ -33,3 +33,15 @@ g++ -O2 -std=c++11 -w \
   -DHAVE_FWRITE_UNLOCKED -DHAVE_FDATASYNC -DHAVE_DECL_FDATASYNC=1 \
   -I"$REF" -I"$REF/include" -o "$HERE/_ref/ref_sstwriter" "$HERE/ref_sstwriter.cc" $ABS -lpthread
 echo "built $HERE/_ref/ref_sstwriter"
+
+# The reference's own WAL/MANIFEST log writer/reader + oracle/ref_logwriter.cc
+# -> oracle/_ref/ref_logwriter, used only to generate tests/golden/log fixtures.
+LSRCS="db/log_writer.cc db/log_reader.cc util/coding.cc util/crc32c.cc util/env.cc util/env_posix.cc
+       util/status.cc util/logging.cc util/atomic.cc port/port_posix.cc"
+LABS=""
+for f in $LSRCS; do LABS="$LABS $REF/$f"; done
+g++ -O2 -std=c++11 -w \
+  -DLEVELDB_PLATFORM_POSIX -DOS_LINUX -DHAVE_FFLUSH_UNLOCKED -DHAVE_FREAD_UNLOCKED \
+  -DHAVE_FWRITE_UNLOCKED -DHAVE_FDATASYNC -DHAVE_DECL_FDATASYNC=1 \
+  -I"$REF" -I"$REF/include" -o "$HERE/_ref/ref_logwriter" "$HERE/ref_logwriter.cc" $LABS -lpthread
+echo "built $HERE/_ref/ref_logwriter"

@@ -194,6 +194,7 @@ def main() -> None:
         json.dump(out, f, separators=(",", ":"))
     print(f"wrote {OUT} ({os.path.getsize(OUT)} bytes)")
     gen_sstables()
+    gen_logs()
 
 
 SST_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "sst")
@@ -226,6 +227,37 @@ def gen_sstables() -> None:
                                 "TableBuilder + Table::Open/iterator with verify_checksums)",
                    "tables": manifest}, f, indent=1)
     print(f"wrote {len(manifest)} sstables to {SST_DIR}")
+
+
+
+LOG_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "log")
+LOG_WRITER = os.path.join(ROOT, "oracle", "_ref", "ref_logwriter")
+# (name, seed, record lengths): written by the reference's log::Writer, re-read by log::Reader
+LOG_SPECS = [
+    # empty + tiny records, a record that leaves a 4-byte block tail (zero trailer), records that
+    # fill a block exactly, and records fragmented First/Middle/Last across 2-3 blocks
+    ("wal_mixed", 11, [0, 1, 7, 100, 32757, 10, 32761 - 17, 40000, 70000, 5, 6, 13, 200, 3000, 0]),
+    ("manifest_small", 12, [int(x) for x in np.random.Generator(np.random.PCG64(12)).integers(0, 400, 300)]),
+]
+
+
+def gen_logs() -> None:
+    import subprocess
+
+    os.makedirs(LOG_DIR, exist_ok=True)
+    manifest = []
+    for name, seed, lens in LOG_SPECS:
+        path = os.path.join(LOG_DIR, name + ".log")
+        rec = json.loads(subprocess.check_output([LOG_WRITER, path, str(seed)] + [str(x) for x in lens],
+                                                 text=True))
+        assert rec["reference_verify_ok"], rec
+        rec.update({"name": name, "file": name + ".log", "seed": seed, "lengths": lens,
+                    "payload": "record k: byte j = byte (j%8) of splitmix64(seed + k + 3, j//8)"})
+        manifest.append(rec)
+    with open(os.path.join(LOG_DIR, "manifest.json"), "w") as f:
+        json.dump({"generator": "tests/golden/gen_golden.py -> oracle/_ref/ref_logwriter (reference "
+                                "log::Writer + log::Reader with checksums)", "logs": manifest}, f, indent=1)
+    print(f"wrote {len(manifest)} logs to {LOG_DIR}")
 
 
 if __name__ == "__main__":
