@@ -43,6 +43,9 @@ def parse():
     ap.add_argument("--no-copy-inclusive", action="store_true")
     ap.add_argument("--diag", action="store_true", help="also time the read-stream calibration kernels")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend (nccl = RCCL over xGMI; gloo only to rehearse the "
+                         "multi-rank flow with ranks sharing one GPU)")
     return ap.parse_args()
 
 
@@ -64,12 +67,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    ndev = torch.cuda.device_count()
+    gpu = local % ndev if args.backend == "gloo" else local  # gloo rehearsal may share a GPU
+    torch.cuda.set_device(gpu)
     distributed = world > 1
     if distributed:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    crc32c.init_device(local)
-    dev = torch.device("cuda", local)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group("gloo")
+    crc32c.init_device(gpu)
+    dev = torch.device("cuda", gpu)
+    cdev = dev if args.backend == "nccl" else torch.device("cpu")  # collective tensors
     stream = torch.cuda.current_stream()
 
     # ---- the rank's shard index: scattered from rank 0 over RCCL (the only collective) -------
@@ -77,7 +86,7 @@ def main():
         n_total = 0
     else:
         n_total = args.nblk * world
-    lo, hi = scatter_block_ranges(n_total, world, rank, dev, dist if distributed else None)
+    lo, hi = scatter_block_ranges(n_total, world, rank, cdev, dist if distributed else None)
 
     # ---- synthetic, device-resident input ---------------------------------------------------
     if args.workload == "c2":
@@ -155,14 +164,14 @@ def main():
     kern_ms = [s.elapsed_time(e) for s, e in ev]
     kern_avg_ms = float(np.mean(kern_ms))
 
-    t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    t = torch.tensor([wall], dtype=torch.float64, device=cdev)
     if distributed:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall_max = float(t.item())
 
     # checksum of checksums (outside the timed region) gathered to rank 0
     xs = torch.tensor([int(np.bitwise_xor.reduce(out.cpu().numpy().view(np.uint32)))], dtype=torch.int64,
-                      device=dev)
+                      device=cdev)
     if distributed:
         allx = [torch.zeros_like(xs) for _ in range(world)]
         dist.all_gather(allx, xs)
@@ -202,7 +211,9 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (splitmix64 seed 301, generated on device)",
-            "config": dict(workload, parallelism=f"block-range shards x{world}"),
+            "config": dict(workload, parallelism=f"block-range shards x{world}",
+                           collectives="index broadcast + checksum all-gather (" +
+                                       ("RCCL" if args.backend == "nccl" else "gloo") + "), none on the data path"),
             "hbm_frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
             "roofline": {
                 "bound": "hbm",

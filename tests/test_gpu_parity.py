@@ -196,3 +196,31 @@ def test_all_fast_variants_bit_exact(crc, oracle_lib):
             assert (got == exp).all(), f"variant {v}"
     finally:
         lib().pdb_diag_set_variant(0)
+
+
+def test_device_entry_points_capture_into_hip_graph(crc, oracle_lib):
+    """Device entry points are stream-ordered and allocation-free (include/pdb_crc32c.h): a
+    captured hipGraph replays them and recomputes after the input changes."""
+    nblk = 4096 + 3
+    d = torch.empty(nblk * 4096, dtype=torch.uint8, device="cuda")
+    crc.fill_splitmix(d, 77)
+    blk = crc.blocks_to_device(crc.make_blocks(np.arange(nblk) * 4096 + 1, np.full(nblk, 4095)))
+    out1 = torch.empty(nblk, dtype=torch.int32, device="cuda")
+    out2 = torch.empty(nblk, dtype=torch.int32, device="cuda")
+    crc.batch_fixed(d, 4096, 4096, nblk, out=out1)  # warm (per-device state exists before capture)
+    crc.batch(d, blk, out=out2)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        crc.batch_fixed(d, 4096, 4096, nblk, out=out1)
+        crc.batch(d, blk, out=out2)
+    for seed in (78, 79):
+        crc.fill_splitmix(d, seed)
+        out1.zero_()
+        out2.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        host = d.cpu().numpy()
+        e1 = oracle_lib.batch(host, crc.make_blocks(np.arange(nblk) * 4096, np.full(nblk, 4096)), nthreads=8)
+        e2 = oracle_lib.batch(host, crc.make_blocks(np.arange(nblk) * 4096 + 1, np.full(nblk, 4095)), nthreads=8)
+        assert (_u32(out1) == e1).all() and (_u32(out2) == e2).all()
