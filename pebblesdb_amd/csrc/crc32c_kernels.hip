@@ -807,7 +807,7 @@ __global__ __launch_bounds__(256) void read_stream_kernel(const u32x4* __restric
 //   kPat 0: lane l reads bytes [64l, 64l+64) of the block (the fast path's pattern)
 //   kPat 1: lane l reads 16 B at 16l + 1024j, j = 0..3 (each instruction 1 KiB contiguous)
 //   kDepth: blocks in flight per wave; kAssign 0: wave-interleaved blocks, 1: contiguous per WG
-template <int kPat, int kDepth, int kAssign>
+template <int kPat, int kDepth, int kAssign, bool kSync = false>
 __global__ __launch_bounds__(kThreads) void read_pattern4k_kernel(const uint8_t* __restrict__ base,
                                                                   uint64_t nblk,
                                                                   uint32_t* __restrict__ out) {
@@ -826,7 +826,9 @@ __global__ __launch_bounds__(kThreads) void read_pattern4k_kernel(const uint8_t*
     step = kWavesPerWg;
     last = lo + per < nblk ? lo + per : nblk;
   }
-  for (uint64_t b = first; b < last; b += step * kDepth) {
+  const uint64_t wg_first = static_cast<uint64_t>(blockIdx.x) * kWavesPerWg;
+  for (uint64_t b = first, bw = wg_first; (kSync ? bw : b) < last; b += step * kDepth, bw += step * kDepth) {
+    if constexpr (kSync) __syncthreads();
     u32x4 x = {0, 0, 0, 0};
 #pragma unroll
     for (int k = 0; k < kDepth; ++k) {
@@ -998,6 +1000,11 @@ hipError_t launch_read_pattern4k(const LaunchGeom& g, const uint8_t* base, uint6
     case 7: PDB_RP(0, 4, 0); break;
     case 8: PDB_RP(2, 1, 0); break;
     case 9: PDB_RP(2, 2, 0); break;
+    // workgroup lock-step (one barrier per iteration), as in the shipped CRC kernels
+    case 10: hipLaunchKernelGGL((read_pattern4k_kernel<2, 1, 0, true>), grid, block, 0, s, base, nblk, out); break;
+    case 11: hipLaunchKernelGGL((read_pattern4k_kernel<1, 1, 0, true>), grid, block, 0, s, base, nblk, out); break;
+    case 12: hipLaunchKernelGGL((read_pattern4k_kernel<2, 4, 0, true>), grid, block, 0, s, base, nblk, out); break;
+    case 13: hipLaunchKernelGGL((read_pattern4k_kernel<1, 4, 0, true>), grid, block, 0, s, base, nblk, out); break;
     default: PDB_RP(0, 1, 0); break;
   }
 #undef PDB_RP
