@@ -1,0 +1,551 @@
+// crc32c_device.h -- device-side building blocks of the gfx950 CRC32C kernels, shared by the
+// shipped kernels (crc32c_kernels.hip) and the A/B variants and diagnostics (crc32c_variants.hip).
+// Everything is in an anonymous namespace: each translation unit instantiates what it uses.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "crc32c_internal.h"
+#include "crc32c_math.h"
+
+namespace pdb {
+namespace {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+
+constexpr uint32_t kThreads = 1024;
+constexpr uint32_t kWavesPerWg = kThreads / 64;
+
+// v_perm_b32 selectors: result = [lb.byte0, x.byte j, lb.byte2, 0x00]  (S0 = lb, S1 = x)
+constexpr uint32_t sel_byte(uint32_t j) { return 0x0C060004u | (j << 8); }
+
+struct LaneTabs {
+  uint32_t t3, t2, t1, t0;  // per-lane LDS address bases of T3..T0 (replica = lane & 31)
+};
+
+__device__ __forceinline__ LaneTabs lane_tabs(uint32_t lane) {
+  const uint32_t r = (lane & 31u) << 2;
+  return LaneTabs{0x10080u | r, 0x10000u | r, 0x00080u | r, r};
+}
+
+__device__ __forceinline__ uint32_t lds_u32(const char* lds, uint32_t addr) {
+  return *reinterpret_cast<const uint32_t*>(lds + addr);
+}
+
+// One slice-by-4 step: c' = shift(c ^ w, 4 bytes).
+__device__ __forceinline__ uint32_t step4(const char* lds, const LaneTabs& lt, uint32_t c,
+                                          uint32_t w) {
+  const uint32_t x = c ^ w;
+  const uint32_t a3 = __builtin_amdgcn_perm(lt.t3, x, sel_byte(0));
+  const uint32_t a2 = __builtin_amdgcn_perm(lt.t2, x, sel_byte(1));
+  const uint32_t a1 = __builtin_amdgcn_perm(lt.t1, x, sel_byte(2));
+  const uint32_t a0 = __builtin_amdgcn_perm(lt.t0, x, sel_byte(3));
+  return (lds_u32(lds, a3) ^ lds_u32(lds, a2)) ^ (lds_u32(lds, a1) ^ lds_u32(lds, a0));
+}
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // gfx950 v_bitop3_b32: a ^ b ^ c
+}
+
+// x' = shift(x, 4 bytes) ^ w_next: one slice-by-4 step whose input is already crc ^ word, with
+// the next word folded in (chains carry x = state ^ next data word).
+__device__ __forceinline__ uint32_t step4x(const char* lds, const LaneTabs& lt, uint32_t x,
+                                           uint32_t wnext) {
+  const uint32_t a3 = __builtin_amdgcn_perm(lt.t3, x, sel_byte(0));
+  const uint32_t a2 = __builtin_amdgcn_perm(lt.t2, x, sel_byte(1));
+  const uint32_t a1 = __builtin_amdgcn_perm(lt.t1, x, sel_byte(2));
+  const uint32_t a0 = __builtin_amdgcn_perm(lt.t0, x, sel_byte(3));
+  return xor3(xor3(lds_u32(lds, a3), lds_u32(lds, a2), lds_u32(lds, a1)), lds_u32(lds, a0), wnext);
+}
+
+// Byte step (util/crc32c.cc:601): c' = T0[(c ^ b) & 0xff] ^ (c >> 8).
+__device__ __forceinline__ uint32_t step1(const char* lds, const LaneTabs& lt, uint32_t c,
+                                          uint32_t b) {
+  return lds_u32(lds, __builtin_amdgcn_perm(lt.t0, c ^ b, sel_byte(0))) ^ (c >> 8);
+}
+
+// shift(c, D) through operator `op` (4 x 256 entries, one LDS copy).
+__device__ __forceinline__ uint32_t shift_op(const char* lds, uint32_t op, uint32_t c) {
+  const uint32_t base = PDB_MAIN_BYTES + op * 4096u;
+  const uint32_t v0 = lds_u32(lds, base + ((c & 0xffu) << 2));
+  const uint32_t v1 = lds_u32(lds, base + 1024u + (((c >> 8) & 0xffu) << 2));
+  const uint32_t v2 = lds_u32(lds, base + 2048u + (((c >> 16) & 0xffu) << 2));
+  const uint32_t v3 = lds_u32(lds, base + 3072u + ((c >> 24) << 2));
+  return (v0 ^ v1) ^ (v2 ^ v3);
+}
+
+// shift(c, D_op) ^ y
+__device__ __forceinline__ uint32_t shift_op_x(const char* lds, uint32_t op, uint32_t c, uint32_t y) {
+  const uint32_t base = PDB_MAIN_BYTES + op * 4096u;
+  const uint32_t v0 = lds_u32(lds, base + ((c & 0xffu) << 2));
+  const uint32_t v1 = lds_u32(lds, base + 1024u + (((c >> 8) & 0xffu) << 2));
+  const uint32_t v2 = lds_u32(lds, base + 2048u + (((c >> 16) & 0xffu) << 2));
+  const uint32_t v3 = lds_u32(lds, base + 3072u + ((c >> 24) << 2));
+  return xor3(xor3(v0, v1, v2), v3, y);
+}
+
+// Same fold with the partner values moved by DPP (levels 0-3, row_shl), ds_swizzle (level 4,
+// xor 16 within 32-lane halves) and readlane (level 5): one LDS round trip fewer per level
+// than ds_bpermute.  Result valid in lane 0.
+template <bool kL5Twice = false>
+__device__ __forceinline__ uint32_t wave_tree_dpp(const char* lds, uint32_t lane, uint32_t c) {
+  uint32_t y;
+  y = __builtin_amdgcn_update_dpp(0u, c, 0x101, 0xF, 0xF, false);  // row_shl:1
+  if ((lane & 1u) == 0) c = shift_op_x(lds, 0, c, y);
+  y = __builtin_amdgcn_update_dpp(0u, c, 0x102, 0xF, 0xF, false);  // row_shl:2
+  if ((lane & 3u) == 0) c = shift_op_x(lds, 1, c, y);
+  y = __builtin_amdgcn_update_dpp(0u, c, 0x104, 0xF, 0xF, false);  // row_shl:4
+  if ((lane & 7u) == 0) c = shift_op_x(lds, 2, c, y);
+  y = __builtin_amdgcn_update_dpp(0u, c, 0x108, 0xF, 0xF, false);  // row_shl:8
+  if ((lane & 15u) == 0) c = shift_op_x(lds, 3, c, y);
+  y = __builtin_amdgcn_ds_swizzle(c, 0x401F);  // bitmask mode: lane ^ 16 within 32
+  if ((lane & 31u) == 0) c = shift_op_x(lds, 4, c, y);
+  y = __builtin_amdgcn_readlane(c, 32);
+  if (lane == 0) {
+    if constexpr (kL5Twice)  // slot 5 left free (LDS scratch): shift 2P = shift P twice
+      c = shift_op_x(lds, 4, shift_op(lds, 4, c), y);
+    else
+      c = shift_op_x(lds, 5, c, y);
+  }
+  return c;
+}
+
+__device__ __forceinline__ uint32_t finalize(uint32_t raw, uint32_t flags) {
+  const uint32_t crc = ~raw;
+  return (flags & PDB_CRC_MASK_OUTPUT) ? pdb_mask(crc) : crc;
+}
+
+// Unaligned 32-bit little-endian load that never touches an aligned dword holding no byte of
+// [q, q+4).
+__device__ __forceinline__ uint32_t ld32u(const uint8_t* q) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(q);
+  const uint32_t s = static_cast<uint32_t>(a & 3u);
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~static_cast<uintptr_t>(3));
+  const uint32_t lo = w[0];
+  if (s == 0) return lo;
+  return __builtin_amdgcn_alignbyte(w[1], lo, s);
+}
+
+// Stage the table image into LDS: T0..T3 written 32x (8 x 16-B stores per entry); tree
+// operators catalog[kTree .. kTree+5] -> slots 0..5; catalog[kHorner] -> slot 6 (if >= 0).
+template <int kTree, int kHorner, int kSlot7 = -1, bool kSkipSlot5 = false>
+__device__ __forceinline__ void stage_tables(char* lds, const uint32_t* __restrict__ tabs) {
+  for (uint32_t i = threadIdx.x; i < 4u * 256u * 8u; i += blockDim.x) {
+    const uint32_t k = i >> 11, b = (i >> 3) & 255u, part = i & 7u;
+    const uint32_t v = tabs[k * 256u + b];
+    const uint32_t addr = ((k >> 1) << 16) | (b << 8) | ((k & 1u) << 7) | (part << 4);
+    *reinterpret_cast<u32x4*>(lds + addr) = u32x4{v, v, v, v};
+  }
+  const u32x4* cat = reinterpret_cast<const u32x4*>(tabs + 1024);
+  constexpr uint32_t nslots = kSlot7 >= 0 ? 8u : (kHorner >= 0 ? 7u : 6u);
+  for (uint32_t i = threadIdx.x; i < nslots * 256u; i += blockDim.x) {
+    const uint32_t slot = i >> 8;
+    if (kSkipSlot5 && slot == 5) continue;
+    const uint32_t src = slot < 6 ? kTree + slot
+                                  : (slot == 6 ? static_cast<uint32_t>(kHorner) : static_cast<uint32_t>(kSlot7));
+    *reinterpret_cast<u32x4*>(lds + PDB_MAIN_BYTES + i * 16u) = cat[src * 256u + (i & 255u)];
+  }
+}
+
+__device__ __forceinline__ uint64_t wave_id_uniform() {
+  const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  return static_cast<uint64_t>(blockIdx.x) * kWavesPerWg + w;
+}
+
+// ---- fixed-stride batch, 4-KiB fast path ------------------------------------------------------
+// len == 4096, base and stride 16-B aligned, one round, no head.  Lane l owns kNP pieces of
+// P = 64/kNP contiguous bytes: piece p at p*(4096/kNP) + l*P.  kNP = 1 is the lane-contiguous
+// layout (each 16-B load instruction spans 4 KiB); kNP = 4 makes every load instruction read
+// 1 KiB contiguous (coalesced) at the price of a Horner shift over the (4096/kNP - P)-byte gap
+// between a lane's pieces (LDS slot 6).  Each wave walks blocks b, b+W, ... (W = waves in the
+// grid) with kDepth blocks of loads in flight ahead of the one it hashes.
+template <int kNP>
+__device__ __forceinline__ void load4k(u32x4 (&v)[4], const uint8_t* base, uint64_t stride, uint64_t b,
+                                       uint32_t lane) {
+  constexpr uint32_t P = 64u / kNP, gap = 4096u / kNP, per = 4u / kNP;
+  const uint8_t* blk = base + b * stride + lane * P;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    v[i] = *reinterpret_cast<const u32x4*>(blk + (i / per) * gap + (i % per) * 16u);
+}
+
+// The lane's 16 dwords are hashed as NCH independent slice-by-4 chains (ILP: half or a quarter
+// of the serial LDS round trips), then folded with the slot-6 operator "shift by the distance
+// between consecutive chain ends" (32 B for kNP=1, 2048 B for kNP=2, 1024 B for kNP=4).
+template <int kNP>
+__device__ __forceinline__ uint32_t hash4k(const char* lds, const LaneTabs& lt, uint32_t lane,
+                                           uint32_t c0, const u32x4 (&v)[4]) {
+  const uint32_t d[16] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w,
+                          v[2].x, v[2].y, v[2].z, v[2].w, v[3].x, v[3].y, v[3].z, v[3].w};
+  constexpr int NCH = kNP == 1 ? 2 : kNP;
+  constexpr int per = 16 / NCH;
+  uint32_t x[NCH];
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch) x[ch] = (ch == 0 ? c0 : 0u) ^ d[ch * per];
+#pragma unroll
+  for (int i = 1; i <= per; ++i)
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) x[ch] = step4x(lds, lt, x[ch], i < per ? d[ch * per + i] : 0u);
+  uint32_t c = x[0];
+#pragma unroll
+  for (int ch = 1; ch < NCH; ++ch) c = shift_op_x(lds, PDB_SLOT_HORNER, c, x[ch]);
+  return wave_tree_dpp(lds, lane, c);
+}
+
+// ---- fixed-stride batch, 4-KiB packed-tree path ------------------------------------------------
+// Same per-block loads and chains as crc_fast4k_kernel<2,1> (64 lanes per block, two 32-B pieces
+// per lane), but a wave hashes 4 blocks back to back and folds their 4 x 64 lane partials in ONE
+// packed tree: level 0 pairs lanes (2m, 2m+1) of blocks {0,1} and then {2,3} with every lane
+// doing useful work, level 1 pairs quads of all 4 blocks in one full-wave round, levels 2-5 run
+// once for all 4 blocks.  7 shift operations per 4 blocks instead of 24.
+__device__ __forceinline__ uint32_t sel(bool c, uint32_t a, uint32_t b) { return c ? a : b; }
+
+// Returns block (lane & 3)'s raw state in lanes 0..3.
+__device__ __forceinline__ uint32_t tree4_packed(const char* lds, uint32_t u, uint32_t p0, uint32_t p1,
+                                                 uint32_t p2, uint32_t p3) {
+  const bool odd = u & 1u;
+  // level 0 (shift 32): even lane 2m -> block 0/2 pair m, odd lane 2m+1 -> block 1/3 pair m
+  const uint32_t p0n = __builtin_amdgcn_update_dpp(0u, p0, 0x101, 0xF, 0xF, false);  // p0[L+1]
+  const uint32_t p1p = __builtin_amdgcn_update_dpp(0u, p1, 0x111, 0xF, 0xF, false);  // p1[L-1]
+  const uint32_t r0 = shift_op_x(lds, 0, sel(odd, p1p, p0), sel(odd, p1, p0n));
+  const uint32_t p2n = __builtin_amdgcn_update_dpp(0u, p2, 0x101, 0xF, 0xF, false);
+  const uint32_t p3p = __builtin_amdgcn_update_dpp(0u, p3, 0x111, 0xF, 0xF, false);
+  const uint32_t r1 = shift_op_x(lds, 0, sel(odd, p3p, p2), sel(odd, p3, p2n));
+  // level 1 (shift 64): lane 4j+r -> block r pair j.  r<2 reads r0 at L, L+2; r>=2 reads r1 at L-2, L
+  const bool hi = u & 2u;
+  const uint32_t r0n = __builtin_amdgcn_update_dpp(0u, r0, 0x102, 0xF, 0xF, false);  // r0[L+2]
+  const uint32_t r1p = __builtin_amdgcn_update_dpp(0u, r1, 0x112, 0xF, 0xF, false);  // r1[L-2]
+  uint32_t v = shift_op_x(lds, 1, sel(hi, r1p, r0), sel(hi, r1, r0n));
+  // levels 2..5: lane 4j+r holds block r; pair (L, L + 4*2^(k-2))
+  uint32_t y = __builtin_amdgcn_update_dpp(0u, v, 0x104, 0xF, 0xF, false);  // row_shl:4
+  if ((u & 4u) == 0) v = shift_op_x(lds, 2, v, y);
+  y = __builtin_amdgcn_update_dpp(0u, v, 0x108, 0xF, 0xF, false);  // row_shl:8
+  if ((u & 12u) == 0) v = shift_op_x(lds, 3, v, y);
+  y = __builtin_amdgcn_ds_swizzle(v, 0x401F);  // lane ^ 16
+  if ((u & 28u) == 0) v = shift_op_x(lds, 4, v, y);
+  y = __shfl_down(v, 32, 64);
+  if ((u & 60u) == 0) v = shift_op_x(lds, 5, v, y);
+  return v;
+}
+
+__device__ __forceinline__ uint32_t partial4k(const char* lds, const LaneTabs& lt, uint32_t c0,
+                                              const u32x4 (&v)[4]) {
+  uint32_t xa = c0 ^ v[0].x, xb = v[2].x;
+  const uint32_t da[8] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w};
+  const uint32_t db[8] = {v[2].x, v[2].y, v[2].z, v[2].w, v[3].x, v[3].y, v[3].z, v[3].w};
+#pragma unroll
+  for (int i = 1; i <= 8; ++i) {
+    xa = step4x(lds, lt, xa, i < 8 ? da[i] : 0u);
+    xb = step4x(lds, lt, xb, i < 8 ? db[i] : 0u);
+  }
+  return shift_op_x(lds, PDB_SLOT_HORNER, xa, xb);  // shift 2048
+}
+
+template <int kSync>
+__global__ __launch_bounds__(kThreads) void crc_pack4k_kernel(
+    const uint32_t* __restrict__ tabs, const uint8_t* __restrict__ base, uint64_t stride,
+    uint64_t nblk, uint32_t flags, uint32_t init, uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
+  char* lds = reinterpret_cast<char*>(lds_words);
+  const uint32_t u = threadIdx.x & 63u;
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWavesPerWg;
+  const uint64_t w = wave_id_uniform();
+  u32x4 buf[4];
+  load4k<2>(buf, base, stride, w < nblk ? w : nblk - 1, u);
+  stage_tables<PDB_CAT_TREE32, PDB_CAT_S2048>(lds, tabs);
+  __syncthreads();
+  if (kSync == 0 && w >= nblk) return;
+  const LaneTabs lt = lane_tabs(u);
+  const uint32_t init_raw = (flags & PDB_CRC_USE_INIT) ? ~init : 0xFFFFFFFFu;
+  const uint32_t c0 = u == 0 ? init_raw : 0u;
+  uint32_t res = 0, it = 0;
+  // kSync: the workgroup's 16 waves (16 consecutive blocks) stay in lock step, one barrier per
+  // 4-block group, so their outstanding loads cover one compact 64-KiB span at a time.
+  const uint64_t wg_first = static_cast<uint64_t>(blockIdx.x) * kWavesPerWg;
+  if (kSync > 0 && wg_first >= nblk) return;
+  uint32_t grp = 0;
+  uint64_t win0 = w;
+  for (uint64_t g = w, gw = wg_first; (kSync > 0 ? gw : g) < nblk; g += 4 * nw, gw += 4 * nw) {
+    if constexpr (kSync > 0) {
+      if ((grp++ % kSync) == 0) __syncthreads();
+    }
+    uint32_t p[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint64_t bk = g + r * nw;
+      u32x4 cur[4] = {buf[0], buf[1], buf[2], buf[3]};
+      const uint64_t bn = bk + nw;
+      if (bn < nblk) load4k<2>(buf, base, stride, bn, u);  // wave-uniform
+      p[r] = bk < nblk ? partial4k(lds, lt, c0, cur) : 0u;
+    }
+    const uint32_t v = tree4_packed(lds, u, p[0], p[1], p[2], p[3]);
+    // lane 4j+r of the 64-block window holds block (window + (4j+r)*nw): move lanes 0..3's
+    // results up by 4*(group mod 16) with one DPP-free bpermute, park, flush every 16 groups.
+    const uint32_t slot = (it & 15u) * 4u;
+    const uint32_t vv = __shfl(v, u & 3u, 64);
+    if ((u & ~3u) == slot) res = finalize(vv, flags);
+    if ((++it & 15u) == 0) {
+      const uint64_t bo = win0 + static_cast<uint64_t>(u) * nw;
+      if (bo < nblk) out[bo] = res;
+      win0 += 64 * nw;
+    }
+  }
+  if (it & 15u) {
+    const uint64_t bo = win0 + static_cast<uint64_t>(u) * nw;
+    if (u < (it & 15u) * 4u && bo < nblk) out[bo] = res;
+  }
+}
+
+// ---- generic stream kernel: any length, any alignment, fixed-stride / descriptors / sstable --
+// One wave per block; the wave walks its blocks (i, i+W, ...) and each block's rounds as one
+// software-pipelined stream of items: while item (i, r) is hashed, item (i, r+1) -- or round 0
+// of the next block, with its descriptor and head words -- is already loading.
+//   block of n bytes = head (t = n % 32 bytes) + K = n / 32 pieces of 32 B at p + t + 32c;
+//   piece c -> lane c % 64, j = c / 64; a round is 4 KiB: lane u hashes pieces j = 2r (at
+//   4096r + 32u) and 2r+1 (2048 higher) as two independent chains, folded with "shift 2048"
+//   (slot 7); rounds chain per lane with "shift 2016" (slot 6) -- the 4-KiB fast path's
+//   geometry generalised.  The head is hashed by every lane (broadcast words) from the Extend
+//   seed and becomes lane 0's starting state; lanes are rotated when K % 64 != 0 so lane v's
+//   partial ends 32*(63-v) bytes before the end; then the 6-level DPP tree (slots 0..5: 32 << k).
+struct BlkDesc {
+  const uint8_t* p;
+  uint32_t n;
+  uint32_t init_raw;  // ~Extend seed
+};
+
+struct FixedSrc {
+  const uint8_t* base;
+  uint64_t stride;
+  uint32_t len;
+  uint32_t init_raw;
+  __device__ __forceinline__ BlkDesc get(uint64_t i) const { return {base + i * stride, len, init_raw}; }
+};
+
+struct DescSrc {
+  const uint8_t* base;
+  const pdb_blk* blk;
+  uint32_t flags;
+  __device__ __forceinline__ BlkDesc get(uint64_t i) const {
+    const pdb_blk d = blk[i];
+    return {base + d.off, d.len, (flags & PDB_CRC_USE_INIT) ? ~d.init : 0xFFFFFFFFu};
+  }
+};
+
+// sstable handle: CRC over contents || type (table/table_builder.cc:197-198; format.cc:98).
+struct SstSrc {
+  uint8_t* buf;
+  const pdb_block_handle* h;
+  __device__ __forceinline__ BlkDesc get(uint64_t i) const {
+    const pdb_block_handle x = h[i];
+    return {buf + x.offset, static_cast<uint32_t>(x.size + 1), 0xFFFFFFFFu};
+  }
+};
+
+struct OutSink {
+  uint32_t* out;
+  uint32_t flags;
+  __device__ __forceinline__ void put(uint64_t i, uint32_t raw, const BlkDesc&) const {
+    out[i] = finalize(raw, flags);
+  }
+};
+
+struct VerifySink {
+  const uint32_t* expected;
+  uint8_t* ok;
+  uint32_t* nbad;
+  uint32_t flags;
+  __device__ __forceinline__ void put(uint64_t i, uint32_t raw, const BlkDesc&) const {
+    const bool good = finalize(raw, flags) == expected[i];
+    if (ok) ok[i] = good ? 1 : 0;
+    if (!good && nbad) atomicAdd(nbad, 1u);
+  }
+};
+
+// Seal: EncodeFixed32(trailer + 1, Mask(crc)) at contents + size + 1 = p + n.
+struct SealSink {
+  __device__ __forceinline__ void put(uint64_t, uint32_t raw, const BlkDesc& d) const {
+    uint8_t* tr = const_cast<uint8_t*>(d.p) + d.n;
+    const uint32_t m = pdb_mask(~raw);
+    tr[0] = static_cast<uint8_t>(m);
+    tr[1] = static_cast<uint8_t>(m >> 8);
+    tr[2] = static_cast<uint8_t>(m >> 16);
+    tr[3] = static_cast<uint8_t>(m >> 24);
+  }
+};
+
+// ReadBlock's check: Unmask(DecodeFixed32(data + n + 1)) == crc (format.cc:96-104).
+struct SstVerifySink {
+  uint8_t* ok;
+  uint32_t* nbad;
+  __device__ __forceinline__ void put(uint64_t i, uint32_t raw, const BlkDesc& d) const {
+    const uint8_t* tr = d.p + d.n;
+    const uint32_t stored = static_cast<uint32_t>(tr[0]) | (static_cast<uint32_t>(tr[1]) << 8) |
+                            (static_cast<uint32_t>(tr[2]) << 16) | (static_cast<uint32_t>(tr[3]) << 24);
+    const bool good = pdb_unmask(stored) == ~raw;
+    if (ok) ok[i] = good ? 1 : 0;
+    if (!good && nbad) atomicAdd(nbad, 1u);
+  }
+};
+
+// Raw (possibly misaligned) 32-B piece: e[0..8] are the aligned dwords covering [q - s, q - s + 36).
+struct RawPiece {
+  uint32_t e[9];
+};
+
+__device__ __forceinline__ void issue_piece(RawPiece& r, const uint8_t* q, uint32_t s) {
+  const u32x4a4* v = reinterpret_cast<const u32x4a4*>(q - s);
+  const u32x4a4 x0 = v[0], x1 = v[1];
+  r.e[0] = x0.x; r.e[1] = x0.y; r.e[2] = x0.z; r.e[3] = x0.w;
+  r.e[4] = x1.x; r.e[5] = x1.y; r.e[6] = x1.z; r.e[7] = x1.w;
+  // the 9th dword holds the piece's last byte(s) only when misaligned (never past the block)
+  r.e[8] = s ? *reinterpret_cast<const uint32_t*>(q - s + 32) : 0u;
+}
+
+// Chain over one 32-B piece: returns shift(x0_state ^ piece ...), i.e. the raw state after the
+// piece starting from `start` (injected into the first word).
+__device__ __forceinline__ uint32_t chain_piece(const char* lds, const LaneTabs& lt, uint32_t start,
+                                                const RawPiece& r, uint32_t s) {
+  uint32_t w[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) w[j] = s ? __builtin_amdgcn_alignbyte(r.e[j + 1], r.e[j], s) : r.e[j];
+  uint32_t x = start ^ w[0];
+#pragma unroll
+  for (int j = 1; j <= 8; ++j) x = step4x(lds, lt, x, j < 8 ? w[j] : 0u);
+  return x;
+}
+
+// kSync (equal-length sources): the workgroup's 16 waves advance one item at a time in lock
+// step (one barrier per item), so their outstanding loads stay within one compact span of
+// consecutive blocks -- DRAM row locality that free-running waves lose as they drift apart
+// (measured on the 4-KiB path: +8 %).
+// kDyn (unequal lengths: descriptors, sstable handles): workgroup g owns the contiguous block
+// range [g*N/G, (g+1)*N/G) and its 16 waves take the next block from an LDS counter (LDS slot 5,
+// freed by folding tree level 5 as two "shift 512"s): the CU's work is balanced and its
+// outstanding loads stay on a compact run of consecutive blocks.
+template <class Src, class Sink, int kSync, bool kDyn = false>
+__global__ __launch_bounds__(kThreads) void crc_stream_kernel(const uint32_t* __restrict__ tabs,
+                                                               Src src, uint64_t nblk, Sink sink) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
+  char* lds = reinterpret_cast<char*>(lds_words);
+  stage_tables<PDB_CAT_TREE32, PDB_CAT_H2016, PDB_CAT_S2048, kDyn>(lds, tabs);
+  uint32_t* ctr = reinterpret_cast<uint32_t*>(lds + PDB_MAIN_BYTES + 5 * 4096u);
+  const uint64_t g_lo = nblk * blockIdx.x / gridDim.x, g_hi = nblk * (blockIdx.x + 1) / gridDim.x;
+  if (kDyn && threadIdx.x == 0) *ctr = kWavesPerWg;  // next block, relative to g_lo
+  __syncthreads();
+  const uint32_t u = threadIdx.x & 63u;
+  const LaneTabs lt = lane_tabs(u);
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWavesPerWg;
+  auto next_block = [&](uint64_t cur) -> uint64_t {
+    if constexpr (kDyn) {
+      uint32_t r = 0;
+      if (u == 0) r = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      return g_lo + __builtin_amdgcn_readfirstlane(r);
+    } else {
+      return cur + nw;
+    }
+  };
+  const uint64_t nend = kDyn ? g_hi : nblk;
+  uint64_t i = kDyn ? g_lo + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : wave_id_uniform();
+  bool active = i < nend;
+  if (kSync == 0 && !active) return;
+
+  // the item being loaded: block d, round k
+  BlkDesc d{};
+  uint32_t k = 0;
+  RawPiece na, nb;
+  uint32_t nhw = 0, nhb = 0;
+  auto issue = [&](const BlkDesc& bd, uint32_t kk) {
+    const uint32_t t = bd.n & 31u, K = bd.n >> 5;
+    const uint8_t* q0 = bd.p + t;
+    const uint32_t s = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(q0) & 3u);
+    const uint32_t ca = u + (kk << 7), cb = ca + 64u;
+    if (ca < K) issue_piece(na, q0 + static_cast<uint64_t>(ca) * 32u, s);
+    if (cb < K) issue_piece(nb, q0 + static_cast<uint64_t>(cb) * 32u, s);
+    if (kk == 0) {
+      const uint32_t lead = t & 3u, nh = t >> 2;
+      if (u >= 1 && u <= nh) nhw = ld32u(bd.p + lead + 4u * (u - 1));
+      if (u == 0 && lead) {
+        uint32_t v = bd.p[0];
+        if (lead > 1) v |= static_cast<uint32_t>(bd.p[1]) << 8;
+        if (lead > 2) v |= static_cast<uint32_t>(bd.p[2]) << 16;
+        nhb = v;
+      }
+    }
+  };
+  if (active) {
+    d = src.get(i);
+    issue(d, 0);
+  }
+  uint32_t acc = 0;
+  // kSync (equal lengths): every wave of the workgroup runs as many items as its first wave
+  // (the one with the most blocks), so a plain barrier per item needs no LDS reduction.
+  uint64_t items_left = 0, item = 0;
+  if constexpr (kSync > 0) {
+    const uint64_t wg_first = static_cast<uint64_t>(blockIdx.x) * kWavesPerWg;
+    if (wg_first >= nblk) return;
+    const uint32_t n0 = src.get(wg_first).n, K0 = n0 >> 5;
+    items_left = ((nblk - wg_first + nw - 1) / nw) * (K0 ? (K0 + 127u) >> 7 : 1u);
+  }
+  for (;;) {
+    if constexpr (kSync > 0) {
+      if (items_left-- == 0) break;
+      if ((item++ % kSync) == 0) __syncthreads();
+      if (!active) continue;
+    }
+    const RawPiece ca_ = na, cb_ = nb;
+    const uint32_t chw = nhw, chb = nhb;
+    const BlkDesc cd = d;
+    const uint32_t ck = k;
+    const uint32_t K = cd.n >> 5;
+    const uint32_t R = K ? (K + 127u) >> 7 : 1u;
+    const bool last_round = ck + 1 >= R;
+    const uint64_t ni = last_round ? next_block(i) : i;
+    const bool have_next = ni < nend;
+    if (last_round && have_next) d = src.get(ni);
+    k = last_round ? 0 : ck + 1;
+    if (have_next) issue(d, k);
+
+    if (ck == 0) {  // head: every lane hashes the same (broadcast) head bytes from the seed
+      const uint32_t t = cd.n & 31u, lead = t & 3u, nh = t >> 2;
+      uint32_t h = cd.init_raw;
+      const uint32_t lb = __builtin_amdgcn_readfirstlane(chb);
+      for (uint32_t j = 0; j < lead; ++j) h = step1(lds, lt, h, (lb >> (8 * j)) & 0xffu);
+      for (uint32_t j = 0; j < nh; ++j) h = step4(lds, lt, h, __builtin_amdgcn_readlane(chw, j + 1));
+      acc = (u == 0) ? h : 0u;
+    }
+    const uint32_t s = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(cd.p + (cd.n & 31u)) & 3u);
+    const uint32_t ca = u + (ck << 7), cb = ca + 64u;
+    if (cb < K) {
+      const uint32_t start = ck ? shift_op(lds, PDB_SLOT_HORNER, acc) : acc;
+      const uint32_t xa = chain_piece(lds, lt, start, ca_, s);
+      const uint32_t xb = chain_piece(lds, lt, 0u, cb_, s);
+      acc = shift_op_x(lds, 7, xa, xb);
+    } else if (ca < K) {
+      const uint32_t start = ck ? shift_op(lds, PDB_SLOT_HORNER, acc) : acc;
+      acc = chain_piece(lds, lt, start, ca_, s);
+    }
+    if (last_round) {
+      uint32_t raw = acc;
+      if (K) {
+        const uint32_t q = K & 63u;
+        if (q) acc = __shfl(acc, (u + q) & 63u, 64);
+        raw = wave_tree_dpp<kDyn>(lds, u, acc);
+      }
+      if (u == 0) sink.put(i, raw, cd);
+      i = ni;
+      if (!have_next) {
+        active = false;
+        if constexpr (kSync == 0) break;
+      }
+    }
+  }
+}
+
+uint32_t grid_for(const LaunchGeom& g, uint64_t nblk) {
+  const uint64_t want = (nblk + kWavesPerWg - 1) / kWavesPerWg;
+  return static_cast<uint32_t>(want < g.grid ? (want ? want : 1) : g.grid);
+}
+
+}  // namespace
+}  // namespace pdb

@@ -38,6 +38,13 @@ hipError_t launch_desc(const LaunchGeom& g, const uint32_t* d_tables, const uint
 hipError_t launch_sst(const LaunchGeom& g, const uint32_t* d_tables, uint8_t* buf, uint64_t buf_len,
                       const pdb_block_handle* h, uint64_t n, bool seal, uint8_t* ok, uint32_t* nbad,
                       hipStream_t s);
+// crc32c_variants.hip -- A/B variants (pdb_diag_set_variant) and calibration kernels
+hipError_t launch_fixed_variant(int v, const LaunchGeom& g, const uint32_t* d_tables, const uint8_t* base,
+                                uint64_t stride, uint32_t len, uint64_t nblk, uint32_t flags, uint32_t init,
+                                uint32_t* out, hipStream_t s);
+hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tables, const uint8_t* base,
+                               const pdb_blk* blk, uint64_t nblk, uint32_t flags, uint32_t* out,
+                               hipStream_t s);
 hipError_t launch_read_stream(const uint8_t* base, uint64_t nbytes, uint32_t* out, hipStream_t s);
 hipError_t launch_read_pattern4k(const LaunchGeom& g, const uint8_t* base, uint64_t nblk,
                                  int variant, uint32_t* out, hipStream_t s);

@@ -1,0 +1,400 @@
+// crc32c_variants.hip -- A/B kernel variants (selected with pdb_diag_set_variant, all
+// parity-tested in tests/test_gpu_parity.py) and the load-pattern calibration kernels behind the
+// roofline numbers in DESIGN.md §6.  Not on the shipped path unless a variant is selected.
+#include "crc32c_device.h"
+
+namespace pdb {
+namespace {
+
+template <int kNP, int kDepth, bool kIssueFirst = false>
+__global__ __launch_bounds__(kThreads) void crc_fast4k_kernel(
+    const uint32_t* __restrict__ tabs, const uint8_t* __restrict__ base, uint64_t stride,
+    uint64_t nblk, uint32_t flags, uint32_t init, uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
+  char* lds = reinterpret_cast<char*>(lds_words);
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWavesPerWg;
+  const uint64_t b0 = wave_id_uniform();
+  // Issue the first kDepth blocks' loads before staging the tables: the table copy then
+  // overlaps the first HBM round trip.
+  u32x4 buf[kDepth][4];
+#pragma unroll
+  for (int k = 0; k < kDepth; ++k) {
+    const uint64_t b = b0 + k * nw;
+    load4k<kNP>(buf[k], base, stride, b < nblk ? b : (nblk - 1), lane);
+  }
+  constexpr int kTree = kNP == 1 ? PDB_CAT_TREE64 : (kNP == 2 ? PDB_CAT_TREE32 : PDB_CAT_TREE16);
+  constexpr int kHorner = kNP == 1 ? PDB_CAT_TREE32 : (kNP == 2 ? PDB_CAT_S2048 : PDB_CAT_S1024);
+  stage_tables<kTree, kHorner>(lds, tabs);
+  __syncthreads();
+  const LaneTabs lt = lane_tabs(lane);
+  const uint32_t init_raw = (flags & PDB_CRC_USE_INIT) ? ~init : 0xFFFFFFFFu;
+  // Results are parked in a register (lane j holds the j-th block's CRC of the current 64-block
+  // window) and flushed with one scattered 64-lane store per window: a per-block store from
+  // lane 0 would sit in vmcnt behind the next block's loads and make every wait drain it.
+  uint32_t res = 0;
+  uint32_t it = 0;
+  uint64_t win0 = b0;  // first block of the current window
+  for (uint64_t b = b0; b < nblk; b += kDepth * nw) {
+#pragma unroll
+    for (int k = 0; k < kDepth; ++k) {
+      const uint64_t bk = b + k * nw;
+      if (bk >= nblk) break;  // wave-uniform
+      u32x4 cur[4] = {buf[k][0], buf[k][1], buf[k][2], buf[k][3]};
+      const uint64_t bn = bk + kDepth * nw;
+      load4k<kNP>(buf[k], base, stride, bn < nblk ? bn : bk, lane);  // clamp: valid block
+      if constexpr (kIssueFirst) __builtin_amdgcn_sched_barrier(0);
+      const uint32_t c = hash4k<kNP>(lds, lt, lane, lane == 0 ? init_raw : 0u, cur);
+      const uint32_t v = finalize(__builtin_amdgcn_readfirstlane(c), flags);
+      if (lane == (it & 63u)) res = v;
+      if ((++it & 63u) == 0) {
+        out[win0 + static_cast<uint64_t>(lane) * nw] = res;
+        win0 += 64 * nw;
+      }
+    }
+  }
+  if ((it & 63u) && lane < (it & 63u)) out[win0 + static_cast<uint64_t>(lane) * nw] = res;
+}
+
+// ---- fixed-stride batch, 4-KiB ping-pong path ----------------------------------------------------
+// crc_fast4k_kernel<2,1> with two named load buffers and a scheduling barrier right after each
+// load issue, so the next block's 4 KiB is in flight for the WHOLE hash of the current block
+// (hipcc otherwise sinks the loads a third of the way into the chain to reuse registers).
+__global__ __launch_bounds__(kThreads) void crc_pingpong4k_kernel(
+    const uint32_t* __restrict__ tabs, const uint8_t* __restrict__ base, uint64_t stride,
+    uint64_t nblk, uint32_t flags, uint32_t init, uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
+  char* lds = reinterpret_cast<char*>(lds_words);
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWavesPerWg;
+  const uint64_t b0 = wave_id_uniform();
+  u32x4 A[4], B[4];
+  load4k<2>(A, base, stride, b0 < nblk ? b0 : nblk - 1, lane);
+  stage_tables<PDB_CAT_TREE32, PDB_CAT_S2048>(lds, tabs);
+  __syncthreads();
+  if (b0 >= nblk) return;
+  const LaneTabs lt = lane_tabs(lane);
+  const uint32_t init_raw = (flags & PDB_CRC_USE_INIT) ? ~init : 0xFFFFFFFFu;
+  const uint32_t c0 = lane == 0 ? init_raw : 0u;
+  uint32_t res = 0, it = 0;
+  uint64_t win0 = b0;
+  auto emit = [&](uint32_t c) {
+    const uint32_t v = finalize(__builtin_amdgcn_readfirstlane(c), flags);
+    if (lane == (it & 63u)) res = v;
+    if ((++it & 63u) == 0) {
+      out[win0 + static_cast<uint64_t>(lane) * nw] = res;
+      win0 += 64 * nw;
+    }
+  };
+  for (uint64_t b = b0; b < nblk; b += 2 * nw) {
+    const uint64_t b1 = b + nw, b2 = b + 2 * nw;
+    load4k<2>(B, base, stride, b1 < nblk ? b1 : b, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    emit(hash4k<2>(lds, lt, lane, c0, A));
+    if (b1 >= nblk) break;
+    load4k<2>(A, base, stride, b2 < nblk ? b2 : b1, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    emit(hash4k<2>(lds, lt, lane, c0, B));
+  }
+  if ((it & 63u) && lane < (it & 63u)) out[win0 + static_cast<uint64_t>(lane) * nw] = res;
+}
+
+// Dynamic variant of the packed kernel: workgroup g owns blocks [g*N/G, (g+1)*N/G); each wave
+// takes 4 consecutive blocks at a time from an LDS counter (operator slot 7 is unused here) and
+// writes their 4 CRCs with one 16-B store.
+__global__ __launch_bounds__(kThreads) void crc_pack4k_dyn_kernel(
+    const uint32_t* __restrict__ tabs, const uint8_t* __restrict__ base, uint64_t stride,
+    uint64_t nblk, uint32_t flags, uint32_t init, uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
+  char* lds = reinterpret_cast<char*>(lds_words);
+  uint32_t* ctr = reinterpret_cast<uint32_t*>(lds + PDB_MAIN_BYTES + 7 * 4096u);
+  const uint32_t u = threadIdx.x & 63u;
+  const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t g_lo = nblk * blockIdx.x / gridDim.x, g_hi = nblk * (blockIdx.x + 1) / gridDim.x;
+  uint64_t grp = g_lo + 4u * wid;  // first group of this wave (static), then from the counter
+  u32x4 buf[4];
+  load4k<2>(buf, base, stride, grp < g_hi ? grp : (nblk ? nblk - 1 : 0), u);
+  stage_tables<PDB_CAT_TREE32, PDB_CAT_S2048>(lds, tabs);
+  if (threadIdx.x == 0) *ctr = kWavesPerWg;  // next group, in groups relative to g_lo
+  __syncthreads();
+  const LaneTabs lt = lane_tabs(u);
+  const uint32_t init_raw = (flags & PDB_CRC_USE_INIT) ? ~init : 0xFFFFFFFFu;
+  const uint32_t c0 = u == 0 ? init_raw : 0u;
+  while (grp < g_hi) {
+    uint32_t r0 = 0;
+    if (u == 0) r0 = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const uint64_t ngrp = g_lo + 4u * static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(r0));
+    uint32_t p[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint64_t bk = grp + r;
+      u32x4 cur[4] = {buf[0], buf[1], buf[2], buf[3]};
+      const uint64_t bn = r < 3 ? bk + 1 : ngrp;
+      if (bn < g_hi) load4k<2>(buf, base, stride, bn, u);  // wave-uniform
+      p[r] = bk < g_hi ? partial4k(lds, lt, c0, cur) : 0u;
+    }
+    const uint32_t v = tree4_packed(lds, u, p[0], p[1], p[2], p[3]);
+    if (u < 4 && grp + u < g_hi) out[grp + u] = finalize(v, flags);
+    grp = ngrp;
+  }
+}
+
+// ---- fixed-stride batch, 4-KiB team path ----------------------------------------------------
+// A wave hashes T = 64/kG consecutive 4-KiB blocks at once: team t (lanes [t*kG, (t+1)*kG))
+// owns block t.  Within a team, lane u owns R = 4096/(32*kG) pieces of 32 B, piece r at
+// r*32*kG + 32*u, so every 16-B load instruction covers T blocks x kG lanes at a 32-B lane
+// stride.  Each piece is an independent 8-step chain; the R chains fold with "shift by
+// 32*kG bytes" (slot 6), then a log2(kG)-level team tree (slots 0.., shift by 32 << k) whose
+// VALU/LDS instructions serve all T blocks at once -- the per-block tree cost drops by T.
+template <int kG>
+__device__ __forceinline__ uint32_t team_tree(const char* lds, uint32_t u, uint32_t c) {
+  uint32_t y;
+  y = __builtin_amdgcn_update_dpp(0u, c, 0x101, 0xF, 0xF, false);
+  if ((u & 1u) == 0) c = shift_op_x(lds, 0, c, y);
+  y = __builtin_amdgcn_update_dpp(0u, c, 0x102, 0xF, 0xF, false);
+  if ((u & 3u) == 0) c = shift_op_x(lds, 1, c, y);
+  y = __builtin_amdgcn_update_dpp(0u, c, 0x104, 0xF, 0xF, false);
+  if ((u & 7u) == 0) c = shift_op_x(lds, 2, c, y);
+  y = __builtin_amdgcn_update_dpp(0u, c, 0x108, 0xF, 0xF, false);
+  if ((u & 15u) == 0) c = shift_op_x(lds, 3, c, y);
+  if constexpr (kG >= 32) {
+    y = __builtin_amdgcn_ds_swizzle(c, 0x401F);
+    if ((u & 31u) == 0) c = shift_op_x(lds, 4, c, y);
+  }
+  if constexpr (kG >= 64) {
+    y = __builtin_amdgcn_readlane(c, 32);
+    if (u == 0) c = shift_op_x(lds, 5, c, y);
+  }
+  return c;
+}
+
+template <int kG, int kDepth>
+__global__ __launch_bounds__(kThreads) void crc_team4k_kernel(
+    const uint32_t* __restrict__ tabs, const uint8_t* __restrict__ base, uint64_t stride,
+    uint64_t nblk, uint32_t flags, uint32_t init, uint32_t* __restrict__ out) {
+  constexpr uint32_t T = 64 / kG;             // blocks per wave-iteration
+  constexpr uint32_t R = 4096 / (32 * kG);    // 32-B pieces per lane per block
+  constexpr uint32_t ROW = 32 * kG;           // bytes between a lane's pieces
+  constexpr int kFold = kG == 32 ? PDB_CAT_S1024 : (kG == 16 ? 5 /* 512 */ : PDB_CAT_S2048);
+  __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
+  char* lds = reinterpret_cast<char*>(lds_words);
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t t = lane / kG, u = lane % kG;
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWavesPerWg;
+  const uint64_t ngroups = (nblk + T - 1) / T;  // wave-iterations needed in total
+  const uint64_t g0 = wave_id_uniform();
+
+  auto load = [&](u32x4 (&v)[2 * R], uint64_t g) {
+    uint64_t b = g * T + t;
+    if (b >= nblk) b = nblk - 1;  // clamp: a valid block (result discarded)
+    const uint8_t* p = base + b * stride + u * 32u;
+#pragma unroll
+    for (uint32_t r = 0; r < R; ++r) {
+      v[2 * r] = *reinterpret_cast<const u32x4*>(p + r * ROW);
+      v[2 * r + 1] = *reinterpret_cast<const u32x4*>(p + r * ROW + 16u);
+    }
+  };
+
+  u32x4 nxt[2 * R];
+  if constexpr (kDepth > 0) load(nxt, g0 < ngroups ? g0 : 0);
+  stage_tables<PDB_CAT_TREE32, kFold>(lds, tabs);
+  __syncthreads();
+  const LaneTabs lt = lane_tabs(lane);
+  const uint32_t init_raw = (flags & PDB_CRC_USE_INIT) ? ~init : 0xFFFFFFFFu;
+  for (uint64_t g = g0; g < ngroups; g += nw) {
+    u32x4 cur[2 * R];
+    if constexpr (kDepth > 0) {
+#pragma unroll
+      for (uint32_t i = 0; i < 2 * R; ++i) cur[i] = nxt[i];
+      const uint64_t gn = g + nw;
+      load(nxt, gn < ngroups ? gn : g);
+    } else {
+      load(cur, g);
+    }
+    uint32_t x[R];
+#pragma unroll
+    for (uint32_t r = 0; r < R; ++r) x[r] = cur[2 * r].x ^ ((r == 0 && u == 0) ? init_raw : 0u);
+#pragma unroll
+    for (int i = 1; i <= 8; ++i) {
+#pragma unroll
+      for (uint32_t r = 0; r < R; ++r) {
+        const u32x4& a = cur[2 * r];
+        const u32x4& bq = cur[2 * r + 1];
+        const uint32_t w = i == 1 ? a.y : i == 2 ? a.z : i == 3 ? a.w : i == 4 ? bq.x
+                         : i == 5 ? bq.y : i == 6 ? bq.z : i == 7 ? bq.w : 0u;
+        x[r] = step4x(lds, lt, x[r], w);
+      }
+    }
+    uint32_t c = x[0];
+#pragma unroll
+    for (uint32_t r = 1; r < R; ++r) c = shift_op_x(lds, PDB_SLOT_HORNER, c, x[r]);
+    c = team_tree<kG>(lds, u, c);
+    const uint64_t b = g * T + t;
+    if (u == 0 && b < nblk) out[b] = finalize(c, flags);
+  }
+}
+
+// ---- diagnostics ------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void read_stream_kernel(const u32x4* __restrict__ src,
+                                                          uint64_t n16, uint32_t* __restrict__ out) {
+  u32x4 acc = {0, 0, 0, 0};
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < n16; i += 4 * stride) {
+    const u32x4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+    acc ^= a ^ b ^ c ^ d;
+  }
+  for (; i < n16; i += stride) acc ^= src[i];
+  uint32_t r = acc.x ^ acc.y ^ acc.z ^ acc.w;
+  for (int k = 32; k; k >>= 1) r ^= __shfl_xor(r, k, 64);
+  if ((threadIdx.x & 63) == 0) atomicXor(out, r);
+}
+
+// Load-pattern calibration for 4-KiB blocks, no CRC work.
+//   kPat 0: lane l reads bytes [64l, 64l+64) of the block (the fast path's pattern)
+//   kPat 1: lane l reads 16 B at 16l + 1024j, j = 0..3 (each instruction 1 KiB contiguous)
+//   kDepth: blocks in flight per wave; kAssign 0: wave-interleaved blocks, 1: contiguous per WG
+template <int kPat, int kDepth, int kAssign, bool kSync = false>
+__global__ __launch_bounds__(kThreads) void read_pattern4k_kernel(const uint8_t* __restrict__ base,
+                                                                  uint64_t nblk,
+                                                                  uint32_t* __restrict__ out) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWavesPerWg;
+  uint32_t acc = 0;
+  uint64_t first, step, last;
+  if constexpr (kAssign == 0) {
+    first = wave_id_uniform();
+    step = nw;
+    last = nblk;
+  } else {
+    const uint64_t per = (nblk + gridDim.x - 1) / gridDim.x;
+    const uint64_t lo = blockIdx.x * per;
+    first = lo + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    step = kWavesPerWg;
+    last = lo + per < nblk ? lo + per : nblk;
+  }
+  const uint64_t wg_first = static_cast<uint64_t>(blockIdx.x) * kWavesPerWg;
+  for (uint64_t b = first, bw = wg_first; (kSync ? bw : b) < last; b += step * kDepth, bw += step * kDepth) {
+    if constexpr (kSync) __syncthreads();
+    u32x4 x = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < kDepth; ++k) {
+      const uint64_t bk = b + k * step;
+      if (bk < last) {
+        const uint8_t* blk = base + bk * 4096u;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t off = kPat == 0 ? lane * 64u + j * 16u
+                             : (kPat == 1 ? lane * 16u + j * 1024u
+                                          : lane * 32u + (j >> 1) * 2048u + (j & 1) * 16u);
+          x ^= *reinterpret_cast<const u32x4*>(blk + off);
+        }
+      }
+    }
+    acc ^= x.x ^ x.y ^ x.z ^ x.w;
+  }
+  for (int k = 32; k; k >>= 1) acc ^= __shfl_xor(acc, k, 64);
+  if (lane == 0) atomicXor(out, acc);
+}
+
+}  // namespace
+
+hipError_t launch_fixed_variant(int v, const LaunchGeom& g, const uint32_t* d_tables, const uint8_t* base,
+                                uint64_t stride, uint32_t len, uint64_t nblk, uint32_t flags, uint32_t init,
+                                uint32_t* out, hipStream_t s) {
+  const dim3 grid(grid_for(g, nblk)), block(kThreads);
+  const bool fast = len == 4096u && (reinterpret_cast<uintptr_t>(base) & 15u) == 0 &&
+                    (stride & 15u) == 0;
+  if (!fast) {
+    const FixedSrc src{base, stride, len, (flags & PDB_CRC_USE_INIT) ? ~init : 0xFFFFFFFFu};
+#define PDB_STREAM_FIXED(P)                                                                       \
+  hipLaunchKernelGGL((crc_stream_kernel<FixedSrc, OutSink, P>), grid, block, 0, s, d_tables, src, nblk, \
+                     OutSink{out, flags})
+    switch (v) {  // lock-step period in items (0 = free-running, static strided blocks)
+      case 8: PDB_STREAM_FIXED(0); break;
+      case 9: PDB_STREAM_FIXED(1); break;
+      case 10: PDB_STREAM_FIXED(4); break;
+      case 11: PDB_STREAM_FIXED(8); break;
+      default:
+        hipLaunchKernelGGL((crc_stream_kernel<FixedSrc, OutSink, 0, true>), grid, block, 0, s, d_tables, src,
+                           nblk, OutSink{out, flags});
+        break;
+    }
+#undef PDB_STREAM_FIXED
+    return hipGetLastError();
+  }
+#define PDB_FAST(NP, D)                                                                       \
+  hipLaunchKernelGGL((crc_fast4k_kernel<NP, D>), grid, block, 0, s, d_tables, base, stride, nblk, \
+                     flags, init, out)
+#define PDB_TEAM(G, D)                                                                        \
+  hipLaunchKernelGGL((crc_team4k_kernel<G, D>), grid, block, 0, s, d_tables, base, stride, nblk, \
+                     flags, init, out)
+#define PDB_K(K) hipLaunchKernelGGL(K, grid, block, 0, s, d_tables, base, stride, nblk, flags, init, out)
+  switch (v) {
+    case 1: PDB_FAST(2, 1); break;  // one 64-lane tree per block, free-running
+    case 2: PDB_FAST(1, 1); break;  // 64-B lane pieces
+    case 3: PDB_FAST(4, 1); break;  // coalesced 16-B pieces, 4 chains + 3 Horner shifts
+    case 4: PDB_TEAM(32, 1); break;  // 2 blocks per wave, 32-lane teams
+    case 5: PDB_TEAM(16, 0); break;  // 4 blocks per wave, 16-lane teams
+    case 6: PDB_K(crc_pingpong4k_kernel); break;
+    case 7: PDB_K((crc_fast4k_kernel<2, 1, true>)); break;  // loads issued before the hash
+    case 8: PDB_K(crc_pack4k_kernel<0>); break;  // packed tree, free-running
+    case 9: PDB_K(crc_pack4k_kernel<2>); break;  // lock-step every 2 groups
+    case 10: PDB_K(crc_pack4k_kernel<4>); break;
+    case 11: PDB_K(crc_pack4k_dyn_kernel); break;  // workgroup-local dynamic groups
+    default: PDB_K(crc_pack4k_kernel<1>); break;
+  }
+#undef PDB_FAST
+#undef PDB_TEAM
+#undef PDB_K
+  return hipGetLastError();
+}
+
+hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tables, const uint8_t* base,
+                               const pdb_blk* blk, uint64_t nblk, uint32_t flags, uint32_t* out,
+                               hipStream_t s) {
+  const dim3 grid(grid_for(g, nblk)), block(kThreads);
+  const DescSrc src{base, blk, flags};
+  if (v == 8)  // static strided assignment (free-running)
+    hipLaunchKernelGGL((crc_stream_kernel<DescSrc, OutSink, 0, false>), grid, block, 0, s, d_tables, src,
+                       nblk, OutSink{out, flags});
+  else
+    hipLaunchKernelGGL((crc_stream_kernel<DescSrc, OutSink, 0, true>), grid, block, 0, s, d_tables, src, nblk,
+                       OutSink{out, flags});
+  return hipGetLastError();
+}
+
+hipError_t launch_read_stream(const uint8_t* base, uint64_t nbytes, uint32_t* out, hipStream_t s) {
+  const uint64_t n16 = nbytes / 16;
+  hipLaunchKernelGGL(read_stream_kernel, dim3(256 * 16), dim3(256), 0, s,
+                     reinterpret_cast<const u32x4*>(base), n16, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_read_pattern4k(const LaunchGeom& g, const uint8_t* base, uint64_t nblk,
+                                 int variant, uint32_t* out, hipStream_t s) {
+  const dim3 grid(g.grid), block(kThreads);
+#define PDB_RP(P, D, A) \
+  hipLaunchKernelGGL((read_pattern4k_kernel<P, D, A>), grid, block, 0, s, base, nblk, out)
+  switch (variant) {
+    case 1: PDB_RP(1, 1, 0); break;
+    case 2: PDB_RP(0, 2, 0); break;
+    case 3: PDB_RP(1, 2, 0); break;
+    case 4: PDB_RP(0, 1, 1); break;
+    case 5: PDB_RP(1, 1, 1); break;
+    case 6: PDB_RP(1, 4, 0); break;
+    case 7: PDB_RP(0, 4, 0); break;
+    case 8: PDB_RP(2, 1, 0); break;
+    case 9: PDB_RP(2, 2, 0); break;
+    // workgroup lock-step (one barrier per iteration), as in the shipped CRC kernels
+    case 10: hipLaunchKernelGGL((read_pattern4k_kernel<2, 1, 0, true>), grid, block, 0, s, base, nblk, out); break;
+    case 11: hipLaunchKernelGGL((read_pattern4k_kernel<1, 1, 0, true>), grid, block, 0, s, base, nblk, out); break;
+    case 12: hipLaunchKernelGGL((read_pattern4k_kernel<2, 4, 0, true>), grid, block, 0, s, base, nblk, out); break;
+    case 13: hipLaunchKernelGGL((read_pattern4k_kernel<1, 4, 0, true>), grid, block, 0, s, base, nblk, out); break;
+    default: PDB_RP(0, 1, 0); break;
+  }
+#undef PDB_RP
+  return hipGetLastError();
+}
+
+}  // namespace pdb
