@@ -24,7 +24,8 @@
  *   - Caller owns every buffer.  Device-resident entry points allocate nothing and are
  *     stream-ordered (capturable into a hipGraph).  Host entry points stage through a cached
  *     per-device workspace that only grows.
- *   - Per-block length is < 2^32 bytes (the reference narrows to uint32_t: util/crc32c.cc:19-23,589).
+ *   - Per-block length in batches is < 2^32 bytes (the reference narrows to uint32_t:
+ *     util/crc32c.cc:19-23,589); a single span (pdb_crc32c_extend*) may be longer.
  *   - Thread-safe: host entry points serialise per device; device entry points are pure launches.
  */
 #ifndef PDB_CRC32C_H_
@@ -75,10 +76,19 @@ const char* pdb_last_error(void); /* thread-local message of the last failure */
 int pdb_crc32c_current_device(void);
 
 /* ---- scalar, LevelDB-compatible (util/crc32c.h:17-40) ---------------------------------------- */
-uint32_t pdb_crc32c_extend(uint32_t init_crc, const void* data, size_t n); /* host data */
+uint32_t pdb_crc32c_extend(uint32_t init_crc, const void* data, size_t n); /* host data; spans
+                                                                             >= 8 MiB are split */
 uint32_t pdb_crc32c_value(const void* data, size_t n);                     /* host data */
 uint32_t pdb_crc32c_mask(uint32_t crc);
 uint32_t pdb_crc32c_unmask(uint32_t masked_crc);
+
+/* ---- long spans ------------------------------------------------------------------------------
+ * One span of any length (up to 2^45 bytes, so also past the reference's silent 4 GiB length
+ * narrowing, util/crc32c.cc:19-23): hashed as up to 16384 segments in parallel, folded on the
+ * device.  *d_out = Extend(init_crc, d_data[0..n)).  d_scratch: >= extend_scratch_words(n) u32. */
+uint64_t pdb_crc32c_extend_scratch_words(uint64_t n);
+int pdb_crc32c_extend_device(uint32_t init_crc, const void* d_data, uint64_t n, uint32_t* d_scratch,
+                             uint64_t scratch_words, uint32_t* d_out, void* stream);
 
 /* ---- device-resident batches (the hot path) ------------------------------------------------ */
 /* Blocks i in [0,nblk): bytes [d_base + i*stride, +len).  Seed `init` applies to every block when

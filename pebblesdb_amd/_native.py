@@ -46,6 +46,8 @@ SIGNATURES = {
     "pdb_crc32c_value": (_U32, [_V, ctypes.c_size_t]),
     "pdb_crc32c_mask": (_U32, [_U32]),
     "pdb_crc32c_unmask": (_U32, [_U32]),
+    "pdb_crc32c_extend_scratch_words": (_U64, [_U64]),
+    "pdb_crc32c_extend_device": (_I, [_U32, _V, _U64, _V, _U64, _V, _V]),
     "pdb_crc32c_batch_device_fixed": (_I, [_V, _U64, _U32, _U64, _U32, _U32, _V, _V]),
     "pdb_crc32c_batch_device": (_I, [_V, _V, _U64, _U32, _V, _V]),
     "pdb_crc32c_verify_device": (_I, [_V, _V, _U64, _U32, _V, _V, _V, _V]),

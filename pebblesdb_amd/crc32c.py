@@ -34,7 +34,7 @@ HANDLE_DTYPE = np.dtype([("offset", "<u8"), ("size", "<u8")])  # == pdb_block_ha
 __all__ = [
     "extend", "value", "mask", "unmask", "batch_fixed", "batch", "verify", "batch_host",
     "make_blocks", "blocks_to_device", "PdbError", "MASK_OUTPUT", "USE_INIT", "BLK_DTYPE",
-    "HANDLE_DTYPE", "init_device", "launch_geometry", "fill_splitmix",
+    "HANDLE_DTYPE", "init_device", "launch_geometry", "fill_splitmix", "extend_device",
 ]
 
 
@@ -176,6 +176,19 @@ def batch_host(base, blocks: np.ndarray, *, masked: bool = False, use_init: bool
     flags = (MASK_OUTPUT if masked else 0) | (USE_INIT if use_init else 0)
     check(lib().pdb_crc32c_batch_host(p, n, blocks.ctypes.data, len(blocks), flags, out.ctypes.data))
     return out
+
+
+def extend_device(init_crc: int, d_data, nbytes: int | None = None, stream=None) -> int:
+    """Extend(init_crc, span) for ONE device-resident span of any length (split into up to 16384
+    segments hashed in parallel and folded on the device).  Returns the CRC (synchronises)."""
+    torch = _torch()
+    n = d_data.numel() * d_data.element_size() if nbytes is None else nbytes
+    words = int(lib().pdb_crc32c_extend_scratch_words(n))
+    scratch = torch.empty(words, dtype=torch.int32, device=d_data.device)
+    out = torch.empty(1, dtype=torch.int32, device=d_data.device)
+    check(lib().pdb_crc32c_extend_device(init_crc & 0xFFFFFFFF, _dev_ptr(d_data), n, _dev_ptr(scratch), words,
+                                         _dev_ptr(out), _stream_ptr(stream)))
+    return int(out.cpu().numpy().view(np.uint32)[0])
 
 
 def launch_geometry(device: int = -1):

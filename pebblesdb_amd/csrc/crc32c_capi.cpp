@@ -34,6 +34,7 @@ int hip_fail(hipError_t e, const char* what) {
 struct DevState {
   int device = -1;
   uint32_t* d_tables = nullptr;
+  uint32_t* d_pow2 = nullptr;  // 64 power-of-two shift operators (long-span combine)
   LaunchGeom geom{256, 1024};
   hipStream_t stream = nullptr;
   std::mutex mu;  // guards the host-staging workspace below
@@ -80,6 +81,12 @@ int get_state(DevState** out) {
   if (e != hipSuccess) return hip_fail(e, "hipMalloc(tables)");
   e = hipMemcpy(s->d_tables, tabs.data(), tabs.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
   if (e != hipSuccess) return hip_fail(e, "hipMemcpy(tables)");
+  std::vector<uint32_t> pow2(PDB_POW2_WORDS);
+  build_pow2_tables(pow2.data());
+  e = hipMalloc(&s->d_pow2, pow2.size() * sizeof(uint32_t));
+  if (e != hipSuccess) return hip_fail(e, "hipMalloc(pow2)");
+  e = hipMemcpy(s->d_pow2, pow2.data(), pow2.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+  if (e != hipSuccess) return hip_fail(e, "hipMemcpy(pow2)");
   e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
   if (e != hipSuccess) return hip_fail(e, "hipStreamCreate");
   __atomic_store_n(&g_dev[dev], s.get(), __ATOMIC_RELEASE);
@@ -181,6 +188,35 @@ int host_desc(const uint8_t* base, uint64_t base_len, const pdb_blk* blk, uint64
   return PDB_OK;
 }
 
+constexpr uint64_t kSpanMaxBytes = 1ull << 45;        // 16383 segments of <= 2 GiB
+constexpr uint64_t kSpanHostThreshold = 8ull << 20;  // scalar Extend: split spans >= 8 MiB
+
+// Scalar Extend over a long host span: H2D, parallel segments + tree combine, 4-byte D2H.
+int host_span(uint32_t init, const uint8_t* data, uint64_t n, uint32_t* out) {
+  if (n > kSpanMaxBytes) return fail(PDB_ERANGE, "span longer than 2^45 bytes");
+  DevState* st;
+  int rc = get_state(&st);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(st->mu);
+  hipError_t e = hipSetDevice(st->device);
+  if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+  const size_t off_scr = align_up(n + 16, 256);
+  const size_t off_out = align_up(off_scr + span_scratch_words(n) * 4, 256);
+  rc = ensure_ws(st, off_out + 256);
+  if (rc) return rc;
+  hipStream_t s = st->stream;
+  uint8_t* ws = st->d_ws;
+  if ((e = hipMemcpyAsync(ws, data, n, hipMemcpyHostToDevice, s)) != hipSuccess)
+    return hip_fail(e, "hipMemcpyAsync(span)");
+  e = launch_span(st->geom, st->d_tables, st->d_pow2, init, ws, n, reinterpret_cast<uint32_t*>(ws + off_scr),
+                  reinterpret_cast<uint32_t*>(ws + off_out), s);
+  if (e != hipSuccess) return hip_fail(e, "launch_span");
+  if ((e = hipMemcpyAsync(out, ws + off_out, 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
+    return hip_fail(e, "hipMemcpyAsync(out)");
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+  return PDB_OK;
+}
+
 int host_sst(uint8_t* buf, uint64_t buf_len, const pdb_block_handle* h, uint64_t n, bool seal,
              uint8_t* ok, int64_t* nbad_out) {
   if (n == 0) {
@@ -277,14 +313,15 @@ uint32_t pdb_crc32c_unmask(uint32_t m) { return pdb_unmask(m); }
 
 uint32_t pdb_crc32c_extend(uint32_t init_crc, const void* data, size_t n) {
   if (n == 0) return init_crc;  // Extend over nothing is the identity (util/crc32c.cc:25-32)
-  if (n > 0xFFFFFFFFull) {
-    fprintf(stderr, "pdb_crc32c_extend: span >= 4 GiB is not supported\n");
-    abort();
-  }
-  pdb_blk b{0, static_cast<uint32_t>(n), init_crc};
   uint32_t out = 0;
-  int rc = host_desc(static_cast<const uint8_t*>(data), n, &b, 1, PDB_CRC_USE_INIT, kModeOut, nullptr,
-                     &out, nullptr, nullptr);
+  int rc;
+  if (n >= kSpanHostThreshold) {  // long span: split across waves, combined on the device
+    rc = host_span(init_crc, static_cast<const uint8_t*>(data), n, &out);
+  } else {
+    pdb_blk b{0, static_cast<uint32_t>(n), init_crc};
+    rc = host_desc(static_cast<const uint8_t*>(data), n, &b, 1, PDB_CRC_USE_INIT, kModeOut, nullptr, &out,
+                   nullptr, nullptr);
+  }
   if (rc) {
     fprintf(stderr, "pdb_crc32c_extend: device CRC failed (%d): %s\n", rc, g_err.c_str());
     abort();
@@ -293,6 +330,22 @@ uint32_t pdb_crc32c_extend(uint32_t init_crc, const void* data, size_t n) {
 }
 
 uint32_t pdb_crc32c_value(const void* data, size_t n) { return pdb_crc32c_extend(0, data, n); }
+
+uint64_t pdb_crc32c_extend_scratch_words(uint64_t n) { return span_scratch_words(n); }
+
+int pdb_crc32c_extend_device(uint32_t init_crc, const void* d_data, uint64_t n, uint32_t* d_scratch,
+                             uint64_t scratch_words, uint32_t* d_out, void* stream) {
+  if (!d_out || (n && !d_data)) return fail(PDB_EINVAL, "null argument");
+  if (n > kSpanMaxBytes) return fail(PDB_ERANGE, "span longer than 2^45 bytes");
+  if (!d_scratch || scratch_words < span_scratch_words(n))
+    return fail(PDB_EINVAL, "scratch smaller than pdb_crc32c_extend_scratch_words(n)");
+  DevState* st;
+  int rc = get_state(&st);
+  if (rc) return rc;
+  hipError_t e = launch_span(st->geom, st->d_tables, st->d_pow2, init_crc, static_cast<const uint8_t*>(d_data),
+                             n, d_scratch, d_out, pick_stream(st, stream));
+  return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_span");
+}
 
 int pdb_crc32c_batch_device_fixed(const void* d_base, uint64_t stride, uint32_t len, uint64_t nblk,
                                   uint32_t flags, uint32_t init, uint32_t* d_out, void* stream) {

@@ -12,6 +12,7 @@ namespace pdb {
 // crc32c_tables.cpp
 void build_byte_table(uint32_t t0[256]);
 void build_device_tables(uint32_t* out);  // PDB_TABLE_WORDS
+void build_pow2_tables(uint32_t* out);    // PDB_POW2_WORDS
 uint32_t host_shift(uint32_t c, uint64_t nbytes);
 
 // Kernel launch modes for the descriptor kernel.
@@ -38,6 +39,14 @@ hipError_t launch_desc(const LaunchGeom& g, const uint32_t* d_tables, const uint
 hipError_t launch_sst(const LaunchGeom& g, const uint32_t* d_tables, uint8_t* buf, uint64_t buf_len,
                       const pdb_block_handle* h, uint64_t n, bool seal, uint8_t* ok, uint32_t* nbad,
                       hipStream_t s);
+// Long span: raw CRCs of `nseg` segments of 2^seg_log2 bytes (+ the tail) in parallel, then a
+// one-workgroup tree combine with the power-of-two operators.  `scratch` holds
+// span_scratch_words(n) u32.  *out = Extend(init, data[0..n)).
+uint64_t span_scratch_words(uint64_t n);
+hipError_t launch_span(const LaunchGeom& g, const uint32_t* d_tables, const uint32_t* d_pow2,
+                       uint32_t init, const uint8_t* data, uint64_t n, uint32_t* scratch, uint32_t* out,
+                       hipStream_t s);
+
 // crc32c_variants.hip -- A/B variants (pdb_diag_set_variant) and calibration kernels
 hipError_t launch_fixed_variant(int v, const LaunchGeom& g, const uint32_t* d_tables, const uint8_t* base,
                                 uint64_t stride, uint32_t len, uint64_t nblk, uint32_t flags, uint32_t init,

@@ -54,9 +54,80 @@ __global__ __launch_bounds__(256) void fill_splitmix_kernel(uint8_t* __restrict_
   }
 }
 
+// ---- long spans: parallel segments + one-workgroup tree combine ------------------------------
+// A span of n bytes = a head leaf (n mod S bytes, hashed from the Extend seed) followed by nf
+// full segments of S = 2^seg_log2 bytes (hashed from state 0 by the batch kernels, one wave
+// each).  The nf + 1 raw leaf states are left-padded with zero leaves to M = 2^m (zero leaves are
+// free: R(0^k || X) = R(X) from state 0) and folded by a log2(M)-level tree whose level-k
+// operator is "shift S * 2^k" (staged in LDS from the power-of-two catalog); the root is the raw
+// state of the whole span, so Extend = ~root.  Leaf i's raw state arrives complemented (the
+// batch kernels emit ~state), hence the ~ when loading.
+struct SpanGeom {
+  uint32_t seg_log2, m_log2;
+  uint64_t nf, head;
+};
+
+__host__ __device__ inline SpanGeom span_geom(uint64_t n) {
+  SpanGeom g;
+  g.seg_log2 = PDB_SPAN_MIN_SEG_LOG2;
+  while ((n >> g.seg_log2) + 1 > (1ull << PDB_SPAN_MAX_SEGS_LOG2)) ++g.seg_log2;
+  g.nf = n >> g.seg_log2;
+  g.head = n & ((1ull << g.seg_log2) - 1);
+  g.m_log2 = 0;
+  while ((1ull << g.m_log2) < g.nf + 1) ++g.m_log2;
+  return g;
+}
+
+__global__ __launch_bounds__(1024) void span_combine_kernel(const uint32_t* __restrict__ pow2,
+                                                            const uint32_t* __restrict__ leaves,
+                                                            uint32_t seg_log2, uint32_t m_log2,
+                                                            uint64_t nleaves, uint32_t* __restrict__ out) {
+  __shared__ uint32_t sw[1u << PDB_SPAN_MAX_SEGS_LOG2];
+  __shared__ uint32_t ops[PDB_SPAN_MAX_SEGS_LOG2][1024];
+  const uint32_t M = 1u << m_log2;
+  for (uint32_t i = threadIdx.x; i < m_log2 * 1024u; i += blockDim.x)
+    ops[i >> 10][i & 1023u] = pow2[(seg_log2 + (i >> 10)) * 1024u + (i & 1023u)];
+  const uint32_t pad = M - static_cast<uint32_t>(nleaves);
+  for (uint32_t i = threadIdx.x; i < M; i += blockDim.x) sw[i] = i < pad ? 0u : ~leaves[i - pad];
+  __syncthreads();
+  for (uint32_t k = 0; k < m_log2; ++k) {
+    const uint32_t half = 1u << k, pairs = M >> (k + 1);
+    for (uint32_t j = threadIdx.x; j < pairs; j += blockDim.x) {
+      const uint32_t i = j << (k + 1);
+      const uint32_t c = sw[i];
+      const uint32_t* op = ops[k];
+      sw[i] = op[c & 0xffu] ^ op[256u + ((c >> 8) & 0xffu)] ^ op[512u + ((c >> 16) & 0xffu)] ^
+              op[768u + (c >> 24)] ^ sw[i + half];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = ~sw[0];
+}
+
 }  // namespace
 
 int g_fast_variant = 0;  // diagnostics: pdb_diag_set_variant()
+
+uint64_t span_scratch_words(uint64_t n) { return span_geom(n).nf + 1; }
+
+hipError_t launch_span(const LaunchGeom& g, const uint32_t* d_tables, const uint32_t* d_pow2,
+                       uint32_t init, const uint8_t* data, uint64_t n, uint32_t* scratch, uint32_t* out,
+                       hipStream_t s) {
+  const SpanGeom sg = span_geom(n);
+  // head leaf from the Extend seed (n mod S bytes, possibly empty), then the full segments
+  hipError_t e = launch_fixed(g, d_tables, data, 0, static_cast<uint32_t>(sg.head), 1, PDB_CRC_USE_INIT,
+                              init, scratch, s);
+  if (e != hipSuccess) return e;
+  if (sg.nf) {
+    const uint64_t S = 1ull << sg.seg_log2;
+    e = launch_fixed(g, d_tables, data + sg.head, S, static_cast<uint32_t>(S), sg.nf, PDB_CRC_USE_INIT,
+                     0xFFFFFFFFu, scratch + 1, s);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(span_combine_kernel, dim3(1), dim3(1024), 0, s, d_pow2, scratch, sg.seg_log2,
+                     sg.m_log2, sg.nf + 1, out);
+  return hipGetLastError();
+}
 
 hipError_t launch_fixed(const LaunchGeom& g, const uint32_t* d_tables, const uint8_t* base,
                         uint64_t stride, uint32_t len, uint64_t nblk, uint32_t flags, uint32_t init,

@@ -65,5 +65,10 @@ PDB_HD uint32_t pdb_unmask(uint32_t m) {
 #define PDB_CAT_H4032 10   /* 4096 - 64: generic kernel, rounds of 64 x 64 B */
 static const unsigned long long kPdbCatDist[PDB_NCAT] = {16,   32,   64,   128,  256, 512,
                                                            1024, 2048, 1008, 2016, 4032};
+/* Long spans (pdb_crc32c_extend*): 64 power-of-two shift operators in device memory, and the
+ * segment geometry of the parallel split + tree combine. */
+#define PDB_POW2_WORDS (64u * 1024u)
+#define PDB_SPAN_MIN_SEG_LOG2 16      /* segments of >= 64 KiB */
+#define PDB_SPAN_MAX_SEGS_LOG2 14     /* <= 16384 segments: the combine tree fits 64 KiB of LDS */
 /* Device table source: T0..T3 (1024 u32) then the catalog (PDB_NCAT * 1024 u32). */
 #define PDB_TABLE_WORDS (1024u + PDB_NCAT * 1024u)

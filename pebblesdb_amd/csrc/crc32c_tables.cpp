@@ -82,4 +82,18 @@ void build_device_tables(uint32_t* out) {
   }
 }
 
+// 64 operators (PDB_POW2_WORDS u32): op k = shift by 2^k bytes, 4 x 256 entries each, for the
+// long-span combine (any distance = product of the operators of its set bits).
+void build_pow2_tables(uint32_t* out) {
+  uint32_t t0[256];
+  build_byte_table(t0);
+  Gf2Mat m = one_zero_byte(t0);
+  for (int k = 0; k < 64; ++k) {
+    uint32_t* op = out + k * 1024;
+    for (int j = 0; j < 4; ++j)
+      for (uint32_t b = 0; b < 256; ++b) op[j * 256 + b] = mat_vec(m, b << (8 * j));
+    m = mat_mul(m, m);
+  }
+}
+
 }  // namespace pdb

@@ -224,3 +224,37 @@ def test_device_entry_points_capture_into_hip_graph(crc, oracle_lib):
         e1 = oracle_lib.batch(host, crc.make_blocks(np.arange(nblk) * 4096, np.full(nblk, 4096)), nthreads=8)
         e2 = oracle_lib.batch(host, crc.make_blocks(np.arange(nblk) * 4096 + 1, np.full(nblk, 4095)), nthreads=8)
         assert (_u32(out1) == e1).all() and (_u32(out2) == e2).all()
+
+
+@pytest.mark.parametrize("n", [0, 1, 65535, 65536, 65537, 3 * 65536 + 5, (64 << 20) + 13, (1 << 30) + 7])
+def test_long_span_extend_device(crc, oracle_lib, n):
+    """One span split into parallel segments + device tree combine."""
+    d = torch.empty(max(n, 1) + 3, dtype=torch.uint8, device="cuda")
+    crc.fill_splitmix(d, 555 + n)
+    view = d[3 : 3 + n]  # misaligned start
+    init = 0x9E3779B9
+    host = view.cpu().numpy()
+    assert crc.extend_device(init, view, n) == oracle_lib.extend(init, host)
+    assert crc.extend_device(0, view, n) == oracle_lib.value(host)
+
+
+def test_long_span_past_4gib(crc, oracle_lib):
+    """> 2^32 bytes in one Extend: the true CRC32C (the reference narrows the length to uint32,
+    util/crc32c.cc:19-23,589, so it has no defined answer there; the oracle keeps size_t)."""
+    n = (4 << 30) + 4099
+    d = torch.empty(n, dtype=torch.uint8, device="cuda")
+    crc.fill_splitmix(d, 4242)
+    got = crc.extend_device(0x12345678, d, n)
+    host = d.cpu().numpy()
+    del d
+    torch.cuda.empty_cache()
+    assert got == oracle_lib.extend(0x12345678, host)
+
+
+def test_scalar_extend_long_host_span(crc, oracle_lib):
+    """pdb_crc32c_extend on host data >= 8 MiB takes the split path."""
+    import oracle
+
+    for n in ((8 << 20) + 3, (40 << 20) + 1):
+        data = oracle.splitmix_bytes(n, 777 + n)
+        assert crc.extend(0xDEADBEEF, data) == oracle_lib.extend(0xDEADBEEF, data)
