@@ -40,6 +40,13 @@ struct DevState {
   std::mutex mu;  // guards the host-staging workspace below
   uint8_t* d_ws = nullptr;
   size_t ws_cap = 0;
+  // scalar Extend: pinned, device-mapped staging ([256-B result area][bytes]); the kernels read
+  // the bytes across PCIe and write the CRC back into it, so a call is memcpy + launch(es) + sync
+  uint8_t* h_stage = nullptr;
+  uint8_t* d_stage = nullptr;  // device alias of h_stage
+  size_t stage_cap = 0;
+  uint32_t seq = 0;          // scalar-call sentinel sequence
+  bool scalar_poll = true;   // PDB_SCALAR_WAIT=sync: wait on the stream instead (A/B diagnostics)
 };
 
 constexpr int kMaxDev = 64;
@@ -87,6 +94,8 @@ int get_state(DevState** out) {
   if (e != hipSuccess) return hip_fail(e, "hipMalloc(pow2)");
   e = hipMemcpy(s->d_pow2, pow2.data(), pow2.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
   if (e != hipSuccess) return hip_fail(e, "hipMemcpy(pow2)");
+  const char* wait = getenv("PDB_SCALAR_WAIT");
+  s->scalar_poll = !(wait && strcmp(wait, "sync") == 0);
   e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
   if (e != hipSuccess) return hip_fail(e, "hipStreamCreate");
   __atomic_store_n(&g_dev[dev], s.get(), __ATOMIC_RELEASE);
@@ -117,6 +126,31 @@ int ensure_ws(DevState* st, size_t bytes) {
 }
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+constexpr size_t kStageHdr = 256;  // result words ahead of the staged bytes (keeps them 256-B aligned)
+
+int ensure_stage(DevState* st, size_t bytes) {
+  if (bytes <= st->stage_cap) return PDB_OK;
+  if (st->h_stage) {
+    (void)hipStreamSynchronize(st->stream);
+    (void)hipHostFree(st->h_stage);
+    st->h_stage = st->d_stage = nullptr;
+    st->stage_cap = 0;
+  }
+  size_t cap = std::max<size_t>(bytes, 64 << 10);
+  hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&st->h_stage), cap,
+                               hipHostMallocMapped | hipHostMallocCoherent);
+  if (e != hipSuccess) return fail(PDB_ENOMEM, std::string("hipHostMalloc(stage): ") + hipGetErrorString(e));
+  void* dp = nullptr;
+  if ((e = hipHostGetDevicePointer(&dp, st->h_stage, 0)) != hipSuccess) {
+    (void)hipHostFree(st->h_stage);
+    st->h_stage = nullptr;
+    return hip_fail(e, "hipHostGetDevicePointer(stage)");
+  }
+  st->d_stage = static_cast<uint8_t*>(dp);
+  st->stage_cap = cap;
+  return PDB_OK;
+}
 
 // Host batch over descriptors: stage [lo, hi) of the host span, the rebased descriptors and the
 // outputs in one workspace; one H2D span copy, one H2D descriptor copy, kernel, one D2H.
@@ -189,7 +223,55 @@ int host_desc(const uint8_t* base, uint64_t base_len, const pdb_blk* blk, uint64
 }
 
 constexpr uint64_t kSpanMaxBytes = 1ull << 45;        // 16383 segments of <= 2 GiB
-constexpr uint64_t kSpanHostThreshold = 8ull << 20;  // scalar Extend: split spans >= 8 MiB
+constexpr uint64_t kSpanHostThreshold = 8ull << 20;  // scalar Extend: device-copy spans >= 8 MiB
+constexpr uint64_t kScalarOneLeaf = 64ull << 10;     // below: one launch, one wave; above: span split
+
+// Scalar Extend below kSpanHostThreshold (the per-record / per-block call of log_writer.cc:121,
+// table_builder.cc:197-199, format.cc:97): latency-bound, so no DMA copies at all -- the bytes are
+// staged in pinned mapped memory, read by the kernel across PCIe, and the CRC is written back into
+// the same mapping.  < 64 KiB: one launch_fixed of one block; larger: launch_span (parallel 64-KiB
+// segments + tree combine, scratch in the device workspace).
+int host_scalar(uint32_t init, const uint8_t* data, uint64_t n, uint32_t* out) {
+  DevState* st;
+  int rc = get_state(&st);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(st->mu);
+  hipError_t e = hipSetDevice(st->device);
+  if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+  if ((rc = ensure_stage(st, kStageHdr + align_up(n, 256)))) return rc;
+  memcpy(st->h_stage + kStageHdr, data, n);
+  uint32_t* d_res = reinterpret_cast<uint32_t*>(st->d_stage);
+  volatile uint32_t* h_res = reinterpret_cast<volatile uint32_t*>(st->h_stage);
+  hipStream_t s = st->stream;
+  if (n < kScalarOneLeaf) {
+    // The kernel's only host write is the result, after its last read of the staged bytes, so
+    // seeing it change means the call is complete: spin on it instead of waiting for the
+    // end-of-kernel signal.  A CRC equal to the sentinel just falls through to the stream sync.
+    const uint32_t sentinel = st->seq++ * 0x9E3779B9u ^ 0x5A5A5A5Au;
+    *h_res = sentinel;
+    e = launch_fixed(st->geom, st->d_tables, st->d_stage + kStageHdr, 0, static_cast<uint32_t>(n), 1,
+                     PDB_CRC_USE_INIT, init, d_res, s);
+    if (e != hipSuccess) return hip_fail(e, "launch_fixed(scalar)");
+    if (st->scalar_poll) {
+      for (uint32_t spin = 0; spin < (1u << 22); ++spin) {
+        const uint32_t v = *h_res;
+        if (v != sentinel) {
+          *out = v;
+          return PDB_OK;
+        }
+        __builtin_ia32_pause();
+      }
+    }
+  } else {
+    if ((rc = ensure_ws(st, span_scratch_words(n) * 4 + 256))) return rc;
+    e = launch_span(st->geom, st->d_tables, st->d_pow2, init, st->d_stage + kStageHdr, n,
+                    reinterpret_cast<uint32_t*>(st->d_ws), d_res, s);
+    if (e != hipSuccess) return hip_fail(e, "launch_span(scalar)");
+  }
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+  *out = *h_res;
+  return PDB_OK;
+}
 
 // Scalar Extend over a long host span: H2D, parallel segments + tree combine, 4-byte D2H.
 int host_span(uint32_t init, const uint8_t* data, uint64_t n, uint32_t* out) {
@@ -318,9 +400,7 @@ uint32_t pdb_crc32c_extend(uint32_t init_crc, const void* data, size_t n) {
   if (n >= kSpanHostThreshold) {  // long span: split across waves, combined on the device
     rc = host_span(init_crc, static_cast<const uint8_t*>(data), n, &out);
   } else {
-    pdb_blk b{0, static_cast<uint32_t>(n), init_crc};
-    rc = host_desc(static_cast<const uint8_t*>(data), n, &b, 1, PDB_CRC_USE_INIT, kModeOut, nullptr, &out,
-                   nullptr, nullptr);
+    rc = host_scalar(init_crc, static_cast<const uint8_t*>(data), n, &out);
   }
   if (rc) {
     fprintf(stderr, "pdb_crc32c_extend: device CRC failed (%d): %s\n", rc, g_err.c_str());

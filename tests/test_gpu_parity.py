@@ -258,3 +258,20 @@ def test_scalar_extend_long_host_span(crc, oracle_lib):
     for n in ((8 << 20) + 3, (40 << 20) + 1):
         data = oracle.splitmix_bytes(n, 777 + n)
         assert crc.extend(0xDEADBEEF, data) == oracle_lib.extend(0xDEADBEEF, data)
+
+
+@pytest.mark.gpu
+def test_scalar_extend_zero_copy_sizes(crc, oracle_lib):
+    """pdb_crc32c_extend below 8 MiB (pinned mapped staging, no DMA): one-leaf launches below
+    64 KiB (incl. the 4096-B packed kernel), span split above; unaligned source pointers; the
+    staging buffer growing between calls; results identical to the oracle."""
+    import oracle
+
+    sizes = (1, 7, 63, 4095, 4096, 4097, 32768 + 7, 65535, 65536, 65537, (1 << 20) + 3,
+             (8 << 20) - 1, 100, 4096)
+    for i, n in enumerate(sizes):
+        buf = oracle.splitmix_bytes(n + 5, 31 + i)
+        data = buf[i % 5 : i % 5 + n]  # caller pointer at every alignment
+        init = (0x9E3779B9 * (i + 1)) & 0xFFFFFFFF
+        assert crc.extend(init, data) == oracle_lib.extend(init, data), n
+        assert crc.value(data) == oracle_lib.value(data), n
