@@ -28,9 +28,11 @@ _u8p = ctypes.c_void_p
 
 
 def build() -> None:
-    """Compile the C restatement (and the reference shim when the reference is present)."""
+    """Compile the C restatement and, when the reference is present, the reference shim and
+    the reference's db_bench (as-is and GPU-hooked; needs pebblesdb_amd's library built)."""
     subprocess.check_call([os.path.join(HERE, "build_oracle.sh")])
     subprocess.check_call([os.path.join(HERE, "build_ref.sh")])
+    subprocess.check_call([os.path.join(HERE, "build_ref_dbbench.sh")])
 
 
 def _bind(lib, prefix: str) -> None:

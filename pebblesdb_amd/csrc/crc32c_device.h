@@ -160,14 +160,23 @@ __device__ __forceinline__ uint64_t wave_id_uniform() {
 // 1 KiB contiguous (coalesced) at the price of a Horner shift over the (4096/kNP - P)-byte gap
 // between a lane's pieces (LDS slot 6).  Each wave walks blocks b, b+W, ... (W = waves in the
 // grid) with kDepth blocks of loads in flight ahead of the one it hashes.
-template <int kNP>
+// kNT: non-temporal (streaming) policy.  With kNP = 4 every load instruction reads 1 KiB
+// contiguous, and nt loads of that shape read ~12 % faster than any default-policy pattern
+// (`read_pattern4k` variants 18/21 vs 12: 6.96 vs 6.22 TB/s); at a 32-B lane stride (kNP = 2)
+// nt gains nothing.
+template <int kNP, bool kNT = false>
 __device__ __forceinline__ void load4k(u32x4 (&v)[4], const uint8_t* base, uint64_t stride, uint64_t b,
                                        uint32_t lane) {
   constexpr uint32_t P = 64u / kNP, gap = 4096u / kNP, per = 4u / kNP;
   const uint8_t* blk = base + b * stride + lane * P;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
-    v[i] = *reinterpret_cast<const u32x4*>(blk + (i / per) * gap + (i % per) * 16u);
+  for (int i = 0; i < 4; ++i) {
+    const u32x4* q = reinterpret_cast<const u32x4*>(blk + (i / per) * gap + (i % per) * 16u);
+    if constexpr (kNT)
+      v[i] = __builtin_nontemporal_load(q);
+    else
+      v[i] = *q;
+  }
 }
 
 // The lane's 16 dwords are hashed as NCH independent slice-by-4 chains (ILP: half or a quarter
@@ -229,8 +238,28 @@ __device__ __forceinline__ uint32_t tree4_packed(const char* lds, uint32_t u, ui
   return v;
 }
 
+// Lane partial of one 4-KiB block.  kNP = 2: two 32-B pieces (at 32l and 2048+32l) folded with
+// shift 2048 (slot 6), partials 32 B apart.  kNP = 4: four 16-B pieces at 16l + 1024j, four
+// 4-word chains folded as shift2048(shift1024(x0)^x1) ^ (shift1024(x2)^x3) (slots 6, 7), partials
+// 16 B apart.
+template <int kNP = 2>
 __device__ __forceinline__ uint32_t partial4k(const char* lds, const LaneTabs& lt, uint32_t c0,
                                               const u32x4 (&v)[4]) {
+  if constexpr (kNP == 4) {
+    uint32_t x0 = c0 ^ v[0].x, x1 = v[1].x, x2 = v[2].x, x3 = v[3].x;
+    const uint32_t d0[4] = {v[0].x, v[0].y, v[0].z, v[0].w}, d1[4] = {v[1].x, v[1].y, v[1].z, v[1].w};
+    const uint32_t d2[4] = {v[2].x, v[2].y, v[2].z, v[2].w}, d3[4] = {v[3].x, v[3].y, v[3].z, v[3].w};
+#pragma unroll
+    for (int i = 1; i <= 4; ++i) {
+      x0 = step4x(lds, lt, x0, i < 4 ? d0[i] : 0u);
+      x1 = step4x(lds, lt, x1, i < 4 ? d1[i] : 0u);
+      x2 = step4x(lds, lt, x2, i < 4 ? d2[i] : 0u);
+      x3 = step4x(lds, lt, x3, i < 4 ? d3[i] : 0u);
+    }
+    const uint32_t a = shift_op_x(lds, PDB_SLOT_HORNER, x0, x1);
+    const uint32_t b = shift_op_x(lds, PDB_SLOT_HORNER, x2, x3);
+    return shift_op_x(lds, PDB_SLOT_HORNER + 1, a, b);
+  }
   uint32_t xa = c0 ^ v[0].x, xb = v[2].x;
   const uint32_t da[8] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w};
   const uint32_t db[8] = {v[2].x, v[2].y, v[2].z, v[2].w, v[3].x, v[3].y, v[3].z, v[3].w};
@@ -242,18 +271,22 @@ __device__ __forceinline__ uint32_t partial4k(const char* lds, const LaneTabs& l
   return shift_op_x(lds, PDB_SLOT_HORNER, xa, xb);  // shift 2048
 }
 
-template <int kSync>
+template <int kSync, int kNP = 2, bool kNT = false>
 __global__ __launch_bounds__(kThreads) void crc_pack4k_kernel(
     const uint32_t* __restrict__ tabs, const uint8_t* __restrict__ base, uint64_t stride,
     uint64_t nblk, uint32_t flags, uint32_t init, uint32_t* __restrict__ out) {
+  static_assert(kNP == 2 || kNP == 4, "lane pieces: 2 x 32 B or 4 x 16 B");
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
   char* lds = reinterpret_cast<char*>(lds_words);
   const uint32_t u = threadIdx.x & 63u;
   const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWavesPerWg;
   const uint64_t w = wave_id_uniform();
   u32x4 buf[4];
-  load4k<2>(buf, base, stride, w < nblk ? w : nblk - 1, u);
-  stage_tables<PDB_CAT_TREE32, PDB_CAT_S2048>(lds, tabs);
+  load4k<kNP, kNT>(buf, base, stride, w < nblk ? w : nblk - 1, u);
+  if constexpr (kNP == 4)
+    stage_tables<PDB_CAT_TREE16, PDB_CAT_S1024, PDB_CAT_S2048>(lds, tabs);
+  else
+    stage_tables<PDB_CAT_TREE32, PDB_CAT_S2048>(lds, tabs);
   __syncthreads();
   if (kSync == 0 && w >= nblk) return;
   const LaneTabs lt = lane_tabs(u);
@@ -276,8 +309,8 @@ __global__ __launch_bounds__(kThreads) void crc_pack4k_kernel(
       const uint64_t bk = g + r * nw;
       u32x4 cur[4] = {buf[0], buf[1], buf[2], buf[3]};
       const uint64_t bn = bk + nw;
-      if (bn < nblk) load4k<2>(buf, base, stride, bn, u);  // wave-uniform
-      p[r] = bk < nblk ? partial4k(lds, lt, c0, cur) : 0u;
+      if (bn < nblk) load4k<kNP, kNT>(buf, base, stride, bn, u);  // wave-uniform
+      p[r] = bk < nblk ? partial4k<kNP>(lds, lt, c0, cur) : 0u;
     }
     const uint32_t v = tree4_packed(lds, u, p[0], p[1], p[2], p[3]);
     // lane 4j+r of the 64-block window holds block (window + (4j+r)*nw): move lanes 0..3's

@@ -254,7 +254,7 @@ __global__ __launch_bounds__(256) void read_stream_kernel(const u32x4* __restric
 //   kPat 0: lane l reads bytes [64l, 64l+64) of the block (the fast path's pattern)
 //   kPat 1: lane l reads 16 B at 16l + 1024j, j = 0..3 (each instruction 1 KiB contiguous)
 //   kDepth: blocks in flight per wave; kAssign 0: wave-interleaved blocks, 1: contiguous per WG
-template <int kPat, int kDepth, int kAssign, bool kSync = false>
+template <int kPat, int kDepth, int kAssign, bool kSync = false, bool kNT = false>
 __global__ __launch_bounds__(kThreads) void read_pattern4k_kernel(const uint8_t* __restrict__ base,
                                                                   uint64_t nblk,
                                                                   uint32_t* __restrict__ out) {
@@ -287,11 +287,69 @@ __global__ __launch_bounds__(kThreads) void read_pattern4k_kernel(const uint8_t*
           const uint32_t off = kPat == 0 ? lane * 64u + j * 16u
                              : (kPat == 1 ? lane * 16u + j * 1024u
                                           : lane * 32u + (j >> 1) * 2048u + (j & 1) * 16u);
-          x ^= *reinterpret_cast<const u32x4*>(blk + off);
+          if constexpr (kNT)
+            x ^= __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(blk + off));
+          else
+            x ^= *reinterpret_cast<const u32x4*>(blk + off);
         }
       }
     }
     acc ^= x.x ^ x.y ^ x.z ^ x.w;
+  }
+  for (int k = 32; k; k >>= 1) acc ^= __shfl_xor(acc, k, 64);
+  if (lane == 0) atomicXor(out, acc);
+}
+
+// LDS-DMA calibration: each wave streams whole 4-KiB blocks into its own LDS ring with
+// global_load_lds_dwordx4 (4 instructions per block, each 1 KiB contiguous, lane-linear image),
+// kDepth blocks in flight per wave; kAux = cache policy bits (0 default, 2 = nt).  The block is then
+// read back from LDS (ds_read_b128) and folded, so the LDS round trip is paid as a CRC kernel would.
+template <int kAux, int kDepth, int kUnitKiB = 4, int kWaves = kWavesPerWg>
+__global__ __launch_bounds__(kWaves * 64) void read_glds4k_kernel(const uint8_t* __restrict__ base,
+                                                                  uint64_t nblk,
+                                                                  uint32_t* __restrict__ out) {
+  constexpr uint32_t kUnit = kUnitKiB * 1024u;
+  __shared__ __attribute__((aligned(16))) uint8_t ring[kWaves * kDepth * kUnit];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint8_t* my = ring + wv * (kDepth * kUnit);
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWaves;
+  const uint64_t nunit = nblk * (4096u / kUnit);
+  const uint64_t first = static_cast<uint64_t>(blockIdx.x) * kWaves + wv;
+  uint32_t acc = 0;
+  auto issue = [&](uint64_t u, uint32_t slot) {
+    const uint8_t* g = base + u * kUnit + lane * 16u;
+    uint8_t* l = my + slot * kUnit;
+#pragma unroll
+    for (int j = 0; j < kUnitKiB; ++j)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(g + j * 1024),
+                                       reinterpret_cast<__attribute__((address_space(3))) void*>(
+                                           reinterpret_cast<uintptr_t>(l + j * 1024)),
+                                       16, 0, kAux);
+  };
+  uint64_t u = first;
+#pragma unroll
+  for (int k = 0; k < kDepth - 1; ++k)
+    if (u + k * nw < nunit) issue(u + k * nw, k);
+  uint32_t slot = 0;
+  for (; u < nunit; u += nw) {
+    const uint64_t ahead = u + (kDepth - 1) * nw;
+    const uint32_t aslot = (slot + kDepth - 1) % kDepth;
+    if (ahead < nunit) {
+      issue(ahead, aslot);
+      // leave the (kDepth-1) newer units' loads in flight (kDepth 2 only; else drain)
+      if constexpr (kDepth == 2 && kUnitKiB == 4) __builtin_amdgcn_s_waitcnt(0x0F74);       // vmcnt(4)
+      else if constexpr (kDepth == 2 && kUnitKiB == 2) __builtin_amdgcn_s_waitcnt(0x0F72);  // vmcnt(2)
+      else __builtin_amdgcn_s_waitcnt(0x0F70);
+    } else {
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    }
+    const u32x4* l = reinterpret_cast<const u32x4*>(my + slot * kUnit);
+    u32x4 x = l[lane];
+#pragma unroll
+    for (int j = 1; j < kUnitKiB; ++j) x ^= l[lane + 64 * j];
+    acc ^= x.x ^ x.y ^ x.z ^ x.w;
+    slot = (slot + 1) % kDepth;
   }
   for (int k = 32; k; k >>= 1) acc ^= __shfl_xor(acc, k, 64);
   if (lane == 0) atomicXor(out, acc);
@@ -342,6 +400,14 @@ hipError_t launch_fixed_variant(int v, const LaunchGeom& g, const uint32_t* d_ta
     case 9: PDB_K(crc_pack4k_kernel<2>); break;  // lock-step every 2 groups
     case 10: PDB_K(crc_pack4k_kernel<4>); break;
     case 11: PDB_K(crc_pack4k_dyn_kernel); break;  // workgroup-local dynamic groups
+    // coalesced 4 x 16-B lane pieces (each load instruction 1 KiB contiguous), nt loads
+    case 12: PDB_K((crc_pack4k_kernel<1, 4, true>)); break;
+    case 13: PDB_K((crc_pack4k_kernel<0, 4, true>)); break;
+    case 14: PDB_K((crc_pack4k_kernel<1, 2, true>)); break;
+    case 15: PDB_K((crc_pack4k_kernel<0, 4, false>)); break;
+    case 16: PDB_K((crc_pack4k_kernel<2, 4, true>)); break;
+    case 17: PDB_K((crc_pack4k_kernel<4, 4, true>)); break;
+    case 18: PDB_K((crc_pack4k_kernel<8, 4, true>)); break;
     default: PDB_K(crc_pack4k_kernel<1>); break;
   }
 #undef PDB_FAST
@@ -391,6 +457,24 @@ hipError_t launch_read_pattern4k(const LaunchGeom& g, const uint8_t* base, uint6
     case 11: hipLaunchKernelGGL((read_pattern4k_kernel<1, 1, 0, true>), grid, block, 0, s, base, nblk, out); break;
     case 12: hipLaunchKernelGGL((read_pattern4k_kernel<2, 4, 0, true>), grid, block, 0, s, base, nblk, out); break;
     case 13: hipLaunchKernelGGL((read_pattern4k_kernel<1, 4, 0, true>), grid, block, 0, s, base, nblk, out); break;
+    // LDS-DMA (global_load_lds_dwordx4) into a per-wave ring: default / nt policy, depth 1-2
+    case 14: hipLaunchKernelGGL((read_glds4k_kernel<0, 1>), grid, block, 0, s, base, nblk, out); break;
+    case 15: hipLaunchKernelGGL((read_glds4k_kernel<2, 1>), grid, block, 0, s, base, nblk, out); break;
+    case 16: hipLaunchKernelGGL((read_glds4k_kernel<0, 2>), grid, block, 0, s, base, nblk, out); break;
+    case 17: hipLaunchKernelGGL((read_glds4k_kernel<2, 2>), grid, block, 0, s, base, nblk, out); break;
+    // register loads with the nt policy (__builtin_nontemporal_load)
+    case 18: hipLaunchKernelGGL((read_pattern4k_kernel<1, 1, 0, false, true>), grid, block, 0, s, base, nblk, out); break;
+    case 19: hipLaunchKernelGGL((read_pattern4k_kernel<2, 1, 0, false, true>), grid, block, 0, s, base, nblk, out); break;
+    case 20: hipLaunchKernelGGL((read_pattern4k_kernel<2, 1, 0, true, true>), grid, block, 0, s, base, nblk, out); break;
+    case 21: hipLaunchKernelGGL((read_pattern4k_kernel<1, 4, 0, true, true>), grid, block, 0, s, base, nblk, out); break;
+    // LDS-DMA nt with less LDS: 2-KiB units (32 KiB ring per CU), 8 waves x 4 KiB, 2-KiB depth 2
+    case 22: hipLaunchKernelGGL((read_glds4k_kernel<2, 1, 2>), grid, block, 0, s, base, nblk, out); break;
+    case 23: hipLaunchKernelGGL((read_glds4k_kernel<2, 1, 4, 8>), grid, dim3(512), 0, s, base, nblk, out); break;
+    case 24: hipLaunchKernelGGL((read_glds4k_kernel<2, 2, 2>), grid, block, 0, s, base, nblk, out); break;
+    case 25: hipLaunchKernelGGL((read_glds4k_kernel<2, 1, 1>), grid, block, 0, s, base, nblk, out); break;
+    // nt register loads, coalesced: depth 2 / sync period per 4 blocks
+    case 26: hipLaunchKernelGGL((read_pattern4k_kernel<1, 2, 0, false, true>), grid, block, 0, s, base, nblk, out); break;
+    case 27: hipLaunchKernelGGL((read_pattern4k_kernel<1, 1, 1, false, true>), grid, block, 0, s, base, nblk, out); break;
     default: PDB_RP(0, 1, 0); break;
   }
 #undef PDB_RP
