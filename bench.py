@@ -35,7 +35,9 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    # 40: the first ~20-30 launches of a cold GPU run slower (clock / power settling; see
+    # DESIGN.md §6), so the default warmup covers them
+    ap.add_argument("--warmup", type=int, default=40)
     ap.add_argument("--workload", default="c2", choices=["c2", "c3", "sstable"])
     ap.add_argument("--nblk", type=int, default=1 << 20, help="blocks per GPU (c2/sstable)")
     ap.add_argument("--c3-bytes", type=int, default=16 << 30, help="bytes per GPU for c3 (Zipf)")
@@ -239,7 +241,9 @@ def main():
 
 def diag(crc32c, torch, dev, data, stream):
     """Achievable read bandwidth on this box: a coalesced 16-B/lane stream and the exact load
-    pattern of the 4-KiB fast path with no CRC work."""
+    pattern of the 4-KiB fast path with no CRC work (read_pattern4k variant 21: 1-KiB-contiguous
+    nt load instructions, 4 blocks per wave between workgroup barriers -- also the FETCH_SIZE
+    calibration kernel of tools/pmc_traffic.py)."""
     from pebblesdb_amd._native import check, lib
 
     nbytes = data.numel()
@@ -247,7 +251,7 @@ def diag(crc32c, torch, dev, data, stream):
     res = {}
     for name, fn in (
         ("read_stream", lambda: check(lib().pdb_diag_read_stream(data.data_ptr(), nbytes, o.data_ptr(), stream.cuda_stream))),
-        ("read_pattern4k", lambda: check(lib().pdb_diag_read_pattern4k(data.data_ptr(), nbytes // 4096, 0, o.data_ptr(), stream.cuda_stream))),
+        ("read_pattern4k", lambda: check(lib().pdb_diag_read_pattern4k(data.data_ptr(), nbytes // 4096, 21, o.data_ptr(), stream.cuda_stream))),
     ):
         for _ in range(3):
             fn()

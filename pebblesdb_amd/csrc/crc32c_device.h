@@ -271,18 +271,21 @@ __device__ __forceinline__ uint32_t partial4k(const char* lds, const LaneTabs& l
   return shift_op_x(lds, PDB_SLOT_HORNER, xa, xb);  // shift 2048
 }
 
-template <int kSync, int kNP = 2, bool kNT = false>
-__global__ __launch_bounds__(kThreads) void crc_pack4k_kernel(
+// kPair: the wave hashes blocks two at a time (8 independent chains, next pair's 8 KiB in flight)
+// -- the ILP that lets 8 waves per CU (kWaves = 8, the nt loads' best shape) hide LDS latency.
+template <int kSync, int kNP = 2, bool kNT = false, int kWaves = kWavesPerWg, bool kPair = false>
+__global__ __launch_bounds__(kWaves * 64) void crc_pack4k_kernel(
     const uint32_t* __restrict__ tabs, const uint8_t* __restrict__ base, uint64_t stride,
     uint64_t nblk, uint32_t flags, uint32_t init, uint32_t* __restrict__ out) {
   static_assert(kNP == 2 || kNP == 4, "lane pieces: 2 x 32 B or 4 x 16 B");
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
   char* lds = reinterpret_cast<char*>(lds_words);
   const uint32_t u = threadIdx.x & 63u;
-  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWavesPerWg;
-  const uint64_t w = wave_id_uniform();
-  u32x4 buf[4];
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWaves;
+  const uint64_t w = static_cast<uint64_t>(blockIdx.x) * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  u32x4 buf[4], buf2[4];
   load4k<kNP, kNT>(buf, base, stride, w < nblk ? w : nblk - 1, u);
+  if constexpr (kPair) load4k<kNP, kNT>(buf2, base, stride, w + nw < nblk ? w + nw : nblk - 1, u);
   if constexpr (kNP == 4)
     stage_tables<PDB_CAT_TREE16, PDB_CAT_S1024, PDB_CAT_S2048>(lds, tabs);
   else
@@ -295,7 +298,7 @@ __global__ __launch_bounds__(kThreads) void crc_pack4k_kernel(
   uint32_t res = 0, it = 0;
   // kSync: the workgroup's 16 waves (16 consecutive blocks) stay in lock step, one barrier per
   // 4-block group, so their outstanding loads cover one compact 64-KiB span at a time.
-  const uint64_t wg_first = static_cast<uint64_t>(blockIdx.x) * kWavesPerWg;
+  const uint64_t wg_first = static_cast<uint64_t>(blockIdx.x) * kWaves;
   if (kSync > 0 && wg_first >= nblk) return;
   uint32_t grp = 0;
   uint64_t win0 = w;
@@ -304,13 +307,27 @@ __global__ __launch_bounds__(kThreads) void crc_pack4k_kernel(
       if ((grp++ % kSync) == 0) __syncthreads();
     }
     uint32_t p[4];
+    if constexpr (kPair) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const uint64_t bk = g + r * nw;
-      u32x4 cur[4] = {buf[0], buf[1], buf[2], buf[3]};
-      const uint64_t bn = bk + nw;
-      if (bn < nblk) load4k<kNP, kNT>(buf, base, stride, bn, u);  // wave-uniform
-      p[r] = bk < nblk ? partial4k<kNP>(lds, lt, c0, cur) : 0u;
+      for (int r = 0; r < 4; r += 2) {
+        const uint64_t bk = g + r * nw;
+        u32x4 cur[4] = {buf[0], buf[1], buf[2], buf[3]};
+        u32x4 cur2[4] = {buf2[0], buf2[1], buf2[2], buf2[3]};
+        const uint64_t bn = bk + 2 * nw;
+        if (bn < nblk) load4k<kNP, kNT>(buf, base, stride, bn, u);  // wave-uniform
+        if (bn + nw < nblk) load4k<kNP, kNT>(buf2, base, stride, bn + nw, u);
+        p[r] = bk < nblk ? partial4k<kNP>(lds, lt, c0, cur) : 0u;
+        p[r + 1] = bk + nw < nblk ? partial4k<kNP>(lds, lt, c0, cur2) : 0u;
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const uint64_t bk = g + r * nw;
+        u32x4 cur[4] = {buf[0], buf[1], buf[2], buf[3]};
+        const uint64_t bn = bk + nw;
+        if (bn < nblk) load4k<kNP, kNT>(buf, base, stride, bn, u);  // wave-uniform
+        p[r] = bk < nblk ? partial4k<kNP>(lds, lt, c0, cur) : 0u;
+      }
     }
     const uint32_t v = tree4_packed(lds, u, p[0], p[1], p[2], p[3]);
     // lane 4j+r of the 64-block window holds block (window + (4j+r)*nw): move lanes 0..3's
@@ -571,6 +588,178 @@ __global__ __launch_bounds__(kThreads) void crc_stream_kernel(const uint32_t* __
         active = false;
         if constexpr (kSync == 0) break;
       }
+    }
+  }
+}
+
+// ---- coalesced stream kernel: 16-B lane pieces, every load instruction 1 KiB contiguous ------
+// Same scheduling as crc_stream_kernel (one wave per block, items = 4-KiB rounds prefetched one
+// ahead, workgroup-local dynamic blocks), with the load shape the nt calibration favours:
+//   block of n bytes = head (t = n % 16 bytes) + K = n / 16 pieces of 16 B at q0 = p + t + 16c;
+//   round r holds pieces c = 256r + 64j + u (j = 0..3) -> lane u, chain j, so load instruction j
+//   of a round reads 1 KiB contiguous.  A lane's 4 chains (4 words each) fold as
+//   a = x0, a = shift1024(a) ^ xj (slot 7); rounds chain with start = shift1008(acc) (slot 6)
+//   injected into chain 0; rotation by K % 64 and the 6-level tree with slots 0..5 = 16 << k.
+// Misaligned q0 (s = q0 & 3): each lane loads the 4-B aligned 16 B at q0 + 16c - s and takes
+// the 17th..20th byte -- the next lane's first dword -- by DPP wave_shl:1 (lane 63: lane 0 of
+// the next chain by readlane); only the lane ending a round's last chain or the block's last
+// piece loads that dword itself.
+template <bool kNT>
+__device__ __forceinline__ u32x4 ldq(const uint8_t* q) {
+  const u32x4a4* v = reinterpret_cast<const u32x4a4*>(q);
+  if constexpr (kNT)
+    return __builtin_nontemporal_load(v);
+  else
+    return *v;
+}
+
+__device__ __forceinline__ uint32_t chain16(const char* lds, const LaneTabs& lt, uint32_t start,
+                                            const u32x4& e, uint32_t nx, uint32_t s) {
+  uint32_t w0 = e.x, w1 = e.y, w2 = e.z, w3 = e.w;
+  if (s) {
+    w0 = __builtin_amdgcn_alignbyte(e.y, e.x, s);
+    w1 = __builtin_amdgcn_alignbyte(e.z, e.y, s);
+    w2 = __builtin_amdgcn_alignbyte(e.w, e.z, s);
+    w3 = __builtin_amdgcn_alignbyte(nx, e.w, s);
+  }
+  uint32_t x = start ^ w0;
+  x = step4x(lds, lt, x, w1);
+  x = step4x(lds, lt, x, w2);
+  x = step4x(lds, lt, x, w3);
+  return step4x(lds, lt, x, 0u);
+}
+
+template <class Src, class Sink, bool kDyn, bool kNT>
+__global__ __launch_bounds__(kThreads) void crc_stream16_kernel(const uint32_t* __restrict__ tabs,
+                                                                 Src src, uint64_t nblk, Sink sink) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
+  char* lds = reinterpret_cast<char*>(lds_words);
+  stage_tables<PDB_CAT_TREE16, PDB_CAT_H1008, PDB_CAT_S1024, kDyn>(lds, tabs);
+  uint32_t* ctr = reinterpret_cast<uint32_t*>(lds + PDB_MAIN_BYTES + 5 * 4096u);
+  const uint64_t g_lo = nblk * blockIdx.x / gridDim.x, g_hi = nblk * (blockIdx.x + 1) / gridDim.x;
+  if (kDyn && threadIdx.x == 0) *ctr = kWavesPerWg;  // next block, relative to g_lo
+  __syncthreads();
+  const uint32_t u = threadIdx.x & 63u;
+  const LaneTabs lt = lane_tabs(u);
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWavesPerWg;
+  auto next_block = [&](uint64_t cur) -> uint64_t {
+    if constexpr (kDyn) {
+      uint32_t r = 0;
+      if (u == 0) r = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      return g_lo + __builtin_amdgcn_readfirstlane(r);
+    } else {
+      return cur + nw;
+    }
+  };
+  const uint64_t nend = kDyn ? g_hi : nblk;
+  uint64_t i = kDyn ? g_lo + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : wave_id_uniform();
+  if (i >= nend) return;
+
+  // the item being loaded: block d, round k
+  BlkDesc d{};
+  uint32_t k = 0;
+  u32x4 ne[4] = {};
+  uint32_t nxt = 0, nhw = 0, nhb = 0;
+  auto issue = [&](const BlkDesc& bd, uint32_t kk) {
+    const uint32_t t = bd.n & 15u, K = bd.n >> 4;
+    const uint8_t* q0 = bd.p + t;
+    const uint32_t s = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(q0) & 3u);
+    const uint8_t* qa = q0 - s;
+    const uint32_t c0 = kk << 8;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t c = c0 + 64u * j + u;
+      if (c < K) ne[j] = ldq<kNT>(qa + 16ull * c);
+    }
+    if (s && K) {
+      // the dword after a piece whose right neighbour is not in this round's registers
+      const uint32_t cl = K - 1;
+      uint32_t cx = 0xFFFFFFFFu;
+      if (u == 63u && c0 + 255u < K) cx = c0 + 255u;
+      if ((cl >> 8) == kk && (cl & 63u) == u) cx = cl;
+      if (cx != 0xFFFFFFFFu) nxt = *reinterpret_cast<const uint32_t*>(qa + 16ull * (cx + 1u));
+    }
+    if (kk == 0) {
+      const uint32_t lead = t & 3u, nh = t >> 2;
+      if (u >= 1 && u <= nh) nhw = ld32u(bd.p + lead + 4u * (u - 1));
+      if (u == 0 && lead) {
+        uint32_t v = bd.p[0];
+        if (lead > 1) v |= static_cast<uint32_t>(bd.p[1]) << 8;
+        if (lead > 2) v |= static_cast<uint32_t>(bd.p[2]) << 16;
+        nhb = v;
+      }
+    }
+  };
+  d = src.get(i);
+  issue(d, 0);
+  uint32_t acc = 0;
+  for (;;) {
+    const u32x4 e0 = ne[0], e1 = ne[1], e2 = ne[2], e3 = ne[3];
+    const uint32_t cx = nxt, chw = nhw, chb = nhb;
+    const BlkDesc cd = d;
+    const uint32_t ck = k;
+    const uint32_t K = cd.n >> 4;
+    const uint32_t R = K ? (K + 255u) >> 8 : 1u;
+    const bool last_round = ck + 1 >= R;
+    const uint64_t ni = last_round ? next_block(i) : i;
+    const bool have_next = ni < nend;
+    if (last_round && have_next) d = src.get(ni);
+    k = last_round ? 0 : ck + 1;
+    if (have_next) issue(d, k);
+
+    if (ck == 0) {  // head: every lane hashes the same (broadcast) head bytes from the seed
+      const uint32_t t = cd.n & 15u, lead = t & 3u, nh = t >> 2;
+      uint32_t h = cd.init_raw;
+      const uint32_t lb = __builtin_amdgcn_readfirstlane(chb);
+      for (uint32_t j = 0; j < lead; ++j) h = step1(lds, lt, h, (lb >> (8 * j)) & 0xffu);
+      for (uint32_t j = 0; j < nh; ++j) h = step4(lds, lt, h, __builtin_amdgcn_readlane(chw, j + 1));
+      acc = (u == 0) ? h : 0u;
+    }
+    const uint32_t c0 = ck << 8;
+    const uint32_t rem = K - c0;  // pieces left from this round on (>= 1 unless K == 0)
+    const uint32_t J = rem >= 256u ? 4u : (rem > u ? ((rem - u - 1u) >> 6) + 1u : 0u);
+    // neighbour dwords for misaligned pieces, computed with every lane active (DPP sources)
+    const uint32_t s = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(cd.p + (cd.n & 15u)) & 3u);
+    uint32_t n0 = 0, n1 = 0, n2 = 0, n3 = 0;
+    if (s) {  // uniform branch
+      // lane u+1's first dword (wave_shl:1); lane 63 keeps `old` = lane 0 of the next chain, or
+      // for chain 3 the dword it loaded itself
+      n0 = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(e1.x, 0), e0.x, 0x130, 0xF, 0xF, false);
+      n1 = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(e2.x, 0), e1.x, 0x130, 0xF, 0xF, false);
+      n2 = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(e3.x, 0), e2.x, 0x130, 0xF, 0xF, false);
+      n3 = __builtin_amdgcn_update_dpp(cx, e3.x, 0x130, 0xF, 0xF, false);
+      // the block's last piece takes the dword its lane loaded itself
+      const uint32_t cl = K - 1u;
+      if (K && (cl >> 8) == ck && (cl & 63u) == u) {
+        const uint32_t jl = (cl >> 6) & 3u;
+        n0 = jl == 0 ? cx : n0;
+        n1 = jl == 1 ? cx : n1;
+        n2 = jl == 2 ? cx : n2;
+        n3 = jl == 3 ? cx : n3;
+      }
+    }
+    if (J) {
+      const uint32_t start = ck ? shift_op(lds, PDB_SLOT_HORNER, acc) : acc;
+      const uint32_t x0 = chain16(lds, lt, start, e0, n0, s);
+      const uint32_t x1 = chain16(lds, lt, 0u, e1, n1, s);
+      const uint32_t x2 = chain16(lds, lt, 0u, e2, n2, s);
+      const uint32_t x3 = chain16(lds, lt, 0u, e3, n3, s);
+      uint32_t a = x0;
+      if (J > 1) a = shift_op_x(lds, 7, a, x1);
+      if (J > 2) a = shift_op_x(lds, 7, a, x2);
+      if (J > 3) a = shift_op_x(lds, 7, a, x3);
+      acc = a;
+    }
+    if (last_round) {
+      uint32_t raw = acc;
+      if (K) {
+        const uint32_t q = K & 63u;
+        if (q) acc = __shfl(acc, (u + q) & 63u, 64);
+        raw = wave_tree_dpp<kDyn>(lds, u, acc);
+      }
+      if (u == 0) sink.put(i, raw, cd);
+      i = ni;
+      if (!have_next) break;
     }
   }
 }

@@ -139,9 +139,11 @@ hipError_t launch_fixed(const LaunchGeom& g, const uint32_t* d_tables, const uin
   const bool fast = len == 4096u && (reinterpret_cast<uintptr_t>(base) & 15u) == 0 &&
                     (stride & 15u) == 0;
   if (fast) {
-    // 4 blocks per wave-iteration, one packed tree, workgroup lock-step per 4-block group
-    hipLaunchKernelGGL(crc_pack4k_kernel<1>, grid, block, 0, s, d_tables, base, stride, nblk, flags, init,
-                       out);
+    // 4 blocks per wave-iteration, one packed tree, workgroup lock-step per 4-block group; lane
+    // pieces 4 x 16 B so every load instruction reads 1 KiB contiguous, with the nt policy
+    // (A/B: profiles/r01_ab_pack4k_nt*.json, +7-10 % over 2 x 32-B pieces with default loads)
+    hipLaunchKernelGGL((crc_pack4k_kernel<1, 4, true>), grid, block, 0, s, d_tables, base, stride, nblk, flags,
+                       init, out);
   } else {
     // any length / alignment: stream kernel with workgroup-local dynamic blocks
     const FixedSrc src{base, stride, len, (flags & PDB_CRC_USE_INIT) ? ~init : 0xFFFFFFFFu};

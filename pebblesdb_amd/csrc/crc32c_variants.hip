@@ -254,26 +254,26 @@ __global__ __launch_bounds__(256) void read_stream_kernel(const u32x4* __restric
 //   kPat 0: lane l reads bytes [64l, 64l+64) of the block (the fast path's pattern)
 //   kPat 1: lane l reads 16 B at 16l + 1024j, j = 0..3 (each instruction 1 KiB contiguous)
 //   kDepth: blocks in flight per wave; kAssign 0: wave-interleaved blocks, 1: contiguous per WG
-template <int kPat, int kDepth, int kAssign, bool kSync = false, bool kNT = false>
-__global__ __launch_bounds__(kThreads) void read_pattern4k_kernel(const uint8_t* __restrict__ base,
-                                                                  uint64_t nblk,
-                                                                  uint32_t* __restrict__ out) {
+template <int kPat, int kDepth, int kAssign, bool kSync = false, bool kNT = false, int kWaves = kWavesPerWg>
+__global__ __launch_bounds__(kWaves * 64) void read_pattern4k_kernel(const uint8_t* __restrict__ base,
+                                                                     uint64_t nblk,
+                                                                     uint32_t* __restrict__ out) {
   const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWavesPerWg;
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWaves;
   uint32_t acc = 0;
   uint64_t first, step, last;
   if constexpr (kAssign == 0) {
-    first = wave_id_uniform();
+    first = static_cast<uint64_t>(blockIdx.x) * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     step = nw;
     last = nblk;
   } else {
     const uint64_t per = (nblk + gridDim.x - 1) / gridDim.x;
     const uint64_t lo = blockIdx.x * per;
     first = lo + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    step = kWavesPerWg;
+    step = kWaves;
     last = lo + per < nblk ? lo + per : nblk;
   }
-  const uint64_t wg_first = static_cast<uint64_t>(blockIdx.x) * kWavesPerWg;
+  const uint64_t wg_first = static_cast<uint64_t>(blockIdx.x) * kWaves;
   for (uint64_t b = first, bw = wg_first; (kSync ? bw : b) < last; b += step * kDepth, bw += step * kDepth) {
     if constexpr (kSync) __syncthreads();
     u32x4 x = {0, 0, 0, 0};
@@ -357,6 +357,12 @@ __global__ __launch_bounds__(kWaves * 64) void read_glds4k_kernel(const uint8_t*
 
 }  // namespace
 
+uint32_t grid_forw(const LaunchGeom& g, uint64_t nblk, uint32_t waves) {
+  const uint64_t want = (nblk + waves - 1) / waves;
+  return static_cast<uint32_t>(want < g.grid ? (want ? want : 1) : g.grid);
+}
+uint32_t grid_for8(const LaunchGeom& g, uint64_t nblk) { return grid_forw(g, nblk, 8); }
+
 hipError_t launch_fixed_variant(int v, const LaunchGeom& g, const uint32_t* d_tables, const uint8_t* base,
                                 uint64_t stride, uint32_t len, uint64_t nblk, uint32_t flags, uint32_t init,
                                 uint32_t* out, hipStream_t s) {
@@ -373,6 +379,18 @@ hipError_t launch_fixed_variant(int v, const LaunchGeom& g, const uint32_t* d_ta
       case 9: PDB_STREAM_FIXED(1); break;
       case 10: PDB_STREAM_FIXED(4); break;
       case 11: PDB_STREAM_FIXED(8); break;
+      case 12:
+        hipLaunchKernelGGL((crc_stream16_kernel<FixedSrc, OutSink, true, true>), grid, block, 0, s, d_tables,
+                           src, nblk, OutSink{out, flags});
+        break;
+      case 13:
+        hipLaunchKernelGGL((crc_stream16_kernel<FixedSrc, OutSink, true, false>), grid, block, 0, s, d_tables,
+                           src, nblk, OutSink{out, flags});
+        break;
+      case 14:
+        hipLaunchKernelGGL((crc_stream16_kernel<FixedSrc, OutSink, false, true>), grid, block, 0, s, d_tables,
+                           src, nblk, OutSink{out, flags});
+        break;
       default:
         hipLaunchKernelGGL((crc_stream_kernel<FixedSrc, OutSink, 0, true>), grid, block, 0, s, d_tables, src,
                            nblk, OutSink{out, flags});
@@ -400,15 +418,32 @@ hipError_t launch_fixed_variant(int v, const LaunchGeom& g, const uint32_t* d_ta
     case 9: PDB_K(crc_pack4k_kernel<2>); break;  // lock-step every 2 groups
     case 10: PDB_K(crc_pack4k_kernel<4>); break;
     case 11: PDB_K(crc_pack4k_dyn_kernel); break;  // workgroup-local dynamic groups
-    // coalesced 4 x 16-B lane pieces (each load instruction 1 KiB contiguous), nt loads
-    case 12: PDB_K((crc_pack4k_kernel<1, 4, true>)); break;
+    // coalesced 4 x 16-B lane pieces (each load instruction 1 KiB contiguous), nt loads (13-25;
+    // the shipped default is crc_pack4k_kernel<1, 4, true>)
+    case 12: PDB_K((crc_pack4k_kernel<1>)); break;  // previous default: 2 x 32-B pieces, default policy
     case 13: PDB_K((crc_pack4k_kernel<0, 4, true>)); break;
     case 14: PDB_K((crc_pack4k_kernel<1, 2, true>)); break;
     case 15: PDB_K((crc_pack4k_kernel<0, 4, false>)); break;
     case 16: PDB_K((crc_pack4k_kernel<2, 4, true>)); break;
     case 17: PDB_K((crc_pack4k_kernel<4, 4, true>)); break;
     case 18: PDB_K((crc_pack4k_kernel<8, 4, true>)); break;
-    default: PDB_K(crc_pack4k_kernel<1>); break;
+    // 8 waves per CU (512-thread workgroups)
+    case 19: hipLaunchKernelGGL((crc_pack4k_kernel<1, 4, true, 8>), dim3(grid_for8(g, nblk)), dim3(512), 0, s, d_tables,
+                                base, stride, nblk, flags, init, out); break;
+    case 20: hipLaunchKernelGGL((crc_pack4k_kernel<0, 4, true, 8>), dim3(grid_for8(g, nblk)), dim3(512), 0, s, d_tables,
+                                base, stride, nblk, flags, init, out); break;
+    // blocks in pairs (8 chains per wave): 8 waves / 16 waves, lock-step / free
+    case 21: hipLaunchKernelGGL((crc_pack4k_kernel<1, 4, true, 8, true>), dim3(grid_for8(g, nblk)), dim3(512), 0, s,
+                                d_tables, base, stride, nblk, flags, init, out); break;
+    case 22: hipLaunchKernelGGL((crc_pack4k_kernel<0, 4, true, 8, true>), dim3(grid_for8(g, nblk)), dim3(512), 0, s,
+                                d_tables, base, stride, nblk, flags, init, out); break;
+    case 23: PDB_K((crc_pack4k_kernel<1, 4, true, 16, true>)); break;
+    // 12 waves per CU (768-thread workgroups): 48 KiB in flight
+    case 24: hipLaunchKernelGGL((crc_pack4k_kernel<1, 4, true, 12>), dim3(grid_forw(g, nblk, 12)), dim3(768), 0, s,
+                                d_tables, base, stride, nblk, flags, init, out); break;
+    case 25: hipLaunchKernelGGL((crc_pack4k_kernel<2, 4, true, 12>), dim3(grid_forw(g, nblk, 12)), dim3(768), 0, s,
+                                d_tables, base, stride, nblk, flags, init, out); break;
+    default: PDB_K((crc_pack4k_kernel<1, 4, true>)); break;
   }
 #undef PDB_FAST
 #undef PDB_TEAM
@@ -423,6 +458,15 @@ hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tab
   const DescSrc src{base, blk, flags};
   if (v == 8)  // static strided assignment (free-running)
     hipLaunchKernelGGL((crc_stream_kernel<DescSrc, OutSink, 0, false>), grid, block, 0, s, d_tables, src,
+                       nblk, OutSink{out, flags});
+  else if (v == 12)  // coalesced 16-B pieces, nt loads, dynamic blocks
+    hipLaunchKernelGGL((crc_stream16_kernel<DescSrc, OutSink, true, true>), grid, block, 0, s, d_tables, src,
+                       nblk, OutSink{out, flags});
+  else if (v == 13)  // coalesced 16-B pieces, default-policy loads
+    hipLaunchKernelGGL((crc_stream16_kernel<DescSrc, OutSink, true, false>), grid, block, 0, s, d_tables, src,
+                       nblk, OutSink{out, flags});
+  else if (v == 14)  // coalesced 16-B pieces, nt loads, static strided blocks
+    hipLaunchKernelGGL((crc_stream16_kernel<DescSrc, OutSink, false, true>), grid, block, 0, s, d_tables, src,
                        nblk, OutSink{out, flags});
   else
     hipLaunchKernelGGL((crc_stream_kernel<DescSrc, OutSink, 0, true>), grid, block, 0, s, d_tables, src, nblk,
@@ -475,6 +519,12 @@ hipError_t launch_read_pattern4k(const LaunchGeom& g, const uint8_t* base, uint6
     // nt register loads, coalesced: depth 2 / sync period per 4 blocks
     case 26: hipLaunchKernelGGL((read_pattern4k_kernel<1, 2, 0, false, true>), grid, block, 0, s, base, nblk, out); break;
     case 27: hipLaunchKernelGGL((read_pattern4k_kernel<1, 1, 1, false, true>), grid, block, 0, s, base, nblk, out); break;
+    // 8 waves per CU (512-thread workgroups), nt coalesced: depth 1 / 2 / lock-step
+    case 28: hipLaunchKernelGGL((read_pattern4k_kernel<1, 1, 0, false, true, 8>), grid, dim3(512), 0, s, base, nblk, out); break;
+    case 29: hipLaunchKernelGGL((read_pattern4k_kernel<1, 2, 0, false, true, 8>), grid, dim3(512), 0, s, base, nblk, out); break;
+    case 30: hipLaunchKernelGGL((read_pattern4k_kernel<1, 1, 0, true, true, 8>), grid, dim3(512), 0, s, base, nblk, out); break;
+    case 31: hipLaunchKernelGGL((read_pattern4k_kernel<1, 1, 0, false, true, 12>), grid, dim3(768), 0, s, base, nblk, out); break;
+    case 32: hipLaunchKernelGGL((read_pattern4k_kernel<1, 1, 0, true, true, 12>), grid, dim3(768), 0, s, base, nblk, out); break;
     default: PDB_RP(0, 1, 0); break;
   }
 #undef PDB_RP

@@ -190,7 +190,7 @@ def test_all_fast_variants_bit_exact(crc, oracle_lib):
     exp = oracle_lib.batch(d.cpu().numpy(), crc.make_blocks(np.arange(nblk) * 4096, np.full(nblk, 4096)),
                            nthreads=8)
     try:
-        for v in range(19):
+        for v in range(26):
             lib().pdb_diag_set_variant(v)
             got = _u32(crc.batch_fixed(d, 4096, 4096, nblk))
             assert (got == exp).all(), f"variant {v}"
@@ -275,3 +275,41 @@ def test_scalar_extend_zero_copy_sizes(crc, oracle_lib):
         init = (0x9E3779B9 * (i + 1)) & 0xFFFFFFFF
         assert crc.extend(init, data) == oracle_lib.extend(init, data), n
         assert crc.value(data) == oracle_lib.value(data), n
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", [12, 13, 14])
+def test_stream16_variants_exact(crc, golden, oracle_lib, variant):
+    """Coalesced 16-B-piece stream kernel (A/B variants 12-14 of the descriptor / generic fixed
+    paths): the golden sweep (every alignment x every length 0..300), the golden batches, and
+    unaligned / multi-round fixed strides, all against the reference's vectors and the oracle."""
+    from pebblesdb_amd._native import lib
+
+    try:
+        lib().pdb_diag_set_variant(variant)
+        sw = golden["sweep"]
+        buf = _materialize(sw["input"])
+        offs, lens = np.meshgrid(np.arange(sw["offsets"]), np.arange(sw["max_len"] + 1), indexing="ij")
+        blk = crc.make_blocks(offs.reshape(-1), lens.reshape(-1))
+        got = _u32(crc.batch(torch.from_numpy(buf).cuda(), crc.blocks_to_device(blk)))
+        exp = np.array(sw["crc"], dtype=np.uint64).reshape(-1).astype(np.uint32)
+        bad = np.nonzero(got != exp)[0]
+        assert bad.size == 0, f"{bad.size} sweep mismatches, first (off,len)={divmod(int(bad[0]), 301)}"
+        for b in golden["batches"]:
+            d_base = torch.empty(b["total_bytes"], dtype=torch.uint8, device="cuda")
+            crc.fill_splitmix(d_base, b["seed"])
+            blk = crc.make_blocks(b["off"], b["len"], b["init"] if b["use_init"] else None)
+            got = _u32(crc.batch(d_base, crc.blocks_to_device(blk), use_init=b["use_init"], masked=True))
+            assert (got == np.array(b["masked"], dtype=np.uint32)).all(), b["name"]
+        for stride, length, nblk, shift in ((4101, 4097, 777, 0), (1000, 999, 1000, 1), (65536 + 3, 65536 + 3, 40, 2),
+                                            (4096, 4096, 513, 4), (63, 63, 500, 2), (12345, 12289, 100, 3)):
+            total = shift + (nblk - 1) * stride + length
+            d = torch.empty(total + 16, dtype=torch.uint8, device="cuda")
+            crc.fill_splitmix(d, 7 + stride)
+            view = d[shift : shift + total]
+            got = _u32(crc.batch_fixed(view, stride, length, nblk, init=0xDEADBEEF))
+            blk = crc.make_blocks(np.arange(nblk) * stride, np.full(nblk, length), np.full(nblk, 0xDEADBEEF))
+            exp = oracle_lib.batch(view.cpu().numpy(), blk, flags=2, nthreads=8)
+            assert (got == exp).all(), (stride, length, int(np.nonzero(got != exp)[0][0]))
+    finally:
+        lib().pdb_diag_set_variant(0)

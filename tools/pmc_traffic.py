@@ -32,8 +32,8 @@ def durations(sub):
     d = []
     for r in rows("trace/**/*kernel_trace.csv"):
         if sub in kname(r):
-            d.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)  # ns -> ms
-    return d
+            d.append((int(r["Start_Timestamp"]), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6))
+    return [x for _, x in sorted(d)]  # launch order, ns -> ms
 
 
 def counter(name, sub):
@@ -51,11 +51,16 @@ write = counter("WRITE_SIZE", target)
 cal_fetch = counter("FETCH_SIZE", "read_pattern4k_kernel")
 # known bytes for the calibration kernel: the whole buffer (bench allocs it; read from its log)
 known = None
+steps = None
+bench_avg = None
 try:
     with open(os.path.join(out_dir, "trace.log")) as fh:
         for ln in fh:
             if ln.startswith("{"):
-                known = json.loads(ln)["config"]["bytes_per_gpu"]
+                line = json.loads(ln)
+                known = line["config"]["bytes_per_gpu"]
+                steps = line["steps"]
+                bench_avg = line["roofline"]["kernel_avg_ms"]
 except (OSError, ValueError, KeyError):
     pass
 factor = 2.0
@@ -66,6 +71,10 @@ entry = {
     "launches_traced": len(dur),
     "avg_ms": round(statistics.mean(dur), 4) if dur else None,
     "median_ms": round(statistics.median(dur), 4) if dur else None,
+    # the bench's timed region = the last `steps` launches (warmup launches come first)
+    "timed_launches": steps,
+    "avg_ms_timed_launches": round(statistics.mean(dur[-steps:]), 4) if dur and steps else None,
+    "bench_hip_event_avg_ms": bench_avg,
     "fetch_size_kb_median": statistics.median(fetch) if fetch else None,
     "write_size_kb_median": statistics.median(write) if write else None,
     "fetch_correction_factor": round(factor, 4),
