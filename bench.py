@@ -318,6 +318,13 @@ def cpu_baseline(data, L, stride, nblk, args, d_blk):
             if dt > (6.0 if nt == 1 else 4.0) or reps >= 50:
                 break
         res[nt] = sample_bytes * reps / dt / GIB
+    dbb = None
+    if kind == "reference":  # db_bench's own `crc32c` microbench loop, 1 thread
+        try:
+            mib_s, c = lib.dbbench_crc32c(500 << 20)
+            dbb = {"MiB/s": round(mib_s, 1), "crc": f"0x{c:08x}", "loop": "4096 x 'x', 500 MiB, 1 thread"}
+        except RuntimeError:
+            pass
     cpu_model = ""
     try:
         with open("/proc/cpuinfo") as f:
@@ -334,6 +341,7 @@ def cpu_baseline(data, L, stride, nblk, args, d_blk):
         "kind": kind,
         "sample": f"{ns} blocks ({sample_bytes / GIB:.2f} GiB) of the same workload, repeated ~4-6 s",
         "single_thread_GiB/s": round(res[1], 3),
+        "db_bench_crc32c": dbb,
         "cpu_model": cpu_model,
         "nproc": os.cpu_count(),
     }

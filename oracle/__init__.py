@@ -111,6 +111,18 @@ class Reference(_CrcLib):
 
     def __init__(self, path: str = REF_SO):
         super().__init__(path, "ref")
+        self._dbb = getattr(self.lib, "ref_crc32c_dbbench_loop", None)
+        if self._dbb is not None:
+            self._dbb.restype = ctypes.c_double
+            self._dbb.argtypes = [ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint32)]
+
+    def dbbench_crc32c(self, total: int = 500 << 20) -> tuple[float, int]:
+        """db_bench's `crc32c` loop (db/db_bench.cc:1112-1129) in C: (MiB/s, last crc)."""
+        if self._dbb is None:
+            raise RuntimeError("oracle/_ref/libpdbref.so predates ref_crc32c_dbbench_loop; rebuild")
+        c = ctypes.c_uint32(0)
+        secs = self._dbb(total, ctypes.byref(c))
+        return total / secs / (1 << 20), int(c.value)
 
 
 def reference_available() -> bool:

@@ -11,6 +11,9 @@
 #include <pthread.h>
 #include <stddef.h>
 #include <stdint.h>
+#include <time.h>
+
+#include <string>
 
 #include "util/crc32c.h"
 
@@ -60,5 +63,22 @@ int ref_crc32c_batch(const char* base, const void* blk, size_t nblk, uint32_t fl
   Work(&jobs[0]);
   for (int t = 1; t < nthreads; ++t) pthread_join(th[t], nullptr);
   return 0;
+}
+
+// db_bench's `crc32c` benchmark loop (reference db/db_bench.cc:1112-1129): Value() over the same
+// 4096 x 'x' buffer until `total` bytes; returns seconds, the last CRC in *crc (0xa46ab21f).
+double ref_crc32c_dbbench_loop(uint64_t total, uint32_t* crc) {
+  const std::string data(4096, 'x');
+  uint64_t bytes = 0;
+  uint32_t c = 0;
+  timespec t0, t1;
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  while (bytes < total) {
+    c = leveldb::crc32c::Value(data.data(), data.size());
+    bytes += data.size();
+  }
+  clock_gettime(CLOCK_MONOTONIC, &t1);
+  if (crc) *crc = c;
+  return (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
 }
 }

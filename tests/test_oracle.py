@@ -95,3 +95,11 @@ def test_reference_vs_restatement_random():
         n = int(rng.integers(0, 70000))
         init = int(rng.integers(0, 2**32))
         assert ref.extend(init, buf[off : off + n]) == o.extend(init, buf[off : off + n])
+
+
+@pytest.mark.skipif(not oracle.reference_available(), reason="oracle/_ref not built (reference absent)")
+def test_reference_dbbench_loop_golden():
+    """db_bench's `crc32c` loop (db/db_bench.cc:1112-1129) run on the reference's own code prints
+    crc=0xa46ab21f; bench.py's cpu_baseline reports its MiB/s next to the GPU rate."""
+    mib_s, c = oracle.Reference().dbbench_crc32c(8 << 20)
+    assert c == 0xA46AB21F and mib_s > 0
