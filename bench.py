@@ -224,8 +224,8 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": {"c2": "crc_pack4k_kernel", "sstable": "crc_stream_kernel<FixedSrc,OutSink,0,dyn>",
-                           "c3": "crc_stream_kernel<DescSrc,OutSink,0,dyn>"}[args.workload],
+                "kernel": {"c2": "crc_pack4k_kernel<1,4,nt>", "sstable": "crc_stream_kernel<FixedSrc,OutSink,0,dyn,pack>",
+                           "c3": "crc_stream16_kernel<DescSrc,OutSink,dyn,nt,pack>"}[args.workload],
                 "algorithmic_bytes_per_launch": algo_bytes,
                 "kernel_avg_ms": round(kern_avg_ms, 4),
                 "kernel_min_ms": round(float(np.min(kern_ms)), 4),

@@ -211,6 +211,7 @@ __device__ __forceinline__ uint32_t hash4k(const char* lds, const LaneTabs& lt, 
 __device__ __forceinline__ uint32_t sel(bool c, uint32_t a, uint32_t b) { return c ? a : b; }
 
 // Returns block (lane & 3)'s raw state in lanes 0..3.
+template <bool kL5Twice = false>
 __device__ __forceinline__ uint32_t tree4_packed(const char* lds, uint32_t u, uint32_t p0, uint32_t p1,
                                                  uint32_t p2, uint32_t p3) {
   const bool odd = u & 1u;
@@ -234,7 +235,12 @@ __device__ __forceinline__ uint32_t tree4_packed(const char* lds, uint32_t u, ui
   y = __builtin_amdgcn_ds_swizzle(v, 0x401F);  // lane ^ 16
   if ((u & 28u) == 0) v = shift_op_x(lds, 4, v, y);
   y = __shfl_down(v, 32, 64);
-  if ((u & 60u) == 0) v = shift_op_x(lds, 5, v, y);
+  if ((u & 60u) == 0) {
+    if constexpr (kL5Twice)  // slot 5 left free (LDS scratch): shift 2P = shift P twice
+      v = shift_op_x(lds, 4, shift_op(lds, 4, v), y);
+    else
+      v = shift_op_x(lds, 5, v, y);
+  }
   return v;
 }
 
@@ -473,9 +479,15 @@ __device__ __forceinline__ uint32_t chain_piece(const char* lds, const LaneTabs&
 // range [g*N/G, (g+1)*N/G) and its 16 waves take the next block from an LDS counter (LDS slot 5,
 // freed by folding tree level 5 as two "shift 512"s): the CU's work is balanced and its
 // outstanding loads stay on a compact run of consecutive blocks.
-template <class Src, class Sink, int kSync, bool kDyn = false>
+// kPack (kSync == 0 only): finished blocks are not folded one by one; each block's rotated lane
+// partials are parked (up to 4 per wave, with their index and descriptor) and the 4 blocks are
+// folded by ONE packed tree (tree4_packed: 7 shift operations per 4 blocks instead of 24), then
+// lanes 0..3 hand block r's state to the sink.  A block with no 32-B piece parks its head state
+// in lane 63 (the tree's unshifted position).
+template <class Src, class Sink, int kSync, bool kDyn = false, bool kPack = false>
 __global__ __launch_bounds__(kThreads) void crc_stream_kernel(const uint32_t* __restrict__ tabs,
                                                                Src src, uint64_t nblk, Sink sink) {
+  static_assert(!kPack || kSync == 0, "packed trees need free-running waves");
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
   char* lds = reinterpret_cast<char*>(lds_words);
   stage_tables<PDB_CAT_TREE32, PDB_CAT_H2016, PDB_CAT_S2048, kDyn>(lds, tabs);
@@ -528,6 +540,20 @@ __global__ __launch_bounds__(kThreads) void crc_stream_kernel(const uint32_t* __
     issue(d, 0);
   }
   uint32_t acc = 0;
+  // kPack: parked blocks
+  uint32_t park0 = 0, park1 = 0, park2 = 0, park3 = 0, npark = 0;
+  uint64_t pid0 = 0, pid1 = 0, pid2 = 0, pid3 = 0;
+  BlkDesc pd0{}, pd1{}, pd2{}, pd3{};
+  auto flush = [&]() {
+    const uint32_t v = tree4_packed<kDyn>(lds, u, park0, park1, park2, park3);
+    if (u < npark) {
+      const uint64_t id = u == 0 ? pid0 : (u == 1 ? pid1 : (u == 2 ? pid2 : pid3));
+      const BlkDesc bd = u == 0 ? pd0 : (u == 1 ? pd1 : (u == 2 ? pd2 : pd3));
+      sink.put(id, v, bd);
+    }
+    npark = 0;
+    park0 = park1 = park2 = park3 = 0;
+  };
   // kSync (equal lengths): every wave of the workgroup runs as many items as its first wave
   // (the one with the most blocks), so a plain barrier per item needs no LDS reduction.
   uint64_t items_left = 0, item = 0;
@@ -576,19 +602,40 @@ __global__ __launch_bounds__(kThreads) void crc_stream_kernel(const uint32_t* __
       acc = chain_piece(lds, lt, start, ca_, s);
     }
     if (last_round) {
-      uint32_t raw = acc;
-      if (K) {
-        const uint32_t q = K & 63u;
-        if (q) acc = __shfl(acc, (u + q) & 63u, 64);
-        raw = wave_tree_dpp<kDyn>(lds, u, acc);
+      if constexpr (kPack) {
+        uint32_t part;
+        if (K) {
+          const uint32_t q = K & 63u;
+          part = q ? __shfl(acc, (u + q) & 63u, 64) : acc;
+        } else {
+          part = __builtin_amdgcn_readfirstlane(acc);  // head state (lane 0)
+          part = u == 63u ? part : 0u;
+        }
+        switch (npark) {  // wave-uniform
+          case 0: park0 = part; pid0 = i; pd0 = cd; break;
+          case 1: park1 = part; pid1 = i; pd1 = cd; break;
+          case 2: park2 = part; pid2 = i; pd2 = cd; break;
+          default: park3 = part; pid3 = i; pd3 = cd; break;
+        }
+        if (++npark == 4) flush();
+      } else {
+        uint32_t raw = acc;
+        if (K) {
+          const uint32_t q = K & 63u;
+          if (q) acc = __shfl(acc, (u + q) & 63u, 64);
+          raw = wave_tree_dpp<kDyn>(lds, u, acc);
+        }
+        if (u == 0) sink.put(i, raw, cd);
       }
-      if (u == 0) sink.put(i, raw, cd);
       i = ni;
       if (!have_next) {
         active = false;
         if constexpr (kSync == 0) break;
       }
     }
+  }
+  if constexpr (kPack) {
+    if (npark) flush();
   }
 }
 
@@ -629,7 +676,7 @@ __device__ __forceinline__ uint32_t chain16(const char* lds, const LaneTabs& lt,
   return step4x(lds, lt, x, 0u);
 }
 
-template <class Src, class Sink, bool kDyn, bool kNT>
+template <class Src, class Sink, bool kDyn, bool kNT, bool kPack = false>
 __global__ __launch_bounds__(kThreads) void crc_stream16_kernel(const uint32_t* __restrict__ tabs,
                                                                  Src src, uint64_t nblk, Sink sink) {
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
@@ -693,6 +740,19 @@ __global__ __launch_bounds__(kThreads) void crc_stream16_kernel(const uint32_t* 
   d = src.get(i);
   issue(d, 0);
   uint32_t acc = 0;
+  uint32_t park0 = 0, park1 = 0, park2 = 0, park3 = 0, npark = 0;
+  uint64_t pid0 = 0, pid1 = 0, pid2 = 0, pid3 = 0;
+  BlkDesc pd0{}, pd1{}, pd2{}, pd3{};
+  auto flush = [&]() {
+    const uint32_t v = tree4_packed<kDyn>(lds, u, park0, park1, park2, park3);
+    if (u < npark) {
+      const uint64_t id = u == 0 ? pid0 : (u == 1 ? pid1 : (u == 2 ? pid2 : pid3));
+      const BlkDesc bd = u == 0 ? pd0 : (u == 1 ? pd1 : (u == 2 ? pd2 : pd3));
+      sink.put(id, v, bd);
+    }
+    npark = 0;
+    park0 = park1 = park2 = park3 = 0;
+  };
   for (;;) {
     const u32x4 e0 = ne[0], e1 = ne[1], e2 = ne[2], e3 = ne[3];
     const uint32_t cx = nxt, chw = nhw, chb = nhb;
@@ -751,16 +811,37 @@ __global__ __launch_bounds__(kThreads) void crc_stream16_kernel(const uint32_t* 
       acc = a;
     }
     if (last_round) {
-      uint32_t raw = acc;
-      if (K) {
-        const uint32_t q = K & 63u;
-        if (q) acc = __shfl(acc, (u + q) & 63u, 64);
-        raw = wave_tree_dpp<kDyn>(lds, u, acc);
+      if constexpr (kPack) {
+        uint32_t part;
+        if (K) {
+          const uint32_t q = K & 63u;
+          part = q ? __shfl(acc, (u + q) & 63u, 64) : acc;
+        } else {
+          part = __builtin_amdgcn_readfirstlane(acc);  // head state (lane 0)
+          part = u == 63u ? part : 0u;
+        }
+        switch (npark) {  // wave-uniform
+          case 0: park0 = part; pid0 = i; pd0 = cd; break;
+          case 1: park1 = part; pid1 = i; pd1 = cd; break;
+          case 2: park2 = part; pid2 = i; pd2 = cd; break;
+          default: park3 = part; pid3 = i; pd3 = cd; break;
+        }
+        if (++npark == 4) flush();
+      } else {
+        uint32_t raw = acc;
+        if (K) {
+          const uint32_t q = K & 63u;
+          if (q) acc = __shfl(acc, (u + q) & 63u, 64);
+          raw = wave_tree_dpp<kDyn>(lds, u, acc);
+        }
+        if (u == 0) sink.put(i, raw, cd);
       }
-      if (u == 0) sink.put(i, raw, cd);
       i = ni;
       if (!have_next) break;
     }
+  }
+  if constexpr (kPack) {
+    if (npark) flush();
   }
 }
 

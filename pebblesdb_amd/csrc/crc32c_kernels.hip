@@ -145,10 +145,18 @@ hipError_t launch_fixed(const LaunchGeom& g, const uint32_t* d_tables, const uin
     hipLaunchKernelGGL((crc_pack4k_kernel<1, 4, true>), grid, block, 0, s, d_tables, base, stride, nblk, flags,
                        init, out);
   } else {
-    // any length / alignment: stream kernel with workgroup-local dynamic blocks
+    // any length / alignment: stream kernels with workgroup-local dynamic blocks and packed
+    // 4-block trees.  4-B-aligned pieces: 16-B lane pieces with nt loads; otherwise 32-B pieces
+    // (per-block misalignment makes the 16-B kernel's neighbour-dword path cost more than nt
+    // gains: sstable layout 6.1 vs 5.8 TB/s, profiles/r01_ab_gen_pack.json)
     const FixedSrc src{base, stride, len, (flags & PDB_CRC_USE_INIT) ? ~init : 0xFFFFFFFFu};
-    hipLaunchKernelGGL((crc_stream_kernel<FixedSrc, OutSink, 0, true>), grid, block, 0, s, d_tables, src,
-                       nblk, OutSink{out, flags});
+    const bool aligned4 = ((reinterpret_cast<uintptr_t>(base) + (len & 15u)) & 3u) == 0 && (stride & 3u) == 0;
+    if (aligned4)
+      hipLaunchKernelGGL((crc_stream16_kernel<FixedSrc, OutSink, true, true, true>), grid, block, 0, s, d_tables,
+                         src, nblk, OutSink{out, flags});
+    else
+      hipLaunchKernelGGL((crc_stream_kernel<FixedSrc, OutSink, 0, true, true>), grid, block, 0, s, d_tables, src,
+                         nblk, OutSink{out, flags});
   }
   return hipGetLastError();
 }
@@ -161,13 +169,15 @@ hipError_t launch_desc(const LaunchGeom& g, const uint32_t* d_tables, const uint
   if (mode == kModeOut && g_fast_variant != 0)
     return launch_desc_variant(g_fast_variant, g, d_tables, base, blk, nblk, flags, out, s);
   const dim3 grid(grid_for(g, nblk)), block(kThreads);
+  // descriptor lists (C3: Zipf sizes at byte offsets): 16-B lane pieces with nt loads, dynamic
+  // blocks, packed 4-block trees (A/B: profiles/r01_ab_c3_pack*.json)
   const DescSrc src{base, blk, flags};
   if (mode == kModeOut)
-    hipLaunchKernelGGL((crc_stream_kernel<DescSrc, OutSink, 0, true>), grid, block, 0, s, d_tables, src, nblk,
-                       OutSink{out, flags});
+    hipLaunchKernelGGL((crc_stream16_kernel<DescSrc, OutSink, true, true, true>), grid, block, 0, s, d_tables,
+                       src, nblk, OutSink{out, flags});
   else
-    hipLaunchKernelGGL((crc_stream_kernel<DescSrc, VerifySink, 0, true>), grid, block, 0, s, d_tables, src, nblk,
-                       VerifySink{expected, ok, nbad, flags});
+    hipLaunchKernelGGL((crc_stream16_kernel<DescSrc, VerifySink, true, true, true>), grid, block, 0, s, d_tables,
+                       src, nblk, VerifySink{expected, ok, nbad, flags});
   return hipGetLastError();
 }
 
@@ -178,13 +188,14 @@ hipError_t launch_sst(const LaunchGeom& g, const uint32_t* d_tables, uint8_t* bu
   (void)buf_len;
   if (n == 0) return hipSuccess;
   const dim3 grid(grid_for(g, n)), block(kThreads);
+  // sstable blocks (contents + type, ~4 KiB at byte offsets): 32-B pieces, packed 4-block trees
   const SstSrc src{buf, h};
   if (seal)
-    hipLaunchKernelGGL((crc_stream_kernel<SstSrc, SealSink, 0, true>), grid, block, 0, s, d_tables, src, n,
+    hipLaunchKernelGGL((crc_stream_kernel<SstSrc, SealSink, 0, true, true>), grid, block, 0, s, d_tables, src, n,
                        SealSink{});
   else
-    hipLaunchKernelGGL((crc_stream_kernel<SstSrc, SstVerifySink, 0, true>), grid, block, 0, s, d_tables, src, n,
-                       SstVerifySink{ok, nbad});
+    hipLaunchKernelGGL((crc_stream_kernel<SstSrc, SstVerifySink, 0, true, true>), grid, block, 0, s, d_tables,
+                       src, n, SstVerifySink{ok, nbad});
   return hipGetLastError();
 }
 

@@ -391,6 +391,14 @@ hipError_t launch_fixed_variant(int v, const LaunchGeom& g, const uint32_t* d_ta
         hipLaunchKernelGGL((crc_stream16_kernel<FixedSrc, OutSink, false, true>), grid, block, 0, s, d_tables,
                            src, nblk, OutSink{out, flags});
         break;
+      case 15:
+        hipLaunchKernelGGL((crc_stream_kernel<FixedSrc, OutSink, 0, true, true>), grid, block, 0, s, d_tables,
+                           src, nblk, OutSink{out, flags});
+        break;
+      case 16:
+        hipLaunchKernelGGL((crc_stream16_kernel<FixedSrc, OutSink, true, true, true>), grid, block, 0, s,
+                           d_tables, src, nblk, OutSink{out, flags});
+        break;
       default:
         hipLaunchKernelGGL((crc_stream_kernel<FixedSrc, OutSink, 0, true>), grid, block, 0, s, d_tables, src,
                            nblk, OutSink{out, flags});
@@ -468,6 +476,12 @@ hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tab
   else if (v == 14)  // coalesced 16-B pieces, nt loads, static strided blocks
     hipLaunchKernelGGL((crc_stream16_kernel<DescSrc, OutSink, false, true>), grid, block, 0, s, d_tables, src,
                        nblk, OutSink{out, flags});
+  else if (v == 15)  // 32-B pieces, dynamic blocks, packed 4-block trees
+    hipLaunchKernelGGL((crc_stream_kernel<DescSrc, OutSink, 0, true, true>), grid, block, 0, s, d_tables, src,
+                       nblk, OutSink{out, flags});
+  else if (v == 16)  // coalesced 16-B pieces, nt loads, dynamic blocks, packed 4-block trees
+    hipLaunchKernelGGL((crc_stream16_kernel<DescSrc, OutSink, true, true, true>), grid, block, 0, s, d_tables,
+                       src, nblk, OutSink{out, flags});
   else
     hipLaunchKernelGGL((crc_stream_kernel<DescSrc, OutSink, 0, true>), grid, block, 0, s, d_tables, src, nblk,
                        OutSink{out, flags});

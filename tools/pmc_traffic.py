@@ -14,7 +14,7 @@ import statistics
 import sys
 
 out_dir, workload = sys.argv[1], (sys.argv[2] if len(sys.argv) > 2 else "c2")
-KERNELS = {"c2": "crc_pack4k_kernel", "sstable": "crc_stream_kernel", "c3": "crc_stream_kernel"}
+KERNELS = {"c2": "crc_pack4k_kernel", "sstable": "crc_stream_kernel", "c3": "crc_stream16_kernel"}
 target = KERNELS[workload]
 
 
