@@ -129,22 +129,47 @@ __device__ __forceinline__ uint32_t ld32u(const uint8_t* q) {
 
 // Stage the table image into LDS: T0..T3 written 32x (8 x 16-B stores per entry); tree
 // operators catalog[kTree .. kTree+5] -> slots 0..5; catalog[kHorner] -> slot 6 (if >= 0).
+// Loads are issued in batches of 8 per thread before their LDS stores, so staging costs ~2 L2
+// round trips instead of one per element (it is most of a small launch's time: the scalar
+// Extend path launches one block).
 template <int kTree, int kHorner, int kSlot7 = -1, bool kSkipSlot5 = false>
 __device__ __forceinline__ void stage_tables(char* lds, const uint32_t* __restrict__ tabs) {
-  for (uint32_t i = threadIdx.x; i < 4u * 256u * 8u; i += blockDim.x) {
-    const uint32_t k = i >> 11, b = (i >> 3) & 255u, part = i & 7u;
-    const uint32_t v = tabs[k * 256u + b];
-    const uint32_t addr = ((k >> 1) << 16) | (b << 8) | ((k & 1u) << 7) | (part << 4);
-    *reinterpret_cast<u32x4*>(lds + addr) = u32x4{v, v, v, v};
+  constexpr uint32_t kMain = 4u * 256u * 8u;  // 16-B stores of the replicated T0..T3
+  for (uint32_t i0 = 0; i0 < kMain; i0 += 8u * blockDim.x) {
+    uint32_t v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t i = i0 + threadIdx.x + j * blockDim.x;
+      v[j] = i < kMain ? tabs[(i >> 11) * 256u + ((i >> 3) & 255u)] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t i = i0 + threadIdx.x + j * blockDim.x;
+      const uint32_t k = i >> 11, b = (i >> 3) & 255u, part = i & 7u;
+      const uint32_t addr = ((k >> 1) << 16) | (b << 8) | ((k & 1u) << 7) | (part << 4);
+      if (i < kMain) *reinterpret_cast<u32x4*>(lds + addr) = u32x4{v[j], v[j], v[j], v[j]};
+    }
   }
   const u32x4* cat = reinterpret_cast<const u32x4*>(tabs + 1024);
   constexpr uint32_t nslots = kSlot7 >= 0 ? 8u : (kHorner >= 0 ? 7u : 6u);
-  for (uint32_t i = threadIdx.x; i < nslots * 256u; i += blockDim.x) {
-    const uint32_t slot = i >> 8;
-    if (kSkipSlot5 && slot == 5) continue;
-    const uint32_t src = slot < 6 ? kTree + slot
-                                  : (slot == 6 ? static_cast<uint32_t>(kHorner) : static_cast<uint32_t>(kSlot7));
-    *reinterpret_cast<u32x4*>(lds + PDB_MAIN_BYTES + i * 16u) = cat[src * 256u + (i & 255u)];
+  constexpr uint32_t kCat = nslots * 256u;
+  auto src_of = [](uint32_t slot) -> uint32_t {
+    return slot < 6 ? kTree + slot : (slot == 6 ? static_cast<uint32_t>(kHorner) : static_cast<uint32_t>(kSlot7));
+  };
+  for (uint32_t i0 = 0; i0 < kCat; i0 += 4u * blockDim.x) {
+    u32x4 c[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t i = i0 + threadIdx.x + j * blockDim.x;
+      const bool use = i < kCat && !(kSkipSlot5 && (i >> 8) == 5);
+      c[j] = use ? cat[src_of(i >> 8) * 256u + (i & 255u)] : u32x4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t i = i0 + threadIdx.x + j * blockDim.x;
+      const bool use = i < kCat && !(kSkipSlot5 && (i >> 8) == 5);
+      if (use) *reinterpret_cast<u32x4*>(lds + PDB_MAIN_BYTES + i * 16u) = c[j];
+    }
   }
 }
 

@@ -34,6 +34,11 @@ for v in variants:
     if ref is None:
         ref = out.clone()
     assert torch.equal(out, ref), v
+# warm the GPU first: a cold GPU runs its first ~40 launches slower while clocks / power settle
+# (DESIGN.md §6), which would bias whichever variant is timed first
+for _ in range(15):
+    crc32c.batch(d, blk, out=out)
+torch.cuda.synchronize()
 s = torch.cuda.current_stream()
 times = {v: [] for v in variants}
 for r in range(rounds):

@@ -31,6 +31,11 @@ for v in variants:
     if ref is None:
         ref = o
     assert torch.equal(o, ref), f"variant {v} differs from variant {variants[0]}"
+# warm the GPU first: a cold GPU runs its first ~40 launches slower while clocks / power settle
+# (DESIGN.md §6), which would bias whichever variant is timed first
+for _ in range(60):
+    crc32c.batch_fixed(d, 4096, 4096, nblk, out=out)
+torch.cuda.synchronize()
 times = {v: [] for v in variants}
 s = torch.cuda.current_stream()
 for r in range(rounds):

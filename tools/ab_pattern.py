@@ -18,6 +18,11 @@ crc32c.init_device(0)
 d = torch.empty(nblk * 4096, dtype=torch.uint8, device="cuda")
 crc32c.fill_splitmix(d, 301)
 o = torch.zeros(1, dtype=torch.int32, device="cuda")
+# warm the GPU first: a cold GPU runs its first ~40 launches slower while clocks / power settle
+# (DESIGN.md §6), which would bias whichever variant is timed first
+for _ in range(60):
+    check(lib().pdb_diag_read_pattern4k(d.data_ptr(), nblk, variants[0], o.data_ptr(), torch.cuda.current_stream().cuda_stream))
+torch.cuda.synchronize()
 s = torch.cuda.current_stream()
 times = {v: [] for v in variants}
 for r in range(rounds):
