@@ -132,6 +132,10 @@ int pdb_diag_read_pattern4k(const void* d_base, uint64_t nblk, int variant, uint
 /* Fill d_dst[0..nbytes) with the splitmix64 synthetic stream (seed, byte_offset). */
 int pdb_fill_splitmix_device(void* d_dst, uint64_t nbytes, uint64_t seed, uint64_t byte_offset,
                              void* stream);
+/* Park the scalar Extend server and read the exit statistics of its last instance: out4 =
+ * {requests, ticks (10 ns) from seeing a request to answering it, polls, lifetime ticks}.
+ * Returns 1 if its request box is device memory, 0 if pinned host memory, or a negative error. */
+int pdb_diag_server_stats(uint64_t* out4);
 /* Select a 4-KiB fast-path kernel variant (A/B experiments only; 0 = shipped default).
  * Returns the previous selection. */
 int pdb_diag_set_variant(int v);

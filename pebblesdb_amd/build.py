@@ -17,7 +17,7 @@ LIBDIR = os.path.join(PKG, "_lib")
 LIB = os.path.join(LIBDIR, "libpdb_crc32c.so")
 ARCH = "gfx950"
 
-SOURCES = ["crc32c_kernels.hip", "crc32c_variants.hip", "crc32c_capi.cpp", "crc32c_tables.cpp"]
+SOURCES = ["crc32c_kernels.hip", "crc32c_server.hip", "crc32c_variants.hip", "crc32c_capi.cpp", "crc32c_tables.cpp"]
 HEADERS = ["crc32c_math.h", "crc32c_internal.h", "crc32c_device.h"]
 
 

@@ -7,6 +7,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include <algorithm>
 #include <memory>
@@ -46,8 +47,28 @@ struct DevState {
   uint8_t* d_stage = nullptr;  // device alias of h_stage
   size_t stage_cap = 0;
   uint32_t seq = 0;          // scalar-call sentinel sequence
-  bool scalar_poll = true;   // PDB_SCALAR_WAIT=sync: wait on the stream instead (A/B diagnostics)
+  // Scalar calls <= kServerCap: kScalarServer (default) posts them to the persistent server
+  // kernel (crc32c_server.hip); PDB_SCALAR_WAIT=poll launches one kernel per call and spins on
+  // the result, =sync waits on the stream (A/B diagnostics, tools/scalar_latency.py).
+  int scalar_mode = 0;
+  ServerBox* srv_in_h = nullptr;   // request box + data area (kServerBytes), host-writable address
+  ServerBox* srv_in_d = nullptr;   // its device address
+  bool srv_in_device = false;      // request box in fine-grained device memory (large BAR)
+  ServerBox* srv_out_h = nullptr;  // response box (pinned host memory)
+  ServerBox* srv_out_d = nullptr;
+  bool large_bar = false;
+  hipStream_t srv_stream = nullptr;
+  uint32_t srv_epoch = 0;      // epoch of the most recently launched server
+  uint32_t srv_seq = 0;        // last request posted
+  bool srv_live = false;       // a server of srv_epoch may still be in its loop (guarded by mu)
 };
+
+enum ScalarMode : int { kScalarServer = 0, kScalarPoll = 1, kScalarSync = 2 };
+// Server lifetime (s_memrealtime ticks, 100 MHz): it leaves after 20 ms without a request or
+// 200 ms in total; the next call relaunches it (~20 us), so a process that dies or forgets to stop
+// it never leaves a kernel spinning for long.
+constexpr uint64_t kServerIdleTicks = 2000000ull;
+constexpr uint64_t kServerLifeTicks = 20000000ull;
 
 constexpr int kMaxDev = 64;
 std::mutex g_init_mu;
@@ -55,11 +76,15 @@ DevState* g_dev[kMaxDev] = {};
 
 int get_state(DevState** out) {
   int dev = 0;
-  int n = 0;
-  hipError_t e = hipGetDeviceCount(&n);
-  if (e != hipSuccess || n <= 0)
-    return fail(PDB_ENODEV, "no HIP device visible (pdb_crc32c has no CPU fallback)");
-  e = hipGetDevice(&dev);
+  static int g_ndev = 0;  // device count, cached once positive
+  if (__atomic_load_n(&g_ndev, __ATOMIC_ACQUIRE) <= 0) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n <= 0)
+      return fail(PDB_ENODEV, "no HIP device visible (pdb_crc32c has no CPU fallback)");
+    __atomic_store_n(&g_ndev, n, __ATOMIC_RELEASE);
+  }
+  hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
   if (dev < 0 || dev >= kMaxDev) return fail(PDB_ENODEV, "device index out of range");
   DevState* st = __atomic_load_n(&g_dev[dev], __ATOMIC_ACQUIRE);
@@ -82,6 +107,7 @@ int get_state(DevState** out) {
                                 prop.gcnArchName);
   s->geom.grid = prop.multiProcessorCount > 0 ? static_cast<uint32_t>(prop.multiProcessorCount) : 256;
   s->geom.block = 1024;
+  s->large_bar = prop.isLargeBar != 0;
   std::vector<uint32_t> tabs(PDB_TABLE_WORDS);
   build_device_tables(tabs.data());
   e = hipMalloc(&s->d_tables, tabs.size() * sizeof(uint32_t));
@@ -95,7 +121,9 @@ int get_state(DevState** out) {
   e = hipMemcpy(s->d_pow2, pow2.data(), pow2.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
   if (e != hipSuccess) return hip_fail(e, "hipMemcpy(pow2)");
   const char* wait = getenv("PDB_SCALAR_WAIT");
-  s->scalar_poll = !(wait && strcmp(wait, "sync") == 0);
+  s->scalar_mode = !wait ? kScalarServer
+                          : strcmp(wait, "sync") == 0 ? kScalarSync
+                          : strcmp(wait, "poll") == 0 ? kScalarPoll : kScalarServer;
   e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
   if (e != hipSuccess) return hip_fail(e, "hipStreamCreate");
   __atomic_store_n(&g_dev[dev], s.get(), __ATOMIC_RELEASE);
@@ -152,6 +180,154 @@ int ensure_stage(DevState* st, size_t bytes) {
   return PDB_OK;
 }
 
+// ---- scalar Extend service (crc32c_server.hip) -------------------------------------------------
+double now_s() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec + 1e-9 * ts.tv_nsec;
+}
+
+uint32_t box_load(const uint32_t* p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
+
+// Post request word {init, len, seq} (st->mu held); returns its seq.  The request box may be device
+// memory written through the BAR (write-combined): the fences order the staged bytes before the
+// request word and push the word out at once.
+uint32_t server_post(DevState* st, uint32_t init, uint32_t len) {
+  const uint32_t seq = st->srv_seq = (st->srv_seq + 1) & kServerSeqMask;
+  const uint64_t w = (static_cast<uint64_t>((seq << 17) | len) << 32) | init;
+  __builtin_ia32_sfence();
+  __atomic_store_n(&st->srv_in_h->req, w, __ATOMIC_RELEASE);
+  __builtin_ia32_sfence();
+  return seq;
+}
+
+bool server_exited(const DevState* st) { return box_load(&st->srv_out_h->exit_epoch) == st->srv_epoch; }
+
+uint64_t server_resp(const DevState* st) { return __atomic_load_n(&st->srv_out_h->resp, __ATOMIC_ACQUIRE); }
+
+// Ask the server of st->srv_epoch to leave and wait until it has (st->mu held).  Host memory only,
+// no HIP call, so it is safe inside stream capture.  The server answers within one poll (~2 us);
+// its lifetime bounds the wait in any case.
+int server_park(DevState* st) {
+  if (!st->srv_live) return PDB_OK;
+  if (!server_exited(st)) {
+    server_post(st, 0u, kServerStop);
+    const double t0 = now_s();
+    while (!server_exited(st)) {
+      __builtin_ia32_pause();
+      if (now_s() - t0 > 2.0) return fail(PDB_EHIP, "scalar server did not stop within 2 s");
+    }
+  }
+  __atomic_store_n(&st->srv_live, false, __ATOMIC_RELEASE);
+  return PDB_OK;
+}
+
+// Batch launches need every CU's full LDS: park a live server first.
+int quiesce(DevState* st) {
+  if (!__atomic_load_n(&st->srv_live, __ATOMIC_ACQUIRE)) return PDB_OK;
+  std::lock_guard<std::mutex> lk(st->mu);
+  return server_park(st);
+}
+
+void park_all_at_exit() {
+  for (int d = 0; d < kMaxDev; ++d) {
+    DevState* st = __atomic_load_n(&g_dev[d], __ATOMIC_ACQUIRE);
+    if (!st || !__atomic_load_n(&st->srv_live, __ATOMIC_ACQUIRE)) continue;
+    std::unique_lock<std::mutex> lk(st->mu, std::try_to_lock);
+    if (!lk.owns_lock()) continue;  // a call in flight at exit: the idle timeout ends the server
+    if (!server_exited(st)) server_post(st, 0u, kServerStop);
+    const double t0 = now_s();
+    while (!server_exited(st) && now_s() - t0 < 0.5) __builtin_ia32_pause();
+  }
+}
+
+int alloc_pinned(size_t bytes, ServerBox** h, ServerBox** d) {
+  void* hp = nullptr;
+  hipError_t e = hipHostMalloc(&hp, bytes, hipHostMallocMapped | hipHostMallocCoherent);
+  if (e != hipSuccess) return fail(PDB_ENOMEM, std::string("hipHostMalloc(server): ") + hipGetErrorString(e));
+  memset(hp, 0, bytes);
+  void* dp = nullptr;
+  if ((e = hipHostGetDevicePointer(&dp, hp, 0)) != hipSuccess) {
+    (void)hipHostFree(hp);
+    return hip_fail(e, "hipHostGetDevicePointer(server)");
+  }
+  *h = static_cast<ServerBox*>(hp);
+  *d = static_cast<ServerBox*>(dp);
+  return PDB_OK;
+}
+
+int server_alloc(DevState* st) {
+  hipError_t e;
+  int rc;
+  // request box: fine-grained device memory written by the host through the large BAR (the server
+  // polls local HBM: ~0.37 us per poll vs ~1.2 us across PCIe, tools/server_probe.hip), else pinned
+  // host memory.  PDB_SERVER_BOX=host forces the latter (A/B).
+  const char* where = getenv("PDB_SERVER_BOX");
+  const bool want_dev = st->large_bar && !(where && strcmp(where, "host") == 0);
+  if (want_dev) {
+    void* p = nullptr;
+    e = hipExtMallocWithFlags(&p, kServerBytes, hipDeviceMallocFinegrained);
+    if (e == hipSuccess) {
+      if ((e = hipMemset(p, 0, kServerBytes)) != hipSuccess) return hip_fail(e, "hipMemset(server box)");
+      st->srv_in_h = st->srv_in_d = static_cast<ServerBox*>(p);
+      st->srv_in_device = true;
+    }
+  }
+  if (!st->srv_in_h && (rc = alloc_pinned(kServerBytes, &st->srv_in_h, &st->srv_in_d))) return rc;
+  if ((rc = alloc_pinned(sizeof(ServerBox), &st->srv_out_h, &st->srv_out_d))) return rc;
+  if ((e = hipStreamCreateWithFlags(&st->srv_stream, hipStreamNonBlocking)) != hipSuccess)
+    return hip_fail(e, "hipStreamCreate(server)");
+  static std::once_flag once;
+  std::call_once(once, [] { atexit(park_all_at_exit); });
+  return PDB_OK;
+}
+
+// Launch a server instance (st->mu held).  `pending`: a request of seq st->srv_seq is waiting.
+int server_launch(DevState* st, bool pending) {
+  int rc;
+  if (!st->srv_stream && (rc = server_alloc(st))) return rc;
+  hipError_t e = hipSetDevice(st->device);
+  if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+  const uint32_t epoch = ++st->srv_epoch;
+  const uint32_t served0 = pending ? (st->srv_seq - 1) & kServerSeqMask : st->srv_seq;
+  e = launch_server(st->d_tables, st->srv_in_d, st->srv_out_d, epoch, served0, kServerIdleTicks, kServerLifeTicks,
+                    st->srv_stream);
+  if (e != hipSuccess) return hip_fail(e, "launch_server");
+  __atomic_store_n(&st->srv_live, true, __ATOMIC_RELEASE);
+  return PDB_OK;
+}
+
+// One request (st->mu held, n <= kServerCap): stage the bytes, post the request word, spin on the
+// response word.  A server that left its loop without taking the request (idle / lifetime exit
+// racing the post) is relaunched; the new instance serves the pending request.
+int server_call(DevState* st, uint32_t init, const uint8_t* data, uint64_t n, uint32_t* out) {
+  int rc;
+  if (!st->srv_live || server_exited(st))
+    if ((rc = server_launch(st, false))) return rc;
+  uint8_t* area = reinterpret_cast<uint8_t*>(st->srv_in_h) + sizeof(ServerBox);
+  memcpy(area + ((0u - static_cast<uint32_t>(n)) & 15u), data, n);
+  const uint32_t seq = server_post(st, init, static_cast<uint32_t>(n));
+  double t0 = 0;
+  for (uint32_t spin = 1;; ++spin) {
+    const uint64_t r = server_resp(st);
+    if (static_cast<uint32_t>(r >> 32) == seq) {
+      *out = static_cast<uint32_t>(r);
+      return PDB_OK;
+    }
+    if (server_exited(st)) {
+      // re-check the answer first: the server may have answered and then left
+      if (static_cast<uint32_t>(server_resp(st) >> 32) == seq) continue;
+      if ((rc = server_launch(st, true))) return rc;
+    }
+    __builtin_ia32_pause();
+    if ((spin & 0xFFFFu) == 0) {
+      const double t = now_s();
+      if (t0 == 0) t0 = t;
+      else if (t - t0 > 10.0) return fail(PDB_EHIP, "scalar server gave no answer within 10 s");
+    }
+  }
+}
+
 // Host batch over descriptors: stage [lo, hi) of the host span, the rebased descriptors and the
 // outputs in one workspace; one H2D span copy, one H2D descriptor copy, kernel, one D2H.
 int host_desc(const uint8_t* base, uint64_t base_len, const pdb_blk* blk, uint64_t nblk,
@@ -176,6 +352,7 @@ int host_desc(const uint8_t* base, uint64_t base_len, const pdb_blk* blk, uint64
   int rc = get_state(&st);
   if (rc) return rc;
   std::lock_guard<std::mutex> lk(st->mu);
+  if ((rc = server_park(st))) return rc;
   hipError_t e = hipSetDevice(st->device);
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
   const size_t span = hi - lo;
@@ -236,8 +413,10 @@ int host_scalar(uint32_t init, const uint8_t* data, uint64_t n, uint32_t* out) {
   int rc = get_state(&st);
   if (rc) return rc;
   std::lock_guard<std::mutex> lk(st->mu);
+  if (st->scalar_mode == kScalarServer && n <= kServerCap) return server_call(st, init, data, n, out);
   hipError_t e = hipSetDevice(st->device);
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+  if ((rc = server_park(st))) return rc;
   if ((rc = ensure_stage(st, kStageHdr + align_up(n, 256)))) return rc;
   memcpy(st->h_stage + kStageHdr, data, n);
   uint32_t* d_res = reinterpret_cast<uint32_t*>(st->d_stage);
@@ -252,7 +431,7 @@ int host_scalar(uint32_t init, const uint8_t* data, uint64_t n, uint32_t* out) {
     e = launch_fixed(st->geom, st->d_tables, st->d_stage + kStageHdr, 0, static_cast<uint32_t>(n), 1,
                      PDB_CRC_USE_INIT, init, d_res, s);
     if (e != hipSuccess) return hip_fail(e, "launch_fixed(scalar)");
-    if (st->scalar_poll) {
+    if (st->scalar_mode == kScalarPoll) {
       for (uint32_t spin = 0; spin < (1u << 22); ++spin) {
         const uint32_t v = *h_res;
         if (v != sentinel) {
@@ -280,6 +459,7 @@ int host_span(uint32_t init, const uint8_t* data, uint64_t n, uint32_t* out) {
   int rc = get_state(&st);
   if (rc) return rc;
   std::lock_guard<std::mutex> lk(st->mu);
+  if ((rc = server_park(st))) return rc;
   hipError_t e = hipSetDevice(st->device);
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
   const size_t off_scr = align_up(n + 16, 256);
@@ -321,6 +501,7 @@ int host_sst(uint8_t* buf, uint64_t buf_len, const pdb_block_handle* h, uint64_t
   int rc = get_state(&st);
   if (rc) return rc;
   std::lock_guard<std::mutex> lk(st->mu);
+  if ((rc = server_park(st))) return rc;
   hipError_t e = hipSetDevice(st->device);
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
   const size_t span = hi - lo;
@@ -422,6 +603,7 @@ int pdb_crc32c_extend_device(uint32_t init_crc, const void* d_data, uint64_t n, 
   DevState* st;
   int rc = get_state(&st);
   if (rc) return rc;
+  if ((rc = quiesce(st))) return rc;
   hipError_t e = launch_span(st->geom, st->d_tables, st->d_pow2, init_crc, static_cast<const uint8_t*>(d_data),
                              n, d_scratch, d_out, pick_stream(st, stream));
   return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_span");
@@ -434,6 +616,7 @@ int pdb_crc32c_batch_device_fixed(const void* d_base, uint64_t stride, uint32_t 
   DevState* st;
   int rc = get_state(&st);
   if (rc) return rc;
+  if ((rc = quiesce(st))) return rc;
   hipError_t e = launch_fixed(st->geom, st->d_tables, static_cast<const uint8_t*>(d_base), stride, len,
                               nblk, flags, init, d_out, pick_stream(st, stream));
   return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_fixed");
@@ -446,6 +629,7 @@ int pdb_crc32c_batch_device(const void* d_base, const pdb_blk* d_blk, uint64_t n
   DevState* st;
   int rc = get_state(&st);
   if (rc) return rc;
+  if ((rc = quiesce(st))) return rc;
   hipError_t e = launch_desc(st->geom, st->d_tables, static_cast<const uint8_t*>(d_base), d_blk, nblk,
                              flags, kModeOut, nullptr, d_out, nullptr, nullptr, pick_stream(st, stream));
   return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_desc");
@@ -459,6 +643,7 @@ int pdb_crc32c_verify_device(const void* d_base, const pdb_blk* d_blk, uint64_t 
   DevState* st;
   int rc = get_state(&st);
   if (rc) return rc;
+  if ((rc = quiesce(st))) return rc;
   hipError_t e = launch_desc(st->geom, st->d_tables, static_cast<const uint8_t*>(d_base), d_blk, nblk,
                              flags, kModeVerify, d_expected, nullptr, d_ok, d_nbad,
                              pick_stream(st, stream));
@@ -479,6 +664,7 @@ int pdb_sst_seal_device(void* d_buf, uint64_t buf_len, const pdb_block_handle* d
   DevState* st;
   int rc = get_state(&st);
   if (rc) return rc;
+  if ((rc = quiesce(st))) return rc;
   hipError_t e = launch_sst(st->geom, st->d_tables, static_cast<uint8_t*>(d_buf), buf_len, d_h, n, true,
                             nullptr, nullptr, pick_stream(st, stream));
   return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_sst(seal)");
@@ -491,6 +677,7 @@ int pdb_sst_verify_device(const void* d_buf, uint64_t buf_len, const pdb_block_h
   DevState* st;
   int rc = get_state(&st);
   if (rc) return rc;
+  if ((rc = quiesce(st))) return rc;
   hipError_t e = launch_sst(st->geom, st->d_tables, static_cast<uint8_t*>(const_cast<void*>(d_buf)),
                             buf_len, d_h, n, false, d_ok, d_nbad, pick_stream(st, stream));
   return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_sst(verify)");
@@ -511,6 +698,7 @@ int pdb_diag_read_stream(const void* d_base, uint64_t nbytes, uint32_t* d_out, v
   DevState* st;
   int rc = get_state(&st);
   if (rc) return rc;
+  if ((rc = quiesce(st))) return rc;
   hipError_t e = launch_read_stream(static_cast<const uint8_t*>(d_base), nbytes, d_out,
                                     pick_stream(st, stream));
   return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_read_stream");
@@ -521,6 +709,7 @@ int pdb_diag_read_pattern4k(const void* d_base, uint64_t nblk, int variant, uint
   DevState* st;
   int rc = get_state(&st);
   if (rc) return rc;
+  if ((rc = quiesce(st))) return rc;
   hipError_t e = launch_read_pattern4k(st->geom, static_cast<const uint8_t*>(d_base), nblk, variant, d_out,
                                        pick_stream(st, stream));
   return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_read_pattern4k");
@@ -534,6 +723,21 @@ int pdb_fill_splitmix_device(void* d_dst, uint64_t nbytes, uint64_t seed, uint64
   hipError_t e = launch_fill_splitmix(static_cast<uint8_t*>(d_dst), nbytes, seed, byte_offset,
                                       pick_stream(st, stream));
   return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_fill_splitmix");
+}
+
+int pdb_diag_server_stats(uint64_t* out4) {
+  DevState* st;
+  int rc = get_state(&st);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(st->mu);
+  if ((rc = server_park(st))) return rc;
+  if (!st->srv_out_h) return fail(PDB_EINVAL, "the scalar server has not run");
+  const ServerBox* b = st->srv_out_h;
+  out4[0] = b->stat_requests;
+  out4[1] = b->stat_serve_ticks;
+  out4[2] = b->stat_polls;
+  out4[3] = b->stat_life_ticks;
+  return st->srv_in_device ? 1 : 0;
 }
 
 int pdb_diag_set_variant(int v) {

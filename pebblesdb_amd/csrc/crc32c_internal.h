@@ -47,6 +47,37 @@ hipError_t launch_span(const LaunchGeom& g, const uint32_t* d_tables, const uint
                        uint32_t init, const uint8_t* data, uint64_t n, uint32_t* scratch, uint32_t* out,
                        hipStream_t s);
 
+// crc32c_server.hip -- the scalar Extend service (persistent one-workgroup kernel).  Two boxes:
+// the request box `in` (request word + the caller's bytes, placed so that they end on a 16-B
+// boundary: data = in + sizeof(ServerBox) + ((-n) & 15)) lives in fine-grained device memory the
+// host writes through the large BAR (the GPU then polls and reads local HBM), or in pinned host
+// memory when the BAR is small; the response box `out` (resp word, exit_epoch) is pinned host
+// memory the GPU writes across PCIe.
+//   req  (host -> device, one 64-bit word, so one poll reads a whole request):
+//        bits 0..31 init (the Extend seed), 32..48 len (<= kServerCap, or kServerStop),
+//        49..63 seq (15 bits, bumped per request)
+//   resp (device -> host, one 64-bit word): bits 0..31 crc, 32..46 seq of the answered request
+//   exit_epoch: epoch of the last server instance that has left its loop
+struct ServerBox {
+  uint64_t req;
+  uint64_t pad0[7];
+  uint64_t resp;
+  uint32_t exit_epoch;
+  uint32_t pad1[13];
+  // written at exit (diagnostics): requests served, ticks (10 ns) from seeing a request to
+  // issuing its answer, polls, lifetime ticks
+  uint64_t stat_requests, stat_serve_ticks, stat_polls, stat_life_ticks;
+  uint64_t pad2[12];
+};
+static_assert(sizeof(ServerBox) == 256, "mailbox is 4 cache lines");
+constexpr uint32_t kServerCap = 64u << 10;  // largest request the server takes
+constexpr uint32_t kServerStop = 0x1FFFFu;  // len value of a stop request
+constexpr uint32_t kServerSeqMask = 0x7FFFu;
+constexpr size_t kServerBytes = sizeof(ServerBox) + kServerCap + 16;
+// served0: the seq the new instance treats as already answered.
+hipError_t launch_server(const uint32_t* d_tables, ServerBox* d_in, ServerBox* d_out, uint32_t epoch,
+                         uint32_t served0, uint64_t idle_ticks, uint64_t life_ticks, hipStream_t s);
+
 // crc32c_variants.hip -- A/B variants (pdb_diag_set_variant) and calibration kernels
 hipError_t launch_fixed_variant(int v, const LaunchGeom& g, const uint32_t* d_tables, const uint8_t* base,
                                 uint64_t stride, uint32_t len, uint64_t nblk, uint32_t flags, uint32_t init,

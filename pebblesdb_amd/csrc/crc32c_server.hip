@@ -1,0 +1,168 @@
+// crc32c_server.hip -- the scalar Extend service: a persistent one-workgroup kernel that serves
+// leveldb::crc32c::Extend calls (util/crc32c.h:17; called per WAL record by log_writer.cc:121,
+// per sstable block by table_builder.cc:197-199 and format.cc:97) from a pinned host mailbox.
+//
+// Why: a synchronous scalar call is latency-bound.  Launching a kernel per call costs ~10 us
+// (dispatch, wave launch, staging the 160-KiB LDS image, PCIe reads, result write;
+// profiles/r01_scalar_latency_poll.json).  The server pays dispatch and LDS staging once per
+// lifetime and then only polls its mailbox across PCIe, reads the caller's bytes, hashes them
+// with one wave and posts the CRC back into the same mapping.
+//
+// Protocol (ServerBox, crc32c_internal.h): the host writes the bytes (placed so that they END on
+// a 16-B boundary), then ONE 64-bit request word {init, len, seq}; the server polls that word
+// (one PCIe read carries the whole request), reads the bytes (one more round trip per 16 KiB)
+// and answers with ONE 64-bit word {crc, seq}.  The server exits on a stop request (len =
+// kServerStop), after `idle_ticks` without a request, or after `life_ticks` in total
+// (s_memrealtime, 100 MHz), and writes exit_epoch = its epoch as its last act, so the host can
+// tell a live server from a finished one without a HIP call.  Every wave reaches the exit: waves 1..3 leave after staging,
+// wave 0's loop is bounded by the lifetime.
+//
+// Per request, wave 0 hashes n bytes with the geometry of crc_stream16_kernel (16-B lane pieces,
+// rounds of 4 KiB: piece c = 256r + 64j + u on lane u, chain j; 4 chains folded with shift 1024,
+// rounds chained with shift 1008, rotation by K mod 64, 6-level DPP tree over 16 << k), with every
+// piece 16-B aligned by the host's placement; the t = n mod 16 head bytes are hashed from the
+// seed on broadcast words.  Loads of up to 4 rounds (16 KiB) are issued together so a request
+// pays about one PCIe round trip per 16 KiB.
+#include "crc32c_device.h"
+
+namespace pdb {
+namespace {
+
+__device__ __forceinline__ uint64_t sys_load64(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ __forceinline__ void sys_store64(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ __forceinline__ void sys_store32(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// System-coherent 16-B load (sc0 sc1: bypasses the GPU caches, so bytes the host wrote into a
+// mailbox in host memory or in fine-grained device memory are never served stale from L2).
+__device__ __forceinline__ u32x4 ld_sys16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 17));
+}
+
+__device__ __forceinline__ uint32_t u4(const u32x4& v, uint32_t i) {
+  return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
+}
+
+// Raw state after the n bytes at byte offset data_off of the request box from state init_raw;
+// valid in lane 0.  q0 = data_off + n % 16 is 16-B aligned and the head (n % 16 bytes) is the tail
+// of the aligned 16 B before q0.  Every load of a 16-KiB batch is issued unconditionally
+// (out-of-range pieces read q0 - 16 and are ignored), so a batch costs one memory round trip.
+__device__ __forceinline__ uint32_t server_hash(const char* lds, const LaneTabs& lt, uint32_t u,
+                                                __amdgpu_buffer_rsrc_t rin, uint32_t data_off, uint32_t n,
+                                                uint32_t init_raw) {
+  const uint32_t t = n & 15u, lead = t & 3u, nh = t >> 2, K = n >> 4;
+  const uint32_t q0 = data_off + t;
+  const uint32_t R = (K + 255u) >> 8;
+  uint32_t acc = 0, h = init_raw;
+  for (uint32_t r0 = 0; r0 < R || r0 == 0; r0 += 4) {
+    u32x4 e[4][4];
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t c = ((r0 + rr) << 8) + 64u * j + u;
+        e[rr][j] = ld_sys16(rin, c < K ? q0 + 16u * c : q0 - 16u);
+      }
+    if (r0 == 0) {
+      // head: dwords 4-nh..3 of the 16 B before q0, preceded by the top `lead` bytes of dword 3-nh
+      const u32x4 hv = ld_sys16(rin, q0 - 16u);
+      if (lead) {
+        const uint32_t lb = u4(hv, 3u - nh) >> (8u * (4u - lead));
+        for (uint32_t j = 0; j < lead; ++j) h = step1(lds, lt, h, (lb >> (8u * j)) & 0xffu);
+      }
+      for (uint32_t j = 4u - nh; j < 4u; ++j) h = step4(lds, lt, h, u4(hv, j));
+      acc = u == 0 ? h : 0u;
+    }
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const uint32_t ck = r0 + rr;
+      if (ck >= R) break;  // wave-uniform
+      const uint32_t rem = K - (ck << 8);
+      const uint32_t J = rem >= 256u ? 4u : (rem > u ? ((rem - u - 1u) >> 6) + 1u : 0u);
+      if (J) {
+        const uint32_t start = ck ? shift_op(lds, PDB_SLOT_HORNER, acc) : acc;
+        const uint32_t x0 = chain16(lds, lt, start, e[rr][0], 0u, 0u);
+        const uint32_t x1 = chain16(lds, lt, 0u, e[rr][1], 0u, 0u);
+        const uint32_t x2 = chain16(lds, lt, 0u, e[rr][2], 0u, 0u);
+        const uint32_t x3 = chain16(lds, lt, 0u, e[rr][3], 0u, 0u);
+        uint32_t a = x0;
+        if (J > 1) a = shift_op_x(lds, 7, a, x1);
+        if (J > 2) a = shift_op_x(lds, 7, a, x2);
+        if (J > 3) a = shift_op_x(lds, 7, a, x3);
+        acc = a;
+      }
+    }
+  }
+  if (K == 0) return h;
+  const uint32_t q = K & 63u;
+  if (q) acc = __shfl(acc, (u + q) & 63u, 64);
+  return wave_tree_dpp<false>(lds, u, acc);
+}
+
+__global__ __launch_bounds__(256) void crc_server_kernel(const uint32_t* __restrict__ tabs, ServerBox* in,
+                                                          ServerBox* out, uint32_t epoch, uint32_t served0,
+                                                          uint64_t idle_ticks, uint64_t life_ticks) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
+  char* lds = reinterpret_cast<char*>(lds_words);
+  stage_tables<PDB_CAT_TREE16, PDB_CAT_H1008, PDB_CAT_S1024>(lds, tabs);
+  __syncthreads();
+  if (threadIdx.x >= 64) return;
+  const uint32_t u = threadIdx.x;
+  const LaneTabs lt = lane_tabs(u);
+  const __amdgpu_buffer_rsrc_t rin =
+      __builtin_amdgcn_make_buffer_rsrc(in, 0, static_cast<int>(kServerBytes), 0x00020000);
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  uint64_t t_last = t0;
+  uint32_t served = served0;
+  uint64_t n_req = 0, n_poll = 0, serve_ticks = 0;
+  for (;;) {
+    const uint64_t rq = sys_load64(&in->req);
+    ++n_poll;
+    const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(rq >> 32));
+    const uint32_t seq = hi >> 17, n = hi & 0x1FFFFu;
+    const uint64_t now = __builtin_amdgcn_s_memrealtime();
+    if (seq != served) {
+      served = seq;
+      if (n > kServerCap) break;  // stop request
+      // no acquire fence: every load of the request bytes is system-coherent (sc0 sc1) and is
+      // issued only after this poll returned (control dependency), so it sees the bytes the host
+      // wrote before the request word (x86 store order + sfence, PCIe posted-write order)
+      const uint32_t init = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(rq));
+      const uint32_t crc =
+          ~server_hash(lds, lt, u, rin, static_cast<uint32_t>(sizeof(ServerBox)) + ((0u - n) & 15u), n, ~init);
+      if (u == 0) sys_store64(&out->resp, (static_cast<uint64_t>(seq) << 32) | crc);
+      t_last = now;
+      ++n_req;
+      serve_ticks += __builtin_amdgcn_s_memrealtime() - now;
+      continue;
+    }
+    if (now - t_last > idle_ticks || now - t0 > life_ticks) break;
+    __builtin_amdgcn_s_sleep(2);
+  }
+  if (u == 0) {
+    sys_store64(&out->stat_requests, n_req);
+    sys_store64(&out->stat_serve_ticks, serve_ticks);
+    sys_store64(&out->stat_polls, n_poll);
+    sys_store64(&out->stat_life_ticks, __builtin_amdgcn_s_memrealtime() - t0);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    sys_store32(&out->exit_epoch, epoch);
+  }
+}
+
+}  // namespace
+
+hipError_t launch_server(const uint32_t* d_tables, ServerBox* d_in, ServerBox* d_out, uint32_t epoch,
+                         uint32_t served0, uint64_t idle_ticks, uint64_t life_ticks, hipStream_t s) {
+  hipLaunchKernelGGL(crc_server_kernel, dim3(1), dim3(256), 0, s, d_tables, d_in, d_out, epoch, served0,
+                     idle_ticks, life_ticks);
+  return hipGetLastError();
+}
+
+}  // namespace pdb
