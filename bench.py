@@ -34,7 +34,7 @@ METRIC = "GiB/s CRC32C over batched 4 KiB sstable blocks (device-resident); % HB
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=200)
     # 40: the first ~20-30 launches of a cold GPU run slower (clock / power settling; see
     # DESIGN.md §6), so the default warmup covers them
     ap.add_argument("--warmup", type=int, default=40)

@@ -507,7 +507,7 @@ int host_sst(uint8_t* buf, uint64_t buf_len, const pdb_block_handle* h, uint64_t
   const size_t span = hi - lo;
   const size_t off_h = align_up(span + 16, 256);
   const size_t off_ok = align_up(off_h + n * sizeof(pdb_block_handle), 256);
-  const size_t off_nbad = align_up(off_ok + n, 256);
+  const size_t off_nbad = align_up(off_ok + 4 * n, 256);  // ok bytes (verify) or masked CRCs (seal)
   rc = ensure_ws(st, off_nbad + 256);
   if (rc) return rc;
   std::vector<pdb_block_handle> rh(h, h + n);
@@ -520,21 +520,32 @@ int host_sst(uint8_t* buf, uint64_t buf_len, const pdb_block_handle* h, uint64_t
   if ((e = hipMemcpyAsync(ws + off_h, rh.data(), n * sizeof(pdb_block_handle), hipMemcpyHostToDevice,
                           s)) != hipSuccess)
     return hip_fail(e, "hipMemcpyAsync(handles)");
-  if ((e = hipMemsetAsync(d_nbad, 0, 4, s)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
-  e = launch_sst(st->geom, st->d_tables, ws, span, reinterpret_cast<const pdb_block_handle*>(ws + off_h),
-                 n, seal, ws + off_ok, d_nbad, s);
-  if (e != hipSuccess) return hip_fail(e, "launch_sst");
   if (seal) {
-    // Copy back only the 4 CRC bytes of every trailer (the rest of the image is unchanged).
-    // Done as one span copy into a host temp, then scattered, to keep it to one D2H.
-    std::vector<uint8_t> tmp(span);
-    if ((e = hipMemcpyAsync(tmp.data(), ws, span, hipMemcpyDeviceToHost, s)) != hipSuccess)
-      return hip_fail(e, "hipMemcpyAsync(span back)");
+    // Only the 4 CRC bytes of every trailer change: the kernel writes the masked CRCs into a
+    // compact array, 4 B per block come back across PCIe (not the span), and the host encodes
+    // them little-endian at offset + size + 1 (table_builder.cc:199-200).
+    uint32_t* d_crc = reinterpret_cast<uint32_t*>(ws + off_ok);
+    e = launch_sst_masked(st->geom, st->d_tables, ws, reinterpret_cast<const pdb_block_handle*>(ws + off_h), n,
+                          d_crc, s);
+    if (e != hipSuccess) return hip_fail(e, "launch_sst_masked");
+    std::vector<uint32_t> crc(n);
+    if ((e = hipMemcpyAsync(crc.data(), d_crc, n * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
+      return hip_fail(e, "hipMemcpyAsync(crcs)");
     if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
-    for (uint64_t i = 0; i < n; ++i) memcpy(buf + h[i].offset + h[i].size + 1, tmp.data() + rh[i].offset + h[i].size + 1, 4);
+    for (uint64_t i = 0; i < n; ++i) {
+      uint8_t* tr = buf + h[i].offset + h[i].size + 1;
+      tr[0] = static_cast<uint8_t>(crc[i]);
+      tr[1] = static_cast<uint8_t>(crc[i] >> 8);
+      tr[2] = static_cast<uint8_t>(crc[i] >> 16);
+      tr[3] = static_cast<uint8_t>(crc[i] >> 24);
+    }
     if (nbad_out) *nbad_out = 0;
     return PDB_OK;
   }
+  if ((e = hipMemsetAsync(d_nbad, 0, 4, s)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
+  e = launch_sst(st->geom, st->d_tables, ws, span, reinterpret_cast<const pdb_block_handle*>(ws + off_h),
+                 n, false, ws + off_ok, d_nbad, s);
+  if (e != hipSuccess) return hip_fail(e, "launch_sst");
   uint32_t nb = 0;
   if (ok && (e = hipMemcpyAsync(ok, ws + off_ok, n, hipMemcpyDeviceToHost, s)) != hipSuccess)
     return hip_fail(e, "hipMemcpyAsync(ok)");

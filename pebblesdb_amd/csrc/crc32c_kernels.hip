@@ -7,14 +7,16 @@
 // (table/format.cc:96-98).  Results are bit-identical (tests/golden + oracle parity).
 //
 // Shipped launches (the kernels themselves live in crc32c_device.h):
-//   * crc_pack4k_kernel<1> -- fixed stride, 4-KiB, 16-B aligned blocks (BASELINE configs 2/4).
-//     One wave per block, lane l owns two 32-B pieces (32l and 2048+32l) hashed as two
-//     independent slice-by-4 chains, 4 blocks per wave-iteration folded in one packed tree,
-//     one barrier per 4-block group keeps the workgroup's 16 waves on 16 consecutive blocks.
-//   * crc_stream_kernel<Src, Sink, 0, dyn> -- any length / alignment (fixed stride, descriptor
-//     lists, sstable seal / verify): 32-B pieces in 4-KiB rounds with per-lane Horner shifts, a
-//     broadcast head, lane rotation, DPP tree, one-item-ahead prefetch, and workgroup-local
-//     dynamic block scheduling from an LDS counter.
+//   * crc_pack4k_kernel<1, 4, nt> -- fixed stride, 4-KiB, 16-B aligned blocks (BASELINE configs
+//     2/4).  One wave per block, lane l owns four 16-B pieces (16l + 1024j, so every load
+//     instruction reads 1 KiB contiguous, non-temporal) hashed as four independent slice-by-4
+//     chains, 4 blocks per wave-iteration folded in one packed tree, one barrier per 4-block
+//     group keeps the workgroup's 16 waves on 16 consecutive blocks.
+//   * crc_stream_kernel / crc_stream16_kernel -- any length / alignment (fixed stride, descriptor
+//     lists, sstable seal / verify): 4-KiB rounds of 32-B (or 16-B, nt) lane pieces with per-lane
+//     Horner shifts, a broadcast head, lane rotation, packed 4-block trees, one-item-ahead
+//     prefetch, and workgroup-local dynamic block scheduling from an LDS counter.
+//   * crc_server_kernel (crc32c_server.hip) -- the persistent scalar Extend service.
 // LDS image (crc32c_math.h): T0..T3 replicated 32x (128 KiB) so each lane reads its own bank +
 // 8 shift-operator slots (32 KiB): the whole 160 KiB of a CU; one 1024-thread workgroup per CU
 // stages it once and walks blocks persistently.  DESIGN.md §3-§6 has the measurements.
@@ -196,6 +198,16 @@ hipError_t launch_sst(const LaunchGeom& g, const uint32_t* d_tables, uint8_t* bu
   else
     hipLaunchKernelGGL((crc_stream_kernel<SstSrc, SstVerifySink, 0, true, true>), grid, block, 0, s, d_tables,
                        src, n, SstVerifySink{ok, nbad});
+  return hipGetLastError();
+}
+
+hipError_t launch_sst_masked(const LaunchGeom& g, const uint32_t* d_tables, uint8_t* buf, const pdb_block_handle* h,
+                             uint64_t n, uint32_t* out, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const dim3 grid(grid_for(g, n)), block(kThreads);
+  // the seal's CRCs into a compact array (host seal: 4 B per block back across PCIe, not the span)
+  hipLaunchKernelGGL((crc_stream_kernel<SstSrc, OutSink, 0, true, true>), grid, block, 0, s, d_tables,
+                     SstSrc{buf, h}, n, OutSink{out, PDB_CRC_MASK_OUTPUT});
   return hipGetLastError();
 }
 
