@@ -104,9 +104,14 @@ int pdb_crc32c_verify_device(const void* d_base, const pdb_blk* d_blk, uint64_t 
                              const uint32_t* d_expected, uint8_t* d_ok, uint32_t* d_nbad,
                              void* stream);
 
-/* ---- host batches (copy-inclusive: H2D + kernel + D2H on the internal stream) --------------- */
+/* ---- host batches (copy-inclusive: H2D + kernel + D2H on the internal stream) ---------------
+ * Staged in groups of at most 256 MiB of span, so the device workspace stays bounded. */
 int pdb_crc32c_batch_host(const void* base, uint64_t base_len, const pdb_blk* blk, uint64_t nblk,
                           uint32_t flags, uint32_t* out);
+/* ReadBlock's check for host blocks: ok[i] = (crc_i == expected[i]) (expected masked iff
+ * PDB_CRC_MASK_OUTPUT; ok may be NULL).  Returns the number of mismatches or a negative error. */
+int64_t pdb_crc32c_verify_host(const void* base, uint64_t base_len, const pdb_blk* blk, uint64_t nblk,
+                               uint32_t flags, const uint32_t* expected, uint8_t* ok);
 
 /* ---- sstable block trailers (table/table_builder.cc:187-205, table/format.cc:66-104) ---------
  * `buf` holds an sstable image (or any span of one) in which each handle's block is followed by
@@ -136,6 +141,8 @@ int pdb_fill_splitmix_device(void* d_dst, uint64_t nbytes, uint64_t seed, uint64
  * {requests, ticks (10 ns) from seeing a request to answering it, polls, lifetime ticks}.
  * Returns 1 if its request box is device memory, 0 if pinned host memory, or a negative error. */
 int pdb_diag_server_stats(uint64_t* out4);
+/* Set the host batches' staging group span in bytes (0 = leave); returns the previous value. */
+uint64_t pdb_diag_set_host_chunk(uint64_t bytes);
 /* Select a 4-KiB fast-path kernel variant (A/B experiments only; 0 = shipped default).
  * Returns the previous selection. */
 int pdb_diag_set_variant(int v);

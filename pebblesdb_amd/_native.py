@@ -52,11 +52,13 @@ SIGNATURES = {
     "pdb_crc32c_batch_device": (_I, [_V, _V, _U64, _U32, _V, _V]),
     "pdb_crc32c_verify_device": (_I, [_V, _V, _U64, _U32, _V, _V, _V, _V]),
     "pdb_crc32c_batch_host": (_I, [_V, _U64, _V, _U64, _U32, _V]),
+    "pdb_crc32c_verify_host": (ctypes.c_int64, [_V, _U64, _V, _U64, _U32, _V, _V]),
     "pdb_sst_seal_device": (_I, [_V, _U64, _V, _U64, _V]),
     "pdb_sst_seal_host": (_I, [_V, _U64, _V, _U64]),
     "pdb_sst_verify_host": (ctypes.c_int64, [_V, _U64, _V, _U64, _V]),
     "pdb_sst_verify_device": (_I, [_V, _U64, _V, _U64, _V, _V, _V]),
     "pdb_diag_server_stats": (_I, [_V]),
+    "pdb_diag_set_host_chunk": (_U64, [_U64]),
     "pdb_diag_read_stream": (_I, [_V, _U64, _V, _V]),
     "pdb_diag_read_pattern4k": (_I, [_V, _U64, _I, _V, _V]),
     "pdb_fill_splitmix_device": (_I, [_V, _U64, _U64, _U64, _V]),

@@ -12,6 +12,7 @@ plus the batch entry points the reference lacks (one call per many independent b
     batch(d_base, d_blocks)                       device-resident descriptor list
     verify(d_base, d_blocks, d_expected)          device-resident verify (ReadBlock's check)
     batch_host(base, blocks)                      host buffers, H2D + kernel + D2H
+    verify_host(base, blocks, expected)           host ReadBlock check over many blocks
 
 Every checksum comes from the HIP library; nothing here computes a CRC on the CPU.
 """
@@ -32,7 +33,7 @@ BLK_DTYPE = np.dtype([("off", "<u8"), ("len", "<u4"), ("init", "<u4")])  # == pd
 HANDLE_DTYPE = np.dtype([("offset", "<u8"), ("size", "<u8")])  # == pdb_block_handle
 
 __all__ = [
-    "extend", "value", "mask", "unmask", "batch_fixed", "batch", "verify", "batch_host",
+    "extend", "value", "mask", "unmask", "batch_fixed", "batch", "verify", "batch_host", "verify_host",
     "make_blocks", "blocks_to_device", "PdbError", "MASK_OUTPUT", "USE_INIT", "BLK_DTYPE",
     "HANDLE_DTYPE", "init_device", "launch_geometry", "fill_splitmix", "extend_device",
 ]
@@ -176,6 +177,22 @@ def batch_host(base, blocks: np.ndarray, *, masked: bool = False, use_init: bool
     flags = (MASK_OUTPUT if masked else 0) | (USE_INIT if use_init else 0)
     check(lib().pdb_crc32c_batch_host(p, n, blocks.ctypes.data, len(blocks), flags, out.ctypes.data))
     return out
+
+
+def verify_host(base, blocks: np.ndarray, expected, *, masked: bool = True, use_init: bool = False):
+    """(ok uint8 array, nbad) for host blocks against host expected CRCs (copy-inclusive
+    ReadBlock check, table/format.cc:96-104)."""
+    p, n, _keep = _buf(base)
+    blocks = np.ascontiguousarray(blocks, dtype=BLK_DTYPE)
+    exp = np.ascontiguousarray(expected, dtype=np.uint32)
+    if exp.size != len(blocks):
+        raise ValueError("one expected CRC per block")
+    ok = np.zeros(len(blocks), dtype=np.uint8)
+    flags = (MASK_OUTPUT if masked else 0) | (USE_INIT if use_init else 0)
+    nbad = lib().pdb_crc32c_verify_host(p, n, blocks.ctypes.data, len(blocks), flags, exp.ctypes.data,
+                                        ok.ctypes.data)
+    check(int(nbad))
+    return ok, int(nbad)
 
 
 def extend_device(init_crc: int, d_data, nbytes: int | None = None, stream=None) -> int:

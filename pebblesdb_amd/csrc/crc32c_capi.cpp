@@ -328,8 +328,19 @@ int server_call(DevState* st, uint32_t init, const uint8_t* data, uint64_t n, ui
   }
 }
 
-// Host batch over descriptors: stage [lo, hi) of the host span, the rebased descriptors and the
-// outputs in one workspace; one H2D span copy, one H2D descriptor copy, kernel, one D2H.
+// Host batches are staged in groups whose byte span is at most g_host_chunk (a block longer than
+// that forms its own group), so the device workspace stays bounded however large the host batch;
+// groups run back to back on the library's stream (copies and kernels are stream-ordered) and the
+// call synchronises once at the end.  Kernel time is ~1 % of the PCIe copy, so nothing is lost by
+// not overlapping them.
+uint64_t g_host_chunk = 256ull << 20;
+
+struct HostGroup {
+  uint64_t first, count, lo, hi;
+};
+
+// Host batch over descriptors: per group, stage [lo, hi) of the host span, the rebased
+// descriptors (and expected CRCs) in the workspace; H2D span + descriptors, kernel, D2H results.
 int host_desc(const uint8_t* base, uint64_t base_len, const pdb_blk* blk, uint64_t nblk,
               uint32_t flags, int mode, const uint32_t* expected, uint32_t* out, uint8_t* ok,
               uint64_t* nbad_out) {
@@ -338,16 +349,38 @@ int host_desc(const uint8_t* base, uint64_t base_len, const pdb_blk* blk, uint64
     return PDB_OK;
   }
   if (!base || !blk) return fail(PDB_EINVAL, "null argument");
-  uint64_t lo = UINT64_MAX, hi = 0;
+  std::vector<HostGroup> groups;
+  HostGroup g{0, 0, UINT64_MAX, 0};
   for (uint64_t i = 0; i < nblk; ++i) {
     if (blk[i].off > base_len || blk[i].len > base_len - blk[i].off)
       return fail(PDB_ERANGE, "block " + std::to_string(i) + " exceeds base_len");
-    if (blk[i].len == 0) continue;
-    lo = std::min(lo, blk[i].off);
-    hi = std::max(hi, blk[i].off + blk[i].len);
+    if (blk[i].len) {
+      const uint64_t lo = std::min(g.lo, blk[i].off & ~static_cast<uint64_t>(15));
+      const uint64_t hi = std::max(g.hi, blk[i].off + blk[i].len);
+      if (g.count && g.lo != UINT64_MAX && hi - lo > g_host_chunk) {
+        groups.push_back(g);
+        g = HostGroup{i, 0, blk[i].off & ~static_cast<uint64_t>(15), blk[i].off + blk[i].len};
+      } else {
+        g.lo = lo;
+        g.hi = hi;
+      }
+    }
+    ++g.count;
   }
-  if (lo == UINT64_MAX) lo = hi = 0;
-  lo &= ~static_cast<uint64_t>(15);  // keep the source's 16-B phase so fast loads stay aligned
+  groups.push_back(g);
+  // lo keeps the source's 16-B phase so the kernels' fast loads stay aligned
+  size_t need = 0;
+  uint64_t max_count = 0;
+  for (auto& x : groups) {
+    if (x.lo == UINT64_MAX) x.lo = x.hi = 0;
+    need = std::max<size_t>(need, x.hi - x.lo);
+    max_count = std::max(max_count, x.count);
+  }
+  const size_t off_desc = align_up(need + 16, 256);
+  const size_t off_out = align_up(off_desc + max_count * sizeof(pdb_blk), 256);
+  const size_t off_exp = align_up(off_out + max_count * sizeof(uint32_t), 256);
+  const size_t off_ok = align_up(off_exp + (mode == kModeVerify ? max_count * 4 : 0), 256);
+  const size_t off_nbad = align_up(off_ok + (mode == kModeVerify ? max_count : 0), 256);
   DevState* st;
   int rc = get_state(&st);
   if (rc) return rc;
@@ -355,47 +388,44 @@ int host_desc(const uint8_t* base, uint64_t base_len, const pdb_blk* blk, uint64
   if ((rc = server_park(st))) return rc;
   hipError_t e = hipSetDevice(st->device);
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
-  const size_t span = hi - lo;
-  const size_t off_desc = align_up(span + 16, 256);
-  const size_t off_out = align_up(off_desc + nblk * sizeof(pdb_blk), 256);
-  const size_t off_exp = align_up(off_out + nblk * sizeof(uint32_t), 256);
-  const size_t off_ok = align_up(off_exp + (mode == kModeVerify ? nblk * 4 : 0), 256);
-  const size_t off_nbad = align_up(off_ok + (mode == kModeVerify ? nblk : 0), 256);
-  rc = ensure_ws(st, off_nbad + 256);
-  if (rc) return rc;
-  std::vector<pdb_blk> rb(blk, blk + nblk);
-  for (auto& b : rb) b.off = b.len ? b.off - lo : 0;
+  if ((rc = ensure_ws(st, off_nbad + 256))) return rc;
   hipStream_t s = st->stream;
   uint8_t* ws = st->d_ws;
-  if (span && (e = hipMemcpyAsync(ws, base + lo, span, hipMemcpyHostToDevice, s)) != hipSuccess)
-    return hip_fail(e, "hipMemcpyAsync(span)");
-  if ((e = hipMemcpyAsync(ws + off_desc, rb.data(), nblk * sizeof(pdb_blk), hipMemcpyHostToDevice,
-                          s)) != hipSuccess)
-    return hip_fail(e, "hipMemcpyAsync(desc)");
   uint32_t* d_nbad = reinterpret_cast<uint32_t*>(ws + off_nbad);
-  if (mode == kModeVerify) {
-    if ((e = hipMemcpyAsync(ws + off_exp, expected, nblk * 4, hipMemcpyHostToDevice, s)) != hipSuccess)
+  if (mode == kModeVerify && (e = hipMemsetAsync(d_nbad, 0, 4, s)) != hipSuccess)
+    return hip_fail(e, "hipMemsetAsync");
+  // rebased descriptors stay alive until the final synchronisation (async H2D sources)
+  std::vector<std::vector<pdb_blk>> rbs(groups.size());
+  for (size_t k = 0; k < groups.size(); ++k) {
+    const HostGroup& x = groups[k];
+    std::vector<pdb_blk>& rb = rbs[k];
+    rb.assign(blk + x.first, blk + x.first + x.count);
+    for (auto& b : rb) b.off = b.len ? b.off - x.lo : 0;
+    if (x.hi > x.lo && (e = hipMemcpyAsync(ws, base + x.lo, x.hi - x.lo, hipMemcpyHostToDevice, s)) != hipSuccess)
+      return hip_fail(e, "hipMemcpyAsync(span)");
+    if ((e = hipMemcpyAsync(ws + off_desc, rb.data(), x.count * sizeof(pdb_blk), hipMemcpyHostToDevice, s)) !=
+        hipSuccess)
+      return hip_fail(e, "hipMemcpyAsync(desc)");
+    if (mode == kModeVerify &&
+        (e = hipMemcpyAsync(ws + off_exp, expected + x.first, x.count * 4, hipMemcpyHostToDevice, s)) != hipSuccess)
       return hip_fail(e, "hipMemcpyAsync(expected)");
-    if ((e = hipMemsetAsync(d_nbad, 0, 4, s)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
-  }
-  e = launch_desc(st->geom, st->d_tables, ws, reinterpret_cast<const pdb_blk*>(ws + off_desc), nblk,
-                  flags, mode, reinterpret_cast<const uint32_t*>(ws + off_exp),
-                  reinterpret_cast<uint32_t*>(ws + off_out), ws + off_ok, d_nbad, s);
-  if (e != hipSuccess) return hip_fail(e, "launch_desc");
-  if (mode == kModeOut) {
-    if ((e = hipMemcpyAsync(out, ws + off_out, nblk * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
-      return hip_fail(e, "hipMemcpyAsync(out)");
-  } else {
-    uint32_t nb = 0;
-    if (ok && (e = hipMemcpyAsync(ok, ws + off_ok, nblk, hipMemcpyDeviceToHost, s)) != hipSuccess)
+    e = launch_desc(st->geom, st->d_tables, ws, reinterpret_cast<const pdb_blk*>(ws + off_desc), x.count, flags,
+                    mode, reinterpret_cast<const uint32_t*>(ws + off_exp), reinterpret_cast<uint32_t*>(ws + off_out),
+                    ws + off_ok, d_nbad, s);
+    if (e != hipSuccess) return hip_fail(e, "launch_desc");
+    if (mode == kModeOut) {
+      if ((e = hipMemcpyAsync(out + x.first, ws + off_out, x.count * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
+        return hip_fail(e, "hipMemcpyAsync(out)");
+    } else if (ok && (e = hipMemcpyAsync(ok + x.first, ws + off_ok, x.count, hipMemcpyDeviceToHost, s)) !=
+                         hipSuccess) {
       return hip_fail(e, "hipMemcpyAsync(ok)");
-    if ((e = hipMemcpyAsync(&nb, d_nbad, 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
-      return hip_fail(e, "hipMemcpyAsync(nbad)");
-    if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
-    if (nbad_out) *nbad_out = nb;
-    return PDB_OK;
+    }
   }
+  uint32_t nb = 0;
+  if (mode == kModeVerify && (e = hipMemcpyAsync(&nb, d_nbad, 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
+    return hip_fail(e, "hipMemcpyAsync(nbad)");
   if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+  if (nbad_out) *nbad_out = nb;
   return PDB_OK;
 }
 
@@ -666,6 +696,21 @@ int pdb_crc32c_batch_host(const void* base, uint64_t base_len, const pdb_blk* bl
   if (nblk && !out) return fail(PDB_EINVAL, "null out");
   return host_desc(static_cast<const uint8_t*>(base), base_len, blk, nblk, flags, kModeOut, nullptr,
                    out, nullptr, nullptr);
+}
+
+int64_t pdb_crc32c_verify_host(const void* base, uint64_t base_len, const pdb_blk* blk, uint64_t nblk,
+                               uint32_t flags, const uint32_t* expected, uint8_t* ok) {
+  if (nblk && !expected) return fail(PDB_EINVAL, "null expected");
+  uint64_t nbad = 0;
+  const int rc = host_desc(static_cast<const uint8_t*>(base), base_len, blk, nblk, flags, kModeVerify, expected,
+                           nullptr, ok, &nbad);
+  return rc ? rc : static_cast<int64_t>(nbad);
+}
+
+uint64_t pdb_diag_set_host_chunk(uint64_t bytes) {
+  const uint64_t old = g_host_chunk;
+  if (bytes) g_host_chunk = bytes;
+  return old;
 }
 
 int pdb_sst_seal_device(void* d_buf, uint64_t buf_len, const pdb_block_handle* d_h, uint64_t n,

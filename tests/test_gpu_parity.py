@@ -313,3 +313,35 @@ def test_stream_variants_exact(crc, golden, oracle_lib, variant):
             assert (got == exp).all(), (stride, length, int(np.nonzero(got != exp)[0][0]))
     finally:
         lib().pdb_diag_set_variant(0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("chunk", [0, 1 << 16, 3 << 20])
+def test_host_batches_grouped_and_verify_host(crc, golden, oracle_lib, chunk):
+    """pdb_crc32c_batch_host / pdb_crc32c_verify_host over the golden Zipf and ragged batches
+    (empty blocks, unaligned offsets, blocks larger than a staging group), with the staging group
+    span forced small so one call runs many groups: CRCs equal the reference's, corrupted expected
+    values are counted and flagged exactly."""
+    from pebblesdb_amd._native import lib
+
+    prev = lib().pdb_diag_set_host_chunk(chunk)
+    try:
+        for b in golden["batches"]:
+            if b["total_bytes"] > (64 << 20):
+                continue
+            base = _materialize({"kind": "splitmix", "len": b["total_bytes"], "seed": b["seed"]})
+            use_init = b["use_init"]
+            blk = crc.make_blocks(b["off"], b["len"], b["init"] if use_init else None)
+            exp = np.array(b["crc"], dtype=np.uint64).astype(np.uint32)
+            got = crc.batch_host(base, blk, use_init=use_init)
+            assert (got == exp).all(), b["name"]
+            ok, nbad = crc.verify_host(base, blk, exp, masked=False, use_init=use_init)
+            assert nbad == 0 and ok.all(), b["name"]
+            bad = exp.copy()
+            flip = np.arange(0, len(bad), 7)
+            bad[flip] ^= 1
+            ok, nbad = crc.verify_host(base, blk, bad, masked=False, use_init=use_init)
+            assert nbad == len(flip), b["name"]
+            assert (ok[flip] == 0).all() and ok.sum() == len(bad) - len(flip), b["name"]
+    finally:
+        lib().pdb_diag_set_host_chunk(prev)
