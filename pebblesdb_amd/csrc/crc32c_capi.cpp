@@ -516,17 +516,36 @@ int host_sst(uint8_t* buf, uint64_t buf_len, const pdb_block_handle* h, uint64_t
     return PDB_OK;
   }
   if (!buf || !h) return fail(PDB_EINVAL, "null argument");
-  uint64_t lo = UINT64_MAX, hi = 0;
+  // staging groups of at most g_host_chunk bytes of span (block + trailer), as for host_desc
+  std::vector<HostGroup> groups;
+  HostGroup g{0, 0, UINT64_MAX, 0};
   for (uint64_t i = 0; i < n; ++i) {
     // block + 5-byte trailer must lie inside the buffer (table/format.cc:84-87 "truncated")
     if (h[i].offset > buf_len || h[i].size > buf_len - h[i].offset ||
         buf_len - h[i].offset - h[i].size < 5)
       return fail(PDB_ERANGE, "block handle " + std::to_string(i) + " (+trailer) exceeds buffer");
     if (h[i].size + 1 > 0xFFFFFFFFull) return fail(PDB_ERANGE, "block larger than 4 GiB");
-    lo = std::min(lo, h[i].offset);
-    hi = std::max(hi, h[i].offset + h[i].size + 5);
+    const uint64_t blo = h[i].offset & ~static_cast<uint64_t>(15), bhi = h[i].offset + h[i].size + 5;
+    const uint64_t lo = std::min(g.lo, blo), hi = std::max(g.hi, bhi);
+    if (g.count && hi - lo > g_host_chunk) {
+      groups.push_back(g);
+      g = HostGroup{i, 1, blo, bhi};
+    } else {
+      g.lo = lo;
+      g.hi = hi;
+      ++g.count;
+    }
   }
-  lo &= ~static_cast<uint64_t>(15);
+  groups.push_back(g);
+  size_t need = 0;
+  uint64_t max_count = 0;
+  for (const auto& x : groups) {
+    need = std::max<size_t>(need, x.hi - x.lo);
+    max_count = std::max(max_count, x.count);
+  }
+  const size_t off_h = align_up(need + 16, 256);
+  const size_t off_ok = align_up(off_h + max_count * sizeof(pdb_block_handle), 256);
+  const size_t off_nbad = align_up(off_ok + 4 * max_count, 256);  // ok bytes (verify) or masked CRCs (seal)
   DevState* st;
   int rc = get_state(&st);
   if (rc) return rc;
@@ -534,54 +553,52 @@ int host_sst(uint8_t* buf, uint64_t buf_len, const pdb_block_handle* h, uint64_t
   if ((rc = server_park(st))) return rc;
   hipError_t e = hipSetDevice(st->device);
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
-  const size_t span = hi - lo;
-  const size_t off_h = align_up(span + 16, 256);
-  const size_t off_ok = align_up(off_h + n * sizeof(pdb_block_handle), 256);
-  const size_t off_nbad = align_up(off_ok + 4 * n, 256);  // ok bytes (verify) or masked CRCs (seal)
-  rc = ensure_ws(st, off_nbad + 256);
-  if (rc) return rc;
-  std::vector<pdb_block_handle> rh(h, h + n);
-  for (auto& x : rh) x.offset -= lo;
+  if ((rc = ensure_ws(st, off_nbad + 256))) return rc;
   hipStream_t s = st->stream;
   uint8_t* ws = st->d_ws;
   uint32_t* d_nbad = reinterpret_cast<uint32_t*>(ws + off_nbad);
-  if ((e = hipMemcpyAsync(ws, buf + lo, span, hipMemcpyHostToDevice, s)) != hipSuccess)
-    return hip_fail(e, "hipMemcpyAsync(span)");
-  if ((e = hipMemcpyAsync(ws + off_h, rh.data(), n * sizeof(pdb_block_handle), hipMemcpyHostToDevice,
-                          s)) != hipSuccess)
-    return hip_fail(e, "hipMemcpyAsync(handles)");
-  if (seal) {
-    // Only the 4 CRC bytes of every trailer change: the kernel writes the masked CRCs into a
-    // compact array, 4 B per block come back across PCIe (not the span), and the host encodes
-    // them little-endian at offset + size + 1 (table_builder.cc:199-200).
-    uint32_t* d_crc = reinterpret_cast<uint32_t*>(ws + off_ok);
-    e = launch_sst_masked(st->geom, st->d_tables, ws, reinterpret_cast<const pdb_block_handle*>(ws + off_h), n,
-                          d_crc, s);
-    if (e != hipSuccess) return hip_fail(e, "launch_sst_masked");
-    std::vector<uint32_t> crc(n);
-    if ((e = hipMemcpyAsync(crc.data(), d_crc, n * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
-      return hip_fail(e, "hipMemcpyAsync(crcs)");
-    if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
-    for (uint64_t i = 0; i < n; ++i) {
-      uint8_t* tr = buf + h[i].offset + h[i].size + 1;
-      tr[0] = static_cast<uint8_t>(crc[i]);
-      tr[1] = static_cast<uint8_t>(crc[i] >> 8);
-      tr[2] = static_cast<uint8_t>(crc[i] >> 16);
-      tr[3] = static_cast<uint8_t>(crc[i] >> 24);
+  if (!seal && (e = hipMemsetAsync(d_nbad, 0, 4, s)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
+  // Seal: only the 4 CRC bytes of every trailer change, so the kernel writes the masked CRCs into
+  // a compact array, 4 B per block come back across PCIe (not the span), and the host encodes
+  // them little-endian at offset + size + 1 (table_builder.cc:199-200).
+  std::vector<uint32_t> crc(seal ? n : 0);
+  std::vector<std::vector<pdb_block_handle>> rhs(groups.size());  // async H2D sources
+  for (size_t k = 0; k < groups.size(); ++k) {
+    const HostGroup& x = groups[k];
+    std::vector<pdb_block_handle>& rh = rhs[k];
+    rh.assign(h + x.first, h + x.first + x.count);
+    for (auto& y : rh) y.offset -= x.lo;
+    if ((e = hipMemcpyAsync(ws, buf + x.lo, x.hi - x.lo, hipMemcpyHostToDevice, s)) != hipSuccess)
+      return hip_fail(e, "hipMemcpyAsync(span)");
+    if ((e = hipMemcpyAsync(ws + off_h, rh.data(), x.count * sizeof(pdb_block_handle), hipMemcpyHostToDevice,
+                            s)) != hipSuccess)
+      return hip_fail(e, "hipMemcpyAsync(handles)");
+    const pdb_block_handle* d_h = reinterpret_cast<const pdb_block_handle*>(ws + off_h);
+    if (seal) {
+      uint32_t* d_crc = reinterpret_cast<uint32_t*>(ws + off_ok);
+      if ((e = launch_sst_masked(st->geom, st->d_tables, ws, d_h, x.count, d_crc, s)) != hipSuccess)
+        return hip_fail(e, "launch_sst_masked");
+      if ((e = hipMemcpyAsync(crc.data() + x.first, d_crc, x.count * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
+        return hip_fail(e, "hipMemcpyAsync(crcs)");
+    } else {
+      if ((e = launch_sst(st->geom, st->d_tables, ws, x.hi - x.lo, d_h, x.count, false, ws + off_ok, d_nbad, s)) !=
+          hipSuccess)
+        return hip_fail(e, "launch_sst");
+      if (ok && (e = hipMemcpyAsync(ok + x.first, ws + off_ok, x.count, hipMemcpyDeviceToHost, s)) != hipSuccess)
+        return hip_fail(e, "hipMemcpyAsync(ok)");
     }
-    if (nbad_out) *nbad_out = 0;
-    return PDB_OK;
   }
-  if ((e = hipMemsetAsync(d_nbad, 0, 4, s)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
-  e = launch_sst(st->geom, st->d_tables, ws, span, reinterpret_cast<const pdb_block_handle*>(ws + off_h),
-                 n, false, ws + off_ok, d_nbad, s);
-  if (e != hipSuccess) return hip_fail(e, "launch_sst");
   uint32_t nb = 0;
-  if (ok && (e = hipMemcpyAsync(ok, ws + off_ok, n, hipMemcpyDeviceToHost, s)) != hipSuccess)
-    return hip_fail(e, "hipMemcpyAsync(ok)");
-  if ((e = hipMemcpyAsync(&nb, d_nbad, 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
+  if (!seal && (e = hipMemcpyAsync(&nb, d_nbad, 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
     return hip_fail(e, "hipMemcpyAsync(nbad)");
   if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+  for (uint64_t i = 0; i < crc.size(); ++i) {
+    uint8_t* tr = buf + h[i].offset + h[i].size + 1;
+    tr[0] = static_cast<uint8_t>(crc[i]);
+    tr[1] = static_cast<uint8_t>(crc[i] >> 8);
+    tr[2] = static_cast<uint8_t>(crc[i] >> 16);
+    tr[3] = static_cast<uint8_t>(crc[i] >> 24);
+  }
   if (nbad_out) *nbad_out = nb;
   return PDB_OK;
 }
