@@ -304,7 +304,10 @@ __device__ __forceinline__ uint32_t partial4k(const char* lds, const LaneTabs& l
 
 // kPair: the wave hashes blocks two at a time (8 independent chains, next pair's 8 KiB in flight)
 // -- the ILP that lets 8 waves per CU (kWaves = 8, the nt loads' best shape) hide LDS latency.
-template <int kSync, int kNP = 2, bool kNT = false, int kWaves = kWavesPerWg, bool kPair = false>
+// kXcd: workgroups are dispatched to the 8 XCDs round-robin (blockIdx.x % 8); kXcd renumbers
+// them so each XCD's CUs own consecutive 64-KiB block windows (A/B diagnostics).
+template <int kSync, int kNP = 2, bool kNT = false, int kWaves = kWavesPerWg, bool kPair = false,
+          bool kXcd = false>
 __global__ __launch_bounds__(kWaves * 64) void crc_pack4k_kernel(
     const uint32_t* __restrict__ tabs, const uint8_t* __restrict__ base, uint64_t stride,
     uint64_t nblk, uint32_t flags, uint32_t init, uint32_t* __restrict__ out) {
@@ -313,7 +316,9 @@ __global__ __launch_bounds__(kWaves * 64) void crc_pack4k_kernel(
   char* lds = reinterpret_cast<char*>(lds_words);
   const uint32_t u = threadIdx.x & 63u;
   const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWaves;
-  const uint64_t w = static_cast<uint64_t>(blockIdx.x) * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t wg = (kXcd && (gridDim.x & 7u) == 0) ? (blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3)
+                                                       : blockIdx.x;
+  const uint64_t w = static_cast<uint64_t>(wg) * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   u32x4 buf[4], buf2[4];
   load4k<kNP, kNT>(buf, base, stride, w < nblk ? w : nblk - 1, u);
   if constexpr (kPair) load4k<kNP, kNT>(buf2, base, stride, w + nw < nblk ? w + nw : nblk - 1, u);
@@ -329,7 +334,7 @@ __global__ __launch_bounds__(kWaves * 64) void crc_pack4k_kernel(
   uint32_t res = 0, it = 0;
   // kSync: the workgroup's 16 waves (16 consecutive blocks) stay in lock step, one barrier per
   // 4-block group, so their outstanding loads cover one compact 64-KiB span at a time.
-  const uint64_t wg_first = static_cast<uint64_t>(blockIdx.x) * kWaves;
+  const uint64_t wg_first = static_cast<uint64_t>(wg) * kWaves;
   if (kSync > 0 && wg_first >= nblk) return;
   uint32_t grp = 0;
   uint64_t win0 = w;

@@ -451,6 +451,9 @@ hipError_t launch_fixed_variant(int v, const LaunchGeom& g, const uint32_t* d_ta
                                 d_tables, base, stride, nblk, flags, init, out); break;
     case 25: hipLaunchKernelGGL((crc_pack4k_kernel<2, 4, true, 12>), dim3(grid_forw(g, nblk, 12)), dim3(768), 0, s,
                                 d_tables, base, stride, nblk, flags, init, out); break;
+    // XCD-contiguous workgroup numbering (lock-step / free-running)
+    case 26: PDB_K((crc_pack4k_kernel<1, 4, true, 16, false, true>)); break;
+    case 27: PDB_K((crc_pack4k_kernel<0, 4, true, 16, false, true>)); break;
     default: PDB_K((crc_pack4k_kernel<1, 4, true>)); break;
   }
 #undef PDB_FAST
