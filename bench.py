@@ -38,7 +38,10 @@ def parse():
     # 40: the first ~20-30 launches of a cold GPU run slower (clock / power settling; see
     # DESIGN.md §6), so the default warmup covers them
     ap.add_argument("--warmup", type=int, default=40)
-    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "sstable"])
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "sstable", "sst_verify", "sst_seal", "wal"],
+                    help="c2 (default, the headline) / c3: BASELINE configs; sstable: the C2 blocks in "
+                         "sstable layout; sst_verify / sst_seal: SURVEY §8(f) rows 1-2 on a device sstable "
+                         "image of ~4.17-KiB blocks; wal: row 3, the log record CRC over 32-KiB log blocks")
     ap.add_argument("--nblk", type=int, default=1 << 20, help="blocks per GPU (c2/sstable)")
     ap.add_argument("--c3-bytes", type=int, default=16 << 30, help="bytes per GPU for c3 (Zipf)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -49,6 +52,27 @@ def parse():
                     help="process-group backend (nccl = RCCL over xGMI; gloo only to rehearse the "
                          "multi-rank flow with ranks sharing one GPU)")
     return ap.parse_args()
+
+
+def wal_layout(total_bytes: int, payload: int, block: int = 32768):
+    """(offsets, lengths) of the CRC'd spans (type byte + fragment) of a log image holding
+    `payload`-byte records back to back: a record that does not fit the rest of a 32-KiB block is
+    fragmented (FIRST/MIDDLE/LAST), and a block tail < 7 B is zero padding (db/log_writer.cc:39-81)."""
+    offs, lens = [], []
+    pos, left, end = 0, payload, block
+    while pos < total_bytes:
+        avail = end - pos
+        if avail < 7:
+            pos, end = end, end + block
+            continue
+        frag = min(left, avail - 7)
+        offs.append(pos + 6)
+        lens.append(frag + 1)
+        pos += 7 + frag
+        left = left - frag or payload
+        if pos == end:
+            end += block
+    return np.asarray(offs, dtype=np.int64), np.asarray(lens, dtype=np.int64)
 
 
 def zipf_kib_sizes(n: int, seed: int, kmax: int = 64) -> np.ndarray:
@@ -120,6 +144,62 @@ def main():
 
         workload = {"workload": "sstable layout: 4096 B contents + type byte, stride 4101 (unaligned)",
                     "block_bytes": L, "blocks_per_gpu": nblk, "bytes_per_gpu": hashed}
+    elif args.workload in ("sst_verify", "sst_seal"):
+        # sstable image: contents of 4166..4174 B (db_bench data blocks flush just past the 4-KiB
+        # block_size: 4171-4175 B with the type byte), type 0, 5-B trailer
+        from pebblesdb_amd import table as T
+        from pebblesdb_amd._native import check, lib
+
+        nblk = hi - lo
+        rng = np.random.Generator(np.random.PCG64(301 + rank))
+        sizes = rng.integers(4166, 4175, size=nblk).astype(np.int64)
+        offs = np.concatenate([[0], np.cumsum(sizes + 5)[:-1]])
+        total = int(offs[-1] + sizes[-1] + 5)
+        data = torch.empty(total, dtype=torch.uint8, device=dev)
+        crc32c.fill_splitmix(data, 301 + rank)
+        data[torch.from_numpy(offs + sizes).to(dev)] = 0  # kNoCompression type bytes
+        h = np.zeros(nblk, dtype=crc32c.HANDLE_DTYPE)
+        h["offset"], h["size"] = offs, sizes
+        d_h = T.handles_to_device(h, dev)
+        T.seal_device(data, d_h)  # untimed: a sealed image, so verification passes
+        ok = torch.empty(nblk, dtype=torch.uint8, device=dev)
+        nbad = torch.zeros(1, dtype=torch.int32, device=dev)
+        L = stride = None
+        hashed = int((sizes + 1).sum())  # contents || type under the CRC
+        out = torch.zeros(1, dtype=torch.int32, device=dev)
+        sp = int(stream.cuda_stream)
+        if args.workload == "sst_verify":
+            algo_bytes_per_blk = None  # per block: size + 5 read, 16 B handle, 1 B ok
+
+            def step():
+                check(lib().pdb_sst_verify_device(data.data_ptr(), total, d_h.data_ptr(), nblk, ok.data_ptr(),
+                                                  nbad.data_ptr(), sp))
+        else:
+            def step():
+                check(lib().pdb_sst_seal_device(data.data_ptr(), total, d_h.data_ptr(), nblk, sp))
+
+        workload = {"workload": f"{args.workload}: sstable image in HBM, 1M blocks of 4166-4174 B + type + "
+                                "5-B trailer, pdb_sst_" + args.workload.split("_")[1] + "_device",
+                    "blocks_per_gpu": nblk, "bytes_per_gpu": hashed}
+    elif args.workload == "wal":
+        # log file image: 32-KiB log blocks of physical records [crc 4][len 2][type 1][payload]
+        # (db/log_format.h:27-30); fillseq-like 1055-B logical records (1 KiB value + key + batch
+        # header) fragmented at block ends; the CRC covers type || fragment (log_writer.cc:111-121)
+        offs, lens = wal_layout(args.nblk * 4096, 1055)
+        nblk = len(offs)
+        total = int(offs[-1] + lens[-1])
+        data = torch.empty(total, dtype=torch.uint8, device=dev)
+        crc32c.fill_splitmix(data, 305 + rank)
+        d_blk = crc32c.blocks_to_device(crc32c.make_blocks(offs, lens), dev)
+        L = stride = None
+        hashed = int(lens.sum())
+        out = torch.empty(nblk, dtype=torch.int32, device=dev)
+
+        def step():
+            crc32c.batch(data, d_blk, out=out)
+
+        workload = {"workload": "wal: 4 GiB log image, 32-KiB blocks, 1055-B records -> type||payload "
+                                "fragments (descriptor list)", "blocks_per_gpu": nblk, "bytes_per_gpu": hashed}
     else:
         # c3: Zipf 1..64 KiB blocks packed back to back, args.c3_bytes per GPU
         sizes = zipf_kib_sizes(int(args.c3_bytes / (13.5 * 1024) * 1.1) + 16, 301 + rank)
@@ -142,7 +222,11 @@ def main():
 
         workload = {"workload": "c3: Zipf 1-64 KiB blocks, packed, descriptor list",
                     "blocks_per_gpu": nblk, "bytes_per_gpu": hashed}
-    algo_bytes = hashed + 4 * nblk + (16 * nblk if args.workload == "c3" else 0)
+    algo_bytes = hashed + 4 * nblk + (16 * nblk if args.workload in ("c3", "wal") else 0)
+    if args.workload == "sst_verify":  # + the 4-B stored trailer read, 16-B handle, 1-B ok written
+        algo_bytes = hashed + nblk * (4 + 16 + 1)
+    elif args.workload == "sst_seal":  # + 4-B trailer written, 16-B handle
+        algo_bytes = hashed + nblk * (4 + 16)
 
     # ---- warmup + timed region -------------------------------------------------------------
     for _ in range(args.warmup):
@@ -192,11 +276,12 @@ def main():
     if rank == 0:
         if args.diag:
             extra["diag"] = diag(crc32c, torch, dev, data, stream)
-        if not args.no_copy_inclusive and args.workload != "c3":
+        if not args.no_copy_inclusive and args.workload in ("c2", "sstable"):
             extra["copy_inclusive"] = copy_inclusive(crc32c, data, L, stride, min(nblk, 1 << 18))
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(data, L, stride, nblk, args, d_blk if args.workload == "c3" else None)
+            if args.workload in ("c2", "sstable", "c3", "wal"):
+                cpu = cpu_baseline(data, L, stride, nblk, args, d_blk if args.workload in ("c3", "wal") else None)
 
     if rank == 0:
         traffic = pmc_traffic(args.workload)
@@ -225,7 +310,10 @@ def main():
                 "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "kernel": {"c2": "crc_pack4k_kernel<1,4,nt>", "sstable": "crc_stream_kernel<FixedSrc,OutSink,0,dyn,pack>",
-                           "c3": "crc_stream16_kernel<DescSrc,OutSink,dyn,nt,pack>"}[args.workload],
+                           "c3": "crc_stream16_kernel<DescSrc,OutSink,dyn,nt,pack>",
+                           "wal": "crc_stream16_kernel<DescSrc,OutSink,dyn,nt,pack>",
+                           "sst_verify": "crc_stream_kernel<SstSrc,SstVerifySink,0,dyn,pack>",
+                           "sst_seal": "crc_stream_kernel<SstSrc,SealSink,0,dyn,pack>"}[args.workload],
                 "algorithmic_bytes_per_launch": algo_bytes,
                 "kernel_avg_ms": round(kern_avg_ms, 4),
                 "kernel_min_ms": round(float(np.min(kern_ms)), 4),

@@ -65,6 +65,20 @@ __device__ __forceinline__ uint32_t step1(const char* lds, const LaneTabs& lt, u
   return lds_u32(lds, __builtin_amdgcn_perm(lt.t0, c ^ b, sel_byte(0))) ^ (c >> 8);
 }
 
+// k = 1..3 bytes (low bytes of lb) in one step: x = c ^ lb, c' = XOR_j T_{k-1-j}[x_j] ^ (x >> 8k)
+// -- the slice-by-k step, k lookups in parallel instead of k dependent byte steps.
+__device__ __forceinline__ uint32_t stepk(const char* lds, const LaneTabs& lt, uint32_t c, uint32_t lb,
+                                          uint32_t k) {
+  const uint32_t x = c ^ lb;
+  if (k == 1) return lds_u32(lds, __builtin_amdgcn_perm(lt.t0, x, sel_byte(0))) ^ (x >> 8);
+  if (k == 2)
+    return lds_u32(lds, __builtin_amdgcn_perm(lt.t1, x, sel_byte(0))) ^
+           lds_u32(lds, __builtin_amdgcn_perm(lt.t0, x, sel_byte(1))) ^ (x >> 16);
+  return xor3(lds_u32(lds, __builtin_amdgcn_perm(lt.t2, x, sel_byte(0))),
+              lds_u32(lds, __builtin_amdgcn_perm(lt.t1, x, sel_byte(1))),
+              lds_u32(lds, __builtin_amdgcn_perm(lt.t0, x, sel_byte(2)))) ^ (x >> 24);
+}
+
 // shift(c, D) through operator `op` (4 x 256 entries, one LDS copy).
 __device__ __forceinline__ uint32_t shift_op(const char* lds, uint32_t op, uint32_t c) {
   const uint32_t base = PDB_MAIN_BYTES + op * 4096u;
@@ -408,13 +422,24 @@ struct FixedSrc {
   __device__ __forceinline__ BlkDesc get(uint64_t i) const { return {base + i * stride, len, init_raw}; }
 };
 
+// Descriptor fields are loaded by every lane from one address, so the compiler sees per-lane
+// (VGPR) values; readfirstlane makes them wave-uniform SGPRs, which keeps the block geometry
+// (rounds, chains, head) on scalar branches instead of exec-masked divergent code.
+__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
+  const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v)));
+  const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32)));
+  return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+
 struct DescSrc {
   const uint8_t* base;
   const pdb_blk* blk;
   uint32_t flags;
   __device__ __forceinline__ BlkDesc get(uint64_t i) const {
     const pdb_blk d = blk[i];
-    return {base + d.off, d.len, (flags & PDB_CRC_USE_INIT) ? ~d.init : 0xFFFFFFFFu};
+    const uint32_t init = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(d.init));
+    const uint32_t len = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(d.len));
+    return {base + uniform64(d.off), len, (flags & PDB_CRC_USE_INIT) ? ~init : 0xFFFFFFFFu};
   }
 };
 
@@ -424,7 +449,7 @@ struct SstSrc {
   const pdb_block_handle* h;
   __device__ __forceinline__ BlkDesc get(uint64_t i) const {
     const pdb_block_handle x = h[i];
-    return {buf + x.offset, static_cast<uint32_t>(x.size + 1), 0xFFFFFFFFu};
+    return {buf + uniform64(x.offset), static_cast<uint32_t>(uniform64(x.size)) + 1u, 0xFFFFFFFFu};
   }
 };
 
@@ -473,6 +498,21 @@ struct SstVerifySink {
     if (!good && nbad) atomicAdd(nbad, 1u);
   }
 };
+
+// Rounds of a block of K 32-B pieces: 128 pieces (4 KiB) per round, and the block's last round
+// may take up to 64 more as a third chain (piece u + 128 on lane u), so a block of 4 KiB + a few
+// bytes -- every real sstable data block: 4171-4175 B with the type byte -- is one round, not a
+// full second round for its last 2 pieces.
+__device__ __forceinline__ uint32_t rounds32(uint32_t K) {
+  const uint32_t r = (K + 63u) >> 7;
+  return r ? r : 1u;
+}
+
+// Same for the 16-B-piece kernels: 256 pieces per round, up to 64 more as a fifth chain.
+__device__ __forceinline__ uint32_t rounds16(uint32_t K) {
+  const uint32_t r = (K + 191u) >> 8;
+  return r ? r : 1u;
+}
 
 // Raw (possibly misaligned) 32-B piece: e[0..8] are the aligned dwords covering [q - s, q - s + 36).
 struct RawPiece {
@@ -545,15 +585,16 @@ __global__ __launch_bounds__(kThreads) void crc_stream_kernel(const uint32_t* __
   // the item being loaded: block d, round k
   BlkDesc d{};
   uint32_t k = 0;
-  RawPiece na, nb;
+  RawPiece na, nb, nc;
   uint32_t nhw = 0, nhb = 0;
   auto issue = [&](const BlkDesc& bd, uint32_t kk) {
     const uint32_t t = bd.n & 31u, K = bd.n >> 5;
     const uint8_t* q0 = bd.p + t;
     const uint32_t s = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(q0) & 3u);
-    const uint32_t ca = u + (kk << 7), cb = ca + 64u;
+    const uint32_t ca = u + (kk << 7), cb = ca + 64u, cc = ca + 128u;
     if (ca < K) issue_piece(na, q0 + static_cast<uint64_t>(ca) * 32u, s);
     if (cb < K) issue_piece(nb, q0 + static_cast<uint64_t>(cb) * 32u, s);
+    if (kk + 1 >= rounds32(K) && cc < K) issue_piece(nc, q0 + static_cast<uint64_t>(cc) * 32u, s);
     if (kk == 0) {
       const uint32_t lead = t & 3u, nh = t >> 2;
       if (u >= 1 && u <= nh) nhw = ld32u(bd.p + lead + 4u * (u - 1));
@@ -569,6 +610,12 @@ __global__ __launch_bounds__(kThreads) void crc_stream_kernel(const uint32_t* __
     d = src.get(i);
     issue(d, 0);
   }
+  // descriptor lookahead: the block after the one being loaded, its descriptor load in flight
+  // (a descriptor fetched only when its block is due would put one full memory latency in front
+  // of every block's loads)
+  uint64_t ia = active ? next_block(i) : nend;
+  BlkDesc da{};
+  if (ia < nend) da = src.get(ia);
   uint32_t acc = 0;
   // kPack: parked blocks
   uint32_t park0 = 0, park1 = 0, park2 = 0, park3 = 0, npark = 0;
@@ -591,7 +638,7 @@ __global__ __launch_bounds__(kThreads) void crc_stream_kernel(const uint32_t* __
     const uint64_t wg_first = static_cast<uint64_t>(blockIdx.x) * kWavesPerWg;
     if (wg_first >= nblk) return;
     const uint32_t n0 = src.get(wg_first).n, K0 = n0 >> 5;
-    items_left = ((nblk - wg_first + nw - 1) / nw) * (K0 ? (K0 + 127u) >> 7 : 1u);
+    items_left = ((nblk - wg_first + nw - 1) / nw) * rounds32(K0);
   }
   for (;;) {
     if constexpr (kSync > 0) {
@@ -599,16 +646,20 @@ __global__ __launch_bounds__(kThreads) void crc_stream_kernel(const uint32_t* __
       if ((item++ % kSync) == 0) __syncthreads();
       if (!active) continue;
     }
-    const RawPiece ca_ = na, cb_ = nb;
+    const RawPiece ca_ = na, cb_ = nb, cc_ = nc;
     const uint32_t chw = nhw, chb = nhb;
     const BlkDesc cd = d;
     const uint32_t ck = k;
     const uint32_t K = cd.n >> 5;
-    const uint32_t R = K ? (K + 127u) >> 7 : 1u;
+    const uint32_t R = rounds32(K);
     const bool last_round = ck + 1 >= R;
-    const uint64_t ni = last_round ? next_block(i) : i;
+    const uint64_t ni = last_round ? ia : i;
     const bool have_next = ni < nend;
-    if (last_round && have_next) d = src.get(ni);
+    if (last_round && have_next) {
+      d = da;
+      ia = next_block(ni);
+      if (ia < nend) da = src.get(ia);
+    }
     k = last_round ? 0 : ck + 1;
     if (have_next) issue(d, k);
 
@@ -616,20 +667,33 @@ __global__ __launch_bounds__(kThreads) void crc_stream_kernel(const uint32_t* __
       const uint32_t t = cd.n & 31u, lead = t & 3u, nh = t >> 2;
       uint32_t h = cd.init_raw;
       const uint32_t lb = __builtin_amdgcn_readfirstlane(chb);
-      for (uint32_t j = 0; j < lead; ++j) h = step1(lds, lt, h, (lb >> (8 * j)) & 0xffu);
+      if (lead) h = stepk(lds, lt, h, lb, lead);  // the 1-3 leading bytes in one table step
       for (uint32_t j = 0; j < nh; ++j) h = step4(lds, lt, h, __builtin_amdgcn_readlane(chw, j + 1));
       acc = (u == 0) ? h : 0u;
     }
     const uint32_t s = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(cd.p + (cd.n & 31u)) & 3u);
-    const uint32_t ca = u + (ck << 7), cb = ca + 64u;
-    if (cb < K) {
+    const uint32_t ca = u + (ck << 7), cb = ca + 64u, cc = ca + 128u;
+    // Every chain the round needs runs once for the whole wave (wave-uniform conditions: is there
+    // any lane with a second / third piece?) and lanes without that piece discard it by select:
+    // per-lane if/else would serialise the 1-, 2- and 3-chain cases of a partial round.
+    {
+      const uint32_t c0 = ck << 7;
+      const bool anyb = K > c0 + 64u, anyc = last_round && K > c0 + 128u;  // wave-uniform
       const uint32_t start = ck ? shift_op(lds, PDB_SLOT_HORNER, acc) : acc;
       const uint32_t xa = chain_piece(lds, lt, start, ca_, s);
-      const uint32_t xb = chain_piece(lds, lt, 0u, cb_, s);
-      acc = shift_op_x(lds, 7, xa, xb);
-    } else if (ca < K) {
-      const uint32_t start = ck ? shift_op(lds, PDB_SLOT_HORNER, acc) : acc;
-      acc = chain_piece(lds, lt, start, ca_, s);
+      uint32_t xb = 0, xc = 0;
+      if (anyb) xb = chain_piece(lds, lt, 0u, cb_, s);
+      if (anyc) xc = chain_piece(lds, lt, 0u, cc_, s);
+      uint32_t v = ca < K ? xa : acc;  // a lane with no piece this round keeps its partial
+      if (anyb) {
+        const uint32_t vb = shift_op_x(lds, 7, xa, xb);
+        v = cb < K ? vb : v;
+      }
+      if (anyc) {
+        const uint32_t vc = shift_op_x(lds, 7, v, xc);
+        v = (cc < K) ? vc : v;
+      }
+      acc = v;
     }
     if (last_round) {
       if constexpr (kPack) {
@@ -735,7 +799,7 @@ __global__ __launch_bounds__(kThreads) void crc_stream16_kernel(const uint32_t* 
   // the item being loaded: block d, round k
   BlkDesc d{};
   uint32_t k = 0;
-  u32x4 ne[4] = {};
+  u32x4 ne[5] = {};
   uint32_t nxt = 0, nhw = 0, nhb = 0;
   auto issue = [&](const BlkDesc& bd, uint32_t kk) {
     const uint32_t t = bd.n & 15u, K = bd.n >> 4;
@@ -743,17 +807,20 @@ __global__ __launch_bounds__(kThreads) void crc_stream16_kernel(const uint32_t* 
     const uint32_t s = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(q0) & 3u);
     const uint8_t* qa = q0 - s;
     const uint32_t c0 = kk << 8;
+    const bool last = kk + 1 >= rounds16(K);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < 5; ++j) {
       const uint32_t c = c0 + 64u * j + u;
-      if (c < K) ne[j] = ldq<kNT>(qa + 16ull * c);
+      if ((j < 4 || last) && c < K) ne[j] = ldq<kNT>(qa + 16ull * c);  // chain 4: last round only
     }
     if (s && K) {
-      // the dword after a piece whose right neighbour is not in this round's registers
+      // the dword after a piece whose right neighbour is not in this round's registers: lane 63's
+      // chain-3 piece in a non-last round (its neighbour opens the next round), and the block's
+      // last piece (always in the last round)
       const uint32_t cl = K - 1;
       uint32_t cx = 0xFFFFFFFFu;
-      if (u == 63u && c0 + 255u < K) cx = c0 + 255u;
-      if ((cl >> 8) == kk && (cl & 63u) == u) cx = cl;
+      if (u == 63u && !last) cx = c0 + 255u;
+      if (last && (cl & 63u) == u) cx = cl;
       if (cx != 0xFFFFFFFFu) nxt = *reinterpret_cast<const uint32_t*>(qa + 16ull * (cx + 1u));
     }
     if (kk == 0) {
@@ -769,6 +836,10 @@ __global__ __launch_bounds__(kThreads) void crc_stream16_kernel(const uint32_t* 
   };
   d = src.get(i);
   issue(d, 0);
+  // descriptor lookahead (as in crc_stream_kernel)
+  uint64_t ia = next_block(i);
+  BlkDesc da{};
+  if (ia < nend) da = src.get(ia);
   uint32_t acc = 0;
   uint32_t park0 = 0, park1 = 0, park2 = 0, park3 = 0, npark = 0;
   uint64_t pid0 = 0, pid1 = 0, pid2 = 0, pid3 = 0;
@@ -784,16 +855,20 @@ __global__ __launch_bounds__(kThreads) void crc_stream16_kernel(const uint32_t* 
     park0 = park1 = park2 = park3 = 0;
   };
   for (;;) {
-    const u32x4 e0 = ne[0], e1 = ne[1], e2 = ne[2], e3 = ne[3];
+    const u32x4 e0 = ne[0], e1 = ne[1], e2 = ne[2], e3 = ne[3], e4 = ne[4];
     const uint32_t cx = nxt, chw = nhw, chb = nhb;
     const BlkDesc cd = d;
     const uint32_t ck = k;
     const uint32_t K = cd.n >> 4;
-    const uint32_t R = K ? (K + 255u) >> 8 : 1u;
+    const uint32_t R = rounds16(K);
     const bool last_round = ck + 1 >= R;
-    const uint64_t ni = last_round ? next_block(i) : i;
+    const uint64_t ni = last_round ? ia : i;
     const bool have_next = ni < nend;
-    if (last_round && have_next) d = src.get(ni);
+    if (last_round && have_next) {
+      d = da;
+      ia = next_block(ni);
+      if (ia < nend) da = src.get(ia);
+    }
     k = last_round ? 0 : ck + 1;
     if (have_next) issue(d, k);
 
@@ -801,31 +876,35 @@ __global__ __launch_bounds__(kThreads) void crc_stream16_kernel(const uint32_t* 
       const uint32_t t = cd.n & 15u, lead = t & 3u, nh = t >> 2;
       uint32_t h = cd.init_raw;
       const uint32_t lb = __builtin_amdgcn_readfirstlane(chb);
-      for (uint32_t j = 0; j < lead; ++j) h = step1(lds, lt, h, (lb >> (8 * j)) & 0xffu);
+      if (lead) h = stepk(lds, lt, h, lb, lead);  // the 1-3 leading bytes in one table step
       for (uint32_t j = 0; j < nh; ++j) h = step4(lds, lt, h, __builtin_amdgcn_readlane(chw, j + 1));
       acc = (u == 0) ? h : 0u;
     }
     const uint32_t c0 = ck << 8;
     const uint32_t rem = K - c0;  // pieces left from this round on (>= 1 unless K == 0)
-    const uint32_t J = rem >= 256u ? 4u : (rem > u ? ((rem - u - 1u) >> 6) + 1u : 0u);
+    // chains this lane runs: 4 in a full round; the last round holds up to 256 + 64 pieces
+    const uint32_t J = !last_round ? 4u : (rem > u ? ((rem - u - 1u) >> 6) + 1u : 0u);
     // neighbour dwords for misaligned pieces, computed with every lane active (DPP sources)
     const uint32_t s = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(cd.p + (cd.n & 15u)) & 3u);
-    uint32_t n0 = 0, n1 = 0, n2 = 0, n3 = 0;
+    uint32_t n0 = 0, n1 = 0, n2 = 0, n3 = 0, n4 = 0;
     if (s) {  // uniform branch
       // lane u+1's first dword (wave_shl:1); lane 63 keeps `old` = lane 0 of the next chain, or
-      // for chain 3 the dword it loaded itself
+      // for chain 3 of a non-last round the dword it loaded itself
+      const bool five = last_round && rem > 256u;  // a fifth chain holds piece c0 + 256
       n0 = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(e1.x, 0), e0.x, 0x130, 0xF, 0xF, false);
       n1 = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(e2.x, 0), e1.x, 0x130, 0xF, 0xF, false);
       n2 = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(e3.x, 0), e2.x, 0x130, 0xF, 0xF, false);
-      n3 = __builtin_amdgcn_update_dpp(cx, e3.x, 0x130, 0xF, 0xF, false);
+      n3 = __builtin_amdgcn_update_dpp(five ? __builtin_amdgcn_readlane(e4.x, 0) : cx, e3.x, 0x130, 0xF, 0xF, false);
+      n4 = __builtin_amdgcn_update_dpp(cx, e4.x, 0x130, 0xF, 0xF, false);
       // the block's last piece takes the dword its lane loaded itself
       const uint32_t cl = K - 1u;
-      if (K && (cl >> 8) == ck && (cl & 63u) == u) {
-        const uint32_t jl = (cl >> 6) & 3u;
+      if (K && last_round && (cl & 63u) == u) {
+        const uint32_t jl = (cl - c0) >> 6;
         n0 = jl == 0 ? cx : n0;
         n1 = jl == 1 ? cx : n1;
         n2 = jl == 2 ? cx : n2;
         n3 = jl == 3 ? cx : n3;
+        n4 = jl == 4 ? cx : n4;
       }
     }
     if (J) {
@@ -834,10 +913,13 @@ __global__ __launch_bounds__(kThreads) void crc_stream16_kernel(const uint32_t* 
       const uint32_t x1 = chain16(lds, lt, 0u, e1, n1, s);
       const uint32_t x2 = chain16(lds, lt, 0u, e2, n2, s);
       const uint32_t x3 = chain16(lds, lt, 0u, e3, n3, s);
+      // the fifth chain runs once for the wave when any lane has one (wave-uniform condition)
+      const uint32_t x4 = (last_round && rem > 256u) ? chain16(lds, lt, 0u, e4, n4, s) : 0u;
       uint32_t a = x0;
       if (J > 1) a = shift_op_x(lds, 7, a, x1);
       if (J > 2) a = shift_op_x(lds, 7, a, x2);
       if (J > 3) a = shift_op_x(lds, 7, a, x3);
+      if (J > 4) a = shift_op_x(lds, 7, a, x4);
       acc = a;
     }
     if (last_round) {

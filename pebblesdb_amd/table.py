@@ -250,3 +250,48 @@ def verify_table(image) -> tuple[TableLayout, np.ndarray]:
     ONE GPU batch.  Returns (layout, ok flags in all_handles() order)."""
     lay = table_layout(image, verify_checksums=False)
     return lay, verify_blocks(image, lay.all_handles())
+
+
+# ---- device-resident sstable images (pdb_sst_seal_device / pdb_sst_verify_device) -------------
+# The same two hooks on an image already in HBM (a compaction output being assembled on the GPU,
+# or a table read in bulk): handles are a device tensor of pdb_block_handle {u64 offset; u64
+# size} (16 B each); everything is stream-ordered and capturable.
+def handles_to_device(handles, device=None):
+    """BlockHandles (or (offset, size) pairs, or a HANDLE_DTYPE array) -> uint8 device tensor."""
+    import torch
+
+    h = handles if isinstance(handles, np.ndarray) else _handles_array(handles)
+    raw = np.ascontiguousarray(h, dtype=HANDLE_DTYPE).view(np.uint8)
+    return torch.from_numpy(raw.copy()).to(device or "cuda")
+
+
+def _dev(t) -> int:
+    if not t.is_cuda or not t.is_contiguous():
+        raise ValueError("expected a contiguous device tensor")
+    return int(t.data_ptr())
+
+
+def _stream(stream) -> int:
+    import torch
+
+    return int((stream if stream is not None else torch.cuda.current_stream()).cuda_stream)
+
+
+def seal_device(d_image, d_handles, stream=None) -> None:
+    """WriteRawBlock's trailer for every handle of a device image: Mask(crc32c(contents||type))
+    little-endian at offset+size+1 (the type byte at offset+size is input)."""
+    n = d_handles.numel() * d_handles.element_size() // 16
+    check(lib().pdb_sst_seal_device(_dev(d_image), d_image.numel() * d_image.element_size(), _dev(d_handles), n,
+                                    _stream(stream)))
+
+
+def verify_device(d_image, d_handles, stream=None):
+    """ReadBlock's check for every handle of a device image -> (ok uint8 tensor, nbad int32[1])."""
+    import torch
+
+    n = d_handles.numel() * d_handles.element_size() // 16
+    ok = torch.empty(n, dtype=torch.uint8, device=d_image.device)
+    nbad = torch.zeros(1, dtype=torch.int32, device=d_image.device)
+    check(lib().pdb_sst_verify_device(_dev(d_image), d_image.numel() * d_image.element_size(), _dev(d_handles), n,
+                                      _dev(ok), _dev(nbad), _stream(stream)))
+    return ok, nbad

@@ -345,3 +345,52 @@ def test_host_batches_grouped_and_verify_host(crc, golden, oracle_lib, chunk):
             assert (ok[flip] == 0).all() and ok.sum() == len(bad) - len(flip), b["name"]
     finally:
         lib().pdb_diag_set_host_chunk(prev)
+
+
+@pytest.mark.gpu
+def test_round_boundaries_all_stream_paths(crc, oracle_lib):
+    """Block lengths around every round boundary of the stream kernels -- 4-KiB rounds, the last
+    round's extra chain (up to +2 KiB of 32-B pieces / +1 KiB of 16-B pieces), one past it -- at
+    every 4-B phase, through the descriptor path (16-B kernel), the unaligned fixed-stride path
+    (32-B kernel), the 4-B-aligned fixed-stride path (16-B kernel) and the sstable hooks."""
+    import oracle
+    from pebblesdb_amd import table as T
+
+    deltas = [-33, -17, -1, 0, 1, 15, 31, 32, 33, 100, 1007, 1023, 1024, 1025, 1040, 1041, 2047, 2048,
+              2049, 2080, 2081, 3000]
+    lens = sorted({4096 * r + d for r in (0, 1, 2, 3) for d in deltas if 4096 * r + d > 0})
+    offs, cur = [], 0
+    for i, n in enumerate(lens * 4):
+        cur += (i % 4) + 1  # every 4-B phase
+        offs.append(cur)
+        cur += n
+    all_lens = lens * 4
+    base = oracle.splitmix_bytes(cur + 64, 999)
+    blk = crc.make_blocks(offs, all_lens)
+    exp = oracle_lib.batch(base, blk)
+    d_base = torch.from_numpy(base).cuda()
+    got = _u32(crc.batch(d_base, crc.blocks_to_device(blk)))
+    assert (got == exp).all(), [all_lens[i] for i in np.nonzero(got != exp)[0][:5]]
+    for n in lens:
+        for stride, lo in ((n + 5, 1), (n + (-n) % 4 + 4, 0)):  # unaligned (32-B) / 4-B aligned (16-B)
+            nb = 33
+            b2 = crc.make_blocks(lo + np.arange(nb) * stride, np.full(nb, n))
+            e2 = oracle_lib.batch(base[: lo + nb * stride + 8], b2)
+            g2 = _u32(crc.batch_fixed(d_base[lo:], stride, n, nb))
+            assert (g2 == e2).all(), (n, stride)
+    # sstable hooks: handles of these sizes (contents n-1 + type byte under the CRC)
+    img = bytearray(base[: sum(lens) + 5 * len(lens) + 16].tobytes())
+    hs, pos = [], 3
+    for n in lens:
+        hs.append((pos, n - 1))
+        img[pos + n - 1] = 0
+        pos += n + 4
+    d_img = torch.frombuffer(img, dtype=torch.uint8).cuda()
+    d_h = T.handles_to_device(hs)
+    T.seal_device(d_img, d_h)
+    sealed = d_img.cpu().numpy()
+    for (o, sz) in hs:
+        want = oracle_lib.mask(oracle_lib.value(sealed[o : o + sz + 1]))
+        assert int.from_bytes(sealed[o + sz + 1 : o + sz + 5].tobytes(), "little") == want, sz
+    ok, nbad = T.verify_device(d_img, d_h)
+    assert int(nbad.item()) == 0 and bool(ok.all())
