@@ -312,8 +312,8 @@ def main():
                 "kernel": {"c2": "crc_pack4k_kernel<1,4,nt>", "sstable": "crc_stream_kernel<FixedSrc,OutSink,0,dyn,pack>",
                            "c3": "crc_stream16_kernel<DescSrc,OutSink,dyn,nt,pack>",
                            "wal": "crc_stream16_kernel<DescSrc,OutSink,dyn,nt,pack>",
-                           "sst_verify": "crc_stream_kernel<SstSrc,SstVerifySink,0,dyn,pack>",
-                           "sst_seal": "crc_stream_kernel<SstSrc,SealSink,0,dyn,pack>"}[args.workload],
+                           "sst_verify": "crc_stream16_kernel<SstSrc,SstVerifySink,dyn,nt,pack>",
+                           "sst_seal": "crc_stream16_kernel<SstSrc,SealSink,dyn,nt,pack>"}[args.workload],
                 "algorithmic_bytes_per_launch": algo_bytes,
                 "kernel_avg_ms": round(kern_avg_ms, 4),
                 "kernel_min_ms": round(float(np.min(kern_ms)), 4),

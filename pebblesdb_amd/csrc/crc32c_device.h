@@ -770,7 +770,10 @@ __device__ __forceinline__ uint32_t chain16(const char* lds, const LaneTabs& lt,
   return step4x(lds, lt, x, 0u);
 }
 
-template <class Src, class Sink, bool kDyn, bool kNT, bool kPack = false>
+// kDepth: items (4-KiB rounds) in flight per wave beyond the one being hashed.  Small or
+// round-and-a-bit blocks leave a wave with little data in flight per memory latency; depth 2
+// keeps two items' loads outstanding.
+template <class Src, class Sink, bool kDyn, bool kNT, bool kPack = false, int kDepth = 1>
 __global__ __launch_bounds__(kThreads) void crc_stream16_kernel(const uint32_t* __restrict__ tabs,
                                                                  Src src, uint64_t nblk, Sink sink) {
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
@@ -796,12 +799,21 @@ __global__ __launch_bounds__(kThreads) void crc_stream16_kernel(const uint32_t* 
   uint64_t i = kDyn ? g_lo + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : wave_id_uniform();
   if (i >= nend) return;
 
-  // the item being loaded: block d, round k
-  BlkDesc d{};
-  uint32_t k = 0;
-  u32x4 ne[5] = {};
-  uint32_t nxt = 0, nhw = 0, nhb = 0;
-  auto issue = [&](const BlkDesc& bd, uint32_t kk) {
+  // item = (block descriptor, block index, round); its loads live in a Buf16
+  struct Meta {
+    BlkDesc d;
+    uint64_t i;
+    uint32_t k;
+    bool v;
+  };
+  struct Buf16 {
+    u32x4 e[5];
+    uint32_t nxt, hw, hb;
+  };
+  // Every load instruction is issued on every item (per-lane conditions only mask lanes), so the
+  // compiler's vmcnt bookkeeping stays exact and hashing an item waits only for that item's loads;
+  // a data-dependent (uniform) branch around a load would make it wait for everything in flight.
+  auto issue = [&](Buf16& b, const BlkDesc& bd, uint32_t kk) {
     const uint32_t t = bd.n & 15u, K = bd.n >> 4;
     const uint8_t* q0 = bd.p + t;
     const uint32_t s = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(q0) & 3u);
@@ -811,7 +823,7 @@ __global__ __launch_bounds__(kThreads) void crc_stream16_kernel(const uint32_t* 
 #pragma unroll
     for (int j = 0; j < 5; ++j) {
       const uint32_t c = c0 + 64u * j + u;
-      if ((j < 4 || last) && c < K) ne[j] = ldq<kNT>(qa + 16ull * c);  // chain 4: last round only
+      if ((j < 4 || last) && c < K) b.e[j] = ldq<kNT>(qa + 16ull * c);  // chain 4: last round only
     }
     if (s && K) {
       // the dword after a piece whose right neighbour is not in this round's registers: lane 63's
@@ -821,25 +833,38 @@ __global__ __launch_bounds__(kThreads) void crc_stream16_kernel(const uint32_t* 
       uint32_t cx = 0xFFFFFFFFu;
       if (u == 63u && !last) cx = c0 + 255u;
       if (last && (cl & 63u) == u) cx = cl;
-      if (cx != 0xFFFFFFFFu) nxt = *reinterpret_cast<const uint32_t*>(qa + 16ull * (cx + 1u));
+      if (cx != 0xFFFFFFFFu) b.nxt = *reinterpret_cast<const uint32_t*>(qa + 16ull * (cx + 1u));
     }
     if (kk == 0) {
       const uint32_t lead = t & 3u, nh = t >> 2;
-      if (u >= 1 && u <= nh) nhw = ld32u(bd.p + lead + 4u * (u - 1));
+      if (u >= 1 && u <= nh) b.hw = ld32u(bd.p + lead + 4u * (u - 1));
       if (u == 0 && lead) {
         uint32_t v = bd.p[0];
         if (lead > 1) v |= static_cast<uint32_t>(bd.p[1]) << 8;
         if (lead > 2) v |= static_cast<uint32_t>(bd.p[2]) << 16;
-        nhb = v;
+        b.hb = v;
       }
     }
   };
-  d = src.get(i);
-  issue(d, 0);
-  // descriptor lookahead (as in crc_stream_kernel)
+  // descriptor lookahead: the next block after the queued items, its descriptor load in flight
   uint64_t ia = next_block(i);
   BlkDesc da{};
   if (ia < nend) da = src.get(ia);
+  auto advance = [&](const Meta& m) -> Meta {  // the item after m
+    if (m.v && m.k + 1 < rounds16(m.d.n >> 4)) return Meta{m.d, m.i, m.k + 1, true};
+    if (!m.v || ia >= nend) return Meta{BlkDesc{}, 0, 0, false};
+    const Meta r{da, ia, 0, true};
+    ia = next_block(ia);
+    if (ia < nend) da = src.get(ia);
+    return r;
+  };
+  Meta mB{src.get(i), i, 0, true}, mC{};
+  Buf16 B{}, C{};
+  issue(B, mB.d, 0);
+  if constexpr (kDepth > 1) {
+    mC = advance(mB);
+    if (mC.v) issue(C, mC.d, mC.k);
+  }
   uint32_t acc = 0;
   uint32_t park0 = 0, park1 = 0, park2 = 0, park3 = 0, npark = 0;
   uint64_t pid0 = 0, pid1 = 0, pid2 = 0, pid3 = 0;
@@ -854,23 +879,28 @@ __global__ __launch_bounds__(kThreads) void crc_stream16_kernel(const uint32_t* 
     npark = 0;
     park0 = park1 = park2 = park3 = 0;
   };
-  for (;;) {
-    const u32x4 e0 = ne[0], e1 = ne[1], e2 = ne[2], e3 = ne[3], e4 = ne[4];
-    const uint32_t cx = nxt, chw = nhw, chb = nhb;
-    const BlkDesc cd = d;
-    const uint32_t ck = k;
-    const uint32_t K = cd.n >> 4;
-    const uint32_t R = rounds16(K);
-    const bool last_round = ck + 1 >= R;
-    const uint64_t ni = last_round ? ia : i;
-    const bool have_next = ni < nend;
-    if (last_round && have_next) {
-      d = da;
-      ia = next_block(ni);
-      if (ia < nend) da = src.get(ia);
+  // A data-dependent branch around a load (or two alternating buffers) makes the compiler's vmcnt
+  // bookkeeping conservative -- hashing an item then waits for the NEXT item's loads too, which
+  // serialises memory and compute (a ping-pong version measured 3x slower): keep one loop, one
+  // issue site, and copy the loaded buffer.
+  while (mB.v) {
+    const Buf16 cur = B;
+    const Meta mcur = mB;
+    if constexpr (kDepth > 1) {
+      B = C;
+      mB = mC;
+      mC = advance(mC);
+      if (mC.v) issue(C, mC.d, mC.k);
+    } else {
+      mB = advance(mcur);
+      if (mB.v) issue(B, mB.d, mB.k);
     }
-    k = last_round ? 0 : ck + 1;
-    if (have_next) issue(d, k);
+    const u32x4 e0 = cur.e[0], e1 = cur.e[1], e2 = cur.e[2], e3 = cur.e[3], e4 = cur.e[4];
+    const uint32_t cx = cur.nxt, chw = cur.hw, chb = cur.hb;
+    const BlkDesc cd = mcur.d;
+    const uint32_t ck = mcur.k;
+    const uint32_t K = cd.n >> 4;
+    const bool last_round = ck + 1 >= rounds16(K);
 
     if (ck == 0) {  // head: every lane hashes the same (broadcast) head bytes from the seed
       const uint32_t t = cd.n & 15u, lead = t & 3u, nh = t >> 2;
@@ -908,18 +938,27 @@ __global__ __launch_bounds__(kThreads) void crc_stream16_kernel(const uint32_t* 
       }
     }
     if (J) {
+      // chain j runs (once, for the whole wave) only if some lane has a piece in it: a block of
+      // 1 KiB needs 2 of the 5 chains, not all of them (wave-uniform conditions on rem)
       const uint32_t start = ck ? shift_op(lds, PDB_SLOT_HORNER, acc) : acc;
-      const uint32_t x0 = chain16(lds, lt, start, e0, n0, s);
-      const uint32_t x1 = chain16(lds, lt, 0u, e1, n1, s);
-      const uint32_t x2 = chain16(lds, lt, 0u, e2, n2, s);
-      const uint32_t x3 = chain16(lds, lt, 0u, e3, n3, s);
-      // the fifth chain runs once for the wave when any lane has one (wave-uniform condition)
-      const uint32_t x4 = (last_round && rem > 256u) ? chain16(lds, lt, 0u, e4, n4, s) : 0u;
-      uint32_t a = x0;
-      if (J > 1) a = shift_op_x(lds, 7, a, x1);
-      if (J > 2) a = shift_op_x(lds, 7, a, x2);
-      if (J > 3) a = shift_op_x(lds, 7, a, x3);
-      if (J > 4) a = shift_op_x(lds, 7, a, x4);
+      const bool full = !last_round;
+      uint32_t a = chain16(lds, lt, start, e0, n0, s);
+      if (full || rem > 64u) {
+        const uint32_t x1 = chain16(lds, lt, 0u, e1, n1, s);
+        if (J > 1) a = shift_op_x(lds, 7, a, x1);
+      }
+      if (full || rem > 128u) {
+        const uint32_t x2 = chain16(lds, lt, 0u, e2, n2, s);
+        if (J > 2) a = shift_op_x(lds, 7, a, x2);
+      }
+      if (full || rem > 192u) {
+        const uint32_t x3 = chain16(lds, lt, 0u, e3, n3, s);
+        if (J > 3) a = shift_op_x(lds, 7, a, x3);
+      }
+      if (!full && rem > 256u) {  // the last round's fifth chain
+        const uint32_t x4 = chain16(lds, lt, 0u, e4, n4, s);
+        if (J > 4) a = shift_op_x(lds, 7, a, x4);
+      }
       acc = a;
     }
     if (last_round) {
@@ -933,10 +972,10 @@ __global__ __launch_bounds__(kThreads) void crc_stream16_kernel(const uint32_t* 
           part = u == 63u ? part : 0u;
         }
         switch (npark) {  // wave-uniform
-          case 0: park0 = part; pid0 = i; pd0 = cd; break;
-          case 1: park1 = part; pid1 = i; pd1 = cd; break;
-          case 2: park2 = part; pid2 = i; pd2 = cd; break;
-          default: park3 = part; pid3 = i; pd3 = cd; break;
+          case 0: park0 = part; pid0 = mcur.i; pd0 = cd; break;
+          case 1: park1 = part; pid1 = mcur.i; pd1 = cd; break;
+          case 2: park2 = part; pid2 = mcur.i; pd2 = cd; break;
+          default: park3 = part; pid3 = mcur.i; pd3 = cd; break;
         }
         if (++npark == 4) flush();
       } else {
@@ -946,10 +985,8 @@ __global__ __launch_bounds__(kThreads) void crc_stream16_kernel(const uint32_t* 
           if (q) acc = __shfl(acc, (u + q) & 63u, 64);
           raw = wave_tree_dpp<kDyn>(lds, u, acc);
         }
-        if (u == 0) sink.put(i, raw, cd);
+        if (u == 0) sink.put(mcur.i, raw, cd);
       }
-      i = ni;
-      if (!have_next) break;
     }
   }
   if constexpr (kPack) {

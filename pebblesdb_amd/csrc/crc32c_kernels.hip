@@ -190,13 +190,24 @@ hipError_t launch_sst(const LaunchGeom& g, const uint32_t* d_tables, uint8_t* bu
   (void)buf_len;
   if (n == 0) return hipSuccess;
   const dim3 grid(grid_for(g, n)), block(kThreads);
-  // sstable blocks (contents + type, ~4 KiB at byte offsets): 32-B pieces, packed 4-block trees
+  // sstable blocks (contents + type, ~4.1 KiB at byte offsets): 16-B pieces with nt loads, DPP
+  // neighbour dwords, conditional chains, packed 4-block trees (A/B vs the 32-B kernel, variant
+  // 18: +3-5 % on db_bench-sized blocks, profiles/r01_ab_sst_hooks.json)
   const SstSrc src{buf, h};
+  if (g_fast_variant == 18) {
+    if (seal)
+      hipLaunchKernelGGL((crc_stream_kernel<SstSrc, SealSink, 0, true, true>), grid, block, 0, s, d_tables, src, n,
+                         SealSink{});
+    else
+      hipLaunchKernelGGL((crc_stream_kernel<SstSrc, SstVerifySink, 0, true, true>), grid, block, 0, s, d_tables,
+                         src, n, SstVerifySink{ok, nbad});
+    return hipGetLastError();
+  }
   if (seal)
-    hipLaunchKernelGGL((crc_stream_kernel<SstSrc, SealSink, 0, true, true>), grid, block, 0, s, d_tables, src, n,
+    hipLaunchKernelGGL((crc_stream16_kernel<SstSrc, SealSink, true, true, true>), grid, block, 0, s, d_tables, src, n,
                        SealSink{});
   else
-    hipLaunchKernelGGL((crc_stream_kernel<SstSrc, SstVerifySink, 0, true, true>), grid, block, 0, s, d_tables,
+    hipLaunchKernelGGL((crc_stream16_kernel<SstSrc, SstVerifySink, true, true, true>), grid, block, 0, s, d_tables,
                        src, n, SstVerifySink{ok, nbad});
   return hipGetLastError();
 }
@@ -206,7 +217,7 @@ hipError_t launch_sst_masked(const LaunchGeom& g, const uint32_t* d_tables, uint
   if (n == 0) return hipSuccess;
   const dim3 grid(grid_for(g, n)), block(kThreads);
   // the seal's CRCs into a compact array (host seal: 4 B per block back across PCIe, not the span)
-  hipLaunchKernelGGL((crc_stream_kernel<SstSrc, OutSink, 0, true, true>), grid, block, 0, s, d_tables,
+  hipLaunchKernelGGL((crc_stream16_kernel<SstSrc, OutSink, true, true, true>), grid, block, 0, s, d_tables,
                      SstSrc{buf, h}, n, OutSink{out, PDB_CRC_MASK_OUTPUT});
   return hipGetLastError();
 }

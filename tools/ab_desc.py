@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""Interleaved A/B of descriptor-path variants (pdb_diag_set_variant) on descriptor workloads:
+  wal  : 32-KiB log blocks of 1055-B records (bench.py --workload wal)
+  sst  : back-to-back blocks of 4167-4175 B (sstable data blocks + type byte, any alignment)
+  c3   : Zipf 1-64 KiB (BASELINE config 3)
+  small: 256-B records
+argv[1] = variants (e.g. 16,17), argv[2] = workloads.  Prints one JSON object (GB/s, median)."""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import wal_layout, zipf_kib_sizes  # noqa: E402
+from pebblesdb_amd import crc32c  # noqa: E402
+from pebblesdb_amd._native import lib  # noqa: E402
+
+variants = [int(x) for x in sys.argv[1].split(",")]
+works = sys.argv[2].split(",") if len(sys.argv) > 2 else ["wal", "sst", "c3", "small"]
+total = 4 << 30
+crc32c.init_device(0)
+d = torch.empty(total + (1 << 20), dtype=torch.uint8, device="cuda")
+crc32c.fill_splitmix(d, 11)
+for _ in range(20):
+    crc32c.batch_fixed(d, 4096, 4096, total // 4096)
+
+
+def layout(w):
+    if w == "wal":
+        return wal_layout(total, 1055)
+    rng = np.random.Generator(np.random.PCG64(5))
+    if w == "sst":
+        lens = rng.integers(4167, 4176, size=total // 4172)
+    elif w == "c3":
+        lens = zipf_kib_sizes(total // (13 << 10), 301)
+    else:
+        lens = np.full(total // 256, 256)
+    lens = lens[: int(np.searchsorted(np.cumsum(lens), total))]
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]])
+    return offs, lens
+
+
+res = {}
+for w in works:
+    offs, lens = layout(w)
+    blk = crc32c.blocks_to_device(crc32c.make_blocks(offs, lens))
+    n = len(lens)
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    ref = None
+    for v in variants:
+        lib().pdb_diag_set_variant(v)
+        crc32c.batch(d, blk, out=out)
+        torch.cuda.synchronize()
+        if ref is None:
+            ref = out.clone()
+        assert torch.equal(out, ref), (w, v)
+    times = {v: [] for v in variants}
+    for _ in range(4):
+        for v in variants:
+            lib().pdb_diag_set_variant(v)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(3):
+                crc32c.batch(d, blk, out=out)
+            e1.record()
+            torch.cuda.synchronize()
+            times[v].append(e0.elapsed_time(e1) / 3)
+    algo = int(lens.sum()) + 20 * n
+    res[w] = {v: round(algo / (np.median(t) * 1e-3) / 1e9, 1) for v, t in times.items()}
+lib().pdb_diag_set_variant(0)
+print(json.dumps(res))
