@@ -414,43 +414,60 @@ struct BlkDesc {
   uint32_t init_raw;  // ~Extend seed
 };
 
+// Sources: get(i) = the descriptor of block i.  load(i) / finish(raw) split it so a kernel can
+// issue block i's descriptor load one block ahead and only touch the value when the block is
+// due: load() is a vector load into VGPRs (never an SMEM load, whose lgkmcnt would also stall the
+// kernel's LDS lookups) and finish() makes the fields wave-uniform.
 struct FixedSrc {
   const uint8_t* base;
   uint64_t stride;
   uint32_t len;
   uint32_t init_raw;
-  __device__ __forceinline__ BlkDesc get(uint64_t i) const { return {base + i * stride, len, init_raw}; }
+  using Raw = uint64_t;
+  __device__ __forceinline__ Raw load(uint64_t i) const { return i; }
+  __device__ __forceinline__ BlkDesc finish(Raw i) const { return {base + i * stride, len, init_raw}; }
+  __device__ __forceinline__ BlkDesc get(uint64_t i) const { return finish(i); }
 };
 
 // Descriptor fields are loaded by every lane from one address, so the compiler sees per-lane
 // (VGPR) values; readfirstlane makes them wave-uniform SGPRs, which keeps the block geometry
 // (rounds, chains, head) on scalar branches instead of exec-masked divergent code.
-__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
-  const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v)));
-  const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32)));
-  return (static_cast<uint64_t>(hi) << 32) | lo;
+__device__ __forceinline__ uint64_t uniform64(uint32_t lo, uint32_t hi) {
+  const uint32_t l = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(lo));
+  const uint32_t h = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(hi));
+  return (static_cast<uint64_t>(h) << 32) | l;
 }
 
 struct DescSrc {
   const uint8_t* base;
   const pdb_blk* blk;
   uint32_t flags;
-  __device__ __forceinline__ BlkDesc get(uint64_t i) const {
-    const pdb_blk d = blk[i];
-    const uint32_t init = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(d.init));
-    const uint32_t len = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(d.len));
-    return {base + uniform64(d.off), len, (flags & PDB_CRC_USE_INIT) ? ~init : 0xFFFFFFFFu};
+  using Raw = u32x4;  // pdb_blk {off lo, off hi, len, init}
+  __device__ __forceinline__ Raw load(uint64_t i) const {
+    // 8-B alignment is all pdb_blk guarantees: a 4-B-aligned 16-B load
+    return __builtin_nontemporal_load(reinterpret_cast<const u32x4a4*>(blk + i));
   }
+  __device__ __forceinline__ BlkDesc finish(const Raw& r) const {
+    const uint32_t len = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(r.z));
+    const uint32_t init = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(r.w));
+    return {base + uniform64(r.x, r.y), len, (flags & PDB_CRC_USE_INIT) ? ~init : 0xFFFFFFFFu};
+  }
+  __device__ __forceinline__ BlkDesc get(uint64_t i) const { return finish(load(i)); }
 };
 
 // sstable handle: CRC over contents || type (table/table_builder.cc:197-198; format.cc:98).
 struct SstSrc {
   uint8_t* buf;
   const pdb_block_handle* h;
-  __device__ __forceinline__ BlkDesc get(uint64_t i) const {
-    const pdb_block_handle x = h[i];
-    return {buf + uniform64(x.offset), static_cast<uint32_t>(uniform64(x.size)) + 1u, 0xFFFFFFFFu};
+  using Raw = u32x4;  // pdb_block_handle {offset lo, hi, size lo, hi}
+  __device__ __forceinline__ Raw load(uint64_t i) const {
+    return __builtin_nontemporal_load(reinterpret_cast<const u32x4a4*>(h + i));
   }
+  __device__ __forceinline__ BlkDesc finish(const Raw& r) const {
+    return {buf + uniform64(r.x, r.y), static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(r.z)) + 1u,
+            0xFFFFFFFFu};
+  }
+  __device__ __forceinline__ BlkDesc get(uint64_t i) const { return finish(load(i)); }
 };
 
 struct OutSink {
@@ -524,8 +541,9 @@ __device__ __forceinline__ void issue_piece(RawPiece& r, const uint8_t* q, uint3
   const u32x4a4 x0 = v[0], x1 = v[1];
   r.e[0] = x0.x; r.e[1] = x0.y; r.e[2] = x0.z; r.e[3] = x0.w;
   r.e[4] = x1.x; r.e[5] = x1.y; r.e[6] = x1.z; r.e[7] = x1.w;
-  // the 9th dword holds the piece's last byte(s) only when misaligned (never past the block)
-  r.e[8] = s ? *reinterpret_cast<const uint32_t*>(q - s + 32) : 0u;
+  // the 9th dword holds the piece's last byte(s) only when misaligned (never past the block);
+  // aligned (s uniform 0) it re-reads the 8th, so the instruction is issued either way
+  r.e[8] = *reinterpret_cast<const uint32_t*>(q - s + (s ? 32 : 28));
 }
 
 // Chain over one 32-B piece: returns shift(x0_state ^ piece ...), i.e. the raw state after the
@@ -587,24 +605,34 @@ __global__ __launch_bounds__(kThreads) void crc_stream_kernel(const uint32_t* __
   uint32_t k = 0;
   RawPiece na, nb, nc;
   uint32_t nhw = 0, nhb = 0;
+  // Unmasked, unconditional loads (as in crc_stream16_kernel): a lane past the block's last
+  // piece re-reads it, a lane with no head word reads the table buffer; a masked load would make
+  // the next item's loads wait for this item's.
+  const uint8_t* dummy = reinterpret_cast<const uint8_t*>(tabs);
   auto issue = [&](const BlkDesc& bd, uint32_t kk) {
     const uint32_t t = bd.n & 31u, K = bd.n >> 5;
-    const uint8_t* q0 = bd.p + t;
-    const uint32_t s = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(q0) & 3u);
+    const uint8_t* q0 = K ? bd.p + t : dummy;
+    const uint32_t s = K ? static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
+                               static_cast<uint32_t>(reinterpret_cast<uintptr_t>(q0) & 3u)))
+                         : 0u;
+    const uint32_t cmax = K ? K - 1u : 0u;
     const uint32_t ca = u + (kk << 7), cb = ca + 64u, cc = ca + 128u;
-    if (ca < K) issue_piece(na, q0 + static_cast<uint64_t>(ca) * 32u, s);
-    if (cb < K) issue_piece(nb, q0 + static_cast<uint64_t>(cb) * 32u, s);
-    if (kk + 1 >= rounds32(K) && cc < K) issue_piece(nc, q0 + static_cast<uint64_t>(cc) * 32u, s);
-    if (kk == 0) {
-      const uint32_t lead = t & 3u, nh = t >> 2;
-      if (u >= 1 && u <= nh) nhw = ld32u(bd.p + lead + 4u * (u - 1));
-      if (u == 0 && lead) {
-        uint32_t v = bd.p[0];
-        if (lead > 1) v |= static_cast<uint32_t>(bd.p[1]) << 8;
-        if (lead > 2) v |= static_cast<uint32_t>(bd.p[2]) << 16;
-        nhb = v;
-      }
-    }
+    const bool last = kk + 1 >= rounds32(K);
+    issue_piece(na, q0 + static_cast<uint64_t>(min(ca, cmax)) * 32u, s);
+    issue_piece(nb, q0 + static_cast<uint64_t>(min(cb, cmax)) * 32u, s);
+    issue_piece(nc, q0 + static_cast<uint64_t>(min(last ? cc : cb, cmax)) * 32u, s);  // chain c: last round
+    const uint32_t lead = t & 3u, nh = t >> 2;
+    const bool hw_on = kk == 0 && nh, hb_on = kk == 0 && lead;
+    const uint32_t hs = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
+        static_cast<uint32_t>(reinterpret_cast<uintptr_t>(bd.p + lead) & 3u)));
+    const uint8_t* hp = hw_on ? bd.p + lead + 4u * (min(max(u, 1u), nh) - 1u) - hs : dummy;
+    const uint32_t w0 = *reinterpret_cast<const uint32_t*>(hp);
+    const uint32_t w1 = *reinterpret_cast<const uint32_t*>(hp + (hw_on && hs ? 4u : 0u));
+    nhw = __builtin_amdgcn_alignbyte(w1, w0, hw_on ? hs : 0u);
+    const uint8_t* bp = hb_on ? bd.p : dummy;
+    const uint32_t lm = hb_on ? lead - 1u : 0u;
+    const uint32_t b0 = bp[0], b1 = bp[min(1u, lm)], b2 = bp[min(2u, lm)];
+    nhb = b0 | (lead > 1 ? b1 << 8 : 0u) | (lead > 2 ? b2 << 16 : 0u);
   };
   if (active) {
     d = src.get(i);
@@ -614,8 +642,7 @@ __global__ __launch_bounds__(kThreads) void crc_stream_kernel(const uint32_t* __
   // (a descriptor fetched only when its block is due would put one full memory latency in front
   // of every block's loads)
   uint64_t ia = active ? next_block(i) : nend;
-  BlkDesc da{};
-  if (ia < nend) da = src.get(ia);
+  typename Src::Raw ra = src.load(ia < nend ? ia : (nend ? nend - 1 : 0));
   uint32_t acc = 0;
   // kPack: parked blocks
   uint32_t park0 = 0, park1 = 0, park2 = 0, park3 = 0, npark = 0;
@@ -656,12 +683,14 @@ __global__ __launch_bounds__(kThreads) void crc_stream_kernel(const uint32_t* __
     const uint64_t ni = last_round ? ia : i;
     const bool have_next = ni < nend;
     if (last_round && have_next) {
-      d = da;
+      d = src.finish(ra);
       ia = next_block(ni);
-      if (ia < nend) da = src.get(ia);
     }
+    // unconditional loads (see issue): the lookahead descriptor (clamped) and the next item (an
+    // exhausted wave re-reads round 0 of its last block)
+    ra = src.load(ia < nend ? ia : nend - 1);
     k = last_round ? 0 : ck + 1;
-    if (have_next) issue(d, k);
+    issue(d, k);
 
     if (ck == 0) {  // head: every lane hashes the same (broadcast) head bytes from the seed
       const uint32_t t = cd.n & 31u, lead = t & 3u, nh = t >> 2;
@@ -770,10 +799,7 @@ __device__ __forceinline__ uint32_t chain16(const char* lds, const LaneTabs& lt,
   return step4x(lds, lt, x, 0u);
 }
 
-// kDepth: items (4-KiB rounds) in flight per wave beyond the one being hashed.  Small or
-// round-and-a-bit blocks leave a wave with little data in flight per memory latency; depth 2
-// keeps two items' loads outstanding.
-template <class Src, class Sink, bool kDyn, bool kNT, bool kPack = false, int kDepth = 1>
+template <class Src, class Sink, bool kDyn, bool kNT, bool kPack = false>
 __global__ __launch_bounds__(kThreads) void crc_stream16_kernel(const uint32_t* __restrict__ tabs,
                                                                  Src src, uint64_t nblk, Sink sink) {
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
@@ -810,61 +836,68 @@ __global__ __launch_bounds__(kThreads) void crc_stream16_kernel(const uint32_t* 
     u32x4 e[5];
     uint32_t nxt, hw, hb;
   };
-  // Every load instruction is issued on every item (per-lane conditions only mask lanes), so the
-  // compiler's vmcnt bookkeeping stays exact and hashing an item waits only for that item's loads;
-  // a data-dependent (uniform) branch around a load would make it wait for everything in flight.
+  // Every item issues the same load instructions with every lane active and no branch around
+  // any of them: a lane with nothing to load re-reads a valid address (the block's last piece, or
+  // the table buffer `tabs` as a dummy), and the values it gets are never used.  A masked load
+  // keeps its register's old value in inactive lanes, which makes the compiler wait for the
+  // previous item's loads before issuing the next ones (no prefetch at all); a branch around a
+  // load makes its vmcnt bookkeeping conservative.  Fixed, unmasked loads keep hashing an item
+  // waiting only for that item's data.
+  const uint8_t* dummy = reinterpret_cast<const uint8_t*>(tabs);
   auto issue = [&](Buf16& b, const BlkDesc& bd, uint32_t kk) {
     const uint32_t t = bd.n & 15u, K = bd.n >> 4;
     const uint8_t* q0 = bd.p + t;
-    const uint32_t s = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(q0) & 3u);
-    const uint8_t* qa = q0 - s;
+    const uint32_t s = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
+        static_cast<uint32_t>(reinterpret_cast<uintptr_t>(q0) & 3u)));
+    const uint8_t* qa = K ? q0 - s : dummy;
+    const uint32_t cmax = K ? K - 1u : 0u;
     const uint32_t c0 = kk << 8;
-    const bool last = kk + 1 >= rounds16(K);
+    const bool last = kk + 1 >= rounds16(K);  // wave-uniform
 #pragma unroll
-    for (int j = 0; j < 5; ++j) {
-      const uint32_t c = c0 + 64u * j + u;
-      if ((j < 4 || last) && c < K) b.e[j] = ldq<kNT>(qa + 16ull * c);  // chain 4: last round only
-    }
-    if (s && K) {
-      // the dword after a piece whose right neighbour is not in this round's registers: lane 63's
-      // chain-3 piece in a non-last round (its neighbour opens the next round), and the block's
-      // last piece (always in the last round)
-      const uint32_t cl = K - 1;
-      uint32_t cx = 0xFFFFFFFFu;
-      if (u == 63u && !last) cx = c0 + 255u;
-      if (last && (cl & 63u) == u) cx = cl;
-      if (cx != 0xFFFFFFFFu) b.nxt = *reinterpret_cast<const uint32_t*>(qa + 16ull * (cx + 1u));
-    }
-    if (kk == 0) {
-      const uint32_t lead = t & 3u, nh = t >> 2;
-      if (u >= 1 && u <= nh) b.hw = ld32u(bd.p + lead + 4u * (u - 1));
-      if (u == 0 && lead) {
-        uint32_t v = bd.p[0];
-        if (lead > 1) v |= static_cast<uint32_t>(bd.p[1]) << 8;
-        if (lead > 2) v |= static_cast<uint32_t>(bd.p[2]) << 16;
-        b.hb = v;
-      }
-    }
+    for (int j = 0; j < 4; ++j) b.e[j] = ldq<kNT>(qa + 16ull * min(c0 + 64u * j + u, cmax));
+    // chain 4 exists only in the last round; otherwise re-read chain 3's (cached) piece
+    b.e[4] = ldq<kNT>(qa + 16ull * min(c0 + (last ? 256u : 192u) + u, cmax));
+    // the dword after a piece whose right neighbour is not in this round's registers: lane 63's
+    // chain-3 piece in a non-last round (its neighbour opens the next round), and the block's
+    // last piece (always in the last round); with s == 0 nothing is needed (re-read inside)
+    const uint32_t cx = (u == 63u && !last) ? c0 + 255u : cmax;
+    b.nxt = *reinterpret_cast<const uint32_t*>(qa + 16ull * cx + (s ? 16u : 0u));
+    // head (round 0): word j (unaligned, hs) on lane j + 1, lead bytes on every lane
+    const uint32_t lead = t & 3u, nh = t >> 2;
+    const bool hw_on = kk == 0 && nh, hb_on = kk == 0 && lead;
+    const uint32_t hs = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
+        static_cast<uint32_t>(reinterpret_cast<uintptr_t>(bd.p + lead) & 3u)));
+    const uint8_t* hp = hw_on ? bd.p + lead + 4u * (min(max(u, 1u), nh) - 1u) - hs : dummy;
+    const uint32_t w0 = *reinterpret_cast<const uint32_t*>(hp);
+    const uint32_t w1 = *reinterpret_cast<const uint32_t*>(hp + (hw_on && hs ? 4u : 0u));
+    b.hw = __builtin_amdgcn_alignbyte(w1, w0, hs);
+    const uint8_t* bp = hb_on ? bd.p : dummy;
+    const uint32_t lm = hb_on ? lead - 1u : 0u;
+    const uint32_t b0 = bp[0], b1 = bp[min(1u, lm)], b2 = bp[min(2u, lm)];
+    b.hb = b0 | (lead > 1 ? b1 << 8 : 0u) | (lead > 2 ? b2 << 16 : 0u);
   };
-  // descriptor lookahead: the next block after the queued items, its descriptor load in flight
+
+  // descriptor lookahead: block ia's descriptor is loaded one block before it is due.  Every
+  // iteration issues exactly one descriptor load and one item's loads, whatever the block
+  // geometry (an exhausted wave re-loads its last item as a dummy): a data-dependent branch
+  // around a load makes the compiler's vmcnt bookkeeping conservative, and the wait for the
+  // current item would then also wait for the loads just issued for the next one.
   uint64_t ia = next_block(i);
-  BlkDesc da{};
-  if (ia < nend) da = src.get(ia);
-  auto advance = [&](const Meta& m) -> Meta {  // the item after m
-    if (m.v && m.k + 1 < rounds16(m.d.n >> 4)) return Meta{m.d, m.i, m.k + 1, true};
-    if (!m.v || ia >= nend) return Meta{BlkDesc{}, 0, 0, false};
-    const Meta r{da, ia, 0, true};
-    ia = next_block(ia);
-    if (ia < nend) da = src.get(ia);
+  typename Src::Raw ra = src.load(ia < nend ? ia : nend - 1);
+  auto advance = [&](const Meta& m) -> Meta {  // the item after m (m.d is always a real block)
+    Meta r{m.d, m.i, m.k, false};
+    if (m.v && m.k + 1 < rounds16(m.d.n >> 4)) {
+      r = Meta{m.d, m.i, m.k + 1, true};
+    } else if (m.v && ia < nend) {
+      r = Meta{src.finish(ra), ia, 0, true};
+      ia = next_block(ia);
+    }
+    ra = src.load(ia < nend ? ia : nend - 1);
     return r;
   };
-  Meta mB{src.get(i), i, 0, true}, mC{};
-  Buf16 B{}, C{};
+  Meta mB{src.get(i), i, 0, true};
+  Buf16 B{};
   issue(B, mB.d, 0);
-  if constexpr (kDepth > 1) {
-    mC = advance(mB);
-    if (mC.v) issue(C, mC.d, mC.k);
-  }
   uint32_t acc = 0;
   uint32_t park0 = 0, park1 = 0, park2 = 0, park3 = 0, npark = 0;
   uint64_t pid0 = 0, pid1 = 0, pid2 = 0, pid3 = 0;
@@ -879,22 +912,12 @@ __global__ __launch_bounds__(kThreads) void crc_stream16_kernel(const uint32_t* 
     npark = 0;
     park0 = park1 = park2 = park3 = 0;
   };
-  // A data-dependent branch around a load (or two alternating buffers) makes the compiler's vmcnt
-  // bookkeeping conservative -- hashing an item then waits for the NEXT item's loads too, which
-  // serialises memory and compute (a ping-pong version measured 3x slower): keep one loop, one
-  // issue site, and copy the loaded buffer.
-  while (mB.v) {
+  for (;;) {
     const Buf16 cur = B;
     const Meta mcur = mB;
-    if constexpr (kDepth > 1) {
-      B = C;
-      mB = mC;
-      mC = advance(mC);
-      if (mC.v) issue(C, mC.d, mC.k);
-    } else {
-      mB = advance(mcur);
-      if (mB.v) issue(B, mB.d, mB.k);
-    }
+    if (!mcur.v) break;
+    mB = advance(mcur);
+    issue(B, mB.d, mB.k);  // unconditional (see above)
     const u32x4 e0 = cur.e[0], e1 = cur.e[1], e2 = cur.e[2], e3 = cur.e[3], e4 = cur.e[4];
     const uint32_t cx = cur.nxt, chw = cur.hw, chb = cur.hb;
     const BlkDesc cd = mcur.d;

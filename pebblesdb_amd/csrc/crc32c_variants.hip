@@ -485,9 +485,7 @@ hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tab
   else if (v == 16)  // coalesced 16-B pieces, nt loads, dynamic blocks, packed 4-block trees
     hipLaunchKernelGGL((crc_stream16_kernel<DescSrc, OutSink, true, true, true>), grid, block, 0, s, d_tables,
                        src, nblk, OutSink{out, flags});
-  else if (v == 17)  // ... two items in flight per wave
-    hipLaunchKernelGGL((crc_stream16_kernel<DescSrc, OutSink, true, true, true, 2>), grid, block, 0, s, d_tables,
-                       src, nblk, OutSink{out, flags});
+
   else
     hipLaunchKernelGGL((crc_stream_kernel<DescSrc, OutSink, 0, true>), grid, block, 0, s, d_tables, src, nblk,
                        OutSink{out, flags});

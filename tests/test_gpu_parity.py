@@ -278,7 +278,7 @@ def test_scalar_extend_zero_copy_sizes(crc, oracle_lib):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [12, 13, 14, 15, 16, 17])
+@pytest.mark.parametrize("variant", [12, 13, 14, 15, 16])
 def test_stream_variants_exact(crc, golden, oracle_lib, variant):
     """A/B variants of the descriptor / generic fixed paths (12-14: coalesced 16-B-piece stream
     kernel; 15: 32-B pieces with packed 4-block trees): the golden sweep (every alignment x every length 0..300), the golden batches, and
