@@ -309,11 +309,11 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": {"c2": "crc_pack4k_kernel<1,4,nt>", "sstable": "crc_stream_kernel<FixedSrc,OutSink,0,dyn,pack>",
+                "kernel": {"c2": "crc_pack4k_kernel<1,4,nt>", "sstable": "crc_sst4k_kernel<FixedSrc,OutSink,nt>",
                            "c3": "crc_stream16_kernel<DescSrc,OutSink,dyn,nt,pack>",
                            "wal": "crc_stream16_kernel<DescSrc,OutSink,dyn,nt,pack>",
-                           "sst_verify": "crc_stream16_kernel<SstSrc,SstVerifySink,dyn,nt,pack>",
-                           "sst_seal": "crc_stream16_kernel<SstSrc,SealSink,dyn,nt,pack>"}[args.workload],
+                           "sst_verify": "crc_sst4k_kernel<SstSrc,SstVerifySink,nt>",
+                           "sst_seal": "crc_sst4k_kernel<SstSrc,SealSink,nt>"}[args.workload],
                 "algorithmic_bytes_per_launch": algo_bytes,
                 "kernel_avg_ms": round(kern_avg_ms, 4),
                 "kernel_min_ms": round(float(np.min(kern_ms)), 4),

@@ -427,6 +427,7 @@ struct FixedSrc {
   __device__ __forceinline__ Raw load(uint64_t i) const { return i; }
   __device__ __forceinline__ BlkDesc finish(Raw i) const { return {base + i * stride, len, init_raw}; }
   __device__ __forceinline__ BlkDesc get(uint64_t i) const { return finish(i); }
+  __device__ __forceinline__ BlkDesc lane(Raw i) const { return finish(i); }  // per-lane fields
 };
 
 // Descriptor fields are loaded by every lane from one address, so the compiler sees per-lane
@@ -468,6 +469,9 @@ struct SstSrc {
             0xFFFFFFFFu};
   }
   __device__ __forceinline__ BlkDesc get(uint64_t i) const { return finish(load(i)); }
+  __device__ __forceinline__ BlkDesc lane(const Raw& r) const {  // per-lane fields (no readfirstlane)
+    return {buf + ((static_cast<uint64_t>(r.y) << 32) | r.x), r.z + 1u, 0xFFFFFFFFu};
+  }
 };
 
 struct OutSink {
@@ -513,6 +517,50 @@ struct SstVerifySink {
     const bool good = pdb_unmask(stored) == ~raw;
     if (ok) ok[i] = good ? 1 : 0;
     if (!good && nbad) atomicAdd(nbad, 1u);
+  }
+};
+
+// Sink access for crc_sst4k_kernel: pre() issues whatever the sink reads (the stored trailer a
+// verify compares with) a group ahead, so put() never waits on a load issued after the next
+// group's prefetch; all accesses through global-address-space pointers (the kernel's block
+// addresses are integers; a flat access would also count in lgkmcnt and stall LDS lookups).
+template <class Sink>
+struct SinkOps {
+  __device__ static __forceinline__ uint32_t pre(const Sink&, const BlkDesc&) { return 0u; }
+  __device__ static __forceinline__ void put(const Sink& k, uint64_t i, uint32_t raw, const BlkDesc& d, uint32_t) {
+    k.put(i, raw, d);
+  }
+};
+
+template <>
+struct SinkOps<SealSink> {
+  __device__ static __forceinline__ uint32_t pre(const SealSink&, const BlkDesc&) { return 0u; }
+  __device__ static __forceinline__ void put(const SealSink&, uint64_t, uint32_t raw, const BlkDesc& d, uint32_t) {
+    typedef __attribute__((address_space(1))) uint8_t g_u8;
+    g_u8* tr = reinterpret_cast<g_u8*>(reinterpret_cast<uintptr_t>(d.p) + d.n);
+    const uint32_t m = pdb_mask(~raw);
+    tr[0] = static_cast<uint8_t>(m);
+    tr[1] = static_cast<uint8_t>(m >> 8);
+    tr[2] = static_cast<uint8_t>(m >> 16);
+    tr[3] = static_cast<uint8_t>(m >> 24);
+  }
+};
+
+template <>
+struct SinkOps<SstVerifySink> {
+  // the stored trailer word at p + n (any alignment): the two aligned dwords holding it
+  __device__ static __forceinline__ uint32_t pre(const SstVerifySink&, const BlkDesc& d) {
+    typedef __attribute__((address_space(1))) const uint32_t g_u32_;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(d.p) + d.n;
+    const uint32_t s = static_cast<uint32_t>(a & 3u);
+    const uint32_t lo = *reinterpret_cast<g_u32_*>(a - s), hi = *reinterpret_cast<g_u32_*>(a - s + (s ? 4u : 0u));
+    return __builtin_amdgcn_alignbyte(hi, lo, s);
+  }
+  __device__ static __forceinline__ void put(const SstVerifySink& k, uint64_t i, uint32_t raw, const BlkDesc&,
+                                             uint32_t stored) {
+    const bool good = pdb_unmask(stored) == ~raw;
+    if (k.ok) k.ok[i] = good ? 1 : 0;
+    if (!good && k.nbad) atomicAdd(k.nbad, 1u);
   }
 };
 
@@ -1014,6 +1062,324 @@ __global__ __launch_bounds__(kThreads) void crc_stream16_kernel(const uint32_t* 
   }
   if constexpr (kPack) {
     if (npark) flush();
+  }
+}
+
+// ---- sstable-sized blocks: one exact 4-KiB body + a batched prefix ------------------------------
+// Every data block TableBuilder emits is a little over block_size = 4096 B (table_builder.cc:
+// 127-130; the CRC covers contents || type, 197-198): db_bench's are 4167-4175 B.  The generic
+// stream kernels pay for that shape with a fifth chain (4 extra 16-B pieces run by the whole
+// wave), a serial broadcast head and a lane rotation per block.  Here a block of n bytes,
+// 4096 <= n <= 4352, is split as
+//   prefix = its first m = n - 4096 bytes,  body = its last 4096 bytes (at bs = p + m)
+// and hashed from state 0 with the seed folded in up front:
+//   * prefix: front-padded with z = (-m) mod 16 zero bytes to E = ceil(m/16) <= 16 pieces.
+//     Hashing 0^z || prefix from U[z] = shift^-z(0xFFFFFFFF) gives exactly R(prefix) from
+//     Value()'s seed (the z zeros carry U[z] to 0xFFFFFFFF).  The prefixes of a wave's 4 blocks
+//     are hashed together: row r (lanes 16r..16r+15) takes block r, lane w the 16 B ending
+//     16 (15 - w) bytes before bs (zero-masked below p; never loading a dword wholly below p),
+//     and a 4-level DPP row tree (shift 16..128) leaves the prefix state P_r in lane 16r.
+//   * body: exactly crc_pack4k_kernel<kNP = 4>'s geometry -- lane u owns the 16-B pieces at
+//     bs + 16u + 1024j, every load instruction 1 KiB contiguous and non-temporal, chains folded
+//     by Horner with "shift 1024" -- with P_r injected as lane 0's starting state.  bs has any
+//     alignment: 4-B aligned dwordx4 loads, the 17th-20th byte from the next lane by DPP, one
+//     extra dword for the block's last piece (as crc_stream16_kernel).
+//   * the 4 blocks' lane partials fold in one tree4_packed (no rotation: the body is exactly 256
+//     pieces); lanes 0..3 hand the raw states to the sink.
+// Workgroup g owns blocks [g*N/G, (g+1)*N/G) and its waves take 4-block groups from an LDS
+// counter (slot 7; the measured locality of crc_pack4k_dyn_kernel).  Loads run one block ahead
+// (body) and one group ahead (descriptors, prefixes), every one unmasked and unconditional.
+// Blocks outside [4096, 4352] (an index / metaindex / a table's last data block) take
+// sst_slow_block on the same wave: the block front-padded to whole 4-KiB bodies, one Horner
+// sequence of 16-B pieces at stride 1024 per lane, then one wave tree; its raw state is parked
+// in lane 63 (the packed tree's unshifted position).
+// Valid only for Value()-seeded CRCs (init 0xFFFFFFFF): SstSrc always, FixedSrc without an Extend
+// seed.
+constexpr uint32_t kSstMin = 4096u, kSstMax = 4096u + 256u;
+
+// The 16 bytes at A (any alignment) with the bytes below `lo` zeroed.  Never reads an aligned
+// dword wholly below lo, nor -- A 4-B aligned -- the dword after the piece.
+// Loads through integer addresses (the kernel computes block addresses as integers: readlane
+// halves, selects against a dummy): cast to global-address-space pointers, or the compiler emits
+// flat loads, whose lgkmcnt would make every LDS lookup wait for them too.
+typedef __attribute__((address_space(1))) const uint32_t g_u32;
+typedef __attribute__((address_space(1))) const u32x4a4 g_u32x4;
+
+__device__ __forceinline__ uint32_t gload32(uintptr_t a) { return *reinterpret_cast<g_u32*>(a); }
+
+template <bool kNT>
+__device__ __forceinline__ u32x4 gload128(uintptr_t a) {
+  if constexpr (kNT)
+    return __builtin_nontemporal_load(reinterpret_cast<g_u32x4*>(a));
+  else
+    return *reinterpret_cast<g_u32x4*>(a);
+}
+
+// A descriptor load whose last dword is never used (a handle's size_hi) leaves that register
+// free for reuse, and reusing the destination of a load in flight waits for the load: keep the
+// whole 16 B live until the descriptor is consumed.
+__device__ __forceinline__ void keep_alive(const u32x4& r) { asm volatile("" ::"v"(r.w)); }
+__device__ __forceinline__ void keep_alive(uint64_t) {}
+
+struct MaskedPiece {
+  uint32_t e[5];
+  uint32_t s;   // A & 3
+  int32_t zl;   // lo - A (bytes to zero, before clamping to [0, 16])
+};
+
+__device__ __forceinline__ void issue_masked(MaskedPiece& f, uintptr_t A, uintptr_t lo) {
+  const uintptr_t l4 = lo & ~static_cast<uintptr_t>(3);
+  const uint32_t s = static_cast<uint32_t>(A & 3u);
+  const uintptr_t a0 = A - s;
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    uintptr_t ad = a0 + 4u * (i < 4 ? static_cast<uint32_t>(i) : (s ? 4u : 3u));
+    ad = ad < l4 ? l4 : ad;
+    f.e[i] = gload32(ad);
+  }
+  f.s = s;
+  const intptr_t zl = static_cast<intptr_t>(lo - A);
+  f.zl = zl < -1 ? -1 : (zl > 16 ? 16 : static_cast<int32_t>(zl));
+}
+
+// The piece's raw state from `start` (0 for zero pieces: the masked bytes are zeros).
+__device__ __forceinline__ uint32_t hash_masked(const char* lds, const LaneTabs& lt, const MaskedPiece& f,
+                                                uint32_t start) {
+  const uint32_t z = f.zl < 0 ? 0u : static_cast<uint32_t>(f.zl);
+  uint32_t w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t v = __builtin_amdgcn_alignbyte(f.e[i + 1], f.e[i], f.s);
+    const uint32_t sh = z > 4u * i ? min(z - 4u * i, 4u) : 0u;
+    w[i] = sh >= 4u ? 0u : (v & (0xFFFFFFFFu << (8u * sh)));
+  }
+  return chain16(lds, lt, start, u32x4{w[0], w[1], w[2], w[3]}, 0u, 0u);
+}
+
+// Start state of a masked piece: U[z] on the piece holding the block's first byte (0 <= lo - A <
+// 16), else 0.  ureg: lane l holds U[l & 15].  All lanes must be active (bpermute).
+__device__ __forceinline__ uint32_t masked_start(const MaskedPiece& f, uint32_t ureg) {
+  const uint32_t z = static_cast<uint32_t>(f.zl) & 15u;
+  const uint32_t uz = __shfl(ureg, z, 64);
+  return (f.zl >= 0 && f.zl < 16) ? uz : 0u;
+}
+
+// Levels 0..3 of the wave tree inside each row of 16 lanes (row_shl never crosses a row):
+// lane 16r gets sum_w shift(c_w, 16 (15 - w)).
+__device__ __forceinline__ uint32_t row_tree16(const char* lds, uint32_t lane, uint32_t c) {
+  uint32_t y;
+  y = __builtin_amdgcn_update_dpp(0u, c, 0x101, 0xF, 0xF, false);  // row_shl:1
+  if ((lane & 1u) == 0) c = shift_op_x(lds, 0, c, y);
+  y = __builtin_amdgcn_update_dpp(0u, c, 0x102, 0xF, 0xF, false);  // row_shl:2
+  if ((lane & 3u) == 0) c = shift_op_x(lds, 1, c, y);
+  y = __builtin_amdgcn_update_dpp(0u, c, 0x104, 0xF, 0xF, false);  // row_shl:4
+  if ((lane & 7u) == 0) c = shift_op_x(lds, 2, c, y);
+  y = __builtin_amdgcn_update_dpp(0u, c, 0x108, 0xF, 0xF, false);  // row_shl:8
+  if ((lane & 15u) == 0) c = shift_op_x(lds, 3, c, y);
+  return c;
+}
+
+// Raw state of one block of any length (Value() seed) on the whole wave: the block front-padded
+// with zeros to V = 4096 * ceil(n / 4096) bytes; lane u hashes the pieces at 16u + 1024k of the
+// padded span (k = 0 .. V/1024 - 1) as one Horner sequence (shift 1024 between consecutive
+// pieces: the same lane-partial geometry as the body), zero-masked below p with U[z] on the piece
+// holding p; then the 6-level wave tree.  The next body's 4 pieces load while one is hashed.
+// Uniform result.
+__device__ __forceinline__ uint32_t sst_slow_block(const char* lds, const LaneTabs& lt, uint32_t u,
+                                                   uint32_t ureg, uintptr_t p, uint32_t n) {
+  if (n == 0) return 0xFFFFFFFFu;
+  const uint32_t nb = static_cast<uint32_t>((static_cast<uint64_t>(n) + 4095u) >> 12);  // 4-KiB bodies
+  const uintptr_t vbs = p + n - (static_cast<uintptr_t>(nb) << 12) + 16u * u;
+  uint32_t acc = 0;
+  MaskedPiece f[4], g[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) issue_masked(f[j], vbs + 1024u * j, p);
+  for (uint32_t q = 0; q < nb; ++q) {
+    const uint32_t qn = q + 1 < nb ? q + 1 : q;  // the last body re-reads itself (unconditional)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) issue_masked(g[j], vbs + (static_cast<uintptr_t>(qn) << 12) + 1024u * j, p);
+    uint32_t x[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) x[j] = hash_masked(lds, lt, f[j], masked_start(f[j], ureg));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc = shift_op_x(lds, PDB_SLOT_HORNER, acc, x[j]);  // shift(0) = 0 first
+#pragma unroll
+    for (int j = 0; j < 4; ++j) f[j] = g[j];
+  }
+  return __builtin_amdgcn_readfirstlane(wave_tree_dpp(lds, u, acc));
+}
+
+// A wave defers the blocks outside [4096, 4352] to a list (lane k holds the k-th, relative to
+// the workgroup's first block) and hashes them with sst_slow_block after its fast loop, so the
+// slow path's registers never compete with the pipeline's; a full list ends the fast loop, is
+// drained, and the pipeline restarts at the group it stopped at.
+constexpr uint32_t kSlowList = 64u;
+
+template <class Src, class Sink, bool kNT>
+__global__ __launch_bounds__(kThreads) void crc_sst4k_kernel(const uint32_t* __restrict__ tabs, Src src,
+                                                             uint64_t nblk, Sink sink) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
+  char* lds = reinterpret_cast<char*>(lds_words);
+  stage_tables<PDB_CAT_TREE16, PDB_CAT_S1024>(lds, tabs);  // slots 0..5 = 16..512, 6 = 1024
+  uint32_t* ctr = reinterpret_cast<uint32_t*>(lds + PDB_MAIN_BYTES + 7 * 4096u);
+  const uint64_t g_lo = nblk * blockIdx.x / gridDim.x, g_hi = nblk * (blockIdx.x + 1) / gridDim.x;
+  if (threadIdx.x == 0) *ctr = kWavesPerWg;  // next 4-block group, in groups relative to g_lo
+  const uint32_t u = threadIdx.x & 63u;
+  const uint32_t ureg = tabs[PDB_UNSHIFT_OFF + (u & 15u)];
+  __syncthreads();
+  const LaneTabs lt = lane_tabs(u);
+  uint64_t grp = g_lo + 4u * static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
+  if (grp >= g_hi) return;
+  const uintptr_t dummy = reinterpret_cast<uintptr_t>(tabs);  // >= 4 KiB + 256 B of valid bytes
+  auto next_group = [&]() -> uint64_t {
+    uint32_t r = 0;
+    if (u == 0) r = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return g_lo + 4u * static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(r));
+  };
+  // lane u holds block (group + (u & 3))'s descriptor (clamped into the range: a group past the
+  // end re-reads the last block, never used)
+  auto load_desc = [&](uint64_t gg) {
+    const uint64_t i = gg + (u & 3u);
+    return src.load(i < g_hi ? i : g_hi - 1);
+  };
+  struct Grp {
+    BlkDesc ld;      // per lane: block (u & 3)
+    uintptr_t p[4];  // uniform
+    uint32_t n[4];
+  };
+  auto finish = [&](const typename Src::Raw& raw) -> Grp {
+    keep_alive(raw);
+    Grp G;
+    G.ld = src.lane(raw);
+    const uintptr_t lp = reinterpret_cast<uintptr_t>(G.ld.p);
+    const uint32_t lo = static_cast<uint32_t>(lp), hi = static_cast<uint32_t>(static_cast<uint64_t>(lp) >> 32);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      G.p[r] = static_cast<uintptr_t>(uniform64(__builtin_amdgcn_readlane(lo, r), __builtin_amdgcn_readlane(hi, r)));
+      G.n[r] = __builtin_amdgcn_readlane(G.ld.n, r);
+    }
+    return G;
+  };
+  auto fast = [](uint32_t n) { return n - kSstMin <= kSstMax - kSstMin; };
+  auto body_at = [&](const Grp& G, int r) -> uintptr_t {
+    return fast(G.n[r]) ? G.p[r] + G.n[r] - 4096u : dummy;
+  };
+  // body loads of one block: 4 x 16 B per lane (4-B aligned) + the dword after the last piece
+  auto issue_body = [&](u32x4 (&b)[4], uint32_t& last, uintptr_t bs) {
+    const uint32_t s = static_cast<uint32_t>(bs & 3u);
+    const uintptr_t q = bs - s;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b[j] = gload128<kNT>(q + 16u * u + 1024u * j);
+    last = gload32(q + (s ? 4096u : 4092u));
+  };
+  // prefix loads of a group: row r = u >> 4 takes block r, lane w the 16 B at bs - 256 + 16w
+  auto issue_prefix = [&](MaskedPiece& f, const Grp& G) {
+    const uint32_t row = u >> 4, w = u & 15u;
+    // block `row`'s descriptor from lane `row` (bpermute: no per-lane indexing of G.p / G.n)
+    const uint64_t lp = reinterpret_cast<uintptr_t>(G.ld.p);
+    const uint32_t plo = __shfl(static_cast<uint32_t>(lp), row, 64), phi = __shfl(static_cast<uint32_t>(lp >> 32), row, 64);
+    const uintptr_t p = static_cast<uintptr_t>((static_cast<uint64_t>(phi) << 32) | plo);
+    const uint32_t n = __shfl(G.ld.n, row, 64);
+    const bool ok = fast(n);
+    const uintptr_t A = ok ? p + n - kSstMax + 16u * w : dummy + 16u * w;
+    issue_masked(f, A, ok ? p : dummy + 256u);  // a slow block's row: all masked
+  };
+
+  uint32_t slow = 0, nslow = 0;  // deferred blocks (lane k: the k-th, minus g_lo)
+  uint64_t ngrp = next_group();
+  for (;;) {  // (re)start the pipeline at grp (ngrp already taken from the counter)
+    typename Src::Raw nraw = load_desc(ngrp);
+    Grp G = finish(load_desc(grp));
+    uint32_t pre = SinkOps<Sink>::pre(sink, G.ld);
+    MaskedPiece pf;
+    issue_prefix(pf, G);
+    u32x4 buf[4];
+    uint32_t blast;
+    issue_body(buf, blast, body_at(G, 0));
+    bool done = false;
+    for (;;) {
+      // the group's prefix states: P_r in lane 16r (E_r = 0, n = 4096: the seed itself)
+      const uint32_t pref = row_tree16(lds, u, hash_masked(lds, lt, pf, masked_start(pf, ureg)));
+      uint32_t P[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) P[r] = G.n[r] == kSstMin ? 0xFFFFFFFFu : __builtin_amdgcn_readlane(pref, 16 * r);
+      Grp NG = G;
+      uint32_t npre = pre;
+      MaskedPiece npf = pf;
+      uint64_t nngrp = ngrp;
+      uint32_t part[4];
+      const uint32_t nv = static_cast<uint32_t>(g_hi - grp < 4 ? g_hi - grp : 4);
+      uint32_t fastbits = 0;  // blocks of this group on the fast path (bit r)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) fastbits |= fast(G.n[r]) ? 1u << r : 0u;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const u32x4 e0 = buf[0], e1 = buf[1], e2 = buf[2], e3 = buf[3];
+        const uint32_t cl = blast;
+        if (r < 3) {
+          issue_body(buf, blast, body_at(G, r + 1));
+        } else {  // next group: descriptors (loaded a group ago), first body, prefixes, lookahead
+          NG = finish(nraw);
+          issue_body(buf, blast, body_at(NG, 0));
+          issue_prefix(npf, NG);
+          npre = SinkOps<Sink>::pre(sink, NG.ld);
+          if (ngrp < g_hi) nngrp = next_group();
+          nraw = load_desc(nngrp < g_hi ? nngrp : ngrp);
+        }
+        part[r] = 0;
+        if ((fastbits >> r) & 1u) {
+          const uint32_t s = static_cast<uint32_t>((G.p[r] + G.n[r]) & 3u);  // bs & 3
+          uint32_t n0 = 0, n1 = 0, n2 = 0, n3 = 0;
+          if (s) {  // neighbour dwords: lane u + 1's first dword; lane 63 the next chain's lane 0
+            n0 = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(e1.x, 0), e0.x, 0x130, 0xF, 0xF, false);
+            n1 = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(e2.x, 0), e1.x, 0x130, 0xF, 0xF, false);
+            n2 = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(e3.x, 0), e2.x, 0x130, 0xF, 0xF, false);
+            n3 = __builtin_amdgcn_update_dpp(cl, e3.x, 0x130, 0xF, 0xF, false);
+          }
+          const uint32_t x0 = chain16(lds, lt, u == 0 ? P[r] : 0u, e0, n0, s);
+          const uint32_t x1 = chain16(lds, lt, 0u, e1, n1, s);
+          const uint32_t x2 = chain16(lds, lt, 0u, e2, n2, s);
+          const uint32_t x3 = chain16(lds, lt, 0u, e3, n3, s);
+          part[r] = shift_op_x(lds, PDB_SLOT_HORNER,
+                               shift_op_x(lds, PDB_SLOT_HORNER, shift_op_x(lds, PDB_SLOT_HORNER, x0, x1), x2), x3);
+        }
+      }
+      const uint32_t v = tree4_packed(lds, u, part[0], part[1], part[2], part[3]);
+      if (u < nv && ((fastbits >> u) & 1u)) SinkOps<Sink>::put(sink, grp + u, v, G.ld, pre);
+      // blocks outside [4096, 4352] join the deferred list
+      const uint32_t slowbits = ~fastbits & ((1u << nv) - 1u);
+      if (slowbits) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if ((slowbits >> r) & 1u) {
+            slow = u == nslow ? static_cast<uint32_t>(grp + r - g_lo) : slow;
+            ++nslow;
+          }
+      }
+      if (ngrp >= g_hi) {
+        done = true;
+        break;
+      }
+      grp = ngrp;
+      ngrp = nngrp;
+      G = NG;
+      pre = npre;
+      pf = npf;
+      if (nslow > kSlowList - 4u) break;  // no room for another group's slow blocks: drain first
+    }
+    // drain the deferred blocks (the pipeline's loads in flight are abandoned)
+    for (uint32_t k = 0; k < nslow; ++k) {
+      const uint64_t i = g_lo + __builtin_amdgcn_readlane(slow, k);
+      const BlkDesc d = src.lane(src.load(i));
+      const uintptr_t p = static_cast<uintptr_t>(uniform64(
+          static_cast<uint32_t>(reinterpret_cast<uintptr_t>(d.p)),
+          static_cast<uint32_t>(static_cast<uint64_t>(reinterpret_cast<uintptr_t>(d.p)) >> 32)));
+      const uint32_t dpre = SinkOps<Sink>::pre(sink, d);
+      const uint32_t raw_state = sst_slow_block(lds, lt, u, ureg, p, __builtin_amdgcn_readfirstlane(d.n));
+      if (u == 0) SinkOps<Sink>::put(sink, i, raw_state, d, dpre);
+    }
+    nslow = 0;
+    if (done) break;
   }
 }
 

@@ -16,6 +16,10 @@
 //     lists, sstable seal / verify): 4-KiB rounds of 32-B (or 16-B, nt) lane pieces with per-lane
 //     Horner shifts, a broadcast head, lane rotation, packed 4-block trees, one-item-ahead
 //     prefetch, and workgroup-local dynamic block scheduling from an LDS counter.
+//   * crc_sst4k_kernel -- sstable-sized blocks (4096..4352 B: every data block TableBuilder
+//     emits, contents + type): the block's last 4 KiB hashed with the 4-KiB path's geometry, the
+//     leading 0..256 B of 4 blocks hashed together as zero-padded pieces from an "unshifted"
+//     seed; other lengths in the same launch take a whole-wave slow path.
 //   * crc_server_kernel (crc32c_server.hip) -- the persistent scalar Extend service.
 // LDS image (crc32c_math.h): T0..T3 replicated 32x (128 KiB) so each lane reads its own bank +
 // 8 shift-operator slots (32 KiB): the whole 160 KiB of a CU; one 1024-thread workgroup per CU
@@ -106,6 +110,31 @@ __global__ __launch_bounds__(1024) void span_combine_kernel(const uint32_t* __re
   if (threadIdx.x == 0) out[0] = ~sw[0];
 }
 
+// Seal's second half (A/B variant 35): trailer word i (masked CRC, from a compact array) to
+// buf + offset_i + size_i + 1, one thread per block.
+__global__ __launch_bounds__(256) void trailer_scatter_kernel(uint8_t* __restrict__ buf,
+                                                              const pdb_block_handle* __restrict__ h,
+                                                              const uint32_t* __restrict__ crc, uint64_t n) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t* tr = buf + h[i].offset + h[i].size + 1;
+  const uint32_t m = crc[i];
+  tr[0] = static_cast<uint8_t>(m);
+  tr[1] = static_cast<uint8_t>(m >> 8);
+  tr[2] = static_cast<uint8_t>(m >> 16);
+  tr[3] = static_cast<uint8_t>(m >> 24);
+}
+
+struct NtSealSink {  // A/B variant 34: the trailer as non-temporal byte stores
+  __device__ __forceinline__ void put(uint64_t, uint32_t raw, const BlkDesc& d) const {
+    typedef __attribute__((address_space(1))) uint8_t g_u8;
+    g_u8* tr = reinterpret_cast<g_u8*>(reinterpret_cast<uintptr_t>(d.p) + d.n);
+    const uint32_t m = pdb_mask(~raw);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) __builtin_nontemporal_store(static_cast<uint8_t>(m >> (8 * k)), tr + k);
+  }
+};
+
 }  // namespace
 
 int g_fast_variant = 0;  // diagnostics: pdb_diag_set_variant()
@@ -152,6 +181,13 @@ hipError_t launch_fixed(const LaunchGeom& g, const uint32_t* d_tables, const uin
     // (per-block misalignment makes the 16-B kernel's neighbour-dword path cost more than nt
     // gains: sstable layout 6.1 vs 5.8 TB/s, profiles/r01_ab_gen_pack.json)
     const FixedSrc src{base, stride, len, (flags & PDB_CRC_USE_INIT) ? ~init : 0xFFFFFFFFu};
+    if (len - kSstMin <= kSstMax - kSstMin && src.init_raw == 0xFFFFFFFFu) {
+      // sstable-sized blocks (4096..4352 B, any alignment, Value() seed): exact 4-KiB body +
+      // batched prefix (profiles/r01_ab_sst4k.json)
+      hipLaunchKernelGGL((crc_sst4k_kernel<FixedSrc, OutSink, true>), grid, block, 0, s, d_tables, src, nblk,
+                         OutSink{out, flags});
+      return hipGetLastError();
+    }
     const bool aligned4 = ((reinterpret_cast<uintptr_t>(base) + (len & 15u)) & 3u) == 0 && (stride & 3u) == 0;
     if (aligned4)
       hipLaunchKernelGGL((crc_stream16_kernel<FixedSrc, OutSink, true, true, true>), grid, block, 0, s, d_tables,
@@ -194,6 +230,47 @@ hipError_t launch_sst(const LaunchGeom& g, const uint32_t* d_tables, uint8_t* bu
   // neighbour dwords, conditional chains, packed 4-block trees (A/B vs the 32-B kernel, variant
   // 18: +3-5 % on db_bench-sized blocks, profiles/r01_ab_sst_hooks.json)
   const SstSrc src{buf, h};
+  if (g_fast_variant == 0) {
+    // exact 4-KiB body + batched prefix for the 4096..4352-B blocks (every data block
+    // TableBuilder emits), sst_slow_block for the rest (profiles/r01_ab_sst4k.json)
+    if (seal)
+      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SealSink, true>), grid, block, 0, s, d_tables, src, n, SealSink{});
+    else
+      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstVerifySink, true>), grid, block, 0, s, d_tables, src, n,
+                         SstVerifySink{ok, nbad});
+    return hipGetLastError();
+  }
+  if (g_fast_variant >= 31 && g_fast_variant <= 35) {  // A/B diagnostics of the seal's writes
+    static uint32_t* scratch = nullptr;                 // (variants 32, 35: CRCs to a scratch array)
+    static uint64_t scratch_n = 0;
+    if ((g_fast_variant == 32 || g_fast_variant == 35) && scratch_n < n) {
+      if (scratch) (void)hipFree(scratch);
+      if (hipMalloc(&scratch, n * 4) != hipSuccess) return hipErrorOutOfMemory;
+      scratch_n = n;
+    }
+    if (!seal)  // verify: 31 default-policy loads, else the shipped kernel
+      if (g_fast_variant == 31)
+        hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstVerifySink, false>), grid, block, 0, s, d_tables, src, n,
+                           SstVerifySink{ok, nbad});
+      else
+        hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstVerifySink, true>), grid, block, 0, s, d_tables, src, n,
+                           SstVerifySink{ok, nbad});
+    else if (g_fast_variant == 31)  // default-policy loads
+      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SealSink, false>), grid, block, 0, s, d_tables, src, n, SealSink{});
+    else if (g_fast_variant == 32 || g_fast_variant == 35) {  // compact 4-B output (+ 35: scatter pass)
+      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, OutSink, true>), grid, block, 0, s, d_tables, src, n,
+                         OutSink{scratch, PDB_CRC_MASK_OUTPUT});
+      if (g_fast_variant == 35)
+        hipLaunchKernelGGL(trailer_scatter_kernel, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256), 0, s, buf,
+                           h, scratch, n);
+    } else if (g_fast_variant == 34)
+      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, NtSealSink, true>), grid, block, 0, s, d_tables, src, n,
+                         NtSealSink{});
+    else  // 33: the seal's kernel with its stores dropped (a verify with nowhere to report)
+      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstVerifySink, true>), grid, block, 0, s, d_tables, src, n,
+                         SstVerifySink{nullptr, nullptr});
+    return hipGetLastError();
+  }
   if (g_fast_variant == 18) {
     if (seal)
       hipLaunchKernelGGL((crc_stream_kernel<SstSrc, SealSink, 0, true, true>), grid, block, 0, s, d_tables, src, n,
@@ -217,8 +294,12 @@ hipError_t launch_sst_masked(const LaunchGeom& g, const uint32_t* d_tables, uint
   if (n == 0) return hipSuccess;
   const dim3 grid(grid_for(g, n)), block(kThreads);
   // the seal's CRCs into a compact array (host seal: 4 B per block back across PCIe, not the span)
-  hipLaunchKernelGGL((crc_stream16_kernel<SstSrc, OutSink, true, true, true>), grid, block, 0, s, d_tables,
-                     SstSrc{buf, h}, n, OutSink{out, PDB_CRC_MASK_OUTPUT});
+  if (g_fast_variant == 0)
+    hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, OutSink, true>), grid, block, 0, s, d_tables, SstSrc{buf, h}, n,
+                       OutSink{out, PDB_CRC_MASK_OUTPUT});
+  else
+    hipLaunchKernelGGL((crc_stream16_kernel<SstSrc, OutSink, true, true, true>), grid, block, 0, s, d_tables,
+                       SstSrc{buf, h}, n, OutSink{out, PDB_CRC_MASK_OUTPUT});
   return hipGetLastError();
 }
 

@@ -70,5 +70,11 @@ static const unsigned long long kPdbCatDist[PDB_NCAT] = {16,   32,   64,   128, 
 #define PDB_POW2_WORDS (64u * 1024u)
 #define PDB_SPAN_MIN_SEG_LOG2 16      /* segments of >= 64 KiB */
 #define PDB_SPAN_MAX_SEGS_LOG2 14     /* <= 16384 segments: the combine tree fits 64 KiB of LDS */
-/* Device table source: T0..T3 (1024 u32) then the catalog (PDB_NCAT * 1024 u32). */
-#define PDB_TABLE_WORDS (1024u + PDB_NCAT * 1024u)
+/* Unshifted seeds (crc_sst4k_kernel): U[z] = shift^-z(0xFFFFFFFF), z = 0..16 -- the state that
+ * reaches Value()'s starting state 0xFFFFFFFF after z zero bytes, so a block can be hashed
+ * front-padded with z zeros (R(0^z || X) from U[z] == R(X) from 0xFFFFFFFF). */
+#define PDB_UNSHIFT_OFF (1024u + PDB_NCAT * 1024u)
+#define PDB_UNSHIFT_WORDS 64u
+/* Device table source: T0..T3 (1024 u32), the catalog (PDB_NCAT * 1024 u32), the unshifted
+ * seeds (64 u32, 17 used). */
+#define PDB_TABLE_WORDS (PDB_UNSHIFT_OFF + PDB_UNSHIFT_WORDS)

@@ -64,8 +64,18 @@ uint32_t host_shift(uint32_t c, uint64_t nbytes) {
   return mat_vec(mat_pow(one_zero_byte(t0), nbytes), c);
 }
 
+// One zero byte backwards: the state c with T0[c & 0xff] ^ (c >> 8) == c'.  The top byte of c'
+// is the top byte of T0[c & 0xff] (c >> 8 has none), and T0's top bytes are a permutation of
+// 0..255, so the low byte of c is found by lookup and the rest follows.
+static uint32_t unshift_byte(const uint32_t* t0, uint32_t c1) {
+  uint32_t idx = 0;
+  while ((t0[idx] >> 24) != (c1 >> 24)) ++idx;
+  return ((c1 ^ t0[idx]) << 8) | idx;
+}
+
 // Fills `out` (PDB_TABLE_WORDS u32): [T0|T1|T2|T3] then the PDB_NCAT catalog operators, each as
-// 4 sub-tables j=0..3 of 256 entries: op[j][b] = shift(b << 8j, D).
+// 4 sub-tables j=0..3 of 256 entries: op[j][b] = shift(b << 8j, D); then the unshifted seeds
+// U[z] = shift^-z(0xFFFFFFFF), z = 0..16 (PDB_UNSHIFT_OFF).
 void build_device_tables(uint32_t* out) {
   uint32_t t[4][256];
   build_byte_table(t[0]);
@@ -80,6 +90,15 @@ void build_device_tables(uint32_t* out) {
     for (int j = 0; j < 4; ++j)
       for (uint32_t b = 0; b < 256; ++b) op[j * 256 + b] = mat_vec(m, b << (8 * j));
   }
+  uint32_t* un = out + PDB_UNSHIFT_OFF;
+  memset(un, 0, PDB_UNSHIFT_WORDS * sizeof(uint32_t));
+  uint32_t c = 0xFFFFFFFFu;
+  for (uint32_t z = 0; z <= 16; ++z) {
+    un[z] = c;
+    c = unshift_byte(t[0], c);
+  }
+  for (uint32_t z = 0; z <= 16; ++z)  // shift(U[z], z) == 0xFFFFFFFF
+    if (mat_vec(mat_pow(z1, z), un[z]) != 0xFFFFFFFFu) __builtin_trap();
 }
 
 // 64 operators (PDB_POW2_WORDS u32): op k = shift by 2^k bytes, 4 x 256 entries each, for the
