@@ -196,7 +196,7 @@ def main():
         out = torch.empty(nblk, dtype=torch.int32, device=dev)
 
         def step():
-            crc32c.batch(data, d_blk, out=out)
+            crc32c.batch(data, d_blk, out=out, size_hint="1k")
 
         workload = {"workload": "wal: 4 GiB log image, 32-KiB blocks, 1055-B records -> type||payload "
                                 "fragments (descriptor list)", "blocks_per_gpu": nblk, "bytes_per_gpu": hashed}
@@ -311,7 +311,7 @@ def main():
                 "traffic": traffic,
                 "kernel": {"c2": "crc_pack4k_kernel<1,4,nt>", "sstable": "crc_sst4k_kernel<FixedSrc,OutSink,nt>",
                            "c3": "crc_stream16_kernel<DescSrc,OutSink,dyn,nt,pack>",
-                           "wal": "crc_stream16_kernel<DescSrc,OutSink,dyn,nt,pack>",
+                           "wal": "crc_sst1k_kernel<DescSrc,OutSink,nt>",
                            "sst_verify": "crc_sst4k_kernel<SstSrc,SstVerifySink,nt>",
                            "sst_seal": "crc_sst4k_kernel<SstSrc,SealSink,nt>"}[args.workload],
                 "algorithmic_bytes_per_launch": algo_bytes,

@@ -27,6 +27,9 @@ from ._native import PdbError, check, lib
 
 MASK_OUTPUT = 0x1  # PDB_CRC_MASK_OUTPUT
 USE_INIT = 0x2  # PDB_CRC_USE_INIT
+SIZE_1K = 0x4  # PDB_CRC_SIZE_1K: most blocks 1024..1280 B (WAL records) -- a speed hint only
+SIZE_4K = 0x8  # PDB_CRC_SIZE_4K: most blocks 4096..4352 B (sstable data blocks)
+_SIZE_HINT = {None: 0, "1k": SIZE_1K, "4k": SIZE_4K}
 K_MASK_DELTA = 0xA282EAD8  # util/crc32c.h:24
 
 BLK_DTYPE = np.dtype([("off", "<u8"), ("len", "<u4"), ("init", "<u4")])  # == pdb_blk (16 B)
@@ -145,24 +148,27 @@ def batch_fixed(d_base, stride: int, length: int, nblk: int, *, masked: bool = F
     return out
 
 
-def batch(d_base, d_blocks, *, masked: bool = False, use_init: bool = False, out=None, stream=None):
-    """CRC of each descriptor (pdb_blk, 16 B each, device tensor) -> int32 tensor."""
+def batch(d_base, d_blocks, *, masked: bool = False, use_init: bool = False, out=None, stream=None,
+          size_hint: str | None = None):
+    """CRC of each descriptor (pdb_blk, 16 B each, device tensor) -> int32 tensor.  size_hint "1k"
+    / "4k" selects the sized kernel for batches of mostly WAL-record / sstable-block lengths (the
+    device cannot see the lengths before launching; the results do not depend on it)."""
     n = d_blocks.numel() * d_blocks.element_size() // 16
     out = _out_tensor(n, d_base, out)
-    flags = (MASK_OUTPUT if masked else 0) | (USE_INIT if use_init else 0)
+    flags = (MASK_OUTPUT if masked else 0) | (USE_INIT if use_init else 0) | _SIZE_HINT[size_hint]
     check(lib().pdb_crc32c_batch_device(
         _dev_ptr(d_base), _dev_ptr(d_blocks), n, flags, _dev_ptr(out), _stream_ptr(stream)))
     return out
 
 
 def verify(d_base, d_blocks, d_expected, *, masked: bool = True, use_init: bool = False,
-           stream=None):
+           stream=None, size_hint: str | None = None):
     """(ok uint8 tensor, nbad int32 tensor[1]) -- ReadBlock's check for many blocks at once."""
     torch = _torch()
     n = d_blocks.numel() * d_blocks.element_size() // 16
     ok = torch.empty(n, dtype=torch.uint8, device=d_base.device)
     nbad = torch.zeros(1, dtype=torch.int32, device=d_base.device)
-    flags = (MASK_OUTPUT if masked else 0) | (USE_INIT if use_init else 0)
+    flags = (MASK_OUTPUT if masked else 0) | (USE_INIT if use_init else 0) | _SIZE_HINT[size_hint]
     check(lib().pdb_crc32c_verify_device(
         _dev_ptr(d_base), _dev_ptr(d_blocks), n, flags, _dev_ptr(d_expected), _dev_ptr(ok),
         _dev_ptr(nbad), _stream_ptr(stream)))

@@ -454,6 +454,9 @@ struct DescSrc {
     return {base + uniform64(r.x, r.y), len, (flags & PDB_CRC_USE_INIT) ? ~init : 0xFFFFFFFFu};
   }
   __device__ __forceinline__ BlkDesc get(uint64_t i) const { return finish(load(i)); }
+  __device__ __forceinline__ BlkDesc lane(const Raw& r) const {  // per-lane fields (no readfirstlane)
+    return {base + ((static_cast<uint64_t>(r.y) << 32) | r.x), r.z, (flags & PDB_CRC_USE_INIT) ? ~r.w : 0xFFFFFFFFu};
+  }
 };
 
 // sstable handle: CRC over contents || type (table/table_builder.cc:197-198; format.cc:98).
@@ -526,15 +529,29 @@ struct SstVerifySink {
 // addresses are integers; a flat access would also count in lgkmcnt and stall LDS lookups).
 template <class Sink>
 struct SinkOps {
-  __device__ static __forceinline__ uint32_t pre(const Sink&, const BlkDesc&) { return 0u; }
+  __device__ static __forceinline__ uint32_t pre(const Sink&, uint64_t, const BlkDesc&) { return 0u; }
   __device__ static __forceinline__ void put(const Sink& k, uint64_t i, uint32_t raw, const BlkDesc& d, uint32_t) {
     k.put(i, raw, d);
   }
 };
 
 template <>
+struct SinkOps<VerifySink> {  // the expected CRC, loaded a group ahead
+  __device__ static __forceinline__ uint32_t pre(const VerifySink& k, uint64_t i, const BlkDesc&) {
+    typedef __attribute__((address_space(1))) const uint32_t g_u32_;
+    return *reinterpret_cast<g_u32_*>(reinterpret_cast<uintptr_t>(k.expected + i));
+  }
+  __device__ static __forceinline__ void put(const VerifySink& k, uint64_t i, uint32_t raw, const BlkDesc&,
+                                             uint32_t expected) {
+    const bool good = finalize(raw, k.flags) == expected;
+    if (k.ok) k.ok[i] = good ? 1 : 0;
+    if (!good && k.nbad) atomicAdd(k.nbad, 1u);
+  }
+};
+
+template <>
 struct SinkOps<SealSink> {
-  __device__ static __forceinline__ uint32_t pre(const SealSink&, const BlkDesc&) { return 0u; }
+  __device__ static __forceinline__ uint32_t pre(const SealSink&, uint64_t, const BlkDesc&) { return 0u; }
   __device__ static __forceinline__ void put(const SealSink&, uint64_t, uint32_t raw, const BlkDesc& d, uint32_t) {
     typedef __attribute__((address_space(1))) uint8_t g_u8;
     g_u8* tr = reinterpret_cast<g_u8*>(reinterpret_cast<uintptr_t>(d.p) + d.n);
@@ -549,7 +566,7 @@ struct SinkOps<SealSink> {
 template <>
 struct SinkOps<SstVerifySink> {
   // the stored trailer word at p + n (any alignment): the two aligned dwords holding it
-  __device__ static __forceinline__ uint32_t pre(const SstVerifySink&, const BlkDesc& d) {
+  __device__ static __forceinline__ uint32_t pre(const SstVerifySink&, uint64_t, const BlkDesc& d) {
     typedef __attribute__((address_space(1))) const uint32_t g_u32_;
     const uintptr_t a = reinterpret_cast<uintptr_t>(d.p) + d.n;
     const uint32_t s = static_cast<uint32_t>(a & 3u);
@@ -1089,12 +1106,14 @@ __global__ __launch_bounds__(kThreads) void crc_stream16_kernel(const uint32_t* 
 // Workgroup g owns blocks [g*N/G, (g+1)*N/G) and its waves take 4-block groups from an LDS
 // counter (slot 7; the measured locality of crc_pack4k_dyn_kernel).  Loads run one block ahead
 // (body) and one group ahead (descriptors, prefixes), every one unmasked and unconditional.
-// Blocks outside [4096, 4352] (an index / metaindex / a table's last data block) take
-// sst_slow_block on the same wave: the block front-padded to whole 4-KiB bodies, one Horner
-// sequence of 16-B pieces at stride 1024 per lane, then one wave tree; its raw state is parked
-// in lane 63 (the packed tree's unshifted position).
-// Valid only for Value()-seeded CRCs (init 0xFFFFFFFF): SstSrc always, FixedSrc without an Extend
-// seed.
+// Blocks outside [4096, 4352] (an index / metaindex / a table's last data block) are deferred
+// and hashed after the loop by the slow path (below).
+// crc_sst1k_kernel is the same design for ~1-KiB blocks (WAL physical records: type || fragment
+// of a ~1-KiB write batch, db/log_writer.cc:111-121): body = the last 1 KiB (one chain per lane,
+// the 4 blocks of a group in 4 chains), fast range [1024, 1280], the next group's 4 bodies in
+// flight while one group is hashed.
+// Valid only for Value()-seeded CRCs (init 0xFFFFFFFF): SstSrc always, FixedSrc / DescSrc without
+// an Extend seed.
 constexpr uint32_t kSstMin = 4096u, kSstMax = 4096u + 256u;
 
 // The 16 bytes at A (any alignment) with the bytes below `lo` zeroed.  Never reads an aligned
@@ -1179,45 +1198,67 @@ __device__ __forceinline__ uint32_t row_tree16(const char* lds, uint32_t lane, u
   return c;
 }
 
-// Raw state of one block of any length (Value() seed) on the whole wave: the block front-padded
-// with zeros to V = 4096 * ceil(n / 4096) bytes; lane u hashes the pieces at 16u + 1024k of the
-// padded span (k = 0 .. V/1024 - 1) as one Horner sequence (shift 1024 between consecutive
-// pieces: the same lane-partial geometry as the body), zero-masked below p with U[z] on the piece
-// holding p; then the 6-level wave tree.  The next body's 4 pieces load while one is hashed.
-// Uniform result.
-__device__ __forceinline__ uint32_t sst_slow_block(const char* lds, const LaneTabs& lt, uint32_t u,
-                                                   uint32_t ureg, uintptr_t p, uint32_t n) {
+// Slow path: the raw state of one block of any length (Value() seed) on the whole wave.  The
+// block is front-padded with zeros to V = 4096 * ceil(n / 4096) bytes; lane u hashes the pieces at
+// 16u + 1024k of the padded span (k = 0 .. V/1024 - 1) as one Horner sequence (shift 1024 between
+// consecutive pieces: the body's lane-partial geometry), zero-masked below p with U[z] on the piece
+// holding p; then the 6-level wave tree.  Rows (1-KiB steps) wholly below p are skipped (a 300-B
+// WAL fragment costs one chain, not four).  Split in two so the drain can issue block k+1's first
+// body while block k is hashed: slow_issue (loads of the first 4-KiB body) and slow_finish.
+struct SlowFirst {
+  MaskedPiece f[4];
+};
+
+__device__ __forceinline__ uintptr_t slow_vbs(uintptr_t p, uint32_t n) {
+  const uint32_t nb = static_cast<uint32_t>((static_cast<uint64_t>(n) + 4095u) >> 12);
+  return p + n - (static_cast<uintptr_t>(nb) << 12);
+}
+
+__device__ __forceinline__ void slow_issue(SlowFirst& sf, uintptr_t p, uint32_t n, uint32_t u) {
+  const uintptr_t v = slow_vbs(p, n) + 16u * u;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) issue_masked(sf.f[j], v + 1024u * j, p);
+}
+
+__device__ __forceinline__ uint32_t slow_finish(const char* lds, const LaneTabs& lt, uint32_t u, uint32_t ureg,
+                                                const SlowFirst& sf, uintptr_t p, uint32_t n) {
   if (n == 0) return 0xFFFFFFFFu;
-  const uint32_t nb = static_cast<uint32_t>((static_cast<uint64_t>(n) + 4095u) >> 12);  // 4-KiB bodies
-  const uintptr_t vbs = p + n - (static_cast<uintptr_t>(nb) << 12) + 16u * u;
+  const uint32_t nb = static_cast<uint32_t>((static_cast<uint64_t>(n) + 4095u) >> 12);
+  const uintptr_t vbs = slow_vbs(p, n);
   uint32_t acc = 0;
-  MaskedPiece f[4], g[4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) issue_masked(f[j], vbs + 1024u * j, p);
-  for (uint32_t q = 0; q < nb; ++q) {
-    const uint32_t qn = q + 1 < nb ? q + 1 : q;  // the last body re-reads itself (unconditional)
+  for (int j = 0; j < 4; ++j)
+    if (vbs + 1024u * (j + 1) > p)  // wave-uniform: a row holding block bytes
+      acc = shift_op_x(lds, PDB_SLOT_HORNER, acc, hash_masked(lds, lt, sf.f[j], masked_start(sf.f[j], ureg)));
+  if (nb > 1) {  // full bodies, the next one loading while one is hashed
+    MaskedPiece f[4], g[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) issue_masked(g[j], vbs + (static_cast<uintptr_t>(qn) << 12) + 1024u * j, p);
-    uint32_t x[4];
+    for (int j = 0; j < 4; ++j) issue_masked(f[j], vbs + 4096u + 16u * u + 1024u * j, p);
+    for (uint32_t q = 1; q < nb; ++q) {
+      const uint32_t qn = q + 1 < nb ? q + 1 : q;  // the last body re-reads itself (unconditional)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) x[j] = hash_masked(lds, lt, f[j], masked_start(f[j], ureg));
+      for (int j = 0; j < 4; ++j) issue_masked(g[j], vbs + (static_cast<uintptr_t>(qn) << 12) + 16u * u + 1024u * j, p);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc = shift_op_x(lds, PDB_SLOT_HORNER, acc, x[j]);  // shift(0) = 0 first
+      for (int j = 0; j < 4; ++j) acc = shift_op_x(lds, PDB_SLOT_HORNER, acc, hash_masked(lds, lt, f[j], 0u));
 #pragma unroll
-    for (int j = 0; j < 4; ++j) f[j] = g[j];
+      for (int j = 0; j < 4; ++j) f[j] = g[j];
+    }
   }
   return __builtin_amdgcn_readfirstlane(wave_tree_dpp(lds, u, acc));
 }
 
-// A wave defers the blocks outside [4096, 4352] to a list (lane k holds the k-th, relative to
-// the workgroup's first block) and hashes them with sst_slow_block after its fast loop, so the
-// slow path's registers never compete with the pipeline's; a full list ends the fast loop, is
-// drained, and the pipeline restarts at the group it stopped at.
+// A wave defers the blocks outside the fast range to a list (lane k holds the k-th, relative to
+// the workgroup's first block) and hashes them with the slow path after its fast loop, so the slow
+// path's registers never compete with the pipeline's; a full list ends the fast loop, is drained,
+// and the pipeline restarts at the group it stopped at.
 constexpr uint32_t kSlowList = 64u;
 
-template <class Src, class Sink, bool kNT>
-__global__ __launch_bounds__(kThreads) void crc_sst4k_kernel(const uint32_t* __restrict__ tabs, Src src,
-                                                             uint64_t nblk, Sink sink) {
+// kRows = body size in KiB: 4 (crc_sst4k_kernel) or 1 (crc_sst1k_kernel).
+template <class Src, class Sink, bool kNT, int kRows>
+__device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ tabs, Src src, uint64_t nblk,
+                                                  Sink sink) {
+  static_assert(kRows == 1 || kRows == 4, "bodies of 1 or 4 KiB");
+  constexpr uint32_t kBody = 1024u * kRows, kMin = kBody, kMax = kBody + 256u;
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
   char* lds = reinterpret_cast<char*>(lds_words);
   stage_tables<PDB_CAT_TREE16, PDB_CAT_S1024>(lds, tabs);  // slots 0..5 = 16..512, 6 = 1024
@@ -1238,10 +1279,11 @@ __global__ __launch_bounds__(kThreads) void crc_sst4k_kernel(const uint32_t* __r
   };
   // lane u holds block (group + (u & 3))'s descriptor (clamped into the range: a group past the
   // end re-reads the last block, never used)
-  auto load_desc = [&](uint64_t gg) {
+  auto lane_idx = [&](uint64_t gg) -> uint64_t {
     const uint64_t i = gg + (u & 3u);
-    return src.load(i < g_hi ? i : g_hi - 1);
+    return i < g_hi ? i : g_hi - 1;
   };
+  auto load_desc = [&](uint64_t gg) { return src.load(lane_idx(gg)); };
   struct Grp {
     BlkDesc ld;      // per lane: block (u & 3)
     uintptr_t p[4];  // uniform
@@ -1260,17 +1302,17 @@ __global__ __launch_bounds__(kThreads) void crc_sst4k_kernel(const uint32_t* __r
     }
     return G;
   };
-  auto fast = [](uint32_t n) { return n - kSstMin <= kSstMax - kSstMin; };
+  auto fast = [](uint32_t n) { return n - kMin <= kMax - kMin; };
   auto body_at = [&](const Grp& G, int r) -> uintptr_t {
-    return fast(G.n[r]) ? G.p[r] + G.n[r] - 4096u : dummy;
+    return fast(G.n[r]) ? G.p[r] + G.n[r] - kBody : dummy;
   };
-  // body loads of one block: 4 x 16 B per lane (4-B aligned) + the dword after the last piece
-  auto issue_body = [&](u32x4 (&b)[4], uint32_t& last, uintptr_t bs) {
+  // body loads of one block: kRows x 16 B per lane (4-B aligned) + the dword after the last piece
+  auto issue_body = [&](u32x4* b, uint32_t& last, uintptr_t bs) {
     const uint32_t s = static_cast<uint32_t>(bs & 3u);
     const uintptr_t q = bs - s;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) b[j] = gload128<kNT>(q + 16u * u + 1024u * j);
-    last = gload32(q + (s ? 4096u : 4092u));
+    for (int j = 0; j < kRows; ++j) b[j] = gload128<kNT>(q + 16u * u + 1024u * j);
+    last = gload32(q + (s ? kBody : kBody - 4u));
   };
   // prefix loads of a group: row r = u >> 4 takes block r, lane w the 16 B at bs - 256 + 16w
   auto issue_prefix = [&](MaskedPiece& f, const Grp& G) {
@@ -1281,106 +1323,200 @@ __global__ __launch_bounds__(kThreads) void crc_sst4k_kernel(const uint32_t* __r
     const uintptr_t p = static_cast<uintptr_t>((static_cast<uint64_t>(phi) << 32) | plo);
     const uint32_t n = __shfl(G.ld.n, row, 64);
     const bool ok = fast(n);
-    const uintptr_t A = ok ? p + n - kSstMax + 16u * w : dummy + 16u * w;
+    const uintptr_t A = ok ? p + n - kMax + 16u * w : dummy + 16u * w;
     issue_masked(f, A, ok ? p : dummy + 256u);  // a slow block's row: all masked
+  };
+  // the group's prefix states: P_r in lane 16r (E_r = 0, n = kBody: the seed itself)
+  auto prefix_states = [&](const MaskedPiece& pf, const Grp& G, uint32_t (&P)[4]) {
+    const uint32_t pref = row_tree16(lds, u, hash_masked(lds, lt, pf, masked_start(pf, ureg)));
+#pragma unroll
+    for (int r = 0; r < 4; ++r) P[r] = G.n[r] == kMin ? 0xFFFFFFFFu : __builtin_amdgcn_readlane(pref, 16 * r);
+  };
+  // one body's lane partial: chains j (16-B pieces at bs + 16u + 1024j) with the DPP neighbour
+  // dword, Horner-folded with shift 1024, P injected as lane 0's start
+  auto body_partial = [&](const u32x4* e, uint32_t cl, uint32_t s, uint32_t P) -> uint32_t {
+    uint32_t nx[kRows];
+#pragma unroll
+    for (int j = 0; j < kRows; ++j) nx[j] = 0;
+    if (s) {  // neighbour dwords: lane u + 1's first dword; lane 63 the next chain's lane 0
+#pragma unroll
+      for (int j = 0; j < kRows; ++j)
+        nx[j] = __builtin_amdgcn_update_dpp(j + 1 < kRows ? __builtin_amdgcn_readlane(e[j + 1 < kRows ? j + 1 : j].x, 0) : cl,
+                                            e[j].x, 0x130, 0xF, 0xF, false);
+    }
+    uint32_t a = chain16(lds, lt, u == 0 ? P : 0u, e[0], nx[0], s);
+#pragma unroll
+    for (int j = 1; j < kRows; ++j) a = shift_op_x(lds, PDB_SLOT_HORNER, a, chain16(lds, lt, 0u, e[j], nx[j], s));
+    return a;
   };
 
   uint32_t slow = 0, nslow = 0;  // deferred blocks (lane k: the k-th, minus g_lo)
+  auto defer = [&](const Grp& G, uint32_t fastbits, uint32_t nv) {
+    const uint32_t slowbits = ~fastbits & ((1u << nv) - 1u);
+    if (slowbits) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if ((slowbits >> r) & 1u) {
+          slow = u == nslow ? static_cast<uint32_t>(grp + r - g_lo) : slow;
+          ++nslow;
+        }
+    }
+  };
+  auto fast_bits = [&](const Grp& G) {
+    uint32_t fb = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) fb |= fast(G.n[r]) ? 1u << r : 0u;
+    return fb;
+  };
   uint64_t ngrp = next_group();
   for (;;) {  // (re)start the pipeline at grp (ngrp already taken from the counter)
     typename Src::Raw nraw = load_desc(ngrp);
     Grp G = finish(load_desc(grp));
-    uint32_t pre = SinkOps<Sink>::pre(sink, G.ld);
+    uint32_t pre = SinkOps<Sink>::pre(sink, lane_idx(grp), G.ld);
     MaskedPiece pf;
     issue_prefix(pf, G);
-    u32x4 buf[4];
-    uint32_t blast;
-    issue_body(buf, blast, body_at(G, 0));
     bool done = false;
-    for (;;) {
-      // the group's prefix states: P_r in lane 16r (E_r = 0, n = 4096: the seed itself)
-      const uint32_t pref = row_tree16(lds, u, hash_masked(lds, lt, pf, masked_start(pf, ureg)));
-      uint32_t P[4];
+    if constexpr (kRows == 4) {
+      // bodies one block ahead; the next group's descriptors, prefixes and first body at block 3
+      u32x4 buf[4];
+      uint32_t blast;
+      issue_body(buf, blast, body_at(G, 0));
+      for (;;) {
+        uint32_t P[4];
+        prefix_states(pf, G, P);
+        Grp NG = G;
+        uint32_t npre = pre;
+        MaskedPiece npf = pf;
+        uint64_t nngrp = ngrp;
+        uint32_t part[4];
+        const uint32_t nv = static_cast<uint32_t>(g_hi - grp < 4 ? g_hi - grp : 4);
+        const uint32_t fastbits = fast_bits(G);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) P[r] = G.n[r] == kSstMin ? 0xFFFFFFFFu : __builtin_amdgcn_readlane(pref, 16 * r);
-      Grp NG = G;
-      uint32_t npre = pre;
-      MaskedPiece npf = pf;
-      uint64_t nngrp = ngrp;
-      uint32_t part[4];
-      const uint32_t nv = static_cast<uint32_t>(g_hi - grp < 4 ? g_hi - grp : 4);
-      uint32_t fastbits = 0;  // blocks of this group on the fast path (bit r)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) fastbits |= fast(G.n[r]) ? 1u << r : 0u;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const u32x4 e0 = buf[0], e1 = buf[1], e2 = buf[2], e3 = buf[3];
-        const uint32_t cl = blast;
-        if (r < 3) {
-          issue_body(buf, blast, body_at(G, r + 1));
-        } else {  // next group: descriptors (loaded a group ago), first body, prefixes, lookahead
-          NG = finish(nraw);
-          issue_body(buf, blast, body_at(NG, 0));
-          issue_prefix(npf, NG);
-          npre = SinkOps<Sink>::pre(sink, NG.ld);
-          if (ngrp < g_hi) nngrp = next_group();
-          nraw = load_desc(nngrp < g_hi ? nngrp : ngrp);
-        }
-        part[r] = 0;
-        if ((fastbits >> r) & 1u) {
-          const uint32_t s = static_cast<uint32_t>((G.p[r] + G.n[r]) & 3u);  // bs & 3
-          uint32_t n0 = 0, n1 = 0, n2 = 0, n3 = 0;
-          if (s) {  // neighbour dwords: lane u + 1's first dword; lane 63 the next chain's lane 0
-            n0 = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(e1.x, 0), e0.x, 0x130, 0xF, 0xF, false);
-            n1 = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(e2.x, 0), e1.x, 0x130, 0xF, 0xF, false);
-            n2 = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(e3.x, 0), e2.x, 0x130, 0xF, 0xF, false);
-            n3 = __builtin_amdgcn_update_dpp(cl, e3.x, 0x130, 0xF, 0xF, false);
+        for (int r = 0; r < 4; ++r) {
+          const u32x4 e[4] = {buf[0], buf[1], buf[2], buf[3]};
+          const uint32_t cl = blast;
+          if (r < 3) {
+            issue_body(buf, blast, body_at(G, r + 1));
+          } else {
+            NG = finish(nraw);
+            issue_body(buf, blast, body_at(NG, 0));
+            issue_prefix(npf, NG);
+            npre = SinkOps<Sink>::pre(sink, lane_idx(ngrp), NG.ld);
+            if (ngrp < g_hi) nngrp = next_group();
+            nraw = load_desc(nngrp < g_hi ? nngrp : ngrp);
           }
-          const uint32_t x0 = chain16(lds, lt, u == 0 ? P[r] : 0u, e0, n0, s);
-          const uint32_t x1 = chain16(lds, lt, 0u, e1, n1, s);
-          const uint32_t x2 = chain16(lds, lt, 0u, e2, n2, s);
-          const uint32_t x3 = chain16(lds, lt, 0u, e3, n3, s);
-          part[r] = shift_op_x(lds, PDB_SLOT_HORNER,
-                               shift_op_x(lds, PDB_SLOT_HORNER, shift_op_x(lds, PDB_SLOT_HORNER, x0, x1), x2), x3);
+          part[r] = 0;
+          if ((fastbits >> r) & 1u)
+            part[r] = body_partial(e, cl, static_cast<uint32_t>((G.p[r] + G.n[r]) & 3u), P[r]);
         }
+        const uint32_t v = tree4_packed(lds, u, part[0], part[1], part[2], part[3]);
+        if (u < nv && ((fastbits >> u) & 1u)) SinkOps<Sink>::put(sink, grp + u, v, G.ld, pre);
+        defer(G, fastbits, nv);
+        if (ngrp >= g_hi) {
+          done = true;
+          break;
+        }
+        grp = ngrp;
+        ngrp = nngrp;
+        G = NG;
+        pre = npre;
+        pf = npf;
+        if (nslow > kSlowList - 4u) break;  // no room for another group's slow blocks: drain first
       }
-      const uint32_t v = tree4_packed(lds, u, part[0], part[1], part[2], part[3]);
-      if (u < nv && ((fastbits >> u) & 1u)) SinkOps<Sink>::put(sink, grp + u, v, G.ld, pre);
-      // blocks outside [4096, 4352] join the deferred list
-      const uint32_t slowbits = ~fastbits & ((1u << nv) - 1u);
-      if (slowbits) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if ((slowbits >> r) & 1u) {
-            slow = u == nslow ? static_cast<uint32_t>(grp + r - g_lo) : slow;
-            ++nslow;
-          }
+    } else {
+      // 1-KiB bodies: the next group's 4 bodies, prefixes and descriptors issued at the top of a
+      // group (4 KiB + 1 KiB in flight per wave while this group hashes)
+      u32x4 b0, b1, b2, b3;
+      uint32_t l0, l1, l2, l3;
+      issue_body(&b0, l0, body_at(G, 0));
+      issue_body(&b1, l1, body_at(G, 1));
+      issue_body(&b2, l2, body_at(G, 2));
+      issue_body(&b3, l3, body_at(G, 3));
+      for (;;) {
+        const u32x4 c0 = b0, c1 = b1, c2 = b2, c3 = b3;
+        const uint32_t cl0 = l0, cl1 = l1, cl2 = l2, cl3 = l3;
+        const MaskedPiece cpf = pf;
+        const Grp NG = finish(nraw);
+        issue_body(&b0, l0, body_at(NG, 0));
+        issue_body(&b1, l1, body_at(NG, 1));
+        issue_body(&b2, l2, body_at(NG, 2));
+        issue_body(&b3, l3, body_at(NG, 3));
+        issue_prefix(pf, NG);
+        const uint32_t npre = SinkOps<Sink>::pre(sink, lane_idx(ngrp), NG.ld);
+        uint64_t nngrp = ngrp;
+        if (ngrp < g_hi) nngrp = next_group();
+        nraw = load_desc(nngrp < g_hi ? nngrp : ngrp);
+        uint32_t P[4];
+        prefix_states(cpf, G, P);
+        const uint32_t nv = static_cast<uint32_t>(g_hi - grp < 4 ? g_hi - grp : 4);
+        const uint32_t fastbits = fast_bits(G);
+        uint32_t part[4] = {0, 0, 0, 0};
+        if (fastbits & 1u) part[0] = body_partial(&c0, cl0, static_cast<uint32_t>((G.p[0] + G.n[0]) & 3u), P[0]);
+        if (fastbits & 2u) part[1] = body_partial(&c1, cl1, static_cast<uint32_t>((G.p[1] + G.n[1]) & 3u), P[1]);
+        if (fastbits & 4u) part[2] = body_partial(&c2, cl2, static_cast<uint32_t>((G.p[2] + G.n[2]) & 3u), P[2]);
+        if (fastbits & 8u) part[3] = body_partial(&c3, cl3, static_cast<uint32_t>((G.p[3] + G.n[3]) & 3u), P[3]);
+        const uint32_t v = tree4_packed(lds, u, part[0], part[1], part[2], part[3]);
+        if (u < nv && ((fastbits >> u) & 1u)) SinkOps<Sink>::put(sink, grp + u, v, G.ld, pre);
+        defer(G, fastbits, nv);
+        if (ngrp >= g_hi) {
+          done = true;
+          break;
+        }
+        grp = ngrp;
+        ngrp = nngrp;
+        G = NG;
+        pre = npre;
+        if (nslow > kSlowList - 4u) break;  // drain first (pf already holds grp's prefixes)
       }
-      if (ngrp >= g_hi) {
-        done = true;
-        break;
-      }
-      grp = ngrp;
-      ngrp = nngrp;
-      G = NG;
-      pre = npre;
-      pf = npf;
-      if (nslow > kSlowList - 4u) break;  // no room for another group's slow blocks: drain first
     }
-    // drain the deferred blocks (the pipeline's loads in flight are abandoned)
-    for (uint32_t k = 0; k < nslow; ++k) {
-      const uint64_t i = g_lo + __builtin_amdgcn_readlane(slow, k);
-      const BlkDesc d = src.lane(src.load(i));
-      const uintptr_t p = static_cast<uintptr_t>(uniform64(
-          static_cast<uint32_t>(reinterpret_cast<uintptr_t>(d.p)),
-          static_cast<uint32_t>(static_cast<uint64_t>(reinterpret_cast<uintptr_t>(d.p)) >> 32)));
-      const uint32_t dpre = SinkOps<Sink>::pre(sink, d);
-      const uint32_t raw_state = sst_slow_block(lds, lt, u, ureg, p, __builtin_amdgcn_readfirstlane(d.n));
-      if (u == 0) SinkOps<Sink>::put(sink, i, raw_state, d, dpre);
+    // drain the deferred blocks, block k+1's descriptor and first body loading while k hashes
+    // (the pipeline's loads in flight are abandoned)
+    if (nslow) {
+      auto idx = [&](uint32_t k) { return g_lo + __builtin_amdgcn_readlane(slow, k < nslow ? k : nslow - 1); };
+      struct Slow {
+        BlkDesc d;
+        uintptr_t p;
+        uint32_t n, pre;
+        uint64_t i;
+        SlowFirst sf;
+      };
+      auto stage = [&](Slow& S, uint64_t i, const typename Src::Raw& raw) {
+        keep_alive(raw);
+        S.i = i;
+        S.d = src.lane(raw);
+        const uint64_t lp = reinterpret_cast<uintptr_t>(S.d.p);
+        S.p = static_cast<uintptr_t>(uniform64(static_cast<uint32_t>(lp), static_cast<uint32_t>(lp >> 32)));
+        S.n = __builtin_amdgcn_readfirstlane(S.d.n);
+        S.pre = SinkOps<Sink>::pre(sink, i, S.d);
+        slow_issue(S.sf, S.p, S.n, u);
+      };
+      Slow cur;
+      stage(cur, idx(0), src.load(idx(0)));
+      typename Src::Raw rn = src.load(idx(1));
+      for (uint32_t k = 0; k < nslow; ++k) {
+        Slow nxt;
+        stage(nxt, idx(k + 1), rn);  // past the end: re-stages the last block (unconditional)
+        rn = src.load(idx(k + 2));
+        const uint32_t raw_state = slow_finish(lds, lt, u, ureg, cur.sf, cur.p, cur.n);
+        if (u == 0) SinkOps<Sink>::put(sink, cur.i, raw_state, cur.d, cur.pre);
+        cur = nxt;
+      }
+      nslow = 0;
     }
-    nslow = 0;
     if (done) break;
   }
+}
+
+template <class Src, class Sink, bool kNT>
+__global__ __launch_bounds__(kThreads) void crc_sst4k_kernel(const uint32_t* __restrict__ tabs, Src src,
+                                                             uint64_t nblk, Sink sink) {
+  sized_kernel_body<Src, Sink, kNT, 4>(tabs, src, nblk, sink);
+}
+
+template <class Src, class Sink, bool kNT>
+__global__ __launch_bounds__(kThreads) void crc_sst1k_kernel(const uint32_t* __restrict__ tabs, Src src,
+                                                             uint64_t nblk, Sink sink) {
+  sized_kernel_body<Src, Sink, kNT, 1>(tabs, src, nblk, sink);
 }
 
 uint32_t grid_for(const LaunchGeom& g, uint64_t nblk) {

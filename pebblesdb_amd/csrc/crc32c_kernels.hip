@@ -204,12 +204,28 @@ hipError_t launch_desc(const LaunchGeom& g, const uint32_t* d_tables, const uint
                        const uint32_t* expected, uint32_t* out, uint8_t* ok, uint32_t* nbad,
                        hipStream_t s) {
   if (nblk == 0) return hipSuccess;
-  if (mode == kModeOut && g_fast_variant != 0)
+  if (mode == kModeOut && g_fast_variant != 0 && g_fast_variant != 40)  // 40: ignore size hints
     return launch_desc_variant(g_fast_variant, g, d_tables, base, blk, nblk, flags, out, s);
   const dim3 grid(grid_for(g, nblk)), block(kThreads);
+  const DescSrc src{base, blk, flags};
+  // size-class hints (Value() seeds only): the sized kernels (exact 1-/4-KiB body + batched
+  // prefix; other lengths take their slow path in the same launch)
+  if (!(flags & PDB_CRC_USE_INIT) && (flags & (PDB_CRC_SIZE_1K | PDB_CRC_SIZE_4K)) && g_fast_variant != 40) {
+    const bool k1 = flags & PDB_CRC_SIZE_1K;
+#define PDB_SIZED(K, SINK, ...)                                                                                   \
+  hipLaunchKernelGGL((K<DescSrc, SINK, true>), grid, block, 0, s, d_tables, src, nblk, SINK{__VA_ARGS__})
+    if (mode == kModeOut) {
+      if (k1) PDB_SIZED(crc_sst1k_kernel, OutSink, out, flags);
+      else PDB_SIZED(crc_sst4k_kernel, OutSink, out, flags);
+    } else {
+      if (k1) PDB_SIZED(crc_sst1k_kernel, VerifySink, expected, ok, nbad, flags);
+      else PDB_SIZED(crc_sst4k_kernel, VerifySink, expected, ok, nbad, flags);
+    }
+#undef PDB_SIZED
+    return hipGetLastError();
+  }
   // descriptor lists (C3: Zipf sizes at byte offsets): 16-B lane pieces with nt loads, dynamic
   // blocks, packed 4-block trees (A/B: profiles/r01_ab_c3_pack*.json)
-  const DescSrc src{base, blk, flags};
   if (mode == kModeOut)
     hipLaunchKernelGGL((crc_stream16_kernel<DescSrc, OutSink, true, true, true>), grid, block, 0, s, d_tables,
                        src, nblk, OutSink{out, flags});

@@ -194,3 +194,99 @@ def test_new_path_matches_previous_kernel(crc):
         finally:
             lib().pdb_diag_set_variant(0)
     assert (outs[0] == outs[1]).all()
+
+
+# ---- descriptor batches with a size-class hint: crc_sst1k_kernel / crc_sst4k_kernel<DescSrc> ----
+EDGE_1K = [0, 1, 2, 3, 4, 15, 16, 17, 100, 255, 256, 257, 1000, 1023, 1024, 1025, 1026, 1027, 1039, 1040,
+           1041, 1055, 1056, 1100, 1264, 1265, 1279, 1280, 1281, 1282, 2048, 4095, 4096, 4097, 5000, 70000]
+
+
+def _desc_case(crc, sizes, seed, gap_max=7):
+    import oracle
+
+    rng = np.random.Generator(np.random.PCG64(seed))
+    sizes = np.asarray(sizes, dtype=np.int64)
+    gaps = rng.integers(0, gap_max + 1, size=len(sizes))
+    offs = np.concatenate([[0], np.cumsum(sizes + gaps)[:-1]]) + int(rng.integers(0, 4))
+    total = int(offs[-1] + sizes[-1] + 16)
+    base = oracle.splitmix_bytes(total, seed)
+    return base, crc.make_blocks(offs, sizes)
+
+
+@pytest.mark.parametrize("hint", ["1k", "4k"])
+def test_size_hint_edge_lengths(crc, oracle_lib, hint):
+    """Both sized kernels on every fast-range boundary of both classes and slow lengths either
+    side, each repeated at 8 alignments, masked and unmasked, batch and verify."""
+    sizes = [n for n in EDGE_1K + EDGE_N for _ in range(8)]
+    base, blk = _desc_case(crc, sizes, 51)
+    d_base = torch.from_numpy(base).cuda()
+    d_blk = crc.blocks_to_device(blk)
+    for masked in (False, True):
+        got = crc.batch(d_base, d_blk, masked=masked, size_hint=hint).cpu().numpy().view(np.uint32)
+        exp = oracle_lib.batch(base, blk, flags=1 if masked else 0, nthreads=8)
+        bad = np.nonzero(got != exp)[0]
+        assert bad.size == 0, (hint, masked, bad.size, int(blk["len"][bad[0]]))
+    exp = oracle_lib.batch(base, blk, flags=1, nthreads=8)
+    wrong = exp.copy()
+    flip = np.arange(0, len(exp), 5)
+    wrong[flip] ^= 0x10
+    ok, nbad = crc.verify(d_base, d_blk, torch.from_numpy(wrong.view(np.int32)).cuda(), size_hint=hint)
+    assert int(nbad.item()) == len(flip)
+    assert (ok.cpu().numpy() == 0).sum() == len(flip) and (ok.cpu().numpy()[flip] == 0).all()
+
+
+def test_size_hint_wal_layout(crc, oracle_lib):
+    """A WAL image (32-KiB log blocks, 1055-B records fragmented at block ends: type || fragment
+    under the CRC) through the 1-KiB kernel, fragments on its slow path."""
+    import oracle
+    from bench import wal_layout
+
+    offs, lens = wal_layout(24 << 20, 1055)
+    total = int(offs[-1] + lens[-1] + 16)
+    base = oracle.splitmix_bytes(total, 61)
+    blk = crc.make_blocks(offs, lens)
+    got = crc.batch(torch.from_numpy(base).cuda(), crc.blocks_to_device(blk), size_hint="1k")
+    assert (got.cpu().numpy().view(np.uint32) == oracle_lib.batch(base, blk, nthreads=8)).all()
+
+
+def test_size_hint_ignored_with_extend_seed(crc, oracle_lib):
+    rng = np.random.Generator(np.random.PCG64(71))
+    sizes = rng.integers(1024, 1281, size=3000)
+    base, blk = _desc_case(crc, sizes, 72)
+    blk["init"] = rng.integers(0, 1 << 32, size=len(sizes), dtype=np.uint64).astype(np.uint32)
+    got = crc.batch(torch.from_numpy(base).cuda(), crc.blocks_to_device(blk), use_init=True, size_hint="1k")
+    assert (got.cpu().numpy().view(np.uint32) == oracle_lib.batch(base, blk, flags=2, nthreads=8)).all()
+
+
+@pytest.mark.parametrize("lo,hi", [(1024, 1281), (4096, 4353), (900, 1400)])
+def test_host_batch_picks_size_class(crc, oracle_lib, lo, hi):
+    """pdb_crc32c_batch_host / verify_host choose the sized kernel from the host-visible lengths."""
+    rng = np.random.Generator(np.random.PCG64(lo))
+    sizes = rng.integers(lo, hi, size=6000)
+    sizes[::17] = rng.integers(0, 9000, size=len(sizes[::17]))
+    base, blk = _desc_case(crc, sizes, lo + 1)
+    exp = oracle_lib.batch(base, blk, flags=1, nthreads=8)
+    assert (crc.batch_host(base, blk, masked=True) == exp).all()
+    ok, nbad = crc.verify_host(base, blk, exp)
+    assert nbad == 0 and ok.all()
+
+
+def test_sized_kernels_match_generic_kernel(crc):
+    """Variant 40 ignores the hints (crc_stream16_kernel): identical CRCs on a mixed batch."""
+    from pebblesdb_amd._native import lib
+
+    rng = np.random.Generator(np.random.PCG64(81))
+    sizes = np.concatenate([rng.integers(1024, 1281, size=4000), rng.integers(4096, 4353, size=4000),
+                            rng.integers(0, 20000, size=2000)])
+    rng.shuffle(sizes)
+    base, blk = _desc_case(crc, sizes, 82)
+    d_base, d_blk = torch.from_numpy(base).cuda(), crc.blocks_to_device(blk)
+    res = []
+    for v in (0, 40):
+        lib().pdb_diag_set_variant(v)
+        try:
+            res.append([crc.batch(d_base, d_blk, size_hint=h).cpu().numpy() for h in ("1k", "4k")])
+        finally:
+            lib().pdb_diag_set_variant(0)
+    for a, b in zip(res[0], res[1]):
+        assert (a == b).all()

@@ -4,7 +4,9 @@
   sst  : back-to-back blocks of 4167-4175 B (sstable data blocks + type byte, any alignment)
   c3   : Zipf 1-64 KiB (BASELINE config 3)
   small: 256-B records
-argv[1] = variants (e.g. 16,17), argv[2] = workloads.  Prints one JSON object (GB/s, median)."""
+argv[1] = variants (e.g. 16,17), argv[2] = workloads.  Prints one JSON object (GB/s, median).
+wal / sst pass the size-class hint ("1k" / "4k": the sized kernels); variant 40 ignores it (the
+generic crc_stream16_kernel)."""
 import json
 import os
 import sys
@@ -43,6 +45,7 @@ def layout(w):
 
 
 res = {}
+HINT = {"wal": "1k", "sst": "4k"}
 for w in works:
     offs, lens = layout(w)
     blk = crc32c.blocks_to_device(crc32c.make_blocks(offs, lens))
@@ -51,7 +54,7 @@ for w in works:
     ref = None
     for v in variants:
         lib().pdb_diag_set_variant(v)
-        crc32c.batch(d, blk, out=out)
+        crc32c.batch(d, blk, out=out, size_hint=HINT.get(w))
         torch.cuda.synchronize()
         if ref is None:
             ref = out.clone()
@@ -63,7 +66,7 @@ for w in works:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(3):
-                crc32c.batch(d, blk, out=out)
+                crc32c.batch(d, blk, out=out, size_hint=HINT.get(w))
             e1.record()
             torch.cuda.synchronize()
             times[v].append(e0.elapsed_time(e1) / 3)
