@@ -1183,18 +1183,27 @@ __device__ __forceinline__ uint32_t masked_start(const MaskedPiece& f, uint32_t 
   return (f.zl >= 0 && f.zl < 16) ? uz : 0u;
 }
 
-// Levels 0..3 of the wave tree inside each row of 16 lanes (row_shl never crosses a row):
-// lane 16r gets sum_w shift(c_w, 16 (15 - w)).
-__device__ __forceinline__ uint32_t row_tree16(const char* lds, uint32_t lane, uint32_t c) {
+// Levels of the wave tree inside each row of 16 lanes, folded toward the row's LAST lane
+// (row_shr never crosses a row): lane 16r + 15 gets sum_w shift(c_w, 16 (15 - w)).  A prefix of
+// E pieces sits in the row's last E lanes, so L = ceil(log2 E) levels suffice (wave-uniform).
+__device__ __forceinline__ uint32_t row_suffix_tree(const char* lds, uint32_t lane, uint32_t c, uint32_t L) {
   uint32_t y;
-  y = __builtin_amdgcn_update_dpp(0u, c, 0x101, 0xF, 0xF, false);  // row_shl:1
-  if ((lane & 1u) == 0) c = shift_op_x(lds, 0, c, y);
-  y = __builtin_amdgcn_update_dpp(0u, c, 0x102, 0xF, 0xF, false);  // row_shl:2
-  if ((lane & 3u) == 0) c = shift_op_x(lds, 1, c, y);
-  y = __builtin_amdgcn_update_dpp(0u, c, 0x104, 0xF, 0xF, false);  // row_shl:4
-  if ((lane & 7u) == 0) c = shift_op_x(lds, 2, c, y);
-  y = __builtin_amdgcn_update_dpp(0u, c, 0x108, 0xF, 0xF, false);  // row_shl:8
-  if ((lane & 15u) == 0) c = shift_op_x(lds, 3, c, y);
+  if (L > 0) {
+    y = __builtin_amdgcn_update_dpp(0u, c, 0x111, 0xF, 0xF, false);  // row_shr:1
+    if ((lane & 1u) == 1u) c = shift_op_x(lds, 0, y, c);
+  }
+  if (L > 1) {
+    y = __builtin_amdgcn_update_dpp(0u, c, 0x112, 0xF, 0xF, false);  // row_shr:2
+    if ((lane & 3u) == 3u) c = shift_op_x(lds, 1, y, c);
+  }
+  if (L > 2) {
+    y = __builtin_amdgcn_update_dpp(0u, c, 0x114, 0xF, 0xF, false);  // row_shr:4
+    if ((lane & 7u) == 7u) c = shift_op_x(lds, 2, y, c);
+  }
+  if (L > 3) {
+    y = __builtin_amdgcn_update_dpp(0u, c, 0x118, 0xF, 0xF, false);  // row_shr:8
+    if ((lane & 15u) == 15u) c = shift_op_x(lds, 3, y, c);
+  }
   return c;
 }
 
@@ -1326,11 +1335,20 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
     const uintptr_t A = ok ? p + n - kMax + 16u * w : dummy + 16u * w;
     issue_masked(f, A, ok ? p : dummy + 256u);  // a slow block's row: all masked
   };
-  // the group's prefix states: P_r in lane 16r (E_r = 0, n = kBody: the seed itself)
+  // the group's prefix states: P_r in lane 16r + 15 (E_r = 0, n = kBody: the seed itself); the
+  // row tree runs only the levels the longest prefix of the group needs
   auto prefix_states = [&](const MaskedPiece& pf, const Grp& G, uint32_t (&P)[4]) {
-    const uint32_t pref = row_tree16(lds, u, hash_masked(lds, lt, pf, masked_start(pf, ureg)));
+    uint32_t emax = 0;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) P[r] = G.n[r] == kMin ? 0xFFFFFFFFu : __builtin_amdgcn_readlane(pref, 16 * r);
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t e = fast(G.n[r]) ? (G.n[r] - kMin + 15u) >> 4 : 0u;
+      emax = e > emax ? e : emax;
+    }
+    const uint32_t L = emax <= 1 ? 0u : (emax <= 2 ? 1u : (emax <= 4 ? 2u : (emax <= 8 ? 3u : 4u)));
+    const uint32_t pref = row_suffix_tree(lds, u, hash_masked(lds, lt, pf, masked_start(pf, ureg)), L);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      P[r] = G.n[r] == kMin ? 0xFFFFFFFFu : __builtin_amdgcn_readlane(pref, 16 * r + 15);
   };
   // one body's lane partial: chains j (16-B pieces at bs + 16u + 1024j) with the DPP neighbour
   // dword, Horner-folded with shift 1024, P injected as lane 0's start
