@@ -135,6 +135,24 @@ struct NtSealSink {  // A/B variant 34: the trailer as non-temporal byte stores
   }
 };
 
+// A/B variant 36: the seal, with the line holding each trailer read (default policy) a group
+// before the trailer is written, so the write lands on a valid L2 line.
+struct SealTouchSink {};
+
+template <>
+struct SinkOps<SealTouchSink> {
+  __device__ static __forceinline__ uint32_t pre(const SealTouchSink&, uint64_t, const BlkDesc& d) {
+    typedef __attribute__((address_space(1))) const uint32_t g_u32_;
+    const uintptr_t a = (reinterpret_cast<uintptr_t>(d.p) + d.n) & ~static_cast<uintptr_t>(3);
+    return *reinterpret_cast<g_u32_*>(a);
+  }
+  __device__ static __forceinline__ void put(const SealTouchSink&, uint64_t i, uint32_t raw, const BlkDesc& d,
+                                             uint32_t touched) {
+    asm volatile("" ::"v"(touched));
+    SinkOps<SealSink>::put(SealSink{}, i, raw, d, 0u);
+  }
+};
+
 }  // namespace
 
 int g_fast_variant = 0;  // diagnostics: pdb_diag_set_variant()
@@ -256,7 +274,12 @@ hipError_t launch_sst(const LaunchGeom& g, const uint32_t* d_tables, uint8_t* bu
                          SstVerifySink{ok, nbad});
     return hipGetLastError();
   }
-  if (g_fast_variant >= 31 && g_fast_variant <= 35) {  // A/B diagnostics of the seal's writes
+  if (g_fast_variant == 36 && seal) {
+    hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SealTouchSink, true>), grid, block, 0, s, d_tables, src, n,
+                       SealTouchSink{});
+    return hipGetLastError();
+  }
+  if (g_fast_variant >= 31 && g_fast_variant <= 36) {  // A/B diagnostics of the seal's writes
     static uint32_t* scratch = nullptr;                 // (variants 32, 35: CRCs to a scratch array)
     static uint64_t scratch_n = 0;
     if ((g_fast_variant == 32 || g_fast_variant == 35) && scratch_n < n) {
