@@ -146,7 +146,9 @@ __device__ __forceinline__ uint32_t ld32u(const uint8_t* q) {
 // Loads are issued in batches of 8 per thread before their LDS stores, so staging costs ~2 L2
 // round trips instead of one per element (it is most of a small launch's time: the scalar
 // Extend path launches one block).
-template <int kTree, int kHorner, int kSlot7 = -1, bool kSkipSlot5 = false>
+// kQuadTree: slots 0..5 hold the quad-transposed tree's operators {1024, 2048, 64, 128, 256, 512}
+// (catalog 6, 7, 2, 3, 4, 5) instead of kTree .. kTree + 5.
+template <int kTree, int kHorner, int kSlot7 = -1, bool kSkipSlot5 = false, bool kQuadTree = false>
 __device__ __forceinline__ void stage_tables(char* lds, const uint32_t* __restrict__ tabs) {
   constexpr uint32_t kMain = 4u * 256u * 8u;  // 16-B stores of the replicated T0..T3
   for (uint32_t i0 = 0; i0 < kMain; i0 += 8u * blockDim.x) {
@@ -168,6 +170,7 @@ __device__ __forceinline__ void stage_tables(char* lds, const uint32_t* __restri
   constexpr uint32_t nslots = kSlot7 >= 0 ? 8u : (kHorner >= 0 ? 7u : 6u);
   constexpr uint32_t kCat = nslots * 256u;
   auto src_of = [](uint32_t slot) -> uint32_t {
+    if (kQuadTree && slot < 6) return slot < 2 ? PDB_CAT_S1024 + slot : slot;
     return slot < 6 ? kTree + slot : (slot == 6 ? static_cast<uint32_t>(kHorner) : static_cast<uint32_t>(kSlot7));
   };
   for (uint32_t i0 = 0; i0 < kCat; i0 += 4u * blockDim.x) {
@@ -283,6 +286,62 @@ __device__ __forceinline__ uint32_t tree4_packed(const char* lds, uint32_t u, ui
   return v;
 }
 
+// ---- quad-transposed 4-KiB geometry -------------------------------------------------------------
+// The coalesced loads leave lane u = 4m + b with the 16-B pieces at 16u + 1024j (j = 0..3): four
+// chains that must be folded with three "shift 1024/2048" operator lookups per lane (single-copy
+// LDS tables, ~3 cycles of bank conflicts per lookup).  A 4x4 transpose of 16-B elements inside
+// each quad (two DPP butterfly stages, quad_perm xor 1 / xor 2) gives lane (m, b) instead the 64
+// CONTIGUOUS bytes at 1024b + 64m, hashed as one 16-step chain through the replicated,
+// conflict-free T0..T3 -- no per-lane fold at all; the tree's levels become "shift 1024" (bit 0 of
+// the lane = b), "shift 2048" (bit 1), then 64, 128, 256, 512 (m): same op count as before.
+// One butterfly stage on the register pair (A, B) = (R[j], R[j ^ K]): the lane with bit K clear
+// keeps A and takes its partner's A into B; the lane with bit K set keeps B and takes its
+// partner's B into A.
+template <int kCtrl>
+__device__ __forceinline__ void quad_swap(u32x4& A, u32x4& B, bool hi) {
+  const u32x4 snd = hi ? A : B;
+  u32x4 rcv;
+  rcv.x = __builtin_amdgcn_mov_dpp(snd.x, kCtrl, 0xF, 0xF, true);
+  rcv.y = __builtin_amdgcn_mov_dpp(snd.y, kCtrl, 0xF, 0xF, true);
+  rcv.z = __builtin_amdgcn_mov_dpp(snd.z, kCtrl, 0xF, 0xF, true);
+  rcv.w = __builtin_amdgcn_mov_dpp(snd.w, kCtrl, 0xF, 0xF, true);
+  A = hi ? rcv : A;
+  B = hi ? B : rcv;
+}
+
+__device__ __forceinline__ void quad_transpose(u32x4 (&R)[4], uint32_t lane) {
+  const bool h1 = (lane & 1u) != 0, h2 = (lane & 2u) != 0;
+  quad_swap<0xB1>(R[0], R[1], h1);  // quad_perm [1,0,3,2]: partner lane ^ 1
+  quad_swap<0xB1>(R[2], R[3], h1);
+  quad_swap<0x4E>(R[0], R[2], h2);  // quad_perm [2,3,0,1]: partner lane ^ 2
+  quad_swap<0x4E>(R[1], R[3], h2);
+}
+
+// One 16-step chain over 64 contiguous bytes (4 x u32x4 in order) from `start`.
+__device__ __forceinline__ uint32_t chain64(const char* lds, const LaneTabs& lt, uint32_t start, const u32x4 (&R)[4]) {
+  const uint32_t w[16] = {R[0].x, R[0].y, R[0].z, R[0].w, R[1].x, R[1].y, R[1].z, R[1].w,
+                          R[2].x, R[2].y, R[2].z, R[2].w, R[3].x, R[3].y, R[3].z, R[3].w};
+  uint32_t x = start ^ w[0];
+#pragma unroll
+  for (int i = 1; i <= 16; ++i) x = step4x(lds, lt, x, i < 16 ? w[i] : 0u);
+  return x;
+}
+
+// The same 64 bytes as two independent 8-step chains folded with "shift 32" (slot 6): ILP 2 for
+// one operator lookup per lane.
+__device__ __forceinline__ uint32_t chain64x2(const char* lds, const LaneTabs& lt, uint32_t start,
+                                              const u32x4 (&R)[4]) {
+  const uint32_t a[8] = {R[0].x, R[0].y, R[0].z, R[0].w, R[1].x, R[1].y, R[1].z, R[1].w};
+  const uint32_t b[8] = {R[2].x, R[2].y, R[2].z, R[2].w, R[3].x, R[3].y, R[3].z, R[3].w};
+  uint32_t xa = start ^ a[0], xb = b[0];
+#pragma unroll
+  for (int i = 1; i <= 8; ++i) {
+    xa = step4x(lds, lt, xa, i < 8 ? a[i] : 0u);
+    xb = step4x(lds, lt, xb, i < 8 ? b[i] : 0u);
+  }
+  return shift_op_x(lds, PDB_SLOT_HORNER, xa, xb);
+}
+
 // Lane partial of one 4-KiB block.  kNP = 2: two 32-B pieces (at 32l and 2048+32l) folded with
 // shift 2048 (slot 6), partials 32 B apart.  kNP = 4: four 16-B pieces at 16l + 1024j, four
 // 4-word chains folded as shift2048(shift1024(x0)^x1) ^ (shift1024(x2)^x3) (slots 6, 7), partials
@@ -321,7 +380,7 @@ __device__ __forceinline__ uint32_t partial4k(const char* lds, const LaneTabs& l
 // kXcd: workgroups are dispatched to the 8 XCDs round-robin (blockIdx.x % 8); kXcd renumbers
 // them so each XCD's CUs own consecutive 64-KiB block windows (A/B diagnostics).
 template <int kSync, int kNP = 2, bool kNT = false, int kWaves = kWavesPerWg, bool kPair = false,
-          bool kXcd = false>
+          bool kXcd = false, int kQuad = 0>
 __global__ __launch_bounds__(kWaves * 64) void crc_pack4k_kernel(
     const uint32_t* __restrict__ tabs, const uint8_t* __restrict__ base, uint64_t stride,
     uint64_t nblk, uint32_t flags, uint32_t init, uint32_t* __restrict__ out) {
@@ -337,7 +396,7 @@ __global__ __launch_bounds__(kWaves * 64) void crc_pack4k_kernel(
   load4k<kNP, kNT>(buf, base, stride, w < nblk ? w : nblk - 1, u);
   if constexpr (kPair) load4k<kNP, kNT>(buf2, base, stride, w + nw < nblk ? w + nw : nblk - 1, u);
   if constexpr (kNP == 4)
-    stage_tables<PDB_CAT_TREE16, PDB_CAT_S1024, PDB_CAT_S2048>(lds, tabs);
+    stage_tables<PDB_CAT_TREE16, kQuad == 2 ? 1 : PDB_CAT_S1024, PDB_CAT_S2048, false, kQuad != 0>(lds, tabs);
   else
     stage_tables<PDB_CAT_TREE32, PDB_CAT_S2048>(lds, tabs);
   __syncthreads();
@@ -376,7 +435,16 @@ __global__ __launch_bounds__(kWaves * 64) void crc_pack4k_kernel(
         u32x4 cur[4] = {buf[0], buf[1], buf[2], buf[3]};
         const uint64_t bn = bk + nw;
         if (bn < nblk) load4k<kNP, kNT>(buf, base, stride, bn, u);  // wave-uniform
-        p[r] = bk < nblk ? partial4k<kNP>(lds, lt, c0, cur) : 0u;
+        if constexpr (kQuad != 0) {
+          static_assert(kNP == 4, "the quad transpose needs 4 x 16-B lane pieces");
+          quad_transpose(cur, u);
+          if constexpr (kQuad == 1)
+            p[r] = bk < nblk ? chain64(lds, lt, c0, cur) : 0u;
+          else
+            p[r] = bk < nblk ? chain64x2(lds, lt, c0, cur) : 0u;
+        } else {
+          p[r] = bk < nblk ? partial4k<kNP>(lds, lt, c0, cur) : 0u;
+        }
       }
     }
     const uint32_t v = tree4_packed(lds, u, p[0], p[1], p[2], p[3]);
@@ -1263,7 +1331,7 @@ __device__ __forceinline__ uint32_t slow_finish(const char* lds, const LaneTabs&
 constexpr uint32_t kSlowList = 64u;
 
 // kRows = body size in KiB: 4 (crc_sst4k_kernel) or 1 (crc_sst1k_kernel).
-template <class Src, class Sink, bool kNT, int kRows>
+template <class Src, class Sink, bool kNT, int kRows, bool kDiagNoFold = false>
 __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ tabs, Src src, uint64_t nblk,
                                                   Sink sink) {
   static_assert(kRows == 1 || kRows == 4, "bodies of 1 or 4 KiB");
@@ -1364,7 +1432,12 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
     }
     uint32_t a = chain16(lds, lt, u == 0 ? P : 0u, e[0], nx[0], s);
 #pragma unroll
-    for (int j = 1; j < kRows; ++j) a = shift_op_x(lds, PDB_SLOT_HORNER, a, chain16(lds, lt, 0u, e[j], nx[j], s));
+    for (int j = 1; j < kRows; ++j) {
+      const uint32_t x = chain16(lds, lt, 0u, e[j], nx[j], s);
+      // kDiagNoFold (A/B diagnostics only, WRONG CRCs): the Horner fold replaced by a XOR, to price
+      // the shift-operator lookups
+      a = kDiagNoFold ? (a ^ x) : shift_op_x(lds, PDB_SLOT_HORNER, a, x);
+    }
     return a;
   };
 
@@ -1529,6 +1602,12 @@ template <class Src, class Sink, bool kNT>
 __global__ __launch_bounds__(kThreads) void crc_sst4k_kernel(const uint32_t* __restrict__ tabs, Src src,
                                                              uint64_t nblk, Sink sink) {
   sized_kernel_body<Src, Sink, kNT, 4>(tabs, src, nblk, sink);
+}
+
+template <class Src, class Sink, bool kNT>
+__global__ __launch_bounds__(kThreads) void crc_sst4k_nofold_kernel(const uint32_t* __restrict__ tabs, Src src,
+                                                                    uint64_t nblk, Sink sink) {
+  sized_kernel_body<Src, Sink, kNT, 4, true>(tabs, src, nblk, sink);
 }
 
 template <class Src, class Sink, bool kNT>

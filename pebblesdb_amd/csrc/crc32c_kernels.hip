@@ -274,6 +274,11 @@ hipError_t launch_sst(const LaunchGeom& g, const uint32_t* d_tables, uint8_t* bu
                          SstVerifySink{ok, nbad});
     return hipGetLastError();
   }
+  if (g_fast_variant == 97 && !seal) {  // diagnostics, WRONG CRCs: verify without the Horner folds
+    hipLaunchKernelGGL((crc_sst4k_nofold_kernel<SstSrc, SstVerifySink, true>), grid, block, 0, s, d_tables, src, n,
+                       SstVerifySink{ok, nullptr});  // no nbad: every block "fails"; 1M atomics would dominate
+    return hipGetLastError();
+  }
   if (g_fast_variant == 36 && seal) {
     hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SealTouchSink, true>), grid, block, 0, s, d_tables, src, n,
                        SealTouchSink{});

@@ -454,6 +454,9 @@ hipError_t launch_fixed_variant(int v, const LaunchGeom& g, const uint32_t* d_ta
     // XCD-contiguous workgroup numbering (lock-step / free-running)
     case 26: PDB_K((crc_pack4k_kernel<1, 4, true, 16, false, true>)); break;
     case 27: PDB_K((crc_pack4k_kernel<0, 4, true, 16, false, true>)); break;
+    // quad-transposed lanes: 64 contiguous bytes per lane, no per-lane Horner folds
+    case 28: PDB_K((crc_pack4k_kernel<1, 4, true, 16, false, false, 1>)); break;
+    case 29: PDB_K((crc_pack4k_kernel<1, 4, true, 16, false, false, 2>)); break;  // 2 chains + shift 32
     default: PDB_K((crc_pack4k_kernel<1, 4, true>)); break;
   }
 #undef PDB_FAST
