@@ -48,6 +48,9 @@ def parse():
     ap.add_argument("--no-copy-inclusive", action="store_true")
     ap.add_argument("--diag", action="store_true", help="also time the read-stream calibration kernels")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--timing", default="region", choices=["per-launch", "region"],
+                    help="HIP events around every launch (per-launch kernel times) or one pair around "
+                         "the timed region (no event packets between launches)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend (nccl = RCCL over xGMI; gloo only to rehearse the "
                          "multi-rank flow with ranks sharing one GPU)")
@@ -235,19 +238,26 @@ def main():
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
+    per_launch = args.timing == "per-launch"
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
+          for _ in range(args.steps if per_launch else 1)]
     t0 = time.perf_counter()
-    for s, e in ev:
-        s.record(stream)
-        step()
-        e.record(stream)
+    if per_launch:
+        for s, e in ev:
+            s.record(stream)
+            step()
+            e.record(stream)
+    else:  # one event pair around all K launches: the average includes the launch gaps
+        ev[0][0].record(stream)
+        for _ in range(args.steps):
+            step()
+        ev[0][1].record(stream)
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    kern_ms = [s.elapsed_time(e) for s, e in ev]
+    kern_ms = [s.elapsed_time(e) for s, e in ev] if per_launch else [ev[0][0].elapsed_time(ev[0][1]) / args.steps]
     kern_avg_ms = float(np.mean(kern_ms))
 
     t = torch.tensor([wall], dtype=torch.float64, device=cdev)
@@ -317,6 +327,7 @@ def main():
                 "algorithmic_bytes_per_launch": algo_bytes,
                 "kernel_avg_ms": round(kern_avg_ms, 4),
                 "kernel_min_ms": round(float(np.min(kern_ms)), 4),
+                "timing": args.timing,
             },
             "cpu_baseline": cpu,
             "xor_of_crcs": f"{xor_all:08x}",
