@@ -164,6 +164,7 @@ def main():
         h = np.zeros(nblk, dtype=crc32c.HANDLE_DTYPE)
         h["offset"], h["size"] = offs, sizes
         d_h = T.handles_to_device(h, dev)
+        cpu_blk = crc32c.make_blocks(offs, sizes + 1)  # the CPU reference's CRC spans (contents || type)
         T.seal_device(data, d_h)  # untimed: a sealed image, so verification passes
         ok = torch.empty(nblk, dtype=torch.uint8, device=dev)
         nbad = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -292,6 +293,8 @@ def main():
         if not args.no_cpu_baseline and world == 1:
             if args.workload in ("c2", "sstable", "c3", "wal"):
                 cpu = cpu_baseline(data, L, stride, nblk, args, d_blk if args.workload in ("c3", "wal") else None)
+            else:  # sst_verify / sst_seal: the reference's CRC over each block's contents || type
+                cpu = cpu_baseline(data, L, stride, nblk, args, cpu_blk)
 
     if rank == 0:
         traffic = pmc_traffic(args.workload)
@@ -400,7 +403,7 @@ def cpu_baseline(data, L, stride, nblk, args, d_blk):
         blk["off"] = np.arange(ns) * stride
         blk["len"] = L
     else:
-        b = d_blk.cpu().numpy().view(oracle.BLK_DTYPE)
+        b = d_blk if isinstance(d_blk, np.ndarray) else d_blk.cpu().numpy().view(oracle.BLK_DTYPE)
         end = np.cumsum(b["len"].astype(np.int64))
         ns = int(np.searchsorted(end, 1 << 30, side="right")) or 1
         blk = b[:ns].copy()
