@@ -88,6 +88,11 @@ hipError_t launch_fixed_variant(int v, const LaunchGeom& g, const uint32_t* d_ta
 hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tables, const uint8_t* base,
                                const pdb_blk* blk, uint64_t nblk, uint32_t flags, uint32_t* out,
                                hipStream_t s);
+// sstable hooks: 18 = crc_stream_kernel (32-B pieces), 30 = crc_stream16_kernel (the previous
+// default), 31-36 seal-write diagnostics, 97 verify without the Horner folds (wrong CRCs)
+hipError_t launch_sst_variant(int v, const LaunchGeom& g, const uint32_t* d_tables, uint8_t* buf,
+                              const pdb_block_handle* h, uint64_t n, bool seal, uint8_t* ok, uint32_t* nbad,
+                              hipStream_t s);
 hipError_t launch_read_stream(const uint8_t* base, uint64_t nbytes, uint32_t* out, hipStream_t s);
 hipError_t launch_read_pattern4k(const LaunchGeom& g, const uint8_t* base, uint64_t nblk,
                                  int variant, uint32_t* out, hipStream_t s);

@@ -110,49 +110,6 @@ __global__ __launch_bounds__(1024) void span_combine_kernel(const uint32_t* __re
   if (threadIdx.x == 0) out[0] = ~sw[0];
 }
 
-// Seal's second half (A/B variant 35): trailer word i (masked CRC, from a compact array) to
-// buf + offset_i + size_i + 1, one thread per block.
-__global__ __launch_bounds__(256) void trailer_scatter_kernel(uint8_t* __restrict__ buf,
-                                                              const pdb_block_handle* __restrict__ h,
-                                                              const uint32_t* __restrict__ crc, uint64_t n) {
-  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint8_t* tr = buf + h[i].offset + h[i].size + 1;
-  const uint32_t m = crc[i];
-  tr[0] = static_cast<uint8_t>(m);
-  tr[1] = static_cast<uint8_t>(m >> 8);
-  tr[2] = static_cast<uint8_t>(m >> 16);
-  tr[3] = static_cast<uint8_t>(m >> 24);
-}
-
-struct NtSealSink {  // A/B variant 34: the trailer as non-temporal byte stores
-  __device__ __forceinline__ void put(uint64_t, uint32_t raw, const BlkDesc& d) const {
-    typedef __attribute__((address_space(1))) uint8_t g_u8;
-    g_u8* tr = reinterpret_cast<g_u8*>(reinterpret_cast<uintptr_t>(d.p) + d.n);
-    const uint32_t m = pdb_mask(~raw);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) __builtin_nontemporal_store(static_cast<uint8_t>(m >> (8 * k)), tr + k);
-  }
-};
-
-// A/B variant 36: the seal, with the line holding each trailer read (default policy) a group
-// before the trailer is written, so the write lands on a valid L2 line.
-struct SealTouchSink {};
-
-template <>
-struct SinkOps<SealTouchSink> {
-  __device__ static __forceinline__ uint32_t pre(const SealTouchSink&, uint64_t, const BlkDesc& d) {
-    typedef __attribute__((address_space(1))) const uint32_t g_u32_;
-    const uintptr_t a = (reinterpret_cast<uintptr_t>(d.p) + d.n) & ~static_cast<uintptr_t>(3);
-    return *reinterpret_cast<g_u32_*>(a);
-  }
-  __device__ static __forceinline__ void put(const SealTouchSink&, uint64_t i, uint32_t raw, const BlkDesc& d,
-                                             uint32_t touched) {
-    asm volatile("" ::"v"(touched));
-    SinkOps<SealSink>::put(SealSink{}, i, raw, d, 0u);
-  }
-};
-
 }  // namespace
 
 int g_fast_variant = 0;  // diagnostics: pdb_diag_set_variant()
@@ -259,77 +216,17 @@ hipError_t launch_sst(const LaunchGeom& g, const uint32_t* d_tables, uint8_t* bu
                       hipStream_t s) {
   (void)buf_len;
   if (n == 0) return hipSuccess;
+  if (g_fast_variant != 0) return launch_sst_variant(g_fast_variant, g, d_tables, buf, h, n, seal, ok, nbad, s);
   const dim3 grid(grid_for(g, n)), block(kThreads);
-  // sstable blocks (contents + type, ~4.1 KiB at byte offsets): 16-B pieces with nt loads, DPP
-  // neighbour dwords, conditional chains, packed 4-block trees (A/B vs the 32-B kernel, variant
-  // 18: +3-5 % on db_bench-sized blocks, profiles/r01_ab_sst_hooks.json)
+  // exact 4-KiB body + batched prefix for the 4096..4352-B blocks (every data block TableBuilder
+  // emits: contents + type), the slow path in the same launch for the rest
+  // (profiles/r01_ab_sst4k.json: verify +45 %, seal +27 % over crc_stream16_kernel)
   const SstSrc src{buf, h};
-  if (g_fast_variant == 0) {
-    // exact 4-KiB body + batched prefix for the 4096..4352-B blocks (every data block
-    // TableBuilder emits), sst_slow_block for the rest (profiles/r01_ab_sst4k.json)
-    if (seal)
-      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SealSink, true>), grid, block, 0, s, d_tables, src, n, SealSink{});
-    else
-      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstVerifySink, true>), grid, block, 0, s, d_tables, src, n,
-                         SstVerifySink{ok, nbad});
-    return hipGetLastError();
-  }
-  if (g_fast_variant == 97 && !seal) {  // diagnostics, WRONG CRCs: verify without the Horner folds
-    hipLaunchKernelGGL((crc_sst4k_nofold_kernel<SstSrc, SstVerifySink, true>), grid, block, 0, s, d_tables, src, n,
-                       SstVerifySink{ok, nullptr});  // no nbad: every block "fails"; 1M atomics would dominate
-    return hipGetLastError();
-  }
-  if (g_fast_variant == 36 && seal) {
-    hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SealTouchSink, true>), grid, block, 0, s, d_tables, src, n,
-                       SealTouchSink{});
-    return hipGetLastError();
-  }
-  if (g_fast_variant >= 31 && g_fast_variant <= 36) {  // A/B diagnostics of the seal's writes
-    static uint32_t* scratch = nullptr;                 // (variants 32, 35: CRCs to a scratch array)
-    static uint64_t scratch_n = 0;
-    if ((g_fast_variant == 32 || g_fast_variant == 35) && scratch_n < n) {
-      if (scratch) (void)hipFree(scratch);
-      if (hipMalloc(&scratch, n * 4) != hipSuccess) return hipErrorOutOfMemory;
-      scratch_n = n;
-    }
-    if (!seal)  // verify: 31 default-policy loads, else the shipped kernel
-      if (g_fast_variant == 31)
-        hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstVerifySink, false>), grid, block, 0, s, d_tables, src, n,
-                           SstVerifySink{ok, nbad});
-      else
-        hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstVerifySink, true>), grid, block, 0, s, d_tables, src, n,
-                           SstVerifySink{ok, nbad});
-    else if (g_fast_variant == 31)  // default-policy loads
-      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SealSink, false>), grid, block, 0, s, d_tables, src, n, SealSink{});
-    else if (g_fast_variant == 32 || g_fast_variant == 35) {  // compact 4-B output (+ 35: scatter pass)
-      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, OutSink, true>), grid, block, 0, s, d_tables, src, n,
-                         OutSink{scratch, PDB_CRC_MASK_OUTPUT});
-      if (g_fast_variant == 35)
-        hipLaunchKernelGGL(trailer_scatter_kernel, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256), 0, s, buf,
-                           h, scratch, n);
-    } else if (g_fast_variant == 34)
-      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, NtSealSink, true>), grid, block, 0, s, d_tables, src, n,
-                         NtSealSink{});
-    else  // 33: the seal's kernel with its stores dropped (a verify with nowhere to report)
-      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstVerifySink, true>), grid, block, 0, s, d_tables, src, n,
-                         SstVerifySink{nullptr, nullptr});
-    return hipGetLastError();
-  }
-  if (g_fast_variant == 18) {
-    if (seal)
-      hipLaunchKernelGGL((crc_stream_kernel<SstSrc, SealSink, 0, true, true>), grid, block, 0, s, d_tables, src, n,
-                         SealSink{});
-    else
-      hipLaunchKernelGGL((crc_stream_kernel<SstSrc, SstVerifySink, 0, true, true>), grid, block, 0, s, d_tables,
-                         src, n, SstVerifySink{ok, nbad});
-    return hipGetLastError();
-  }
   if (seal)
-    hipLaunchKernelGGL((crc_stream16_kernel<SstSrc, SealSink, true, true, true>), grid, block, 0, s, d_tables, src, n,
-                       SealSink{});
+    hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SealSink, true>), grid, block, 0, s, d_tables, src, n, SealSink{});
   else
-    hipLaunchKernelGGL((crc_stream16_kernel<SstSrc, SstVerifySink, true, true, true>), grid, block, 0, s, d_tables,
-                       src, n, SstVerifySink{ok, nbad});
+    hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstVerifySink, true>), grid, block, 0, s, d_tables, src, n,
+                       SstVerifySink{ok, nbad});
   return hipGetLastError();
 }
 

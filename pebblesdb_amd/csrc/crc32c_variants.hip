@@ -1,6 +1,8 @@
 // crc32c_variants.hip -- A/B kernel variants (selected with pdb_diag_set_variant, all
 // parity-tested in tests/test_gpu_parity.py) and the load-pattern calibration kernels behind the
 // roofline numbers in DESIGN.md §6.  Not on the shipped path unless a variant is selected.
+#include <mutex>
+
 #include "crc32c_device.h"
 
 namespace pdb {
@@ -362,6 +364,124 @@ uint32_t grid_forw(const LaunchGeom& g, uint64_t nblk, uint32_t waves) {
   return static_cast<uint32_t>(want < g.grid ? (want ? want : 1) : g.grid);
 }
 uint32_t grid_for8(const LaunchGeom& g, uint64_t nblk) { return grid_forw(g, nblk, 8); }
+
+namespace {
+
+// Seal's second half (A/B variant 35): trailer word i (masked CRC, from a compact array) to
+// buf + offset_i + size_i + 1, one thread per block.
+__global__ __launch_bounds__(256) void trailer_scatter_kernel(uint8_t* __restrict__ buf,
+                                                              const pdb_block_handle* __restrict__ h,
+                                                              const uint32_t* __restrict__ crc, uint64_t n) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t* tr = buf + h[i].offset + h[i].size + 1;
+  const uint32_t m = crc[i];
+  tr[0] = static_cast<uint8_t>(m);
+  tr[1] = static_cast<uint8_t>(m >> 8);
+  tr[2] = static_cast<uint8_t>(m >> 16);
+  tr[3] = static_cast<uint8_t>(m >> 24);
+}
+
+struct NtSealSink {  // A/B variant 34: the trailer as non-temporal byte stores
+  __device__ __forceinline__ void put(uint64_t, uint32_t raw, const BlkDesc& d) const {
+    typedef __attribute__((address_space(1))) uint8_t g_u8;
+    g_u8* tr = reinterpret_cast<g_u8*>(reinterpret_cast<uintptr_t>(d.p) + d.n);
+    const uint32_t m = pdb_mask(~raw);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) __builtin_nontemporal_store(static_cast<uint8_t>(m >> (8 * k)), tr + k);
+  }
+};
+
+// A/B variant 36: the seal, with the line holding each trailer read (default policy) a group
+// before the trailer is written, so the write lands on a valid L2 line.
+struct SealTouchSink {};
+
+template <>
+struct SinkOps<SealTouchSink> {
+  __device__ static __forceinline__ uint32_t pre(const SealTouchSink&, uint64_t, const BlkDesc& d) {
+    typedef __attribute__((address_space(1))) const uint32_t g_u32_;
+    const uintptr_t a = (reinterpret_cast<uintptr_t>(d.p) + d.n) & ~static_cast<uintptr_t>(3);
+    return *reinterpret_cast<g_u32_*>(a);
+  }
+  __device__ static __forceinline__ void put(const SealTouchSink&, uint64_t i, uint32_t raw, const BlkDesc& d,
+                                             uint32_t touched) {
+    asm volatile("" ::"v"(touched));
+    SinkOps<SealSink>::put(SealSink{}, i, raw, d, 0u);
+  }
+};
+
+
+}  // namespace
+
+hipError_t launch_sst_variant(int v, const LaunchGeom& g, const uint32_t* d_tables, uint8_t* buf,
+                              const pdb_block_handle* h, uint64_t n, bool seal, uint8_t* ok, uint32_t* nbad,
+                              hipStream_t s) {
+  const dim3 grid(grid_for(g, n)), block(kThreads);
+  const SstSrc src{buf, h};
+  if (v == 97 && !seal) {  // WRONG CRCs by design: verify without the Horner folds (prices them)
+    hipLaunchKernelGGL((crc_sst4k_nofold_kernel<SstSrc, SstVerifySink, true>), grid, block, 0, s, d_tables, src, n,
+                       SstVerifySink{ok, nullptr});  // no nbad: every block "fails"; 1M atomics would dominate
+    return hipGetLastError();
+  }
+  if (v == 36 && seal) {  // trailer line read a group before the write
+    hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SealTouchSink, true>), grid, block, 0, s, d_tables, src, n,
+                       SealTouchSink{});
+    return hipGetLastError();
+  }
+  if (v >= 31 && v <= 36) {  // seal-write diagnostics (verify: 31 default-policy loads, else shipped)
+    static std::mutex mu;   // diagnostics only: one scratch array for variants 32 / 35
+    static uint32_t* scratch = nullptr;
+    static uint64_t scratch_n = 0;
+    std::lock_guard<std::mutex> lk(mu);
+    if ((v == 32 || v == 35) && scratch_n < n) {
+      if (scratch) (void)hipFree(scratch);
+      scratch = nullptr;
+      scratch_n = 0;
+      if (hipMalloc(&scratch, n * 4) != hipSuccess) return hipErrorOutOfMemory;
+      scratch_n = n;
+    }
+    if (!seal) {
+      if (v == 31)
+        hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstVerifySink, false>), grid, block, 0, s, d_tables, src, n,
+                           SstVerifySink{ok, nbad});
+      else
+        hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstVerifySink, true>), grid, block, 0, s, d_tables, src, n,
+                           SstVerifySink{ok, nbad});
+    } else if (v == 31) {  // default-policy loads
+      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SealSink, false>), grid, block, 0, s, d_tables, src, n, SealSink{});
+    } else if (v == 32 || v == 35) {  // compact 4-B output (+ 35: a separate trailer scatter pass)
+      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, OutSink, true>), grid, block, 0, s, d_tables, src, n,
+                         OutSink{scratch, PDB_CRC_MASK_OUTPUT});
+      if (v == 35)
+        hipLaunchKernelGGL(trailer_scatter_kernel, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256), 0, s, buf,
+                           h, scratch, n);
+    } else if (v == 34) {  // trailers as nt byte stores
+      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, NtSealSink, true>), grid, block, 0, s, d_tables, src, n,
+                         NtSealSink{});
+    } else {  // 33: the seal's kernel with its stores dropped (a verify with nowhere to report)
+      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstVerifySink, true>), grid, block, 0, s, d_tables, src, n,
+                         SstVerifySink{nullptr, nullptr});
+    }
+    return hipGetLastError();
+  }
+  if (v == 18) {  // 32-B-piece stream kernel
+    if (seal)
+      hipLaunchKernelGGL((crc_stream_kernel<SstSrc, SealSink, 0, true, true>), grid, block, 0, s, d_tables, src, n,
+                         SealSink{});
+    else
+      hipLaunchKernelGGL((crc_stream_kernel<SstSrc, SstVerifySink, 0, true, true>), grid, block, 0, s, d_tables,
+                         src, n, SstVerifySink{ok, nbad});
+    return hipGetLastError();
+  }
+  // any other variant (30): the previous default, crc_stream16_kernel
+  if (seal)
+    hipLaunchKernelGGL((crc_stream16_kernel<SstSrc, SealSink, true, true, true>), grid, block, 0, s, d_tables, src, n,
+                       SealSink{});
+  else
+    hipLaunchKernelGGL((crc_stream16_kernel<SstSrc, SstVerifySink, true, true, true>), grid, block, 0, s, d_tables,
+                       src, n, SstVerifySink{ok, nbad});
+  return hipGetLastError();
+}
 
 hipError_t launch_fixed_variant(int v, const LaunchGeom& g, const uint32_t* d_tables, const uint8_t* base,
                                 uint64_t stride, uint32_t len, uint64_t nblk, uint32_t flags, uint32_t init,
