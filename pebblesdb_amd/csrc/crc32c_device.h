@@ -286,6 +286,41 @@ __device__ __forceinline__ uint32_t tree4_packed(const char* lds, uint32_t u, ui
   return v;
 }
 
+// The same packed fold for 8 blocks (partials 16 B apart in every lane): level 0 pairs lanes of
+// blocks (0,1), (2,3), (4,5), (6,7) (4 full-wave ops), level 1 quads of blocks 0..3 and 4..7 (2 ops),
+// level 2 interleaves the two halves so that lane 8j + b holds block b (1 op), levels 3..5 once
+// for all 8 blocks: 10 shift operations per 8 blocks instead of 14.  Block b's raw state ends in
+// lane b (b = 0..7).
+__device__ __forceinline__ uint32_t tree8_packed(const char* lds, uint32_t u, const uint32_t (&p)[8]) {
+  const bool odd = u & 1u, hi = u & 2u, h4 = u & 4u;
+  uint32_t r[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {  // level 0 (shift 16): even lane 2m -> block 2k pair m, odd -> 2k+1
+    const uint32_t pn = __builtin_amdgcn_update_dpp(0u, p[2 * k], 0x101, 0xF, 0xF, false);      // p[2k][L+1]
+    const uint32_t pp = __builtin_amdgcn_update_dpp(0u, p[2 * k + 1], 0x111, 0xF, 0xF, false);  // p[2k+1][L-1]
+    r[k] = shift_op_x(lds, 0, sel(odd, pp, p[2 * k]), sel(odd, p[2 * k + 1], pn));
+  }
+  uint32_t v[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {  // level 1 (shift 32): lane 4j + q -> block 4h + q, quad j
+    const uint32_t rn = __builtin_amdgcn_update_dpp(0u, r[2 * h], 0x102, 0xF, 0xF, false);      // [L+2]
+    const uint32_t rp = __builtin_amdgcn_update_dpp(0u, r[2 * h + 1], 0x112, 0xF, 0xF, false);  // [L-2]
+    v[h] = shift_op_x(lds, 1, sel(hi, rp, r[2 * h]), sel(hi, r[2 * h + 1], rn));
+  }
+  // level 2 (shift 64): lane 8j + q (q < 4) from v0 at L, L+4; lane 8j + 4 + q from v1 at L-4, L
+  const uint32_t vn = __builtin_amdgcn_update_dpp(0u, v[0], 0x104, 0xF, 0xF, false);  // v0[L+4]
+  const uint32_t vp = __builtin_amdgcn_update_dpp(0u, v[1], 0x114, 0xF, 0xF, false);  // v1[L-4]
+  uint32_t w = shift_op_x(lds, 2, sel(h4, vp, v[0]), sel(h4, v[1], vn));
+  // levels 3..5: lane 8j + b holds block b; pair (L, L + 8 * 2^(k-3))
+  uint32_t y = __builtin_amdgcn_update_dpp(0u, w, 0x108, 0xF, 0xF, false);  // row_shl:8
+  if ((u & 8u) == 0) w = shift_op_x(lds, 3, w, y);
+  y = __builtin_amdgcn_ds_swizzle(w, 0x401F);  // lane ^ 16
+  if ((u & 24u) == 0) w = shift_op_x(lds, 4, w, y);
+  y = __shfl_down(w, 32, 64);
+  if ((u & 56u) == 0) w = shift_op_x(lds, 5, w, y);
+  return w;
+}
+
 // ---- quad-transposed 4-KiB geometry -------------------------------------------------------------
 // The coalesced loads leave lane u = 4m + b with the 16-B pieces at 16u + 1024j (j = 0..3): four
 // chains that must be folded with three "shift 1024/2048" operator lookups per lane (single-copy
@@ -1331,40 +1366,44 @@ __device__ __forceinline__ uint32_t slow_finish(const char* lds, const LaneTabs&
 constexpr uint32_t kSlowList = 64u;
 
 // kRows = body size in KiB: 4 (crc_sst4k_kernel) or 1 (crc_sst1k_kernel).
-template <class Src, class Sink, bool kNT, int kRows, bool kDiagNoFold = false>
+// kBlk = blocks per group: 4 (rows of 16 lanes hash the prefixes: <= 256 B) or, for 1-KiB bodies,
+// 8 (rows of 8 lanes: prefixes <= 128 B, one packed tree per 8 blocks).
+template <class Src, class Sink, bool kNT, int kRows, bool kDiagNoFold = false, int kBlk = 4>
 __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ tabs, Src src, uint64_t nblk,
                                                   Sink sink) {
   static_assert(kRows == 1 || kRows == 4, "bodies of 1 or 4 KiB");
-  constexpr uint32_t kBody = 1024u * kRows, kMin = kBody, kMax = kBody + 256u;
+  static_assert(kBlk == 4 || (kBlk == 8 && kRows == 1), "4-block groups, or 8 with 1-KiB bodies");
+  constexpr uint32_t kRowLanes = 64u / kBlk, kRowShift = kBlk == 4 ? 4u : 3u;
+  constexpr uint32_t kBody = 1024u * kRows, kMin = kBody, kMax = kBody + 16u * kRowLanes;
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
   char* lds = reinterpret_cast<char*>(lds_words);
   stage_tables<PDB_CAT_TREE16, PDB_CAT_S1024>(lds, tabs);  // slots 0..5 = 16..512, 6 = 1024
   uint32_t* ctr = reinterpret_cast<uint32_t*>(lds + PDB_MAIN_BYTES + 7 * 4096u);
   const uint64_t g_lo = nblk * blockIdx.x / gridDim.x, g_hi = nblk * (blockIdx.x + 1) / gridDim.x;
-  if (threadIdx.x == 0) *ctr = kWavesPerWg;  // next 4-block group, in groups relative to g_lo
+  if (threadIdx.x == 0) *ctr = kWavesPerWg;  // next kBlk-block group, in groups relative to g_lo
   const uint32_t u = threadIdx.x & 63u;
   const uint32_t ureg = tabs[PDB_UNSHIFT_OFF + (u & 15u)];
   __syncthreads();
   const LaneTabs lt = lane_tabs(u);
-  uint64_t grp = g_lo + 4u * static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
+  uint64_t grp = g_lo + kBlk * static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
   if (grp >= g_hi) return;
   const uintptr_t dummy = reinterpret_cast<uintptr_t>(tabs);  // >= 4 KiB + 256 B of valid bytes
   auto next_group = [&]() -> uint64_t {
     uint32_t r = 0;
     if (u == 0) r = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    return g_lo + 4u * static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(r));
+    return g_lo + kBlk * static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(r));
   };
-  // lane u holds block (group + (u & 3))'s descriptor (clamped into the range: a group past the
-  // end re-reads the last block, never used)
+  // lane u holds block (group + (u % kBlk))'s descriptor (clamped into the range: a group past
+  // the end re-reads the last block, never used)
   auto lane_idx = [&](uint64_t gg) -> uint64_t {
-    const uint64_t i = gg + (u & 3u);
+    const uint64_t i = gg + (u & (kBlk - 1u));
     return i < g_hi ? i : g_hi - 1;
   };
   auto load_desc = [&](uint64_t gg) { return src.load(lane_idx(gg)); };
   struct Grp {
-    BlkDesc ld;      // per lane: block (u & 3)
-    uintptr_t p[4];  // uniform
-    uint32_t n[4];
+    BlkDesc ld;         // per lane: block (u % kBlk)
+    uintptr_t p[kBlk];  // uniform
+    uint32_t n[kBlk];
   };
   auto finish = [&](const typename Src::Raw& raw) -> Grp {
     keep_alive(raw);
@@ -1373,7 +1412,7 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
     const uintptr_t lp = reinterpret_cast<uintptr_t>(G.ld.p);
     const uint32_t lo = static_cast<uint32_t>(lp), hi = static_cast<uint32_t>(static_cast<uint64_t>(lp) >> 32);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < kBlk; ++r) {
       G.p[r] = static_cast<uintptr_t>(uniform64(__builtin_amdgcn_readlane(lo, r), __builtin_amdgcn_readlane(hi, r)));
       G.n[r] = __builtin_amdgcn_readlane(G.ld.n, r);
     }
@@ -1391,9 +1430,10 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
     for (int j = 0; j < kRows; ++j) b[j] = gload128<kNT>(q + 16u * u + 1024u * j);
     last = gload32(q + (s ? kBody : kBody - 4u));
   };
-  // prefix loads of a group: row r = u >> 4 takes block r, lane w the 16 B at bs - 256 + 16w
+  // prefix loads of a group: row r (kRowLanes lanes) takes block r, lane w the 16 B at
+  // bs - 16 kRowLanes + 16w
   auto issue_prefix = [&](MaskedPiece& f, const Grp& G) {
-    const uint32_t row = u >> 4, w = u & 15u;
+    const uint32_t row = u >> kRowShift, w = u & (kRowLanes - 1u);
     // block `row`'s descriptor from lane `row` (bpermute: no per-lane indexing of G.p / G.n)
     const uint64_t lp = reinterpret_cast<uintptr_t>(G.ld.p);
     const uint32_t plo = __shfl(static_cast<uint32_t>(lp), row, 64), phi = __shfl(static_cast<uint32_t>(lp >> 32), row, 64);
@@ -1403,20 +1443,20 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
     const uintptr_t A = ok ? p + n - kMax + 16u * w : dummy + 16u * w;
     issue_masked(f, A, ok ? p : dummy + 256u);  // a slow block's row: all masked
   };
-  // the group's prefix states: P_r in lane 16r + 15 (E_r = 0, n = kBody: the seed itself); the
-  // row tree runs only the levels the longest prefix of the group needs
-  auto prefix_states = [&](const MaskedPiece& pf, const Grp& G, uint32_t (&P)[4]) {
+  // the group's prefix states: P_r in the row's last lane (E_r = 0, n = kBody: the seed itself);
+  // the row tree runs only the levels the longest prefix of the group needs
+  auto prefix_states = [&](const MaskedPiece& pf, const Grp& G, uint32_t (&P)[kBlk]) {
     uint32_t emax = 0;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < kBlk; ++r) {
       const uint32_t e = fast(G.n[r]) ? (G.n[r] - kMin + 15u) >> 4 : 0u;
       emax = e > emax ? e : emax;
     }
     const uint32_t L = emax <= 1 ? 0u : (emax <= 2 ? 1u : (emax <= 4 ? 2u : (emax <= 8 ? 3u : 4u)));
     const uint32_t pref = row_suffix_tree(lds, u, hash_masked(lds, lt, pf, masked_start(pf, ureg)), L);
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-      P[r] = G.n[r] == kMin ? 0xFFFFFFFFu : __builtin_amdgcn_readlane(pref, 16 * r + 15);
+    for (int r = 0; r < kBlk; ++r)
+      P[r] = G.n[r] == kMin ? 0xFFFFFFFFu : __builtin_amdgcn_readlane(pref, kRowLanes * r + kRowLanes - 1);
   };
   // one body's lane partial: chains j (16-B pieces at bs + 16u + 1024j) with the DPP neighbour
   // dword, Horner-folded with shift 1024, P injected as lane 0's start
@@ -1446,7 +1486,7 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
     const uint32_t slowbits = ~fastbits & ((1u << nv) - 1u);
     if (slowbits) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
+      for (int r = 0; r < kBlk; ++r)
         if ((slowbits >> r) & 1u) {
           slow = u == nslow ? static_cast<uint32_t>(grp + r - g_lo) : slow;
           ++nslow;
@@ -1456,7 +1496,7 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
   auto fast_bits = [&](const Grp& G) {
     uint32_t fb = 0;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) fb |= fast(G.n[r]) ? 1u << r : 0u;
+    for (int r = 0; r < kBlk; ++r) fb |= fast(G.n[r]) ? 1u << r : 0u;
     return fb;
   };
   uint64_t ngrp = next_group();
@@ -1512,9 +1552,9 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
         G = NG;
         pre = npre;
         pf = npf;
-        if (nslow > kSlowList - 4u) break;  // no room for another group's slow blocks: drain first
+        if (nslow > kSlowList - kBlk) break;  // no room for another group's slow blocks: drain first
       }
-    } else {
+    } else if constexpr (kBlk == 4) {
       // 1-KiB bodies: the next group's 4 bodies, prefixes and descriptors issued at the top of a
       // group (4 KiB + 1 KiB in flight per wave while this group hashes)
       u32x4 b0, b1, b2, b3;
@@ -1557,7 +1597,64 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
         ngrp = nngrp;
         G = NG;
         pre = npre;
-        if (nslow > kSlowList - 4u) break;  // drain first (pf already holds grp's prefixes)
+        if (nslow > kSlowList - kBlk) break;  // drain first (pf already holds grp's prefixes)
+      }
+    } else {
+      // 1-KiB bodies, 8-block groups: half a group's bodies in flight -- blocks 4..7 load while
+      // 0..3 hash, the next group's 0..3 (with its prefixes and the lookahead descriptors) while
+      // 4..7 hash -- and one tree8_packed per 8 blocks
+      u32x4 b0, b1, b2, b3;
+      uint32_t l0, l1, l2, l3;
+      issue_body(&b0, l0, body_at(G, 0));
+      issue_body(&b1, l1, body_at(G, 1));
+      issue_body(&b2, l2, body_at(G, 2));
+      issue_body(&b3, l3, body_at(G, 3));
+      for (;;) {
+        uint32_t P[8];
+        uint32_t part[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        const uint32_t nv = static_cast<uint32_t>(g_hi - grp < 8 ? g_hi - grp : 8);
+        const uint32_t fastbits = fast_bits(G);
+        {  // blocks 0..3 (loaded a half-group ago); blocks 4..7 start loading
+          const u32x4 c0 = b0, c1 = b1, c2 = b2, c3 = b3;
+          const uint32_t cl0 = l0, cl1 = l1, cl2 = l2, cl3 = l3;
+          issue_body(&b0, l0, body_at(G, 4));
+          issue_body(&b1, l1, body_at(G, 5));
+          issue_body(&b2, l2, body_at(G, 6));
+          issue_body(&b3, l3, body_at(G, 7));
+          prefix_states(pf, G, P);
+          if (fastbits & 1u) part[0] = body_partial(&c0, cl0, static_cast<uint32_t>((G.p[0] + G.n[0]) & 3u), P[0]);
+          if (fastbits & 2u) part[1] = body_partial(&c1, cl1, static_cast<uint32_t>((G.p[1] + G.n[1]) & 3u), P[1]);
+          if (fastbits & 4u) part[2] = body_partial(&c2, cl2, static_cast<uint32_t>((G.p[2] + G.n[2]) & 3u), P[2]);
+          if (fastbits & 8u) part[3] = body_partial(&c3, cl3, static_cast<uint32_t>((G.p[3] + G.n[3]) & 3u), P[3]);
+        }
+        const u32x4 c4 = b0, c5 = b1, c6 = b2, c7 = b3;
+        const uint32_t cl4 = l0, cl5 = l1, cl6 = l2, cl7 = l3;
+        const Grp NG = finish(nraw);
+        issue_body(&b0, l0, body_at(NG, 0));
+        issue_body(&b1, l1, body_at(NG, 1));
+        issue_body(&b2, l2, body_at(NG, 2));
+        issue_body(&b3, l3, body_at(NG, 3));
+        issue_prefix(pf, NG);
+        const uint32_t npre = SinkOps<Sink>::pre(sink, lane_idx(ngrp), NG.ld);
+        uint64_t nngrp = ngrp;
+        if (ngrp < g_hi) nngrp = next_group();
+        nraw = load_desc(nngrp < g_hi ? nngrp : ngrp);
+        if (fastbits & 16u) part[4] = body_partial(&c4, cl4, static_cast<uint32_t>((G.p[4] + G.n[4]) & 3u), P[4]);
+        if (fastbits & 32u) part[5] = body_partial(&c5, cl5, static_cast<uint32_t>((G.p[5] + G.n[5]) & 3u), P[5]);
+        if (fastbits & 64u) part[6] = body_partial(&c6, cl6, static_cast<uint32_t>((G.p[6] + G.n[6]) & 3u), P[6]);
+        if (fastbits & 128u) part[7] = body_partial(&c7, cl7, static_cast<uint32_t>((G.p[7] + G.n[7]) & 3u), P[7]);
+        const uint32_t v = tree8_packed(lds, u, part);
+        if (u < nv && ((fastbits >> u) & 1u)) SinkOps<Sink>::put(sink, grp + u, v, G.ld, pre);
+        defer(G, fastbits, nv);
+        if (ngrp >= g_hi) {
+          done = true;
+          break;
+        }
+        grp = ngrp;
+        ngrp = nngrp;
+        G = NG;
+        pre = npre;
+        if (nslow > kSlowList - kBlk) break;  // drain first (pf already holds grp's prefixes)
       }
     }
     // drain the deferred blocks, block k+1's descriptor and first body loading while k hashes
@@ -1610,10 +1707,10 @@ __global__ __launch_bounds__(kThreads) void crc_sst4k_nofold_kernel(const uint32
   sized_kernel_body<Src, Sink, kNT, 4, true>(tabs, src, nblk, sink);
 }
 
-template <class Src, class Sink, bool kNT>
+template <class Src, class Sink, bool kNT, int kBlk = 8>
 __global__ __launch_bounds__(kThreads) void crc_sst1k_kernel(const uint32_t* __restrict__ tabs, Src src,
                                                              uint64_t nblk, Sink sink) {
-  sized_kernel_body<Src, Sink, kNT, 1>(tabs, src, nblk, sink);
+  sized_kernel_body<Src, Sink, kNT, 1, false, kBlk>(tabs, src, nblk, sink);
 }
 
 uint32_t grid_for(const LaunchGeom& g, uint64_t nblk) {

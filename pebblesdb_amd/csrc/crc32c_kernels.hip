@@ -179,7 +179,8 @@ hipError_t launch_desc(const LaunchGeom& g, const uint32_t* d_tables, const uint
                        const uint32_t* expected, uint32_t* out, uint8_t* ok, uint32_t* nbad,
                        hipStream_t s) {
   if (nblk == 0) return hipSuccess;
-  if (mode == kModeOut && g_fast_variant != 0 && g_fast_variant != 40)  // 40: ignore size hints
+  // 40: ignore size hints; 41: the 1-KiB kernel with 4-block groups
+  if (mode == kModeOut && g_fast_variant != 0 && g_fast_variant != 40 && g_fast_variant != 41)
     return launch_desc_variant(g_fast_variant, g, d_tables, base, blk, nblk, flags, out, s);
   const dim3 grid(grid_for(g, nblk)), block(kThreads);
   const DescSrc src{base, blk, flags};
@@ -189,13 +190,22 @@ hipError_t launch_desc(const LaunchGeom& g, const uint32_t* d_tables, const uint
     const bool k1 = flags & PDB_CRC_SIZE_1K;
 #define PDB_SIZED(K, SINK, ...)                                                                                   \
   hipLaunchKernelGGL((K<DescSrc, SINK, true>), grid, block, 0, s, d_tables, src, nblk, SINK{__VA_ARGS__})
+#define PDB_SIZED1K4(SINK, ...)                                                                                  \
+  hipLaunchKernelGGL((crc_sst1k_kernel<DescSrc, SINK, true, 4>), grid, block, 0, s, d_tables, src, nblk,         \
+                     SINK{__VA_ARGS__})
+    // 1-KiB class: 8-block groups (fast range 1024..1152 B: WAL records of ~1-KiB batches), A/B
+    // variant 41 the 4-block version (1024..1280 B)
+    const bool g4 = g_fast_variant == 41;
     if (mode == kModeOut) {
-      if (k1) PDB_SIZED(crc_sst1k_kernel, OutSink, out, flags);
+      if (k1 && g4) PDB_SIZED1K4(OutSink, out, flags);
+      else if (k1) PDB_SIZED(crc_sst1k_kernel, OutSink, out, flags);
       else PDB_SIZED(crc_sst4k_kernel, OutSink, out, flags);
     } else {
-      if (k1) PDB_SIZED(crc_sst1k_kernel, VerifySink, expected, ok, nbad, flags);
+      if (k1 && g4) PDB_SIZED1K4(VerifySink, expected, ok, nbad, flags);
+      else if (k1) PDB_SIZED(crc_sst1k_kernel, VerifySink, expected, ok, nbad, flags);
       else PDB_SIZED(crc_sst4k_kernel, VerifySink, expected, ok, nbad, flags);
     }
+#undef PDB_SIZED1K4
 #undef PDB_SIZED
     return hipGetLastError();
   }

@@ -198,7 +198,8 @@ def test_new_path_matches_previous_kernel(crc):
 
 # ---- descriptor batches with a size-class hint: crc_sst1k_kernel / crc_sst4k_kernel<DescSrc> ----
 EDGE_1K = [0, 1, 2, 3, 4, 15, 16, 17, 100, 255, 256, 257, 1000, 1023, 1024, 1025, 1026, 1027, 1039, 1040,
-           1041, 1055, 1056, 1100, 1264, 1265, 1279, 1280, 1281, 1282, 2048, 4095, 4096, 4097, 5000, 70000]
+           1041, 1055, 1056, 1100, 1136, 1137, 1151, 1152, 1153, 1168, 1264, 1265, 1279, 1280, 1281, 1282, 2048,
+           4095, 4096, 4097, 5000, 70000]
 
 
 def _desc_case(crc, sizes, seed, gap_max=7):
@@ -272,7 +273,8 @@ def test_host_batch_picks_size_class(crc, oracle_lib, lo, hi):
 
 
 def test_sized_kernels_match_generic_kernel(crc):
-    """Variant 40 ignores the hints (crc_stream16_kernel): identical CRCs on a mixed batch."""
+    """Variant 40 ignores the hints (crc_stream16_kernel), 41 runs the 1-KiB kernel with 4-block
+    groups: identical CRCs on a mixed batch."""
     from pebblesdb_amd._native import lib
 
     rng = np.random.Generator(np.random.PCG64(81))
@@ -282,11 +284,12 @@ def test_sized_kernels_match_generic_kernel(crc):
     base, blk = _desc_case(crc, sizes, 82)
     d_base, d_blk = torch.from_numpy(base).cuda(), crc.blocks_to_device(blk)
     res = []
-    for v in (0, 40):
+    for v in (0, 40, 41):
         lib().pdb_diag_set_variant(v)
         try:
             res.append([crc.batch(d_base, d_blk, size_hint=h).cpu().numpy() for h in ("1k", "4k")])
         finally:
             lib().pdb_diag_set_variant(0)
-    for a, b in zip(res[0], res[1]):
-        assert (a == b).all()
+    for other in res[1:]:
+        for a, b in zip(res[0], other):
+            assert (a == b).all()
