@@ -59,7 +59,7 @@ typedef struct pdb_block_handle {
 #define PDB_CRC_USE_INIT 0x2u    /* crc = Extend(blk.init, ...) instead of Value(...) */
 /* Size-class hints for descriptor batches (speed only: results are identical with or without;
  * ignored with PDB_CRC_USE_INIT).  Host batch entries pick the class themselves from the lengths. */
-#define PDB_CRC_SIZE_1K 0x4u /* most blocks 1024..1280 B: WAL physical records (type || fragment) */
+#define PDB_CRC_SIZE_1K 0x4u /* most blocks 1024..1152 B: WAL physical records (type || fragment) */
 #define PDB_CRC_SIZE_4K 0x8u /* most blocks 4096..4352 B: sstable data blocks (contents || type) */
 
 /* error codes */

@@ -27,7 +27,7 @@ from ._native import PdbError, check, lib
 
 MASK_OUTPUT = 0x1  # PDB_CRC_MASK_OUTPUT
 USE_INIT = 0x2  # PDB_CRC_USE_INIT
-SIZE_1K = 0x4  # PDB_CRC_SIZE_1K: most blocks 1024..1280 B (WAL records) -- a speed hint only
+SIZE_1K = 0x4  # PDB_CRC_SIZE_1K: most blocks 1024..1152 B (WAL records) -- a speed hint only
 SIZE_4K = 0x8  # PDB_CRC_SIZE_4K: most blocks 4096..4352 B (sstable data blocks)
 _SIZE_HINT = {None: 0, "1k": SIZE_1K, "4k": SIZE_4K}
 K_MASK_DELTA = 0xA282EAD8  # util/crc32c.h:24

@@ -355,7 +355,7 @@ int host_desc(const uint8_t* base, uint64_t base_len, const pdb_blk* blk, uint64
   for (uint64_t i = 0; i < nblk; ++i) {
     if (blk[i].off > base_len || blk[i].len > base_len - blk[i].off)
       return fail(PDB_ERANGE, "block " + std::to_string(i) + " exceeds base_len");
-    n1k += blk[i].len - 1024u <= 256u;
+    n1k += blk[i].len - 1024u <= 128u;
     n4k += blk[i].len - 4096u <= 256u;
     if (blk[i].len) {
       const uint64_t lo = std::min(g.lo, blk[i].off & ~static_cast<uint64_t>(15));

@@ -1213,8 +1213,9 @@ __global__ __launch_bounds__(kThreads) void crc_stream16_kernel(const uint32_t* 
 // and hashed after the loop by the slow path (below).
 // crc_sst1k_kernel is the same design for ~1-KiB blocks (WAL physical records: type || fragment
 // of a ~1-KiB write batch, db/log_writer.cc:111-121): body = the last 1 KiB (one chain per lane,
-// the 4 blocks of a group in 4 chains), fast range [1024, 1280], the next group's 4 bodies in
-// flight while one group is hashed.
+// one block per chain), 8-block groups whose prefixes are hashed in rows of 8 lanes (fast range
+// [1024, 1152]) and folded by one tree8_packed, half a group's bodies in flight; kBlk = 4 (A/B)
+// keeps rows of 16 lanes ([1024, 1280]) and 4-block trees.
 // Valid only for Value()-seeded CRCs (init 0xFFFFFFFF): SstSrc always, FixedSrc / DescSrc without
 // an Extend seed.
 constexpr uint32_t kSstMin = 4096u, kSstMax = 4096u + 256u;

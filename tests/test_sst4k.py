@@ -259,7 +259,7 @@ def test_size_hint_ignored_with_extend_seed(crc, oracle_lib):
     assert (got.cpu().numpy().view(np.uint32) == oracle_lib.batch(base, blk, flags=2, nthreads=8)).all()
 
 
-@pytest.mark.parametrize("lo,hi", [(1024, 1281), (4096, 4353), (900, 1400)])
+@pytest.mark.parametrize("lo,hi", [(1024, 1153), (4096, 4353), (900, 1400)])
 def test_host_batch_picks_size_class(crc, oracle_lib, lo, hi):
     """pdb_crc32c_batch_host / verify_host choose the sized kernel from the host-visible lengths."""
     rng = np.random.Generator(np.random.PCG64(lo))
