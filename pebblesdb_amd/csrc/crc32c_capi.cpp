@@ -585,7 +585,7 @@ int host_sst(uint8_t* buf, uint64_t buf_len, const pdb_block_handle* h, uint64_t
     const pdb_block_handle* d_h = reinterpret_cast<const pdb_block_handle*>(ws + off_h);
     if (seal) {
       uint32_t* d_crc = reinterpret_cast<uint32_t*>(ws + off_ok);
-      if ((e = launch_sst_masked(st->geom, st->d_tables, ws, d_h, x.count, d_crc, s)) != hipSuccess)
+      if ((e = launch_sst_masked(st->geom, st->d_tables, ws, x.hi - x.lo, d_h, x.count, d_crc, s)) != hipSuccess)
         return hip_fail(e, "launch_sst_masked");
       if ((e = hipMemcpyAsync(crc.data() + x.first, d_crc, x.count * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
         return hip_fail(e, "hipMemcpyAsync(crcs)");
@@ -743,6 +743,9 @@ int pdb_sst_seal_device(void* d_buf, uint64_t buf_len, const pdb_block_handle* d
                         void* stream) {
   if (n == 0) return PDB_OK;
   if (!d_buf || !d_h) return fail(PDB_EINVAL, "null argument");
+  // a handle whose block + trailer leaves the buffer is reported bad (verify) or skipped (seal)
+  // by the kernel; below one trailer there is no valid handle at all
+  if (buf_len < 5) return fail(PDB_ERANGE, "buffer smaller than one block trailer");
   DevState* st;
   int rc = get_state(&st);
   if (rc) return rc;
@@ -756,6 +759,9 @@ int pdb_sst_verify_device(const void* d_buf, uint64_t buf_len, const pdb_block_h
                           uint64_t n, uint8_t* d_ok, uint32_t* d_nbad, void* stream) {
   if (n == 0) return PDB_OK;
   if (!d_buf || !d_h) return fail(PDB_EINVAL, "null argument");
+  // a handle whose block + trailer leaves the buffer is reported bad (verify) or skipped (seal)
+  // by the kernel; below one trailer there is no valid handle at all
+  if (buf_len < 5) return fail(PDB_ERANGE, "buffer smaller than one block trailer");
   DevState* st;
   int rc = get_state(&st);
   if (rc) return rc;

@@ -563,20 +563,26 @@ struct DescSrc {
 };
 
 // sstable handle: CRC over contents || type (table/table_builder.cc:197-198; format.cc:98).
+// A handle whose block + 5-byte trailer does not fit the buffer (ReadBlock's "truncated block
+// read", table/format.cc:84-87 -- a corrupt index must not make the kernel read or write outside
+// the image) maps to {buf, 0, 0}: nothing is hashed, and init_raw 0 (never Value()'s seed) tells
+// the sst sinks to report the block bad (verify) or leave it alone (seal).
 struct SstSrc {
   uint8_t* buf;
   const pdb_block_handle* h;
+  uint64_t len;  // image bytes
   using Raw = u32x4;  // pdb_block_handle {offset lo, hi, size lo, hi}
   __device__ __forceinline__ Raw load(uint64_t i) const {
     return __builtin_nontemporal_load(reinterpret_cast<const u32x4a4*>(h + i));
   }
-  __device__ __forceinline__ BlkDesc finish(const Raw& r) const {
-    return {buf + uniform64(r.x, r.y), static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(r.z)) + 1u,
-            0xFFFFFFFFu};
+  __device__ __forceinline__ BlkDesc make(uint64_t off, uint64_t size) const {
+    const bool ok = len >= 5 && off <= len - 5 && size <= len - 5 - off && size < 0xFFFFFFFFull;
+    return ok ? BlkDesc{buf + off, static_cast<uint32_t>(size) + 1u, 0xFFFFFFFFu} : BlkDesc{buf, 0u, 0u};
   }
+  __device__ __forceinline__ BlkDesc finish(const Raw& r) const { return make(uniform64(r.x, r.y), uniform64(r.z, r.w)); }
   __device__ __forceinline__ BlkDesc get(uint64_t i) const { return finish(load(i)); }
   __device__ __forceinline__ BlkDesc lane(const Raw& r) const {  // per-lane fields (no readfirstlane)
-    return {buf + ((static_cast<uint64_t>(r.y) << 32) | r.x), r.z + 1u, 0xFFFFFFFFu};
+    return make((static_cast<uint64_t>(r.y) << 32) | r.x, (static_cast<uint64_t>(r.w) << 32) | r.z);
   }
 };
 
@@ -603,6 +609,7 @@ struct VerifySink {
 // Seal: EncodeFixed32(trailer + 1, Mask(crc)) at contents + size + 1 = p + n.
 struct SealSink {
   __device__ __forceinline__ void put(uint64_t, uint32_t raw, const BlkDesc& d) const {
+    if (d.init_raw == 0) return;  // invalid handle (SstSrc): nothing to seal
     uint8_t* tr = const_cast<uint8_t*>(d.p) + d.n;
     const uint32_t m = pdb_mask(~raw);
     tr[0] = static_cast<uint8_t>(m);
@@ -620,7 +627,7 @@ struct SstVerifySink {
     const uint8_t* tr = d.p + d.n;
     const uint32_t stored = static_cast<uint32_t>(tr[0]) | (static_cast<uint32_t>(tr[1]) << 8) |
                             (static_cast<uint32_t>(tr[2]) << 16) | (static_cast<uint32_t>(tr[3]) << 24);
-    const bool good = pdb_unmask(stored) == ~raw;
+    const bool good = d.init_raw != 0 && pdb_unmask(stored) == ~raw;  // init_raw 0: invalid handle
     if (ok) ok[i] = good ? 1 : 0;
     if (!good && nbad) atomicAdd(nbad, 1u);
   }
@@ -656,6 +663,7 @@ template <>
 struct SinkOps<SealSink> {
   __device__ static __forceinline__ uint32_t pre(const SealSink&, uint64_t, const BlkDesc&) { return 0u; }
   __device__ static __forceinline__ void put(const SealSink&, uint64_t, uint32_t raw, const BlkDesc& d, uint32_t) {
+    if (d.init_raw == 0) return;  // invalid handle (SstSrc): nothing to seal
     typedef __attribute__((address_space(1))) uint8_t g_u8;
     g_u8* tr = reinterpret_cast<g_u8*>(reinterpret_cast<uintptr_t>(d.p) + d.n);
     const uint32_t m = pdb_mask(~raw);
@@ -676,9 +684,9 @@ struct SinkOps<SstVerifySink> {
     const uint32_t lo = *reinterpret_cast<g_u32_*>(a - s), hi = *reinterpret_cast<g_u32_*>(a - s + (s ? 4u : 0u));
     return __builtin_amdgcn_alignbyte(hi, lo, s);
   }
-  __device__ static __forceinline__ void put(const SstVerifySink& k, uint64_t i, uint32_t raw, const BlkDesc&,
+  __device__ static __forceinline__ void put(const SstVerifySink& k, uint64_t i, uint32_t raw, const BlkDesc& d,
                                              uint32_t stored) {
-    const bool good = pdb_unmask(stored) == ~raw;
+    const bool good = d.init_raw != 0 && pdb_unmask(stored) == ~raw;  // init_raw 0: invalid handle
     if (k.ok) k.ok[i] = good ? 1 : 0;
     if (!good && k.nbad) atomicAdd(k.nbad, 1u);
   }
@@ -1327,10 +1335,12 @@ __device__ __forceinline__ uintptr_t slow_vbs(uintptr_t p, uint32_t n) {
   return p + n - (static_cast<uintptr_t>(nb) << 12);
 }
 
-__device__ __forceinline__ void slow_issue(SlowFirst& sf, uintptr_t p, uint32_t n, uint32_t u) {
-  const uintptr_t v = slow_vbs(p, n) + 16u * u;
+// An empty block reads nothing of its own: its (discarded) loads go to `dummy`.
+__device__ __forceinline__ void slow_issue(SlowFirst& sf, uintptr_t p, uint32_t n, uint32_t u, uintptr_t dummy) {
+  const uintptr_t lo = n ? p : dummy;
+  const uintptr_t v = (n ? slow_vbs(p, n) : dummy) + 16u * u;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) issue_masked(sf.f[j], v + 1024u * j, p);
+  for (int j = 0; j < 4; ++j) issue_masked(sf.f[j], v + 1024u * j, lo);
 }
 
 __device__ __forceinline__ uint32_t slow_finish(const char* lds, const LaneTabs& lt, uint32_t u, uint32_t ureg,
@@ -1677,7 +1687,7 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
         S.p = static_cast<uintptr_t>(uniform64(static_cast<uint32_t>(lp), static_cast<uint32_t>(lp >> 32)));
         S.n = __builtin_amdgcn_readfirstlane(S.d.n);
         S.pre = SinkOps<Sink>::pre(sink, i, S.d);
-        slow_issue(S.sf, S.p, S.n, u);
+        slow_issue(S.sf, S.p, S.n, u, dummy);
       };
       Slow cur;
       stage(cur, idx(0), src.load(idx(0)));

@@ -40,8 +40,8 @@ hipError_t launch_sst(const LaunchGeom& g, const uint32_t* d_tables, uint8_t* bu
                       const pdb_block_handle* h, uint64_t n, bool seal, uint8_t* ok, uint32_t* nbad,
                       hipStream_t s);
 // out[i] = Mask(crc32c(contents_i || type_i)) -- the trailer word a seal writes, as an array.
-hipError_t launch_sst_masked(const LaunchGeom& g, const uint32_t* d_tables, uint8_t* buf, const pdb_block_handle* h,
-                             uint64_t n, uint32_t* out, hipStream_t s);
+hipError_t launch_sst_masked(const LaunchGeom& g, const uint32_t* d_tables, uint8_t* buf, uint64_t buf_len,
+                             const pdb_block_handle* h, uint64_t n, uint32_t* out, hipStream_t s);
 // Long span: raw CRCs of `nseg` segments of 2^seg_log2 bytes (+ the tail) in parallel, then a
 // one-workgroup tree combine with the power-of-two operators.  `scratch` holds
 // span_scratch_words(n) u32.  *out = Extend(init, data[0..n)).
@@ -90,7 +90,7 @@ hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tab
                                hipStream_t s);
 // sstable hooks: 18 = crc_stream_kernel (32-B pieces), 30 = crc_stream16_kernel (the previous
 // default), 31-36 seal-write diagnostics, 97 verify without the Horner folds (wrong CRCs)
-hipError_t launch_sst_variant(int v, const LaunchGeom& g, const uint32_t* d_tables, uint8_t* buf,
+hipError_t launch_sst_variant(int v, const LaunchGeom& g, const uint32_t* d_tables, uint8_t* buf, uint64_t buf_len,
                               const pdb_block_handle* h, uint64_t n, bool seal, uint8_t* ok, uint32_t* nbad,
                               hipStream_t s);
 hipError_t launch_read_stream(const uint8_t* base, uint64_t nbytes, uint32_t* out, hipStream_t s);

@@ -224,14 +224,13 @@ hipError_t launch_desc(const LaunchGeom& g, const uint32_t* d_tables, const uint
 hipError_t launch_sst(const LaunchGeom& g, const uint32_t* d_tables, uint8_t* buf, uint64_t buf_len,
                       const pdb_block_handle* h, uint64_t n, bool seal, uint8_t* ok, uint32_t* nbad,
                       hipStream_t s) {
-  (void)buf_len;
   if (n == 0) return hipSuccess;
-  if (g_fast_variant != 0) return launch_sst_variant(g_fast_variant, g, d_tables, buf, h, n, seal, ok, nbad, s);
+  if (g_fast_variant != 0) return launch_sst_variant(g_fast_variant, g, d_tables, buf, buf_len, h, n, seal, ok, nbad, s);
   const dim3 grid(grid_for(g, n)), block(kThreads);
   // exact 4-KiB body + batched prefix for the 4096..4352-B blocks (every data block TableBuilder
   // emits: contents + type), the slow path in the same launch for the rest
   // (profiles/r01_ab_sst4k.json: verify +45 %, seal +27 % over crc_stream16_kernel)
-  const SstSrc src{buf, h};
+  const SstSrc src{buf, h, buf_len};  // handles outside the image are reported, never followed
   if (seal)
     hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SealSink, true>), grid, block, 0, s, d_tables, src, n, SealSink{});
   else
@@ -240,17 +239,17 @@ hipError_t launch_sst(const LaunchGeom& g, const uint32_t* d_tables, uint8_t* bu
   return hipGetLastError();
 }
 
-hipError_t launch_sst_masked(const LaunchGeom& g, const uint32_t* d_tables, uint8_t* buf, const pdb_block_handle* h,
-                             uint64_t n, uint32_t* out, hipStream_t s) {
+hipError_t launch_sst_masked(const LaunchGeom& g, const uint32_t* d_tables, uint8_t* buf, uint64_t buf_len,
+                             const pdb_block_handle* h, uint64_t n, uint32_t* out, hipStream_t s) {
   if (n == 0) return hipSuccess;
   const dim3 grid(grid_for(g, n)), block(kThreads);
   // the seal's CRCs into a compact array (host seal: 4 B per block back across PCIe, not the span)
   if (g_fast_variant == 0)
-    hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, OutSink, true>), grid, block, 0, s, d_tables, SstSrc{buf, h}, n,
+    hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, OutSink, true>), grid, block, 0, s, d_tables, SstSrc{buf, h, buf_len}, n,
                        OutSink{out, PDB_CRC_MASK_OUTPUT});
   else
     hipLaunchKernelGGL((crc_stream16_kernel<SstSrc, OutSink, true, true, true>), grid, block, 0, s, d_tables,
-                       SstSrc{buf, h}, n, OutSink{out, PDB_CRC_MASK_OUTPUT});
+                       SstSrc{buf, h, buf_len}, n, OutSink{out, PDB_CRC_MASK_OUTPUT});
   return hipGetLastError();
 }
 

@@ -413,11 +413,11 @@ struct SinkOps<SealTouchSink> {
 
 }  // namespace
 
-hipError_t launch_sst_variant(int v, const LaunchGeom& g, const uint32_t* d_tables, uint8_t* buf,
+hipError_t launch_sst_variant(int v, const LaunchGeom& g, const uint32_t* d_tables, uint8_t* buf, uint64_t buf_len,
                               const pdb_block_handle* h, uint64_t n, bool seal, uint8_t* ok, uint32_t* nbad,
                               hipStream_t s) {
   const dim3 grid(grid_for(g, n)), block(kThreads);
-  const SstSrc src{buf, h};
+  const SstSrc src{buf, h, buf_len};
   if (v == 97 && !seal) {  // WRONG CRCs by design: verify without the Horner folds (prices them)
     hipLaunchKernelGGL((crc_sst4k_nofold_kernel<SstSrc, SstVerifySink, true>), grid, block, 0, s, d_tables, src, n,
                        SstVerifySink{ok, nullptr});  // no nbad: every block "fails"; 1M atomics would dominate

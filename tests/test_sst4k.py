@@ -293,3 +293,48 @@ def test_sized_kernels_match_generic_kernel(crc):
     for other in res[1:]:
         for a, b in zip(res[0], other):
             assert (a == b).all()
+
+
+@pytest.mark.parametrize("variant", [0, 30])
+def test_handles_outside_image_are_reported_not_followed(crc, oracle_lib, variant):
+    """A corrupt index can hand out any (offset, size): blocks whose contents + 5-byte trailer do
+    not fit the image are bad (verify) and untouched (seal) -- ReadBlock's "truncated block read"
+    (table/format.cc:84-87) -- and the kernel never reads or writes outside the image.  The tail of
+    the image is a guard region the handles must not reach."""
+    from pebblesdb_amd import table as T
+    from pebblesdb_amd._native import lib
+
+    rng = np.random.Generator(np.random.PCG64(91))
+    sizes = rng.integers(4095, 4352, size=600)
+    sizes[::9] = rng.integers(0, 9000, size=len(sizes[::9]))
+    img, offs = _image(sizes, 92)
+    total = int(offs[-1] + sizes[-1] + 5)  # the image proper; img carries 16 more bytes
+    exp = _expected_trailers(oracle_lib, crc, img, offs, sizes)
+    h = np.zeros(len(sizes), dtype=crc.HANDLE_DTYPE)
+    h["offset"], h["size"] = offs, sizes
+    bad = rng.choice(len(sizes), size=40, replace=False)
+    kinds = np.arange(len(bad)) % 4
+    h["offset"][bad[kinds == 0]] = total - 4                   # trailer past the end
+    h["size"][bad[kinds == 1]] = total                         # contents past the end
+    h["offset"][bad[kinds == 2]] = np.uint64(1) << np.uint64(62)  # offset far out
+    h["size"][bad[kinds == 3]] = (np.uint64(1) << np.uint64(32)) + np.uint64(10)  # >= 4 GiB
+    guard = np.full(1 << 16, 0xA5, dtype=np.uint8)
+    d_img = torch.from_numpy(np.concatenate([img[:total], guard])).cuda()
+    d_h = T.handles_to_device(h)
+    before = d_img.cpu().numpy().copy()
+    lib().pdb_diag_set_variant(variant)
+    try:
+        sp = int(torch.cuda.current_stream().cuda_stream)
+        assert lib().pdb_sst_seal_device(d_img.data_ptr(), total, d_h.data_ptr(), len(sizes), sp) == 0
+        after = d_img.cpu().numpy()
+        good = np.setdiff1d(np.arange(len(sizes)), bad)
+        assert (_trailers(after, offs[good], sizes[good]) == exp[good]).all()
+        assert (after[total:] == before[total:]).all(), "seal wrote outside the image"
+        ok = torch.empty(len(sizes), dtype=torch.uint8, device="cuda")
+        nbad = torch.zeros(1, dtype=torch.int32, device="cuda")
+        assert lib().pdb_sst_verify_device(d_img.data_ptr(), total, d_h.data_ptr(), len(sizes), ok.data_ptr(),
+                                           nbad.data_ptr(), sp) == 0
+        okn = ok.cpu().numpy()
+        assert int(nbad.item()) == len(bad) and (okn[bad] == 0).all() and (okn[good] == 1).all()
+    finally:
+        lib().pdb_diag_set_variant(0)
