@@ -38,7 +38,8 @@ def parse():
     # 40: the first ~20-30 launches of a cold GPU run slower (clock / power settling; see
     # DESIGN.md §6), so the default warmup covers them
     ap.add_argument("--warmup", type=int, default=40)
-    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "sstable", "sst_verify", "sst_seal", "wal"],
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "sstable", "sst_verify", "sst_seal", "sst_crc",
+                                                        "wal"],
                     help="c2 (default, the headline) / c3: BASELINE configs; sstable: the C2 blocks in "
                          "sstable layout; sst_verify / sst_seal: SURVEY §8(f) rows 1-2 on a device sstable "
                          "image of ~4.17-KiB blocks; wal: row 3, the log record CRC over 32-KiB log blocks")
@@ -147,7 +148,7 @@ def main():
 
         workload = {"workload": "sstable layout: 4096 B contents + type byte, stride 4101 (unaligned)",
                     "block_bytes": L, "blocks_per_gpu": nblk, "bytes_per_gpu": hashed}
-    elif args.workload in ("sst_verify", "sst_seal"):
+    elif args.workload in ("sst_verify", "sst_seal", "sst_crc"):
         # sstable image: contents of 4166..4174 B (db_bench data blocks flush just past the 4-KiB
         # block_size: 4171-4175 B with the type byte), type 0, 5-B trailer
         from pebblesdb_amd import table as T
@@ -178,6 +179,11 @@ def main():
             def step():
                 check(lib().pdb_sst_verify_device(data.data_ptr(), total, d_h.data_ptr(), nblk, ok.data_ptr(),
                                                   nbad.data_ptr(), sp))
+        elif args.workload == "sst_crc":  # the seal's trailer words into a compact array
+            out = torch.zeros(nblk, dtype=torch.int32, device=dev)
+
+            def step():
+                check(lib().pdb_sst_crc_device(data.data_ptr(), total, d_h.data_ptr(), nblk, out.data_ptr(), sp))
         else:
             def step():
                 check(lib().pdb_sst_seal_device(data.data_ptr(), total, d_h.data_ptr(), nblk, sp))
@@ -229,7 +235,7 @@ def main():
     algo_bytes = hashed + 4 * nblk + (16 * nblk if args.workload in ("c3", "wal") else 0)
     if args.workload == "sst_verify":  # + the 4-B stored trailer read, 16-B handle, 1-B ok written
         algo_bytes = hashed + nblk * (4 + 16 + 1)
-    elif args.workload == "sst_seal":  # + 4-B trailer written, 16-B handle
+    elif args.workload in ("sst_seal", "sst_crc"):  # + 4-B trailer / CRC written, 16-B handle
         algo_bytes = hashed + nblk * (4 + 16)
 
     # ---- warmup + timed region -------------------------------------------------------------
@@ -326,7 +332,8 @@ def main():
                            "c3": "crc_stream16_kernel<DescSrc,OutSink,dyn,nt,pack>",
                            "wal": "crc_sst1k_kernel<DescSrc,OutSink,nt>",
                            "sst_verify": "crc_sst4k_kernel<SstSrc,SstVerifySink,nt>",
-                           "sst_seal": "crc_sst4k_kernel<SstSrc,SealSink,nt>"}[args.workload],
+                           "sst_seal": "crc_sst4k_kernel<SstSrc,SealSink,nt>",
+                           "sst_crc": "crc_sst4k_kernel<SstSrc,SstCrcSink,nt>"}[args.workload],
                 "algorithmic_bytes_per_launch": algo_bytes,
                 "kernel_avg_ms": round(kern_avg_ms, 4),
                 "kernel_min_ms": round(float(np.min(kern_ms)), 4),

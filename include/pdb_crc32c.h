@@ -124,6 +124,12 @@ int64_t pdb_crc32c_verify_host(const void* base, uint64_t base_len, const pdb_bl
 int pdb_sst_seal_device(void* d_buf, uint64_t buf_len, const pdb_block_handle* d_h, uint64_t n,
                         void* stream);
 int pdb_sst_seal_host(void* buf, uint64_t buf_len, const pdb_block_handle* h, uint64_t n);
+/* The seal's trailer words without writing them: d_out[i] = Mask(crc32c(contents||type)) (the
+ * value WriteRawBlock encodes at offset+size+1), for an engine that writes the trailer while it
+ * copies blocks out -- the in-place seal pays for scattered 4-B writes, this form does not.  A
+ * handle whose block + trailer leaves the image leaves d_out[i] untouched. */
+int pdb_sst_crc_device(const void* d_buf, uint64_t buf_len, const pdb_block_handle* d_h, uint64_t n,
+                       uint32_t* d_out, void* stream);
 /* Verify: ok[i] = 1 iff Unmask(DecodeFixed32(trailer+1)) == crc32c(contents||type).
  * Returns the number of mismatching blocks (>= 0) or a negative error. */
 int64_t pdb_sst_verify_host(const void* buf, uint64_t buf_len, const pdb_block_handle* h, uint64_t n,

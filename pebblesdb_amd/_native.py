@@ -57,6 +57,7 @@ SIGNATURES = {
     "pdb_sst_seal_host": (_I, [_V, _U64, _V, _U64]),
     "pdb_sst_verify_host": (ctypes.c_int64, [_V, _U64, _V, _U64, _V]),
     "pdb_sst_verify_device": (_I, [_V, _U64, _V, _U64, _V, _V, _V]),
+    "pdb_sst_crc_device": (_I, [_V, _U64, _V, _U64, _V, _V]),
     "pdb_diag_server_stats": (_I, [_V]),
     "pdb_diag_set_host_chunk": (_U64, [_U64]),
     "pdb_diag_read_stream": (_I, [_V, _U64, _V, _V]),

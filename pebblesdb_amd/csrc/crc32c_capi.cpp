@@ -771,6 +771,20 @@ int pdb_sst_verify_device(const void* d_buf, uint64_t buf_len, const pdb_block_h
   return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_sst(verify)");
 }
 
+int pdb_sst_crc_device(const void* d_buf, uint64_t buf_len, const pdb_block_handle* d_h, uint64_t n,
+                       uint32_t* d_out, void* stream) {
+  if (n == 0) return PDB_OK;
+  if (!d_buf || !d_h || !d_out) return fail(PDB_EINVAL, "null argument");
+  if (buf_len < 5) return fail(PDB_ERANGE, "buffer smaller than one block trailer");
+  DevState* st;
+  int rc = get_state(&st);
+  if (rc) return rc;
+  if ((rc = quiesce(st))) return rc;
+  hipError_t e = launch_sst_masked(st->geom, st->d_tables, static_cast<uint8_t*>(const_cast<void*>(d_buf)), buf_len,
+                                   d_h, n, d_out, pick_stream(st, stream));
+  return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_sst_masked");
+}
+
 int pdb_sst_seal_host(void* buf, uint64_t buf_len, const pdb_block_handle* h, uint64_t n) {
   return host_sst(static_cast<uint8_t*>(buf), buf_len, h, n, true, nullptr, nullptr);
 }

@@ -633,6 +633,15 @@ struct SstVerifySink {
   }
 };
 
+// The seal's trailer words into a compact array (pdb_sst_crc_device, the host seal's staging):
+// out[i] = Mask(crc); an invalid handle (SstSrc init_raw 0) leaves out[i] untouched.
+struct SstCrcSink {
+  uint32_t* out;
+  __device__ __forceinline__ void put(uint64_t i, uint32_t raw, const BlkDesc& d) const {
+    if (d.init_raw != 0) out[i] = pdb_mask(~raw);
+  }
+};
+
 // Sink access for crc_sst4k_kernel: pre() issues whatever the sink reads (the stored trailer a
 // verify compares with) a group ahead, so put() never waits on a load issued after the next
 // group's prefetch; all accesses through global-address-space pointers (the kernel's block

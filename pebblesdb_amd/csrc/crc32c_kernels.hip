@@ -243,13 +243,15 @@ hipError_t launch_sst_masked(const LaunchGeom& g, const uint32_t* d_tables, uint
                              const pdb_block_handle* h, uint64_t n, uint32_t* out, hipStream_t s) {
   if (n == 0) return hipSuccess;
   const dim3 grid(grid_for(g, n)), block(kThreads);
-  // the seal's CRCs into a compact array (host seal: 4 B per block back across PCIe, not the span)
+  // the seal's masked CRCs into a compact array (pdb_sst_crc_device; the host seal brings back 4 B
+  // per block across PCIe, not the span)
+  const SstSrc src{buf, h, buf_len};
   if (g_fast_variant == 0)
-    hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, OutSink, true>), grid, block, 0, s, d_tables, SstSrc{buf, h, buf_len}, n,
-                       OutSink{out, PDB_CRC_MASK_OUTPUT});
+    hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstCrcSink, true>), grid, block, 0, s, d_tables, src, n,
+                       SstCrcSink{out});
   else
-    hipLaunchKernelGGL((crc_stream16_kernel<SstSrc, OutSink, true, true, true>), grid, block, 0, s, d_tables,
-                       SstSrc{buf, h, buf_len}, n, OutSink{out, PDB_CRC_MASK_OUTPUT});
+    hipLaunchKernelGGL((crc_stream16_kernel<SstSrc, SstCrcSink, true, true, true>), grid, block, 0, s, d_tables, src,
+                       n, SstCrcSink{out});
   return hipGetLastError();
 }
 

@@ -285,6 +285,20 @@ def seal_device(d_image, d_handles, stream=None) -> None:
                                     _stream(stream)))
 
 
+def crc_device(d_image, d_handles, stream=None, out=None):
+    """The seal's trailer words without writing them: int32 tensor of Mask(crc32c(contents||type))
+    per handle (an engine writes the trailer while it copies blocks out; the in-place seal pays
+    for scattered 4-B writes).  Out-of-image handles leave their entry untouched (zero here)."""
+    import torch
+
+    n = d_handles.numel() * d_handles.element_size() // 16
+    if out is None:
+        out = torch.zeros(n, dtype=torch.int32, device=d_image.device)
+    check(lib().pdb_sst_crc_device(_dev(d_image), d_image.numel() * d_image.element_size(), _dev(d_handles), n,
+                                   _dev(out), _stream(stream)))
+    return out
+
+
 def verify_device(d_image, d_handles, stream=None):
     """ReadBlock's check for every handle of a device image -> (ok uint8 tensor, nbad int32[1])."""
     import torch

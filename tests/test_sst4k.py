@@ -338,3 +338,25 @@ def test_handles_outside_image_are_reported_not_followed(crc, oracle_lib, varian
         assert int(nbad.item()) == len(bad) and (okn[bad] == 0).all() and (okn[good] == 1).all()
     finally:
         lib().pdb_diag_set_variant(0)
+
+
+def test_sst_crc_device_matches_seal(crc, oracle_lib):
+    """pdb_sst_crc_device: the trailer words a seal would write, as a compact array; out-of-image
+    handles leave their entry untouched."""
+    from pebblesdb_amd import table as T
+
+    rng = np.random.Generator(np.random.PCG64(101))
+    sizes = rng.integers(4095, 4352, size=3000)
+    sizes[::13] = rng.integers(0, 20000, size=len(sizes[::13]))
+    img, offs = _image(sizes, 102)
+    exp = _expected_trailers(oracle_lib, crc, img, offs, sizes)
+    h = np.zeros(len(sizes), dtype=crc.HANDLE_DTYPE)
+    h["offset"], h["size"] = offs, sizes
+    h["offset"][7] = len(img)  # out of the image
+    d_img = torch.from_numpy(img).cuda()
+    out = torch.full((len(sizes),), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+    T.crc_device(d_img, T.handles_to_device(h), out=out)
+    got = out.cpu().numpy().view(np.uint32)
+    keep = np.arange(len(sizes)) != 7
+    assert (got[keep] == exp[keep]).all() and got[7] == 0x5A5A5A5A
+    assert (d_img.cpu().numpy() == img).all()  # nothing written into the image
