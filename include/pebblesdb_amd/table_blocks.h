@@ -89,6 +89,112 @@ inline int64_t VerifyBlocks(const char* image, uint64_t image_len, const BlockHa
 
 inline const char* ChecksumMismatchMessage() { return "block checksum mismatch"; }  // format.cc:101
 
+// ---- table walker: the leveldb-verify / paranoid-scan batch -----------------------------------
+// Footer -> index block -> every data block's handle, metaindex block -> the meta blocks (filter),
+// then ONE pdb_sst_verify_host call over all of them (table/table.cc:70-170 Table::Open/ReadMeta
+// read the same handles one ReadBlock at a time; leveldb-verify.cc:142-164 walks every block).
+static const uint64_t kTableMagicNumber = 0xdb4775248b80fb57ull;          // table/format.h:84
+static const size_t kMaxEncodedHandleLength = 10 + 10;                     // table/format.h:41
+static const size_t kFooterEncodedLength = 2 * kMaxEncodedHandleLength + 8;  // table/format.h:71
+
+inline bool GetVarint64(const char** p, const char* limit, uint64_t* v) {  // util/coding.cc
+  uint64_t r = 0;
+  for (uint32_t shift = 0; shift <= 63 && *p < limit; shift += 7) {
+    const uint64_t b = static_cast<unsigned char>(*(*p)++);
+    r |= (b & 0x7f) << shift;
+    if (!(b & 0x80)) {
+      *v = r;
+      return true;
+    }
+  }
+  return false;
+}
+
+inline bool DecodeHandle(const char** p, const char* limit, BlockHandle* h) {  // format.cc:23-30
+  return GetVarint64(p, limit, &h->offset) && GetVarint64(p, limit, &h->size);
+}
+
+struct TableLayout {
+  BlockHandle metaindex, index;
+  std::vector<BlockHandle> data;  // every data block, in file order
+  std::vector<BlockHandle> meta;  // metaindex values (e.g. the filter block)
+  // data blocks, meta blocks, then the metaindex and index blocks themselves
+  std::vector<BlockHandle> All() const {
+    std::vector<BlockHandle> v(data);
+    v.insert(v.end(), meta.begin(), meta.end());
+    v.push_back(metaindex);
+    v.push_back(index);
+    return v;
+  }
+};
+
+// Values of a block's entries (table/block_builder.cc layout: [shared][non_shared][value_len]
+// varint32s, key delta, value; then uint32 restarts[num_restarts], uint32 num_restarts).
+inline bool BlockValues(const char* b, uint64_t n, std::vector<BlockHandle>* handles, std::string* err) {
+  if (n < 4) return *err = "bad block contents", false;
+  uint32_t nr;
+  memcpy(&nr, b + n - 4, 4);  // little-endian hosts (the reference's port assumption)
+  if (4ull * (nr + 1ull) > n) return *err = "bad block contents", false;
+  const char* p = b;
+  const char* limit = b + n - 4ull * (nr + 1ull);
+  uint64_t key_len = 0;
+  while (p < limit) {
+    uint64_t shared, non_shared, vlen;
+    if (!GetVarint64(&p, limit, &shared) || !GetVarint64(&p, limit, &non_shared) ||
+        !GetVarint64(&p, limit, &vlen) || shared > key_len || non_shared > static_cast<uint64_t>(limit - p) ||
+        vlen > static_cast<uint64_t>(limit - p) - non_shared)
+      return *err = "bad entry in block", false;
+    key_len = shared + non_shared;
+    p += non_shared;
+    const char* v = p;
+    BlockHandle h;
+    if (!DecodeHandle(&v, p + vlen, &h)) return *err = "bad block handle", false;
+    handles->push_back(h);
+    p += vlen;
+  }
+  return true;
+}
+
+// Parses the footer, index and metaindex blocks of a table image (uncompressed blocks: the
+// reference's CMake build never links Snappy, port_posix.h:141-156).  False + *err on corruption.
+inline bool ReadTableLayout(const char* image, uint64_t len, TableLayout* t, std::string* err) {
+  if (len < kFooterEncodedLength) return *err = "file is too short to be an sstable", false;
+  const char* f = image + len - kFooterEncodedLength;
+  uint32_t lo, hi;
+  memcpy(&lo, f + kFooterEncodedLength - 8, 4);
+  memcpy(&hi, f + kFooterEncodedLength - 4, 4);
+  if (((static_cast<uint64_t>(hi) << 32) | lo) != kTableMagicNumber)
+    return *err = "not an sstable (bad magic number)", false;
+  const char* p = f;
+  if (!DecodeHandle(&p, f + 2 * kMaxEncodedHandleLength, &t->metaindex) ||
+      !DecodeHandle(&p, f + 2 * kMaxEncodedHandleLength, &t->index))
+    return *err = "bad block handle", false;
+  const BlockHandle* blocks[2] = {&t->index, &t->metaindex};
+  std::vector<BlockHandle>* outs[2] = {&t->data, &t->meta};
+  for (int k = 0; k < 2; ++k) {
+    const BlockHandle& h = *blocks[k];
+    if (h.offset > len || h.size > len - h.offset || len - h.offset - h.size < kBlockTrailerSize)
+      return *err = "truncated block read", false;  // format.cc:84-87
+    if (image[h.offset + h.size] != 0) return *err = "compressed index/metaindex block", false;
+    if (!BlockValues(image + h.offset, h.size, outs[k], err)) return false;
+  }
+  return true;
+}
+
+// leveldb-verify for one table image: every block's checksum in one GPU batch.  Returns the
+// number of bad blocks (>= 0), a negative PDB_E* code, or -1000 with *err set when the table's
+// structure (footer / index / metaindex) is corrupt.
+inline int64_t VerifyTable(const char* image, uint64_t len, TableLayout* layout, std::vector<uint8_t>* ok,
+                           std::string* err) {
+  TableLayout local;
+  TableLayout& t = layout ? *layout : local;
+  t = TableLayout();
+  std::string e;
+  if (!ReadTableLayout(image, len, &t, err ? err : &e)) return -1000;
+  const std::vector<BlockHandle> all = t.All();
+  return VerifyBlocks(image, len, all.data(), all.size(), ok);
+}
+
 }  // namespace pdb
 
 #endif  // PEBBLESDB_AMD_TABLE_BLOCKS_H_

@@ -28,6 +28,7 @@ def test_cpp_consumer_builds_and_links():
 @pytest.mark.gpu
 def test_cpp_consumer_runs_on_gpu():
     exe = _compile()
-    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    r = subprocess.run([exe, os.path.join(ROOT, "tests", "golden", "sst")], capture_output=True, text=True,
+                       timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "PASS" in r.stdout
