@@ -1391,10 +1391,11 @@ constexpr uint32_t kSlowList = 64u;
 template <class Src, class Sink, bool kNT, int kRows, bool kDiagNoFold = false, int kBlk = 4>
 __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ tabs, Src src, uint64_t nblk,
                                                   Sink sink) {
-  static_assert(kRows == 1 || kRows == 4, "bodies of 1 or 4 KiB");
+  static_assert(kRows == 0 || kRows == 1 || kRows == 4, "no body (records <= 256 B), 1-KiB or 4-KiB bodies");
   static_assert(kBlk == 4 || (kBlk == 8 && kRows == 1), "4-block groups, or 8 with 1-KiB bodies");
   constexpr uint32_t kRowLanes = 64u / kBlk, kRowShift = kBlk == 4 ? 4u : 3u;
-  constexpr uint32_t kBody = 1024u * kRows, kMin = kBody, kMax = kBody + 16u * kRowLanes;
+  // kRows = 0: the whole block is a "prefix" (1..16 kRowLanes bytes), hashed by its row alone
+  constexpr uint32_t kBody = 1024u * kRows, kMin = kRows ? kBody : 1u, kMax = kBody + 16u * kRowLanes;
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
   char* lds = reinterpret_cast<char*>(lds_words);
   stage_tables<PDB_CAT_TREE16, PDB_CAT_S1024>(lds, tabs);  // slots 0..5 = 16..512, 6 = 1024
@@ -1476,12 +1477,12 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
     const uint32_t pref = row_suffix_tree(lds, u, hash_masked(lds, lt, pf, masked_start(pf, ureg)), L);
 #pragma unroll
     for (int r = 0; r < kBlk; ++r)
-      P[r] = G.n[r] == kMin ? 0xFFFFFFFFu : __builtin_amdgcn_readlane(pref, kRowLanes * r + kRowLanes - 1);
+      P[r] = (kRows && G.n[r] == kMin) ? 0xFFFFFFFFu : __builtin_amdgcn_readlane(pref, kRowLanes * r + kRowLanes - 1);
   };
   // one body's lane partial: chains j (16-B pieces at bs + 16u + 1024j) with the DPP neighbour
   // dword, Horner-folded with shift 1024, P injected as lane 0's start
   auto body_partial = [&](const u32x4* e, uint32_t cl, uint32_t s, uint32_t P) -> uint32_t {
-    uint32_t nx[kRows];
+    uint32_t nx[kRows ? kRows : 1];  // (kRows = 0 has no body: never called)
 #pragma unroll
     for (int j = 0; j < kRows; ++j) nx[j] = 0;
     if (s) {  // neighbour dwords: lane u + 1's first dword; lane 63 the next chain's lane 0
@@ -1573,6 +1574,41 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
         pre = npre;
         pf = npf;
         if (nslow > kSlowList - kBlk) break;  // no room for another group's slow blocks: drain first
+      }
+    } else if constexpr (kRows == 0) {
+      // records <= 256 B: no body, no tree -- a row's suffix tree leaves the block's raw state in
+      // the row's last lane.  The next group's descriptors and prefix loads are in flight while
+      // one group hashes.
+      for (;;) {
+        const MaskedPiece cpf = pf;
+        const Grp NG = finish(nraw);
+        issue_prefix(pf, NG);
+        const uint32_t npre = SinkOps<Sink>::pre(sink, lane_idx(ngrp), NG.ld);
+        uint64_t nngrp = ngrp;
+        if (ngrp < g_hi) nngrp = next_group();
+        nraw = load_desc(nngrp < g_hi ? nngrp : ngrp);
+        uint32_t emax = 0;
+#pragma unroll
+        for (int r = 0; r < kBlk; ++r) {
+          const uint32_t e = fast(G.n[r]) ? (G.n[r] + 15u) >> 4 : 0u;
+          emax = e > emax ? e : emax;
+        }
+        const uint32_t L = emax <= 1 ? 0u : (emax <= 2 ? 1u : (emax <= 4 ? 2u : (emax <= 8 ? 3u : 4u)));
+        const uint32_t pref = row_suffix_tree(lds, u, hash_masked(lds, lt, cpf, masked_start(cpf, ureg)), L);
+        const uint32_t v = __shfl(pref, (u & (kBlk - 1u)) * kRowLanes + kRowLanes - 1u, 64);  // lane r: block r
+        const uint32_t nv = static_cast<uint32_t>(g_hi - grp < kBlk ? g_hi - grp : kBlk);
+        const uint32_t fastbits = fast_bits(G);
+        if (u < nv && ((fastbits >> u) & 1u)) SinkOps<Sink>::put(sink, grp + u, v, G.ld, pre);
+        defer(G, fastbits, nv);
+        if (ngrp >= g_hi) {
+          done = true;
+          break;
+        }
+        grp = ngrp;
+        ngrp = nngrp;
+        G = NG;
+        pre = npre;
+        if (nslow > kSlowList - kBlk) break;  // drain first (pf already holds grp's prefixes)
       }
     } else if constexpr (kBlk == 4) {
       // 1-KiB bodies: the next group's 4 bodies, prefixes and descriptors issued at the top of a
@@ -1725,6 +1761,12 @@ template <class Src, class Sink, bool kNT>
 __global__ __launch_bounds__(kThreads) void crc_sst4k_nofold_kernel(const uint32_t* __restrict__ tabs, Src src,
                                                                     uint64_t nblk, Sink sink) {
   sized_kernel_body<Src, Sink, kNT, 4, true>(tabs, src, nblk, sink);
+}
+
+template <class Src, class Sink, bool kNT>
+__global__ __launch_bounds__(kThreads) void crc_rec256_kernel(const uint32_t* __restrict__ tabs, Src src,
+                                                              uint64_t nblk, Sink sink) {
+  sized_kernel_body<Src, Sink, kNT, 0, false, 4>(tabs, src, nblk, sink);
 }
 
 template <class Src, class Sink, bool kNT, int kBlk = 8>

@@ -186,8 +186,18 @@ hipError_t launch_desc(const LaunchGeom& g, const uint32_t* d_tables, const uint
   const DescSrc src{base, blk, flags};
   // size-class hints (Value() seeds only): the sized kernels (exact 1-/4-KiB body + batched
   // prefix; other lengths take their slow path in the same launch)
-  if (!(flags & PDB_CRC_USE_INIT) && (flags & (PDB_CRC_SIZE_1K | PDB_CRC_SIZE_4K)) && g_fast_variant != 40) {
+  if (!(flags & PDB_CRC_USE_INIT) && (flags & (PDB_CRC_SIZE_1K | PDB_CRC_SIZE_4K | PDB_CRC_SIZE_256)) &&
+      g_fast_variant != 40) {
     const bool k1 = flags & PDB_CRC_SIZE_1K;
+    if (!k1 && !(flags & PDB_CRC_SIZE_4K)) {  // records <= 256 B: rows of 16 lanes, no body
+      if (mode == kModeOut)
+        hipLaunchKernelGGL((crc_rec256_kernel<DescSrc, OutSink, true>), grid, block, 0, s, d_tables, src, nblk,
+                           OutSink{out, flags});
+      else
+        hipLaunchKernelGGL((crc_rec256_kernel<DescSrc, VerifySink, true>), grid, block, 0, s, d_tables, src, nblk,
+                           VerifySink{expected, ok, nbad, flags});
+      return hipGetLastError();
+    }
 #define PDB_SIZED(K, SINK, ...)                                                                                   \
   hipLaunchKernelGGL((K<DescSrc, SINK, true>), grid, block, 0, s, d_tables, src, nblk, SINK{__VA_ARGS__})
 #define PDB_SIZED1K4(SINK, ...)                                                                                  \

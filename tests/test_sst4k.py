@@ -214,9 +214,9 @@ def _desc_case(crc, sizes, seed, gap_max=7):
     return base, crc.make_blocks(offs, sizes)
 
 
-@pytest.mark.parametrize("hint", ["1k", "4k"])
+@pytest.mark.parametrize("hint", ["1k", "4k", "256"])
 def test_size_hint_edge_lengths(crc, oracle_lib, hint):
-    """Both sized kernels on every fast-range boundary of both classes and slow lengths either
+    """The sized kernels on every fast-range boundary of every class and slow lengths either
     side, each repeated at 8 alignments, masked and unmasked, batch and verify."""
     sizes = [n for n in EDGE_1K + EDGE_N for _ in range(8)]
     base, blk = _desc_case(crc, sizes, 51)
@@ -259,7 +259,7 @@ def test_size_hint_ignored_with_extend_seed(crc, oracle_lib):
     assert (got.cpu().numpy().view(np.uint32) == oracle_lib.batch(base, blk, flags=2, nthreads=8)).all()
 
 
-@pytest.mark.parametrize("lo,hi", [(1024, 1153), (4096, 4353), (900, 1400)])
+@pytest.mark.parametrize("lo,hi", [(1024, 1153), (4096, 4353), (1, 257), (900, 1400)])
 def test_host_batch_picks_size_class(crc, oracle_lib, lo, hi):
     """pdb_crc32c_batch_host / verify_host choose the sized kernel from the host-visible lengths."""
     rng = np.random.Generator(np.random.PCG64(lo))
@@ -279,7 +279,7 @@ def test_sized_kernels_match_generic_kernel(crc):
 
     rng = np.random.Generator(np.random.PCG64(81))
     sizes = np.concatenate([rng.integers(1024, 1281, size=4000), rng.integers(4096, 4353, size=4000),
-                            rng.integers(0, 20000, size=2000)])
+                            rng.integers(0, 300, size=4000), rng.integers(0, 20000, size=2000)])
     rng.shuffle(sizes)
     base, blk = _desc_case(crc, sizes, 82)
     d_base, d_blk = torch.from_numpy(base).cuda(), crc.blocks_to_device(blk)
@@ -287,7 +287,7 @@ def test_sized_kernels_match_generic_kernel(crc):
     for v in (0, 40, 41):
         lib().pdb_diag_set_variant(v)
         try:
-            res.append([crc.batch(d_base, d_blk, size_hint=h).cpu().numpy() for h in ("1k", "4k")])
+            res.append([crc.batch(d_base, d_blk, size_hint=h).cpu().numpy() for h in ("1k", "4k", "256")])
         finally:
             lib().pdb_diag_set_variant(0)
     for other in res[1:]:

@@ -32,6 +32,8 @@ for _ in range(20):
 def layout(w):
     if w == "wal":
         return wal_layout(total, 1055)
+    if w == "wal100":  # db_bench's default --value_size=100: 131-B write batches (1 GiB of log)
+        return wal_layout(1 << 30, 131)
     rng = np.random.Generator(np.random.PCG64(5))
     if w == "sst":
         lens = rng.integers(4167, 4176, size=total // 4172)
@@ -45,7 +47,7 @@ def layout(w):
 
 
 res = {}
-HINT = {"wal": "1k", "sst": "4k"}
+HINT = {"wal": "1k", "sst": "4k", "small": "256", "wal100": "256"}
 for w in works:
     offs, lens = layout(w)
     blk = crc32c.blocks_to_device(crc32c.make_blocks(offs, lens))
