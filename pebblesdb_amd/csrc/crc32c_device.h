@@ -415,7 +415,7 @@ __device__ __forceinline__ uint32_t partial4k(const char* lds, const LaneTabs& l
 // kXcd: workgroups are dispatched to the 8 XCDs round-robin (blockIdx.x % 8); kXcd renumbers
 // them so each XCD's CUs own consecutive 64-KiB block windows (A/B diagnostics).
 template <int kSync, int kNP = 2, bool kNT = false, int kWaves = kWavesPerWg, bool kPair = false,
-          bool kXcd = false, int kQuad = 0>
+          bool kXcd = false, int kQuad = 0, bool kPrio = false>
 __global__ __launch_bounds__(kWaves * 64) void crc_pack4k_kernel(
     const uint32_t* __restrict__ tabs, const uint8_t* __restrict__ base, uint64_t stride,
     uint64_t nblk, uint32_t flags, uint32_t init, uint32_t* __restrict__ out) {
@@ -469,7 +469,9 @@ __global__ __launch_bounds__(kWaves * 64) void crc_pack4k_kernel(
         const uint64_t bk = g + r * nw;
         u32x4 cur[4] = {buf[0], buf[1], buf[2], buf[3]};
         const uint64_t bn = bk + nw;
+        if constexpr (kPrio) __builtin_amdgcn_s_setprio(2);  // A/B: issue the next block's loads first
         if (bn < nblk) load4k<kNP, kNT>(buf, base, stride, bn, u);  // wave-uniform
+        if constexpr (kPrio) __builtin_amdgcn_s_setprio(0);
         if constexpr (kQuad != 0) {
           static_assert(kNP == 4, "the quad transpose needs 4 x 16-B lane pieces");
           quad_transpose(cur, u);

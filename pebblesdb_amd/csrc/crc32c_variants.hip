@@ -577,6 +577,9 @@ hipError_t launch_fixed_variant(int v, const LaunchGeom& g, const uint32_t* d_ta
     // quad-transposed lanes: 64 contiguous bytes per lane, no per-lane Horner folds
     case 28: PDB_K((crc_pack4k_kernel<1, 4, true, 16, false, false, 1>)); break;
     case 29: PDB_K((crc_pack4k_kernel<1, 4, true, 16, false, false, 2>)); break;  // 2 chains + shift 32
+    // s_setprio 2 around the next block's load issue (free-running / lock-step)
+    case 30: PDB_K((crc_pack4k_kernel<1, 4, true, 16, false, false, 0, true>)); break;
+    case 31: PDB_K((crc_pack4k_kernel<0, 4, true, 16, false, false, 0, true>)); break;
     default: PDB_K((crc_pack4k_kernel<1, 4, true>)); break;
   }
 #undef PDB_FAST

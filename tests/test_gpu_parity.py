@@ -190,7 +190,7 @@ def test_all_fast_variants_bit_exact(crc, oracle_lib):
     exp = oracle_lib.batch(d.cpu().numpy(), crc.make_blocks(np.arange(nblk) * 4096, np.full(nblk, 4096)),
                            nthreads=8)
     try:
-        for v in range(30):
+        for v in range(32):
             lib().pdb_diag_set_variant(v)
             got = _u32(crc.batch_fixed(d, 4096, 4096, nblk))
             assert (got == exp).all(), f"variant {v}"
