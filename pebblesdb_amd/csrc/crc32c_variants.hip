@@ -396,6 +396,20 @@ struct NtSealSink {  // A/B variant 34: the trailer as non-temporal byte stores
 // before the trailer is written, so the write lands on a valid L2 line.
 struct SealTouchSink {};
 
+// A/B variant 37: the trailer word as ONE (possibly unaligned) dword store instead of 4 byte stores.
+struct SealDwordSink {};
+
+template <>
+struct SinkOps<SealDwordSink> {
+  __device__ static __forceinline__ uint32_t pre(const SealDwordSink&, uint64_t, const BlkDesc&) { return 0u; }
+  __device__ static __forceinline__ void put(const SealDwordSink&, uint64_t, uint32_t raw, const BlkDesc& d,
+                                             uint32_t) {
+    if (d.init_raw == 0) return;
+    typedef __attribute__((address_space(1))) uint32_t g_u32u __attribute__((aligned(1)));
+    *reinterpret_cast<g_u32u*>(reinterpret_cast<uintptr_t>(d.p) + d.n) = pdb_mask(~raw);
+  }
+};
+
 template <>
 struct SinkOps<SealTouchSink> {
   __device__ static __forceinline__ uint32_t pre(const SealTouchSink&, uint64_t, const BlkDesc& d) {
@@ -421,6 +435,11 @@ hipError_t launch_sst_variant(int v, const LaunchGeom& g, const uint32_t* d_tabl
   if (v == 97 && !seal) {  // WRONG CRCs by design: verify without the Horner folds (prices them)
     hipLaunchKernelGGL((crc_sst4k_nofold_kernel<SstSrc, SstVerifySink, true>), grid, block, 0, s, d_tables, src, n,
                        SstVerifySink{ok, nullptr});  // no nbad: every block "fails"; 1M atomics would dominate
+    return hipGetLastError();
+  }
+  if (v == 37 && seal) {  // one dword store per trailer
+    hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SealDwordSink, true>), grid, block, 0, s, d_tables, src, n,
+                       SealDwordSink{});
     return hipGetLastError();
   }
   if (v == 36 && seal) {  // trailer line read a group before the write
