@@ -1394,7 +1394,7 @@ template <class Src, class Sink, bool kNT, int kRows, bool kDiagNoFold = false, 
 __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ tabs, Src src, uint64_t nblk,
                                                   Sink sink) {
   static_assert(kRows == 0 || kRows == 1 || kRows == 4, "no body (records <= 256 B), 1-KiB or 4-KiB bodies");
-  static_assert(kBlk == 4 || (kBlk == 8 && kRows == 1), "4-block groups, or 8 with 1-KiB bodies");
+  static_assert(kBlk == 4 || (kBlk == 8 && kRows >= 1), "4-block groups, or 8 with 1- or 4-KiB bodies");
   constexpr uint32_t kRowLanes = 64u / kBlk, kRowShift = kBlk == 4 ? 4u : 3u;
   // kRows = 0: the whole block is a "prefix" (1..16 kRowLanes bytes), hashed by its row alone
   constexpr uint32_t kBody = 1024u * kRows, kMin = kRows ? kBody : 1u, kMax = kBody + 16u * kRowLanes;
@@ -1536,20 +1536,20 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
       uint32_t blast;
       issue_body(buf, blast, body_at(G, 0));
       for (;;) {
-        uint32_t P[4];
+        uint32_t P[kBlk];
         prefix_states(pf, G, P);
         Grp NG = G;
         uint32_t npre = pre;
         MaskedPiece npf = pf;
         uint64_t nngrp = ngrp;
-        uint32_t part[4];
-        const uint32_t nv = static_cast<uint32_t>(g_hi - grp < 4 ? g_hi - grp : 4);
+        uint32_t part[kBlk];
+        const uint32_t nv = static_cast<uint32_t>(g_hi - grp < kBlk ? g_hi - grp : kBlk);
         const uint32_t fastbits = fast_bits(G);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
+        for (int r = 0; r < kBlk; ++r) {
           const u32x4 e[4] = {buf[0], buf[1], buf[2], buf[3]};
           const uint32_t cl = blast;
-          if (r < 3) {
+          if (r < kBlk - 1) {
             issue_body(buf, blast, body_at(G, r + 1));
           } else {
             NG = finish(nraw);
@@ -1563,7 +1563,11 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
           if ((fastbits >> r) & 1u)
             part[r] = body_partial(e, cl, static_cast<uint32_t>((G.p[r] + G.n[r]) & 3u), P[r]);
         }
-        const uint32_t v = tree4_packed(lds, u, part[0], part[1], part[2], part[3]);
+        uint32_t v;
+        if constexpr (kBlk == 4)
+          v = tree4_packed(lds, u, part[0], part[1], part[2], part[3]);
+        else
+          v = tree8_packed(lds, u, part);
         if (u < nv && ((fastbits >> u) & 1u)) SinkOps<Sink>::put(sink, grp + u, v, G.ld, pre);
         defer(G, fastbits, nv);
         if (ngrp >= g_hi) {
@@ -1753,10 +1757,11 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
   }
 }
 
-template <class Src, class Sink, bool kNT>
+// kBlk = 8 (A/B): 8-block groups, prefixes <= 128 B in rows of 8 lanes, one tree8_packed.
+template <class Src, class Sink, bool kNT, int kBlk = 4>
 __global__ __launch_bounds__(kThreads) void crc_sst4k_kernel(const uint32_t* __restrict__ tabs, Src src,
                                                              uint64_t nblk, Sink sink) {
-  sized_kernel_body<Src, Sink, kNT, 4>(tabs, src, nblk, sink);
+  sized_kernel_body<Src, Sink, kNT, 4, false, kBlk>(tabs, src, nblk, sink);
 }
 
 template <class Src, class Sink, bool kNT>

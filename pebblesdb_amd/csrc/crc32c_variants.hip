@@ -437,6 +437,15 @@ hipError_t launch_sst_variant(int v, const LaunchGeom& g, const uint32_t* d_tabl
                        SstVerifySink{ok, nullptr});  // no nbad: every block "fails"; 1M atomics would dominate
     return hipGetLastError();
   }
+  if (v == 38) {  // 8-block groups (prefixes <= 128 B in rows of 8 lanes, tree8_packed)
+    if (seal)
+      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SealSink, true, 8>), grid, block, 0, s, d_tables, src, n,
+                         SealSink{});
+    else
+      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstVerifySink, true, 8>), grid, block, 0, s, d_tables, src, n,
+                         SstVerifySink{ok, nbad});
+    return hipGetLastError();
+  }
   if (v == 37 && seal) {  // one dword store per trailer
     hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SealDwordSink, true>), grid, block, 0, s, d_tables, src, n,
                        SealDwordSink{});

@@ -185,15 +185,17 @@ def test_new_path_matches_previous_kernel(crc):
     h["offset"], h["size"] = offs, sizes
     d_h = T.handles_to_device(h)
     outs = []
-    for v in (0, 30):
+    for v in (0, 30, 38):  # 38: the 8-block-group variant of the sized kernel
         lib().pdb_diag_set_variant(v)
         try:
             d = torch.from_numpy(img).cuda()
             T.seal_device(d, d_h)
             outs.append(d.cpu().numpy())
+            ok, nbad = T.verify_device(d, d_h)
+            assert int(nbad.item()) == 0, v
         finally:
             lib().pdb_diag_set_variant(0)
-    assert (outs[0] == outs[1]).all()
+    assert (outs[0] == outs[1]).all() and (outs[0] == outs[2]).all()
 
 
 # ---- descriptor batches with a size-class hint: crc_sst1k_kernel / crc_sst4k_kernel<DescSrc> ----
