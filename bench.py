@@ -298,7 +298,9 @@ def main():
     if rank == 0:
         if args.diag:
             extra["diag"] = diag(crc32c, torch, dev, data, stream)
-        if not args.no_copy_inclusive and args.workload in ("c2", "sstable"):
+        # the copy-inclusive rate is a one-GPU figure (like the CPU baseline): multi-rank runs skip it,
+        # so no rank sits in the process-group teardown while rank 0 copies for seconds
+        if not args.no_copy_inclusive and world == 1 and args.workload in ("c2", "sstable"):
             extra["copy_inclusive"] = copy_inclusive(crc32c, data, L, stride, min(nblk, 1 << 18))
         cpu = None
         if not args.no_cpu_baseline and world == 1:
