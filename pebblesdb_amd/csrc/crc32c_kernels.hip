@@ -163,6 +163,17 @@ hipError_t launch_fixed(const LaunchGeom& g, const uint32_t* d_tables, const uin
                          OutSink{out, flags});
       return hipGetLastError();
     }
+    if (src.init_raw == 0xFFFFFFFFu && (len - 1024u <= 128u || len - 1u <= 255u)) {
+      // the same size classes as the descriptor hints: 1-KiB records (1024..1152 B) and records
+      // of 1..256 B (tests/test_sst4k.py: fixed strides at every alignment)
+      if (len >= 1024u)
+        hipLaunchKernelGGL((crc_sst1k_kernel<FixedSrc, OutSink, true>), grid, block, 0, s, d_tables, src, nblk,
+                           OutSink{out, flags});
+      else
+        hipLaunchKernelGGL((crc_rec256_kernel<FixedSrc, OutSink, true>), grid, block, 0, s, d_tables, src, nblk,
+                           OutSink{out, flags});
+      return hipGetLastError();
+    }
     const bool aligned4 = ((reinterpret_cast<uintptr_t>(base) + (len & 15u)) & 3u) == 0 && (stride & 3u) == 0;
     if (aligned4)
       hipLaunchKernelGGL((crc_stream16_kernel<FixedSrc, OutSink, true, true, true>), grid, block, 0, s, d_tables,

@@ -362,3 +362,24 @@ def test_sst_crc_device_matches_seal(crc, oracle_lib):
     keep = np.arange(len(sizes)) != 7
     assert (got[keep] == exp[keep]).all() and got[7] == 0x5A5A5A5A
     assert (d_img.cpu().numpy() == img).all()  # nothing written into the image
+
+
+@pytest.mark.parametrize("length", [1, 2, 3, 15, 16, 17, 100, 131, 255, 256, 1024, 1025, 1056, 1151, 1152])
+def test_fixed_stride_small_classes(crc, oracle_lib, length):
+    """pdb_crc32c_batch_device_fixed with len in the 1..256 and 1024..1152 classes (the record
+    kernels) at every alignment and two strides; with an Extend seed the generic kernels."""
+    nblk = 2000
+    for shift in range(4):
+        for stride in (length, length + 5):
+            total = shift + (nblk - 1) * stride + length
+            d = torch.empty(total + 16, dtype=torch.uint8, device="cuda")
+            crc.fill_splitmix(d, 7 * length + stride + shift)
+            view = d[shift : shift + total]
+            host = view.cpu().numpy()
+            for masked, init in ((False, None), (True, None), (False, 0x0BADF00D)):
+                got = crc.batch_fixed(view, stride, length, nblk, masked=masked, init=init).cpu().numpy().view(np.uint32)
+                blk = crc.make_blocks(np.arange(nblk) * stride, np.full(nblk, length),
+                                      None if init is None else np.full(nblk, init))
+                exp = oracle_lib.batch(host, blk, flags=(1 if masked else 0) | (2 if init is not None else 0),
+                                       nthreads=8)
+                assert (got == exp).all(), (shift, stride, masked, init)
