@@ -1782,6 +1782,228 @@ __global__ __launch_bounds__(kThreads) void crc_sst1k_kernel(const uint32_t* __r
   sized_kernel_body<Src, Sink, kNT, 1, false, kBlk>(tabs, src, nblk, sink);
 }
 
+// ---- records of 1..256 B, one lane per record -------------------------------------------------
+// A wave takes 64 consecutive records (lane u: record 64b + u, so descriptors and results are
+// coalesced) and every lane hashes its own record as ONE slice-by-4 chain through the replicated,
+// conflict-free T0..T3: no row tree, no shift operators (a 132-B WAL record is 33 chain steps of
+// one lane, not 16 lanes' pieces plus a 4-level tree of single-copy operator lookups).
+// The record is END-aligned on a grid of G 32-B groups (G = ceil((n + 4) / 32), the wave's max):
+// word i = bytes [e + 4 - 32G + 4i, +4), i = 0 .. 8G - 2, built by one v_perm (the lane's byte
+// shift) from the dwords D[k] at A1 + 4 - 32G + 4k, A1 = the record's last aligned dword.  Bytes
+// before p are zeroed -- the chain starts at 0, so leading zeros are free -- and the word holding p
+// injects U[z] (z zeroed bytes), so the state entering the record is Value()'s 0xFFFFFFFF.
+// Loads are 16-B chunks, 4-B aligned: a chunk wholly below the record's first aligned dword reads
+// a dummy (all its bytes are masked), one straddling it reads up to 12 B before it -- so records
+// less than 16 B after the base take the slow path, with n == 0 and n > 256: those lanes are
+// hashed after the batch, one record per pass of the whole wave (slow_finish).  Value() seeds only
+// (the launchers route Extend seeds elsewhere).
+template <class Src, class Sink, bool kNT>
+__global__ __launch_bounds__(kThreads) void crc_lanerec_kernel(const uint32_t* __restrict__ tabs, Src src,
+                                                               uint64_t nblk, Sink sink) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
+  char* lds = reinterpret_cast<char*>(lds_words);
+  stage_tables<PDB_CAT_TREE16, PDB_CAT_S1024>(lds, tabs);  // slow path: slots 0..5 = 16..512, 6 = 1024
+  const uint32_t u = threadIdx.x & 63u;
+  const uint32_t ureg = tabs[PDB_UNSHIFT_OFF + (u & 15u)];
+  __syncthreads();
+  const LaneTabs lt = lane_tabs(u);
+  const uintptr_t dummy = reinterpret_cast<uintptr_t>(tabs);  // >= 4 KiB + 256 B of valid bytes
+  const uintptr_t lo_ok = reinterpret_cast<uintptr_t>(src.base) + 16u;
+  const uint64_t nbat = (nblk + 63u) >> 6;
+  const uint64_t W = static_cast<uint64_t>(gridDim.x) * kWavesPerWg;
+  uint64_t b = wave_id_uniform();
+  if (b >= nbat) return;
+  auto idx = [&](uint64_t bb) -> uint64_t {
+    const uint64_t i = (bb << 6) + u;
+    return i < nblk ? i : nblk - 1;
+  };
+  typename Src::Raw raw = src.load(idx(b));
+  for (;;) {
+    const uint64_t i = (b << 6) + u, bn = b + W;
+    keep_alive(raw);
+    const BlkDesc d = src.lane(raw);
+    raw = src.load(idx(bn < nbat ? bn : b));  // next batch's descriptors (unconditional)
+    const bool valid = i < nblk;
+    const uint32_t pre = SinkOps<Sink>::pre(sink, idx(b), d);
+    const uintptr_t p0 = reinterpret_cast<uintptr_t>(d.p);
+    const bool fast = (d.n - 1u) <= 255u && d.init_raw == 0xFFFFFFFFu && p0 >= lo_ok;
+    const uintptr_t p = fast ? p0 : dummy + 16u;
+    const uint32_t n = fast ? d.n : 1u;
+    const uintptr_t e = p + n;
+    const uintptr_t A1 = (e - 1u) & ~static_cast<uintptr_t>(3);
+    const uintptr_t A0 = p & ~static_cast<uintptr_t>(3);
+    const uint32_t sel = static_cast<uint32_t>(e - A1) * 0x01010101u + 0x03020100u;  // bytes sb..sb+3
+    uint32_t G = (n + 35u) >> 5;
+#pragma unroll
+    for (int k = 1; k < 64; k <<= 1) {
+      const uint32_t o = __shfl_xor(G, k, 64);
+      G = o > G ? o : G;
+    }
+    G = __builtin_amdgcn_readfirstlane(G);
+    const uintptr_t d0 = A1 + 4u - 32u * static_cast<uintptr_t>(G);
+    // dz = p - (start of the word): word W_{8t-1} (first of iteration t) has 32G - n - 32t
+    int32_t dz = static_cast<int32_t>(32u * G - n);
+    const uint32_t uz = __shfl(ureg, static_cast<uint32_t>(dz) & 3u, 64);
+    auto issue = [&](u32x4 (&g)[2], uint32_t t) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uintptr_t a = d0 + 32u * t + 16u * h;
+        g[h] = gload128<kNT>(a + 12u < A0 ? dummy : a);
+      }
+    };
+    u32x4 nx[2];
+    issue(nx, 0);
+    uint32_t c = 0, carry = 0;
+    for (uint32_t t = 0; t < G; ++t) {
+      const u32x4 g0 = nx[0], g1 = nx[1];
+      issue(nx, t + 1 < G ? t + 1 : t);  // the last group re-reads itself (unconditional)
+      const uint32_t D[9] = {carry, g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+      carry = g1.w;
+      if (__builtin_amdgcn_ballot_w64(dz >= 0) == 0) {  // the whole group inside every record
+#pragma unroll
+        for (int k = 0; k < 8; ++k) c = step4(lds, lt, c, __builtin_amdgcn_perm(D[k + 1], D[k], sel));
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int32_t z = dz - 4 * k;
+          const uint32_t w = __builtin_amdgcn_perm(D[k + 1], D[k], sel);
+          const uint32_t m = z <= 0 ? 0xFFFFFFFFu : (z >= 4 ? 0u : (0xFFFFFFFFu << (8u * static_cast<uint32_t>(z))));
+          const uint32_t inj = static_cast<uint32_t>(z) < 4u ? uz : 0u;
+          c = step4(lds, lt, c ^ inj, w & m);
+        }
+      }
+      dz -= 32;
+    }
+    if (valid && fast) SinkOps<Sink>::put(sink, i, c, d, pre);
+    // the batch's records outside the fast range, one per pass of the whole wave
+    uint64_t slow = __builtin_amdgcn_ballot_w64(valid && !fast);
+    const uint32_t plo = static_cast<uint32_t>(p0), phi = static_cast<uint32_t>(static_cast<uint64_t>(p0) >> 32);
+    while (slow) {
+      const uint32_t k = static_cast<uint32_t>(__builtin_ctzll(slow));
+      slow &= slow - 1;
+      const uintptr_t sp = static_cast<uintptr_t>(uniform64(__builtin_amdgcn_readlane(plo, k), __builtin_amdgcn_readlane(phi, k)));
+      const uint32_t sn = __builtin_amdgcn_readlane(d.n, k);
+      SlowFirst sf;
+      slow_issue(sf, sp, sn, u, dummy);
+      const uint32_t rs = slow_finish(lds, lt, u, ureg, sf, sp, sn);
+      const BlkDesc sd{reinterpret_cast<const uint8_t*>(sp), sn, 0xFFFFFFFFu};
+      if (u == 0) SinkOps<Sink>::put(sink, (b << 6) + k, rs, sd, __builtin_amdgcn_readlane(pre, k));
+    }
+    if (bn >= nbat) break;
+    b = bn;
+  }
+}
+
+// The same lane-per-record geometry on a FIXED window of 9 groups (288 B, every record of 1..256
+// B fits), with the whole window's loads issued up front (a chunk wholly below the record reads
+// the dummy: the same line for every such lane) so a wave pays one memory latency per batch of
+// 64 records instead of one per 32-B group, and the window hashed as two chains for ILP: groups
+// 0..4 (A) and 5..8 (B, the last 128 B), folded as shift128(A) ^ B (slot 3 = shift 128).
+// Groups wholly below every lane's record are skipped (wave-uniform).
+template <class Src, class Sink>
+__global__ __launch_bounds__(kThreads) void crc_lanerec9_kernel(const uint32_t* __restrict__ tabs, Src src,
+                                                                uint64_t nblk, Sink sink) {
+  constexpr uint32_t NG = 9, NA = 5;
+  __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
+  char* lds = reinterpret_cast<char*>(lds_words);
+  stage_tables<PDB_CAT_TREE16, PDB_CAT_S1024>(lds, tabs);  // slots 0..5 = 16..512 (3 = 128), 6 = 1024
+  const uint32_t u = threadIdx.x & 63u;
+  const uint32_t ureg = tabs[PDB_UNSHIFT_OFF + (u & 15u)];
+  __syncthreads();
+  const LaneTabs lt = lane_tabs(u);
+  const uintptr_t dummy = reinterpret_cast<uintptr_t>(tabs);  // >= 4 KiB + 256 B of valid bytes
+  const uintptr_t lo_ok = reinterpret_cast<uintptr_t>(src.base) + 16u;
+  const uint64_t nbat = (nblk + 63u) >> 6;
+  const uint64_t W = static_cast<uint64_t>(gridDim.x) * kWavesPerWg;
+  uint64_t b = wave_id_uniform();
+  if (b >= nbat) return;
+  auto idx = [&](uint64_t bb) -> uint64_t {
+    const uint64_t i = (bb << 6) + u;
+    return i < nblk ? i : nblk - 1;
+  };
+  typename Src::Raw raw = src.load(idx(b));
+  for (;;) {
+    const uint64_t i = (b << 6) + u, bn = b + W;
+    keep_alive(raw);
+    const BlkDesc d = src.lane(raw);
+    const uintptr_t p0 = reinterpret_cast<uintptr_t>(d.p);
+    const bool fast = (d.n - 1u) <= 255u && d.init_raw == 0xFFFFFFFFu && p0 >= lo_ok;
+    const uintptr_t p = fast ? p0 : dummy + 16u;
+    const uint32_t n = fast ? d.n : 1u;
+    const uintptr_t e = p + n;
+    const uintptr_t A1 = (e - 1u) & ~static_cast<uintptr_t>(3);
+    const uintptr_t A0 = p & ~static_cast<uintptr_t>(3);
+    const uintptr_t d0 = A1 + 4u - 32u * NG;
+    u32x4 C[2 * NG];
+    C[0] = u32x4{0, 0, 0, 0};  // dwords 0..3 lie wholly below every record of <= 256 B
+#pragma unroll
+    for (uint32_t h = 1; h < 2 * NG; ++h) {
+      const uintptr_t a = d0 + 16u * h;
+      C[h] = gload128<false>(a + 12u < A0 ? dummy : a);
+    }
+    raw = src.load(idx(bn < nbat ? bn : b));  // next batch's descriptors (unconditional)
+    const bool valid = i < nblk;
+    const uint32_t pre = SinkOps<Sink>::pre(sink, idx(b), d);
+    const uint32_t sel = static_cast<uint32_t>(e - A1) * 0x01010101u + 0x03020100u;  // bytes sb..sb+3
+    const int32_t dz0 = static_cast<int32_t>(32u * NG - n);  // p - start of word W_{-1}
+    const uint32_t uz = __shfl(ureg, static_cast<uint32_t>(dz0) & 3u, 64);
+    // first group holding a byte of some lane's record (wave-uniform): groups below are all zero
+    uint32_t t0 = static_cast<uint32_t>(dz0) >> 5;  // group t holds bytes iff dz0 - 32t < 32
+    t0 = fast ? (t0 < NG - 1 ? t0 : NG - 1) : NG - 1;
+#pragma unroll
+    for (int k = 1; k < 64; k <<= 1) {
+      const uint32_t o = __shfl_xor(t0, k, 64);
+      t0 = o < t0 ? o : t0;
+    }
+    t0 = __builtin_amdgcn_readfirstlane(t0);
+    auto dw = [&](int k) -> uint32_t {  // dword k of the window (k = -1: before it, always masked)
+      if (k < 0) return 0u;
+      const u32x4& q = C[k >> 2];
+      return (k & 3) == 0 ? q.x : ((k & 3) == 1 ? q.y : ((k & 3) == 2 ? q.z : q.w));
+    };
+    auto group = [&](uint32_t& c, int t) {
+      const int32_t dz = dz0 - 32 * t;
+      if (__builtin_amdgcn_ballot_w64(dz >= 0) == 0) {  // the whole group inside every record
+#pragma unroll
+        for (int k = 0; k < 8; ++k) c = step4(lds, lt, c, __builtin_amdgcn_perm(dw(8 * t + k), dw(8 * t + k - 1), sel));
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int32_t z = dz - 4 * k;
+          const uint32_t w = __builtin_amdgcn_perm(dw(8 * t + k), dw(8 * t + k - 1), sel);
+          const uint32_t m = z <= 0 ? 0xFFFFFFFFu : (z >= 4 ? 0u : (0xFFFFFFFFu << (8u * static_cast<uint32_t>(z))));
+          const uint32_t inj = static_cast<uint32_t>(z) < 4u ? uz : 0u;
+          c = step4(lds, lt, c ^ inj, w & m);
+        }
+      }
+    };
+    uint32_t ca = 0, cb = 0;
+#pragma unroll
+    for (int t = 0; t < static_cast<int>(NA); ++t) {
+      if (static_cast<uint32_t>(t) >= t0) group(ca, t);
+      if (t + NA < NG && static_cast<uint32_t>(t) + NA >= t0) group(cb, t + NA);
+    }
+    const uint32_t c = t0 < NA ? shift_op_x(lds, 3, ca, cb) : cb;
+    if (valid && fast) SinkOps<Sink>::put(sink, i, c, d, pre);
+    // the batch's records outside the fast range, one per pass of the whole wave
+    uint64_t slow = __builtin_amdgcn_ballot_w64(valid && !fast);
+    const uint32_t plo = static_cast<uint32_t>(p0), phi = static_cast<uint32_t>(static_cast<uint64_t>(p0) >> 32);
+    while (slow) {
+      const uint32_t k = static_cast<uint32_t>(__builtin_ctzll(slow));
+      slow &= slow - 1;
+      const uintptr_t sp = static_cast<uintptr_t>(uniform64(__builtin_amdgcn_readlane(plo, k), __builtin_amdgcn_readlane(phi, k)));
+      const uint32_t sn = __builtin_amdgcn_readlane(d.n, k);
+      SlowFirst sf;
+      slow_issue(sf, sp, sn, u, dummy);
+      const uint32_t rs = slow_finish(lds, lt, u, ureg, sf, sp, sn);
+      const BlkDesc sd{reinterpret_cast<const uint8_t*>(sp), sn, 0xFFFFFFFFu};
+      if (u == 0) SinkOps<Sink>::put(sink, (b << 6) + k, rs, sd, __builtin_amdgcn_readlane(pre, k));
+    }
+    if (bn >= nbat) break;
+    b = bn;
+  }
+}
+
 uint32_t grid_for(const LaunchGeom& g, uint64_t nblk) {
   const uint64_t want = (nblk + kWavesPerWg - 1) / kWavesPerWg;
   return static_cast<uint32_t>(want < g.grid ? (want ? want : 1) : g.grid);

@@ -169,9 +169,9 @@ hipError_t launch_fixed(const LaunchGeom& g, const uint32_t* d_tables, const uin
       if (len >= 1024u)
         hipLaunchKernelGGL((crc_sst1k_kernel<FixedSrc, OutSink, true>), grid, block, 0, s, d_tables, src, nblk,
                            OutSink{out, flags});
-      else
-        hipLaunchKernelGGL((crc_rec256_kernel<FixedSrc, OutSink, true>), grid, block, 0, s, d_tables, src, nblk,
-                           OutSink{out, flags});
+      else  // one lane per record (profiles/r01_ab_lanerec.json)
+        hipLaunchKernelGGL((crc_lanerec9_kernel<FixedSrc, OutSink>), dim3(grid_for(g, (nblk + 63) / 64)), block, 0,
+                           s, d_tables, src, nblk, OutSink{out, flags});
       return hipGetLastError();
     }
     const bool aligned4 = ((reinterpret_cast<uintptr_t>(base) + (len & 15u)) & 3u) == 0 && (stride & 3u) == 0;
@@ -190,8 +190,29 @@ hipError_t launch_desc(const LaunchGeom& g, const uint32_t* d_tables, const uint
                        const uint32_t* expected, uint32_t* out, uint8_t* ok, uint32_t* nbad,
                        hipStream_t s) {
   if (nblk == 0) return hipSuccess;
-  // 40: ignore size hints; 41: the 1-KiB kernel with 4-block groups
-  if (mode == kModeOut && g_fast_variant != 0 && g_fast_variant != 40 && g_fast_variant != 41)
+  // 40: ignore size hints; 41: the 1-KiB kernel with 4-block groups; 50/51: one lane per record
+  // with 32-B groups loaded one ahead (nt / default loads), 52: the shipped fixed-window version,
+  // for any list; 53: the <= 256-B class on the previous crc_rec256_kernel
+  if (g_fast_variant >= 50 && g_fast_variant <= 52 && !(flags & PDB_CRC_USE_INIT)) {
+    const dim3 grid(grid_for(g, (nblk + 63) / 64)), block(kThreads);
+    const DescSrc src{base, blk, flags};
+    if (mode == kModeOut && g_fast_variant == 52)
+      hipLaunchKernelGGL((crc_lanerec9_kernel<DescSrc, OutSink>), grid, block, 0, s, d_tables, src, nblk,
+                         OutSink{out, flags});
+    else if (mode == kModeOut) {
+      if (g_fast_variant == 50)
+        hipLaunchKernelGGL((crc_lanerec_kernel<DescSrc, OutSink, true>), grid, block, 0, s, d_tables, src, nblk,
+                           OutSink{out, flags});
+      else
+        hipLaunchKernelGGL((crc_lanerec_kernel<DescSrc, OutSink, false>), grid, block, 0, s, d_tables, src, nblk,
+                           OutSink{out, flags});
+    } else {
+      hipLaunchKernelGGL((crc_lanerec9_kernel<DescSrc, VerifySink>), grid, block, 0, s, d_tables, src, nblk,
+                         VerifySink{expected, ok, nbad, flags});
+    }
+    return hipGetLastError();
+  }
+  if (mode == kModeOut && g_fast_variant != 0 && g_fast_variant != 40 && g_fast_variant != 41 && g_fast_variant != 53)
     return launch_desc_variant(g_fast_variant, g, d_tables, base, blk, nblk, flags, out, s);
   const dim3 grid(grid_for(g, nblk)), block(kThreads);
   const DescSrc src{base, blk, flags};
@@ -200,12 +221,20 @@ hipError_t launch_desc(const LaunchGeom& g, const uint32_t* d_tables, const uint
   if (!(flags & PDB_CRC_USE_INIT) && (flags & (PDB_CRC_SIZE_1K | PDB_CRC_SIZE_4K | PDB_CRC_SIZE_256)) &&
       g_fast_variant != 40) {
     const bool k1 = flags & PDB_CRC_SIZE_1K;
-    if (!k1 && !(flags & PDB_CRC_SIZE_4K)) {  // records <= 256 B: rows of 16 lanes, no body
-      if (mode == kModeOut)
+    if (!k1 && !(flags & PDB_CRC_SIZE_4K)) {
+      // records <= 256 B: one lane per record on a fixed 288-B window, all loads up front, two
+      // chains (wal100 1387 -> 3485 GB/s, 256-B records 2507 -> 3835 GB/s over the rows-of-16-lanes
+      // crc_rec256_kernel, A/B variant 53: profiles/r01_ab_lanerec.json); other lengths take the
+      // whole-wave slow path in the same launch
+      const dim3 lgrid(grid_for(g, (nblk + 63) / 64));
+      if (mode == kModeOut && g_fast_variant == 53)
         hipLaunchKernelGGL((crc_rec256_kernel<DescSrc, OutSink, true>), grid, block, 0, s, d_tables, src, nblk,
                            OutSink{out, flags});
+      else if (mode == kModeOut)
+        hipLaunchKernelGGL((crc_lanerec9_kernel<DescSrc, OutSink>), lgrid, block, 0, s, d_tables, src, nblk,
+                           OutSink{out, flags});
       else
-        hipLaunchKernelGGL((crc_rec256_kernel<DescSrc, VerifySink, true>), grid, block, 0, s, d_tables, src, nblk,
+        hipLaunchKernelGGL((crc_lanerec9_kernel<DescSrc, VerifySink>), lgrid, block, 0, s, d_tables, src, nblk,
                            VerifySink{expected, ok, nbad, flags});
       return hipGetLastError();
     }

@@ -276,7 +276,8 @@ def test_host_batch_picks_size_class(crc, oracle_lib, lo, hi):
 
 def test_sized_kernels_match_generic_kernel(crc):
     """Variant 40 ignores the hints (crc_stream16_kernel), 41 runs the 1-KiB kernel with 4-block
-    groups: identical CRCs on a mixed batch."""
+    groups, 50-52 the lane-per-record kernels on every list (larger blocks on their whole-wave slow
+    path), 53 the <= 256-B class on crc_rec256_kernel: identical CRCs on a mixed batch."""
     from pebblesdb_amd._native import lib
 
     rng = np.random.Generator(np.random.PCG64(81))
@@ -286,7 +287,7 @@ def test_sized_kernels_match_generic_kernel(crc):
     base, blk = _desc_case(crc, sizes, 82)
     d_base, d_blk = torch.from_numpy(base).cuda(), crc.blocks_to_device(blk)
     res = []
-    for v in (0, 40, 41):
+    for v in (0, 40, 41, 50, 51, 52, 53):
         lib().pdb_diag_set_variant(v)
         try:
             res.append([crc.batch(d_base, d_blk, size_hint=h).cpu().numpy() for h in ("1k", "4k", "256")])
@@ -383,3 +384,28 @@ def test_fixed_stride_small_classes(crc, oracle_lib, length):
                 exp = oracle_lib.batch(host, blk, flags=(1 if masked else 0) | (2 if init is not None else 0),
                                        nthreads=8)
                 assert (got == exp).all(), (shift, stride, masked, init)
+
+
+@pytest.mark.parametrize("seed", [91, 92])
+def test_lane_per_record_kernel(crc, oracle_lib, seed):
+    """crc_lanerec9_kernel (the <= 256-B class): 100 003 records of 1..256 B at any alignment,
+    back to back or with gaps (the first records within 16 B of the base and a sprinkling of 0- and
+    > 256-B ones take the whole-wave slow path inside the same launch), batch and verify, fixed
+    stride too."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    sizes = rng.integers(1, 257, size=100_003)
+    sizes[::997] = 0
+    sizes[5::1009] = rng.integers(257, 6000, size=len(sizes[5::1009]))
+    base, blk = _desc_case(crc, sizes, seed, gap_max=0 if seed == 91 else 9)
+    d_base, d_blk = torch.from_numpy(base).cuda(), crc.blocks_to_device(blk)
+    for masked in (False, True):
+        got = crc.batch(d_base, d_blk, masked=masked, size_hint="256").cpu().numpy().view(np.uint32)
+        exp = oracle_lib.batch(base, blk, flags=1 if masked else 0, nthreads=8)
+        bad = np.nonzero(got != exp)[0]
+        assert bad.size == 0, (masked, bad.size, int(blk["len"][bad[0]]), int(blk["off"][bad[0]]))
+    wrong = exp.copy()
+    flip = np.arange(3, len(exp), 7)
+    wrong[flip] ^= 0x100
+    ok, nbad = crc.verify(d_base, d_blk, torch.from_numpy(wrong.view(np.int32)).cuda(), size_hint="256")
+    okh = ok.cpu().numpy()
+    assert int(nbad.item()) == len(flip) and (okh == 0).sum() == len(flip) and (okh[flip] == 0).all()
