@@ -339,7 +339,7 @@ def main():
                 "kernel": {"c2": "crc_pack4k_kernel<1,4,nt>", "sstable": "crc_sst4k_kernel<FixedSrc,OutSink,nt>",
                            "c3": "crc_stream16_kernel<DescSrc,OutSink,dyn,nt,pack>",
                            "wal": "crc_sst1k_kernel<DescSrc,OutSink,nt>",
-                           "wal100": "crc_rec256_kernel<DescSrc,OutSink,nt>",
+                           "wal100": "crc_lanerec9_kernel<DescSrc,OutSink>",
                            "sst_verify": "crc_sst4k_kernel<SstSrc,SstVerifySink,nt>",
                            "sst_seal": "crc_sst4k_kernel<SstSrc,SealSink,nt>",
                            "sst_crc": "crc_sst4k_kernel<SstSrc,SstCrcSink,nt>"}[args.workload],
