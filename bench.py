@@ -39,7 +39,7 @@ def parse():
     # DESIGN.md §6), so the default warmup covers them
     ap.add_argument("--warmup", type=int, default=40)
     ap.add_argument("--workload", default="c2", choices=["c2", "c3", "sstable", "sst_verify", "sst_seal", "sst_crc",
-                                                        "wal", "wal100"],
+                                                        "wal", "wal100", "wal400"],
                     help="c2 (default, the headline) / c3: BASELINE configs; sstable: the C2 blocks in "
                          "sstable layout; sst_verify / sst_seal: SURVEY §8(f) rows 1-2 on a device sstable "
                          "image of ~4.17-KiB blocks; wal: row 3, the log record CRC over 32-KiB log blocks")
@@ -191,13 +191,16 @@ def main():
         workload = {"workload": f"{args.workload}: sstable image in HBM, 1M blocks of 4166-4174 B + type + "
                                 "5-B trailer, pdb_sst_" + args.workload.split("_")[1] + "_device",
                     "blocks_per_gpu": nblk, "bytes_per_gpu": hashed}
-    elif args.workload in ("wal", "wal100"):
+    elif args.workload in ("wal", "wal100", "wal400"):
         # log file image: 32-KiB log blocks of physical records [crc 4][len 2][type 1][payload]
         # (db/log_format.h:27-30); fillseq-like 1055-B logical records (1 KiB value + key + batch
         # header) fragmented at block ends; the CRC covers type || fragment (log_writer.cc:111-121)
         # wal100: db_bench's default --value_size=100 -> 131-B batches, a 1 GiB log, the <= 256-B class
+        # wal400: --value_size=400 -> 431-B batches, a 2 GiB log, the 257..512-B class
         small = args.workload == "wal100"
-        offs, lens = wal_layout(args.nblk * (1024 if small else 4096), 131 if small else 1055)
+        mid = args.workload == "wal400"
+        offs, lens = wal_layout(args.nblk * (1024 if small else (2048 if mid else 4096)),
+                                131 if small else (431 if mid else 1055))
         nblk = len(offs)
         total = int(offs[-1] + lens[-1])
         data = torch.empty(total, dtype=torch.uint8, device=dev)
@@ -206,12 +209,13 @@ def main():
         L = stride = None
         hashed = int(lens.sum())
         out = torch.empty(nblk, dtype=torch.int32, device=dev)
-        hint = "256" if small else "1k"
+        hint = "256" if small else ("512" if mid else "1k")
 
         def step():
             crc32c.batch(data, d_blk, out=out, size_hint=hint)
 
         workload = {"workload": ("wal100: 1 GiB log image, 32-KiB blocks, 131-B records" if small else
+                                 "wal400: 2 GiB log image, 32-KiB blocks, 431-B records" if mid else
                                  "wal: 4 GiB log image, 32-KiB blocks, 1055-B records") +
                                 " -> type||payload fragments (descriptor list)",
                     "blocks_per_gpu": nblk, "bytes_per_gpu": hashed}
@@ -237,7 +241,7 @@ def main():
 
         workload = {"workload": "c3: Zipf 1-64 KiB blocks, packed, descriptor list",
                     "blocks_per_gpu": nblk, "bytes_per_gpu": hashed}
-    algo_bytes = hashed + 4 * nblk + (16 * nblk if args.workload in ("c3", "wal", "wal100") else 0)
+    algo_bytes = hashed + 4 * nblk + (16 * nblk if args.workload in ("c3", "wal", "wal100", "wal400") else 0)
     if args.workload == "sst_verify":  # + the 4-B stored trailer read, 16-B handle, 1-B ok written
         algo_bytes = hashed + nblk * (4 + 16 + 1)
     elif args.workload in ("sst_seal", "sst_crc"):  # + 4-B trailer / CRC written, 16-B handle
@@ -304,9 +308,9 @@ def main():
             extra["copy_inclusive"] = copy_inclusive(crc32c, data, L, stride, min(nblk, 1 << 18))
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            if args.workload in ("c2", "sstable", "c3", "wal", "wal100"):
+            if args.workload in ("c2", "sstable", "c3", "wal", "wal100", "wal400"):
                 cpu = cpu_baseline(data, L, stride, nblk, args,
-                                   d_blk if args.workload in ("c3", "wal", "wal100") else None)
+                                   d_blk if args.workload in ("c3", "wal", "wal100", "wal400") else None)
             else:  # sst_verify / sst_seal: the reference's CRC over each block's contents || type
                 cpu = cpu_baseline(data, L, stride, nblk, args, cpu_blk)
 
@@ -340,6 +344,7 @@ def main():
                            "c3": "crc_stream16_kernel<DescSrc,OutSink,dyn,nt,pack>",
                            "wal": "crc_sst1k_kernel<DescSrc,OutSink,nt>",
                            "wal100": "crc_lanerec9_kernel<DescSrc,OutSink>",
+                           "wal400": "crc_lanerec17_kernel<DescSrc,OutSink>",
                            "sst_verify": "crc_sst4k_kernel<SstSrc,SstVerifySink,nt>",
                            "sst_seal": "crc_sst4k_kernel<SstSrc,SealSink,nt>",
                            "sst_crc": "crc_sst4k_kernel<SstSrc,SstCrcSink,nt>"}[args.workload],

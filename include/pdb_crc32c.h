@@ -62,6 +62,7 @@ typedef struct pdb_block_handle {
 #define PDB_CRC_SIZE_1K 0x4u /* most blocks 1024..1152 B: WAL physical records (type || fragment) */
 #define PDB_CRC_SIZE_4K 0x8u /* most blocks 4096..4352 B: sstable data blocks (contents || type) */
 #define PDB_CRC_SIZE_256 0x10u /* most blocks 1..256 B: small WAL / MANIFEST records */
+#define PDB_CRC_SIZE_512 0x20u /* most blocks 257..512 B: WAL records of ~400-B values */
 
 /* error codes */
 #define PDB_OK 0

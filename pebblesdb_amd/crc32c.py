@@ -30,7 +30,8 @@ USE_INIT = 0x2  # PDB_CRC_USE_INIT
 SIZE_1K = 0x4  # PDB_CRC_SIZE_1K: most blocks 1024..1152 B (WAL records) -- a speed hint only
 SIZE_4K = 0x8  # PDB_CRC_SIZE_4K: most blocks 4096..4352 B (sstable data blocks)
 SIZE_256 = 0x10  # PDB_CRC_SIZE_256: most blocks 1..256 B (small WAL / MANIFEST records)
-_SIZE_HINT = {None: 0, "1k": SIZE_1K, "4k": SIZE_4K, "256": SIZE_256}
+SIZE_512 = 0x20  # PDB_CRC_SIZE_512: most blocks 257..512 B (WAL records of ~400-B values)
+_SIZE_HINT = {None: 0, "1k": SIZE_1K, "4k": SIZE_4K, "256": SIZE_256, "512": SIZE_512}
 K_MASK_DELTA = 0xA282EAD8  # util/crc32c.h:24
 
 BLK_DTYPE = np.dtype([("off", "<u8"), ("len", "<u4"), ("init", "<u4")])  # == pdb_blk (16 B)

@@ -1900,10 +1900,15 @@ __global__ __launch_bounds__(kThreads) void crc_lanerec_kernel(const uint32_t* _
 // 64 records instead of one per 32-B group, and the window hashed as two chains for ILP: groups
 // 0..4 (A) and 5..8 (B, the last 128 B), folded as shift128(A) ^ B (slot 3 = shift 128).
 // Groups wholly below every lane's record are skipped (wave-uniform).
-template <class Src, class Sink>
-__global__ __launch_bounds__(kThreads) void crc_lanerec9_kernel(const uint32_t* __restrict__ tabs, Src src,
-                                                                uint64_t nblk, Sink sink) {
-  constexpr uint32_t NG = 9, NA = 5;
+// lanerec_window<NG>: the body for a window of NG groups (records of 1..32*(NG-1) B); chain B
+// takes the last NG - NA groups, a power of two so the fold is one shift slot.  NG = 9 is the
+// <= 256-B class, NG = 17 the 257..512-B class (chain B = 256 B, slot 4).
+template <class Src, class Sink, uint32_t NG, uint32_t kWpw = kWavesPerWg>
+__device__ __forceinline__ void lanerec_window(const uint32_t* __restrict__ tabs, Src src, uint64_t nblk,
+                                               Sink sink) {
+  constexpr uint32_t NA = (NG + 1) / 2, NB = NG - NA, MAXN = 32u * (NG - 1);
+  constexpr int kSlotB = NB == 4 ? 3 : (NB == 8 ? 4 : -1);
+  static_assert(kSlotB >= 0, "chain B must span 128 or 256 B");
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
   char* lds = reinterpret_cast<char*>(lds_words);
   stage_tables<PDB_CAT_TREE16, PDB_CAT_S1024>(lds, tabs);  // slots 0..5 = 16..512 (3 = 128), 6 = 1024
@@ -1914,8 +1919,8 @@ __global__ __launch_bounds__(kThreads) void crc_lanerec9_kernel(const uint32_t* 
   const uintptr_t dummy = reinterpret_cast<uintptr_t>(tabs);  // >= 4 KiB + 256 B of valid bytes
   const uintptr_t lo_ok = reinterpret_cast<uintptr_t>(src.base) + 16u;
   const uint64_t nbat = (nblk + 63u) >> 6;
-  const uint64_t W = static_cast<uint64_t>(gridDim.x) * kWavesPerWg;
-  uint64_t b = wave_id_uniform();
+  const uint64_t W = static_cast<uint64_t>(gridDim.x) * kWpw;
+  uint64_t b = static_cast<uint64_t>(blockIdx.x) * kWpw + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (b >= nbat) return;
   auto idx = [&](uint64_t bb) -> uint64_t {
     const uint64_t i = (bb << 6) + u;
@@ -1927,7 +1932,7 @@ __global__ __launch_bounds__(kThreads) void crc_lanerec9_kernel(const uint32_t* 
     keep_alive(raw);
     const BlkDesc d = src.lane(raw);
     const uintptr_t p0 = reinterpret_cast<uintptr_t>(d.p);
-    const bool fast = (d.n - 1u) <= 255u && d.init_raw == 0xFFFFFFFFu && p0 >= lo_ok;
+    const bool fast = (d.n - 1u) <= MAXN - 1u && d.init_raw == 0xFFFFFFFFu && p0 >= lo_ok;
     const uintptr_t p = fast ? p0 : dummy + 16u;
     const uint32_t n = fast ? d.n : 1u;
     const uintptr_t e = p + n;
@@ -1935,7 +1940,7 @@ __global__ __launch_bounds__(kThreads) void crc_lanerec9_kernel(const uint32_t* 
     const uintptr_t A0 = p & ~static_cast<uintptr_t>(3);
     const uintptr_t d0 = A1 + 4u - 32u * NG;
     u32x4 C[2 * NG];
-    C[0] = u32x4{0, 0, 0, 0};  // dwords 0..3 lie wholly below every record of <= 256 B
+    C[0] = u32x4{0, 0, 0, 0};  // dwords 0..3 lie wholly below every record of <= MAXN B
 #pragma unroll
     for (uint32_t h = 1; h < 2 * NG; ++h) {
       const uintptr_t a = d0 + 16u * h;
@@ -1983,7 +1988,7 @@ __global__ __launch_bounds__(kThreads) void crc_lanerec9_kernel(const uint32_t* 
       if (static_cast<uint32_t>(t) >= t0) group(ca, t);
       if (t + NA < NG && static_cast<uint32_t>(t) + NA >= t0) group(cb, t + NA);
     }
-    const uint32_t c = t0 < NA ? shift_op_x(lds, 3, ca, cb) : cb;
+    const uint32_t c = t0 < NA ? shift_op_x(lds, kSlotB, ca, cb) : cb;
     if (valid && fast) SinkOps<Sink>::put(sink, i, c, d, pre);
     // the batch's records outside the fast range, one per pass of the whole wave
     uint64_t slow = __builtin_amdgcn_ballot_w64(valid && !fast);
@@ -2004,8 +2009,29 @@ __global__ __launch_bounds__(kThreads) void crc_lanerec9_kernel(const uint32_t* 
   }
 }
 
+template <class Src, class Sink>
+__global__ __launch_bounds__(kThreads) void crc_lanerec9_kernel(const uint32_t* __restrict__ tabs, Src src,
+                                                                uint64_t nblk, Sink sink) {
+  lanerec_window<Src, Sink, 9>(tabs, src, nblk, sink);
+}
+
+// 512 threads (8 waves, one workgroup per CU for the 160-KiB LDS image): 256 VGPRs per lane hold
+// the 34 x 16-B window without spilling (1024 threads cap it at 128 and spill ~240 B per lane)
+constexpr uint32_t kThreads17 = 512;
+template <class Src, class Sink>
+__global__ __launch_bounds__(kThreads17) void crc_lanerec17_kernel(const uint32_t* __restrict__ tabs, Src src,
+                                                                   uint64_t nblk, Sink sink) {
+  lanerec_window<Src, Sink, 17, kThreads17 / 64>(tabs, src, nblk, sink);
+}
+
 uint32_t grid_for(const LaunchGeom& g, uint64_t nblk) {
   const uint64_t want = (nblk + kWavesPerWg - 1) / kWavesPerWg;
+  return static_cast<uint32_t>(want < g.grid ? (want ? want : 1) : g.grid);
+}
+
+// crc_lanerec17_kernel: one wave per batch of 64 records, kThreads17 / 64 waves per workgroup
+uint32_t grid17(const LaunchGeom& g, uint64_t nblk) {
+  const uint64_t want = ((nblk + 63) / 64 + kThreads17 / 64 - 1) / (kThreads17 / 64);
   return static_cast<uint32_t>(want < g.grid ? (want ? want : 1) : g.grid);
 }
 

@@ -1,0 +1,66 @@
+#!/usr/bin/env python3
+"""A/B for the 257..512-B record class: crc_lanerec17_kernel (hint "512") against the descriptor
+path with hints ignored (variant 40: the generic stream kernel) and against the <= 256-B kernel
+(hint "256", whose whole-wave slow path these records take).  Records packed back to back (any
+alignment), ~2 GiB per case; GB/s = (record bytes + 16-B descriptor + 4-B result) / kernel time.
+Also the fixed-stride entry at 431 B.  Prints one JSON object."""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from pebblesdb_amd import crc32c  # noqa: E402
+from pebblesdb_amd._native import lib  # noqa: E402
+
+crc32c.init_device(0)
+total = 2 << 30
+d = torch.empty(total + (1 << 20), dtype=torch.uint8, device="cuda")
+crc32c.fill_splitmix(d, 11)
+
+
+def timeit(fn, reps=10):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+rng = np.random.Generator(np.random.PCG64(5))
+cases = {
+    "uniform_257_512": rng.integers(257, 513, size=total // 385),
+    "fixed_431": np.full(total // 431, 431),
+    "uniform_1_512": rng.integers(1, 513, size=total // 257),
+    "fixed_512": np.full(total // 512, 512),
+}
+res = {}
+for name, sizes in cases.items():
+    offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]) + 3
+    d_blk = crc32c.blocks_to_device(crc32c.make_blocks(offs, sizes))
+    out = torch.empty(len(sizes), dtype=torch.int32, device="cuda")
+    nbytes = int(sizes.sum()) + 20 * len(sizes)
+    row = {}
+    ref = None
+    for tag, hint, var in (("lanerec17", "512", 0), ("generic", None, 40), ("lanerec9_slow", "256", 0)):
+        lib().pdb_diag_set_variant(var)
+        try:
+            ms = timeit(lambda: crc32c.batch(d, d_blk, out=out, size_hint=hint))
+            got = out.cpu().numpy().copy()
+        finally:
+            lib().pdb_diag_set_variant(0)
+        ref = got if ref is None else ref
+        row[tag] = {"ms": round(ms, 4), "GB/s": round(nbytes / ms / 1e6, 1), "same": bool((got == ref).all())}
+    res[name] = row
+    del d_blk, out
+L, n = 431, total // 431
+ms = timeit(lambda: crc32c.batch_fixed(d[3:], L, L, n))
+res["fixed_stride_431"] = {"ms": round(ms, 4), "GB/s": round((n * L + 4 * n) / ms / 1e6, 1)}
+print(json.dumps(res))
