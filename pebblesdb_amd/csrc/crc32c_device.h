@@ -1903,7 +1903,7 @@ __global__ __launch_bounds__(kThreads) void crc_lanerec_kernel(const uint32_t* _
 // lanerec_window<NG>: the body for a window of NG groups (records of 1..32*(NG-1) B); chain B
 // takes the last NG - NA groups, a power of two so the fold is one shift slot.  NG = 9 is the
 // <= 256-B class, NG = 17 the 257..512-B class (chain B = 256 B, slot 4).
-template <class Src, class Sink, uint32_t NG, uint32_t kWpw = kWavesPerWg>
+template <class Src, class Sink, uint32_t NG, uint32_t kWpw = kWavesPerWg, uint32_t kChains = 2>
 __device__ __forceinline__ void lanerec_window(const uint32_t* __restrict__ tabs, Src src, uint64_t nblk,
                                                Sink sink) {
   constexpr uint32_t NA = (NG + 1) / 2, NB = NG - NA, MAXN = 32u * (NG - 1);
@@ -1982,13 +1982,34 @@ __device__ __forceinline__ void lanerec_window(const uint32_t* __restrict__ tabs
         }
       }
     };
-    uint32_t ca = 0, cb = 0;
+    uint32_t c;
+    if constexpr (kChains == 2) {
+      uint32_t ca = 0, cb = 0;
 #pragma unroll
-    for (int t = 0; t < static_cast<int>(NA); ++t) {
-      if (static_cast<uint32_t>(t) >= t0) group(ca, t);
-      if (t + NA < NG && static_cast<uint32_t>(t) + NA >= t0) group(cb, t + NA);
+      for (int t = 0; t < static_cast<int>(NA); ++t) {
+        if (static_cast<uint32_t>(t) >= t0) group(ca, t);
+        if (t + NA < NG && static_cast<uint32_t>(t) + NA >= t0) group(cb, t + NA);
+      }
+      c = t0 < NA ? shift_op_x(lds, kSlotB, ca, cb) : cb;
+    } else {
+      // kChains chains: chain 0 = groups [0, L0), chain k >= 1 = the k-th of the last 128-B spans
+      // (4 groups each); folded as c = shift128(c) ^ chain_k (linear: a chain wholly below every
+      // record is 0 and its fold a no-op, so it is skipped wave-uniformly)
+      constexpr int NT = static_cast<int>(kChains) - 1, L0 = static_cast<int>(NG) - 4 * NT;
+      static_assert(L0 >= 4, "chain 0 must be the longest");
+      uint32_t ch[kChains] = {};
+#pragma unroll
+      for (int t = 0; t < L0; ++t) {
+        if (static_cast<uint32_t>(t) >= t0) group(ch[0], t);
+#pragma unroll
+        for (int k = 1; k <= NT; ++k)
+          if (t < 4 && static_cast<uint32_t>(L0 + 4 * (k - 1) + t) >= t0) group(ch[k], L0 + 4 * (k - 1) + t);
+      }
+      c = ch[0];
+#pragma unroll
+      for (int k = 1; k <= NT; ++k)
+        c = t0 < static_cast<uint32_t>(L0 + 4 * (k - 1)) ? shift_op_x(lds, 3, c, ch[k]) : ch[k];
     }
-    const uint32_t c = t0 < NA ? shift_op_x(lds, kSlotB, ca, cb) : cb;
     if (valid && fast) SinkOps<Sink>::put(sink, i, c, d, pre);
     // the batch's records outside the fast range, one per pass of the whole wave
     uint64_t slow = __builtin_amdgcn_ballot_w64(valid && !fast);
@@ -2018,10 +2039,10 @@ __global__ __launch_bounds__(kThreads) void crc_lanerec9_kernel(const uint32_t* 
 // 512 threads (8 waves, one workgroup per CU for the 160-KiB LDS image): 256 VGPRs per lane hold
 // the 34 x 16-B window without spilling (1024 threads cap it at 128 and spill ~240 B per lane)
 constexpr uint32_t kThreads17 = 512;
-template <class Src, class Sink>
+template <class Src, class Sink, uint32_t kChains = 4>
 __global__ __launch_bounds__(kThreads17) void crc_lanerec17_kernel(const uint32_t* __restrict__ tabs, Src src,
                                                                    uint64_t nblk, Sink sink) {
-  lanerec_window<Src, Sink, 17, kThreads17 / 64>(tabs, src, nblk, sink);
+  lanerec_window<Src, Sink, 17, kThreads17 / 64, kChains>(tabs, src, nblk, sink);
 }
 
 uint32_t grid_for(const LaunchGeom& g, uint64_t nblk) {

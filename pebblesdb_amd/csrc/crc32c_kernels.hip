@@ -215,7 +215,8 @@ hipError_t launch_desc(const LaunchGeom& g, const uint32_t* d_tables, const uint
     }
     return hipGetLastError();
   }
-  if (mode == kModeOut && g_fast_variant != 0 && g_fast_variant != 40 && g_fast_variant != 41 && g_fast_variant != 53)
+  if (mode == kModeOut && g_fast_variant != 0 && g_fast_variant != 40 && g_fast_variant != 41 && g_fast_variant != 53 &&
+      g_fast_variant != 54)
     return launch_desc_variant(g_fast_variant, g, d_tables, base, blk, nblk, flags, out, s);
   const dim3 grid(grid_for(g, nblk)), block(kThreads);
   const DescSrc src{base, blk, flags};
@@ -233,7 +234,10 @@ hipError_t launch_desc(const LaunchGeom& g, const uint32_t* d_tables, const uint
       if (!(flags & PDB_CRC_SIZE_256)) {
         // 257..512-B class: the same lane-per-record design on a 17-group (544-B) window, chains
         // of 9 + 8 groups; records of 1..512 B all take the fast path
-        if (mode == kModeOut)
+        if (mode == kModeOut && g_fast_variant == 54)  // A/B: two chains (9 + 8 groups)
+          hipLaunchKernelGGL((crc_lanerec17_kernel<DescSrc, OutSink, 2>), dim3(grid17(g, nblk)), dim3(kThreads17), 0,
+                             s, d_tables, src, nblk, OutSink{out, flags});
+        else if (mode == kModeOut)
           hipLaunchKernelGGL((crc_lanerec17_kernel<DescSrc, OutSink>), dim3(grid17(g, nblk)), dim3(kThreads17), 0, s,
                              d_tables, src, nblk, OutSink{out, flags});
         else

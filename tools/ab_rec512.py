@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""A/B for the 257..512-B record class: crc_lanerec17_kernel (hint "512") against the descriptor
+"""A/B for the 257..512-B record class: crc_lanerec17_kernel (hint "512"; 4 chains, variant 54 the
+two-chain 9 + 8-group version) against the descriptor
 path with hints ignored (variant 40: the generic stream kernel) and against the <= 256-B kernel
 (hint "256", whose whole-wave slow path these records take).  Records packed back to back (any
 alignment), ~2 GiB per case; GB/s = (record bytes + 16-B descriptor + 4-B result) / kernel time.
@@ -49,7 +50,8 @@ for name, sizes in cases.items():
     nbytes = int(sizes.sum()) + 20 * len(sizes)
     row = {}
     ref = None
-    for tag, hint, var in (("lanerec17", "512", 0), ("generic", None, 40), ("lanerec9_slow", "256", 0)):
+    for tag, hint, var in (("lanerec17", "512", 0), ("lanerec17_2chains", "512", 54), ("generic", None, 40),
+                           ("lanerec9_slow", "256", 0)):
         lib().pdb_diag_set_variant(var)
         try:
             ms = timeit(lambda: crc32c.batch(d, d_blk, out=out, size_hint=hint))
