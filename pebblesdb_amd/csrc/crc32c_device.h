@@ -1903,7 +1903,8 @@ __global__ __launch_bounds__(kThreads) void crc_lanerec_kernel(const uint32_t* _
 // lanerec_window<NG>: the body for a window of NG groups (records of 1..32*(NG-1) B); chain B
 // takes the last NG - NA groups, a power of two so the fold is one shift slot.  NG = 9 is the
 // <= 256-B class, NG = 17 the 257..512-B class (chain B = 256 B, slot 4).
-template <class Src, class Sink, uint32_t NG, uint32_t kWpw = kWavesPerWg, uint32_t kChains = 2>
+template <class Src, class Sink, uint32_t NG, uint32_t kWpw = kWavesPerWg, uint32_t kChains = 2,
+          bool kPrefetch = false>
 __device__ __forceinline__ void lanerec_window(const uint32_t* __restrict__ tabs, Src src, uint64_t nblk,
                                                Sink sink) {
   constexpr uint32_t NA = (NG + 1) / 2, NB = NG - NA, MAXN = 32u * (NG - 1);
@@ -1926,27 +1927,52 @@ __device__ __forceinline__ void lanerec_window(const uint32_t* __restrict__ tabs
     const uint64_t i = (bb << 6) + u;
     return i < nblk ? i : nblk - 1;
   };
-  typename Src::Raw raw = src.load(idx(b));
-  for (;;) {
-    const uint64_t i = (b << 6) + u, bn = b + W;
-    keep_alive(raw);
-    const BlkDesc d = src.lane(raw);
-    const uintptr_t p0 = reinterpret_cast<uintptr_t>(d.p);
-    const bool fast = (d.n - 1u) <= MAXN - 1u && d.init_raw == 0xFFFFFFFFu && p0 >= lo_ok;
-    const uintptr_t p = fast ? p0 : dummy + 16u;
-    const uint32_t n = fast ? d.n : 1u;
-    const uintptr_t e = p + n;
-    const uintptr_t A1 = (e - 1u) & ~static_cast<uintptr_t>(3);
-    const uintptr_t A0 = p & ~static_cast<uintptr_t>(3);
-    const uintptr_t d0 = A1 + 4u - 32u * NG;
-    u32x4 C[2 * NG];
-    C[0] = u32x4{0, 0, 0, 0};  // dwords 0..3 lie wholly below every record of <= MAXN B
+  // the window of one lane's record: chunk h (16 B) at d0 + 16 h; chunks wholly below the record
+  // read the dummy line.  Records outside the fast range hash a 1-B stand-in (slow path below).
+  auto issue = [&](const BlkDesc& dd, u32x4 (&CC)[2 * NG]) {
+    const uintptr_t q0 = reinterpret_cast<uintptr_t>(dd.p);
+    const bool f = (dd.n - 1u) <= MAXN - 1u && dd.init_raw == 0xFFFFFFFFu && q0 >= lo_ok;
+    const uintptr_t q = f ? q0 : dummy + 16u;
+    const uintptr_t a1 = (q + (f ? dd.n : 1u) - 1u) & ~static_cast<uintptr_t>(3);
+    const uintptr_t a0 = q & ~static_cast<uintptr_t>(3);
+    const uintptr_t w0 = a1 + 4u - 32u * NG;
+    CC[0] = u32x4{0, 0, 0, 0};  // dwords 0..3 lie wholly below every record of <= MAXN B
 #pragma unroll
     for (uint32_t h = 1; h < 2 * NG; ++h) {
-      const uintptr_t a = d0 + 16u * h;
-      C[h] = gload128<false>(a + 12u < A0 ? dummy : a);
+      const uintptr_t a = w0 + 16u * h;
+      CC[h] = gload128<false>(a + 12u < a0 ? dummy : a);
     }
-    raw = src.load(idx(bn < nbat ? bn : b));  // next batch's descriptors (unconditional)
+  };
+  typename Src::Raw raw = src.load(idx(b));
+  u32x4 C[2 * NG];
+  BlkDesc dnext{};
+  if constexpr (kPrefetch) {  // batch b's window now, the loop issues batch b + W's before hashing b
+    keep_alive(raw);
+    dnext = src.lane(raw);
+    issue(dnext, C);
+    raw = src.load(idx(b + W < nbat ? b + W : b));
+  }
+  for (;;) {
+    const uint64_t i = (b << 6) + u, bn = b + W;
+    BlkDesc d;
+    u32x4 Cn[kPrefetch ? 2 * NG : 1];
+    if constexpr (kPrefetch) {
+      d = dnext;
+      keep_alive(raw);
+      dnext = src.lane(raw);  // batch bn (clamped past the end: valid, unused)
+      issue(dnext, Cn);
+      raw = src.load(idx(bn + W < nbat ? bn + W : bn));
+    } else {
+      keep_alive(raw);
+      d = src.lane(raw);
+      issue(d, C);
+      raw = src.load(idx(bn < nbat ? bn : b));  // next batch's descriptors (unconditional)
+    }
+    const uintptr_t p0 = reinterpret_cast<uintptr_t>(d.p);
+    const bool fast = (d.n - 1u) <= MAXN - 1u && d.init_raw == 0xFFFFFFFFu && p0 >= lo_ok;
+    const uint32_t n = fast ? d.n : 1u;
+    const uintptr_t e = (fast ? p0 : dummy + 16u) + n;
+    const uintptr_t A1 = (e - 1u) & ~static_cast<uintptr_t>(3);
     const bool valid = i < nblk;
     const uint32_t pre = SinkOps<Sink>::pre(sink, idx(b), d);
     const uint32_t sel = static_cast<uint32_t>(e - A1) * 0x01010101u + 0x03020100u;  // bytes sb..sb+3
@@ -2025,6 +2051,10 @@ __device__ __forceinline__ void lanerec_window(const uint32_t* __restrict__ tabs
       const BlkDesc sd{reinterpret_cast<const uint8_t*>(sp), sn, 0xFFFFFFFFu};
       if (u == 0) SinkOps<Sink>::put(sink, (b << 6) + k, rs, sd, __builtin_amdgcn_readlane(pre, k));
     }
+    if constexpr (kPrefetch) {
+#pragma unroll
+      for (uint32_t h = 0; h < 2 * NG; ++h) C[h] = Cn[h];
+    }
     if (bn >= nbat) break;
     b = bn;
   }
@@ -2047,6 +2077,19 @@ __global__ __launch_bounds__(kThreads17) void crc_lanerec17_kernel(const uint32_
 
 uint32_t grid_for(const LaunchGeom& g, uint64_t nblk) {
   const uint64_t want = (nblk + kWavesPerWg - 1) / kWavesPerWg;
+  return static_cast<uint32_t>(want < g.grid ? (want ? want : 1) : g.grid);
+}
+
+// A/B variants: the window of batch b + W issued before batch b is hashed (two windows live):
+// 9 groups at 512 threads (variant 55), 17 groups at 256 threads (variant 56, AGPRs available)
+template <class Src, class Sink, uint32_t NG, uint32_t kWg>
+__global__ __launch_bounds__(kWg) void crc_lanerec_pf_kernel(const uint32_t* __restrict__ tabs, Src src,
+                                                             uint64_t nblk, Sink sink) {
+  lanerec_window<Src, Sink, NG, kWg / 64, NG == 17 ? 4 : 2, true>(tabs, src, nblk, sink);
+}
+
+uint32_t grid_wg(const LaunchGeom& g, uint64_t nblk, uint32_t wg) {
+  const uint64_t want = ((nblk + 63) / 64 + wg / 64 - 1) / (wg / 64);
   return static_cast<uint32_t>(want < g.grid ? (want ? want : 1) : g.grid);
 }
 

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""A/B for the 257..512-B record class: crc_lanerec17_kernel (hint "512"; 4 chains, variant 54 the
+"""A/B for the record classes (variants 55/56: the next batch's window issued before hashing the
+current one).  The 257..512-B record class: crc_lanerec17_kernel (hint "512"; 4 chains, variant 54 the
 two-chain 9 + 8-group version) against the descriptor
 path with hints ignored (variant 40: the generic stream kernel) and against the <= 256-B kernel
 (hint "256", whose whole-wave slow path these records take).  Records packed back to back (any
@@ -41,6 +42,8 @@ cases = {
     "fixed_431": np.full(total // 431, 431),
     "uniform_1_512": rng.integers(1, 513, size=total // 257),
     "fixed_512": np.full(total // 512, 512),
+    "small_fixed_131": np.full(total // 262, 131),
+    "small_uniform_1_256": rng.integers(1, 257, size=total // 258),
 }
 res = {}
 for name, sizes in cases.items():
@@ -50,8 +53,10 @@ for name, sizes in cases.items():
     nbytes = int(sizes.sum()) + 20 * len(sizes)
     row = {}
     ref = None
-    for tag, hint, var in (("lanerec17", "512", 0), ("lanerec17_2chains", "512", 54), ("generic", None, 40),
-                           ("lanerec9_slow", "256", 0)):
+    tags = ((("lanerec9", "256", 0), ("lanerec9_prefetch512", "256", 55)) if name.startswith("small") else
+            (("lanerec17", "512", 0), ("lanerec17_2chains", "512", 54), ("lanerec17_prefetch256", "512", 56),
+             ("generic", None, 40), ("lanerec9_slow", "256", 0)))
+    for tag, hint, var in tags:
         lib().pdb_diag_set_variant(var)
         try:
             ms = timeit(lambda: crc32c.batch(d, d_blk, out=out, size_hint=hint))
