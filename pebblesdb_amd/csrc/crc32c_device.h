@@ -2080,6 +2080,101 @@ uint32_t grid_for(const LaunchGeom& g, uint64_t nblk) {
   return static_cast<uint32_t>(want < g.grid ? (want ? want : 1) : g.grid);
 }
 
+// Four lanes per record (A/B variants 57/58): the lane-per-record kernels are TA-bound (one cache
+// line per lane per load), so here a record's window of 16 R 16-B chunks is loaded with
+// its chunks interleaved across 4 lanes (lane j: chunks 4m + j), i.e. 64 contiguous bytes of one
+// record per lane quad per instruction.  Lane j hashes each of its chunks from 0 and folds
+// c = shift64(c) ^ t; the quad is folded with shift16 / shift32.  The dword before a chunk (for the
+// byte-shift v_perm) comes from the previous lane of the quad (one bpermute per round).
+template <class Src, class Sink, uint32_t R, uint32_t MAXN>
+__global__ __launch_bounds__(kThreads) void crc_quadrec_kernel(const uint32_t* __restrict__ tabs, Src src,
+                                                              uint64_t nblk, Sink sink) {
+  static_assert(MAXN + 4u <= 64u * R, "window too short");
+  __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
+  char* lds = reinterpret_cast<char*>(lds_words);
+  stage_tables<PDB_CAT_TREE16, PDB_CAT_S1024>(lds, tabs);  // slots 0..5 = 16..512, 6 = 1024
+  const uint32_t u = threadIdx.x & 63u, j = u & 3u;
+  const uint32_t ureg = tabs[PDB_UNSHIFT_OFF + (u & 15u)];
+  __syncthreads();
+  const LaneTabs lt = lane_tabs(u);
+  const uintptr_t dummy = reinterpret_cast<uintptr_t>(tabs);
+  const uintptr_t lo_ok = reinterpret_cast<uintptr_t>(src.base) + 16u;
+  const uint64_t nbat = (nblk + 15u) >> 4;
+  const uint64_t W = static_cast<uint64_t>(gridDim.x) * kWavesPerWg;
+  uint64_t b = wave_id_uniform();
+  if (b >= nbat) return;
+  auto idx = [&](uint64_t bb) -> uint64_t {
+    const uint64_t i = (bb << 4) + (u >> 2);
+    return i < nblk ? i : nblk - 1;
+  };
+  const uint32_t from = (u & ~3u) | ((j + 3u) & 3u);  // previous lane of the quad (lane 3 for lane 0)
+  typename Src::Raw raw = src.load(idx(b));
+  for (;;) {
+    const uint64_t i = (b << 4) + (u >> 2), bn = b + W;
+    keep_alive(raw);
+    const BlkDesc d = src.lane(raw);
+    const uintptr_t p0 = reinterpret_cast<uintptr_t>(d.p);
+    const bool fast = (d.n - 1u) <= MAXN - 1u && d.init_raw == 0xFFFFFFFFu && p0 >= lo_ok;
+    const uintptr_t p = fast ? p0 : dummy + 16u;
+    const uint32_t n = fast ? d.n : 1u;
+    const uintptr_t e = p + n;
+    const uintptr_t A1 = (e - 1u) & ~static_cast<uintptr_t>(3);
+    const uintptr_t A0 = p & ~static_cast<uintptr_t>(3);
+    const uintptr_t ws = A1 + 4u - 64u * R;
+    u32x4 C[R];
+#pragma unroll
+    for (uint32_t m = 0; m < R; ++m) {
+      const uintptr_t a = ws + 64u * m + 16u * j;
+      C[m] = gload128<false>(a + 12u < A0 ? dummy : a);
+    }
+    raw = src.load(idx(bn < nbat ? bn : b));
+    const bool valid = i < nblk;
+    const uint32_t pre = SinkOps<Sink>::pre(sink, idx(b), d);
+    const uint32_t sel = static_cast<uint32_t>(e - A1) * 0x01010101u + 0x03020100u;
+    const int32_t dz0 = static_cast<int32_t>(64u * R - n);  // p - start of constructed word 0
+    const uint32_t uz = __shfl(ureg, static_cast<uint32_t>(dz0) & 3u, 64);
+    uint32_t c = 0;
+#pragma unroll
+    for (uint32_t m = 0; m < R; ++m) {
+      const uint32_t send = j < 3u ? C[m].w : (m ? C[m - 1].w : 0u);
+      const uint32_t prev = __shfl(send, from, 64);
+      const int32_t zc = dz0 - static_cast<int32_t>(16u * (4u * m + j));  // z of the chunk's first word
+      if (__builtin_amdgcn_ballot_w64(zc < 16) == 0) continue;  // the round lies below every record
+      const uint32_t dw[5] = {prev, C[m].x, C[m].y, C[m].z, C[m].w};
+      uint32_t t = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int32_t z = zc - 4 * k;
+        const uint32_t w = __builtin_amdgcn_perm(dw[k + 1], dw[k], sel);
+        const uint32_t mk = z <= 0 ? 0xFFFFFFFFu : (z >= 4 ? 0u : (0xFFFFFFFFu << (8u * static_cast<uint32_t>(z))));
+        const uint32_t inj = static_cast<uint32_t>(z) < 4u ? uz : 0u;
+        t = step4(lds, lt, t ^ inj, w & mk);
+      }
+      c = shift_op_x(lds, 2, c, t);  // c = shift64(c) ^ t
+    }
+    uint32_t y = __shfl_down(c, 1, 64);
+    if ((j & 1u) == 0) c = shift_op_x(lds, 0, c, y);
+    y = __shfl_down(c, 2, 64);
+    if (j == 0) c = shift_op_x(lds, 1, c, y);
+    if (valid && fast && j == 0) SinkOps<Sink>::put(sink, i, c, d, pre);
+    uint64_t slow = __builtin_amdgcn_ballot_w64(valid && !fast && j == 0);
+    const uint32_t plo = static_cast<uint32_t>(p0), phi = static_cast<uint32_t>(static_cast<uint64_t>(p0) >> 32);
+    while (slow) {
+      const uint32_t k = static_cast<uint32_t>(__builtin_ctzll(slow));
+      slow &= slow - 1;
+      const uintptr_t sp = static_cast<uintptr_t>(uniform64(__builtin_amdgcn_readlane(plo, k), __builtin_amdgcn_readlane(phi, k)));
+      const uint32_t sn = __builtin_amdgcn_readlane(d.n, k);
+      SlowFirst sf;
+      slow_issue(sf, sp, sn, u, dummy);
+      const uint32_t rs = slow_finish(lds, lt, u, ureg, sf, sp, sn);
+      const BlkDesc sd{reinterpret_cast<const uint8_t*>(sp), sn, 0xFFFFFFFFu};
+      if (u == 0) SinkOps<Sink>::put(sink, (b << 4) + (k >> 2), rs, sd, __builtin_amdgcn_readlane(pre, k));
+    }
+    if (bn >= nbat) break;
+    b = bn;
+  }
+}
+
 // A/B variants: the window of batch b + W issued before batch b is hashed (two windows live):
 // 9 groups at 512 threads (variant 55), 17 groups at 256 threads (variant 56, AGPRs available)
 template <class Src, class Sink, uint32_t NG, uint32_t kWg>

@@ -216,7 +216,7 @@ hipError_t launch_desc(const LaunchGeom& g, const uint32_t* d_tables, const uint
     return hipGetLastError();
   }
   if (mode == kModeOut && g_fast_variant != 0 && g_fast_variant != 40 && g_fast_variant != 41 && g_fast_variant != 53 &&
-      (g_fast_variant < 54 || g_fast_variant > 56))
+      (g_fast_variant < 54 || g_fast_variant > 58))
     return launch_desc_variant(g_fast_variant, g, d_tables, base, blk, nblk, flags, out, s);
   const dim3 grid(grid_for(g, nblk)), block(kThreads);
   const DescSrc src{base, blk, flags};
@@ -234,7 +234,10 @@ hipError_t launch_desc(const LaunchGeom& g, const uint32_t* d_tables, const uint
       if (!(flags & PDB_CRC_SIZE_256)) {
         // 257..512-B class: the same lane-per-record design on a 17-group (544-B) window, chains
         // of 9 + 8 groups; records of 1..512 B all take the fast path
-        if (mode == kModeOut && g_fast_variant == 56)  // A/B: cross-batch prefetch, 256 threads
+        if (mode == kModeOut && g_fast_variant == 58)  // A/B: four lanes per record
+          hipLaunchKernelGGL((crc_quadrec_kernel<DescSrc, OutSink, 9, 512>), dim3(grid_for(g, (nblk + 15) / 16)), block,
+                             0, s, d_tables, src, nblk, OutSink{out, flags});
+        else if (mode == kModeOut && g_fast_variant == 56)  // A/B: cross-batch prefetch, 256 threads
           hipLaunchKernelGGL((crc_lanerec_pf_kernel<DescSrc, OutSink, 17, 256>), dim3(grid_wg(g, nblk, 256)),
                              dim3(256), 0, s, d_tables, src, nblk, OutSink{out, flags});
         else if (mode == kModeOut && g_fast_variant == 54)  // A/B: two chains (9 + 8 groups)
@@ -248,7 +251,10 @@ hipError_t launch_desc(const LaunchGeom& g, const uint32_t* d_tables, const uint
                              s, d_tables, src, nblk, VerifySink{expected, ok, nbad, flags});
         return hipGetLastError();
       }
-      if (mode == kModeOut && g_fast_variant == 55)  // A/B: cross-batch prefetch, 512 threads
+      if (mode == kModeOut && g_fast_variant == 57)  // A/B: four lanes per record
+        hipLaunchKernelGGL((crc_quadrec_kernel<DescSrc, OutSink, 5, 256>), dim3(grid_for(g, (nblk + 15) / 16)), block,
+                           0, s, d_tables, src, nblk, OutSink{out, flags});
+      else if (mode == kModeOut && g_fast_variant == 55)  // A/B: cross-batch prefetch, 512 threads
         hipLaunchKernelGGL((crc_lanerec_pf_kernel<DescSrc, OutSink, 9, 512>), dim3(grid_wg(g, nblk, 512)),
                            dim3(512), 0, s, d_tables, src, nblk, OutSink{out, flags});
       else if (mode == kModeOut && g_fast_variant == 53)

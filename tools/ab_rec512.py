@@ -53,8 +53,10 @@ for name, sizes in cases.items():
     nbytes = int(sizes.sum()) + 20 * len(sizes)
     row = {}
     ref = None
-    tags = ((("lanerec9", "256", 0), ("lanerec9_prefetch512", "256", 55)) if name.startswith("small") else
+    tags = ((("lanerec9", "256", 0), ("lanerec9_prefetch512", "256", 55), ("quadrec5", "256", 57))
+            if name.startswith("small") else
             (("lanerec17", "512", 0), ("lanerec17_2chains", "512", 54), ("lanerec17_prefetch256", "512", 56),
+             ("quadrec9", "512", 58),
              ("generic", None, 40), ("lanerec9_slow", "256", 0)))
     for tag, hint, var in tags:
         lib().pdb_diag_set_variant(var)
