@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "pebblesdb_amd/crc32c.h"
+#include "pebblesdb_amd/log_records.h"
 #include "pebblesdb_amd/table_blocks.h"
 
 static int failures = 0;
@@ -151,6 +152,34 @@ static void VerifyReferenceTables(const std::string& dir) {
   }
 }
 
+// The reference-written logs of tests/golden/log (the reference's own log::Writer): every
+// physical record verified in one batch; the logical record count (Full + Last) matches the
+// manifest; a flipped payload byte or stored-CRC byte fails exactly that record.
+static void VerifyReferenceLogs(const std::string& dir) {
+  struct { const char* name; size_t logical; } logs[] = {{"wal_mixed.log", 15}, {"manifest_small.log", 300}};
+  for (const auto& lg : logs) {
+    const std::string img = ReadFile(dir + "/" + lg.name);
+    EXPECT(!img.empty());
+    if (img.empty()) continue;
+    std::vector<pdb::log::PhysicalRecord> recs;
+    std::vector<uint8_t> ok;
+    EXPECT(pdb::log::VerifyLog(img.data(), img.size(), &recs, &ok) == 0);
+    size_t logical = 0;
+    for (const auto& r : recs) logical += r.type == pdb::log::kFullType || r.type == pdb::log::kLastType;
+    EXPECT(logical == lg.logical && ok.size() == recs.size());
+    for (size_t k = 0; k < recs.size(); k += (recs.size() + 4) / 5) {
+      std::string bad = img;
+      if (recs[k].length) {
+        bad[recs[k].payload_offset() + recs[k].length / 2] ^= 0x20;
+        EXPECT(pdb::log::VerifyLog(bad.data(), bad.size(), &recs, &ok) == 1 && ok[k] == 0);
+      }
+      bad = img;
+      bad[recs[k].offset + 2] ^= 0x01;  // the stored crc
+      EXPECT(pdb::log::VerifyLog(bad.data(), bad.size(), &recs, &ok) == 1 && ok[k] == 0);
+    }
+  }
+}
+
 int main(int argc, char** argv) {
   if (pdb_crc32c_init(0) != 0) {
     fprintf(stderr, "no device: %s\n", pdb_last_error());
@@ -161,6 +190,7 @@ int main(int argc, char** argv) {
   ExtendAndMask();
   TrailerRoundTrip();
   if (argc > 1) VerifyReferenceTables(argv[1]);
+  if (argc > 2) VerifyReferenceLogs(argv[2]);
   if (failures) {
     fprintf(stderr, "%d failures\n", failures);
     return 1;

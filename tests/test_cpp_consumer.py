@@ -1,4 +1,4 @@
-"""The C++ drop-in headers (include/pebblesdb_amd/{crc32c,table_blocks}.h) compile and link
+"""The C++ drop-in headers (include/pebblesdb_amd/{crc32c,table_blocks,log_records}.h) compile and link
 against the library with plain g++ (CPU), and the consumer test passes on the GPU."""
 import os
 import subprocess
@@ -28,7 +28,8 @@ def test_cpp_consumer_builds_and_links():
 @pytest.mark.gpu
 def test_cpp_consumer_runs_on_gpu():
     exe = _compile()
-    r = subprocess.run([exe, os.path.join(ROOT, "tests", "golden", "sst")], capture_output=True, text=True,
+    r = subprocess.run([exe, os.path.join(ROOT, "tests", "golden", "sst"), os.path.join(ROOT, "tests", "golden", "log")],
+                       capture_output=True, text=True,
                        timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "PASS" in r.stdout
