@@ -15,6 +15,7 @@
 
 #include <stdint.h>
 
+#include <string>
 #include <vector>
 
 #include "pdb_crc32c.h"
@@ -94,6 +95,110 @@ inline int64_t VerifyLog(const char* image, uint64_t n, std::vector<PhysicalReco
 }
 
 inline const char* ChecksumMismatchMessage() { return "checksum mismatch"; }  // log_reader.cc:246
+
+// Logical records (Full, or First Middle* Last) from verified physical records, in the spirit of
+// log::Reader::ReadRecord (log_reader.cc:62-183): a record with ok[i] == 0 is dropped together with
+// any fragment being assembled.  Returns the bytes dropped (headers + payloads).
+inline uint64_t AssembleRecords(const char* image, const std::vector<PhysicalRecord>& recs,
+                                const std::vector<uint8_t>& ok, std::vector<std::string>* out) {
+  out->clear();
+  uint64_t dropped = 0;
+  bool in_frag = false;
+  std::string frag;
+  for (size_t i = 0; i < recs.size(); ++i) {
+    const PhysicalRecord& r = recs[i];
+    const char* payload = image + r.payload_offset();
+    const bool good = i < ok.size() && ok[i] &&
+                      (r.type == kFullType || r.type == kFirstType || (in_frag && (r.type == kMiddleType ||
+                                                                                  r.type == kLastType)));
+    if (!good) {
+      dropped += kHeaderSize + r.length + (in_frag ? frag.size() : 0);
+      in_frag = false;
+      frag.clear();
+      continue;
+    }
+    if (r.type == kFullType) {
+      if (in_frag) dropped += frag.size();  // a First without its Last (log_reader.cc:78-95)
+      in_frag = false;
+      frag.clear();
+      out->push_back(std::string(payload, r.length));
+    } else if (r.type == kFirstType) {
+      if (in_frag) dropped += frag.size();
+      frag.assign(payload, r.length);
+      in_frag = true;
+    } else {
+      frag.append(payload, r.length);
+      if (r.type == kLastType) {
+        out->push_back(frag);
+        frag.clear();
+        in_frag = false;
+      }
+    }
+  }
+  return dropped + frag.size();
+}
+
+// Group-commit form of log::Writer (log_writer.cc:28-131): AddRecord fragments and lays out records
+// exactly as the reference writer does (block trailers included), with CRC placeholders; Seal()
+// writes every physical record's Mask(crc32c(type || payload)) from ONE pdb_crc32c_batch_host call.
+class BatchWriter {
+ public:
+  // dest_length: the log file's current length (the writer's block offset starts there, log_writer.cc:16-26)
+  explicit BatchWriter(uint64_t dest_length = 0) : base_(dest_length) {}
+
+  void AddRecord(const char* data, size_t n) {
+    size_t left = n;
+    bool begin = true;
+    do {  // a zero-length record still emits one header (log_writer.cc:63-99)
+      uint64_t block_offset = (base_ + buf_.size()) % kBlockSize;
+      const uint64_t leftover = kBlockSize - block_offset;
+      if (leftover < kHeaderSize) {
+        buf_.append(static_cast<size_t>(leftover), '\0');  // trailer (log_writer.cc:67-76)
+        block_offset = 0;
+      }
+      const size_t avail = static_cast<size_t>(kBlockSize - block_offset - kHeaderSize);
+      const size_t frag = left < avail ? left : avail;
+      const bool end = left == frag;
+      const uint8_t type = begin && end ? kFullType : (begin ? kFirstType : (end ? kLastType : kMiddleType));
+      hdr_.push_back(buf_.size());
+      len_.push_back(static_cast<uint32_t>(frag));
+      const char h[7] = {0, 0, 0, 0, static_cast<char>(frag & 0xff), static_cast<char>(frag >> 8),
+                         static_cast<char>(type)};
+      buf_.append(h, 7);
+      buf_.append(data, frag);
+      data += frag;
+      left -= frag;
+      begin = false;
+    } while (left > 0);
+  }
+
+  // Returns 0 or a negative PDB_E* code; bytes() then holds what Writer::AddRecord would have written.
+  int Seal() {
+    if (hdr_.empty()) return 0;
+    std::vector<pdb_blk> blk(hdr_.size());
+    for (size_t i = 0; i < hdr_.size(); ++i) {
+      blk[i].off = hdr_[i] + 6;
+      blk[i].len = 1 + len_[i];
+      blk[i].init = 0;
+    }
+    std::vector<uint32_t> crc(hdr_.size());
+    const int rc = pdb_crc32c_batch_host(buf_.data(), buf_.size(), blk.data(), blk.size(), PDB_CRC_MASK_OUTPUT,
+                                         crc.data());
+    if (rc) return rc;
+    for (size_t i = 0; i < hdr_.size(); ++i)
+      for (int k = 0; k < 4; ++k) buf_[hdr_[i] + k] = static_cast<char>((crc[i] >> (8 * k)) & 0xff);
+    return 0;
+  }
+
+  const std::string& bytes() const { return buf_; }
+  size_t num_physical_records() const { return hdr_.size(); }
+
+ private:
+  uint64_t base_;
+  std::string buf_;
+  std::vector<uint64_t> hdr_;
+  std::vector<uint32_t> len_;
+};
 
 }  // namespace log
 }  // namespace pdb

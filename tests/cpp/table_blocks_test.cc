@@ -167,6 +167,12 @@ static void VerifyReferenceLogs(const std::string& dir) {
     size_t logical = 0;
     for (const auto& r : recs) logical += r.type == pdb::log::kFullType || r.type == pdb::log::kLastType;
     EXPECT(logical == lg.logical && ok.size() == recs.size());
+    // round trip: logical records -> the group-commit writer -> one sealing batch == the file
+    std::vector<std::string> payloads;
+    EXPECT(pdb::log::AssembleRecords(img.data(), recs, ok, &payloads) == 0 && payloads.size() == lg.logical);
+    pdb::log::BatchWriter w;
+    for (const auto& pl : payloads) w.AddRecord(pl.data(), pl.size());
+    EXPECT(w.num_physical_records() == recs.size() && w.Seal() == 0 && w.bytes() == img);
     for (size_t k = 0; k < recs.size(); k += (recs.size() + 4) / 5) {
       std::string bad = img;
       if (recs[k].length) {
