@@ -63,6 +63,7 @@ typedef struct pdb_block_handle {
 #define PDB_CRC_SIZE_4K 0x8u /* most blocks 4096..4352 B: sstable data blocks (contents || type) */
 #define PDB_CRC_SIZE_256 0x10u /* most blocks 1..256 B: small WAL / MANIFEST records */
 #define PDB_CRC_SIZE_512 0x20u /* most blocks 257..512 B: WAL records of ~400-B values */
+#define PDB_CRC_SIZE_1023 0x40u /* most blocks 513..1023 B: WAL records of ~500..990-B values */
 
 /* error codes */
 #define PDB_OK 0

@@ -351,7 +351,7 @@ int host_desc(const uint8_t* base, uint64_t base_len, const pdb_blk* blk, uint64
   if (!base || !blk) return fail(PDB_EINVAL, "null argument");
   std::vector<HostGroup> groups;
   HostGroup g{0, 0, UINT64_MAX, 0};
-  uint64_t n1k = 0, n4k = 0, n256 = 0, n512 = 0;  // size classes of the sized kernels
+  uint64_t n1k = 0, n4k = 0, n256 = 0, n512 = 0, n1023 = 0;  // size classes of the sized kernels
   for (uint64_t i = 0; i < nblk; ++i) {
     if (blk[i].off > base_len || blk[i].len > base_len - blk[i].off)
       return fail(PDB_ERANGE, "block " + std::to_string(i) + " exceeds base_len");
@@ -359,6 +359,7 @@ int host_desc(const uint8_t* base, uint64_t base_len, const pdb_blk* blk, uint64
     n4k += blk[i].len - 4096u <= 256u;
     n256 += blk[i].len - 1u <= 255u;
     n512 += blk[i].len - 257u <= 255u;
+    n1023 += blk[i].len - 513u <= 510u;
     if (blk[i].len) {
       const uint64_t lo = std::min(g.lo, blk[i].off & ~static_cast<uint64_t>(15));
       const uint64_t hi = std::max(g.hi, blk[i].off + blk[i].len);
@@ -375,11 +376,12 @@ int host_desc(const uint8_t* base, uint64_t base_len, const pdb_blk* blk, uint64
   groups.push_back(g);
   // host-visible lengths pick the kernel: mostly WAL-record or sstable-block sized -> the sized
   // kernels (same results; the hint only changes speed)
-  if (!(flags & (PDB_CRC_USE_INIT | PDB_CRC_SIZE_1K | PDB_CRC_SIZE_4K | PDB_CRC_SIZE_256 | PDB_CRC_SIZE_512))) {
+  if (!(flags & (PDB_CRC_USE_INIT | PDB_CRC_SIZE_1K | PDB_CRC_SIZE_4K | PDB_CRC_SIZE_256 | PDB_CRC_SIZE_512 | PDB_CRC_SIZE_1023))) {
     if (4 * n1k >= 3 * nblk) flags |= PDB_CRC_SIZE_1K;
     else if (4 * n4k >= 3 * nblk) flags |= PDB_CRC_SIZE_4K;
     else if (4 * n256 >= 3 * nblk) flags |= PDB_CRC_SIZE_256;
     else if (4 * (n256 + n512) >= 3 * nblk) flags |= PDB_CRC_SIZE_512;  // the 17-group window takes 1..512 B
+    else if (4 * (n256 + n512 + n1023) >= 3 * nblk) flags |= PDB_CRC_SIZE_1023;  // 33 groups: 1..1024 B
   }
   // lo keeps the source's 16-B phase so the kernels' fast loads stay aligned
   size_t need = 0;

@@ -1908,8 +1908,8 @@ template <class Src, class Sink, uint32_t NG, uint32_t kWpw = kWavesPerWg, uint3
 __device__ __forceinline__ void lanerec_window(const uint32_t* __restrict__ tabs, Src src, uint64_t nblk,
                                                Sink sink) {
   constexpr uint32_t NA = (NG + 1) / 2, NB = NG - NA, MAXN = 32u * (NG - 1);
-  constexpr int kSlotB = NB == 4 ? 3 : (NB == 8 ? 4 : -1);
-  static_assert(kSlotB >= 0, "chain B must span 128 or 256 B");
+  constexpr int kSlotB = NB == 4 ? 3 : (NB == 8 ? 4 : (NB == 16 ? 5 : -1));
+  static_assert(kSlotB >= 0, "chain B must span 128, 256 or 512 B");
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
   char* lds = reinterpret_cast<char*>(lds_words);
   stage_tables<PDB_CAT_TREE16, PDB_CAT_S1024>(lds, tabs);  // slots 0..5 = 16..512 (3 = 128), 6 = 1024
@@ -2181,6 +2181,14 @@ template <class Src, class Sink, uint32_t NG, uint32_t kWg>
 __global__ __launch_bounds__(kWg) void crc_lanerec_pf_kernel(const uint32_t* __restrict__ tabs, Src src,
                                                              uint64_t nblk, Sink sink) {
   lanerec_window<Src, Sink, NG, kWg / 64, NG == 17 ? 4 : 2, true>(tabs, src, nblk, sink);
+}
+
+// Records of 513..1024 B (PDB_CRC_SIZE_1023; fixed strides of 513..1023 B): a 33-group (1056-B)
+// window, 8 chains, 256 threads (one wave per SIMD: the 66 x 16-B window lives in VGPRs + AGPRs)
+template <class Src, class Sink>
+__global__ __launch_bounds__(256) void crc_lanerec33_kernel(const uint32_t* __restrict__ tabs, Src src,
+                                                            uint64_t nblk, Sink sink) {
+  lanerec_window<Src, Sink, 33, 4, 8>(tabs, src, nblk, sink);
 }
 
 uint32_t grid_wg(const LaunchGeom& g, uint64_t nblk, uint32_t wg) {

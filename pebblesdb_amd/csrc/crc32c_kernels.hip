@@ -163,7 +163,7 @@ hipError_t launch_fixed(const LaunchGeom& g, const uint32_t* d_tables, const uin
                          OutSink{out, flags});
       return hipGetLastError();
     }
-    if (src.init_raw == 0xFFFFFFFFu && (len - 1024u <= 128u || len - 1u <= 511u)) {
+    if (src.init_raw == 0xFFFFFFFFu && (len - 1024u <= 128u || len - 1u <= 1022u)) {
       // the same size classes as the descriptor hints: 1-KiB records (1024..1152 B) and records
       // of 1..256 B (tests/test_sst4k.py: fixed strides at every alignment)
       if (len >= 1024u)
@@ -172,6 +172,9 @@ hipError_t launch_fixed(const LaunchGeom& g, const uint32_t* d_tables, const uin
       else if (len <= 256u)  // one lane per record (profiles/r01_ab_lanerec.json)
         hipLaunchKernelGGL((crc_lanerec9_kernel<FixedSrc, OutSink>), dim3(grid_for(g, (nblk + 63) / 64)), block, 0,
                            s, d_tables, src, nblk, OutSink{out, flags});
+      else if (len > 512u)  // 513..1023 B: the 33-group window
+        hipLaunchKernelGGL((crc_lanerec33_kernel<FixedSrc, OutSink>), dim3(grid_wg(g, nblk, 256)), dim3(256), 0, s,
+                           d_tables, src, nblk, OutSink{out, flags});
       else  // 257..512 B: the 17-group window
         hipLaunchKernelGGL((crc_lanerec17_kernel<FixedSrc, OutSink>), dim3(grid17(g, nblk)), dim3(kThreads17), 0,
                            s, d_tables, src, nblk, OutSink{out, flags});
@@ -222,7 +225,7 @@ hipError_t launch_desc(const LaunchGeom& g, const uint32_t* d_tables, const uint
   const DescSrc src{base, blk, flags};
   // size-class hints (Value() seeds only): the sized kernels (exact 1-/4-KiB body + batched
   // prefix; other lengths take their slow path in the same launch)
-  if (!(flags & PDB_CRC_USE_INIT) && (flags & (PDB_CRC_SIZE_1K | PDB_CRC_SIZE_4K | PDB_CRC_SIZE_256 | PDB_CRC_SIZE_512)) &&
+  if (!(flags & PDB_CRC_USE_INIT) && (flags & (PDB_CRC_SIZE_1K | PDB_CRC_SIZE_4K | PDB_CRC_SIZE_256 | PDB_CRC_SIZE_512 | PDB_CRC_SIZE_1023)) &&
       g_fast_variant != 40) {
     const bool k1 = flags & PDB_CRC_SIZE_1K;
     if (!k1 && !(flags & PDB_CRC_SIZE_4K)) {
@@ -231,6 +234,19 @@ hipError_t launch_desc(const LaunchGeom& g, const uint32_t* d_tables, const uint
       // crc_rec256_kernel, A/B variant 53: profiles/r01_ab_lanerec.json); other lengths take the
       // whole-wave slow path in the same launch
       const dim3 lgrid(grid_for(g, (nblk + 63) / 64));
+      if (!(flags & (PDB_CRC_SIZE_256 | PDB_CRC_SIZE_512)) && g_fast_variant != 40) {
+        // 513..1023-B class: the 33-group (1056-B) window, 8 chains, 256-thread workgroups (one wave
+        // per SIMD; the window spills into AGPRs, not scratch): 1.33x the generic kernel on 700-B
+        // records, 1.03-1.07x on uniform 513..1024 B (profiles/r01_ab_rec1023.json)
+        const dim3 g33(grid_wg(g, nblk, 256));
+        if (mode == kModeOut)
+          hipLaunchKernelGGL((crc_lanerec33_kernel<DescSrc, OutSink>), g33, dim3(256), 0, s, d_tables, src, nblk,
+                             OutSink{out, flags});
+        else
+          hipLaunchKernelGGL((crc_lanerec33_kernel<DescSrc, VerifySink>), g33, dim3(256), 0, s, d_tables, src, nblk,
+                             VerifySink{expected, ok, nbad, flags});
+        return hipGetLastError();
+      }
       if (!(flags & PDB_CRC_SIZE_256)) {
         // 257..512-B class: the same lane-per-record design on a 17-group (544-B) window, chains
         // of 9 + 8 groups; records of 1..512 B all take the fast path

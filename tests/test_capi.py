@@ -47,7 +47,7 @@ def test_flag_constants_match_the_python_mirror():
     """Every PDB_CRC_* flag in the header has the same value in pebblesdb_amd.crc32c."""
     src = open(HEADER).read()
     flags = {k: int(v, 16) for k, v in re.findall(r"#define PDB_CRC_(\w+) (0x[0-9a-fA-F]+)u", src)}
-    assert {"MASK_OUTPUT", "USE_INIT", "SIZE_1K", "SIZE_4K", "SIZE_256", "SIZE_512"} <= set(flags)
+    assert {"MASK_OUTPUT", "USE_INIT", "SIZE_1K", "SIZE_4K", "SIZE_256", "SIZE_512", "SIZE_1023"} <= set(flags)
     for k, v in flags.items():
         assert getattr(crc32c, k) == v, k
     assert len(set(flags.values())) == len(flags)  # distinct bits

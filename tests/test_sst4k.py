@@ -201,7 +201,7 @@ def test_new_path_matches_previous_kernel(crc):
 # ---- descriptor batches with a size-class hint: crc_sst1k_kernel / crc_sst4k_kernel<DescSrc> ----
 EDGE_1K = [0, 1, 2, 3, 4, 15, 16, 17, 100, 255, 256, 257, 1000, 1023, 1024, 1025, 1026, 1027, 1039, 1040,
            1041, 1055, 1056, 1100, 1136, 1137, 1151, 1152, 1153, 1168, 1264, 1265, 1279, 1280, 1281, 1282, 2048,
-           4095, 4096, 4097, 5000, 70000, 288, 289, 400, 431, 480, 511, 512, 513, 544]
+           4095, 4096, 4097, 5000, 70000, 288, 289, 400, 431, 480, 511, 512, 513, 544, 700, 1022]
 
 
 def _desc_case(crc, sizes, seed, gap_max=7):
@@ -216,7 +216,7 @@ def _desc_case(crc, sizes, seed, gap_max=7):
     return base, crc.make_blocks(offs, sizes)
 
 
-@pytest.mark.parametrize("hint", ["1k", "4k", "256", "512"])
+@pytest.mark.parametrize("hint", ["1k", "4k", "256", "512", "1023"])
 def test_size_hint_edge_lengths(crc, oracle_lib, hint):
     """The sized kernels on every fast-range boundary of every class and slow lengths either
     side, each repeated at 8 alignments, masked and unmasked, batch and verify."""
@@ -290,7 +290,7 @@ def test_sized_kernels_match_generic_kernel(crc):
     for v in (0, 40, 41, 50, 51, 52, 53):
         lib().pdb_diag_set_variant(v)
         try:
-            res.append([crc.batch(d_base, d_blk, size_hint=h).cpu().numpy() for h in ("1k", "4k", "256", "512")])
+            res.append([crc.batch(d_base, d_blk, size_hint=h).cpu().numpy() for h in ("1k", "4k", "256", "512", "1023")])
         finally:
             lib().pdb_diag_set_variant(0)
     for other in res[1:]:
@@ -365,7 +365,8 @@ def test_sst_crc_device_matches_seal(crc, oracle_lib):
     assert (d_img.cpu().numpy() == img).all()  # nothing written into the image
 
 
-@pytest.mark.parametrize("length", [1, 2, 3, 15, 16, 17, 100, 131, 255, 256, 257, 288, 431, 511, 512, 513, 1024, 1025,
+@pytest.mark.parametrize("length", [1, 2, 3, 15, 16, 17, 100, 131, 255, 256, 257, 288, 431, 511, 512, 513, 700, 1023,
+                                    1024, 1025,
                                     1056, 1151, 1152])
 def test_fixed_stride_small_classes(crc, oracle_lib, length):
     """pdb_crc32c_batch_device_fixed with len in the 1..256, 257..512 and 1024..1152 classes (the record
@@ -385,6 +386,32 @@ def test_fixed_stride_small_classes(crc, oracle_lib, length):
                 exp = oracle_lib.batch(host, blk, flags=(1 if masked else 0) | (2 if init is not None else 0),
                                        nthreads=8)
                 assert (got == exp).all(), (shift, stride, masked, init)
+
+
+@pytest.mark.parametrize("seed", [95, 96])
+def test_lane_per_record_1023_kernel(crc, oracle_lib, seed):
+    """crc_lanerec33_kernel (the 513..1023-B class, 256-thread workgroups, window in VGPRs + AGPRs):
+    30 001 records of 1..1024 B at any alignment, back to back or with gaps, 0- and > 1024-B ones on
+    the slow path; batch and verify; the host entry picks the class from the lengths."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    sizes = rng.integers(513, 1024, size=30_001)
+    sizes[1::4] = rng.integers(1, 1025, size=len(sizes[1::4]))
+    sizes[::997] = 0
+    sizes[5::1009] = rng.integers(1025, 9000, size=len(sizes[5::1009]))
+    base, blk = _desc_case(crc, sizes, seed, gap_max=0 if seed == 95 else 9)
+    d_base, d_blk = torch.from_numpy(base).cuda(), crc.blocks_to_device(blk)
+    for masked in (False, True):
+        got = crc.batch(d_base, d_blk, masked=masked, size_hint="1023").cpu().numpy().view(np.uint32)
+        exp = oracle_lib.batch(base, blk, flags=1 if masked else 0, nthreads=8)
+        bad = np.nonzero(got != exp)[0]
+        assert bad.size == 0, (masked, bad.size, int(blk["len"][bad[0]]), int(blk["off"][bad[0]]))
+    wrong = exp.copy()
+    flip = np.arange(3, len(exp), 7)
+    wrong[flip] ^= 0x100
+    ok, nbad = crc.verify(d_base, d_blk, torch.from_numpy(wrong.view(np.int32)).cuda(), size_hint="1023")
+    okh = ok.cpu().numpy()
+    assert int(nbad.item()) == len(flip) and (okh == 0).sum() == len(flip) and (okh[flip] == 0).all()
+    assert (np.asarray(crc.batch_host(base, blk, masked=True)).view(np.uint32) == exp).all()
 
 
 @pytest.mark.parametrize("seed", [93, 94])

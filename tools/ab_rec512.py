@@ -44,9 +44,14 @@ cases = {
     "fixed_512": np.full(total // 512, 512),
     "small_fixed_131": np.full(total // 262, 131),
     "small_uniform_1_256": rng.integers(1, 257, size=total // 258),
+    "big_fixed_700": np.full(total // 700, 700),
+    "big_uniform_513_1024": rng.integers(513, 1025, size=total // 770),
 }
 res = {}
+only = os.environ.get("AB_CASES")
 for name, sizes in cases.items():
+    if only and not any(name.startswith(o) for o in only.split(",")):
+        continue
     offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]) + 3
     d_blk = crc32c.blocks_to_device(crc32c.make_blocks(offs, sizes))
     out = torch.empty(len(sizes), dtype=torch.int32, device="cuda")
@@ -55,6 +60,9 @@ for name, sizes in cases.items():
     ref = None
     tags = ((("lanerec9", "256", 0), ("lanerec9_prefetch512", "256", 55), ("quadrec5", "256", 57))
             if name.startswith("small") else
+            (("generic", None, 40), ("lanerec33", "1023", 0), 
+             ("lanerec17_slow", "512", 0))
+            if name.startswith("big") else
             (("lanerec17", "512", 0), ("lanerec17_2chains", "512", 54), ("lanerec17_prefetch256", "512", 56),
              ("quadrec9", "512", 58),
              ("generic", None, 40), ("lanerec9_slow", "256", 0)))
