@@ -91,7 +91,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from pebblesdb_amd import crc32c
+    from pebblesdb_amd import crc32c, diag
     from pebblesdb_amd.shard import scatter_block_ranges
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -123,7 +123,7 @@ def main():
         L = stride = 4096
         nblk = hi - lo
         data = torch.empty(nblk * stride, dtype=torch.uint8, device=dev)
-        crc32c.fill_splitmix(data, 301, byte_offset=lo * stride)
+        diag.fill_splitmix(data, 301, byte_offset=lo * stride)
         algo_bytes_per_blk = L + 4  # L read + 4 B CRC written
         hashed = nblk * L
         out = torch.empty(nblk, dtype=torch.int32, device=dev)
@@ -138,7 +138,7 @@ def main():
         L, stride = 4097, 4101
         nblk = hi - lo
         data = torch.empty(nblk * stride, dtype=torch.uint8, device=dev)
-        crc32c.fill_splitmix(data, 301, byte_offset=lo * stride)
+        diag.fill_splitmix(data, 301, byte_offset=lo * stride)
         algo_bytes_per_blk = L + 4
         hashed = nblk * L
         out = torch.empty(nblk, dtype=torch.int32, device=dev)
@@ -160,7 +160,7 @@ def main():
         offs = np.concatenate([[0], np.cumsum(sizes + 5)[:-1]])
         total = int(offs[-1] + sizes[-1] + 5)
         data = torch.empty(total, dtype=torch.uint8, device=dev)
-        crc32c.fill_splitmix(data, 301 + rank)
+        diag.fill_splitmix(data, 301 + rank)
         data[torch.from_numpy(offs + sizes).to(dev)] = 0  # kNoCompression type bytes
         h = np.zeros(nblk, dtype=crc32c.HANDLE_DTYPE)
         h["offset"], h["size"] = offs, sizes
@@ -204,7 +204,7 @@ def main():
         nblk = len(offs)
         total = int(offs[-1] + lens[-1])
         data = torch.empty(total, dtype=torch.uint8, device=dev)
-        crc32c.fill_splitmix(data, 305 + rank)
+        diag.fill_splitmix(data, 305 + rank)
         d_blk = crc32c.blocks_to_device(crc32c.make_blocks(offs, lens), dev)
         L = stride = None
         hashed = int(lens.sum())
@@ -228,7 +228,7 @@ def main():
         offs = np.concatenate([[0], np.cumsum(sizes)[:-1]])
         total = int(sizes.sum())
         data = torch.empty(total, dtype=torch.uint8, device=dev)
-        crc32c.fill_splitmix(data, 303 + rank)
+        diag.fill_splitmix(data, 303 + rank)
         d_blk = crc32c.blocks_to_device(crc32c.make_blocks(offs, sizes), dev)
         nblk = n
         L = stride = None
@@ -301,7 +301,7 @@ def main():
     extra = {}
     if rank == 0:
         if args.diag:
-            extra["diag"] = diag(crc32c, torch, dev, data, stream)
+            extra["diag"] = read_ceiling(torch, dev, data, stream)
         # the copy-inclusive rate is a one-GPU figure (like the CPU baseline): multi-rank runs skip it,
         # so no rank sits in the process-group teardown while rank 0 copies for seconds
         if not args.no_copy_inclusive and world == 1 and args.workload in ("c2", "sstable"):
@@ -362,19 +362,19 @@ def main():
         dist.destroy_process_group()
 
 
-def diag(crc32c, torch, dev, data, stream):
+def read_ceiling(torch, dev, data, stream):
     """Achievable read bandwidth on this box: a coalesced 16-B/lane stream and the exact load
     pattern of the 4-KiB fast path with no CRC work (read_pattern4k variant 21: 1-KiB-contiguous
     nt load instructions, 4 blocks per wave between workgroup barriers -- also the FETCH_SIZE
     calibration kernel of tools/pmc_traffic.py)."""
-    from pebblesdb_amd._native import check, lib
+    from pebblesdb_amd import diag
 
     nbytes = data.numel()
     o = torch.zeros(1, dtype=torch.int32, device=dev)
     res = {}
     for name, fn in (
-        ("read_stream", lambda: check(lib().pdb_diag_read_stream(data.data_ptr(), nbytes, o.data_ptr(), stream.cuda_stream))),
-        ("read_pattern4k", lambda: check(lib().pdb_diag_read_pattern4k(data.data_ptr(), nbytes // 4096, 21, o.data_ptr(), stream.cuda_stream))),
+        ("read_stream", lambda: diag.read_stream(data, nbytes, o, stream)),
+        ("read_pattern4k", lambda: diag.read_pattern4k(data, nbytes // 4096, 21, o, stream)),
     ):
         for _ in range(3):
             fn()

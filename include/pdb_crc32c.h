@@ -27,6 +27,16 @@
  *   - Per-block length in batches is < 2^32 bytes (the reference narrows to uint32_t:
  *     util/crc32c.cc:19-23,589); a single span (pdb_crc32c_extend*) may be longer.
  *   - Thread-safe: host entry points serialise per device; device entry points are pure launches.
+ *     The library has no mutable global switches: every result depends only on the arguments.
+ *   - Device-resident batches may read a few bytes outside a block: up to 15 bytes before its first
+ *     byte and up to 3 bytes past its last one, never outside the 4-B-aligned dwords and 16-B lines
+ *     that hold the block's bytes.  A buffer handed to a device entry point must therefore stay
+ *     readable to the 16-B boundaries around every block (any hipMalloc'd or torch allocation
+ *     does); the bytes outside a block never affect its CRC.
+ *   - Host batches stage at most 256 MiB of span per device copy (PDB_HOST_CHUNK_BYTES, read once
+ *     per process, overrides it); the copies of one group overlap the kernel of the previous one.
+ *   - Bench / test infrastructure (synthetic input, A/B kernel variants, roofline calibration)
+ *     lives in a separate library, include/pdb_crc32c_diag.h; nothing here depends on it.
  */
 #ifndef PDB_CRC32C_H_
 #define PDB_CRC32C_H_
@@ -139,28 +149,6 @@ int64_t pdb_sst_verify_host(const void* buf, uint64_t buf_len, const pdb_block_h
                             uint8_t* ok);
 int pdb_sst_verify_device(const void* d_buf, uint64_t buf_len, const pdb_block_handle* d_h,
                           uint64_t n, uint8_t* d_ok, uint32_t* d_nbad, void* stream);
-
-/* ---- diagnostics (roofline calibration; not part of the reference interface) ---------------- */
-/* Streams nbytes from d_base with coalesced 16-B loads and XOR-folds them into d_out[0..grid). */
-int pdb_diag_read_stream(const void* d_base, uint64_t nbytes, uint32_t* d_out, void* stream);
-/* 4-KiB block load patterns with trivial compute (variant 0 = the fast path's loads: 64 B
- * contiguous per lane, one block in flight per wave; other variants: see crc32c_kernels.hip). */
-int pdb_diag_read_pattern4k(const void* d_base, uint64_t nblk, int variant, uint32_t* d_out,
-                            void* stream);
-/* Fill d_dst[0..nbytes) with the splitmix64 synthetic stream (seed, byte_offset). */
-int pdb_fill_splitmix_device(void* d_dst, uint64_t nbytes, uint64_t seed, uint64_t byte_offset,
-                             void* stream);
-/* Park the scalar Extend server and read the exit statistics of its last instance: out4 =
- * {requests, ticks (10 ns) from seeing a request to answering it, polls, lifetime ticks}.
- * Returns 1 if its request box is device memory, 0 if pinned host memory, or a negative error. */
-int pdb_diag_server_stats(uint64_t* out4);
-/* Set the host batches' staging group span in bytes (0 = leave); returns the previous value. */
-uint64_t pdb_diag_set_host_chunk(uint64_t bytes);
-/* Select a 4-KiB fast-path kernel variant (A/B experiments only; 0 = shipped default).
- * Returns the previous selection. */
-int pdb_diag_set_variant(int v);
-/* Launch geometry actually used (for bench reporting): workgroups and threads per workgroup. */
-int pdb_crc32c_launch_geometry(int device, uint32_t* grid, uint32_t* block, uint32_t* lds_bytes);
 
 #ifdef __cplusplus
 } /* extern "C" */

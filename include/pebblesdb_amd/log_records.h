@@ -6,10 +6,11 @@
 // than the 7-byte header is zero-filled (log_writer.cc:90-97).  The CRC covers type || payload,
 // which are contiguous in the file (log_writer.cc:111-121, log_reader.cc:235-249).
 //
-// ParsePhysicalRecords walks a log image like log::Reader::ReadPhysicalRecord
-// (log_reader.cc:185-260) without checking CRCs; VerifyLog then checks every record with ONE
-// pdb_crc32c_verify_host call (recovery, repair, MANIFEST replay) instead of one crc32c::Value per
-// record.  Header-only, C++11, links against libpdb_crc32c.so.
+// WalkLog walks a log image like log::Reader::ReadPhysicalRecord (log_reader.cc:181-263) without
+// checking CRCs; VerifyLog / ReplayLog then check every record with ONE pdb_crc32c_verify_host
+// call (recovery, repair, MANIFEST replay) instead of one crc32c::Value per record, and ReplayLog
+// reproduces log::Reader::ReadRecord's output (records + corruption reports) exactly.
+// Header-only, C++11, links against libpdb_crc32c.so.
 #ifndef PEBBLESDB_AMD_LOG_RECORDS_H_
 #define PEBBLESDB_AMD_LOG_RECORDS_H_
 
@@ -33,45 +34,77 @@ struct PhysicalRecord {
   uint8_t type;
   uint32_t stored;  // masked crc from the header
   uint64_t payload_offset() const { return offset + kHeaderSize; }
+  uint64_t block() const { return offset / kBlockSize; }
 };
 
-// Walk the blocks: zero-filled block tails and preallocated zero records are skipped; a record
-// whose length runs past its block or the image ends the walk (a truncated tail, which the
-// reference reader reports as kEof / a dropped fragment).  Returns the number of bytes walked.
-inline uint64_t ParsePhysicalRecords(const char* image, uint64_t n, std::vector<PhysicalRecord>* out) {
+// One physical item log::Reader::ReadPhysicalRecord (log_reader.cc:181-263) meets: a record, or
+// the rest of a block it drops without a CRC check -- a record whose length runs past a full
+// block ("bad record length", log_reader.cc:214-220) or a zero-filled preallocated region (type 0,
+// length 0, dropped silently, log_reader.cc:227-233).
+struct LogItem {
+  enum Kind { kRecord = 0, kBadLength = 1, kZeroRegion = 2 };
+  Kind kind;
+  PhysicalRecord rec;   // kRecord: the record; otherwise rec.offset = where the drop starts
+  uint64_t drop_bytes;  // bytes to the end of the block (drops; for a record, from its header)
+};
+
+// The walk trusts every length (CRCs are checked afterwards, in one batch).  The file is read in
+// 32-KiB blocks and only the last, short block is "eof": a record running past it, or a truncated
+// header there, ends the walk without a report (a writer that died mid-record).  A block tail
+// shorter than a header is skipped (the writer's zero trailer, log_writer.cc:67-76).
+inline void WalkLog(const char* image, uint64_t n, std::vector<LogItem>* out) {
   const unsigned char* p = reinterpret_cast<const unsigned char*>(image);
   out->clear();
-  uint64_t pos = 0;
-  while (pos < n) {
-    const uint64_t left_in_block = kBlockSize - (pos % kBlockSize);
-    if (left_in_block < kHeaderSize) {  // trailer
-      pos += left_in_block;
-      continue;
+  for (uint64_t bstart = 0; bstart < n; bstart += kBlockSize) {
+    const uint64_t bend = bstart + kBlockSize < n ? bstart + kBlockSize : n;
+    const bool eof = bend - bstart < kBlockSize;
+    uint64_t pos = bstart;
+    while (bend - pos >= kHeaderSize) {
+      LogItem it;
+      it.rec.offset = pos;
+      it.rec.length = static_cast<uint32_t>(p[pos + 4]) | (static_cast<uint32_t>(p[pos + 5]) << 8);
+      it.rec.type = p[pos + 6];
+      it.rec.stored = static_cast<uint32_t>(p[pos]) | (static_cast<uint32_t>(p[pos + 1]) << 8) |
+                      (static_cast<uint32_t>(p[pos + 2]) << 16) | (static_cast<uint32_t>(p[pos + 3]) << 24);
+      it.drop_bytes = bend - pos;
+      if (kHeaderSize + it.rec.length > bend - pos) {
+        if (eof) return;  // kEof
+        it.kind = LogItem::kBadLength;
+        out->push_back(it);
+        break;
+      }
+      if (it.rec.type == kZeroType && it.rec.length == 0) {
+        it.kind = LogItem::kZeroRegion;
+        out->push_back(it);
+        break;
+      }
+      it.kind = LogItem::kRecord;
+      out->push_back(it);
+      pos += kHeaderSize + it.rec.length;
     }
-    if (pos + kHeaderSize > n) break;
-    const uint32_t stored = static_cast<uint32_t>(p[pos]) | (static_cast<uint32_t>(p[pos + 1]) << 8) |
-                            (static_cast<uint32_t>(p[pos + 2]) << 16) | (static_cast<uint32_t>(p[pos + 3]) << 24);
-    const uint32_t length = static_cast<uint32_t>(p[pos + 4]) | (static_cast<uint32_t>(p[pos + 5]) << 8);
-    const uint8_t type = p[pos + 6];
-    if (type == kZeroType && length == 0) {  // preallocated region (log_reader.cc:226-233)
-      pos += left_in_block;
-      continue;
-    }
-    const uint64_t end = pos + kHeaderSize + length;
-    if (end > n || end > pos - (pos % kBlockSize) + kBlockSize) break;
-    PhysicalRecord r;
-    r.offset = pos;
-    r.length = length;
-    r.type = type;
-    r.stored = stored;
-    out->push_back(r);
-    pos = end;
+    if (eof) return;  // a short tail in the last block is a truncated header
   }
-  return pos < n ? pos : n;
 }
 
-// ok[i] = 1 iff record i's stored CRC == Mask(crc32c(type || payload)).  Returns the number of
-// mismatching records (each one log::Reader drops with "checksum mismatch") or a negative PDB_E*.
+// Every physical record of the walk, without checking CRCs.  Returns the bytes walked.
+inline uint64_t ParsePhysicalRecords(const char* image, uint64_t n, std::vector<PhysicalRecord>* out) {
+  std::vector<LogItem> items;
+  WalkLog(image, n, &items);
+  out->clear();
+  uint64_t walked = 0;
+  for (const LogItem& it : items) {
+    if (it.kind == LogItem::kRecord) {
+      out->push_back(it.rec);
+      walked = it.rec.offset + kHeaderSize + it.rec.length;
+    } else {
+      walked = it.rec.offset + it.drop_bytes;
+    }
+  }
+  return walked;
+}
+
+// ok[i] = 1 iff record i's stored CRC == Mask(crc32c(type || payload)), every record in ONE
+// pdb_crc32c_verify_host call.  Returns the number of mismatching records or a negative PDB_E*.
 inline int64_t VerifyRecords(const char* image, uint64_t n, const std::vector<PhysicalRecord>& recs,
                              std::vector<uint8_t>* ok) {
   ok->assign(recs.size(), 0);
@@ -88,54 +121,145 @@ inline int64_t VerifyRecords(const char* image, uint64_t n, const std::vector<Ph
                                 ok->data());
 }
 
-inline int64_t VerifyLog(const char* image, uint64_t n, std::vector<PhysicalRecord>* recs,
-                         std::vector<uint8_t>* ok) {
-  ParsePhysicalRecords(image, n, recs);
-  return VerifyRecords(image, n, *recs, ok);
-}
-
 inline const char* ChecksumMismatchMessage() { return "checksum mismatch"; }  // log_reader.cc:246
 
-// Logical records (Full, or First Middle* Last) from verified physical records, in the spirit of
-// log::Reader::ReadRecord (log_reader.cc:62-183): a record with ok[i] == 0 is dropped together with
-// any fragment being assembled.  Returns the bytes dropped (headers + payloads).
-inline uint64_t AssembleRecords(const char* image, const std::vector<PhysicalRecord>& recs,
-                                const std::vector<uint8_t>& ok, std::vector<std::string>* out) {
+struct LogicalRecord {
+  uint64_t offset;   // log::Reader::LastRecordOffset() after the record
+  std::string data;  // the payload (fragments joined)
+};
+
+struct CorruptionReport {
+  uint64_t bytes;      // what the Reporter is told
+  std::string reason;  // "Corruption: <message>" (Status::ToString)
+};
+
+// What log::Reader::ReadRecord (log_reader.cc:59-164; checksums on, initial offset 0) delivers from
+// the image: the logical records and the corruption reports.  ok[] are the batched CRC verdicts
+// of the walk's records (in walk order).  A record failing its check drops the rest of its block --
+// the reader no longer trusts the length -- so records walked after it in that block are
+// discarded, never replayed (log_reader.cc:240-247).  Pinned by tests/golden/log/corruptions.json.
+inline void ReplayItems(const char* image, uint64_t n, const std::vector<LogItem>& items, const std::vector<uint8_t>& ok,
+                        std::vector<LogicalRecord>* out, std::vector<CorruptionReport>* reports) {
   out->clear();
-  uint64_t dropped = 0;
+  reports->clear();
+  std::string scratch;
   bool in_frag = false;
-  std::string frag;
-  for (size_t i = 0; i < recs.size(); ++i) {
-    const PhysicalRecord& r = recs[i];
-    const char* payload = image + r.payload_offset();
-    const bool good = i < ok.size() && ok[i] &&
-                      (r.type == kFullType || r.type == kFirstType || (in_frag && (r.type == kMiddleType ||
-                                                                                  r.type == kLastType)));
-    if (!good) {
-      dropped += kHeaderSize + r.length + (in_frag ? frag.size() : 0);
+  uint64_t prospective = 0, pos = 0, dead_block = UINT64_MAX;
+  size_t ri = 0;  // index of the next record verdict
+  auto report = [&](uint64_t bytes, const std::string& why) {
+    reports->push_back(CorruptionReport{bytes, "Corruption: " + why});
+  };
+  auto bad_record = [&]() {  // kBadRecord in ReadRecord (log_reader.cc:143-149)
+    if (in_frag) {
+      report(scratch.size(), "error in middle of record");
       in_frag = false;
-      frag.clear();
+      scratch.clear();
+    }
+  };
+  for (const LogItem& it : items) {
+    const bool is_rec = it.kind == LogItem::kRecord;
+    const bool good = is_rec ? (ri < ok.size() && ok[ri] != 0) : false;
+    if (is_rec) ++ri;
+    const uint64_t blk = it.rec.offset / kBlockSize;
+    if (blk == dead_block) continue;
+    const uint64_t bend = it.rec.offset + it.drop_bytes;
+    if (!is_rec) {
+      if (it.kind == LogItem::kBadLength) report(it.drop_bytes, "bad record length");
+      bad_record();
+      pos = bend;
       continue;
     }
-    if (r.type == kFullType) {
-      if (in_frag) dropped += frag.size();  // a First without its Last (log_reader.cc:78-95)
-      in_frag = false;
-      frag.clear();
-      out->push_back(std::string(payload, r.length));
-    } else if (r.type == kFirstType) {
-      if (in_frag) dropped += frag.size();
-      frag.assign(payload, r.length);
-      in_frag = true;
-    } else {
-      frag.append(payload, r.length);
-      if (r.type == kLastType) {
-        out->push_back(frag);
-        frag.clear();
+    const uint64_t phys = pos;
+    if (!good) {
+      report(it.drop_bytes, ChecksumMismatchMessage());
+      dead_block = blk;
+      bad_record();
+      pos = bend;
+      continue;
+    }
+    const PhysicalRecord& r = it.rec;
+    pos = r.offset + kHeaderSize + r.length;
+    const char* frag = image + r.payload_offset();
+    switch (r.type) {
+      case kFullType:
+        if (in_frag && !scratch.empty()) report(scratch.size(), "partial record without end(1)");
+        out->push_back(LogicalRecord{phys, std::string(frag, r.length)});
+        scratch.clear();
         in_frag = false;
-      }
+        break;
+      case kFirstType:
+        if (in_frag && !scratch.empty()) report(scratch.size(), "partial record without end(2)");
+        prospective = phys;
+        scratch.assign(frag, r.length);
+        in_frag = true;
+        break;
+      case kMiddleType:
+        if (!in_frag) report(r.length, "missing start of fragmented record(1)");
+        else scratch.append(frag, r.length);
+        break;
+      case kLastType:
+        if (!in_frag) {
+          report(r.length, "missing start of fragmented record(2)");
+        } else {
+          scratch.append(frag, r.length);
+          out->push_back(LogicalRecord{prospective, scratch});
+          scratch.clear();
+          in_frag = false;
+        }
+        break;
+      default:
+        report(r.length + (in_frag ? scratch.size() : 0), "unknown record type " + std::to_string(r.type));
+        in_frag = false;
+        scratch.clear();
+        break;
     }
   }
-  return dropped + frag.size();
+  (void)n;
+}
+
+// Walk + ONE batched CRC check + replay.  Returns the number of corruption reports (>= 0) or a
+// negative PDB_E* code.
+inline int64_t ReplayLog(const char* image, uint64_t n, std::vector<LogicalRecord>* out,
+                         std::vector<CorruptionReport>* reports) {
+  std::vector<LogItem> items;
+  WalkLog(image, n, &items);
+  std::vector<PhysicalRecord> recs;
+  for (const LogItem& it : items)
+    if (it.kind == LogItem::kRecord) recs.push_back(it.rec);
+  std::vector<uint8_t> ok;
+  const int64_t rc = VerifyRecords(image, n, recs, &ok);
+  if (rc < 0) return rc;
+  ReplayItems(image, n, items, ok, out, reports);
+  return static_cast<int64_t>(reports->size());
+}
+
+// Recovery / repair / MANIFEST check: every record of the log in one GPU batch.  ok[i] per walked
+// record.  Returns the number of reports the reference reader's CRC and length checks make --
+// "checksum mismatch" for the first failing record of a block (the rest of that block is never
+// read) plus "bad record length" drops -- or a negative PDB_E* code.  Fragment-assembly reports
+// (records missing their start / end) are ReplayLog's.
+inline int64_t VerifyLog(const char* image, uint64_t n, std::vector<PhysicalRecord>* recs, std::vector<uint8_t>* ok) {
+  std::vector<LogItem> items;
+  WalkLog(image, n, &items);
+  recs->clear();
+  for (const LogItem& it : items)
+    if (it.kind == LogItem::kRecord) recs->push_back(it.rec);
+  const int64_t rc = VerifyRecords(image, n, *recs, ok);
+  if (rc < 0) return rc;
+  int64_t reports = 0;
+  uint64_t dead_block = UINT64_MAX;
+  size_t ri = 0;
+  for (const LogItem& it : items) {
+    const uint64_t blk = it.rec.offset / kBlockSize;
+    const bool good = it.kind == LogItem::kRecord ? (*ok)[ri++] != 0 : true;
+    if (blk == dead_block) continue;
+    if (it.kind == LogItem::kBadLength) ++reports;
+    if (!good) {
+      ++reports;
+      dead_block = blk;
+    }
+  }
+  return reports;
 }
 
 // Group-commit form of log::Writer (log_writer.cc:28-131): AddRecord fragments and lays out records

@@ -157,7 +157,11 @@ inline bool BlockValues(const char* b, uint64_t n, std::vector<BlockHandle>* han
 
 // Parses the footer, index and metaindex blocks of a table image (uncompressed blocks: the
 // reference's CMake build never links Snappy, port_posix.h:141-156).  False + *err on corruption.
-inline bool ReadTableLayout(const char* image, uint64_t len, TableLayout* t, std::string* err) {
+// verify_checksums: the index and metaindex blocks' CRCs are checked (one small GPU batch) BEFORE
+// their entries are parsed, so a corrupt index is ReadBlock's "block checksum mismatch"
+// (format.cc:96-102), not a parse error or garbage handles.
+inline bool ReadTableLayout(const char* image, uint64_t len, TableLayout* t, std::string* err,
+                            bool verify_checksums = false) {
   if (len < kFooterEncodedLength) return *err = "file is too short to be an sstable", false;
   const char* f = image + len - kFooterEncodedLength;
   uint32_t lo, hi;
@@ -169,6 +173,16 @@ inline bool ReadTableLayout(const char* image, uint64_t len, TableLayout* t, std
   if (!DecodeHandle(&p, f + 2 * kMaxEncodedHandleLength, &t->metaindex) ||
       !DecodeHandle(&p, f + 2 * kMaxEncodedHandleLength, &t->index))
     return *err = "bad block handle", false;
+  if (verify_checksums) {
+    const BlockHandle hs[2] = {t->index, t->metaindex};
+    for (const BlockHandle& h : hs)
+      if (h.offset > len || h.size > len - h.offset || len - h.offset - h.size < kBlockTrailerSize)
+        return *err = "truncated block read", false;  // format.cc:84-87
+    std::vector<uint8_t> ok;
+    const int64_t bad = VerifyBlocks(image, len, hs, 2, &ok);
+    if (bad < 0) return *err = std::string("device error: ") + pdb_last_error(), false;
+    if (bad > 0) return *err = ChecksumMismatchMessage(), false;
+  }
   const BlockHandle* blocks[2] = {&t->index, &t->metaindex};
   std::vector<BlockHandle>* outs[2] = {&t->data, &t->meta};
   for (int k = 0; k < 2; ++k) {
@@ -183,14 +197,15 @@ inline bool ReadTableLayout(const char* image, uint64_t len, TableLayout* t, std
 
 // leveldb-verify for one table image: every block's checksum in one GPU batch.  Returns the
 // number of bad blocks (>= 0), a negative PDB_E* code, or -1000 with *err set when the table's
-// structure (footer / index / metaindex) is corrupt.
+// structure (footer / index / metaindex) is corrupt -- a corrupt index or metaindex block is
+// reported as "block checksum mismatch" before its entries are parsed.
 inline int64_t VerifyTable(const char* image, uint64_t len, TableLayout* layout, std::vector<uint8_t>* ok,
                            std::string* err) {
   TableLayout local;
   TableLayout& t = layout ? *layout : local;
   t = TableLayout();
   std::string e;
-  if (!ReadTableLayout(image, len, &t, err ? err : &e)) return -1000;
+  if (!ReadTableLayout(image, len, &t, err ? err : &e, true)) return -1000;
   const std::vector<BlockHandle> all = t.All();
   return VerifyBlocks(image, len, all.data(), all.size(), ok);
 }

@@ -45,3 +45,11 @@ g++ -O2 -std=c++11 -w \
   -DHAVE_FWRITE_UNLOCKED -DHAVE_FDATASYNC -DHAVE_DECL_FDATASYNC=1 \
   -I"$REF" -I"$REF/include" -o "$HERE/_ref/ref_logwriter" "$HERE/ref_logwriter.cc" $LABS -lpthread
 echo "built $HERE/_ref/ref_logwriter"
+
+# The reference's own log::Reader on an arbitrary (corrupted) log image + oracle/ref_logreader.cc
+# -> oracle/_ref/ref_logreader, used only to generate tests/golden/log/corruptions.json.
+g++ -O2 -std=c++11 -w \
+  -DLEVELDB_PLATFORM_POSIX -DOS_LINUX -DHAVE_FFLUSH_UNLOCKED -DHAVE_FREAD_UNLOCKED \
+  -DHAVE_FWRITE_UNLOCKED -DHAVE_FDATASYNC -DHAVE_DECL_FDATASYNC=1 \
+  -I"$REF" -I"$REF/include" -o "$HERE/_ref/ref_logreader" "$HERE/ref_logreader.cc" $LABS -lpthread
+echo "built $HERE/_ref/ref_logreader"

@@ -58,13 +58,6 @@ SIGNATURES = {
     "pdb_sst_verify_host": (ctypes.c_int64, [_V, _U64, _V, _U64, _V]),
     "pdb_sst_verify_device": (_I, [_V, _U64, _V, _U64, _V, _V, _V]),
     "pdb_sst_crc_device": (_I, [_V, _U64, _V, _U64, _V, _V]),
-    "pdb_diag_server_stats": (_I, [_V]),
-    "pdb_diag_set_host_chunk": (_U64, [_U64]),
-    "pdb_diag_read_stream": (_I, [_V, _U64, _V, _V]),
-    "pdb_diag_read_pattern4k": (_I, [_V, _U64, _I, _V, _V]),
-    "pdb_fill_splitmix_device": (_I, [_V, _U64, _U64, _U64, _V]),
-    "pdb_crc32c_launch_geometry": (_I, [_I, _V, _V, _V]),
-    "pdb_diag_set_variant": (_I, [_I]),
 }
 
 

@@ -1,7 +1,14 @@
-"""Build the in-tree HIP library ``pebblesdb_amd/_lib/libpdb_crc32c.so`` for gfx950.
+"""Build the in-tree HIP libraries for gfx950.
+
+    pebblesdb_amd/_lib/libpdb_crc32c.so       the product: the C-ABI of include/pdb_crc32c.h
+    pebblesdb_amd/_lib/libpdb_crc32c_diag.so  bench / test infrastructure (include/pdb_crc32c_diag.h):
+                                              synthetic input, A/B variants, roofline calibration
 
 Run ``python -m pebblesdb_amd.build`` (or ``__graft_entry__.build()``).  hipcc cross-compiles
-without a GPU; the .so is git-ignored but travels to the GPU box with the repo snapshot.
+without a GPU; the .so files are git-ignored but travel to the GPU box with the repo snapshot.
+Each source compiles once to an object (in parallel); both libraries export only ``pdb_*``
+symbols (csrc/pdb_exports.map), so the diagnostics library's copy of the shared kernels never
+interposes on the product's.
 """
 from __future__ import annotations
 
@@ -9,16 +16,22 @@ import os
 import shutil
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIBDIR = os.path.join(PKG, "_lib")
+OBJDIR = os.path.join(LIBDIR, "obj")
 LIB = os.path.join(LIBDIR, "libpdb_crc32c.so")
+DIAG_LIB = os.path.join(LIBDIR, "libpdb_crc32c_diag.so")
 ARCH = "gfx950"
 
-SOURCES = ["crc32c_kernels.hip", "crc32c_server.hip", "crc32c_variants.hip", "crc32c_capi.cpp", "crc32c_tables.cpp"]
-HEADERS = ["crc32c_math.h", "crc32c_internal.h", "crc32c_device.h"]
+SOURCES = ["crc32c_kernels.hip", "crc32c_server.hip", "crc32c_capi.cpp", "crc32c_tables.cpp"]
+DIAG_SOURCES = ["diag_variants.hip", "diag_capi.cpp", "crc32c_kernels.hip", "crc32c_tables.cpp"]
+HEADERS = ["crc32c_math.h", "crc32c_internal.h", "crc32c_device.h", "diag_device.h", "diag_internal.h"]
+INCLUDES = ["pdb_crc32c.h", "pdb_crc32c_diag.h"]
+EXPORTS = os.path.join(CSRC, "pdb_exports.map")
 
 
 def _hipcc() -> str:
@@ -28,39 +41,54 @@ def _hipcc() -> str:
     raise RuntimeError("hipcc not found: the pebblesdb_amd HIP library cannot be built")
 
 
-def _stale() -> bool:
-    if not os.path.exists(LIB):
+def _deps_mtime() -> float:
+    deps = [os.path.join(CSRC, f) for f in HEADERS] + [os.path.join(ROOT, "include", f) for f in INCLUDES]
+    deps.append(EXPORTS)
+    return max(os.path.getmtime(d) for d in deps if os.path.exists(d))
+
+
+def _obj(src: str) -> str:
+    return os.path.join(OBJDIR, os.path.splitext(src)[0] + ".o")
+
+
+def _stale(target: str, srcs) -> bool:
+    if not os.path.exists(target):
         return True
-    t = os.path.getmtime(LIB)
-    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
-    deps.append(os.path.join(ROOT, "include", "pdb_crc32c.h"))
-    deps.append(os.path.join(ROOT, "include", "pebblesdb_amd", "crc32c.h"))
-    deps.append(os.path.join(ROOT, "include", "pebblesdb_amd", "table_blocks.h"))
-    return any(os.path.exists(d) and os.path.getmtime(d) > t for d in deps)
+    t = os.path.getmtime(target)
+    return _deps_mtime() > t or any(os.path.getmtime(os.path.join(CSRC, s)) > t for s in srcs)
 
 
-def build(force: bool = False, verbose: bool = True) -> str:
-    if not force and not _stale():
-        return LIB
-    os.makedirs(LIBDIR, exist_ok=True)
-    tmp = LIB + ".tmp"
-    cmd = [
-        _hipcc(),
-        f"--offload-arch={ARCH}",
-        "-O3",
-        "-std=c++17",
-        "-fPIC",
-        "-shared",
-        "-Wall",
-        "-Wno-unused-function",
-        f"-I{os.path.join(ROOT, 'include')}",
-        "-o",
-        tmp,
-    ] + [os.path.join(CSRC, f) for f in SOURCES if os.path.exists(os.path.join(CSRC, f))]
+def _compile(src: str, force: bool, verbose: bool) -> str:
+    o = _obj(src)
+    if not force and not _stale(o, [src]):
+        return o
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
+           f"-I{os.path.join(ROOT, 'include')}", "-c", os.path.join(CSRC, src), "-o", o + ".tmp"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd)
-    os.replace(tmp, LIB)
+    os.replace(o + ".tmp", o)
+    return o
+
+
+def _link(target: str, srcs, verbose: bool) -> None:
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", f"-Wl,--version-script={EXPORTS}", "-o",
+           target + ".tmp"] + [_obj(s) for s in srcs]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.check_call(cmd)
+    os.replace(target + ".tmp", target)
+
+
+def build(force: bool = False, verbose: bool = True) -> str:
+    os.makedirs(OBJDIR, exist_ok=True)
+    srcs = sorted(set(SOURCES) | set(DIAG_SOURCES))
+    jobs = max(1, min(len(srcs), int(os.environ.get("MAX_JOBS", "8"))))
+    with ThreadPoolExecutor(jobs) as ex:
+        list(ex.map(lambda s: _compile(s, force, verbose), srcs))
+    for target, lst in ((LIB, SOURCES), (DIAG_LIB, DIAG_SOURCES)):
+        if force or not os.path.exists(target) or any(os.path.getmtime(_obj(s)) > os.path.getmtime(target) for s in lst):
+            _link(target, lst, verbose)
     return LIB
 
 

@@ -41,7 +41,7 @@ HANDLE_DTYPE = np.dtype([("offset", "<u8"), ("size", "<u8")])  # == pdb_block_ha
 __all__ = [
     "extend", "value", "mask", "unmask", "batch_fixed", "batch", "verify", "batch_host", "verify_host",
     "make_blocks", "blocks_to_device", "PdbError", "MASK_OUTPUT", "USE_INIT", "BLK_DTYPE",
-    "HANDLE_DTYPE", "init_device", "launch_geometry", "fill_splitmix", "extend_device",
+    "HANDLE_DTYPE", "init_device", "extend_device",
 ]
 
 
@@ -215,17 +215,3 @@ def extend_device(init_crc: int, d_data, nbytes: int | None = None, stream=None)
     check(lib().pdb_crc32c_extend_device(init_crc & 0xFFFFFFFF, _dev_ptr(d_data), n, _dev_ptr(scratch), words,
                                          _dev_ptr(out), _stream_ptr(stream)))
     return int(out.cpu().numpy().view(np.uint32)[0])
-
-
-def launch_geometry(device: int = -1):
-    g, b, l = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
-    check(lib().pdb_crc32c_launch_geometry(device, ctypes.byref(g), ctypes.byref(b), ctypes.byref(l)))
-    return g.value, b.value, l.value
-
-
-def fill_splitmix(d_dst, seed: int, byte_offset: int = 0, nbytes: int | None = None, stream=None):
-    """Fill a device tensor with the splitmix64 synthetic byte stream (same as the oracle's)."""
-    nb = d_dst.numel() * d_dst.element_size() if nbytes is None else nbytes
-    check(lib().pdb_fill_splitmix_device(_dev_ptr(d_dst), nb, seed & 0xFFFFFFFFFFFFFFFF,
-                                         byte_offset, _stream_ptr(stream)))
-    return d_dst

@@ -37,7 +37,10 @@ struct DevState {
   uint32_t* d_tables = nullptr;
   uint32_t* d_pow2 = nullptr;  // 64 power-of-two shift operators (long-span combine)
   LaunchGeom geom{256, 1024};
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;       // kernels and result copies of the host entry points
+  hipStream_t copy_stream = nullptr;  // host -> device staging copies (overlap the previous group's kernel)
+  hipEvent_t staged[2] = {};          // group in workspace slot k copied in
+  hipEvent_t drained[2] = {};         // group in workspace slot k hashed and its results copied out
   std::mutex mu;  // guards the host-staging workspace below
   uint8_t* d_ws = nullptr;
   size_t ws_cap = 0;
@@ -126,6 +129,13 @@ int get_state(DevState** out) {
                           : strcmp(wait, "poll") == 0 ? kScalarPoll : kScalarServer;
   e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
   if (e != hipSuccess) return hip_fail(e, "hipStreamCreate");
+  e = hipStreamCreateWithFlags(&s->copy_stream, hipStreamNonBlocking);
+  if (e != hipSuccess) return hip_fail(e, "hipStreamCreate(copy)");
+  for (int k = 0; k < 2; ++k) {
+    if ((e = hipEventCreateWithFlags(&s->staged[k], hipEventDisableTiming)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&s->drained[k], hipEventDisableTiming)) != hipSuccess)
+      return hip_fail(e, "hipEventCreate");
+  }
   __atomic_store_n(&g_dev[dev], s.get(), __ATOMIC_RELEASE);
   *out = s.release();
   return PDB_OK;
@@ -141,6 +151,7 @@ hipStream_t pick_stream(DevState* st, void* stream) {
 int ensure_ws(DevState* st, size_t bytes) {
   if (bytes <= st->ws_cap) return PDB_OK;
   if (st->d_ws) {
+    (void)hipStreamSynchronize(st->copy_stream);
     (void)hipStreamSynchronize(st->stream);
     (void)hipFree(st->d_ws);
     st->d_ws = nullptr;
@@ -328,15 +339,48 @@ int server_call(DevState* st, uint32_t init, const uint8_t* data, uint64_t n, ui
   }
 }
 
-// Host batches are staged in groups whose byte span is at most g_host_chunk (a block longer than
-// that forms its own group), so the device workspace stays bounded however large the host batch;
-// groups run back to back on the library's stream (copies and kernels are stream-ordered) and the
-// call synchronises once at the end.  Kernel time is ~1 % of the PCIe copy, so nothing is lost by
-// not overlapping them.
-uint64_t g_host_chunk = 256ull << 20;
+// Host batches are staged in groups whose byte span is at most host_chunk_bytes() (a block longer than
+// that forms its own group), so the device workspace stays bounded however large the host batch.
+// Groups alternate between two workspace slots (SlotPipe): group k's host->device copies run on
+// copy_stream as soon as slot k & 1 is drained, its kernel and result copy on stream once its copies
+// are in -- group k+1's copies overlap group k's kernel and result copy.  One synchronisation at the
+// end.  The copies dominate (the kernel is ~1 % of a PCIe copy of the same bytes).
+uint64_t host_chunk_bytes() {
+  // 256 MiB by default; PDB_HOST_CHUNK_BYTES (read once per process, >= 4 KiB) overrides it for
+  // experiments and for tests that exercise multi-group staging on small buffers
+  static const uint64_t v = [] {
+    const char* e = getenv("PDB_HOST_CHUNK_BYTES");
+    const unsigned long long x = e ? strtoull(e, nullptr, 10) : 0ull;
+    return x >= 4096ull ? static_cast<uint64_t>(x) : (256ull << 20);
+  }();
+  return v;
+}
 
 struct HostGroup {
   uint64_t first, count, lo, hi;
+};
+
+// Two-slot staging pipeline over copy_stream (H2D) and stream (kernel + D2H).  The destructor drains
+// both streams, so an early error return never leaves a copy in flight from host memory that is
+// about to be freed.
+struct SlotPipe {
+  DevState* st;
+  explicit SlotPipe(DevState* s) : st(s) {}
+  ~SlotPipe() {
+    (void)hipStreamSynchronize(st->copy_stream);
+    (void)hipStreamSynchronize(st->stream);
+  }
+  // before group k's copies: slot k & 1 must be drained (group k - 2 done)
+  hipError_t begin_copies(size_t k) const {
+    return k >= 2 ? hipStreamWaitEvent(st->copy_stream, st->drained[k & 1], 0) : hipSuccess;
+  }
+  // after group k's copies: the kernel stream waits for them
+  hipError_t end_copies(size_t k) const {
+    hipError_t e = hipEventRecord(st->staged[k & 1], st->copy_stream);
+    return e != hipSuccess ? e : hipStreamWaitEvent(st->stream, st->staged[k & 1], 0);
+  }
+  // after group k's kernel and result copies: slot k & 1 is free again
+  hipError_t end_group(size_t k) const { return hipEventRecord(st->drained[k & 1], st->stream); }
 };
 
 // Host batch over descriptors: per group, stage [lo, hi) of the host span, the rebased
@@ -363,7 +407,7 @@ int host_desc(const uint8_t* base, uint64_t base_len, const pdb_blk* blk, uint64
     if (blk[i].len) {
       const uint64_t lo = std::min(g.lo, blk[i].off & ~static_cast<uint64_t>(15));
       const uint64_t hi = std::max(g.hi, blk[i].off + blk[i].len);
-      if (g.count && g.lo != UINT64_MAX && hi - lo > g_host_chunk) {
+      if (g.count && g.lo != UINT64_MAX && hi - lo > host_chunk_bytes()) {
         groups.push_back(g);
         g = HostGroup{i, 0, blk[i].off & ~static_cast<uint64_t>(15), blk[i].off + blk[i].len};
       } else {
@@ -395,7 +439,8 @@ int host_desc(const uint8_t* base, uint64_t base_len, const pdb_blk* blk, uint64
   const size_t off_out = align_up(off_desc + max_count * sizeof(pdb_blk), 256);
   const size_t off_exp = align_up(off_out + max_count * sizeof(uint32_t), 256);
   const size_t off_ok = align_up(off_exp + (mode == kModeVerify ? max_count * 4 : 0), 256);
-  const size_t off_nbad = align_up(off_ok + (mode == kModeVerify ? max_count : 0), 256);
+  const size_t slot_bytes = align_up(off_ok + (mode == kModeVerify ? max_count : 0), 256);
+  const size_t nslots = groups.size() > 1 ? 2 : 1;
   DevState* st;
   int rc = get_state(&st);
   if (rc) return rc;
@@ -403,43 +448,48 @@ int host_desc(const uint8_t* base, uint64_t base_len, const pdb_blk* blk, uint64
   if ((rc = server_park(st))) return rc;
   hipError_t e = hipSetDevice(st->device);
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
-  if ((rc = ensure_ws(st, off_nbad + 256))) return rc;
-  hipStream_t s = st->stream;
-  uint8_t* ws = st->d_ws;
-  uint32_t* d_nbad = reinterpret_cast<uint32_t*>(ws + off_nbad);
-  if (mode == kModeVerify && (e = hipMemsetAsync(d_nbad, 0, 4, s)) != hipSuccess)
-    return hip_fail(e, "hipMemsetAsync");
-  // rebased descriptors stay alive until the final synchronisation (async H2D sources)
-  std::vector<std::vector<pdb_blk>> rbs(groups.size());
-  for (size_t k = 0; k < groups.size(); ++k) {
-    const HostGroup& x = groups[k];
-    std::vector<pdb_blk>& rb = rbs[k];
-    rb.assign(blk + x.first, blk + x.first + x.count);
-    for (auto& b : rb) b.off = b.len ? b.off - x.lo : 0;
-    if (x.hi > x.lo && (e = hipMemcpyAsync(ws, base + x.lo, x.hi - x.lo, hipMemcpyHostToDevice, s)) != hipSuccess)
-      return hip_fail(e, "hipMemcpyAsync(span)");
-    if ((e = hipMemcpyAsync(ws + off_desc, rb.data(), x.count * sizeof(pdb_blk), hipMemcpyHostToDevice, s)) !=
-        hipSuccess)
-      return hip_fail(e, "hipMemcpyAsync(desc)");
-    if (mode == kModeVerify &&
-        (e = hipMemcpyAsync(ws + off_exp, expected + x.first, x.count * 4, hipMemcpyHostToDevice, s)) != hipSuccess)
-      return hip_fail(e, "hipMemcpyAsync(expected)");
-    e = launch_desc(st->geom, st->d_tables, ws, reinterpret_cast<const pdb_blk*>(ws + off_desc), x.count, flags,
-                    mode, reinterpret_cast<const uint32_t*>(ws + off_exp), reinterpret_cast<uint32_t*>(ws + off_out),
-                    ws + off_ok, d_nbad, s);
-    if (e != hipSuccess) return hip_fail(e, "launch_desc");
-    if (mode == kModeOut) {
-      if ((e = hipMemcpyAsync(out + x.first, ws + off_out, x.count * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
-        return hip_fail(e, "hipMemcpyAsync(out)");
-    } else if (ok && (e = hipMemcpyAsync(ok + x.first, ws + off_ok, x.count, hipMemcpyDeviceToHost, s)) !=
-                         hipSuccess) {
-      return hip_fail(e, "hipMemcpyAsync(ok)");
-    }
-  }
+  if ((rc = ensure_ws(st, nslots * slot_bytes + 256))) return rc;
+  hipStream_t s = st->stream, cs = st->copy_stream;
+  uint32_t* d_nbad = reinterpret_cast<uint32_t*>(st->d_ws + nslots * slot_bytes);
+  std::vector<std::vector<pdb_blk>> rbs(groups.size());  // async H2D sources, alive until the drain
   uint32_t nb = 0;
-  if (mode == kModeVerify && (e = hipMemcpyAsync(&nb, d_nbad, 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
-    return hip_fail(e, "hipMemcpyAsync(nbad)");
-  if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+  {
+    SlotPipe pipe(st);
+    if (mode == kModeVerify && (e = hipMemsetAsync(d_nbad, 0, 4, s)) != hipSuccess)
+      return hip_fail(e, "hipMemsetAsync");
+    for (size_t k = 0; k < groups.size(); ++k) {
+      const HostGroup& x = groups[k];
+      uint8_t* ws = st->d_ws + (k % nslots) * slot_bytes;
+      std::vector<pdb_blk>& rb = rbs[k];
+      rb.assign(blk + x.first, blk + x.first + x.count);
+      for (auto& b : rb) b.off = b.len ? b.off - x.lo : 0;
+      if ((e = pipe.begin_copies(k)) != hipSuccess) return hip_fail(e, "hipStreamWaitEvent");
+      if (x.hi > x.lo && (e = hipMemcpyAsync(ws, base + x.lo, x.hi - x.lo, hipMemcpyHostToDevice, cs)) != hipSuccess)
+        return hip_fail(e, "hipMemcpyAsync(span)");
+      if ((e = hipMemcpyAsync(ws + off_desc, rb.data(), x.count * sizeof(pdb_blk), hipMemcpyHostToDevice, cs)) !=
+          hipSuccess)
+        return hip_fail(e, "hipMemcpyAsync(desc)");
+      if (mode == kModeVerify &&
+          (e = hipMemcpyAsync(ws + off_exp, expected + x.first, x.count * 4, hipMemcpyHostToDevice, cs)) != hipSuccess)
+        return hip_fail(e, "hipMemcpyAsync(expected)");
+      if ((e = pipe.end_copies(k)) != hipSuccess) return hip_fail(e, "hipEventRecord(staged)");
+      e = launch_desc(st->geom, st->d_tables, ws, reinterpret_cast<const pdb_blk*>(ws + off_desc), x.count, flags,
+                      mode, reinterpret_cast<const uint32_t*>(ws + off_exp), reinterpret_cast<uint32_t*>(ws + off_out),
+                      ws + off_ok, d_nbad, s);
+      if (e != hipSuccess) return hip_fail(e, "launch_desc");
+      if (mode == kModeOut) {
+        if ((e = hipMemcpyAsync(out + x.first, ws + off_out, x.count * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
+          return hip_fail(e, "hipMemcpyAsync(out)");
+      } else if (ok && (e = hipMemcpyAsync(ok + x.first, ws + off_ok, x.count, hipMemcpyDeviceToHost, s)) !=
+                           hipSuccess) {
+        return hip_fail(e, "hipMemcpyAsync(ok)");
+      }
+      if ((e = pipe.end_group(k)) != hipSuccess) return hip_fail(e, "hipEventRecord(drained)");
+    }
+    if (mode == kModeVerify && (e = hipMemcpyAsync(&nb, d_nbad, 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
+      return hip_fail(e, "hipMemcpyAsync(nbad)");
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+  }
   if (nbad_out) *nbad_out = nb;
   return PDB_OK;
 }
@@ -531,7 +581,7 @@ int host_sst(uint8_t* buf, uint64_t buf_len, const pdb_block_handle* h, uint64_t
     return PDB_OK;
   }
   if (!buf || !h) return fail(PDB_EINVAL, "null argument");
-  // staging groups of at most g_host_chunk bytes of span (block + trailer), as for host_desc
+  // staging groups of at most host_chunk_bytes() of span (block + trailer), as for host_desc
   std::vector<HostGroup> groups;
   HostGroup g{0, 0, UINT64_MAX, 0};
   for (uint64_t i = 0; i < n; ++i) {
@@ -542,7 +592,7 @@ int host_sst(uint8_t* buf, uint64_t buf_len, const pdb_block_handle* h, uint64_t
     if (h[i].size + 1 > 0xFFFFFFFFull) return fail(PDB_ERANGE, "block larger than 4 GiB");
     const uint64_t blo = h[i].offset & ~static_cast<uint64_t>(15), bhi = h[i].offset + h[i].size + 5;
     const uint64_t lo = std::min(g.lo, blo), hi = std::max(g.hi, bhi);
-    if (g.count && hi - lo > g_host_chunk) {
+    if (g.count && hi - lo > host_chunk_bytes()) {
       groups.push_back(g);
       g = HostGroup{i, 1, blo, bhi};
     } else {
@@ -560,7 +610,8 @@ int host_sst(uint8_t* buf, uint64_t buf_len, const pdb_block_handle* h, uint64_t
   }
   const size_t off_h = align_up(need + 16, 256);
   const size_t off_ok = align_up(off_h + max_count * sizeof(pdb_block_handle), 256);
-  const size_t off_nbad = align_up(off_ok + 4 * max_count, 256);  // ok bytes (verify) or masked CRCs (seal)
+  const size_t slot_bytes = align_up(off_ok + 4 * max_count, 256);  // ok bytes (verify) or masked CRCs (seal)
+  const size_t nslots = groups.size() > 1 ? 2 : 1;
   DevState* st;
   int rc = get_state(&st);
   if (rc) return rc;
@@ -568,45 +619,51 @@ int host_sst(uint8_t* buf, uint64_t buf_len, const pdb_block_handle* h, uint64_t
   if ((rc = server_park(st))) return rc;
   hipError_t e = hipSetDevice(st->device);
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
-  if ((rc = ensure_ws(st, off_nbad + 256))) return rc;
-  hipStream_t s = st->stream;
-  uint8_t* ws = st->d_ws;
-  uint32_t* d_nbad = reinterpret_cast<uint32_t*>(ws + off_nbad);
-  if (!seal && (e = hipMemsetAsync(d_nbad, 0, 4, s)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
+  if ((rc = ensure_ws(st, nslots * slot_bytes + 256))) return rc;
+  hipStream_t s = st->stream, cs = st->copy_stream;
+  uint32_t* d_nbad = reinterpret_cast<uint32_t*>(st->d_ws + nslots * slot_bytes);
   // Seal: only the 4 CRC bytes of every trailer change, so the kernel writes the masked CRCs into
   // a compact array, 4 B per block come back across PCIe (not the span), and the host encodes
   // them little-endian at offset + size + 1 (table_builder.cc:199-200).
   std::vector<uint32_t> crc(seal ? n : 0);
   std::vector<std::vector<pdb_block_handle>> rhs(groups.size());  // async H2D sources
-  for (size_t k = 0; k < groups.size(); ++k) {
-    const HostGroup& x = groups[k];
-    std::vector<pdb_block_handle>& rh = rhs[k];
-    rh.assign(h + x.first, h + x.first + x.count);
-    for (auto& y : rh) y.offset -= x.lo;
-    if ((e = hipMemcpyAsync(ws, buf + x.lo, x.hi - x.lo, hipMemcpyHostToDevice, s)) != hipSuccess)
-      return hip_fail(e, "hipMemcpyAsync(span)");
-    if ((e = hipMemcpyAsync(ws + off_h, rh.data(), x.count * sizeof(pdb_block_handle), hipMemcpyHostToDevice,
-                            s)) != hipSuccess)
-      return hip_fail(e, "hipMemcpyAsync(handles)");
-    const pdb_block_handle* d_h = reinterpret_cast<const pdb_block_handle*>(ws + off_h);
-    if (seal) {
-      uint32_t* d_crc = reinterpret_cast<uint32_t*>(ws + off_ok);
-      if ((e = launch_sst_masked(st->geom, st->d_tables, ws, x.hi - x.lo, d_h, x.count, d_crc, s)) != hipSuccess)
-        return hip_fail(e, "launch_sst_masked");
-      if ((e = hipMemcpyAsync(crc.data() + x.first, d_crc, x.count * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
-        return hip_fail(e, "hipMemcpyAsync(crcs)");
-    } else {
-      if ((e = launch_sst(st->geom, st->d_tables, ws, x.hi - x.lo, d_h, x.count, false, ws + off_ok, d_nbad, s)) !=
-          hipSuccess)
-        return hip_fail(e, "launch_sst");
-      if (ok && (e = hipMemcpyAsync(ok + x.first, ws + off_ok, x.count, hipMemcpyDeviceToHost, s)) != hipSuccess)
-        return hip_fail(e, "hipMemcpyAsync(ok)");
-    }
-  }
   uint32_t nb = 0;
-  if (!seal && (e = hipMemcpyAsync(&nb, d_nbad, 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
-    return hip_fail(e, "hipMemcpyAsync(nbad)");
-  if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+  {
+    SlotPipe pipe(st);
+    if (!seal && (e = hipMemsetAsync(d_nbad, 0, 4, s)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
+    for (size_t k = 0; k < groups.size(); ++k) {
+      const HostGroup& x = groups[k];
+      uint8_t* ws = st->d_ws + (k % nslots) * slot_bytes;
+      std::vector<pdb_block_handle>& rh = rhs[k];
+      rh.assign(h + x.first, h + x.first + x.count);
+      for (auto& y : rh) y.offset -= x.lo;
+      if ((e = pipe.begin_copies(k)) != hipSuccess) return hip_fail(e, "hipStreamWaitEvent");
+      if ((e = hipMemcpyAsync(ws, buf + x.lo, x.hi - x.lo, hipMemcpyHostToDevice, cs)) != hipSuccess)
+        return hip_fail(e, "hipMemcpyAsync(span)");
+      if ((e = hipMemcpyAsync(ws + off_h, rh.data(), x.count * sizeof(pdb_block_handle), hipMemcpyHostToDevice,
+                              cs)) != hipSuccess)
+        return hip_fail(e, "hipMemcpyAsync(handles)");
+      if ((e = pipe.end_copies(k)) != hipSuccess) return hip_fail(e, "hipEventRecord(staged)");
+      const pdb_block_handle* d_h = reinterpret_cast<const pdb_block_handle*>(ws + off_h);
+      if (seal) {
+        uint32_t* d_crc = reinterpret_cast<uint32_t*>(ws + off_ok);
+        if ((e = launch_sst_masked(st->geom, st->d_tables, ws, x.hi - x.lo, d_h, x.count, d_crc, s)) != hipSuccess)
+          return hip_fail(e, "launch_sst_masked");
+        if ((e = hipMemcpyAsync(crc.data() + x.first, d_crc, x.count * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
+          return hip_fail(e, "hipMemcpyAsync(crcs)");
+      } else {
+        if ((e = launch_sst(st->geom, st->d_tables, ws, x.hi - x.lo, d_h, x.count, false, ws + off_ok, d_nbad, s)) !=
+            hipSuccess)
+          return hip_fail(e, "launch_sst");
+        if (ok && (e = hipMemcpyAsync(ok + x.first, ws + off_ok, x.count, hipMemcpyDeviceToHost, s)) != hipSuccess)
+          return hip_fail(e, "hipMemcpyAsync(ok)");
+      }
+      if ((e = pipe.end_group(k)) != hipSuccess) return hip_fail(e, "hipEventRecord(drained)");
+    }
+    if (!seal && (e = hipMemcpyAsync(&nb, d_nbad, 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
+      return hip_fail(e, "hipMemcpyAsync(nbad)");
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+  }
   for (uint64_t i = 0; i < crc.size(); ++i) {
     uint8_t* tr = buf + h[i].offset + h[i].size + 1;
     tr[0] = static_cast<uint8_t>(crc[i]);
@@ -739,12 +796,6 @@ int64_t pdb_crc32c_verify_host(const void* base, uint64_t base_len, const pdb_bl
   return rc ? rc : static_cast<int64_t>(nbad);
 }
 
-uint64_t pdb_diag_set_host_chunk(uint64_t bytes) {
-  const uint64_t old = g_host_chunk;
-  if (bytes) g_host_chunk = bytes;
-  return old;
-}
-
 int pdb_sst_seal_device(void* d_buf, uint64_t buf_len, const pdb_block_handle* d_h, uint64_t n,
                         void* stream) {
   if (n == 0) return PDB_OK;
@@ -800,72 +851,6 @@ int64_t pdb_sst_verify_host(const void* buf, uint64_t buf_len, const pdb_block_h
   int64_t nbad = 0;
   int rc = host_sst(static_cast<uint8_t*>(const_cast<void*>(buf)), buf_len, h, n, false, ok, &nbad);
   return rc ? rc : nbad;
-}
-
-int pdb_diag_read_stream(const void* d_base, uint64_t nbytes, uint32_t* d_out, void* stream) {
-  DevState* st;
-  int rc = get_state(&st);
-  if (rc) return rc;
-  if ((rc = quiesce(st))) return rc;
-  hipError_t e = launch_read_stream(static_cast<const uint8_t*>(d_base), nbytes, d_out,
-                                    pick_stream(st, stream));
-  return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_read_stream");
-}
-
-int pdb_diag_read_pattern4k(const void* d_base, uint64_t nblk, int variant, uint32_t* d_out,
-                            void* stream) {
-  DevState* st;
-  int rc = get_state(&st);
-  if (rc) return rc;
-  if ((rc = quiesce(st))) return rc;
-  hipError_t e = launch_read_pattern4k(st->geom, static_cast<const uint8_t*>(d_base), nblk, variant, d_out,
-                                       pick_stream(st, stream));
-  return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_read_pattern4k");
-}
-
-int pdb_fill_splitmix_device(void* d_dst, uint64_t nbytes, uint64_t seed, uint64_t byte_offset,
-                             void* stream) {
-  DevState* st;
-  int rc = get_state(&st);
-  if (rc) return rc;
-  hipError_t e = launch_fill_splitmix(static_cast<uint8_t*>(d_dst), nbytes, seed, byte_offset,
-                                      pick_stream(st, stream));
-  return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_fill_splitmix");
-}
-
-int pdb_diag_server_stats(uint64_t* out4) {
-  DevState* st;
-  int rc = get_state(&st);
-  if (rc) return rc;
-  std::lock_guard<std::mutex> lk(st->mu);
-  if ((rc = server_park(st))) return rc;
-  if (!st->srv_out_h) return fail(PDB_EINVAL, "the scalar server has not run");
-  const ServerBox* b = st->srv_out_h;
-  out4[0] = b->stat_requests;
-  out4[1] = b->stat_serve_ticks;
-  out4[2] = b->stat_polls;
-  out4[3] = b->stat_life_ticks;
-  return st->srv_in_device ? 1 : 0;
-}
-
-int pdb_diag_set_variant(int v) {
-  const int old = g_fast_variant;
-  g_fast_variant = v;
-  return old;
-}
-
-int pdb_crc32c_launch_geometry(int device, uint32_t* grid, uint32_t* block, uint32_t* lds_bytes) {
-  if (device >= 0) {
-    hipError_t e = hipSetDevice(device);
-    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
-  }
-  DevState* st;
-  int rc = get_state(&st);
-  if (rc) return rc;
-  if (grid) *grid = st->geom.grid;
-  if (block) *block = st->geom.block;
-  if (lds_bytes) *lds_bytes = PDB_LDS_BYTES;
-  return PDB_OK;
 }
 
 }  // extern "C"

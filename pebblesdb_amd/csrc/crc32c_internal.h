@@ -26,8 +26,6 @@ struct LaunchGeom {
   uint32_t block;  // threads per workgroup
 };
 
-extern int g_fast_variant;  // diagnostics only: selects a 4-KiB fast-path variant
-
 // crc32c_kernels.hip -- all launches are asynchronous on `s`.
 hipError_t launch_fixed(const LaunchGeom& g, const uint32_t* d_tables, const uint8_t* base,
                         uint64_t stride, uint32_t len, uint64_t nblk, uint32_t flags, uint32_t init,
@@ -80,23 +78,5 @@ constexpr size_t kServerBytes = sizeof(ServerBox) + kServerCap + 16;
 // served0: the seq the new instance treats as already answered.
 hipError_t launch_server(const uint32_t* d_tables, ServerBox* d_in, ServerBox* d_out, uint32_t epoch,
                          uint32_t served0, uint64_t idle_ticks, uint64_t life_ticks, hipStream_t s);
-
-// crc32c_variants.hip -- A/B variants (pdb_diag_set_variant) and calibration kernels
-hipError_t launch_fixed_variant(int v, const LaunchGeom& g, const uint32_t* d_tables, const uint8_t* base,
-                                uint64_t stride, uint32_t len, uint64_t nblk, uint32_t flags, uint32_t init,
-                                uint32_t* out, hipStream_t s);
-hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tables, const uint8_t* base,
-                               const pdb_blk* blk, uint64_t nblk, uint32_t flags, uint32_t* out,
-                               hipStream_t s);
-// sstable hooks: 18 = crc_stream_kernel (32-B pieces), 30 = crc_stream16_kernel (the previous
-// default), 31-36 seal-write diagnostics, 97 verify without the Horner folds (wrong CRCs)
-hipError_t launch_sst_variant(int v, const LaunchGeom& g, const uint32_t* d_tables, uint8_t* buf, uint64_t buf_len,
-                              const pdb_block_handle* h, uint64_t n, bool seal, uint8_t* ok, uint32_t* nbad,
-                              hipStream_t s);
-hipError_t launch_read_stream(const uint8_t* base, uint64_t nbytes, uint32_t* out, hipStream_t s);
-hipError_t launch_read_pattern4k(const LaunchGeom& g, const uint8_t* base, uint64_t nblk,
-                                 int variant, uint32_t* out, hipStream_t s);
-hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed, uint64_t byte_offset,
-                                hipStream_t s);
 
 }  // namespace pdb

@@ -1,12 +1,42 @@
-// crc32c_variants.hip -- A/B kernel variants (selected with pdb_diag_set_variant, all
-// parity-tested in tests/test_gpu_parity.py) and the load-pattern calibration kernels behind the
-// roofline numbers in DESIGN.md §6.  Not on the shipped path unless a variant is selected.
+// diag_variants.hip -- BENCH / TEST INFRASTRUCTURE (libpdb_crc32c_diag.so, never linked into the
+// product): the A/B kernel variants measured against the shipped kernels (selected per call through
+// include/pdb_crc32c_diag.h, all parity-tested in tests/test_gpu_parity.py), the load-pattern
+// calibration kernels behind the roofline numbers in DESIGN.md §6, and the synthetic-input fill.
 #include <mutex>
 
-#include "crc32c_device.h"
+#include "diag_device.h"
+#include "diag_internal.h"
 
 namespace pdb {
 namespace {
+
+__device__ __forceinline__ uint64_t splitmix64_at(uint64_t seed, uint64_t i) {
+  uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// Thread t writes dst[8t .. 8t+8) (bytes of the splitmix stream at byte_offset + 8t + j).
+__global__ __launch_bounds__(256) void fill_splitmix_kernel(uint8_t* __restrict__ dst, uint64_t nbytes, uint64_t seed,
+                                                            uint64_t byte_offset) {
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  const uint32_t sh = static_cast<uint32_t>(byte_offset & 7u);
+  for (uint64_t t = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; t * 8 < nbytes; t += stride) {
+    const uint64_t gb = byte_offset + t * 8;  // first global byte of this thread
+    const uint64_t w0 = splitmix64_at(seed, gb >> 3);
+    uint64_t v = w0;
+    if (sh) {
+      const uint64_t w1 = splitmix64_at(seed, (gb >> 3) + 1);
+      v = (w0 >> (8 * sh)) | (w1 << (64 - 8 * sh));
+    }
+    if (t * 8 + 8 <= nbytes && (reinterpret_cast<uintptr_t>(dst) & 7u) == 0) {
+      *reinterpret_cast<uint64_t*>(dst + t * 8) = v;
+    } else {
+      for (uint32_t j = 0; j < 8 && t * 8 + j < nbytes; ++j) dst[t * 8 + j] = static_cast<uint8_t>(v >> (8 * j));
+    }
+  }
+}
 
 template <int kNP, int kDepth, bool kIssueFirst = false>
 __global__ __launch_bounds__(kThreads) void crc_fast4k_kernel(
@@ -430,6 +460,7 @@ struct SinkOps<SealTouchSink> {
 hipError_t launch_sst_variant(int v, const LaunchGeom& g, const uint32_t* d_tables, uint8_t* buf, uint64_t buf_len,
                               const pdb_block_handle* h, uint64_t n, bool seal, uint8_t* ok, uint32_t* nbad,
                               hipStream_t s) {
+  if (v == 0) return launch_sst(g, d_tables, buf, buf_len, h, n, seal, ok, nbad, s);
   const dim3 grid(grid_for(g, n)), block(kThreads);
   const SstSrc src{buf, h, buf_len};
   if (v == 97 && !seal) {  // WRONG CRCs by design: verify without the Horner folds (prices them)
@@ -514,6 +545,7 @@ hipError_t launch_sst_variant(int v, const LaunchGeom& g, const uint32_t* d_tabl
 hipError_t launch_fixed_variant(int v, const LaunchGeom& g, const uint32_t* d_tables, const uint8_t* base,
                                 uint64_t stride, uint32_t len, uint64_t nblk, uint32_t flags, uint32_t init,
                                 uint32_t* out, hipStream_t s) {
+  if (v == 0) return launch_fixed(g, d_tables, base, stride, len, nblk, flags, init, out, s);
   const dim3 grid(grid_for(g, nblk)), block(kThreads);
   const bool fast = len == 4096u && (reinterpret_cast<uintptr_t>(base) & 15u) == 0 &&
                     (stride & 15u) == 0;
@@ -570,45 +602,45 @@ hipError_t launch_fixed_variant(int v, const LaunchGeom& g, const uint32_t* d_ta
     case 5: PDB_TEAM(16, 0); break;  // 4 blocks per wave, 16-lane teams
     case 6: PDB_K(crc_pingpong4k_kernel); break;
     case 7: PDB_K((crc_fast4k_kernel<2, 1, true>)); break;  // loads issued before the hash
-    case 8: PDB_K(crc_pack4k_kernel<0>); break;  // packed tree, free-running
-    case 9: PDB_K(crc_pack4k_kernel<2>); break;  // lock-step every 2 groups
-    case 10: PDB_K(crc_pack4k_kernel<4>); break;
+    case 8: PDB_K(crc_pack4k_ab_kernel<0>); break;  // packed tree, free-running
+    case 9: PDB_K(crc_pack4k_ab_kernel<2>); break;  // lock-step every 2 groups
+    case 10: PDB_K(crc_pack4k_ab_kernel<4>); break;
     case 11: PDB_K(crc_pack4k_dyn_kernel); break;  // workgroup-local dynamic groups
     // coalesced 4 x 16-B lane pieces (each load instruction 1 KiB contiguous), nt loads (13-25;
-    // the shipped default is crc_pack4k_kernel<1, 4, true>)
-    case 12: PDB_K((crc_pack4k_kernel<1>)); break;  // previous default: 2 x 32-B pieces, default policy
-    case 13: PDB_K((crc_pack4k_kernel<0, 4, true>)); break;
-    case 14: PDB_K((crc_pack4k_kernel<1, 2, true>)); break;
-    case 15: PDB_K((crc_pack4k_kernel<0, 4, false>)); break;
-    case 16: PDB_K((crc_pack4k_kernel<2, 4, true>)); break;
-    case 17: PDB_K((crc_pack4k_kernel<4, 4, true>)); break;
-    case 18: PDB_K((crc_pack4k_kernel<8, 4, true>)); break;
+    // the shipped default is crc_pack4k_ab_kernel<1, 4, true>)
+    case 12: PDB_K((crc_pack4k_ab_kernel<1>)); break;  // previous default: 2 x 32-B pieces, default policy
+    case 13: PDB_K((crc_pack4k_ab_kernel<0, 4, true>)); break;
+    case 14: PDB_K((crc_pack4k_ab_kernel<1, 2, true>)); break;
+    case 15: PDB_K((crc_pack4k_ab_kernel<0, 4, false>)); break;
+    case 16: PDB_K((crc_pack4k_ab_kernel<2, 4, true>)); break;
+    case 17: PDB_K((crc_pack4k_ab_kernel<4, 4, true>)); break;
+    case 18: PDB_K((crc_pack4k_ab_kernel<8, 4, true>)); break;
     // 8 waves per CU (512-thread workgroups)
-    case 19: hipLaunchKernelGGL((crc_pack4k_kernel<1, 4, true, 8>), dim3(grid_for8(g, nblk)), dim3(512), 0, s, d_tables,
+    case 19: hipLaunchKernelGGL((crc_pack4k_ab_kernel<1, 4, true, 8>), dim3(grid_for8(g, nblk)), dim3(512), 0, s, d_tables,
                                 base, stride, nblk, flags, init, out); break;
-    case 20: hipLaunchKernelGGL((crc_pack4k_kernel<0, 4, true, 8>), dim3(grid_for8(g, nblk)), dim3(512), 0, s, d_tables,
+    case 20: hipLaunchKernelGGL((crc_pack4k_ab_kernel<0, 4, true, 8>), dim3(grid_for8(g, nblk)), dim3(512), 0, s, d_tables,
                                 base, stride, nblk, flags, init, out); break;
     // blocks in pairs (8 chains per wave): 8 waves / 16 waves, lock-step / free
-    case 21: hipLaunchKernelGGL((crc_pack4k_kernel<1, 4, true, 8, true>), dim3(grid_for8(g, nblk)), dim3(512), 0, s,
+    case 21: hipLaunchKernelGGL((crc_pack4k_ab_kernel<1, 4, true, 8, true>), dim3(grid_for8(g, nblk)), dim3(512), 0, s,
                                 d_tables, base, stride, nblk, flags, init, out); break;
-    case 22: hipLaunchKernelGGL((crc_pack4k_kernel<0, 4, true, 8, true>), dim3(grid_for8(g, nblk)), dim3(512), 0, s,
+    case 22: hipLaunchKernelGGL((crc_pack4k_ab_kernel<0, 4, true, 8, true>), dim3(grid_for8(g, nblk)), dim3(512), 0, s,
                                 d_tables, base, stride, nblk, flags, init, out); break;
-    case 23: PDB_K((crc_pack4k_kernel<1, 4, true, 16, true>)); break;
+    case 23: PDB_K((crc_pack4k_ab_kernel<1, 4, true, 16, true>)); break;
     // 12 waves per CU (768-thread workgroups): 48 KiB in flight
-    case 24: hipLaunchKernelGGL((crc_pack4k_kernel<1, 4, true, 12>), dim3(grid_forw(g, nblk, 12)), dim3(768), 0, s,
+    case 24: hipLaunchKernelGGL((crc_pack4k_ab_kernel<1, 4, true, 12>), dim3(grid_forw(g, nblk, 12)), dim3(768), 0, s,
                                 d_tables, base, stride, nblk, flags, init, out); break;
-    case 25: hipLaunchKernelGGL((crc_pack4k_kernel<2, 4, true, 12>), dim3(grid_forw(g, nblk, 12)), dim3(768), 0, s,
+    case 25: hipLaunchKernelGGL((crc_pack4k_ab_kernel<2, 4, true, 12>), dim3(grid_forw(g, nblk, 12)), dim3(768), 0, s,
                                 d_tables, base, stride, nblk, flags, init, out); break;
     // XCD-contiguous workgroup numbering (lock-step / free-running)
-    case 26: PDB_K((crc_pack4k_kernel<1, 4, true, 16, false, true>)); break;
-    case 27: PDB_K((crc_pack4k_kernel<0, 4, true, 16, false, true>)); break;
+    case 26: PDB_K((crc_pack4k_ab_kernel<1, 4, true, 16, false, true>)); break;
+    case 27: PDB_K((crc_pack4k_ab_kernel<0, 4, true, 16, false, true>)); break;
     // quad-transposed lanes: 64 contiguous bytes per lane, no per-lane Horner folds
-    case 28: PDB_K((crc_pack4k_kernel<1, 4, true, 16, false, false, 1>)); break;
-    case 29: PDB_K((crc_pack4k_kernel<1, 4, true, 16, false, false, 2>)); break;  // 2 chains + shift 32
+    case 28: PDB_K((crc_pack4k_ab_kernel<1, 4, true, 16, false, false, 1>)); break;
+    case 29: PDB_K((crc_pack4k_ab_kernel<1, 4, true, 16, false, false, 2>)); break;  // 2 chains + shift 32
     // s_setprio 2 around the next block's load issue (free-running / lock-step)
-    case 30: PDB_K((crc_pack4k_kernel<1, 4, true, 16, false, false, 0, true>)); break;
-    case 31: PDB_K((crc_pack4k_kernel<0, 4, true, 16, false, false, 0, true>)); break;
-    default: PDB_K((crc_pack4k_kernel<1, 4, true>)); break;
+    case 30: PDB_K((crc_pack4k_ab_kernel<1, 4, true, 16, false, false, 0, true>)); break;
+    case 31: PDB_K((crc_pack4k_ab_kernel<0, 4, true, 16, false, false, 0, true>)); break;
+    default: PDB_K((crc_pack4k_ab_kernel<1, 4, true>)); break;
   }
 #undef PDB_FAST
 #undef PDB_TEAM
@@ -617,32 +649,73 @@ hipError_t launch_fixed_variant(int v, const LaunchGeom& g, const uint32_t* d_ta
 }
 
 hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tables, const uint8_t* base,
-                               const pdb_blk* blk, uint64_t nblk, uint32_t flags, uint32_t* out,
-                               hipStream_t s) {
+                               const pdb_blk* blk, uint64_t nblk, uint32_t flags, uint32_t* out, hipStream_t s) {
+  if (nblk == 0) return hipSuccess;
   const dim3 grid(grid_for(g, nblk)), block(kThreads);
   const DescSrc src{base, blk, flags};
-  if (v == 8)  // static strided assignment (free-running)
-    hipLaunchKernelGGL((crc_stream_kernel<DescSrc, OutSink, 0, false>), grid, block, 0, s, d_tables, src,
-                       nblk, OutSink{out, flags});
-  else if (v == 12)  // coalesced 16-B pieces, nt loads, dynamic blocks
-    hipLaunchKernelGGL((crc_stream16_kernel<DescSrc, OutSink, true, true>), grid, block, 0, s, d_tables, src,
-                       nblk, OutSink{out, flags});
-  else if (v == 13)  // coalesced 16-B pieces, default-policy loads
-    hipLaunchKernelGGL((crc_stream16_kernel<DescSrc, OutSink, true, false>), grid, block, 0, s, d_tables, src,
-                       nblk, OutSink{out, flags});
-  else if (v == 14)  // coalesced 16-B pieces, nt loads, static strided blocks
-    hipLaunchKernelGGL((crc_stream16_kernel<DescSrc, OutSink, false, true>), grid, block, 0, s, d_tables, src,
-                       nblk, OutSink{out, flags});
-  else if (v == 15)  // 32-B pieces, dynamic blocks, packed 4-block trees
-    hipLaunchKernelGGL((crc_stream_kernel<DescSrc, OutSink, 0, true, true>), grid, block, 0, s, d_tables, src,
-                       nblk, OutSink{out, flags});
-  else if (v == 16)  // coalesced 16-B pieces, nt loads, dynamic blocks, packed 4-block trees
-    hipLaunchKernelGGL((crc_stream16_kernel<DescSrc, OutSink, true, true, true>), grid, block, 0, s, d_tables,
-                       src, nblk, OutSink{out, flags});
-
-  else
-    hipLaunchKernelGGL((crc_stream_kernel<DescSrc, OutSink, 0, true>), grid, block, 0, s, d_tables, src, nblk,
-                       OutSink{out, flags});
+  const OutSink sink{out, flags};
+  const dim3 lgrid(grid_for(g, (nblk + 63) / 64)), qgrid(grid_for(g, (nblk + 15) / 16));
+  switch (v) {
+    case 8:  // 32-B pieces, static strided assignment (free-running)
+      hipLaunchKernelGGL((crc_stream_kernel<DescSrc, OutSink, 0, false>), grid, block, 0, s, d_tables, src, nblk, sink);
+      break;
+    case 12:  // coalesced 16-B pieces, nt loads, dynamic blocks
+      hipLaunchKernelGGL((crc_stream16_kernel<DescSrc, OutSink, true, true>), grid, block, 0, s, d_tables, src, nblk,
+                         sink);
+      break;
+    case 13:  // coalesced 16-B pieces, default-policy loads
+      hipLaunchKernelGGL((crc_stream16_kernel<DescSrc, OutSink, true, false>), grid, block, 0, s, d_tables, src, nblk,
+                         sink);
+      break;
+    case 14:  // coalesced 16-B pieces, nt loads, static strided blocks
+      hipLaunchKernelGGL((crc_stream16_kernel<DescSrc, OutSink, false, true>), grid, block, 0, s, d_tables, src, nblk,
+                         sink);
+      break;
+    case 15:  // 32-B pieces, dynamic blocks, packed 4-block trees
+      hipLaunchKernelGGL((crc_stream_kernel<DescSrc, OutSink, 0, true, true>), grid, block, 0, s, d_tables, src, nblk,
+                         sink);
+      break;
+    case 16:  // 40: size hints ignored -- the any-length kernel (16-B pieces, nt, dynamic, packed trees)
+    case 40:
+      hipLaunchKernelGGL((crc_stream16_kernel<DescSrc, OutSink, true, true, true>), grid, block, 0, s, d_tables, src,
+                         nblk, sink);
+      break;
+    case 41:  // the 1-KiB kernel with 4-block groups (fast range 1024..1280 B)
+      hipLaunchKernelGGL((crc_sst1k_kernel<DescSrc, OutSink, true, 4>), grid, block, 0, s, d_tables, src, nblk, sink);
+      break;
+    case 50:  // one lane per record, 32-B groups loaded one ahead (nt / default policy)
+      hipLaunchKernelGGL((crc_lanerec_kernel<DescSrc, OutSink, true>), lgrid, block, 0, s, d_tables, src, nblk, sink);
+      break;
+    case 51:
+      hipLaunchKernelGGL((crc_lanerec_kernel<DescSrc, OutSink, false>), lgrid, block, 0, s, d_tables, src, nblk, sink);
+      break;
+    case 52:  // the shipped <= 256-B window kernel, for any list
+      hipLaunchKernelGGL((crc_lanerec9_kernel<DescSrc, OutSink>), lgrid, block, 0, s, d_tables, src, nblk, sink);
+      break;
+    case 53:  // the <= 256-B class on the round-1 crc_rec256_kernel (rows of 16 lanes + row tree)
+      hipLaunchKernelGGL((crc_rec256_kernel<DescSrc, OutSink, true>), grid, block, 0, s, d_tables, src, nblk, sink);
+      break;
+    case 54:  // 257..512 B with two chains (9 + 8 groups)
+      hipLaunchKernelGGL((crc_lanerec17_kernel<DescSrc, OutSink, 2>), dim3(grid17(g, nblk)), dim3(kThreads17), 0, s,
+                         d_tables, src, nblk, sink);
+      break;
+    case 55:  // cross-batch prefetch: 9 groups at 512 threads / 17 groups at 256 threads
+      hipLaunchKernelGGL((crc_lanerec_pf_kernel<DescSrc, OutSink, 9, 512>), dim3(grid_wg(g, nblk, 512)), dim3(512), 0,
+                         s, d_tables, src, nblk, sink);
+      break;
+    case 56:
+      hipLaunchKernelGGL((crc_lanerec_pf_kernel<DescSrc, OutSink, 17, 256>), dim3(grid_wg(g, nblk, 256)), dim3(256), 0,
+                         s, d_tables, src, nblk, sink);
+      break;
+    case 57:  // four lanes per record (<= 256 B / <= 512 B)
+      hipLaunchKernelGGL((crc_quadrec_kernel<DescSrc, OutSink, 5, 256>), qgrid, block, 0, s, d_tables, src, nblk, sink);
+      break;
+    case 58:
+      hipLaunchKernelGGL((crc_quadrec_kernel<DescSrc, OutSink, 9, 512>), qgrid, block, 0, s, d_tables, src, nblk, sink);
+      break;
+    default:  // 0 (and unknown ids): the shipped routing
+      return launch_desc(g, d_tables, base, blk, nblk, flags, kModeOut, nullptr, out, nullptr, nullptr, s);
+  }
   return hipGetLastError();
 }
 
@@ -700,6 +773,15 @@ hipError_t launch_read_pattern4k(const LaunchGeom& g, const uint8_t* base, uint6
     default: PDB_RP(0, 1, 0); break;
   }
 #undef PDB_RP
+  return hipGetLastError();
+}
+
+hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed, uint64_t byte_offset, hipStream_t s) {
+  if (nbytes == 0) return hipSuccess;
+  uint64_t blocks = ((nbytes + 7) / 8 + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(fill_splitmix_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, s, dst, nbytes, seed,
+                     byte_offset);
   return hipGetLastError();
 }
 

@@ -40,39 +40,65 @@ class PhysicalRecord:
     def payload_offset(self) -> int:
         return self.offset + K_HEADER_SIZE
 
+    @property
+    def block(self) -> int:
+        return self.offset // K_BLOCK_SIZE
 
-def physical_records(image) -> list[PhysicalRecord]:
-    """Walk the blocks like log::Reader::ReadPhysicalRecord (log_reader.cc:185-260), without
-    checking CRCs: zero-filled block tails and preallocated zero records are skipped; a
-    record whose length runs past its block or the file ends the walk (truncated tail)."""
+
+@dataclass(frozen=True)
+class BlockDrop:
+    """The rest of a block that log::Reader drops without a CRC check: a record whose length runs
+    past a full block ("bad record length", log_reader.cc:214-220) or a zero-filled preallocated
+    region (type 0, length 0: dropped silently, log_reader.cc:227-233)."""
+    offset: int
+    nbytes: int
+    reason: str | None
+
+    @property
+    def block(self) -> int:
+        return self.offset // K_BLOCK_SIZE
+
+
+def walk(image) -> list:
+    """The physical items log::Reader::ReadPhysicalRecord (log_reader.cc:181-263) meets, trusting
+    every length (CRCs are checked afterwards, in one batch): PhysicalRecord or BlockDrop, in file
+    order.  The file is read in 32-KiB blocks; only the last, short block sets eof: a record running
+    past it, or a truncated header there, ends the walk (a writer that died mid-record: no report).
+    A block tail shorter than a header is skipped (the writer's zero trailer)."""
     img = memoryview(bytes(image))
     n = len(img)
     out = []
-    pos = 0
-    while pos < n:
-        left_in_block = K_BLOCK_SIZE - (pos % K_BLOCK_SIZE)
-        if left_in_block < K_HEADER_SIZE:
-            pos += left_in_block  # trailer (log_writer.cc:90-97)
-            continue
-        if pos + K_HEADER_SIZE > n:
-            break
-        stored = int.from_bytes(img[pos : pos + 4], "little")
-        length = img[pos + 4] | (img[pos + 5] << 8)
-        typ = img[pos + 6]
-        if typ == K_ZERO and length == 0:  # preallocated region: skip the rest of the block
-            pos += left_in_block
-            continue
-        end = pos + K_HEADER_SIZE + length
-        if end > n or end > pos - (pos % K_BLOCK_SIZE) + K_BLOCK_SIZE:
-            break
-        out.append(PhysicalRecord(pos, typ, length, stored))
-        pos = end
+    for bstart in range(0, n, K_BLOCK_SIZE):
+        bend = min(bstart + K_BLOCK_SIZE, n)
+        eof = bend - bstart < K_BLOCK_SIZE
+        pos = bstart
+        while bend - pos >= K_HEADER_SIZE:
+            length = img[pos + 4] | (img[pos + 5] << 8)
+            typ = img[pos + 6]
+            if K_HEADER_SIZE + length > bend - pos:
+                if eof:
+                    return out  # kEof: the writer died in the middle of this record
+                out.append(BlockDrop(pos, bend - pos, "bad record length"))
+                break
+            if typ == K_ZERO and length == 0:
+                out.append(BlockDrop(pos, bend - pos, None))
+                break
+            out.append(PhysicalRecord(pos, typ, length, int.from_bytes(img[pos : pos + 4], "little")))
+            pos += K_HEADER_SIZE + length
+        if eof:
+            break  # a short tail in the last block is a truncated header: kEof
     return out
+
+
+def physical_records(image) -> list[PhysicalRecord]:
+    """Every physical record of the walk (see walk()), without checking CRCs."""
+    return [r for r in walk(image) if isinstance(r, PhysicalRecord)]
 
 
 def verify_log(image, records=None) -> tuple[list[PhysicalRecord], np.ndarray]:
     """(records, ok): ok[i] = 1 iff record i's stored CRC matches crc32c(type || payload);
-    all records checked in one GPU batch (pdb_crc32c_batch_host)."""
+    all records checked in one GPU batch (pdb_crc32c_batch_host).  Records the reader would never
+    reach (after a bad one in the same block) are checked too; replay_log() discards them."""
     recs = physical_records(image) if records is None else records
     if not recs:
         return recs, np.zeros(0, dtype=np.uint8)
@@ -82,46 +108,95 @@ def verify_log(image, records=None) -> tuple[list[PhysicalRecord], np.ndarray]:
     return recs, (got == stored).astype(np.uint8)
 
 
-def read_log(image, checksum: bool = True) -> tuple[list[bytes], int]:
-    """Logical records (Full, or First Middle* Last) and the bytes dropped as corrupt, in the
-    spirit of log::Reader::ReadRecord: a bad physical record is dropped and any partially
-    assembled fragment is discarded."""
+@dataclass
+class LogReplay:
+    records: list  # (LastRecordOffset, payload bytes) per logical record, in order
+    reports: list  # (bytes, "Corruption: <reason>") per Reporter::Corruption call, in order
+
+    @property
+    def dropped(self) -> int:
+        return sum(b for b, _ in self.reports)
+
+
+def replay_log(image, checksum: bool = True, ok=None) -> LogReplay:
+    """What log::Reader::ReadRecord (log_reader.cc:59-164, checksums on, initial offset 0) delivers
+    from `image`: the logical records with their LastRecordOffset and the corruption reports, from
+    ONE batched CRC check of every walked record (`ok`, from verify_log when not given).  A record
+    failing its check drops the rest of its block -- the reader no longer trusts the length -- so
+    the records walked after it in that block are discarded, never replayed (log_reader.cc:240-247).
+    Pinned by tests/golden/log/corruptions.json (the reference reader on corrupted logs)."""
     img = bytes(image)
-    recs, ok = verify_log(img) if checksum else (physical_records(img), None)
-    out, dropped = [], 0
-    frag = None
-    for i, r in enumerate(recs):
-        if ok is not None and not ok[i]:
-            dropped += K_HEADER_SIZE + r.length
-            if frag is not None:
-                dropped += len(frag)
-                frag = None
+    items = walk(img)
+    recs = [it for it in items if isinstance(it, PhysicalRecord)]
+    if checksum and ok is None:
+        _, ok = verify_log(img, recs)
+    good = {}
+    if checksum:
+        for r, k in zip(recs, ok):
+            good[r.offset] = bool(k)
+    out, reports = [], []
+    scratch, in_frag = b"", False
+    prospective = 0
+    pos = 0  # reader position before the next physical read (end_of_buffer_offset_ - buffer_.size())
+    dead_block = -1
+
+    def bad_record():  # kBadRecord in ReadRecord (log_reader.cc:143-149)
+        nonlocal scratch, in_frag
+        if in_frag:
+            reports.append((len(scratch), "Corruption: error in middle of record"))
+            in_frag, scratch = False, b""
+
+    for it in items:
+        if it.block == dead_block:
             continue
-        payload = img[r.payload_offset : r.payload_offset + r.length]
-        if r.type == K_FULL:
-            if frag is not None:
-                dropped += len(frag)
-            frag = None
-            out.append(payload)
-        elif r.type == K_FIRST:
-            if frag is not None:
-                dropped += len(frag)
-            frag = bytearray(payload)
-        elif r.type == K_MIDDLE:
-            if frag is None:
-                dropped += r.length
+        bend = min((it.block + 1) * K_BLOCK_SIZE, len(img))
+        if isinstance(it, BlockDrop):
+            if it.reason:
+                reports.append((it.nbytes, "Corruption: " + it.reason))
+            bad_record()
+            pos = bend
+            continue
+        phys_off = pos
+        if checksum and not good[it.offset]:
+            reports.append((bend - it.offset, "Corruption: checksum mismatch"))
+            dead_block = it.block
+            bad_record()
+            pos = bend
+            continue
+        pos = it.offset + K_HEADER_SIZE + it.length
+        frag = img[it.payload_offset : it.payload_offset + it.length]
+        t = it.type
+        if t == K_FULL:
+            if in_frag and scratch:
+                reports.append((len(scratch), "Corruption: partial record without end(1)"))
+            out.append((phys_off, frag))
+            scratch, in_frag = b"", False
+        elif t == K_FIRST:
+            if in_frag and scratch:
+                reports.append((len(scratch), "Corruption: partial record without end(2)"))
+            prospective = phys_off
+            scratch, in_frag = frag, True
+        elif t == K_MIDDLE:
+            if not in_frag:
+                reports.append((len(frag), "Corruption: missing start of fragmented record(1)"))
             else:
-                frag += payload
-        elif r.type == K_LAST:
-            if frag is None:
-                dropped += r.length
+                scratch += frag
+        elif t == K_LAST:
+            if not in_frag:
+                reports.append((len(frag), "Corruption: missing start of fragmented record(2)"))
             else:
-                frag += payload
-                out.append(bytes(frag))
-                frag = None
+                out.append((prospective, scratch + frag))
+                scratch, in_frag = b"", False
         else:
-            dropped += K_HEADER_SIZE + r.length
-    return out, dropped
+            reports.append((len(frag) + (len(scratch) if in_frag else 0), f"Corruption: unknown record type {t}"))
+            scratch, in_frag = b"", False
+    return LogReplay(out, reports)
+
+
+def read_log(image, checksum: bool = True) -> tuple[list[bytes], int]:
+    """Logical records and the bytes the reader reports as dropped (log::Reader::ReadRecord)."""
+    r = replay_log(image, checksum)
+    return [p for _, p in r.records], r.dropped
 
 
 class LogWriter:

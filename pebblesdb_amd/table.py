@@ -247,7 +247,13 @@ def table_layout(image, verify_checksums: bool = True) -> TableLayout:
 
 def verify_table(image) -> tuple[TableLayout, np.ndarray]:
     """leveldb-verify for one table image: every block (data, meta, metaindex, index) checked in
-    ONE GPU batch.  Returns (layout, ok flags in all_handles() order)."""
+    ONE GPU batch.  Returns (layout, ok flags in all_handles() order).  The index and metaindex
+    blocks are checked first (one small batch), so a corrupt index is reported as
+    Corruption("block checksum mismatch") -- ReadBlock's verdict -- before its entries are parsed."""
+    image = bytes(image)
+    f = Footer.decode(image)
+    if not verify_blocks(image, [f.index, f.metaindex]).all():
+        raise Corruption("block checksum mismatch")
     lay = table_layout(image, verify_checksums=False)
     return lay, verify_blocks(image, lay.all_handles())
 

@@ -142,9 +142,15 @@ static void VerifyReferenceTables(const std::string& dir) {
       bad[all[k].offset + all[k].size / 2] ^= 0x04;
       EXPECT(pdb::VerifyTable(bad.data(), bad.size(), nullptr, &ok, nullptr) == 1 && ok[k] == 0);
     }
-    std::string bad = img;  // the stored trailer of the index block
+    std::string bad = img;  // the stored trailer of the index block: checked before it is parsed
     bad[t.index.offset + t.index.size + 3] ^= 0x10;
-    EXPECT(pdb::VerifyTable(bad.data(), bad.size(), nullptr, &ok, nullptr) == 1 && ok.back() == 0);
+    EXPECT(pdb::VerifyTable(bad.data(), bad.size(), nullptr, &ok, &err) == -1000 && err == "block checksum mismatch");
+    bad = img;  // a corrupted index entry: the same verdict, never a parse error or garbage handles
+    bad[t.index.offset + 1] ^= 0x7f;
+    EXPECT(pdb::VerifyTable(bad.data(), bad.size(), nullptr, &ok, &err) == -1000 && err == "block checksum mismatch");
+    bad = img;  // ...and the metaindex block
+    bad[t.metaindex.offset + t.metaindex.size + 1] ^= 0x01;
+    EXPECT(pdb::VerifyTable(bad.data(), bad.size(), nullptr, &ok, &err) == -1000 && err == "block checksum mismatch");
     bad = img;  // a broken magic number is structural corruption, not a checksum count
     bad[bad.size() - 1] ^= 0x01;
     EXPECT(pdb::VerifyTable(bad.data(), bad.size(), nullptr, &ok, &err) == -1000 &&
@@ -167,11 +173,13 @@ static void VerifyReferenceLogs(const std::string& dir) {
     size_t logical = 0;
     for (const auto& r : recs) logical += r.type == pdb::log::kFullType || r.type == pdb::log::kLastType;
     EXPECT(logical == lg.logical && ok.size() == recs.size());
-    // round trip: logical records -> the group-commit writer -> one sealing batch == the file
-    std::vector<std::string> payloads;
-    EXPECT(pdb::log::AssembleRecords(img.data(), recs, ok, &payloads) == 0 && payloads.size() == lg.logical);
+    // round trip: logical records (the log::Reader replay) -> the group-commit writer -> one
+    // sealing batch == the file
+    std::vector<pdb::log::LogicalRecord> payloads;
+    std::vector<pdb::log::CorruptionReport> reports;
+    EXPECT(pdb::log::ReplayLog(img.data(), img.size(), &payloads, &reports) == 0 && payloads.size() == lg.logical);
     pdb::log::BatchWriter w;
-    for (const auto& pl : payloads) w.AddRecord(pl.data(), pl.size());
+    for (const auto& pl : payloads) w.AddRecord(pl.data.data(), pl.data.size());
     EXPECT(w.num_physical_records() == recs.size() && w.Seal() == 0 && w.bytes() == img);
     for (size_t k = 0; k < recs.size(); k += (recs.size() + 4) / 5) {
       std::string bad = img;
@@ -186,7 +194,38 @@ static void VerifyReferenceLogs(const std::string& dir) {
   }
 }
 
+// --replay <log>...: print what pdb::log::ReplayLog delivers (records: [LastRecordOffset, length,
+// FNV-1a-64], reports: [bytes, reason]) in oracle/ref_logreader's JSON format, so the Python test
+// compares it with the reference reader's output on the corrupted logs (corruptions.json).
+static uint64_t Fnv1a64(const std::string& s) {
+  uint64_t h = 1469598103934665603ull;
+  for (unsigned char c : s) h = (h ^ c) * 1099511628211ull;
+  return h;
+}
+
+static int Replay(const char* path) {
+  const std::string img = ReadFile(path);
+  std::vector<pdb::log::LogicalRecord> recs;
+  std::vector<pdb::log::CorruptionReport> reports;
+  if (pdb::log::ReplayLog(img.data(), img.size(), &recs, &reports) < 0) return 1;
+  printf("{\"records\":[");
+  for (size_t i = 0; i < recs.size(); ++i)
+    printf("%s[%llu,%zu,\"%016llx\"]", i ? "," : "", (unsigned long long)recs[i].offset, recs[i].data.size(),
+           (unsigned long long)Fnv1a64(recs[i].data));
+  printf("],\"reports\":[");
+  for (size_t i = 0; i < reports.size(); ++i)
+    printf("%s[%llu,\"%s\"]", i ? "," : "", (unsigned long long)reports[i].bytes, reports[i].reason.c_str());
+  printf("]}\n");
+  return 0;
+}
+
 int main(int argc, char** argv) {
+  if (argc >= 3 && std::string(argv[1]) == "--replay") {  // one JSON line per log file
+    if (pdb_crc32c_init(0) != 0) return 2;
+    for (int a = 2; a < argc; ++a)
+      if (Replay(argv[a])) return 1;
+    return 0;
+  }
   if (pdb_crc32c_init(0) != 0) {
     fprintf(stderr, "no device: %s\n", pdb_last_error());
     return 2;

@@ -260,5 +260,138 @@ def gen_logs() -> None:
     print(f"wrote {len(manifest)} logs to {LOG_DIR}")
 
 
+LOG_READER = os.path.join(ROOT, "oracle", "_ref", "ref_logreader")
+BS, HDR = 32768, 7
+
+
+def _walk_clean(img: bytes):
+    """(header offset, length, type) of every physical record of a CLEAN log (generation helper)."""
+    out, pos, n = [], 0, len(img)
+    while pos + HDR <= n:
+        if BS - pos % BS < HDR:
+            pos += BS - pos % BS
+            continue
+        length, typ = img[pos + 4] | (img[pos + 5] << 8), img[pos + 6]
+        if typ == 0 and length == 0:
+            pos += BS - pos % BS
+            continue
+        out.append((pos, length, typ))
+        pos += HDR + length
+    return out
+
+
+def _corruption_recipes(img: bytes, ref):
+    """Deterministic corruptions of one clean log: (name, ops), ops = ("xor", off, byte) |
+    ("set", off, hex) | ("truncate", nbytes).  "fixcrc" recipes store the re-masked CRC the
+    reference computes for the edited record, so the record passes the check with its new type."""
+    recs = _walk_clean(img)
+    n = len(img)
+    last_block = (n - 1) // BS
+    short_last = n % BS != 0
+
+    def not_last_in_block(i):
+        return i + 1 < len(recs) and recs[i + 1][0] // BS == recs[i][0] // BS
+
+    def fixcrc(off, length, typ):
+        body = bytes([typ]) + img[off + HDR : off + HDR + length]
+        c = ref.mask(ref.value(np.frombuffer(body, dtype=np.uint8)))
+        return ("set", off, int(c).to_bytes(4, "little").hex())
+
+    mid = [i for i in range(len(recs)) if not_last_in_block(i) and recs[i][1] > 1]
+    early = [i for i in mid if recs[i][0] // BS < last_block]
+    r = []
+    i = mid[len(mid) // 2]
+    r.append(("payload_flip_mid_block", [("xor", recs[i][0] + HDR + recs[i][1] // 2, 0x01)]))
+    i = mid[len(mid) // 3]
+    r.append(("crc_byte_flip", [("xor", recs[i][0] + 2, 0x80)]))
+    if early:
+        i = early[len(early) // 2]
+        r.append(("length_overrun_mid_file", [("set", recs[i][0] + 4, "ffff")]))
+    i = mid[len(mid) // 4]
+    L = recs[i][1] - 1
+    r.append(("length_shrink", [("set", recs[i][0] + 4, bytes([L & 0xFF, L >> 8]).hex())]))
+    i = mid[(2 * len(mid)) // 3]
+    r.append(("unknown_type_valid_crc", [("set", recs[i][0] + 6, "09"), fixcrc(recs[i][0], recs[i][1], 9)]))
+    i = mid[len(mid) // 5]
+    r.append(("zero_header_mid_block", [("set", recs[i][0], "00" * HDR)]))
+    firsts = [k for k in range(len(recs)) if recs[k][2] == 2 and recs[k][1] > 0]
+    if firsts:
+        k = firsts[len(firsts) // 2]
+        r.append(("first_fragment_flip", [("xor", recs[k][0] + HDR + recs[k][1] - 1, 0x40)]))
+    tails = [k for k in range(len(recs)) if recs[k][2] in (3, 4)]
+    if tails:
+        k = tails[len(tails) // 2]
+        r.append(("fragment_as_full_valid_crc", [("set", recs[k][0] + 6, "01"), fixcrc(recs[k][0], recs[k][1], 1)]))
+        r.append(("fragment_as_first_valid_crc", [("set", recs[k][0] + 6, "02"), fixcrc(recs[k][0], recs[k][1], 2)]))
+    fulls = [k for k in mid if recs[k][2] == 1]
+    if len(fulls) > 2:
+        k = fulls[len(fulls) // 2]
+        r.append(("full_as_middle_valid_crc", [("set", recs[k][0] + 6, "03"), fixcrc(recs[k][0], recs[k][1], 3)]))
+        k2 = fulls[len(fulls) // 2 + 1]
+        r.append(("full_as_first_then_full", [("set", recs[k2][0] + 6, "02"), fixcrc(recs[k2][0], recs[k2][1], 2)]))
+    lastrec = recs[-1]
+    if lastrec[1] > 2:
+        r.append(("truncate_inside_last_record", [("truncate", lastrec[0] + HDR + lastrec[1] // 2)]))
+    r.append(("truncate_inside_last_header", [("truncate", lastrec[0] + 3)]))
+    if short_last:
+        lr = [k for k in range(len(recs)) if recs[k][0] // BS == last_block and k + 1 < len(recs)]
+        if lr:
+            k = lr[len(lr) // 2]
+            r.append(("length_overrun_last_block", [("set", recs[k][0] + 4, "ffff")]))
+    r.append(("two_bad_records_same_block", [("xor", recs[mid[1]][0] + HDR, 0x01),
+                                             ("xor", recs[mid[1] + 1][0] + HDR + recs[mid[1] + 1][1] - 1, 0x01)]
+              if recs[mid[1] + 1][1] > 0 else [("xor", recs[mid[1]][0] + HDR, 0x01)]))
+    return r
+
+
+def apply_ops(img: bytes, ops) -> bytes:
+    b = bytearray(img)
+    for op in ops:
+        if op[0] == "xor":
+            b[op[1]] ^= op[2]
+        elif op[0] == "set":
+            v = bytes.fromhex(op[2])
+            b[op[1] : op[1] + len(v)] = v
+        elif op[0] == "truncate":
+            del b[op[1] :]
+    return bytes(b)
+
+
+def gen_log_corruptions() -> None:
+    """tests/golden/log/corruptions.json: what the REFERENCE's log::Reader (checksums on) delivers
+    from corrupted copies of the golden logs -- logical records (LastRecordOffset, length, FNV-1a-64)
+    and corruption reports (bytes, reason) -- pinning the batched verifier's replay of
+    log_reader.cc:59-263 (bad CRC drops the rest of the block, bad lengths, zero regions, unknown
+    types, fragment assembly, truncated tails)."""
+    import subprocess
+    import tempfile
+
+    ref = oracle.Reference()
+    with open(os.path.join(LOG_DIR, "manifest.json")) as f:
+        logs = json.load(f)["logs"]
+    cases = []
+    for lg in logs:
+        with open(os.path.join(LOG_DIR, lg["file"]), "rb") as f:
+            img = f.read()
+        for name, ops in [("clean", [])] + _corruption_recipes(img, ref):
+            bad = apply_ops(img, ops)
+            with tempfile.NamedTemporaryFile(suffix=".log") as t:
+                t.write(bad)
+                t.flush()
+                res = json.loads(subprocess.check_output([LOG_READER, t.name], text=True))
+            cases.append({"log": lg["name"], "name": name, "ops": [list(o) for o in ops], "records": res["records"],
+                          "reports": res["reports"]})
+    with open(os.path.join(LOG_DIR, "corruptions.json"), "w") as f:
+        json.dump({"generator": "tests/golden/gen_golden.py -> oracle/_ref/ref_logreader (reference log::Reader, "
+                                "checksums on)",
+                   "record": "[LastRecordOffset, length, fnv1a64 hex]", "report": "[bytes, Status::ToString()]",
+                   "cases": cases}, f, indent=0)
+    print(f"wrote {len(cases)} log corruption cases")
+
+
 if __name__ == "__main__":
-    main()
+    if "--log-corruptions" in sys.argv:
+        gen_log_corruptions()
+    else:
+        main()
+        gen_log_corruptions()

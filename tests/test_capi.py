@@ -14,8 +14,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "pdb_crc32c.h")
 
 
-def declared_functions():
-    src = open(HEADER).read()
+DIAG_HEADER = os.path.join(ROOT, "include", "pdb_crc32c_diag.h")
+
+
+def declared_functions(header=HEADER):
+    src = open(header).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(pdb_[a-z0-9_]+)\s*\(", src)))
 
@@ -41,6 +44,30 @@ def test_every_declared_symbol_is_exported(lib):
     assert not missing, missing
     # and the ctypes binding covers exactly the declared surface
     assert sorted(_native.SIGNATURES) == declared_functions()
+
+
+def test_product_exports_only_the_reference_interface(lib):
+    """libpdb_crc32c.so exports exactly include/pdb_crc32c.h (the reference interface plus
+    init / last_error): no diagnostics, no variant switch, no internal C++ symbols."""
+    out = subprocess.check_output(["nm", "-D", "--defined-only", build.LIB], text=True)
+    exported = sorted(set(re.findall(r" [TtWV] (\w+)$", out, flags=re.M)))
+    assert exported == declared_functions(), sorted(set(exported) ^ set(declared_functions()))
+    assert not [f for f in exported if "diag" in f or "variant" in f]
+
+
+def test_diag_library_is_separate_and_complete(lib):
+    """The bench / test library exports its header's functions only and is never loaded by the
+    product modules."""
+    from pebblesdb_amd import diag
+
+    out = subprocess.check_output(["nm", "-D", "--defined-only", build.DIAG_LIB], text=True)
+    exported = sorted(set(re.findall(r" [TtWV] (\w+)$", out, flags=re.M)))
+    assert exported == declared_functions(DIAG_HEADER)
+    assert sorted(diag.SIGNATURES) == declared_functions(DIAG_HEADER)
+    diag.lib()
+    for mod in ("pebblesdb_amd/crc32c.py", "pebblesdb_amd/_native.py", "pebblesdb_amd/table.py",
+                "pebblesdb_amd/log.py", "pebblesdb_amd/shard.py"):
+        assert "diag" not in open(os.path.join(ROOT, mod)).read().replace("diagnostic", ""), mod
 
 
 def test_flag_constants_match_the_python_mirror():

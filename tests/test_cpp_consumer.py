@@ -33,3 +33,28 @@ def test_cpp_consumer_runs_on_gpu():
                        timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "PASS" in r.stdout
+
+
+@pytest.mark.gpu
+def test_cpp_log_replay_matches_reference_reader(tmp_path):
+    """pdb::log::ReplayLog (one GPU verify batch + the log::Reader replay) on every corrupted log of
+    tests/golden/log/corruptions.json: records and corruption reports identical to what the
+    reference's own log::Reader delivered from the same bytes."""
+    import json
+
+    from test_log import CORR, _corrupted
+
+    exe = _compile()
+    paths = []
+    for i, case in enumerate(CORR):
+        p = tmp_path / f"case{i}.log"
+        p.write_bytes(_corrupted(case))
+        paths.append(str(p))
+    r = subprocess.run([exe, "--replay"] + paths, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    lines = r.stdout.strip().split("\n")
+    assert len(lines) == len(CORR)
+    for case, line in zip(CORR, lines):
+        got = json.loads(line)
+        assert got["records"] == case["records"], (case["log"], case["name"])
+        assert got["reports"] == case["reports"], (case["log"], case["name"])

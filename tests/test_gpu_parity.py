@@ -9,6 +9,8 @@ pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
 
+from pebblesdb_amd import diag  # noqa: E402  (bench / test infrastructure: synthetic input, A/B variants)
+
 
 @pytest.fixture(scope="module")
 def crc():
@@ -93,7 +95,7 @@ def test_sweep_offsets_lengths(crc, golden):
 def test_golden_batches_device(crc, golden, name):
     b = next(x for x in golden["batches"] if x["name"] == name)
     d_base = torch.empty(b["total_bytes"], dtype=torch.uint8, device="cuda")
-    crc.fill_splitmix(d_base, b["seed"])
+    diag.fill_splitmix(d_base, b["seed"])
     blk = crc.make_blocks(b["off"], b["len"], b["init"] if b["use_init"] else None)
     d_blk = crc.blocks_to_device(blk)
     got = _u32(crc.batch(d_base, d_blk, use_init=b["use_init"]))
@@ -108,7 +110,7 @@ def test_device_fill_matches_numpy(crc):
     for off in (0, 3, 8, 13):
         n = 4096 + 5
         d = torch.empty(n, dtype=torch.uint8, device="cuda")
-        crc.fill_splitmix(d, 301, byte_offset=off)
+        diag.fill_splitmix(d, 301, byte_offset=off)
         assert (d.cpu().numpy() == oracle.splitmix_bytes(n, 301, off)).all()
 
 
@@ -124,7 +126,7 @@ def test_device_fill_matches_numpy(crc):
 def test_fixed_stride_vs_oracle(crc, oracle_lib, stride, length, nblk, shift):
     total = shift + (nblk - 1) * stride + length
     d = torch.empty(total + 16, dtype=torch.uint8, device="cuda")
-    crc.fill_splitmix(d, 7 + stride)
+    diag.fill_splitmix(d, 7 + stride)
     view = d[shift : shift + total]
     for masked, init in ((False, None), (True, None), (False, 0xDEADBEEF)):
         got = _u32(crc.batch_fixed(view, stride, length, nblk, masked=masked, init=init))
@@ -139,7 +141,7 @@ def test_fixed_stride_vs_oracle(crc, oracle_lib, stride, length, nblk, shift):
 def test_verify_detects_single_byte_flip(crc):
     n, L = 2048, 4097
     d = torch.empty(n * L, dtype=torch.uint8, device="cuda")
-    crc.fill_splitmix(d, 99)
+    diag.fill_splitmix(d, 99)
     blk = crc.blocks_to_device(crc.make_blocks(np.arange(n) * L, np.full(n, L)))
     exp = crc.batch(d, blk, masked=True)
     ok, nbad = crc.verify(d, blk, exp, masked=True)
@@ -156,7 +158,7 @@ def test_full_size_config2_vs_oracle(crc, oracle_lib):
     against the oracle (multi-threaded) on the same bytes, plus idempotence of the launch."""
     nblk, L = 1 << 20, 4096
     d = torch.empty(nblk * L, dtype=torch.uint8, device="cuda")
-    crc.fill_splitmix(d, 301)
+    diag.fill_splitmix(d, 301)
     got = _u32(crc.batch_fixed(d, L, L, nblk))
     again = _u32(crc.batch_fixed(d, L, L, nblk))
     assert (got == again).all()
@@ -172,7 +174,7 @@ def test_fast_path_partial_groups(crc, oracle_lib, nblk):
     """4-KiB fast path (4 blocks per wave-iteration, 64-block result windows): every count
     around the wave / group / window boundaries, with seed and mask flags."""
     d = torch.empty(nblk * 4096, dtype=torch.uint8, device="cuda")
-    crc.fill_splitmix(d, 1000 + nblk)
+    diag.fill_splitmix(d, 1000 + nblk)
     host = d.cpu().numpy()
     blk = crc.make_blocks(np.arange(nblk) * 4096, np.full(nblk, 4096), np.full(nblk, 0x1234567))
     got = _u32(crc.batch_fixed(d, 4096, 4096, nblk, masked=True, init=0x1234567))
@@ -181,21 +183,15 @@ def test_fast_path_partial_groups(crc, oracle_lib, nblk):
 
 
 def test_all_fast_variants_bit_exact(crc, oracle_lib):
-    """The A/B variants selectable through pdb_diag_set_variant are all exact."""
-    from pebblesdb_amd._native import lib
-
+    """The A/B variants of the 4-KiB path (libpdb_crc32c_diag.so) are all exact."""
     nblk = 3 * 4096 * 4 + 7
     d = torch.empty(nblk * 4096, dtype=torch.uint8, device="cuda")
-    crc.fill_splitmix(d, 4242)
+    diag.fill_splitmix(d, 4242)
     exp = oracle_lib.batch(d.cpu().numpy(), crc.make_blocks(np.arange(nblk) * 4096, np.full(nblk, 4096)),
                            nthreads=8)
-    try:
-        for v in range(32):
-            lib().pdb_diag_set_variant(v)
-            got = _u32(crc.batch_fixed(d, 4096, 4096, nblk))
-            assert (got == exp).all(), f"variant {v}"
-    finally:
-        lib().pdb_diag_set_variant(0)
+    for v in range(32):
+        got = _u32(diag.batch_fixed(v, d, 4096, 4096, nblk))
+        assert (got == exp).all(), f"variant {v}"
 
 
 def test_device_entry_points_capture_into_hip_graph(crc, oracle_lib):
@@ -203,7 +199,7 @@ def test_device_entry_points_capture_into_hip_graph(crc, oracle_lib):
     captured hipGraph replays them and recomputes after the input changes."""
     nblk = 4096 + 3
     d = torch.empty(nblk * 4096, dtype=torch.uint8, device="cuda")
-    crc.fill_splitmix(d, 77)
+    diag.fill_splitmix(d, 77)
     blk = crc.blocks_to_device(crc.make_blocks(np.arange(nblk) * 4096 + 1, np.full(nblk, 4095)))
     out1 = torch.empty(nblk, dtype=torch.int32, device="cuda")
     out2 = torch.empty(nblk, dtype=torch.int32, device="cuda")
@@ -215,7 +211,7 @@ def test_device_entry_points_capture_into_hip_graph(crc, oracle_lib):
         crc.batch_fixed(d, 4096, 4096, nblk, out=out1)
         crc.batch(d, blk, out=out2)
     for seed in (78, 79):
-        crc.fill_splitmix(d, seed)
+        diag.fill_splitmix(d, seed)
         out1.zero_()
         out2.zero_()
         g.replay()
@@ -230,7 +226,7 @@ def test_device_entry_points_capture_into_hip_graph(crc, oracle_lib):
 def test_long_span_extend_device(crc, oracle_lib, n):
     """One span split into parallel segments + device tree combine."""
     d = torch.empty(max(n, 1) + 3, dtype=torch.uint8, device="cuda")
-    crc.fill_splitmix(d, 555 + n)
+    diag.fill_splitmix(d, 555 + n)
     view = d[3 : 3 + n]  # misaligned start
     init = 0x9E3779B9
     host = view.cpu().numpy()
@@ -243,7 +239,7 @@ def test_long_span_past_4gib(crc, oracle_lib):
     util/crc32c.cc:19-23,589, so it has no defined answer there; the oracle keeps size_t)."""
     n = (4 << 30) + 4099
     d = torch.empty(n, dtype=torch.uint8, device="cuda")
-    crc.fill_splitmix(d, 4242)
+    diag.fill_splitmix(d, 4242)
     got = crc.extend_device(0x12345678, d, n)
     host = d.cpu().numpy()
     del d
@@ -281,70 +277,94 @@ def test_scalar_extend_zero_copy_sizes(crc, oracle_lib):
 @pytest.mark.parametrize("variant", [12, 13, 14, 15, 16])
 def test_stream_variants_exact(crc, golden, oracle_lib, variant):
     """A/B variants of the descriptor / generic fixed paths (12-14: coalesced 16-B-piece stream
-    kernel; 15: 32-B pieces with packed 4-block trees): the golden sweep (every alignment x every length 0..300), the golden batches, and
-    unaligned / multi-round fixed strides, all against the reference's vectors and the oracle."""
-    from pebblesdb_amd._native import lib
-
-    try:
-        lib().pdb_diag_set_variant(variant)
-        sw = golden["sweep"]
-        buf = _materialize(sw["input"])
-        offs, lens = np.meshgrid(np.arange(sw["offsets"]), np.arange(sw["max_len"] + 1), indexing="ij")
-        blk = crc.make_blocks(offs.reshape(-1), lens.reshape(-1))
-        got = _u32(crc.batch(torch.from_numpy(buf).cuda(), crc.blocks_to_device(blk)))
-        exp = np.array(sw["crc"], dtype=np.uint64).reshape(-1).astype(np.uint32)
-        bad = np.nonzero(got != exp)[0]
-        assert bad.size == 0, f"{bad.size} sweep mismatches, first (off,len)={divmod(int(bad[0]), 301)}"
-        for b in golden["batches"]:
-            d_base = torch.empty(b["total_bytes"], dtype=torch.uint8, device="cuda")
-            crc.fill_splitmix(d_base, b["seed"])
-            blk = crc.make_blocks(b["off"], b["len"], b["init"] if b["use_init"] else None)
-            got = _u32(crc.batch(d_base, crc.blocks_to_device(blk), use_init=b["use_init"], masked=True))
-            assert (got == np.array(b["masked"], dtype=np.uint32)).all(), b["name"]
-        for stride, length, nblk, shift in ((4101, 4097, 777, 0), (1000, 999, 1000, 1), (65536 + 3, 65536 + 3, 40, 2),
-                                            (4096, 4096, 513, 4), (63, 63, 500, 2), (12345, 12289, 100, 3)):
-            total = shift + (nblk - 1) * stride + length
-            d = torch.empty(total + 16, dtype=torch.uint8, device="cuda")
-            crc.fill_splitmix(d, 7 + stride)
-            view = d[shift : shift + total]
-            got = _u32(crc.batch_fixed(view, stride, length, nblk, init=0xDEADBEEF))
-            blk = crc.make_blocks(np.arange(nblk) * stride, np.full(nblk, length), np.full(nblk, 0xDEADBEEF))
-            exp = oracle_lib.batch(view.cpu().numpy(), blk, flags=2, nthreads=8)
-            assert (got == exp).all(), (stride, length, int(np.nonzero(got != exp)[0][0]))
-    finally:
-        lib().pdb_diag_set_variant(0)
+    kernel; 15: 32-B pieces with packed 4-block trees; 16: the shipped any-length kernel): the
+    golden sweep (every alignment x every length 0..300), the golden batches, and unaligned /
+    multi-round fixed strides, all against the reference's vectors and the oracle."""
+    sw = golden["sweep"]
+    buf = _materialize(sw["input"])
+    offs, lens = np.meshgrid(np.arange(sw["offsets"]), np.arange(sw["max_len"] + 1), indexing="ij")
+    blk = crc.make_blocks(offs.reshape(-1), lens.reshape(-1))
+    got = _u32(diag.batch_desc(variant, torch.from_numpy(buf).cuda(), crc.blocks_to_device(blk)))
+    exp = np.array(sw["crc"], dtype=np.uint64).reshape(-1).astype(np.uint32)
+    bad = np.nonzero(got != exp)[0]
+    assert bad.size == 0, f"{bad.size} sweep mismatches, first (off,len)={divmod(int(bad[0]), 301)}"
+    for b in golden["batches"]:
+        d_base = torch.empty(b["total_bytes"], dtype=torch.uint8, device="cuda")
+        diag.fill_splitmix(d_base, b["seed"])
+        blk = crc.make_blocks(b["off"], b["len"], b["init"] if b["use_init"] else None)
+        flags = crc.MASK_OUTPUT | (crc.USE_INIT if b["use_init"] else 0)
+        got = _u32(diag.batch_desc(variant, d_base, crc.blocks_to_device(blk), flags=flags))
+        assert (got == np.array(b["masked"], dtype=np.uint32)).all(), b["name"]
+    for stride, length, nblk, shift in ((4101, 4097, 777, 0), (1000, 999, 1000, 1), (65536 + 3, 65536 + 3, 40, 2),
+                                        (4096, 4096, 513, 4), (63, 63, 500, 2), (12345, 12289, 100, 3)):
+        total = shift + (nblk - 1) * stride + length
+        d = torch.empty(total + 16, dtype=torch.uint8, device="cuda")
+        diag.fill_splitmix(d, 7 + stride)
+        view = d[shift : shift + total]
+        got = _u32(diag.batch_fixed(variant, view, stride, length, nblk, init=0xDEADBEEF))
+        blk = crc.make_blocks(np.arange(nblk) * stride, np.full(nblk, length), np.full(nblk, 0xDEADBEEF))
+        exp = oracle_lib.batch(view.cpu().numpy(), blk, flags=2, nthreads=8)
+        assert (got == exp).all(), (stride, length, int(np.nonzero(got != exp)[0][0]))
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("chunk", [0, 1 << 16, 3 << 20])
-def test_host_batches_grouped_and_verify_host(crc, golden, oracle_lib, chunk):
+def test_host_batches_grouped_and_verify_host(crc, golden, oracle_lib):
     """pdb_crc32c_batch_host / pdb_crc32c_verify_host over the golden Zipf and ragged batches
-    (empty blocks, unaligned offsets, blocks larger than a staging group), with the staging group
-    span forced small so one call runs many groups: CRCs equal the reference's, corrupted expected
-    values are counted and flagged exactly."""
-    from pebblesdb_amd._native import lib
+    (empty blocks, unaligned offsets, blocks larger than a staging group): CRCs equal the
+    reference's, corrupted expected values are counted and flagged exactly.  The same batches laid
+    out 300 MiB apart in one host buffer make one call run several 256-MiB staging groups through
+    the double-buffered pipeline; tests/host_staging_check.py repeats it all with the group span
+    forced down to 8 KiB / 3 MiB (PDB_HOST_CHUNK_BYTES, read once per process, so in a child)."""
+    gap = 300 << 20
+    parts = [b for b in golden["batches"] if b["total_bytes"] <= (64 << 20)]
+    for b in parts:
+        base = _materialize({"kind": "splitmix", "len": b["total_bytes"], "seed": b["seed"]})
+        use_init = b["use_init"]
+        blk = crc.make_blocks(b["off"], b["len"], b["init"] if use_init else None)
+        exp = np.array(b["crc"], dtype=np.uint64).astype(np.uint32)
+        got = crc.batch_host(base, blk, use_init=use_init)
+        assert (got == exp).all(), b["name"]
+        ok, nbad = crc.verify_host(base, blk, exp, masked=False, use_init=use_init)
+        assert nbad == 0 and ok.all(), b["name"]
+        bad = exp.copy()
+        flip = np.arange(0, len(bad), 7)
+        bad[flip] ^= 1
+        ok, nbad = crc.verify_host(base, blk, bad, masked=False, use_init=use_init)
+        assert nbad == len(flip), b["name"]
+        assert (ok[flip] == 0).all() and ok.sum() == len(bad) - len(flip), b["name"]
+    # three copies of two batches, 300 MiB apart: three staging groups in one call
+    big = np.zeros(3 * gap, dtype=np.uint8)
+    blks, exps = [], []
+    for k in range(3):
+        for b in parts[:2]:
+            o = k * gap + (k + 1) * 1000 + (0 if b is parts[0] else 100 << 20)
+            big[o : o + b["total_bytes"]] = _materialize({"kind": "splitmix", "len": b["total_bytes"], "seed": b["seed"]})
+            blk = crc.make_blocks(np.asarray(b["off"], dtype=np.int64) + o, b["len"], b["init"] if b["use_init"] else None)
+            blks.append(blk)
+            exps.append(np.array(b["crc"], dtype=np.uint64).astype(np.uint32))
+    assert not any(b["use_init"] for b in parts[:2])
+    blk, exp = np.concatenate(blks), np.concatenate(exps)
+    assert (crc.batch_host(big, blk) == exp).all()
+    ok, nbad = crc.verify_host(big, blk, exp, masked=False)
+    assert nbad == 0 and ok.all()
 
-    prev = lib().pdb_diag_set_host_chunk(chunk)
-    try:
-        for b in golden["batches"]:
-            if b["total_bytes"] > (64 << 20):
-                continue
-            base = _materialize({"kind": "splitmix", "len": b["total_bytes"], "seed": b["seed"]})
-            use_init = b["use_init"]
-            blk = crc.make_blocks(b["off"], b["len"], b["init"] if use_init else None)
-            exp = np.array(b["crc"], dtype=np.uint64).astype(np.uint32)
-            got = crc.batch_host(base, blk, use_init=use_init)
-            assert (got == exp).all(), b["name"]
-            ok, nbad = crc.verify_host(base, blk, exp, masked=False, use_init=use_init)
-            assert nbad == 0 and ok.all(), b["name"]
-            bad = exp.copy()
-            flip = np.arange(0, len(bad), 7)
-            bad[flip] ^= 1
-            ok, nbad = crc.verify_host(base, blk, bad, masked=False, use_init=use_init)
-            assert nbad == len(flip), b["name"]
-            assert (ok[flip] == 0).all() and ok.sum() == len(bad) - len(flip), b["name"]
-    finally:
-        lib().pdb_diag_set_host_chunk(prev)
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("chunk", [8192, 3 << 20])
+def test_host_staging_small_groups_subprocess(crc, chunk):
+    """The host batch / seal / verify entry points with the staging group span forced small (most
+    groups hold one or two blocks, big blocks their own group), in a child process that sets
+    PDB_HOST_CHUNK_BYTES before loading the library (tests/host_staging_check.py)."""
+    import os
+    import subprocess
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, PDB_HOST_CHUNK_BYTES=str(chunk))
+    r = subprocess.run([sys.executable, os.path.join(here, "host_staging_check.py")], env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "host staging ok" in r.stdout
 
 
 @pytest.mark.gpu

@@ -81,7 +81,7 @@ def test_server_parked_by_batches(crc, oracle_lib):
     import oracle
 
     d = torch.empty(64 * 4096, dtype=torch.uint8, device="cuda")
-    crc.fill_splitmix(d, 77)
+    __import__('pebblesdb_amd.diag', fromlist=['diag']).fill_splitmix(d, 77)
     host = d.cpu().numpy()
     blk = crc.make_blocks(np.arange(64) * 4096, np.full(64, 4096))
     exp_batch = oracle_lib.batch(host, blk)

@@ -11,6 +11,8 @@ pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
 
+from pebblesdb_amd import diag  # noqa: E402  (synthetic input, A/B variants)
+
 # CRC input length n = contents + type byte; the kernel's fast range is 4096 <= n <= 4352
 EDGE_N = [1, 2, 3, 4, 5, 15, 16, 17, 100, 1024, 4080, 4095, 4096, 4097, 4098, 4099, 4100, 4111, 4112,
           4113, 4127, 4128, 4167, 4170, 4175, 4336, 4337, 4351, 4352, 4353, 4354, 4368, 8191, 8192, 8193,
@@ -158,7 +160,7 @@ def test_fixed_stride_sst_range(crc, oracle_lib, length, shift):
     for stride in (length, length + 5):
         total = shift + (nblk - 1) * stride + length
         d = torch.empty(total + 16, dtype=torch.uint8, device="cuda")
-        crc.fill_splitmix(d, 3 + stride + shift)
+        diag.fill_splitmix(d, 3 + stride + shift)
         view = d[shift : shift + total]
         host = view.cpu().numpy()
         for masked, init in ((False, None), (True, None), (False, 0x12345678)):
@@ -173,9 +175,9 @@ def test_fixed_stride_sst_range(crc, oracle_lib, length, shift):
 
 
 def test_new_path_matches_previous_kernel(crc):
-    """Variant 30 routes the hooks through the previous any-length kernel: same trailers."""
+    """Variant 30 (diagnostics library) routes the hooks through the round-1 any-length kernel, 38
+    through the 8-block-group sized kernel: the same trailers as the shipped seal."""
     from pebblesdb_amd import table as T
-    from pebblesdb_amd._native import lib
 
     rng = np.random.Generator(np.random.PCG64(41))
     sizes = rng.integers(4095, 4352, size=5000)
@@ -185,16 +187,15 @@ def test_new_path_matches_previous_kernel(crc):
     h["offset"], h["size"] = offs, sizes
     d_h = T.handles_to_device(h)
     outs = []
-    for v in (0, 30, 38):  # 38: the 8-block-group variant of the sized kernel
-        lib().pdb_diag_set_variant(v)
-        try:
-            d = torch.from_numpy(img).cuda()
+    for v in (0, 30, 38):
+        d = torch.from_numpy(img).cuda()
+        if v == 0:
             T.seal_device(d, d_h)
-            outs.append(d.cpu().numpy())
-            ok, nbad = T.verify_device(d, d_h)
-            assert int(nbad.item()) == 0, v
-        finally:
-            lib().pdb_diag_set_variant(0)
+        else:
+            diag.sst(v, d, d_h, seal=True)
+        outs.append(d.cpu().numpy())
+        ok, nbad = T.verify_device(d, d_h)
+        assert int(nbad.item()) == 0, v
     assert (outs[0] == outs[1]).all() and (outs[0] == outs[2]).all()
 
 
@@ -275,27 +276,22 @@ def test_host_batch_picks_size_class(crc, oracle_lib, lo, hi):
 
 
 def test_sized_kernels_match_generic_kernel(crc):
-    """Variant 40 ignores the hints (crc_stream16_kernel), 41 runs the 1-KiB kernel with 4-block
-    groups, 50-52 the lane-per-record kernels on every list (larger blocks on their whole-wave slow
-    path), 53 the <= 256-B class on crc_rec256_kernel: identical CRCs on a mixed batch."""
-    from pebblesdb_amd._native import lib
-
+    """Diagnostics-library variants -- 40 ignores the hints (crc_stream16_kernel), 41 runs the 1-KiB
+    kernel with 4-block groups, 50-52 the lane-per-record kernels on every list (larger blocks on
+    their whole-wave slow path), 53 the <= 256-B class on crc_rec256_kernel, 54-58 the other
+    lane-per-record A/B forms: identical CRCs on a mixed batch, for every size hint."""
     rng = np.random.Generator(np.random.PCG64(81))
     sizes = np.concatenate([rng.integers(1024, 1281, size=4000), rng.integers(4096, 4353, size=4000),
                             rng.integers(0, 300, size=4000), rng.integers(0, 20000, size=2000)])
     rng.shuffle(sizes)
     base, blk = _desc_case(crc, sizes, 82)
     d_base, d_blk = torch.from_numpy(base).cuda(), crc.blocks_to_device(blk)
-    res = []
-    for v in (0, 40, 41, 50, 51, 52, 53):
-        lib().pdb_diag_set_variant(v)
-        try:
-            res.append([crc.batch(d_base, d_blk, size_hint=h).cpu().numpy() for h in ("1k", "4k", "256", "512", "1023")])
-        finally:
-            lib().pdb_diag_set_variant(0)
-    for other in res[1:]:
-        for a, b in zip(res[0], other):
-            assert (a == b).all()
+    hints = (crc.SIZE_1K, crc.SIZE_4K, crc.SIZE_256, crc.SIZE_512, crc.SIZE_1023)
+    ref = [crc.batch(d_base, d_blk, size_hint=h).cpu().numpy() for h in ("1k", "4k", "256", "512", "1023")]
+    for v in (0, 40, 41, 50, 51, 52, 53, 54, 55, 56, 57, 58):
+        for a, hint in zip(ref, hints):
+            b = diag.batch_desc(v, d_base, d_blk, flags=hint).cpu().numpy()
+            assert (a == b).all(), (v, hint)
 
 
 @pytest.mark.parametrize("variant", [0, 30])
@@ -325,22 +321,26 @@ def test_handles_outside_image_are_reported_not_followed(crc, oracle_lib, varian
     d_img = torch.from_numpy(np.concatenate([img[:total], guard])).cuda()
     d_h = T.handles_to_device(h)
     before = d_img.cpu().numpy().copy()
-    lib().pdb_diag_set_variant(variant)
-    try:
-        sp = int(torch.cuda.current_stream().cuda_stream)
+    sp = int(torch.cuda.current_stream().cuda_stream)
+    dl = diag.lib()
+    if variant == 0:
         assert lib().pdb_sst_seal_device(d_img.data_ptr(), total, d_h.data_ptr(), len(sizes), sp) == 0
-        after = d_img.cpu().numpy()
-        good = np.setdiff1d(np.arange(len(sizes)), bad)
-        assert (_trailers(after, offs[good], sizes[good]) == exp[good]).all()
-        assert (after[total:] == before[total:]).all(), "seal wrote outside the image"
-        ok = torch.empty(len(sizes), dtype=torch.uint8, device="cuda")
-        nbad = torch.zeros(1, dtype=torch.int32, device="cuda")
+    else:
+        assert dl.pdb_diag_sst(variant, d_img.data_ptr(), total, d_h.data_ptr(), len(sizes), 1, None, None, sp) == 0
+    after = d_img.cpu().numpy()
+    good = np.setdiff1d(np.arange(len(sizes)), bad)
+    assert (_trailers(after, offs[good], sizes[good]) == exp[good]).all()
+    assert (after[total:] == before[total:]).all(), "seal wrote outside the image"
+    ok = torch.empty(len(sizes), dtype=torch.uint8, device="cuda")
+    nbad = torch.zeros(1, dtype=torch.int32, device="cuda")
+    if variant == 0:
         assert lib().pdb_sst_verify_device(d_img.data_ptr(), total, d_h.data_ptr(), len(sizes), ok.data_ptr(),
                                            nbad.data_ptr(), sp) == 0
-        okn = ok.cpu().numpy()
-        assert int(nbad.item()) == len(bad) and (okn[bad] == 0).all() and (okn[good] == 1).all()
-    finally:
-        lib().pdb_diag_set_variant(0)
+    else:
+        assert dl.pdb_diag_sst(variant, d_img.data_ptr(), total, d_h.data_ptr(), len(sizes), 0, ok.data_ptr(),
+                               nbad.data_ptr(), sp) == 0
+    okn = ok.cpu().numpy()
+    assert int(nbad.item()) == len(bad) and (okn[bad] == 0).all() and (okn[good] == 1).all()
 
 
 def test_sst_crc_device_matches_seal(crc, oracle_lib):
@@ -376,7 +376,7 @@ def test_fixed_stride_small_classes(crc, oracle_lib, length):
         for stride in (length, length + 5):
             total = shift + (nblk - 1) * stride + length
             d = torch.empty(total + 16, dtype=torch.uint8, device="cuda")
-            crc.fill_splitmix(d, 7 * length + stride + shift)
+            diag.fill_splitmix(d, 7 * length + stride + shift)
             view = d[shift : shift + total]
             host = view.cpu().numpy()
             for masked, init in ((False, None), (True, None), (False, 0x0BADF00D)):

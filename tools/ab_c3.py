@@ -11,6 +11,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from bench import zipf_kib_sizes  # noqa: E402
 from pebblesdb_amd import crc32c  # noqa: E402
+from pebblesdb_amd import diag  # noqa: E402
 from pebblesdb_amd._native import lib  # noqa: E402
 
 variants = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "0,8").split(",")]
@@ -23,13 +24,12 @@ sizes = sizes[:n]
 offs = np.concatenate([[0], np.cumsum(sizes)[:-1]])
 total = int(sizes.sum())
 d = torch.empty(total, dtype=torch.uint8, device="cuda")
-crc32c.fill_splitmix(d, 303)
+diag.fill_splitmix(d, 303)
 blk = crc32c.blocks_to_device(crc32c.make_blocks(offs, sizes))
 out = torch.empty(n, dtype=torch.int32, device="cuda")
 ref = None
 for v in variants:
-    lib().pdb_diag_set_variant(v)
-    crc32c.batch(d, blk, out=out)
+    diag.batch_desc(v, d, blk, out=out)
     torch.cuda.synchronize()
     if ref is None:
         ref = out.clone()
@@ -37,21 +37,19 @@ for v in variants:
 # warm the GPU first: a cold GPU runs its first ~40 launches slower while clocks / power settle
 # (DESIGN.md §6), which would bias whichever variant is timed first
 for _ in range(15):
-    crc32c.batch(d, blk, out=out)
+    diag.batch_desc(0, d, blk, out=out)
 torch.cuda.synchronize()
 s = torch.cuda.current_stream()
 times = {v: [] for v in variants}
 for r in range(rounds):
     for v in variants:
-        lib().pdb_diag_set_variant(v)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(s)
         for _ in range(3):
-            crc32c.batch(d, blk, out=out)
+            diag.batch_desc(v, d, blk, out=out)
         e1.record(s)
         torch.cuda.synchronize()
         times[v].append(e0.elapsed_time(e1) / 3)
-lib().pdb_diag_set_variant(0)
 algo = total + 20 * n
 print(json.dumps({v: {"median_ms": round(float(np.median(t)), 4),
                       "GB/s": round(algo / (np.median(t) * 1e-3) / 1e9, 1)} for v, t in times.items()}, indent=1))

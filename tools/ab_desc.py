@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Interleaved A/B of descriptor-path variants (pdb_diag_set_variant) on descriptor workloads:
+"""Interleaved A/B of descriptor-path variants (per-call variant (pdb_diag_batch_*)) on descriptor workloads:
   wal  : 32-KiB log blocks of 1055-B records (bench.py --workload wal)
   sst  : back-to-back blocks of 4167-4175 B (sstable data blocks + type byte, any alignment)
   c3   : Zipf 1-64 KiB (BASELINE config 3)
@@ -17,6 +17,8 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from bench import wal_layout, zipf_kib_sizes  # noqa: E402
 from pebblesdb_amd import crc32c  # noqa: E402
+from pebblesdb_amd import diag  # noqa: E402
+_HINT_FLAGS = {None: 0, '1k': 0x4, '4k': 0x8, '256': 0x10, '512': 0x20, '1023': 0x40}
 from pebblesdb_amd._native import lib  # noqa: E402
 
 variants = [int(x) for x in sys.argv[1].split(",")]
@@ -24,9 +26,9 @@ works = sys.argv[2].split(",") if len(sys.argv) > 2 else ["wal", "sst", "c3", "s
 total = 4 << 30
 crc32c.init_device(0)
 d = torch.empty(total + (1 << 20), dtype=torch.uint8, device="cuda")
-crc32c.fill_splitmix(d, 11)
+diag.fill_splitmix(d, 11)
 for _ in range(20):
-    crc32c.batch_fixed(d, 4096, 4096, total // 4096)
+    diag.batch_fixed(0, d, 4096, 4096, total // 4096)
 
 
 def layout(w):
@@ -55,8 +57,7 @@ for w in works:
     out = torch.empty(n, dtype=torch.int32, device="cuda")
     ref = None
     for v in variants:
-        lib().pdb_diag_set_variant(v)
-        crc32c.batch(d, blk, out=out, size_hint=HINT.get(w))
+        diag.batch_desc(v, d, blk, out=out, flags=_HINT_FLAGS[HINT.get(w)])
         torch.cuda.synchronize()
         if ref is None:
             ref = out.clone()
@@ -64,15 +65,13 @@ for w in works:
     times = {v: [] for v in variants}
     for _ in range(4):
         for v in variants:
-            lib().pdb_diag_set_variant(v)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(3):
-                crc32c.batch(d, blk, out=out, size_hint=HINT.get(w))
+                diag.batch_desc(v, d, blk, out=out, flags=_HINT_FLAGS[HINT.get(w)])
             e1.record()
             torch.cuda.synchronize()
             times[v].append(e0.elapsed_time(e1) / 3)
     algo = int(lens.sum()) + 20 * n
     res[w] = {v: round(algo / (np.median(t) * 1e-3) / 1e9, 1) for v, t in times.items()}
-lib().pdb_diag_set_variant(0)
 print(json.dumps(res))

@@ -10,6 +10,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from pebblesdb_amd import crc32c  # noqa: E402
+from pebblesdb_amd import diag  # noqa: E402
 from pebblesdb_amd._native import lib  # noqa: E402
 
 variants = [int(x) for x in sys.argv[1].split(",")]
@@ -17,9 +18,9 @@ lens = [int(x) for x in sys.argv[2].split(",")]
 total = 4 << 30
 crc32c.init_device(0)
 d = torch.empty(total + (1 << 20), dtype=torch.uint8, device="cuda")
-crc32c.fill_splitmix(d, 7)
+diag.fill_splitmix(d, 7)
 for _ in range(20):
-    crc32c.batch_fixed(d, 4096, 4096, total // 4096)
+    diag.batch_fixed(0, d, 4096, 4096, total // 4096)
 res = {}
 for L in lens:
     stride = L + 4
@@ -28,22 +29,19 @@ for L in lens:
     ref = None
     times = {v: [] for v in variants}
     for v in variants:
-        lib().pdb_diag_set_variant(v)
-        crc32c.batch_fixed(d, stride, L, n, out=out)
+        diag.batch_fixed(v, d, stride, L, n, out=out)
         torch.cuda.synchronize()
         if ref is None:
             ref = out.clone()
         assert torch.equal(out, ref), (L, v)
     for _ in range(4):
         for v in variants:
-            lib().pdb_diag_set_variant(v)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(3):
-                crc32c.batch_fixed(d, stride, L, n, out=out)
+                diag.batch_fixed(v, d, stride, L, n, out=out)
             e1.record()
             torch.cuda.synchronize()
             times[v].append(e0.elapsed_time(e1) / 3)
     res[L] = {v: round(n * L / (np.median(t) * 1e-3) / 1e9, 1) for v, t in times.items()}
-lib().pdb_diag_set_variant(0)
 print(json.dumps(res, indent=1))

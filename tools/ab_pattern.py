@@ -16,18 +16,18 @@ rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 nblk = 1 << 20
 crc32c.init_device(0)
 d = torch.empty(nblk * 4096, dtype=torch.uint8, device="cuda")
-crc32c.fill_splitmix(d, 301)
+diag.fill_splitmix(d, 301)
 o = torch.zeros(1, dtype=torch.int32, device="cuda")
 # warm the GPU first: a cold GPU runs its first ~40 launches slower while clocks / power settle
 # (DESIGN.md §6), which would bias whichever variant is timed first
 for _ in range(60):
-    check(lib().pdb_diag_read_pattern4k(d.data_ptr(), nblk, variants[0], o.data_ptr(), torch.cuda.current_stream().cuda_stream))
+    diag.read_pattern4k(d, nblk, variants[0], o)
 torch.cuda.synchronize()
 s = torch.cuda.current_stream()
 times = {v: [] for v in variants}
 for r in range(rounds):
     for v in variants:
-        f = lambda: check(lib().pdb_diag_read_pattern4k(d.data_ptr(), nblk, v, o.data_ptr(), s.cuda_stream))
+        f = lambda: diag.read_pattern4k(d, nblk, v, o, s)
         f()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(s)

@@ -15,12 +15,14 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from pebblesdb_amd import crc32c  # noqa: E402
+from pebblesdb_amd import diag  # noqa: E402
+_HINT_FLAGS = {None: 0, '1k': 0x4, '4k': 0x8, '256': 0x10, '512': 0x20, '1023': 0x40}
 from pebblesdb_amd._native import lib  # noqa: E402
 
 crc32c.init_device(0)
 total = 2 << 30
 d = torch.empty(total + (1 << 20), dtype=torch.uint8, device="cuda")
-crc32c.fill_splitmix(d, 11)
+diag.fill_splitmix(d, 11)
 
 
 def timeit(fn, reps=10):
@@ -67,17 +69,13 @@ for name, sizes in cases.items():
              ("quadrec9", "512", 58),
              ("generic", None, 40), ("lanerec9_slow", "256", 0)))
     for tag, hint, var in tags:
-        lib().pdb_diag_set_variant(var)
-        try:
-            ms = timeit(lambda: crc32c.batch(d, d_blk, out=out, size_hint=hint))
-            got = out.cpu().numpy().copy()
-        finally:
-            lib().pdb_diag_set_variant(0)
+        ms = timeit(lambda: diag.batch_desc(var, d, d_blk, out=out, flags=_HINT_FLAGS[hint]))
+        got = out.cpu().numpy().copy()
         ref = got if ref is None else ref
         row[tag] = {"ms": round(ms, 4), "GB/s": round(nbytes / ms / 1e6, 1), "same": bool((got == ref).all())}
     res[name] = row
     del d_blk, out
 L, n = 431, total // 431
-ms = timeit(lambda: crc32c.batch_fixed(d[3:], L, L, n))
+ms = timeit(lambda: diag.batch_fixed(0, d[3:], L, L, n))
 res["fixed_stride_431"] = {"ms": round(ms, 4), "GB/s": round((n * L + 4 * n) / ms / 1e6, 1)}
 print(json.dumps(res))

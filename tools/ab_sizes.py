@@ -18,7 +18,7 @@ lens = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else
 total = 4 << 30
 crc32c.init_device(0)
 d = torch.empty(total + (1 << 20), dtype=torch.uint8, device="cuda")
-crc32c.fill_splitmix(d, 7)
+diag.fill_splitmix(d, 7)
 res = {}
 
 
@@ -36,12 +36,12 @@ def timeit(fn, reps=10):
 
 
 for _ in range(20):  # warm the GPU
-    crc32c.batch_fixed(d, 4096, 4096, total // 4096)
+    diag.batch_fixed(0, d, 4096, 4096, total // 4096)
 for L in lens:
     for stride in (L + 4, (L + 15) // 16 * 16):
         n = total // stride
         out = torch.empty(n, dtype=torch.int32, device="cuda")
-        ms = timeit(lambda: crc32c.batch_fixed(d, stride, L, n, out=out))
+        ms = timeit(lambda: diag.batch_fixed(0, d, stride, L, n, out=out))
         res[f"fixed L={L} stride={stride}"] = round(n * L / (ms * 1e-3) / 1e9, 1)
     # sstable hook, every block `L - 1` contents + type
     n = total // (L + 4)

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Interleaved A/B of the sstable hooks (pdb_sst_seal_device / pdb_sst_verify_device) across
-pdb_diag_set_variant values on bench.py's sst image (1 M blocks of 4166-4174 B + type + trailer).
+diagnostics-library variants (pdb_diag_sst) on bench.py's sst image (1 M blocks of 4166-4174 B + type + trailer).
 argv[1] = variants (e.g. 0,18).  Prints one JSON object (GB/s of algorithmic bytes, median)."""
 import json
 import os
@@ -12,6 +12,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from pebblesdb_amd import crc32c  # noqa: E402
 from pebblesdb_amd import table as T  # noqa: E402
+from pebblesdb_amd import diag  # noqa: E402
 from pebblesdb_amd._native import lib  # noqa: E402
 
 variants = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "0,18").split(",")]
@@ -22,7 +23,7 @@ sizes = rng.integers(4166, 4175, size=nblk).astype(np.int64)
 offs = np.concatenate([[0], np.cumsum(sizes + 5)[:-1]])
 total = int(offs[-1] + sizes[-1] + 5)
 data = torch.empty(total, dtype=torch.uint8, device="cuda")
-crc32c.fill_splitmix(data, 301)
+diag.fill_splitmix(data, 301)
 data[torch.from_numpy(offs + sizes).cuda()] = 0
 h = np.zeros(nblk, dtype=crc32c.HANDLE_DTYPE)
 h["offset"], h["size"] = offs, sizes
@@ -30,13 +31,14 @@ d_h = T.handles_to_device(h)
 T.seal_device(data, d_h)
 ref = data.clone()
 for _ in range(20):
-    crc32c.batch_fixed(data, 4096, 4096, total // 4096 - 1)
+    diag.batch_fixed(0, data, 4096, 4096, total // 4096 - 1)
 res = {"seal": {}, "verify": {}}
 times = {(m, v): [] for m in res for v in variants}
 for v in variants:  # every variant seals the same bytes and verifies them all
-    lib().pdb_diag_set_variant(v)
-    T.seal_device(data, d_h)
-    ok, nbad = T.verify_device(data, d_h)
+    diag.sst(v, data, d_h, seal=True)
+    ok = torch.empty(nblk, dtype=torch.uint8, device="cuda")
+    nbad = torch.zeros(1, dtype=torch.int32, device="cuda")
+    diag.sst(v, data, d_h, seal=False, ok=ok, nbad=nbad)
     torch.cuda.synchronize()
     assert torch.equal(data, ref) and (int(nbad.item()) == 0 or v >= 90), v  # >= 90: wrong by design
 ok = torch.empty(nblk, dtype=torch.uint8, device="cuda")
@@ -44,20 +46,18 @@ nbad = torch.zeros(1, dtype=torch.int32, device="cuda")
 sp = int(torch.cuda.current_stream().cuda_stream)
 for _ in range(4):
     for v in variants:
-        lib().pdb_diag_set_variant(v)
         for m in res:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(3):
                 if m == "seal":
-                    lib().pdb_sst_seal_device(data.data_ptr(), total, d_h.data_ptr(), nblk, sp)
+                    diag.lib().pdb_diag_sst(v, data.data_ptr(), total, d_h.data_ptr(), nblk, 1, None, None, sp)
                 else:
-                    lib().pdb_sst_verify_device(data.data_ptr(), total, d_h.data_ptr(), nblk, ok.data_ptr(),
-                                                nbad.data_ptr(), sp)
+                    diag.lib().pdb_diag_sst(v, data.data_ptr(), total, d_h.data_ptr(), nblk, 0, ok.data_ptr(),
+                                            nbad.data_ptr(), sp)
             e1.record()
             torch.cuda.synchronize()
             times[(m, v)].append(e0.elapsed_time(e1) / 3)
-lib().pdb_diag_set_variant(0)
 hashed = int((sizes + 1).sum())
 for (m, v), t in times.items():
     algo = hashed + nblk * (4 + 16 + (1 if m == "verify" else 0))

@@ -21,6 +21,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import oracle  # noqa: E402  (checker only)
 from pebblesdb_amd import crc32c  # noqa: E402
+from pebblesdb_amd import diag  # noqa: E402
 from pebblesdb_amd._native import lib  # noqa: E402
 
 GIB = float(1 << 30)
@@ -41,7 +42,7 @@ def main():
     res = {"metric": "copy-inclusive GiB/s (host-resident blocks)", "blocks": NBLK}
     # C2 blocks, pageable and pinned
     d = torch.empty(NBLK * 4096, dtype=torch.uint8, device="cuda")
-    crc32c.fill_splitmix(d, 301)
+    diag.fill_splitmix(d, 301)
     page = d.cpu().numpy()
     pin_t = torch.empty(NBLK * 4096, dtype=torch.uint8, pin_memory=True)
     pin_t.copy_(d)
@@ -61,7 +62,7 @@ def main():
     # sstable image: contents 4096 B + type byte + 4-B trailer, stride 4101
     L, stride = 4096, 4101
     img_d = torch.empty(NBLK * stride, dtype=torch.uint8, device="cuda")
-    crc32c.fill_splitmix(img_d, 302)
+    diag.fill_splitmix(img_d, 302)
     img = img_d.cpu().numpy().copy()
     img[L::stride] = 0  # type byte kNoCompression
     h = np.zeros(NBLK, dtype=[("offset", "<u8"), ("size", "<u8")])

@@ -19,7 +19,9 @@ step() {  # step <name> <timeout> <cmd...>
 }
 for s in "$@"; do
   case "$s" in
-    tests) step tests 900 python -m pytest tests -m gpu -x -q ;;
+    tests) step tests 1000 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread ;;
+    cold) step cold 300 python tools/cold_start.py ;;
+    bench_driver) step bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --diag ;;
     bench_sst) step bench_sst 600 python bench.py --workload sstable --no-cpu-baseline --no-copy-inclusive ;;

@@ -39,14 +39,7 @@ int main(void) {
     const double t0 = now_s();
     for (int i = 0; i < reps; ++i) sink ^= pdb_crc32c_extend(i, buf + (i & 7), n);
     const double dt = (now_s() - t0) / reps;
-    uint64_t st[4] = {0, 0, 0, 0};
-    const int box = pdb_diag_server_stats(st); /* parks the server: its last instance's counters */
     printf("%s\"%zu\": {\"us_per_call\": %.3f, \"reps\": %d", k ? ", " : "", n, dt * 1e6, reps);
-    if (box >= 0 && st[0])
-      printf(", \"server\": {\"box\": \"%s\", \"requests\": %llu, \"gpu_us_per_request\": %.3f, "
-             "\"polls_per_request\": %.2f, \"life_ms\": %.2f}",
-             box ? "device" : "host", (unsigned long long)st[0], st[1] * 0.01 / st[0], (double)st[2] / st[0],
-             st[3] * 1e-5);
     printf("}");
     fflush(stdout);
   }

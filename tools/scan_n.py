@@ -15,9 +15,9 @@ from pebblesdb_amd._native import check, lib  # noqa: E402
 variant = int(sys.argv[1]) if len(sys.argv) > 1 else 0
 ns = [4096, 16384, 65536, 262144, 524288, 1 << 20]
 crc32c.init_device(0)
-lib().pdb_diag_set_variant(variant)
+
 d = torch.empty((1 << 20) * 4096, dtype=torch.uint8, device="cuda")
-crc32c.fill_splitmix(d, 301)
+diag.fill_splitmix(d, 301)
 out = torch.empty(1 << 20, dtype=torch.int32, device="cuda")
 o = torch.zeros(1, dtype=torch.int32, device="cuda")
 s = torch.cuda.current_stream()
@@ -39,8 +39,8 @@ def timeit(f, reps=20):
 
 res = {"crc": {}, "pattern": {}, "empty_launch": None}
 for n in ns:
-    res["crc"][n] = timeit(lambda: crc32c.batch_fixed(d, 4096, 4096, n, out=out))
-    res["pattern"][n] = timeit(lambda: check(lib().pdb_diag_read_pattern4k(d.data_ptr(), n, 8, o.data_ptr(), s.cuda_stream)))
+    res["crc"][n] = timeit(lambda: diag.batch_fixed(variant, d, 4096, 4096, n, out=out))
+    res["pattern"][n] = timeit(lambda: diag.read_pattern4k(d, n, 8, o, s))
 for k in ("crc", "pattern"):
     x = np.array(ns, dtype=float)
     y = np.array([res[k][n] for n in ns])

@@ -18,7 +18,7 @@ s = torch.cuda.current_stream()
 for gib in (1, 4, 16):
     n = gib << 30
     d = torch.empty(n, dtype=torch.uint8, device="cuda")
-    crc32c.fill_splitmix(d, 9)
+    diag.fill_splitmix(d, 9)
     words = int(lib().pdb_crc32c_extend_scratch_words(n))
     scratch = torch.empty(words, dtype=torch.int32, device="cuda")
     out = torch.empty(1, dtype=torch.int32, device="cuda")
