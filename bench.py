@@ -86,6 +86,36 @@ def zipf_kib_sizes(n: int, seed: int, kmax: int = 64) -> np.ndarray:
     return (rng.choice(k, size=n, p=p) * 1024).astype(np.int64)
 
 
+def sst_layout(nblk: int, seed: int):
+    """The sst_* workloads' image: `nblk` blocks whose contents are 4166..4174 B (db_bench's data
+    blocks flush just past the 4-KiB block_size), each followed by its 5-byte
+    trailer.  Returns (sizes, offsets, image bytes)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    sizes = rng.integers(4166, 4175, size=nblk).astype(np.int64)
+    offs = np.concatenate([[0], np.cumsum(sizes + 5)[:-1]])
+    return sizes, offs, int(offs[-1] + sizes[-1] + 5)
+
+
+def c3_plan(c3_bytes: int, world: int) -> np.ndarray:
+    """BASELINE config 3 for `world` ranks: ONE Zipf 1-64 KiB size list (seed 301) of world x
+    c3_bytes, which rank 0 splits into contiguous byte-balanced ranges (weak scaling by bytes)."""
+    want = c3_bytes * world
+    sizes = zipf_kib_sizes(int(want / (13.5 * 1024) * 1.1) + 16, 301)
+    return sizes[: int(np.searchsorted(np.cumsum(sizes), want, side="right"))]
+
+
+def gather_rank_rows(row, world: int, cdev, dist=None) -> list:
+    """All ranks' small integer rows on every rank (one all_gather, outside the timed region)."""
+    import torch
+
+    mine = torch.tensor([int(x) for x in row], dtype=torch.int64, device=cdev)
+    if dist is None or world == 1:
+        return [[int(x) for x in mine.cpu().tolist()]]
+    allr = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(allr, mine)
+    return [[int(x) for x in v.cpu().tolist()] for v in allr]
+
+
 def main():
     args = parse()
     import torch
@@ -112,11 +142,14 @@ def main():
     stream = torch.cuda.current_stream()
 
     # ---- the rank's shard index: scattered from rank 0 over RCCL (the only collective) -------
+    c3_sizes = None
     if args.workload == "c3":
-        n_total = 0
+        # ONE Zipf 1-64 KiB list of world x c3_bytes (seed 301), split into contiguous ranges of
+        # ~equal BYTES by rank 0 (shard.byte_balanced_ranges) and broadcast: weak scaling by bytes
+        c3_sizes = c3_plan(args.c3_bytes, world)
+        lo, hi = scatter_block_ranges(len(c3_sizes), world, rank, cdev, dist if distributed else None, lens=c3_sizes)
     else:
-        n_total = args.nblk * world
-    lo, hi = scatter_block_ranges(n_total, world, rank, cdev, dist if distributed else None)
+        lo, hi = scatter_block_ranges(args.nblk * world, world, rank, cdev, dist if distributed else None)
 
     # ---- synthetic, device-resident input ---------------------------------------------------
     if args.workload == "c2":
@@ -155,10 +188,7 @@ def main():
         from pebblesdb_amd._native import check, lib
 
         nblk = hi - lo
-        rng = np.random.Generator(np.random.PCG64(301 + rank))
-        sizes = rng.integers(4166, 4175, size=nblk).astype(np.int64)
-        offs = np.concatenate([[0], np.cumsum(sizes + 5)[:-1]])
-        total = int(offs[-1] + sizes[-1] + 5)
+        sizes, offs, total = sst_layout(nblk, 301 + rank)
         data = torch.empty(total, dtype=torch.uint8, device=dev)
         diag.fill_splitmix(data, 301 + rank)
         data[torch.from_numpy(offs + sizes).to(dev)] = 0  # kNoCompression type bytes
@@ -220,11 +250,9 @@ def main():
                                 " -> type||payload fragments (descriptor list)",
                     "blocks_per_gpu": nblk, "bytes_per_gpu": hashed}
     else:
-        # c3: Zipf 1..64 KiB blocks packed back to back, args.c3_bytes per GPU
-        sizes = zipf_kib_sizes(int(args.c3_bytes / (13.5 * 1024) * 1.1) + 16, 301 + rank)
-        cs = np.cumsum(sizes)
-        n = int(np.searchsorted(cs, args.c3_bytes, side="right"))
-        sizes = sizes[:n]
+        # c3: Zipf 1..64 KiB blocks packed back to back, this rank's byte-balanced range of the list
+        sizes = c3_sizes[lo:hi]
+        n = len(sizes)
         offs = np.concatenate([[0], np.cumsum(sizes)[:-1]])
         total = int(sizes.sum())
         data = torch.empty(total, dtype=torch.uint8, device=dev)
@@ -239,7 +267,7 @@ def main():
         def step():
             crc32c.batch(data, d_blk, out=out)
 
-        workload = {"workload": "c3: Zipf 1-64 KiB blocks, packed, descriptor list",
+        workload = {"workload": "c3: Zipf 1-64 KiB blocks, packed, descriptor list (byte-balanced rank ranges)",
                     "blocks_per_gpu": nblk, "bytes_per_gpu": hashed}
     algo_bytes = hashed + 4 * nblk + (16 * nblk if args.workload in ("c3", "wal", "wal100", "wal400") else 0)
     if args.workload == "sst_verify":  # + the 4-B stored trailer read, 16-B handle, 1-B ok written
@@ -281,19 +309,20 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall_max = float(t.item())
 
-    # checksum of checksums (outside the timed region) gathered to rank 0
-    xs = torch.tensor([int(np.bitwise_xor.reduce(out.cpu().numpy().view(np.uint32)))], dtype=torch.int64,
-                      device=cdev)
-    if distributed:
-        allx = [torch.zeros_like(xs) for _ in range(world)]
-        dist.all_gather(allx, xs)
-        xor_all = 0
-        for v in allx:
-            xor_all ^= int(v.item())
-    else:
-        xor_all = int(xs.item())
+    # per-rank facts (outside the timed region) gathered to rank 0: device, bytes hashed, kernel
+    # time, checksum of checksums -- the SCALE record shows which GPUs RCCL actually saw
+    props = torch.cuda.get_device_properties(gpu)
+    pci = int(getattr(props, "pci_bus_id", -1))
+    xor_local = int(np.bitwise_xor.reduce(out.cpu().numpy().view(np.uint32)))
+    rows = gather_rank_rows([rank, gpu, pci, hashed, int(kern_avg_ms * 1e6), xor_local], world, cdev,
+                            dist if distributed else None)
+    xor_all = 0
+    for r in rows:
+        xor_all ^= r[5]
+    ranks = [{"rank": r[0], "device": r[1], "pci_bus_id": r[2], "bytes": r[3], "kernel_avg_ms": round(r[4] / 1e6, 4)}
+             for r in rows]
 
-    total_bytes = hashed * world * args.steps  # weak scaling: every rank hashes its own shard
+    total_bytes = sum(r[3] for r in rows) * args.steps  # weak scaling: every rank hashes its own shard
     value = total_bytes / wall_max / GIB
     ms_per_step = wall_max / args.steps * 1e3
     achieved_gbs = algo_bytes / (kern_avg_ms * 1e-3) / 1e9
@@ -321,6 +350,7 @@ def main():
             "value": round(value, 3),
             "unit": "GiB/s",
             "n_gpus": world,
+            "world_size": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
@@ -340,6 +370,8 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
+                "traffic_source": "profiles/pmc_traffic.json: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this "
+                                  "workload (tools/profile.sh), per launch, FETCH_SIZE x2 (MI355X_MICROARCH.md)",
                 "kernel": {"c2": "crc_pack4k_kernel<1,4,nt>", "sstable": "crc_sst4k_kernel<FixedSrc,OutSink,nt>",
                            "c3": "crc_stream16_kernel<DescSrc,OutSink,dyn,nt,pack>",
                            "wal": "crc_sst1k_kernel<DescSrc,OutSink,nt>",
@@ -354,6 +386,7 @@ def main():
                 "timing": args.timing,
             },
             "cpu_baseline": cpu,
+            "ranks": ranks,
             "xor_of_crcs": f"{xor_all:08x}",
         }
         line.update(extra)
@@ -406,8 +439,11 @@ def copy_inclusive(crc32c, data, L, stride, nblk):
 
 def cpu_baseline(data, L, stride, nblk, args, d_blk):
     """The reference's own CRC32C (oracle/_ref, compiled from src/util/crc32c.cc) on this box's
-    host cores over a bounded sample of the same blocks; falls back to the C restatement
-    (kind "port") only if the reference .so did not travel."""
+    host cores over a bounded sample of the same blocks (1 GiB): every logical CPU (the primary
+    figure, `cores` = nproc threads), 16 threads, one thread, and each NUMA node's CPUs alone.
+    Threads hash disjoint slices, started together, ~1 s per configuration
+    (oracle.timed_batch).  Falls back to the C restatement (kind "port") only if the reference
+    .so did not travel."""
     import oracle
 
     try:
@@ -416,7 +452,8 @@ def cpu_baseline(data, L, stride, nblk, args, d_blk):
         if not os.path.exists(oracle.ORACLE_SO):
             oracle.build()
         lib, kind = oracle.Oracle(), "port"
-    threads = args.cpu_threads or min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
+    cpus = oracle.host_cpus()
+    threads = args.cpu_threads or cpus["nproc"] or 1
     if d_blk is None:
         ns = min(nblk, 1 << 18)  # 256 Ki blocks = 1 GiB sample of the same workload
         host = data[: ns * stride].cpu().numpy()
@@ -431,16 +468,13 @@ def cpu_baseline(data, L, stride, nblk, args, d_blk):
         hi = int(blk["off"][-1] + blk["len"][-1])
         host = data[:hi].cpu().numpy()
     sample_bytes = int(blk["len"].astype(np.int64).sum())
-    res = {}
-    for nt in sorted({1, threads}):
-        reps, t0 = 0, time.perf_counter()
-        while True:
-            lib.batch(host, blk, flags=0, nthreads=nt)
-            reps += 1
-            dt = time.perf_counter() - t0
-            if dt > (6.0 if nt == 1 else 4.0) or reps >= 50:
-                break
-        res[nt] = sample_bytes * reps / dt / GIB
+    lib.batch(host, blk, nthreads=min(threads, 64))  # touch the sample once (page faults out of the timing)
+    res = {t: oracle.timed_batch(lib, host, blk, t, seconds=1.0)["GiB/s"] for t in sorted({1, 16, threads})}
+    numa = {}
+    for node, node_cpus in cpus["numa"].items():
+        if node_cpus and len(cpus["numa"]) > 1:
+            numa[node] = {"threads": len(node_cpus), "GiB/s": round(
+                oracle.timed_batch(lib, host, blk, len(node_cpus), seconds=1.0, cpus=node_cpus)["GiB/s"], 3)}
     dbb = None
     if kind == "reference":  # db_bench's own `crc32c` microbench loop, 1 thread
         try:
@@ -448,25 +482,21 @@ def cpu_baseline(data, L, stride, nblk, args, d_blk):
             dbb = {"MiB/s": round(mib_s, 1), "crc": f"0x{c:08x}", "loop": "4096 x 'x', 500 MiB, 1 thread"}
         except RuntimeError:
             pass
-    cpu_model = ""
-    try:
-        with open("/proc/cpuinfo") as f:
-            for ln in f:
-                if ln.startswith("model name"):
-                    cpu_model = ln.split(":", 1)[1].strip()
-                    break
-    except OSError:
-        pass
     return {
         "value": round(res[threads], 3),
         "unit": "GiB/s",
         "cores": threads,
         "kind": kind,
-        "sample": f"{ns} blocks ({sample_bytes / GIB:.2f} GiB) of the same workload, repeated ~4-6 s",
+        "sample": f"{ns} blocks ({sample_bytes / GIB:.2f} GiB) of the same workload in host memory, "
+                  f"each thread hashing its own slice over and over for ~1 s",
         "single_thread_GiB/s": round(res[1], 3),
+        "threads16_GiB/s": round(res[16], 3),
+        "per_numa_node": numa or None,
         "db_bench_crc32c": dbb,
-        "cpu_model": cpu_model,
-        "nproc": os.cpu_count(),
+        "cpu_model": cpus.get("cpu_model", ""),
+        "nproc": cpus["nproc"],
+        "affinity_cpus": cpus["affinity"],
+        "cgroup_cpu_quota": cpus["cgroup_cpu_quota"],
     }
 
 

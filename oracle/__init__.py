@@ -15,6 +15,8 @@ from __future__ import annotations
 import ctypes
 import os
 import subprocess
+import threading
+import time
 
 import numpy as np
 
@@ -123,6 +125,85 @@ class Reference(_CrcLib):
         c = ctypes.c_uint32(0)
         secs = self._dbb(total, ctypes.byref(c))
         return total / secs / (1 << 20), int(c.value)
+
+
+def timed_batch(crc, base, blk, nthreads: int, seconds: float = 1.0, cpus=None) -> dict:
+    """Host CPU throughput of `crc` (an Oracle or Reference) over the sample (base, blk): nthreads
+    threads, each hashing its own contiguous slice of the blocks over and over until `seconds`
+    have passed, started together on a barrier (no thread creation inside the timed window).
+    ctypes drops the GIL for the duration of each call, so the threads run in parallel; a call
+    hashes a whole slice (>= MiBs), so the Python loop costs nothing measurable.  cpus: pin thread t
+    to cpus[t % len(cpus)] (NUMA-node runs).  Returns {"GiB/s", "threads", "seconds", "bytes"}."""
+    base = _as_u8(base)
+    blk = np.ascontiguousarray(blk, dtype=BLK_DTYPE)
+    nthreads = max(1, min(int(nthreads), len(blk)))
+    lens = blk["len"].astype(np.int64)
+    cuts = [len(blk) * t // nthreads for t in range(nthreads + 1)]
+    slice_bytes = [int(lens[cuts[t] : cuts[t + 1]].sum()) for t in range(nthreads)]
+    reps = [0] * nthreads
+    stop = threading.Event()
+    start = threading.Barrier(nthreads + 1)
+
+    def work(t):
+        if cpus:
+            try:
+                os.sched_setaffinity(0, {cpus[t % len(cpus)]})
+            except OSError:
+                pass
+        part = blk[cuts[t] : cuts[t + 1]]
+        start.wait()
+        while not stop.is_set():
+            crc.batch(base, part, nthreads=1)
+            reps[t] += 1
+
+    th = [threading.Thread(target=work, args=(t,), daemon=True) for t in range(nthreads)]
+    for x in th:
+        x.start()
+    start.wait()
+    t0 = time.perf_counter()
+    time.sleep(seconds)
+    stop.set()
+    for x in th:
+        x.join()
+    dt = time.perf_counter() - t0
+    total = sum(r * b for r, b in zip(reps, slice_bytes))
+    return {"GiB/s": total / dt / (1 << 30), "threads": nthreads, "seconds": dt, "bytes": total}
+
+
+def host_cpus() -> dict:
+    """The host's CPU picture: logical CPUs, the ones this process may run on, a cgroup CPU quota
+    if one is set, and the CPUs of every NUMA node."""
+    info = {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "cgroup_cpu_quota": None, "numa": {}}
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+            if q != "max":
+                info["cgroup_cpu_quota"] = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    node_dir = "/sys/devices/system/node"
+    try:
+        for d in sorted(os.listdir(node_dir)):
+            if d.startswith("node") and d[4:].isdigit():
+                with open(os.path.join(node_dir, d, "cpulist")) as f:
+                    cpus = []
+                    for part in f.read().strip().split(","):
+                        if part:
+                            a, _, b = part.partition("-")
+                            cpus.extend(range(int(a), int(b or a) + 1))
+                allowed = os.sched_getaffinity(0)
+                info["numa"][d] = [c for c in cpus if c in allowed]
+    except OSError:
+        pass
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    info["cpu_model"] = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return info
 
 
 def reference_available() -> bool:

@@ -90,3 +90,40 @@ def test_gloo_world2_shards_cover_and_checksum_matches(oracle_lib):
     blk["off"] = np.arange(n_total) * 4096
     blk["len"] = 4096
     assert xor == int(np.bitwise_xor.reduce(oracle_lib.batch(data, blk, nthreads=4)))
+
+
+def _bench_worker(rank, world, port, q):
+    """bench.py's multi-rank plumbing (no GPU): the C3 plan, the byte-balanced range scatter and
+    the per-rank row gather that feeds the JSON line's `ranks`."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+
+    sizes = bench.c3_plan(64 << 20, world)  # 64 MiB per rank (the bench default is 16 GiB)
+    lo, hi = scatter_block_ranges(len(sizes), world, rank, torch.device("cpu"), dist, lens=sizes)
+    mine = int(sizes[lo:hi].sum())
+    rows = bench.gather_rank_rows([rank, 0, -1, mine, 123456, rank * 7], world, torch.device("cpu"), dist)
+    if rank == 0:
+        q.put(("rows", rows, len(sizes), int(sizes.sum())))
+    q.put(("range", rank, lo, hi))
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_bench_c3_byte_balanced():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_bench_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(120)
+        assert p.exitcode == 0
+    msgs = [q.get(timeout=10) for _ in range(world + 1)]
+    rows, n, total = next(m[1:] for m in msgs if m[0] == "rows")
+    ranges = sorted((m[1], m[2], m[3]) for m in msgs if m[0] == "range")
+    assert ranges[0][1] == 0 and ranges[-1][2] == n and ranges[0][2] == ranges[1][1]
+    assert [r[0] for r in rows] == [0, 1] and sum(r[3] for r in rows) == total
+    assert abs(rows[0][3] - rows[1][3]) <= 2 * 64 * 1024  # byte-balanced to within a block or two
+    assert abs(total - world * (64 << 20)) <= 64 * 1024

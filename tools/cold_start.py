@@ -37,6 +37,65 @@ def timed(fn, n=100):
     return [round(a.elapsed_time(b), 4) for a, b in ev]
 
 
+class SysfsSampler:
+    """Samples the GPUs' hwmon SCLK (freq1_input), power (power1_input / power1_average) and the
+    active pp_dpm_sclk level every ~1 ms in a background thread (read-only sysfs), so a launch
+    sequence can be lined up with the clock the power manager gave it."""
+
+    def __init__(self):
+        import glob
+        import threading
+
+        self.files = {}
+        for dev in sorted(glob.glob("/sys/class/drm/card*/device")):
+            card = dev.split("/")[4]
+            for hw in glob.glob(dev + "/hwmon/hwmon*"):
+                for nm in ("freq1_input", "power1_input", "power1_average", "temp2_input"):
+                    if os.path.exists(os.path.join(hw, nm)):
+                        self.files[f"{card}:{nm}"] = os.path.join(hw, nm)
+        self.samples = []
+        self._stop = threading.Event()
+        self._th = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self):
+        t0 = time.perf_counter()
+        while not self._stop.is_set():
+            row = {"t_ms": round((time.perf_counter() - t0) * 1e3, 2)}
+            for k, p in self.files.items():
+                try:
+                    with open(p) as f:
+                        row[k] = int(f.read().strip())
+                except (OSError, ValueError):
+                    pass
+            self.samples.append(row)
+            time.sleep(0.001)
+
+    def __enter__(self):
+        self._th.start()
+        return self
+
+    def __exit__(self, *a):
+        self._stop.set()
+        self._th.join()
+
+    def busy_card(self):
+        """The card whose SCLK moved the most (the one our kernels ran on)."""
+        best, spread = None, -1
+        for k in self.files:
+            if k.endswith("freq1_input"):
+                v = [r[k] for r in self.samples if k in r]
+                if v and max(v) - min(v) > spread:
+                    best, spread = k.split(":")[0], max(v) - min(v)
+        return best
+
+    def trace(self):
+        c = self.busy_card()
+        if c is None:
+            return None
+        keys = [k for k in self.files if k.startswith(c + ":")]
+        return {"card": c, "rows": [[r["t_ms"]] + [r.get(k) for k in keys] for r in self.samples], "cols": ["t_ms"] + keys}
+
+
 def clocks():
     try:
         r = subprocess.run(["amd-smi", "metric", "-g", "0", "-c", "--json"], capture_output=True, text=True, timeout=20)
@@ -73,7 +132,22 @@ def main():
     time.sleep(2.0)
     res["D_idle2s_load_only"] = summary(timed(lambda: diag.read_pattern4k(d1, NBLK, 21, o)))
     time.sleep(2.0)
-    res["E_idle2s_crc_again"] = summary(timed(lambda: crc32c.batch_fixed(d1, 4096, 4096, NBLK, out=out), 200))
+    with SysfsSampler() as smp:
+        time.sleep(0.02)
+        tE = time.perf_counter()
+        e_times = timed(lambda: crc32c.batch_fixed(d1, 4096, 4096, NBLK, out=out), 200)
+        res["E_launches_end_ms"] = round((time.perf_counter() - tE) * 1e3, 2)
+        time.sleep(0.02)
+    res["E_idle2s_crc_again"] = summary(e_times)
+    res["E_per_launch_ms"] = e_times
+    res["E_sysfs"] = smp.trace()
+    time.sleep(2.0)
+    with SysfsSampler() as smp2:
+        time.sleep(0.02)
+        d_times = timed(lambda: diag.read_pattern4k(d1, NBLK, 21, o), 200)
+        time.sleep(0.02)
+    res["F_load_only_per_launch_ms"] = d_times
+    res["F_sysfs"] = smp2.trace()
     print(json.dumps(res), flush=True)
 
 
