@@ -1,0 +1,70 @@
+#!/usr/bin/env bash
+# integration/build.sh -- BASELINE configs 1 and 5 end to end: the PebblesDB engine compiled from
+# the reference's own sources IN PLACE under /root/reference (never copied, never modified, not
+# its build system) with this repo's table hooks, plus the db_bench-equivalent harness.
+# Outputs ONLY to integration/_build/ (git-ignored; travels to the GPU box):
+#   pdb_dbbench_cpu        reference engine as shipped (table_builder.cc, format.cc, crc32c.cc)
+#   pdb_dbbench_gpu_table  table/table_builder.cc + table/format.cc replaced by pdb_table_builder.cc
+#                          + pdb_format.cc (batched GPU trailer seals, GPU ReadBlock verify); the
+#                          WAL / MANIFEST keep the reference CRC (util/crc32c.cc)
+#   pdb_dbbench_gpu_all    as gpu_table, and util/crc32c.h -> include/pebblesdb_amd/crc32c.h for every
+#                          other call site (log_writer/log_reader records on the scalar GPU service)
+#   sstwriter_gpu          oracle/ref_sstwriter.cc over the GPU hooks (golden-table parity test)
+set -euo pipefail
+HERE="$(cd "$(dirname "$0")" && pwd)"
+ROOT="$(dirname "$HERE")"
+REF="${PDB_REFERENCE_ROOT:-/root/reference}/src"
+if [ ! -f "$REF/db/db_impl.cc" ]; then
+  echo "integration/build.sh: reference not present at $REF; skipping (prebuilt binaries are used)" >&2
+  exit 0
+fi
+LIB="$ROOT/pebblesdb_amd/_lib/libpdb_crc32c.so"
+[ -f "$LIB" ] || { echo "integration/build.sh: $LIB missing (python -m pebblesdb_amd.build)" >&2; exit 1; }
+B="$HERE/_build"
+mkdir -p "$B/obj_ref" "$B/obj_shim" "$B/obj_hooks"
+ENGINE="db/builder.cc db/db_impl.cc db/db_iter.cc db/dbformat.cc db/filename.cc db/log_reader.cc
+        db/log_writer.cc db/memtable.cc db/murmurhash3.cc db/repair.cc db/replay_iterator.cc
+        db/table_cache.cc db/version_edit.cc db/version_set.cc db/write_batch.cc db/c.cc
+        table/block.cc table/block_builder.cc table/filter_block.cc table/iterator.cc
+        table/merger.cc table/table.cc table/two_level_iterator.cc
+        util/arena.cc util/atomic.cc util/bloom.cc util/cache.cc util/coding.cc util/comparator.cc
+        util/env.cc util/env_posix.cc util/filter_policy.cc util/hash.cc util/histogram.cc
+        util/logging.cc util/options.cc util/status.cc util/testutil.cc port/port_posix.cc"
+TABLE_REF="table/table_builder.cc table/format.cc"
+DEFS="-DLEVELDB_PLATFORM_POSIX -DOS_LINUX -DHAVE_FFLUSH_UNLOCKED -DHAVE_FREAD_UNLOCKED"
+DEFS="$DEFS -DHAVE_FWRITE_UNLOCKED -DHAVE_FDATASYNC -DHAVE_DECL_FDATASYNC=1 -DNDEBUG"
+CXX="g++ -O2 -std=c++11 -w -pthread"
+JOBS="${PDB_BUILD_JOBS:-8}"
+
+compile() {  # $1 = obj dir, $2 = source list, $3.. = include flags (sources under $REF)
+  local od="$1" srcs="$2"; shift 2
+  for f in $srcs; do echo "$f"; done | xargs -P "$JOBS" -I{} sh -c \
+    "o=\"$od/\$(echo {} | tr / _).o\"; [ \"\$o\" -nt \"$REF/{}\" ] || $CXX $DEFS $* -c \"$REF/{}\" -o \"\$o\""
+}
+objs() {  # object paths of a source list in an obj dir
+  local od="$1" f; shift
+  for f in $*; do printf '%s ' "$od/$(echo "$f" | tr / _).o"; done
+}
+
+# reference engine as shipped, and the same sources with util/crc32c.h bound to the GPU
+compile "$B/obj_ref" "$ENGINE $TABLE_REF util/crc32c.cc" "-I$REF -I$REF/include"
+compile "$B/obj_shim" "$ENGINE" "-I$ROOT/oracle/shim_pdb -I$ROOT/include -I$REF -I$REF/include"
+# the hooks and the harness (our sources)
+HOOKI="-I$ROOT/include -I$HERE -I$REF -I$REF/include"
+for f in pdb_table_builder pdb_format; do
+  [ "$B/obj_hooks/$f.o" -nt "$HERE/$f.cc" ] && [ "$B/obj_hooks/$f.o" -nt "$HERE/pdb_hooks.h" ] ||
+    $CXX $DEFS $HOOKI -c "$HERE/$f.cc" -o "$B/obj_hooks/$f.o"
+done
+$CXX $DEFS $HOOKI -DPDB_HOOKS=0 -c "$HERE/pdb_dbbench.cc" -o "$B/obj_hooks/dbbench_cpu.o"
+$CXX $DEFS $HOOKI -DPDB_HOOKS=1 -c "$HERE/pdb_dbbench.cc" -o "$B/obj_hooks/dbbench_hooks.o"
+$CXX $DEFS $HOOKI -c "$ROOT/oracle/ref_sstwriter.cc" -o "$B/obj_hooks/sstwriter.o"
+
+RPATH="-Wl,-rpath,\$ORIGIN/../../pebblesdb_amd/_lib"
+GPU="-L$ROOT/pebblesdb_amd/_lib -lpdb_crc32c $RPATH"
+HOOKS="$B/obj_hooks/pdb_table_builder.o $B/obj_hooks/pdb_format.o"
+$CXX -o "$B/pdb_dbbench_cpu" "$B/obj_hooks/dbbench_cpu.o" $(objs "$B/obj_ref" $ENGINE $TABLE_REF util/crc32c.cc)
+$CXX -o "$B/pdb_dbbench_gpu_table" "$B/obj_hooks/dbbench_hooks.o" $HOOKS \
+  $(objs "$B/obj_ref" $ENGINE util/crc32c.cc) $GPU
+$CXX -o "$B/pdb_dbbench_gpu_all" "$B/obj_hooks/dbbench_hooks.o" $HOOKS $(objs "$B/obj_shim" $ENGINE) $GPU
+$CXX -o "$B/sstwriter_gpu" "$B/obj_hooks/sstwriter.o" $HOOKS $(objs "$B/obj_ref" $ENGINE util/crc32c.cc) $GPU
+echo "built $B/{pdb_dbbench_cpu,pdb_dbbench_gpu_table,pdb_dbbench_gpu_all,sstwriter_gpu}"

@@ -1,0 +1,251 @@
+// integration/pdb_dbbench.cc -- the db_bench-equivalent harness for BASELINE configs 1 and 5
+// (SURVEY §7 step 8): fillseq / fillrandom / readrandom / readseq over the PebblesDB engine with a
+// --verify_checksums switch, which the reference's db_bench lacks (its ReadRandom uses default
+// ReadOptions, db/db_bench.cc:1328-1338, so reads never reach the CRC).
+//
+// Workload definitions follow db_bench (db/db_bench.cc): keys "%016d"; fillseq writes 0..num-1,
+// fillrandom / readrandom draw Random(1000).Next() % num (ThreadState(0), :354-359); values are
+// value_size-byte slices of a 1-MiB pool of test::CompressibleString pieces (RandomGenerator,
+// :152-184); one Put per WriteBatch; Open() uses the reference's Options defaults with
+// bloom_bits 10 and the engine's default block cache (:1194-1208, :137); MB/s counts key + value
+// bytes in MiB (:292-318).  The same source links against either CRC build:
+//   pdb_dbbench_cpu       the reference as shipped (util/crc32c.cc, table_builder.cc, format.cc)
+//   pdb_dbbench_gpu_table table_builder.cc + format.cc replaced by integration/pdb_table_builder.cc
+//                         and pdb_format.cc (batched GPU seals, GPU ReadBlock verify); the WAL /
+//                         MANIFEST keep the reference CRC: the north_star's "block emit/verify hook"
+//   pdb_dbbench_gpu_all   as gpu_table, and util/crc32c.h bound to libpdb_crc32c.so for every other
+//                         call site (WAL / MANIFEST records through the scalar GPU service)
+// Besides db_bench's lines it prints one JSON line per benchmark with the hook counters.
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include <string>
+#include <vector>
+
+#include "pebblesdb/cache.h"
+#include "pebblesdb/db.h"
+#include "pebblesdb/env.h"
+#include "pebblesdb/filter_policy.h"
+#include "pebblesdb/iterator.h"
+#include "pebblesdb/options.h"
+#include "pebblesdb/write_batch.h"
+#include "util/random.h"
+#include "util/testutil.h"
+#if PDB_HOOKS
+#include "pdb_hooks.h"
+#endif
+
+namespace {
+
+struct Flags {
+  std::string benchmarks = "fillrandom,readrandom";
+  int num = 1000000;
+  int reads = -1;
+  int value_size = 1024;
+  int bloom_bits = 10;
+  int cache_size = -1;  // < 0: the engine's default block cache
+  bool verify_checksums = false;
+  bool use_existing_db = false;
+  std::string db = "/tmp/pdb_dbbench";
+} F;
+
+double NowSec() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec + 1e-9 * ts.tv_nsec;
+}
+
+class ValuePool {  // db_bench's RandomGenerator: a 1-MiB pool of compressible pieces
+ public:
+  ValuePool() {
+    leveldb::Random rnd(301);
+    std::string piece;
+    while (data_.size() < 1048576) {
+      leveldb::test::CompressibleString(&rnd, 0.5, 100, &piece);
+      data_.append(piece);
+    }
+  }
+  leveldb::Slice Next(size_t len) {
+    if (pos_ + len > data_.size()) pos_ = 0;
+    pos_ += len;
+    return leveldb::Slice(data_.data() + pos_ - len, len);
+  }
+
+ private:
+  std::string data_;
+  size_t pos_ = 0;
+};
+
+struct Result {
+  const char* name;
+  long ops;
+  double seconds;
+  long long bytes;
+  std::string note;
+};
+
+void Report(const Result& r) {
+  const double us = r.seconds * 1e6 / (r.ops ? r.ops : 1);
+  const double mbs = r.bytes / 1048576.0 / r.seconds;
+  if (r.bytes > 0)
+    printf("%-12s : %11.3f micros/op; %6.1f MB/s %s\n", r.name, us, mbs, r.note.c_str());
+  else
+    printf("%-12s : %11.3f micros/op; %s\n", r.name, us, r.note.c_str());
+  printf("{\"bench\": \"%s\", \"ops\": %ld, \"seconds\": %.4f, \"micros_per_op\": %.4f, \"MB_s\": %.2f, "
+         "\"verify_checksums\": %s",
+         r.name, r.ops, r.seconds, us, r.bytes > 0 ? mbs : 0.0, F.verify_checksums ? "true" : "false");
+#if PDB_HOOKS
+  pdb_hook_stats s;
+  pdb_hook_stats_get(&s);
+  printf(", \"hook\": {\"seal_calls\": %llu, \"seal_blocks\": %llu, \"seal_bytes\": %llu, \"seal_s\": %.4f, "
+         "\"seal_copy_inclusive_MiB_s\": %.1f, \"verify_calls\": %llu, \"verify_bytes\": %llu, \"verify_s\": %.4f, "
+         "\"verify_us_per_call\": %.3f, \"verify_failed\": %llu}",
+         (unsigned long long)s.seal_calls, (unsigned long long)s.seal_blocks, (unsigned long long)s.seal_bytes,
+         s.seal_ns * 1e-9, s.seal_ns ? s.seal_bytes / 1048576.0 / (s.seal_ns * 1e-9) : 0.0,
+         (unsigned long long)s.verify_calls, (unsigned long long)s.verify_bytes, s.verify_ns * 1e-9,
+         s.verify_calls ? s.verify_ns * 1e-3 / s.verify_calls : 0.0, (unsigned long long)s.verify_failed);
+  pdb_hook_stats_reset();
+#endif
+  printf("}\n");
+  fflush(stdout);
+}
+
+leveldb::DB* Open(const leveldb::FilterPolicy* fp, leveldb::Cache* cache) {
+  leveldb::Options o;
+  o.create_if_missing = !F.use_existing_db;
+  o.block_cache = cache;
+  o.filter_policy = fp;
+  leveldb::DB* db = NULL;
+  leveldb::Status s = leveldb::DB::Open(o, F.db, &db);
+  if (!s.ok()) {
+    fprintf(stderr, "open error: %s\n", s.ToString().c_str());
+    exit(1);
+  }
+  return db;
+}
+
+Result Write(leveldb::DB* db, bool seq) {
+  ValuePool values;
+  leveldb::Random rand(1000);
+  leveldb::WriteOptions wo;
+  leveldb::WriteBatch batch;
+  long long bytes = 0;
+  char key[32];
+  const double t0 = NowSec();
+  for (int i = 0; i < F.num; ++i) {
+    const int k = seq ? i : static_cast<int>(rand.Next() % F.num);
+    snprintf(key, sizeof(key), "%016d", k);
+    batch.Clear();
+    batch.Put(key, values.Next(F.value_size));
+    bytes += F.value_size + strlen(key);
+    leveldb::Status s = db->Write(wo, &batch);
+    if (!s.ok()) {
+      fprintf(stderr, "put error: %s\n", s.ToString().c_str());
+      exit(1);
+    }
+  }
+  return Result{seq ? "fillseq" : "fillrandom", F.num, NowSec() - t0, bytes, ""};
+}
+
+Result ReadRandom(leveldb::DB* db) {
+  leveldb::Random rand(1000);
+  leveldb::ReadOptions ro;
+  ro.verify_checksums = F.verify_checksums;
+  std::string value;
+  const int reads = F.reads < 0 ? F.num : F.reads;
+  int found = 0;
+  char key[32];
+  const double t0 = NowSec();
+  for (int i = 0; i < reads; ++i) {
+    snprintf(key, sizeof(key), "%016d", static_cast<int>(rand.Next() % F.num));
+    leveldb::Status s = db->Get(ro, key, &value);
+    if (s.ok()) {
+      ++found;
+    } else if (!s.IsNotFound()) {
+      fprintf(stderr, "get error: %s\n", s.ToString().c_str());
+      exit(1);
+    }
+  }
+  char note[80];
+  snprintf(note, sizeof(note), "(%d of %d found)", found, reads);
+  return Result{"readrandom", reads, NowSec() - t0, 0, note};
+}
+
+Result ReadSeq(leveldb::DB* db) {
+  leveldb::ReadOptions ro;
+  ro.verify_checksums = F.verify_checksums;
+  leveldb::Iterator* it = db->NewIterator(ro);
+  long n = 0;
+  long long bytes = 0;
+  const int reads = F.reads < 0 ? F.num : F.reads;
+  const double t0 = NowSec();
+  for (it->SeekToFirst(); n < reads && it->Valid(); it->Next()) {
+    bytes += it->key().size() + it->value().size();
+    ++n;
+  }
+  if (!it->status().ok()) {
+    fprintf(stderr, "iterator error: %s\n", it->status().ToString().c_str());
+    exit(1);
+  }
+  delete it;
+  return Result{"readseq", n, NowSec() - t0, bytes, ""};
+}
+
+bool Arg(const char* a, const char* name, std::string* v) {
+  const size_t n = strlen(name);
+  if (strncmp(a, name, n) != 0 || a[n] != '=') return false;
+  *v = a + n + 1;
+  return true;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  for (int i = 1; i < argc; ++i) {
+    std::string v;
+    if (Arg(argv[i], "--benchmarks", &v)) F.benchmarks = v;
+    else if (Arg(argv[i], "--num", &v)) F.num = atoi(v.c_str());
+    else if (Arg(argv[i], "--reads", &v)) F.reads = atoi(v.c_str());
+    else if (Arg(argv[i], "--value_size", &v)) F.value_size = atoi(v.c_str());
+    else if (Arg(argv[i], "--bloom_bits", &v)) F.bloom_bits = atoi(v.c_str());
+    else if (Arg(argv[i], "--cache_size", &v)) F.cache_size = atoi(v.c_str());
+    else if (Arg(argv[i], "--verify_checksums", &v)) F.verify_checksums = atoi(v.c_str()) != 0;
+    else if (Arg(argv[i], "--use_existing_db", &v)) F.use_existing_db = atoi(v.c_str()) != 0;
+    else if (Arg(argv[i], "--db", &v)) F.db = v;
+    else {
+      fprintf(stderr, "invalid flag '%s'\n", argv[i]);
+      return 1;
+    }
+  }
+  const leveldb::FilterPolicy* fp = F.bloom_bits >= 0 ? leveldb::NewBloomFilterPolicy(F.bloom_bits) : NULL;
+  leveldb::Cache* cache = F.cache_size >= 0 ? leveldb::NewLRUCache(F.cache_size) : NULL;
+  if (!F.use_existing_db) leveldb::DestroyDB(F.db, leveldb::Options());
+  printf("Keys:       16 bytes each\nValues:     %d bytes each\nEntries:    %d\nverify_checksums: %d\n", F.value_size,
+         F.num, F.verify_checksums ? 1 : 0);
+  leveldb::DB* db = Open(fp, cache);
+  size_t pos = 0;
+  while (pos <= F.benchmarks.size()) {
+    size_t end = F.benchmarks.find(',', pos);
+    if (end == std::string::npos) end = F.benchmarks.size();
+    const std::string name = F.benchmarks.substr(pos, end - pos);
+    pos = end + 1;
+    if (name.empty()) continue;
+#if PDB_HOOKS
+    pdb_hook_stats_reset();
+#endif
+    if (name == "fillseq") Report(Write(db, true));
+    else if (name == "fillrandom") Report(Write(db, false));
+    else if (name == "readrandom") Report(ReadRandom(db));
+    else if (name == "readseq") Report(ReadSeq(db));
+    else {
+      fprintf(stderr, "unknown benchmark '%s'\n", name.c_str());
+      return 1;
+    }
+  }
+  delete db;
+  delete cache;
+  delete fp;
+  return 0;
+}

@@ -1,0 +1,243 @@
+// integration/pdb_table_builder.cc -- drop-in for the reference's table/table_builder.cc whose
+// block trailers are computed on the MI355X in batches (buffered emission).
+//
+// The reference (table/table_builder.cc:187-205) writes every block synchronously:
+//     Append(contents); trailer = [type][Mask(Extend(Value(contents), type))]; Append(trailer)
+// one CRC per block on the building thread (the memtable-flush or compaction thread).  Here
+// WriteRawBlock only STAGES the block -- contents, type byte, a 4-byte placeholder -- and hands out
+// the handle it will have (offsets are known without the CRC), and every kSealBytes of staged
+// blocks, and at Finish(), ONE pdb_sst_seal_host call computes all their trailers on the GPU
+// (H2D of the staged span, crc_sst4k_kernel, 4 B per block back) before ONE Append of the whole
+// span.  The file receives byte for byte what the reference writes (tests: the reference-written
+// golden tables are reproduced exactly), just in fewer, larger appends.
+//
+// Interface: the reference's own include/pebblesdb/table_builder.h (class TableBuilder, private
+// Rep); behaviour of Add/Flush/Finish/Abandon/status/NumEntries/FileSize is the reference's
+// (table_builder.cc:71-280) with two visible differences, both inherent to buffered emission:
+//   * WritableFile::Append/Flush are called once per sealed batch, not per block, so after Flush()
+//     a block may still be staged in memory (Finish() always writes everything; Abandon() drops it);
+//   * a device error surfaces as Status::IOError("pdb_sst_seal_host", <message>) from the call that
+//     sealed (Add, Flush or Finish), never as a wrong trailer (there is no CPU fallback).
+// Batch size: PDB_SEAL_BATCH_BYTES (default 4 MiB of staged blocks).
+#include <stdlib.h>
+
+#include <string>
+#include <vector>
+
+#include "pdb_crc32c.h"
+#include "pdb_hooks.h"
+#include "pebblesdb/comparator.h"
+#include "pebblesdb/env.h"
+#include "pebblesdb/filter_policy.h"
+#include "pebblesdb/options.h"
+#include "pebblesdb/table_builder.h"
+#include "table/block_builder.h"
+#include "table/filter_block.h"
+#include "table/format.h"
+#include "util/coding.h"
+
+namespace leveldb {
+
+namespace {
+size_t SealBatchBytes() {
+  static const size_t v = [] {
+    const char* e = getenv("PDB_SEAL_BATCH_BYTES");
+    const long long x = e ? atoll(e) : 0;
+    return x > 0 ? static_cast<size_t>(x) : static_cast<size_t>(4u << 20);
+  }();
+  return v;
+}
+}  // namespace
+
+struct TableBuilder::Rep {
+  Options options;
+  Options index_block_options;  // restart interval 1: every index key is a restart point
+  WritableFile* file;
+  uint64_t offset;  // file offset of the next block: staged blocks included
+  Status status;
+  BlockBuilder data_block;
+  BlockBuilder index_block;
+  std::string last_key;
+  int64_t num_entries;
+  bool closed;
+  FilterBlockBuilder* filter_block;
+  // The index entry of a finished data block is written when the next block's first key is seen,
+  // so its separator can be short (table_builder.cc:33-41).
+  bool pending_index_entry;
+  BlockHandle pending_handle;
+  std::string compressed_output;
+  // buffered emission: blocks in file order, each [contents][type][crc placeholder]
+  std::string staged;
+  std::vector<pdb_block_handle> staged_handles;  // relative to staged
+
+  Rep(const Options& opt, WritableFile* f)
+      : options(opt),
+        index_block_options(opt),
+        file(f),
+        offset(0),
+        data_block(&options),
+        index_block(&index_block_options),
+        num_entries(0),
+        closed(false),
+        filter_block(opt.filter_policy == NULL ? NULL : new FilterBlockBuilder(opt.filter_policy)),
+        pending_index_entry(false) {
+    index_block_options.block_restart_interval = 1;
+  }
+
+  // Seal every staged trailer in one GPU batch, then append the span to the file.
+  void SealStaged() {
+    if (staged_handles.empty()) return;
+    if (status.ok()) {
+      const uint64_t t0 = pdb_hooks::NowNs();
+      const int rc = pdb_sst_seal_host(&staged[0], staged.size(), staged_handles.data(), staged_handles.size());
+      pdb_hooks::AddSeal(staged_handles.size(), staged.size(), pdb_hooks::NowNs() - t0);
+      if (rc != 0) {
+        status = Status::IOError("pdb_sst_seal_host", pdb_last_error());
+      } else {
+        status = file->Append(Slice(staged));
+        if (status.ok()) status = file->Flush();
+      }
+    }
+    staged.clear();
+    staged_handles.clear();
+  }
+};
+
+TableBuilder::TableBuilder(const Options& options, WritableFile* file) : rep_(new Rep(options, file)) {
+  if (rep_->filter_block != NULL) rep_->filter_block->StartBlock(0);
+}
+
+TableBuilder::~TableBuilder() {
+  assert(rep_->closed);  // Finish() or Abandon() first
+  delete rep_->filter_block;
+  delete rep_;
+}
+
+Status TableBuilder::ChangeOptions(const Options& options) {
+  if (options.comparator != rep_->options.comparator)
+    return Status::InvalidArgument("changing comparator while building table");
+  // the BlockBuilders hold pointers to these, so they see the new options too
+  rep_->options = options;
+  rep_->index_block_options = options;
+  rep_->index_block_options.block_restart_interval = 1;
+  return Status::OK();
+}
+
+void TableBuilder::Add(const Slice& key, const Slice& value) {
+  Rep* r = rep_;
+  assert(!r->closed);
+  if (!ok()) return;
+  if (r->pending_index_entry) {  // first key of a new data block: index the previous one
+    assert(r->data_block.empty());
+    r->options.comparator->FindShortestSeparator(&r->last_key, key);
+    std::string enc;
+    r->pending_handle.EncodeTo(&enc);
+    r->index_block.Add(r->last_key, Slice(enc));
+    r->pending_index_entry = false;
+  }
+  if (r->filter_block != NULL) r->filter_block->AddKey(key);
+  r->last_key.assign(key.data(), key.size());
+  ++r->num_entries;
+  r->data_block.Add(key, value);
+  if (r->data_block.CurrentSizeEstimate() >= r->options.block_size) Flush();
+}
+
+void TableBuilder::Flush() {
+  Rep* r = rep_;
+  assert(!r->closed);
+  if (!ok() || r->data_block.empty()) return;
+  assert(!r->pending_index_entry);
+  WriteBlock(&r->data_block, &r->pending_handle);
+  if (ok()) r->pending_index_entry = true;
+  if (r->filter_block != NULL) r->filter_block->StartBlock(r->offset);
+}
+
+void TableBuilder::WriteBlock(BlockBuilder* block, BlockHandle* handle) {
+  // on disk: contents, 1-byte compression type, 4-byte masked crc (table/format.h:86-87)
+  assert(ok());
+  Rep* r = rep_;
+  const Slice raw = block->Finish();
+  Slice contents = raw;
+  CompressionType type = r->options.compression;
+  if (type == kSnappyCompression) {  // Snappy stays delegated to the port layer (out of scope)
+    std::string* c = &r->compressed_output;
+    if (port::Snappy_Compress(raw.data(), raw.size(), c) && c->size() < raw.size() - raw.size() / 8u) {
+      contents = *c;
+    } else {  // not available, or saves less than 12.5 %: store it uncompressed
+      type = kNoCompression;
+    }
+  } else if (type != kNoCompression) {
+    abort();
+  }
+  WriteRawBlock(contents, type, handle);
+  r->compressed_output.clear();
+  block->Reset();
+}
+
+void TableBuilder::WriteRawBlock(const Slice& contents, CompressionType type, BlockHandle* handle) {
+  Rep* r = rep_;
+  handle->set_offset(r->offset);
+  handle->set_size(contents.size());
+  const uint64_t rel = r->staged.size();
+  r->staged.append(contents.data(), contents.size());
+  const char trailer[kBlockTrailerSize] = {static_cast<char>(type), 0, 0, 0, 0};  // crc: sealed in batch
+  r->staged.append(trailer, kBlockTrailerSize);
+  r->staged_handles.push_back(pdb_block_handle{rel, contents.size()});
+  r->offset += contents.size() + kBlockTrailerSize;
+  if (r->staged.size() >= SealBatchBytes()) r->SealStaged();
+}
+
+Status TableBuilder::status() const { return rep_->status; }
+
+Status TableBuilder::Finish() {
+  Rep* r = rep_;
+  Flush();
+  assert(!r->closed);
+  r->closed = true;
+  BlockHandle filter_handle, metaindex_handle, index_handle;
+  if (ok() && r->filter_block != NULL) WriteRawBlock(r->filter_block->Finish(), kNoCompression, &filter_handle);
+  if (ok()) {  // metaindex: "filter.<policy name>" -> the filter block
+    BlockBuilder meta_index(&r->options);
+    if (r->filter_block != NULL) {
+      std::string enc;
+      filter_handle.EncodeTo(&enc);
+      meta_index.Add("filter." + std::string(r->options.filter_policy->Name()), enc);
+    }
+    WriteBlock(&meta_index, &metaindex_handle);
+  }
+  if (ok()) {
+    if (r->pending_index_entry) {  // the last data block's index entry
+      r->options.comparator->FindShortSuccessor(&r->last_key);
+      std::string enc;
+      r->pending_handle.EncodeTo(&enc);
+      r->index_block.Add(r->last_key, Slice(enc));
+      r->pending_index_entry = false;
+    }
+    WriteBlock(&r->index_block, &index_handle);
+  }
+  r->SealStaged();  // every trailer of the table's last batch, then its bytes
+  if (ok()) {
+    Footer footer;
+    footer.set_metaindex_handle(metaindex_handle);
+    footer.set_index_handle(index_handle);
+    std::string enc;
+    footer.EncodeTo(&enc);
+    r->status = r->file->Append(enc);
+    if (r->status.ok()) r->offset += enc.size();
+  }
+  return r->status;
+}
+
+void TableBuilder::Abandon() {
+  Rep* r = rep_;
+  assert(!r->closed);
+  r->closed = true;
+  r->staged.clear();  // never written: the caller discards the file
+  r->staged_handles.clear();
+}
+
+uint64_t TableBuilder::NumEntries() const { return rep_->num_entries; }
+
+uint64_t TableBuilder::FileSize() const { return rep_->offset; }
+
+}  // namespace leveldb

@@ -21,6 +21,8 @@ for s in "$@"; do
   case "$s" in
     tests) step tests 1000 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread ;;
     cold) step cold 300 python tools/cold_start.py ;;
+    integ) step integ 600 python -u -m pytest tests/test_integration.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
+    fullsize) step fullsize 600 python -u -m pytest tests/test_full_size.py tests/test_gpu_parity.py -m gpu -x -v --timeout 300 --timeout-method thread -k "full_size or host_" ;;
     bench_driver) step bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --diag ;;

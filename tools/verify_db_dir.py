@@ -45,19 +45,28 @@ def main() -> int:
                 res["tables_incomplete"] += 1
                 continue
             hs = lay.all_handles()
-            for h in hs:
-                body = np.frombuffer(img[h.offset : h.offset + h.size + 1], dtype=np.uint8)
-                stored = int.from_bytes(img[h.offset + h.size + 1 : h.offset + h.size + 5], "little")
-                res["blocks_bad_oracle"] += int(orc.unmask(stored) != orc.value(body))
+            u8 = np.frombuffer(img, dtype=np.uint8)
+            offs = np.array([h.offset for h in hs], dtype=np.int64)
+            sizes = np.array([h.size for h in hs], dtype=np.int64)
+            tr = offs + sizes + 1
+            stored = (u8[tr].astype(np.uint32) | (u8[tr + 1].astype(np.uint32) << 8) |
+                      (u8[tr + 2].astype(np.uint32) << 16) | (u8[tr + 3].astype(np.uint32) << 24))
+            blk = np.zeros(len(hs), dtype=[("off", "<u8"), ("len", "<u4"), ("init", "<u4")])
+            blk["off"], blk["len"] = offs, sizes + 1  # contents || type
+            res["blocks_bad_oracle"] += int((orc.batch(u8, blk, flags=1, nthreads=8) != stored).sum())
             if a.gpu:
                 res["blocks_bad_gpu"] += int((T.verify_table(img)[1] == 0).sum())
             res["tables"] += 1
             res["blocks"] += len(hs)
         elif name.endswith(".log") or name.startswith("MANIFEST-"):
             recs = L.physical_records(img)
-            for r in recs:
-                body = np.frombuffer(img[r.offset + 6 : r.payload_offset + r.length], dtype=np.uint8)
-                res["records_bad_oracle"] += int(orc.unmask(r.stored) != orc.value(body))
+            if recs:
+                blk = np.zeros(len(recs), dtype=[("off", "<u8"), ("len", "<u4"), ("init", "<u4")])
+                blk["off"] = [r.offset + 6 for r in recs]  # type || payload
+                blk["len"] = [1 + r.length for r in recs]
+                stored = np.array([r.stored for r in recs], dtype=np.uint32)
+                res["records_bad_oracle"] += int((orc.batch(np.frombuffer(img, dtype=np.uint8), blk, flags=1,
+                                                            nthreads=8) != stored).sum())
             if a.gpu and recs:
                 res["records_bad_gpu"] += int((L.verify_log(img)[1] == 0).sum())
             res["logs"] += 1
