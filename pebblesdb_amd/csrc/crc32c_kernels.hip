@@ -25,6 +25,7 @@
 // 8 shift-operator slots (32 KiB): the whole 160 KiB of a CU; one 1024-thread workgroup per CU
 // stages it once and walks blocks persistently.  DESIGN.md §3-§6 has the measurements.
 #include "crc32c_device.h"
+#include "crc32c_lanespan.h"
 
 namespace pdb {
 namespace {
@@ -130,8 +131,8 @@ hipError_t launch_fixed(const LaunchGeom& g, const uint32_t* d_tables, const uin
       hipLaunchKernelGGL((crc_sst1k_kernel<FixedSrc, OutSink, true>), grid, block, 0, s, d_tables, src, nblk, sink);
       return hipGetLastError();
     }
-    if (len - 1u <= 1022u) {  // one lane per record (profiles/r01_ab_lanerec.json, r01_ab_rec*.json)
-      launch_lanerec(g, d_tables, src, nblk, len <= 256u ? 256u : (len <= 512u ? 512u : 1023u), sink, s);
+    if (len - 1u <= 1022u) {  // one lane per record, bytes staged through LDS (crc32c_lanespan.h)
+      launch_lanespan(g, d_tables, src, nblk, len <= 256u ? 256u : (len <= 512u ? 512u : 1023u), sink, s);
       return hipGetLastError();
     }
   }
@@ -165,9 +166,9 @@ hipError_t launch_desc_sink(const LaunchGeom& g, const uint32_t* d_tables, const
       hipLaunchKernelGGL((crc_sst1k_kernel<DescSrc, Sink, true>), grid, block, 0, s, d_tables, src, nblk, sink);
     else if (flags & PDB_CRC_SIZE_4K)  // sstable data blocks: 4-KiB body + batched prefix
       hipLaunchKernelGGL((crc_sst4k_kernel<DescSrc, Sink, true>), grid, block, 0, s, d_tables, src, nblk, sink);
-    else  // records of 1..1023 B: one lane per record (the window sized by the hint)
-      launch_lanerec(g, d_tables, src, nblk,
-                     (flags & PDB_CRC_SIZE_256) ? 256u : ((flags & PDB_CRC_SIZE_512) ? 512u : 1023u), sink, s);
+    else  // records of 1..1023 B: one lane per record, the bytes staged through LDS by coalesced loads
+      launch_lanespan(g, d_tables, src, nblk,
+                      (flags & PDB_CRC_SIZE_256) ? 256u : ((flags & PDB_CRC_SIZE_512) ? 512u : 1023u), sink, s);
     return hipGetLastError();
   }
   // descriptor lists of any lengths (C3: Zipf sizes at byte offsets): 16-B lane pieces with nt

@@ -713,6 +713,11 @@ hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tab
     case 58:
       hipLaunchKernelGGL((crc_quadrec_kernel<DescSrc, OutSink, 9, 512>), qgrid, block, 0, s, d_tables, src, nblk, sink);
       break;
+    case 60:  // round-1 lane-per-record kernels (direct 16-B window loads) for the <= 256 / 512 / 1023 classes
+    case 61:
+    case 62:
+      launch_lanerec(g, d_tables, src, nblk, v == 60 ? 256u : (v == 61 ? 512u : 1023u), sink, s);
+      break;
     default:  // 0 (and unknown ids): the shipped routing
       return launch_desc(g, d_tables, base, blk, nblk, flags, kModeOut, nullptr, out, nullptr, nullptr, s);
   }

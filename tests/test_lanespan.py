@@ -1,0 +1,127 @@
+"""GPU parity of the LDS-staged record kernel (crc_lanespan_kernel, pebblesdb_amd/csrc/
+crc32c_lanespan.h) behind the PDB_CRC_SIZE_256 / _512 / _1023 hints and the 1..1023-B fixed strides:
+bit-exact against the oracle on WAL layouts (the reference's record framing, db/log_writer.cc), on
+descriptor lists it must cut into smaller groups (spread, unsorted, duplicated, overlapping,
+far apart: the staging may only read 16-B lines within 64 B of a record byte), with records outside
+the class in the same batches, at batch-boundary counts, and in verify mode.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+HINTS = ["256", "512", "1023"]
+
+
+@pytest.fixture(scope="module")
+def crc():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from pebblesdb_amd import crc32c
+
+    crc32c.init_device(0)
+    return crc32c
+
+
+def _check(crc, oracle_lib, base, offs, lens, hint, verify=True):
+    blk = crc.make_blocks(offs, lens)
+    d_base = torch.from_numpy(base).cuda()
+    d_blk = crc.blocks_to_device(blk)
+    exp = oracle_lib.batch(base, blk, flags=1, nthreads=8)
+    got = crc.batch(d_base, d_blk, masked=True, size_hint=hint).cpu().numpy().view(np.uint32)
+    bad = np.nonzero(got != exp)[0]
+    assert bad.size == 0, (hint, bad.size, int(bad[0]), int(lens[bad[0]]), int(offs[bad[0]]))
+    if verify:
+        wrong = exp.copy()
+        flip = np.arange(3, len(exp), 11)
+        wrong[flip] ^= 0x100
+        ok, nbad = crc.verify(d_base, d_blk, torch.from_numpy(wrong.view(np.int32)).cuda(), size_hint=hint)
+        okh = ok.cpu().numpy()
+        assert int(nbad.item()) == len(flip) and (okh[flip] == 0).all() and okh.sum() == len(exp) - len(flip)
+
+
+@pytest.mark.parametrize("payload,hint", [(100, "256"), (131, "256"), (255, "256"), (431, "512"), (300, "512"),
+                                          (511, "512"), (700, "1023"), (1000, "1023"), (131, "1023")])
+def test_wal_layouts(crc, oracle_lib, payload, hint):
+    """Log images as log::Writer lays them out: records + 7-byte headers, fragments at 32-KiB block
+    ends, block trailers; the CRC spans are type || payload."""
+    import oracle
+    from bench import wal_layout
+
+    offs, lens = wal_layout(3 << 20, payload)
+    base = oracle.splitmix_bytes(int(offs[-1] + lens[-1]) + 64, payload)
+    _check(crc, oracle_lib, base, offs, lens, hint)
+
+
+@pytest.mark.parametrize("hint", HINTS)
+def test_spread_unsorted_and_far_records(crc, oracle_lib, hint):
+    """Descriptor lists the span staging must split: gaps of 0..5000 B, a shuffled order, duplicated
+    and overlapping records, records 1 MiB apart, records outside the class among them."""
+    import oracle
+
+    cls = int(hint)
+    rng = np.random.Generator(np.random.PCG64(cls))
+    n = 6000
+    lens = rng.integers(1, cls + 1, size=n)
+    gaps = np.where(rng.random(n) < 0.7, rng.integers(0, 64, size=n), rng.integers(64, 5000, size=n))
+    offs = np.concatenate([[5], 5 + np.cumsum(lens + gaps)[:-1]])
+    far = rng.random(n) < 0.05  # some records 1 MiB further on
+    offs = offs + np.cumsum(far) * (1 << 20)
+    perm = rng.permutation(n)
+    offs, lens = offs.copy(), lens.copy()
+    offs[perm[: n // 4]] = offs[np.sort(perm[: n // 4])]  # a quarter of the list out of order
+    lens[perm[: n // 4]] = lens[np.sort(perm[: n // 4])]
+    dup = rng.choice(n, size=200, replace=False)
+    offs[dup] = offs[(dup + 1) % n]  # duplicates / overlaps of a neighbour
+    out = rng.choice(n, size=100, replace=False)
+    lens[out] = rng.choice([0, cls + 1, 2000, 70000], size=100)  # outside the class (whole-wave path)
+    total = int((offs + lens).max()) + 64
+    base = oracle.splitmix_bytes(total, cls + 1)
+    _check(crc, oracle_lib, base, offs, lens, hint)
+
+
+@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 127, 129, 4095, 4097])
+def test_batch_boundaries(crc, oracle_lib, n):
+    import oracle
+
+    for hint, L in (("256", 131), ("512", 431), ("1023", 1000)):
+        lens = np.full(n, L)
+        lens[::7] = L - 3
+        offs = np.concatenate([[3], 3 + np.cumsum(lens + 7)[:-1]])
+        base = oracle.splitmix_bytes(int(offs[-1] + lens[-1]) + 64, n + L)
+        _check(crc, oracle_lib, base, offs, lens, hint, verify=n > 20)
+
+
+@pytest.mark.parametrize("length", [1, 3, 4, 5, 17, 131, 255, 256, 257, 300, 431, 512, 513, 700, 1000, 1023])
+@pytest.mark.parametrize("shift", [0, 1, 3])
+def test_fixed_strides(crc, oracle_lib, length, shift):
+    """pdb_crc32c_batch_device_fixed with 1..1023-B blocks (the same kernel, FixedSrc)."""
+    from pebblesdb_amd import diag
+
+    nblk = 3001
+    for stride in (length, length + 7):
+        total = shift + (nblk - 1) * stride + length
+        d = torch.empty(total + 64, dtype=torch.uint8, device="cuda")
+        diag.fill_splitmix(d, stride * 3 + shift)
+        view = d[shift : shift + total]
+        got = crc.batch_fixed(view, stride, length, nblk, masked=True).cpu().numpy().view(np.uint32)
+        blk = crc.make_blocks(np.arange(nblk) * stride, np.full(nblk, length))
+        exp = oracle_lib.batch(view.cpu().numpy(), blk, flags=1, nthreads=8)
+        assert (got == exp).all(), (length, stride, shift)
+
+
+def test_matches_round1_lane_kernels(crc, oracle_lib):
+    """The round-1 direct-load kernels (diagnostics variants 60-62) give the same CRCs."""
+    import oracle
+    from bench import wal_layout
+    from pebblesdb_amd import diag
+
+    for payload, hint, v in ((131, crc.SIZE_256, 60), (431, crc.SIZE_512, 61), (700, crc.SIZE_1023, 62)):
+        offs, lens = wal_layout(2 << 20, payload)
+        base = oracle.splitmix_bytes(int(offs[-1] + lens[-1]) + 64, payload + 9)
+        d_base, d_blk = torch.from_numpy(base).cuda(), crc.blocks_to_device(crc.make_blocks(offs, lens))
+        a = diag.batch_desc(0, d_base, d_blk, flags=hint).cpu().numpy()
+        b = diag.batch_desc(v, d_base, d_blk, flags=hint).cpu().numpy()
+        assert (a == b).all()
