@@ -35,8 +35,8 @@ namespace {
 constexpr uint32_t kSpanTabBytes = 64u << 10;
 constexpr uint32_t kSpanOpBase = kSpanTabBytes;                   // ops: 0 = 16, 1 = 64, 2 = 256, 3 = 1024
 constexpr uint32_t kSpanStageBase = kSpanOpBase + 4u * 4096u;     // 80 KiB
-constexpr uint32_t kSpanWaves = 4;
-constexpr uint32_t kSpanJ = 20;                                   // 1-KiB load instructions per item
+constexpr uint32_t kSpanWaves = 8;
+constexpr uint32_t kSpanJ = 10;                                   // 1-KiB load instructions per item
 constexpr uint32_t kSpanRegion = kSpanJ * 1024u;                  // staging bytes per wave
 constexpr uint32_t kSpanUsable = kSpanRegion - 16u;               // span limit: reads stay inside
 static_assert(kSpanStageBase + kSpanWaves * kSpanRegion == PDB_LDS_BYTES, "the whole 160 KiB");
@@ -158,62 +158,76 @@ __device__ __forceinline__ uint32_t span_slow_record(const char* lds, const Lane
   return __builtin_amdgcn_readfirstlane(acc);
 }
 
-// One item: a group of consecutive lanes of a batch whose records' bytes [lo, lo + 1 KiB x chunks)
-// are loaded into the wave's LDS region.  Per lane: the record's local start / end in the region
-// (p_loc = kNoRec for lanes outside the group or outside the class) and the sink's preloaded word.
+// ---- items ---------------------------------------------------------------------------------------
+// A batch is 64 consecutive records (lane r of the batch registers: record 64 * batch + r).  Its
+// in-class records are hashed by items: runs of up to G = floor(64 / k) consecutive records, each
+// record on k consecutive lanes (lane u: record slot u / k, part c = u % k).  Per record 2k chains:
+// chain i covers the words [nw - L(i + 1), nw - L i) counted from the record's END (L = kSpanL
+// words), the last chain (i = 2k - 1, the head) everything before as well; part c runs chains 2c
+// (A) and 2c + 1 (B).  All chains of an item run in lock step for `iters` = max(L, nw - (2k-1) L)
+// steps: the head chain alone for the first iters - L, then every chain for L.  Folds: per lane
+// P = shift(B, 4L) ^ A, then across the k lanes of a record shift(P[c + m], 8Lm) ^ P[c] for m = 1,
+// 2, 4.  k per batch minimises steps per record for its longest in-class record (span_pick).
 constexpr uint32_t kNoRec = 0x3FFFFFFFu;
+constexpr uint32_t kSpanL = 16;  // words per tail chain: 64 B, the slot-1 fold
 
-struct SpanItem {
-  uint64_t batch;   // records 64*batch + lane
-  uintptr_t lo;     // 16-B aligned global address of region byte 0
-  uint32_t nw;      // words to hash: max over the group's records of ceil(n / 4)
-  bool valid;
-  uint32_t p_loc, e_loc, pre;  // per lane
+struct LaneSpanGeom {
+  uint32_t k;      // lanes per record
+  uint32_t g;      // records per item: floor(64 / k)
+  uint32_t magic;  // ceil(65536 / k): u / k = (u * magic) >> 16 for u < 64
+  uint32_t iters;  // chain steps per item
 };
 
-// Lanes per item for a batch: the largest power of two B such that every group of B consecutive
-// lanes (a) spans at most kSpanUsable bytes from its first record's 16-B line, and (b) holds
-// records in ascending address order with gaps of at most 64 B between neighbours -- so every
-// 16-B chunk loaded lies within 64 B of a record byte, on a page that holds one: the staging
-// never reads memory a caller's blocks do not touch (a log image: 6-byte headers, <= 6-byte block
-// trailers between records).  A lane outside the class breaks the chain (groups split around it).
-template <uint32_t kUsable>
-__device__ __forceinline__ uint32_t span_group_size(uint32_t u, bool fast, uintptr_t p, uint32_t n) {
-  const uintptr_t e = p + n;
-  // link u -> u+1
-  const uint32_t np_lo = __shfl_down(static_cast<uint32_t>(p), 1, 64);
-  const uint32_t np_hi = __shfl_down(static_cast<uint32_t>(static_cast<uint64_t>(p) >> 32), 1, 64);
-  const uintptr_t pn = static_cast<uintptr_t>((static_cast<uint64_t>(np_hi) << 32) | np_lo);
-  const uint32_t fn = __shfl_down(fast ? 1u : 0u, 1, 64);
-  const bool link_ok = fast && fn && pn >= p && pn <= e + 64u;
-  const uint64_t broken = __builtin_amdgcn_ballot_w64(!link_ok && u < 63u);
-  uintptr_t mn = fast ? p : ~static_cast<uintptr_t>(0);
-  uintptr_t mx = fast ? e : 0;
-  uint32_t best = 1;
+// max over the wave of a 32-bit value; every lane must be active
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0xB1, 0xF, 0xF, false)));
+  v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x4E, 0xF, 0xF, false)));
+  v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x141, 0xF, 0xF, false)));
+  v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x140, 0xF, 0xF, false)));
+  const uint32_t a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 16);
+  const uint32_t c = __builtin_amdgcn_readlane(v, 32), d = __builtin_amdgcn_readlane(v, 48);
+  return max(max(a, b), max(c, d));
+}
+
+// k for a batch whose longest in-class record has nw words: fewest steps per record, counting the
+// records an item can hold (G, and what fits a staging region at ~4 nw + 8 bytes a record)
+template <uint32_t KMAX>
+__device__ __forceinline__ LaneSpanGeom span_pick(uint32_t nw) {
+  const float fit = static_cast<float>(kSpanUsable) * __builtin_amdgcn_rcpf(static_cast<float>(4u * nw + 8u));
+  uint32_t gfit = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(fit)));
+  gfit = gfit ? gfit : 1u;
+  LaneSpanGeom best{1u, 64u, 65536u, kSpanL};
+  uint32_t best_eff = 1u;
 #pragma unroll
-  for (uint32_t m = 1; m < 64; m <<= 1) {
-    const uint64_t omn = static_cast<uint64_t>(__shfl_xor(static_cast<uint32_t>(mn), m, 64)) |
-                         (static_cast<uint64_t>(__shfl_xor(static_cast<uint32_t>(static_cast<uint64_t>(mn) >> 32), m, 64)) << 32);
-    const uint64_t omx = static_cast<uint64_t>(__shfl_xor(static_cast<uint32_t>(mx), m, 64)) |
-                         (static_cast<uint64_t>(__shfl_xor(static_cast<uint32_t>(static_cast<uint64_t>(mx) >> 32), m, 64)) << 32);
-    mn = omn < mn ? static_cast<uintptr_t>(omn) : mn;
-    mx = omx > mx ? static_cast<uintptr_t>(omx) : mx;
-    const uint32_t B = m << 1;  // group size after this level
-    const bool span_ok = mx == 0 || (mx - (mn & ~static_cast<uintptr_t>(15))) <= kUsable;
-    uint64_t inner = ~0ull;  // link positions inside a group of B lanes (not the last lane of a group)
-#pragma unroll
-    for (uint32_t g = B - 1; g < 64; g += B) inner &= ~(1ull << g);
-    if (__builtin_amdgcn_ballot_w64(!span_ok) == 0 && (broken & inner) == 0) best = B;
-    else break;
+  for (uint32_t k = 1; k <= KMAX; ++k) {
+    const uint32_t g = 64u / k;
+    const uint32_t geff = g < gfit ? g : gfit;
+    const int32_t h = static_cast<int32_t>(nw) - static_cast<int32_t>((2u * k - 1u) * kSpanL);
+    const uint32_t it = h > static_cast<int32_t>(kSpanL) ? static_cast<uint32_t>(h) : kSpanL;
+    if (k == 1 || it * best_eff < best.iters * geff) {
+      best = LaneSpanGeom{k, g, (65536u + k - 1u) / k, it};
+      best_eff = geff;
+    }
   }
   return best;
 }
 
-template <class Src, class Sink, uint32_t MAXN, uint32_t kTailB>
+struct SpanItem {
+  uint64_t batch;   // records 64 * batch + r
+  uintptr_t lo;     // 16-B aligned global address of region byte 0
+  uint32_t hi;      // local end: max over the item's records (0: nothing to hash)
+  uint32_t k, iters;
+  bool valid;
+  uint32_t r, c;               // per lane: record slot in the batch, part
+  uint32_t p_loc, e_loc, pre;  // per lane: local start (kNoRec: no record), local end, sink word
+};
+
+template <class Src, class Sink, uint32_t MAXN>
 __global__ __launch_bounds__(kSpanWaves * 64) void crc_lanespan_kernel(const uint32_t* __restrict__ tabs, Src src,
                                                                        uint64_t nblk, Sink sink) {
-  static_assert(MAXN + 64u <= kSpanUsable, "a record of the class must fit a region");
-  static_assert(kTailB == 64u || kTailB == 256u, "the tail chain folds with slot 1 (64) or 2 (256)");
+  static_assert(MAXN + 32u <= kSpanUsable, "a record of the class must fit a region");
+  constexpr uint32_t KMAX = (MAXN + 8u * kSpanL - 1u) / (8u * kSpanL);  // 2k chains cover MAXN: 2, 4, 8
+  static_assert(KMAX >= 1 && KMAX <= 8, "tree folds for up to 8 lanes per record");
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
   char* lds = reinterpret_cast<char*>(lds_words);
   stage_tables_span(lds, tabs);
@@ -228,39 +242,40 @@ __global__ __launch_bounds__(kSpanWaves * 64) void crc_lanespan_kernel(const uin
   const uint64_t W = static_cast<uint64_t>(gridDim.x) * kSpanWaves;
   uint64_t bnext = static_cast<uint64_t>(blockIdx.x) * kSpanWaves + wv;  // next batch to open
   if (bnext >= nbat) return;  // wave-uniform; no barrier below
-  constexpr uint32_t kTailW = kTailB / 4u;
-  constexpr uint32_t kTailSlot = kTailB == 64u ? 1u : 2u;
 
   auto idx = [&](uint64_t bb) -> uint64_t {
     const uint64_t i = (bb << 6) + u;
     return i < nblk ? i : nblk - 1;
   };
-  // ---- the batch whose items are being issued --------------------------------------------------
+  // the next batch's descriptors and sink words, in flight; reloaded by every next_item call (the
+  // same address when no batch was opened) so no load is ever consumed right after it is issued
   typename Src::Raw raw_next = src.load(idx(bnext));
+  uint32_t pre_next = SinkOps<Sink>::pre(sink, idx(bnext), BlkDesc{nullptr, 0u, 0u});
   uint64_t bcur = 0;
   bool have_batch = false;
-  uintptr_t bp = 0;         // per lane: record start
-  uint32_t bn = 0;          // per lane: record length
-  bool bfast = false;       // per lane: in the class (hashed from LDS)
-  uint32_t bpre = 0;        // per lane: the sink's preloaded word
-  uint32_t bgroup = 64;     // lanes per item of this batch
-  uint32_t bnext_item = 0;  // next group to issue
+  uintptr_t bp = 0;      // per lane: record start
+  uint32_t bn = 0;       // per lane: record length
+  bool bfast = false;    // per lane: in the class (hashed from LDS)
+  uint32_t bpre = 0;     // per lane: the sink's word
+  uint64_t bfastm = 0;   // in-class records
+  uint64_t bbroken = 0;  // bit r: records r and r + 1 may not share an item
+  uint32_t bcursor = 64;
+  LaneSpanGeom bg{1u, 64u, 65536u, kSpanL};
 
-  // make the prefetched descriptors current, prefetch the next batch's; records outside the class
-  // are hashed here by the whole wave (rare: their loads wait behind the items in flight)
+  // make the prefetched batch current; records outside the class are hashed here by the whole
+  // wave (rare: their loads wait behind the items in flight)
   auto open_batch = [&]() -> bool {
     if (bnext >= nbat) return false;
     keep_alive(raw_next);
     const BlkDesc d = src.lane(raw_next);
+    bpre = pre_next;
     bcur = bnext;
     bnext += W;
-    raw_next = src.load(idx(bnext < nbat ? bnext : bcur));  // unconditional
     const uint64_t i = (bcur << 6) + u;
     const bool valid = i < nblk;
     bp = reinterpret_cast<uintptr_t>(d.p);
     bn = d.n;
     bfast = valid && (d.n - 1u) <= MAXN - 1u && d.init_raw == 0xFFFFFFFFu;
-    bpre = SinkOps<Sink>::pre(sink, idx(bcur), d);
     uint64_t sb = __builtin_amdgcn_ballot_w64(valid && !bfast);
     const uint32_t plo = static_cast<uint32_t>(bp), phi = static_cast<uint32_t>(static_cast<uint64_t>(bp) >> 32);
     while (sb) {
@@ -273,144 +288,180 @@ __global__ __launch_bounds__(kSpanWaves * 64) void crc_lanespan_kernel(const uin
         SinkOps<Sink>::put(sink, (bcur << 6) + k, rs, BlkDesc{reinterpret_cast<const uint8_t*>(sp), sn, 0xFFFFFFFFu},
                            __builtin_amdgcn_readlane(bpre, k));
     }
-    bgroup = __builtin_amdgcn_readfirstlane(span_group_size<kSpanUsable>(u, bfast, bp, bn));
-    bnext_item = 0;
+    bfastm = __builtin_amdgcn_ballot_w64(bfast);
+    // link r -> r + 1: both in the class, ascending, at most 64 B apart -- every 16-B chunk an item
+    // stages lies within 64 B of a record byte (a log image: 6-byte headers, <= 6-byte trailers)
+    const uint32_t np_lo = __shfl_down(plo, 1, 64), np_hi = __shfl_down(phi, 1, 64);
+    const uintptr_t pn = static_cast<uintptr_t>((static_cast<uint64_t>(np_hi) << 32) | np_lo);
+    const uint32_t fn = __shfl_down(bfast ? 1u : 0u, 1, 64);
+    const bool link_ok = bfast && fn && pn >= bp && pn <= bp + bn + 64u;
+    bbroken = __builtin_amdgcn_ballot_w64(!link_ok && u < 63u);
+    const uint32_t nw = wave_max_u32(bfast ? (bn + 3u) >> 2 : 0u);
+    bg = span_pick<KMAX>(nw ? nw : 1u);
+    bcursor = 0;
     return true;
   };
 
-  // the next item (a group with at least one record in the class), opening batches as needed
-  auto next_item = [&](SpanItem& it) -> bool {
-    for (;;) {
-      if (!have_batch || bnext_item * bgroup >= 64u) {
-        if (!open_batch()) return false;
-        have_batch = true;
-      }
-      const uint32_t g0 = bnext_item * bgroup;
-      ++bnext_item;
-      const bool mine = bfast && u >= g0 && u < g0 + bgroup;
-      if (__builtin_amdgcn_ballot_w64(mine) == 0) continue;
-      uintptr_t mn = mine ? bp : ~static_cast<uintptr_t>(0);
-      uint32_t w = mine ? (bn + 3u) >> 2 : 0u;
-#pragma unroll
-      for (uint32_t m = 1; m < 64; m <<= 1) {
-        const uint64_t o = static_cast<uint64_t>(__shfl_xor(static_cast<uint32_t>(mn), m, 64)) |
-                           (static_cast<uint64_t>(__shfl_xor(static_cast<uint32_t>(static_cast<uint64_t>(mn) >> 32), m, 64)) << 32);
-        mn = o < mn ? static_cast<uintptr_t>(o) : mn;
-        const uint32_t ow = __shfl_xor(w, m, 64);
-        w = ow > w ? ow : w;
-      }
-      it.lo = static_cast<uintptr_t>(uniform64(static_cast<uint32_t>(mn), static_cast<uint32_t>(static_cast<uint64_t>(mn) >> 32))) &
-              ~static_cast<uintptr_t>(15);
-      it.nw = __builtin_amdgcn_readfirstlane(w);
-      it.batch = bcur;
-      it.valid = true;
-      it.p_loc = mine ? static_cast<uint32_t>(bp - it.lo) : kNoRec;
-      it.e_loc = mine ? static_cast<uint32_t>(bp + bn - it.lo) : 0u;
-      it.pre = bpre;
-      return true;
+  // the next item: the next run of in-class records of the current batch (or of the next batch);
+  // every field is set on every path (a partially written item ends up in scratch)
+  auto next_item = [&](bool want) -> SpanItem {
+    SpanItem it;
+    it.valid = false;
+    it.batch = bcur;
+    it.lo = dummy;
+    it.hi = 0;
+    it.k = bg.k;
+    it.iters = bg.iters;
+    it.r = u;
+    it.c = 0;
+    it.p_loc = kNoRec;
+    it.e_loc = 0;
+    it.pre = 0;
+    if (!want) return it;
+    uint64_t rem = (have_batch && bcursor < 64u) ? (bfastm & (~0ull << bcursor)) : 0ull;
+    if (rem == 0) {
+      if (!open_batch()) return it;
+      have_batch = true;
+      rem = bfastm;
     }
+    raw_next = src.load(idx(bnext < nbat ? bnext : bcur));
+    pre_next = SinkOps<Sink>::pre(sink, idx(bnext < nbat ? bnext : bcur), BlkDesc{nullptr, 0u, 0u});
+    it.valid = true;
+    it.batch = bcur;
+    it.k = bg.k;
+    it.iters = bg.iters;
+    if (rem == 0) {  // every record of the batch was outside the class: an empty item
+      bcursor = 64;
+      return it;
+    }
+    const uint32_t g0 = static_cast<uint32_t>(__builtin_ctzll(rem));
+    const uint64_t br = bbroken >> g0;
+    const uint32_t m1 = br ? static_cast<uint32_t>(__builtin_ctzll(br)) + 1u : 64u - g0;
+    const uint32_t plo = static_cast<uint32_t>(bp), phi = static_cast<uint32_t>(static_cast<uint64_t>(bp) >> 32);
+    const uintptr_t lo = static_cast<uintptr_t>(uniform64(__builtin_amdgcn_readlane(plo, g0), __builtin_amdgcn_readlane(phi, g0))) &
+                         ~static_cast<uintptr_t>(15);
+    const uint64_t over = __builtin_amdgcn_ballot_w64(bfast && u >= g0 && (bp + bn - lo) > kSpanUsable) >> g0;
+    const uint32_t m2 = over ? static_cast<uint32_t>(__builtin_ctzll(over)) : 64u;
+    const uint32_t m = min(min(bg.g, m1), m2);
+    bcursor = g0 + m;
+    const uint32_t slot = (u * bg.magic) >> 16;
+    const uint32_t c = u - slot * bg.k;
+    const bool act = slot < m;
+    const uint32_t rl = act ? g0 + slot : u;
+    const uintptr_t pr = static_cast<uintptr_t>((static_cast<uint64_t>(__shfl(phi, rl, 64)) << 32) | __shfl(plo, rl, 64));
+    const uint32_t nr = __shfl(bn, rl, 64);
+    it.pre = __shfl(bpre, rl, 64);
+    it.r = rl;
+    it.c = c;
+    it.lo = lo;
+    it.p_loc = act ? static_cast<uint32_t>(pr - lo) : kNoRec;
+    it.e_loc = act ? static_cast<uint32_t>(pr + nr - lo) : 0u;
+    it.hi = wave_max_u32(it.e_loc);
+    return it;
   };
 
   // loads of one item: kSpanJ unconditional 16-B loads (1 KiB contiguous per instruction); chunks
-  // wholly past the group's last byte read the dummy line instead
-  auto issue = [&](u32x4 (&A)[kSpanJ], const SpanItem& it, uint32_t& nchunks) {
-    uint32_t hi = it.valid ? it.e_loc : 0u;  // local end, max over lanes
-#pragma unroll
-    for (uint32_t m = 1; m < 64; m <<= 1) {
-      const uint32_t o = __shfl_xor(hi, m, 64);
-      hi = o > hi ? o : hi;
-    }
-    hi = __builtin_amdgcn_readfirstlane(hi);
-    nchunks = (hi + 1023u) >> 10;
-    const uintptr_t lo = it.valid ? it.lo : dummy;
+  // wholly past the item's last byte read the dummy line instead
+  auto issue = [&](u32x4 (&A)[kSpanJ], const SpanItem& it) {
+    const uint32_t hi = it.hi;  // 0 for an invalid or empty item
+    const uintptr_t lo = it.lo;
 #pragma unroll
     for (uint32_t j = 0; j < kSpanJ; ++j) {
       const uint32_t off = 1024u * j + 16u * u;
       A[j] = gload128<true>(off < hi ? lo + off : dummy);
     }
   };
-  auto to_lds = [&](const u32x4 (&A)[kSpanJ], uint32_t nchunks) {
+  // every chunk is written, the dummy ones too: a load whose register is never read stays
+  // outstanding, and the compiler then drains the counter before the register is reloaded
+  auto to_lds = [&](const u32x4 (&A)[kSpanJ]) {
 #pragma unroll
-    for (uint32_t j = 0; j < kSpanJ; ++j)
-      if (j < nchunks) *reinterpret_cast<u32x4*>(region + 1024u * j + 16u * u) = A[j];
+    for (uint32_t j = 0; j < kSpanJ; ++j) *reinterpret_cast<u32x4*>(region + 1024u * j + 16u * u) = A[j];
   };
-  // hash an item staged in the region: chain A = the words before the last kTailB bytes, chain B =
-  // the tail, folded as shift(A, kTailB) ^ B
+  // hash an item staged in the region
   auto hash = [&](const SpanItem& it) {
-    const int32_t nw = static_cast<int32_t>(it.nw);
+    if (it.hi == 0) return;
+    const uint32_t k = it.k, iters = it.iters, lim = iters - kSpanL;
     const int32_t e = static_cast<int32_t>(it.e_loc);
     const int32_t pl = static_cast<int32_t>(it.p_loc);
+    const bool head = it.c == k - 1u;
     const uint32_t sel = static_cast<uint32_t>(e & 3) * 0x01010101u + 0x03020100u;
     const uint32_t uz = __shfl(ureg, static_cast<uint32_t>(pl - e) & 3u, 64);
-    // word j starts at s_j = e - 4 (nw - j): bytes sh.. of the dword pair (D[q_j], D[q_j + 1]),
-    // q_j = s_j >> 2 (floor), masked below p; the word holding p injects U[z]
+    // word at byte s (s = e mod 4): bytes of the dword pair (D[s >> 2], D[(s >> 2) + 1]), masked
+    // below p; the word holding p injects U[z] (z bytes of it before p)
     auto dword = [&](int32_t q) -> uint32_t { return lds_u32(region, static_cast<uint32_t>(q < 0 ? 0 : q) << 2); };
-    auto word = [&](int32_t j, uint32_t& lo_dw) -> uint32_t {
-      const int32_t s = e - 4 * (nw - j);
+    auto word = [&](int32_t s, uint32_t& lo_dw) -> uint32_t {
       const uint32_t hi_dw = dword((s >> 2) + 1);
       const uint32_t w = __builtin_amdgcn_perm(hi_dw, lo_dw, sel);
       lo_dw = hi_dw;
-      const int32_t z = pl - s;  // bytes of the word before the record
-      const uint32_t m = z <= 0 ? 0xFFFFFFFFu : (z >= 4 ? 0u : (0xFFFFFFFFu << (8u * static_cast<uint32_t>(z))));
-      return (w & m) ^ ((z >= 0 && z < 4) ? uz : 0u);
+      const int32_t z = pl - s;
+      const uint32_t zc = static_cast<uint32_t>(z < 0 ? 0 : (z > 4 ? 4 : z));
+      const uint32_t m = static_cast<uint32_t>(0xFFFFFFFFull << (8u * zc));
+      return (w & m) ^ (static_cast<uint32_t>(z) < 4u ? uz : 0u);
     };
-    const int32_t ntail = nw < static_cast<int32_t>(kTailW) ? nw : static_cast<int32_t>(kTailW);
-    const int32_t nhead = nw - ntail;
-    uint32_t la = dword((e - 4 * nw) >> 2), lb = dword((e - 4 * ntail) >> 2);
-    uint32_t xa = nhead > 0 ? word(0, la) : 0u;
-    uint32_t xb = word(nhead, lb);
-    for (int32_t k = 1; k < ntail; ++k) {
-      if (k < nhead) xa = step4x16(lds, lt, xa, word(k, la));
-      xb = step4x16(lds, lt, xb, word(nhead + k, lb));
+    const int32_t sA0 = e - static_cast<int32_t>(8u * kSpanL * it.c) - 4 * static_cast<int32_t>(iters);
+    const int32_t sB0 = sA0 - 4 * static_cast<int32_t>(kSpanL);
+    uint32_t lb = dword(sB0 >> 2);
+    uint32_t xb = word(sB0, lb);
+    if (lim > 0) {  // the head chain's first words (junk on the other lanes, dropped)
+      for (uint32_t t = 1; t < lim; ++t) xb = step4x16(lds, lt, xb, word(sB0 + 4 * static_cast<int32_t>(t), lb));
+      xb = head ? xb : 0u;
+      xb = step4x16(lds, lt, xb, word(sB0 + 4 * static_cast<int32_t>(lim), lb));
     }
-    for (int32_t k = ntail; k < nhead; ++k) xa = step4x16(lds, lt, xa, word(k, la));
-    xb = step4x16(lds, lt, xb, 0u);
-    uint32_t c = xb;
-    if (nhead > 0) c = span_op_x(lds, kTailSlot, step4x16(lds, lt, xa, 0u), xb);
-    if (it.p_loc != kNoRec)
-      SinkOps<Sink>::put(sink, (it.batch << 6) + u, c, BlkDesc{nullptr, 0u, 0xFFFFFFFFu}, it.pre);
+    const int32_t sa = sA0 + 4 * static_cast<int32_t>(lim);
+    const int32_t sb = sB0 + 4 * static_cast<int32_t>(lim);
+    uint32_t la = dword(sa >> 2);
+    uint32_t xa = word(sa, la);
+#pragma unroll
+    for (uint32_t t = 1; t < kSpanL; ++t) {
+      xa = step4x16(lds, lt, xa, word(sa + 4 * static_cast<int32_t>(t), la));
+      xb = step4x16(lds, lt, xb, word(sb + 4 * static_cast<int32_t>(t), lb));
+    }
+    const uint32_t ca = step4x16(lds, lt, xa, 0u), cb = step4x16(lds, lt, xb, 0u);
+    uint32_t P = span_op_x(lds, 1, cb, ca);  // shift(B, 64 B) ^ A
+#pragma unroll
+    for (uint32_t lvl = 0; lvl < 3; ++lvl) {
+      const uint32_t m = 1u << lvl;
+      if (m >= k) break;
+      const uint32_t y = __shfl_down(P, m, 64);  // part c + m: the 128 m bytes before
+      if ((it.c & (2u * m - 1u)) == 0 && it.c + m < k) P = span_shift_x(lds, 3u + lvl, y, P);
+    }
+    if (it.c == 0 && it.p_loc != kNoRec)
+      SinkOps<Sink>::put(sink, (it.batch << 6) + it.r, P, BlkDesc{nullptr, 0u, 0xFFFFFFFFu}, it.pre);
   };
 
-  // ---- pipeline: two items in flight while one is hashed ---------------------------------------
-  SpanItem I0{}, I1{}, I2{};
-  u32x4 A[kSpanJ], B[kSpanJ];
-  uint32_t na = 0, nb = 0;
-  I0.valid = next_item(I0);
-  issue(A, I0, na);
-  I1.valid = I0.valid && next_item(I1);
-  issue(B, I1, nb);
-  while (I0.valid) {
-    to_lds(A, na);
-    I2.valid = I1.valid && next_item(I2);
-    issue(A, I2, na);  // A is free again: the item after next
-    hash(I0);
-    if (!I1.valid) break;
-    to_lds(B, nb);
-    I0 = I2;
-    I2.valid = I0.valid && next_item(I2);
-    issue(B, I2, nb);
-    hash(I1);
-    I1 = I2;
+  // ---- pipeline: the next item's loads in flight while one is hashed ------------------------------
+  // (one register array: with two, the compiler's wait counting across the loop's back edge drains
+  // both arrays at the loop head; eight waves per CU keep ~70 KiB in flight per CU)
+  u32x4 A[kSpanJ];
+  SpanItem cur = next_item(true);
+  issue(A, cur);
+  while (cur.valid) {
+    to_lds(A);
+    const SpanItem nxt = next_item(true);
+    issue(A, nxt);
+    hash(cur);
+    cur = nxt;
   }
 }
 
-// grid: one wave per batch of 64 records, 4 waves per workgroup, at most one workgroup per CU
+// grid: one wave per batch of 64 records, 8 waves per workgroup, at most one workgroup per CU
 inline uint32_t grid_span(const LaunchGeom& g, uint64_t nblk) {
   const uint64_t want = ((nblk + 63) / 64 + kSpanWaves - 1) / kSpanWaves;
   return static_cast<uint32_t>(want < g.grid ? (want ? want : 1) : g.grid);
 }
 
-// Records of 1..1023 B by class: <= 256 B (tail chain 64 B), 257..512 and 513..1023 B (tail 256 B).
+// Records of 1..1023 B by class (the class bounds the lanes per record: 2, 4, 8); longer ones, and
+// empty ones, take the whole-wave path.
 template <class Src, class Sink>
 void launch_lanespan(const LaunchGeom& g, const uint32_t* d_tables, const Src& src, uint64_t nblk, uint32_t cls,
                      const Sink& sink, hipStream_t s) {
   const dim3 grid(grid_span(g, nblk)), block(kSpanWaves * 64);
   if (cls <= 256u)
-    hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 256, 64>), grid, block, 0, s, d_tables, src, nblk, sink);
+    hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 256>), grid, block, 0, s, d_tables, src, nblk, sink);
   else if (cls <= 512u)
-    hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 512, 256>), grid, block, 0, s, d_tables, src, nblk, sink);
+    hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 512>), grid, block, 0, s, d_tables, src, nblk, sink);
   else
-    hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 1023, 256>), grid, block, 0, s, d_tables, src, nblk, sink);
+    hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 1023>), grid, block, 0, s, d_tables, src, nblk, sink);
 }
 
 }  // namespace

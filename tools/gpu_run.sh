@@ -21,6 +21,9 @@ for s in "$@"; do
   case "$s" in
     tests) step tests 1000 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread ;;
     cold) step cold 300 python tools/cold_start.py ;;
+    lanespan) step lanespan 600 python -u -m pytest tests/test_lanespan.py tests/test_sst4k.py -m gpu -x -v --timeout 200 --timeout-method thread ;;
+    ab_lanespan) step ab_lanespan 600 python tools/ab_lanespan.py ;;
+    counters_span) step counters_span 900 bash tools/counters_span.sh ${TAG}_span wal100 wal400 ;;
     integ) step integ 600 python -u -m pytest tests/test_integration.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
     fullsize) step fullsize 600 python -u -m pytest tests/test_full_size.py tests/test_gpu_parity.py -m gpu -x -v --timeout 300 --timeout-method thread -k "full_size or host_" ;;
     bench_driver) step bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
