@@ -9,23 +9,24 @@
 // instruction 1 KiB contiguous), written to the wave's LDS region, and every lane then reads its
 // own record from LDS.
 //
-// LDS image (160 KiB, one 256-thread workgroup = 4 waves per CU):
+// LDS image (160 KiB, one 512-thread workgroup = 8 waves per CU):
 //   [0, 64 KiB)      T0..T3 replicated 16x: entry b of table k, replica r at b<<8 | k<<6 | r<<2 (lane
-//                    l uses replica l & 15: 2-way bank conflicts, the price of fitting the staging)
-//   [64, 80 KiB)     4 shift operators (16, 64, 256, 1024 B), single copy: the chain fold and the
-//                    whole-wave slow path (32 = 16 twice, 128 = 64 twice, 512 = 256 twice)
-//   [80, 160 KiB)    4 x 20 KiB: one staging region per wave
-// A wave handles batches of 64 consecutive records (lane u: record 64b + u).  If the batch's span
-// does not fit a region (records spread out, or large), it is cut into sub-batches of 32, 16, ...
-// lanes (groups of consecutive lanes whose span fits: always possible, a record of the class is
-// < 20 KiB); only the group's lanes hash while it is staged.  Items (sub-batches) are pipelined
-// two deep in registers: while item k is hashed from LDS, items k+1 and k+2 are in flight.
-// Per lane, the record is END-aligned on a grid of 4-byte words: word j = bytes [e - 4(NW - j), +4)
-// built by one v_perm from two LDS dwords, bytes before p zeroed, U[z] injected at the word
-// holding p (z zeroed bytes: the state entering the record is Value()'s 0xFFFFFFFF), hashed as two
-// slice-by-4 chains (the last kTailB bytes separately, folded with one shift operator).  Records
-// outside the class (0 B, > MAXN) are hashed by the whole wave when their batch is opened (slow
-// path: global loads, the same operators; rare, so their loads may wait behind the items in flight).
+//                    l uses replica l & 15: 2-way bank conflicts, the price of fitting the staging;
+//                    slice-by-2 over 32 conflict-free replicas of T0, T1 fits too, but doubles the
+//                    dependent lookups per word and measured slower: the loop is latency- and
+//                    issue-bound, not LDS-bound)
+//   [64, 80 KiB)     4 shift operators (16, 64, 256, 32 B), single copy: the chain and part folds
+//                    and the whole-wave slow path (128 = 64 twice, 512 = 256 twice, 1024 = 256 x 4)
+//   [80, 160 KiB)    8 x 10 KiB: one staging region per wave
+// A wave handles batches of 64 consecutive records; their records are hashed by items (runs of
+// consecutive records whose span fits a region, each record on k lanes: see "items" below).  The
+// next item's loads are in flight while one is hashed.  Per lane, a record part is END-aligned on a
+// grid of 4-byte words built by one v_perm from two LDS dwords and hashed as four interleaved
+// slice-by-4 chains; the word holding the record's first byte p is masked below p and injects U[z]
+// (z masked bytes: the state entering the record is Value()'s 0xFFFFFFFF), and it REPLACES the
+// state of its chain, so no word before it needs masking.  Records outside the class (0 B, > MAXN)
+// are hashed by the whole wave when their batch is opened (slow path: global loads, the same
+// operators; rare, so their loads may wait behind the item in flight).
 #pragma once
 #include "crc32c_device.h"
 
@@ -33,32 +34,13 @@ namespace pdb {
 namespace {
 
 constexpr uint32_t kSpanTabBytes = 64u << 10;
-constexpr uint32_t kSpanOpBase = kSpanTabBytes;                   // ops: 0 = 16, 1 = 64, 2 = 256, 3 = 1024
+constexpr uint32_t kSpanOpBase = kSpanTabBytes;                   // ops: 0 = 16, 1 = 64, 2 = 256, 3 = 32
 constexpr uint32_t kSpanStageBase = kSpanOpBase + 4u * 4096u;     // 80 KiB
 constexpr uint32_t kSpanWaves = 8;
 constexpr uint32_t kSpanJ = 10;                                   // 1-KiB load instructions per item
 constexpr uint32_t kSpanRegion = kSpanJ * 1024u;                  // staging bytes per wave
 constexpr uint32_t kSpanUsable = kSpanRegion - 16u;               // span limit: reads stay inside
 static_assert(kSpanStageBase + kSpanWaves * kSpanRegion == PDB_LDS_BYTES, "the whole 160 KiB");
-
-struct LaneTabs16 {
-  uint32_t t3, t2, t1, t0;  // v_perm byte 0 of the lookup address: k<<6 | replica<<2
-};
-
-__device__ __forceinline__ LaneTabs16 lane_tabs16(uint32_t lane) {
-  const uint32_t r = (lane & 15u) << 2;
-  return LaneTabs16{(3u << 6) | r, (2u << 6) | r, (1u << 6) | r, r};
-}
-
-// x' = shift(x, 4) ^ wnext with the 16-replica layout (the data byte lands in address bits 8..15:
-// one v_perm per lookup, as step4x)
-__device__ __forceinline__ uint32_t step4x16(const char* lds, const LaneTabs16& lt, uint32_t x, uint32_t wnext) {
-  const uint32_t a3 = __builtin_amdgcn_perm(lt.t3, x, sel_byte(0));
-  const uint32_t a2 = __builtin_amdgcn_perm(lt.t2, x, sel_byte(1));
-  const uint32_t a1 = __builtin_amdgcn_perm(lt.t1, x, sel_byte(2));
-  const uint32_t a0 = __builtin_amdgcn_perm(lt.t0, x, sel_byte(3));
-  return xor3(xor3(lds_u32(lds, a3), lds_u32(lds, a2), lds_u32(lds, a1)), lds_u32(lds, a0), wnext);
-}
 
 __device__ __forceinline__ uint32_t span_op_x(const char* lds, uint32_t slot, uint32_t c, uint32_t y) {
   const uint32_t base = kSpanOpBase + slot * 4096u;
@@ -69,48 +51,142 @@ __device__ __forceinline__ uint32_t span_op_x(const char* lds, uint32_t slot, ui
   return xor3(xor3(v0, v1, v2), v3, y);
 }
 
-// shift(c, 16 << k) ^ y for k = 0..6 from the four slots (odd k: the slot below, twice)
+// shift(c, 16 << k) ^ y for k = 0..5 from the four slots (16, 32, 64, 64 x 2, 256, 256 x 2)
 __device__ __forceinline__ uint32_t span_shift_x(const char* lds, uint32_t k, uint32_t c, uint32_t y) {
-  const uint32_t slot = k >> 1;
-  if (k & 1u) c = span_op_x(lds, slot, c, 0u);
-  return span_op_x(lds, slot, c, y);
+  switch (k) {
+    case 0: return span_op_x(lds, 0, c, y);
+    case 1: return span_op_x(lds, 3, c, y);
+    case 2: return span_op_x(lds, 1, c, y);
+    case 3: return span_op_x(lds, 1, span_op_x(lds, 1, c, 0u), y);
+    case 4: return span_op_x(lds, 2, c, y);
+    default: return span_op_x(lds, 2, span_op_x(lds, 2, c, 0u), y);
+  }
 }
 
-__device__ __forceinline__ void stage_tables_span(char* lds, const uint32_t* __restrict__ tabs) {
-  // T0..T3 x 16 replicas: 4 x 256 entries x 4 quads of 16 B
-  for (uint32_t i0 = 0; i0 < 4096u; i0 += 4u * blockDim.x) {
-    uint32_t v[4];
+// Table schemes (the kernel's TP parameter), 64 KiB of LDS each:
+//   TabsS4: slice-by-4, T0..T3 x 16 replicas laid out so that every lookup is bank-conflict free.
+//     A ds_read_b32 serves its 64 lanes as two groups of 32, one bank ((a / 4) mod 32) per lane.
+//     Replica r of T_k sits at dword (k & 1) * 32 + (k >> 1) * 16 + r of each entry's 256 B: bank
+//     (k >> 1) * 16 + r.  Lanes with bit 4 clear do their four lookups in the order T3, T2, T1, T0,
+//     lanes with bit 4 set in the order T1, T0, T3, T2: in every instruction the two halves of a
+//     group read tables in opposite bank halves, each lane of a half its own replica.
+//   TabsS4w: the same tables, every lane in the order T3..T0 (replica r of T_k at bank (k & 1) * 16
+//     + r): 2-way conflicts on every lookup (diagnostics A/B).
+//   TabsS2: slice-by-2, T0, T1 x 32 replicas (two dependent lookup rounds per word; diagnostics).
+struct LaneTabs4 {
+  uint32_t t[4];  // v_perm byte 0 of the lookup address: table and replica bits
+  uint32_t s[4];  // v_perm selector: which byte of the state indexes lookup i
+};
+
+template <bool kSplit>
+struct TabsS4T {
+  typedef LaneTabs4 LT;
+  __device__ static __forceinline__ uint32_t tbyte(uint32_t k, uint32_t r) {
+    return kSplit ? (((k & 1u) << 7) | ((k >> 1) << 6) | (r << 2)) : ((k << 6) | (r << 2));
+  }
+  __device__ static __forceinline__ LT lane(uint32_t u) {
+    const uint32_t r = u & 15u;
+    const bool hi = kSplit && (u & 16u);
+    LT lt;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t i = i0 + threadIdx.x + j * blockDim.x;
-      v[j] = i < 4096u ? tabs[(i >> 2)] : 0u;  // tabs: T0[256] T1[256] T2[256] T3[256]; i >> 2 = k*256 + b
+    for (uint32_t i = 0; i < 4; ++i) {
+      const uint32_t j = hi ? ((i + 2u) & 3u) : i;  // the state byte looked up by instruction i
+      lt.t[i] = tbyte(3u - j, r);                    // byte j of the state indexes T(3 - j)
+      lt.s[i] = sel_byte(j);
     }
+    return lt;
+  }
+  __device__ static __forceinline__ uint32_t step(const char* lds, const LT& lt, uint32_t x, uint32_t w) {
+    const uint32_t a0 = __builtin_amdgcn_perm(lt.t[0], x, lt.s[0]);
+    const uint32_t a1 = __builtin_amdgcn_perm(lt.t[1], x, lt.s[1]);
+    const uint32_t a2 = __builtin_amdgcn_perm(lt.t[2], x, lt.s[2]);
+    const uint32_t a3 = __builtin_amdgcn_perm(lt.t[3], x, lt.s[3]);
+    return xor3(xor3(lds_u32(lds, a0), lds_u32(lds, a1), lds_u32(lds, a2)), lds_u32(lds, a3), w);
+  }
+  __device__ static __forceinline__ void stage(char* lds, const uint32_t* __restrict__ tabs) {
+    // T0..T3 x 16 replicas: 4 x 256 entries x 4 quads of 16 B (quad q = replicas 4q..4q+3)
+    for (uint32_t i0 = 0; i0 < 4096u; i0 += 4u * blockDim.x) {
+      uint32_t v[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t i = i0 + threadIdx.x + j * blockDim.x;
-      const uint32_t k = i >> 10, b = (i >> 2) & 255u, q = i & 3u;
-      if (i < 4096u) *reinterpret_cast<u32x4*>(lds + ((b << 8) | (k << 6) | (q << 4))) = u32x4{v[j], v[j], v[j], v[j]};
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t i = i0 + threadIdx.x + j * blockDim.x;
+        v[j] = i < 4096u ? tabs[(i >> 2)] : 0u;  // tabs: T0[256] T1[256] T2[256] T3[256]; i >> 2 = k*256 + b
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t i = i0 + threadIdx.x + j * blockDim.x;
+        const uint32_t k = i >> 10, b = (i >> 2) & 255u, q = i & 3u;
+        if (i < 4096u) *reinterpret_cast<u32x4*>(lds + ((b << 8) | tbyte(k, 4u * q))) = u32x4{v[j], v[j], v[j], v[j]};
+      }
     }
   }
-  // operators: catalog entries 0 (16), 2 (64), 4 (256), 6 (1024)
+};
+typedef TabsS4T<true> TabsS4;
+typedef TabsS4T<false> TabsS4w;
+
+struct LaneTabs2 {
+  uint32_t t1, t0;  // v_perm byte 0 of the lookup address: j<<7 | replica<<2
+};
+
+// shift(x, 2 bytes): x' = (x >> 16) ^ T1[x & 255] ^ T0[(x >> 8) & 255]
+__device__ __forceinline__ uint32_t half2(const char* lds, const LaneTabs2& lt, uint32_t x) {
+  const uint32_t a1 = __builtin_amdgcn_perm(lt.t1, x, sel_byte(0));
+  const uint32_t a0 = __builtin_amdgcn_perm(lt.t0, x, sel_byte(1));
+  return xor3(lds_u32(lds, a1), lds_u32(lds, a0), x >> 16);
+}
+
+struct TabsS2 {
+  typedef LaneTabs2 LT;
+  __device__ static __forceinline__ LT lane(uint32_t u) {
+    const uint32_t r = (u & 31u) << 2;
+    return LaneTabs2{(1u << 7) | r, r};
+  }
+  __device__ static __forceinline__ uint32_t step(const char* lds, const LT& lt, uint32_t x, uint32_t w) {
+    return half2(lds, lt, half2(lds, lt, x)) ^ w;
+  }
+  __device__ static __forceinline__ void stage(char* lds, const uint32_t* __restrict__ tabs) {
+    // T0, T1 x 32 replicas: 256 entries x 2 tables x 8 quads of 16 B; store i at i << 4 = b<<8 | j<<7 | q<<4
+    for (uint32_t i0 = 0; i0 < 4096u; i0 += 4u * blockDim.x) {
+      uint32_t v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t i = i0 + threadIdx.x + j * blockDim.x;
+        v[j] = i < 4096u ? tabs[((i >> 3) & 1u) * 256u + (i >> 4)] : 0u;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t i = i0 + threadIdx.x + j * blockDim.x;
+        if (i < 4096u) *reinterpret_cast<u32x4*>(lds + (i << 4)) = u32x4{v[j], v[j], v[j], v[j]};
+      }
+    }
+  }
+};
+
+__device__ __forceinline__ void stage_ops_span(char* lds, const uint32_t* __restrict__ tabs) {
+  // operators: catalog entries 0 (16), 2 (64), 4 (256), 1 (32)
   const u32x4* cat = reinterpret_cast<const u32x4*>(tabs + 1024);
-  for (uint32_t i = threadIdx.x; i < 4u * 256u; i += blockDim.x)
-    *reinterpret_cast<u32x4*>(lds + kSpanOpBase + i * 16u) = cat[(2u * (i >> 8)) * 256u + (i & 255u)];
+  for (uint32_t i = threadIdx.x; i < 4u * 256u; i += blockDim.x) {
+    const uint32_t slot = i >> 8;
+    *reinterpret_cast<u32x4*>(lds + kSpanOpBase + i * 16u) = cat[(slot == 3u ? 1u : 2u * slot) * 256u + (i & 255u)];
+  }
 }
 
 // Whole-wave hash of one record of any length from global memory (Value() seed): the slow path of
 // crc_sized_kernel (slow_finish) on this kernel's operator layout.  Rows of 1 KiB: lane u hashes the
 // 16-B pieces at 16u + 1024k of the record front-padded with zeros to whole KiB (masked below p, U[z]
 // on the piece holding p), Horner-folded with shift 1024; then a 6-level tree (16 .. 512).
-__device__ __forceinline__ uint32_t span_chain16(const char* lds, const LaneTabs16& lt, uint32_t start, const uint32_t (&w)[4]) {
+template <class TP>
+__device__ __forceinline__ uint32_t span_chain16(const char* lds, const typename TP::LT& lt, uint32_t start,
+                                                 const uint32_t (&w)[4]) {
   uint32_t x = start ^ w[0];
-  x = step4x16(lds, lt, x, w[1]);
-  x = step4x16(lds, lt, x, w[2]);
-  x = step4x16(lds, lt, x, w[3]);
-  return step4x16(lds, lt, x, 0u);
+  x = TP::step(lds, lt, x, w[1]);
+  x = TP::step(lds, lt, x, w[2]);
+  x = TP::step(lds, lt, x, w[3]);
+  return TP::step(lds, lt, x, 0u);
 }
 
-__device__ __forceinline__ uint32_t span_slow_record(const char* lds, const LaneTabs16& lt, uint32_t u, uint32_t ureg,
+template <class TP>
+__device__ __forceinline__ uint32_t span_slow_record(const char* lds, const typename TP::LT& lt, uint32_t u, uint32_t ureg,
                                                      uintptr_t p, uint32_t n) {
   if (n == 0) return 0xFFFFFFFFu;
   const uint64_t nrows = (static_cast<uint64_t>(n) + 1023u) >> 10;
@@ -139,7 +215,8 @@ __device__ __forceinline__ uint32_t span_slow_record(const char* lds, const Lane
     }
     const uint32_t uz = __shfl(ureg, static_cast<uint32_t>(zl) & 15u, 64);
     const uint32_t start = (zl >= 0 && zl < 16) ? uz : 0u;
-    acc = span_op_x(lds, 3, acc, span_chain16(lds, lt, start, w));  // acc = shift1024(acc) ^ row
+    acc = span_op_x(lds, 2, span_op_x(lds, 2, span_op_x(lds, 2, span_op_x(lds, 2, acc, 0u), 0u), 0u),
+                    span_chain16<TP>(lds, lt, start, w));  // acc = shift1024(acc) ^ row
   }
   // tree over 64 lanes, 16 B apart: shift 16 << k between partners at distance 2^k
   uint32_t y;
@@ -161,21 +238,25 @@ __device__ __forceinline__ uint32_t span_slow_record(const char* lds, const Lane
 // ---- items ---------------------------------------------------------------------------------------
 // A batch is 64 consecutive records (lane r of the batch registers: record 64 * batch + r).  Its
 // in-class records are hashed by items: runs of up to G = floor(64 / k) consecutive records, each
-// record on k consecutive lanes (lane u: record slot u / k, part c = u % k).  Per record 2k chains:
-// chain i covers the words [nw - L(i + 1), nw - L i) counted from the record's END (L = kSpanL
-// words), the last chain (i = 2k - 1, the head) everything before as well; part c runs chains 2c
-// (A) and 2c + 1 (B).  All chains of an item run in lock step for `iters` = max(L, nw - (2k-1) L)
-// steps: the head chain alone for the first iters - L, then every chain for L.  Folds: per lane
-// P = shift(B, 4L) ^ A, then across the k lanes of a record shift(P[c + m], 8Lm) ^ P[c] for m = 1,
-// 2, 4.  k per batch minimises steps per record for its longest in-class record (span_pick).
+// record on k consecutive lanes (lane u: record slot u / k, part c = u % k).  Counted from the
+// record's END, part c covers 33 words (132 B) ending 132 c bytes before the end, as four chains:
+// A its last 8 words, B and C the 8 before each, D the 9 before those; part k - 1's chain D (the
+// head) also runs on to the record's start.  Parts of 33 words put the k lanes of a record on k
+// different LDS banks at every step (128-B parts would put them all on one).  All chains of an item
+// run in lock step for `iters` = max(9, nw - 33 (k - 1) - 24) steps: the head chain alone for the
+// first iters - 9, then D for 9 and A, B, C for the last 8.  Folds: per lane P = shift(shift(D, 32)
+// ^ C, 64) ^ shift(B, 32) ^ A, then across the k lanes of a record shift(P[c + m], 132 m) ^ P[c]
+// for m = 1, 2, 4.  k per batch minimises steps per record for its longest in-class record.
 constexpr uint32_t kNoRec = 0x3FFFFFFFu;
-constexpr uint32_t kSpanL = 16;  // words per tail chain: 64 B, the slot-1 fold
+constexpr uint32_t kSpanLC = 8;                      // words of chains A, B, C: 32 B, the slot-3 fold
+constexpr uint32_t kSpanLD = 9;                      // words of chain D (not the head)
+constexpr uint32_t kSpanPart = 3 * kSpanLC + kSpanLD;  // words per part
 
 struct LaneSpanGeom {
   uint32_t k;      // lanes per record
   uint32_t g;      // records per item: floor(64 / k)
   uint32_t magic;  // ceil(65536 / k): u / k = (u * magic) >> 16 for u < 64
-  uint32_t iters;  // chain steps per item
+  uint32_t iters;  // chain steps per item: max(9, nw - 33 (k - 1) - 24)
 };
 
 // max over the wave of a 32-bit value; every lane must be active
@@ -196,14 +277,14 @@ __device__ __forceinline__ LaneSpanGeom span_pick(uint32_t nw) {
   const float fit = static_cast<float>(kSpanUsable) * __builtin_amdgcn_rcpf(static_cast<float>(4u * nw + 8u));
   uint32_t gfit = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(fit)));
   gfit = gfit ? gfit : 1u;
-  LaneSpanGeom best{1u, 64u, 65536u, kSpanL};
+  LaneSpanGeom best{1u, 64u, 65536u, kSpanLD};
   uint32_t best_eff = 1u;
 #pragma unroll
   for (uint32_t k = 1; k <= KMAX; ++k) {
     const uint32_t g = 64u / k;
     const uint32_t geff = g < gfit ? g : gfit;
-    const int32_t h = static_cast<int32_t>(nw) - static_cast<int32_t>((2u * k - 1u) * kSpanL);
-    const uint32_t it = h > static_cast<int32_t>(kSpanL) ? static_cast<uint32_t>(h) : kSpanL;
+    const int32_t h = static_cast<int32_t>(nw) - static_cast<int32_t>((k - 1u) * kSpanPart + 3u * kSpanLC);
+    const uint32_t it = h > static_cast<int32_t>(kSpanLD) ? static_cast<uint32_t>(h) : kSpanLD;
     if (k == 1 || it * best_eff < best.iters * geff) {
       best = LaneSpanGeom{k, g, (65536u + k - 1u) / k, it};
       best_eff = geff;
@@ -222,20 +303,24 @@ struct SpanItem {
   uint32_t p_loc, e_loc, pre;  // per lane: local start (kNoRec: no record), local end, sink word
 };
 
-template <class Src, class Sink, uint32_t MAXN>
+// MODE (diagnostics only): 0 the product; 1 loads and staging without the hash; 2 the hash over
+// whatever the region holds, without the loads; 3 neither (the per-item bookkeeping alone).  TP: the
+// table scheme.
+template <class Src, class Sink, uint32_t MAXN, int MODE = 0, class TP = TabsS4>
 __global__ __launch_bounds__(kSpanWaves * 64) void crc_lanespan_kernel(const uint32_t* __restrict__ tabs, Src src,
                                                                        uint64_t nblk, Sink sink) {
   static_assert(MAXN + 32u <= kSpanUsable, "a record of the class must fit a region");
-  constexpr uint32_t KMAX = (MAXN + 8u * kSpanL - 1u) / (8u * kSpanL);  // 2k chains cover MAXN: 2, 4, 8
+  constexpr uint32_t KMAX = (MAXN / 4u + kSpanPart) / kSpanPart;  // k parts of 33 words cover MAXN: 2, 4, 8
   static_assert(KMAX >= 1 && KMAX <= 8, "tree folds for up to 8 lanes per record");
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
   char* lds = reinterpret_cast<char*>(lds_words);
-  stage_tables_span(lds, tabs);
+  TP::stage(lds, tabs);
+  stage_ops_span(lds, tabs);
   const uint32_t u = threadIdx.x & 63u;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t ureg = tabs[PDB_UNSHIFT_OFF + (u & 15u)];
   __syncthreads();
-  const LaneTabs16 lt = lane_tabs16(u);
+  const typename TP::LT lt = TP::lane(u);
   char* region = lds + kSpanStageBase + wv * kSpanRegion;
   const uintptr_t dummy = reinterpret_cast<uintptr_t>(tabs);  // >= 4 KiB + 256 B of valid bytes
   const uint64_t nbat = (nblk + 63u) >> 6;
@@ -260,7 +345,7 @@ __global__ __launch_bounds__(kSpanWaves * 64) void crc_lanespan_kernel(const uin
   uint64_t bfastm = 0;   // in-class records
   uint64_t bbroken = 0;  // bit r: records r and r + 1 may not share an item
   uint32_t bcursor = 64;
-  LaneSpanGeom bg{1u, 64u, 65536u, kSpanL};
+  LaneSpanGeom bg{1u, 64u, 65536u, kSpanLD};
 
   // make the prefetched batch current; records outside the class are hashed here by the whole
   // wave (rare: their loads wait behind the items in flight)
@@ -283,7 +368,7 @@ __global__ __launch_bounds__(kSpanWaves * 64) void crc_lanespan_kernel(const uin
       sb &= sb - 1;
       const uintptr_t sp = static_cast<uintptr_t>(uniform64(__builtin_amdgcn_readlane(plo, k), __builtin_amdgcn_readlane(phi, k)));
       const uint32_t sn = __builtin_amdgcn_readlane(bn, k);
-      const uint32_t rs = span_slow_record(lds, lt, u, ureg, sp, sn);
+      const uint32_t rs = span_slow_record<TP>(lds, lt, u, ureg, sp, sn);
       if (u == 0)
         SinkOps<Sink>::put(sink, (bcur << 6) + k, rs, BlkDesc{reinterpret_cast<const uint8_t*>(sp), sn, 0xFFFFFFFFu},
                            __builtin_amdgcn_readlane(bpre, k));
@@ -340,35 +425,47 @@ __global__ __launch_bounds__(kSpanWaves * 64) void crc_lanespan_kernel(const uin
     const uint32_t plo = static_cast<uint32_t>(bp), phi = static_cast<uint32_t>(static_cast<uint64_t>(bp) >> 32);
     const uintptr_t lo = static_cast<uintptr_t>(uniform64(__builtin_amdgcn_readlane(plo, g0), __builtin_amdgcn_readlane(phi, g0))) &
                          ~static_cast<uintptr_t>(15);
-    const uint64_t over = __builtin_amdgcn_ballot_w64(bfast && u >= g0 && (bp + bn - lo) > kSpanUsable) >> g0;
+    const uint32_t lo32 = static_cast<uint32_t>(lo);
+    // within a linked run the records ascend from lo: 32-bit offsets (lanes outside it are cut by m1)
+    const uint64_t over = __builtin_amdgcn_ballot_w64(bfast && u >= g0 && plo + bn - lo32 > kSpanUsable) >> g0;
     const uint32_t m2 = over ? static_cast<uint32_t>(__builtin_ctzll(over)) : 64u;
     const uint32_t m = min(min(bg.g, m1), m2);
     bcursor = g0 + m;
-    const uint32_t slot = (u * bg.magic) >> 16;
-    const uint32_t c = u - slot * bg.k;
-    const bool act = slot < m;
-    const uint32_t rl = act ? g0 + slot : u;
-    const uintptr_t pr = static_cast<uintptr_t>((static_cast<uint64_t>(__shfl(phi, rl, 64)) << 32) | __shfl(plo, rl, 64));
-    const uint32_t nr = __shfl(bn, rl, 64);
-    it.pre = __shfl(bpre, rl, 64);
-    it.r = rl;
-    it.c = c;
     it.lo = lo;
-    it.p_loc = act ? static_cast<uint32_t>(pr - lo) : kNoRec;
-    it.e_loc = act ? static_cast<uint32_t>(pr + nr - lo) : 0u;
+    if (bg.k == 1u && g0 == 0u) {  // the common case: lane u hashes record u
+      const bool act = u < m;
+      it.r = u;
+      it.c = 0;
+      it.pre = bpre;
+      it.p_loc = act ? plo - lo32 : kNoRec;
+      it.e_loc = act ? plo + bn - lo32 : 0u;
+    } else {
+      const uint32_t slot = (u * bg.magic) >> 16;
+      const uint32_t c = u - slot * bg.k;
+      const bool act = slot < m;
+      const uint32_t rl = act ? g0 + slot : u;
+      const uint32_t pr = __shfl(plo, rl, 64);
+      const uint32_t nr = __shfl(bn, rl, 64);
+      it.pre = __shfl(bpre, rl, 64);
+      it.r = rl;
+      it.c = c;
+      it.p_loc = act ? pr - lo32 : kNoRec;
+      it.e_loc = act ? pr + nr - lo32 : 0u;
+    }
     it.hi = wave_max_u32(it.e_loc);
     return it;
   };
 
-  // loads of one item: kSpanJ unconditional 16-B loads (1 KiB contiguous per instruction); chunks
-  // wholly past the item's last byte read the dummy line instead
+  // loads of one item: kSpanJ unconditional 16-B loads (1 KiB contiguous per instruction) from the
+  // item's uniform base; chunks wholly past its last byte re-read its last chunk (an empty item
+  // reads the tables' first 16 B)
   auto issue = [&](u32x4 (&A)[kSpanJ], const SpanItem& it) {
-    const uint32_t hi = it.hi;  // 0 for an invalid or empty item
-    const uintptr_t lo = it.lo;
+    const uint32_t last = it.hi ? (it.hi - 1u) & ~15u : 0u;
+    const uint8_t* base = reinterpret_cast<const uint8_t*>(it.lo);
 #pragma unroll
     for (uint32_t j = 0; j < kSpanJ; ++j) {
       const uint32_t off = 1024u * j + 16u * u;
-      A[j] = gload128<true>(off < hi ? lo + off : dummy);
+      A[j] = gload128<true>(reinterpret_cast<uintptr_t>(base + (MODE >= 2 ? 0u : (off < last ? off : last))));
     }
   };
   // every chunk is written, the dummy ones too: a load whose register is never read stays
@@ -379,53 +476,112 @@ __global__ __launch_bounds__(kSpanWaves * 64) void crc_lanespan_kernel(const uin
   };
   // hash an item staged in the region
   auto hash = [&](const SpanItem& it) {
-    if (it.hi == 0) return;
-    const uint32_t k = it.k, iters = it.iters, lim = iters - kSpanL;
+    if (it.hi == 0 || MODE == 1 || MODE == 3) return;
+    const uint32_t k = it.k, iters = it.iters, lim = iters - kSpanLD;
     const int32_t e = static_cast<int32_t>(it.e_loc);
     const int32_t pl = static_cast<int32_t>(it.p_loc);
+    const bool act = it.p_loc != kNoRec;
     const bool head = it.c == k - 1u;
     const uint32_t sel = static_cast<uint32_t>(e & 3) * 0x01010101u + 0x03020100u;
-    const uint32_t uz = __shfl(ureg, static_cast<uint32_t>(pl - e) & 3u, 64);
-    // word at byte s (s = e mod 4): bytes of the dword pair (D[s >> 2], D[(s >> 2) + 1]), masked
-    // below p; the word holding p injects U[z] (z bytes of it before p)
-    auto dword = [&](int32_t q) -> uint32_t { return lds_u32(region, static_cast<uint32_t>(q < 0 ? 0 : q) << 2); };
-    auto word = [&](int32_t s, uint32_t& lo_dw) -> uint32_t {
-      const uint32_t hi_dw = dword((s >> 2) + 1);
-      const uint32_t w = __builtin_amdgcn_perm(hi_dw, lo_dw, sel);
-      lo_dw = hi_dw;
-      const int32_t z = pl - s;
-      const uint32_t zc = static_cast<uint32_t>(z < 0 ? 0 : (z > 4 ? 4 : z));
-      const uint32_t m = static_cast<uint32_t>(0xFFFFFFFFull << (8u * zc));
-      return (w & m) ^ (static_cast<uint32_t>(z) < 4u ? uz : 0u);
-    };
-    const int32_t sA0 = e - static_cast<int32_t>(8u * kSpanL * it.c) - 4 * static_cast<int32_t>(iters);
-    const int32_t sB0 = sA0 - 4 * static_cast<int32_t>(kSpanL);
-    uint32_t lb = dword(sB0 >> 2);
-    uint32_t xb = word(sB0, lb);
-    if (lim > 0) {  // the head chain's first words (junk on the other lanes, dropped)
-      for (uint32_t t = 1; t < lim; ++t) xb = step4x16(lds, lt, xb, word(sB0 + 4 * static_cast<int32_t>(t), lb));
-      xb = head ? xb : 0u;
-      xb = step4x16(lds, lt, xb, word(sB0 + 4 * static_cast<int32_t>(lim), lb));
+    const uint32_t zp = static_cast<uint32_t>(pl - e) & 3u;  // bytes of the p-word before p
+    const uint32_t uz = __shfl(ureg, zp, 64);
+    // The word at byte s (s = e mod 4) is the dword pair (D[s >> 2], D[(s >> 2) + 1]) through sel.
+    // The p-word (at sp), masked below p with U[z] injected, replaces its chain's state at its
+    // step; a chain wholly before p yields 0.  Chain X (A, B, C, D = 0..3) ends at eA - 32 X and
+    // holds at global step t the word at its end - 4 (iters - t).
+    const int32_t eA = e - static_cast<int32_t>(4u * kSpanPart * it.c);
+    const int32_t sp = act ? pl - static_cast<int32_t>(zp) : e;  // (no record: an address in range)
+    uint32_t pw;
+    {
+      const char* q = region + 4 * (sp >> 2);
+      pw = (__builtin_amdgcn_perm(lds_u32(q, 4), lds_u32(q, 0), sel) & (0xFFFFFFFFu << (8u * zp))) ^ uz;
     }
-    const int32_t sa = sA0 + 4 * static_cast<int32_t>(lim);
-    const int32_t sb = sB0 + 4 * static_cast<int32_t>(lim);
-    uint32_t la = dword(sa >> 2);
-    uint32_t xa = word(sa, la);
+    // the p-word's step in chain A's numbering, then T + 8 X in chain X's, in phase-2 steps
+    const int32_t T = static_cast<int32_t>(iters) - ((eA - sp) >> 2) - static_cast<int32_t>(lim);
+    // the last phase-2 step at which some lane of the item replaces a state (uniform)
+    int32_t lmax = -1;
 #pragma unroll
-    for (uint32_t t = 1; t < kSpanL; ++t) {
-      xa = step4x16(lds, lt, xa, word(sa + 4 * static_cast<int32_t>(t), la));
-      xb = step4x16(lds, lt, xb, word(sb + 4 * static_cast<int32_t>(t), lb));
+    for (int32_t X = 0; X < 4; ++X) {
+      const int32_t t = T + 8 * X;
+      if (t >= (X == 3 ? 0 : 1) && t < static_cast<int32_t>(kSpanLD)) lmax = t;
     }
-    const uint32_t ca = step4x16(lds, lt, xa, 0u), cb = step4x16(lds, lt, xb, 0u);
-    uint32_t P = span_op_x(lds, 1, cb, ca);  // shift(B, 64 B) ^ A
+    const int32_t G = static_cast<int32_t>(wave_max_u32(act ? static_cast<uint32_t>(lmax + 1) : 0u)) - 1;
+    // chain base pointers: word at phase-2 step t is (q[t], q[t + 1])
+    const char* q0 = region + 4 * ((eA - 36) >> 2);  // below the region for short records: unused
+    const char* q1 = q0 - 32;
+    const char* q2 = q0 - 64;
+    const char* q3 = q0 - 96;
+    uint32_t xd = 0, ld;
+    if (lim > 0) {  // the head chain alone (junk on the other lanes, dropped)
+      const int32_t tD = T + 24 + static_cast<int32_t>(lim);  // global step of the p-word in D
+      const char* q = q3 - 4 * static_cast<int32_t>(lim);
+      ld = lds_u32(q, 0);
+      for (int32_t t = 0; t < static_cast<int32_t>(lim); ++t, q += 4) {
+        const uint32_t h = lds_u32(q, 4);
+        const uint32_t w = __builtin_amdgcn_perm(h, ld, sel);
+        ld = h;
+        xd = t == tD ? pw : TP::step(lds, lt, xd, w);
+      }
+      xd = head ? xd : 0u;
+    } else {
+      ld = lds_u32(q3, 0);
+    }
+    {
+      const uint32_t h = lds_u32(q3, 4);
+      const uint32_t w = __builtin_amdgcn_perm(h, ld, sel);
+      ld = h;
+      xd = TP::step(lds, lt, xd, w);
+      if (G >= 0) xd = T + 24 == 0 ? pw : xd;
+    }
+    uint32_t la = lds_u32(q0, 4), lb = lds_u32(q1, 4), lc = lds_u32(q2, 4);
+    uint32_t xa = 0, xb = 0, xc = 0;
 #pragma unroll
-    for (uint32_t lvl = 0; lvl < 3; ++lvl) {
-      const uint32_t m = 1u << lvl;
-      if (m >= k) break;
-      const uint32_t y = __shfl_down(P, m, 64);  // part c + m: the 128 m bytes before
-      if ((it.c & (2u * m - 1u)) == 0 && it.c + m < k) P = span_shift_x(lds, 3u + lvl, y, P);
+    for (int32_t t = 1; t < static_cast<int32_t>(kSpanLD); ++t) {
+      const uint32_t ha = lds_u32(q0, 4u * (t + 1)), hb = lds_u32(q1, 4u * (t + 1));
+      const uint32_t hc = lds_u32(q2, 4u * (t + 1)), hd = lds_u32(q3, 4u * (t + 1));
+      const uint32_t wa = __builtin_amdgcn_perm(ha, la, sel), wb = __builtin_amdgcn_perm(hb, lb, sel);
+      const uint32_t wc = __builtin_amdgcn_perm(hc, lc, sel), wd = __builtin_amdgcn_perm(hd, ld, sel);
+      la = ha, lb = hb, lc = hc, ld = hd;
+      if (t == 1) {
+        xa = wa, xb = wb, xc = wc;
+      } else {
+        xa = TP::step(lds, lt, xa, wa);
+        xb = TP::step(lds, lt, xb, wb);
+        xc = TP::step(lds, lt, xc, wc);
+      }
+      xd = TP::step(lds, lt, xd, wd);
+      if (t <= G) {
+        xa = T == t ? pw : xa;
+        xb = T + 8 == t ? pw : xb;
+        xc = T + 16 == t ? pw : xc;
+        xd = T + 24 == t ? pw : xd;
+      }
     }
-    if (it.c == 0 && it.p_loc != kNoRec)
+    // finish; a chain whose end is at or before the p-word's start holds no byte of the record
+    const int32_t L = static_cast<int32_t>(kSpanLD);
+    const uint32_t ca = T < L ? TP::step(lds, lt, xa, 0u) : 0u;
+    const uint32_t cb = T + 8 < L ? TP::step(lds, lt, xb, 0u) : 0u;
+    const uint32_t cc = T + 16 < L ? TP::step(lds, lt, xc, 0u) : 0u;
+    const uint32_t cd = T + 24 < L ? TP::step(lds, lt, xd, 0u) : 0u;
+    const uint32_t lo2 = span_op_x(lds, 3, cb, ca);  // shift(B, 32) ^ A
+    const uint32_t hi2 = span_op_x(lds, 3, cd, cc);  // shift(D, 32) ^ C
+    uint32_t P = span_op_x(lds, 1, hi2, lo2);        // shift(hi2, 64) ^ lo2
+    // parts c + m (the 132 m bytes before): 132 = 64 + 64 + 4, 264 = 256 + 4 + 4, 528 = 256 + 256 + 16
+    if (k > 1u) {
+      const uint32_t y = __shfl_down(P, 1, 64);
+      if ((it.c & 1u) == 0 && it.c + 1u < k)
+        P = TP::step(lds, lt, span_op_x(lds, 1, span_op_x(lds, 1, y, 0u), 0u), P);
+    }
+    if (k > 2u) {
+      const uint32_t y = __shfl_down(P, 2, 64);
+      if ((it.c & 3u) == 0 && it.c + 2u < k)
+        P = TP::step(lds, lt, TP::step(lds, lt, span_op_x(lds, 2, y, 0u), 0u), P);
+    }
+    if (k > 4u) {
+      const uint32_t y = __shfl_down(P, 4, 64);
+      if ((it.c & 7u) == 0 && it.c + 4u < k) P = span_op_x(lds, 0, span_op_x(lds, 2, span_op_x(lds, 2, y, 0u), 0u), P);
+    }
+    if (it.c == 0 && act)
       SinkOps<Sink>::put(sink, (it.batch << 6) + it.r, P, BlkDesc{nullptr, 0u, 0xFFFFFFFFu}, it.pre);
   };
 
@@ -452,16 +608,16 @@ inline uint32_t grid_span(const LaunchGeom& g, uint64_t nblk) {
 
 // Records of 1..1023 B by class (the class bounds the lanes per record: 2, 4, 8); longer ones, and
 // empty ones, take the whole-wave path.
-template <class Src, class Sink>
+template <class Src, class Sink, int MODE = 0, class TP = TabsS4>
 void launch_lanespan(const LaunchGeom& g, const uint32_t* d_tables, const Src& src, uint64_t nblk, uint32_t cls,
                      const Sink& sink, hipStream_t s) {
   const dim3 grid(grid_span(g, nblk)), block(kSpanWaves * 64);
   if (cls <= 256u)
-    hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 256>), grid, block, 0, s, d_tables, src, nblk, sink);
+    hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 256, MODE, TP>), grid, block, 0, s, d_tables, src, nblk, sink);
   else if (cls <= 512u)
-    hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 512>), grid, block, 0, s, d_tables, src, nblk, sink);
+    hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 512, MODE, TP>), grid, block, 0, s, d_tables, src, nblk, sink);
   else
-    hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 1023>), grid, block, 0, s, d_tables, src, nblk, sink);
+    hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 1023, MODE, TP>), grid, block, 0, s, d_tables, src, nblk, sink);
 }
 
 }  // namespace

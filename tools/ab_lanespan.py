@@ -3,7 +3,8 @@
 round-1 direct-load lane-per-record kernels (diagnostics variants 60 / 61 / 62) on log images of
 131-B (db_bench --value_size=100), 431-B (400) and 700-B / 1000-B records (bench.wal_layout), each
 ~1-2 GiB, device-resident.  GB/s of algorithmic bytes (record bytes + 16-B descriptor + 4-B CRC).
-Prints one JSON object."""
+Variants 63 / 64 time the record kernel's loads + staging alone and its hash alone (diagnostic
+modes, results undefined).  Prints one JSON object."""
 import json
 import os
 import sys
@@ -49,9 +50,13 @@ def main():
         assert (ref == got).all(), name
         for _ in range(20):  # warm: power management settles
             diag.batch_desc(0, d, d_blk, flags=hint, out=out)
-        t = {0: [], old: []}
+        for v in (65, 66):
+            assert (ref == diag.batch_desc(v, d, d_blk, flags=hint).cpu().numpy()).all(), (name, v)
+        # 63 / 64 / 67: the record kernel's loads alone / hash alone / bookkeeping alone; 65: 2-way
+        # conflict tables; 66: slice-by-2 tables
+        t = {0: [], old: [], 63: [], 64: [], 65: [], 66: [], 67: []}
         for _ in range(5):
-            for v in (0, old):
+            for v in t:
                 t[v].append(timeit(lambda: diag.batch_desc(v, d, d_blk, flags=hint, out=out)))
         res[name] = {str(v): {"ms": round(float(np.median(x)), 4), "GB/s": round(algo / (np.median(x) * 1e-3) / 1e9, 1),
                               "frac_8TBs": round(algo / (np.median(x) * 1e-3) / 8e12, 4)} for v, x in t.items()}
