@@ -9,15 +9,19 @@
 // instruction 1 KiB contiguous), written to the wave's LDS region, and every lane then reads its
 // own record from LDS.
 //
-// LDS image (160 KiB, one 512-thread workgroup = 8 waves per CU):
-//   [0, 64 KiB)      T0..T3 replicated 16x: entry b of table k, replica r at b<<8 | k<<6 | r<<2 (lane
-//                    l uses replica l & 15: 2-way bank conflicts, the price of fitting the staging;
-//                    slice-by-2 over 32 conflict-free replicas of T0, T1 fits too, but doubles the
-//                    dependent lookups per word and measured slower: the loop is latency- and
-//                    issue-bound, not LDS-bound)
-//   [64, 80 KiB)     4 shift operators (16, 64, 256, 32 B), single copy: the chain and part folds
-//                    and the whole-wave slow path (128 = 64 twice, 512 = 256 twice, 1024 = 256 x 4)
-//   [80, 160 KiB)    8 x 10 KiB: one staging region per wave
+// LDS image (154 of 160 KiB, one 640-thread workgroup = 10 waves per CU):
+//   [0, 64 KiB)      256 entry blocks of 256 B, block b at b << 8 (v_perm puts a state byte in
+//                    address bits 8..15 in one instruction):
+//                    [0, 128)    T0..T3 x 8 replicas: T_k replica r at dword k * 8 + r, bank
+//                                k * 8 + r.  In lookup instruction i, lane quarter q ((lane >> 3)
+//                                & 3) reads table (q + i) & 3, replica lane & 7: the four quarters
+//                                of each 32-lane group read four tables in four disjoint bank
+//                                ranges, every lookup bank-conflict free on 32 KiB of tables.
+//                    [128, 256)  8 shift operators (16, 32, 64, 256, 1024, 132, 264, 528 B), one
+//                                copy, sub-table j of operator s at dword 32 + ((4 s + j + b) & 31):
+//                                rotated by b so a lookup's lanes spread over the banks.
+//   [64, 154 KiB)    10 x 9 KiB: one staging region per wave (64 records of a 100-B-value log, 138 B
+//                    each with their headers, fit one)
 // A wave handles batches of 64 consecutive records; their records are hashed by items (runs of
 // consecutive records whose span fits a region, each record on k lanes: see "items" below).  The
 // next item's loads are in flight while one is hashed.  Per lane, a record part is END-aligned on a
@@ -33,66 +37,60 @@
 namespace pdb {
 namespace {
 
-constexpr uint32_t kSpanTabBytes = 64u << 10;
-constexpr uint32_t kSpanOpBase = kSpanTabBytes;                   // ops: 0 = 16, 1 = 64, 2 = 256, 3 = 32
-constexpr uint32_t kSpanStageBase = kSpanOpBase + 4u * 4096u;     // 80 KiB
-constexpr uint32_t kSpanWaves = 8;
-constexpr uint32_t kSpanJ = 10;                                   // 1-KiB load instructions per item
-constexpr uint32_t kSpanRegion = kSpanJ * 1024u;                  // staging bytes per wave
-constexpr uint32_t kSpanUsable = kSpanRegion - 16u;               // span limit: reads stay inside
-static_assert(kSpanStageBase + kSpanWaves * kSpanRegion == PDB_LDS_BYTES, "the whole 160 KiB");
+constexpr uint32_t kSpanStageBase = 64u << 10;                    // tables and operators below
+// staging geometry per class: waves per CU and 1-KiB chunks per region (10 x 9 KiB for <= 256-B
+// records: 64 records of a 100-B-value log fit a region; 12 x 8 KiB for the longer classes, whose
+// items hold 8..21 records on 3..8 lanes each -- more waves hide more of the hash's latency)
+template <uint32_t MAXN>
+struct SpanStage {
+  static constexpr uint32_t kWaves = MAXN <= 256u ? 10u : 12u;
+  static constexpr uint32_t kJ = MAXN <= 256u ? 9u : 8u;
+  static constexpr uint32_t kRegion = kJ * 1024u;
+  static constexpr uint32_t kUsable = kRegion - 16u;  // span limit: reads stay inside
+  static_assert((64u << 10) + kWaves * kRegion <= PDB_LDS_BYTES, "fits the 160 KiB");
+};
+// operator slots
+constexpr uint32_t kOp16 = 0, kOp32 = 1, kOp64 = 2, kOp256 = 3, kOp1024 = 4, kOp132 = 5, kOp264 = 6, kOp528 = 7;
 
+// shift(c, D) ^ y for the operator in slot `slot` (byte j of c indexes sub-table j)
 __device__ __forceinline__ uint32_t span_op_x(const char* lds, uint32_t slot, uint32_t c, uint32_t y) {
-  const uint32_t base = kSpanOpBase + slot * 4096u;
-  const uint32_t v0 = lds_u32(lds, base + ((c & 0xffu) << 2));
-  const uint32_t v1 = lds_u32(lds, base + 1024u + (((c >> 8) & 0xffu) << 2));
-  const uint32_t v2 = lds_u32(lds, base + 2048u + (((c >> 16) & 0xffu) << 2));
-  const uint32_t v3 = lds_u32(lds, base + 3072u + ((c >> 24) << 2));
-  return xor3(xor3(v0, v1, v2), v3, y);
+  uint32_t v[4];
+#pragma unroll
+  for (uint32_t j = 0; j < 4; ++j) {
+    const uint32_t bj = (c >> (8u * j)) & 0xffu;
+    v[j] = lds_u32(lds, (bj << 8) | 128u | (((bj + 4u * slot + j) & 31u) << 2));
+  }
+  return xor3(xor3(v[0], v[1], v[2]), v[3], y);
 }
 
-// shift(c, 16 << k) ^ y for k = 0..5 from the four slots (16, 32, 64, 64 x 2, 256, 256 x 2)
+// shift(c, 16 << k) ^ y for k = 0..5 (16, 32, 64, 64 x 2, 256, 256 x 2)
 __device__ __forceinline__ uint32_t span_shift_x(const char* lds, uint32_t k, uint32_t c, uint32_t y) {
   switch (k) {
-    case 0: return span_op_x(lds, 0, c, y);
-    case 1: return span_op_x(lds, 3, c, y);
-    case 2: return span_op_x(lds, 1, c, y);
-    case 3: return span_op_x(lds, 1, span_op_x(lds, 1, c, 0u), y);
-    case 4: return span_op_x(lds, 2, c, y);
-    default: return span_op_x(lds, 2, span_op_x(lds, 2, c, 0u), y);
+    case 0: return span_op_x(lds, kOp16, c, y);
+    case 1: return span_op_x(lds, kOp32, c, y);
+    case 2: return span_op_x(lds, kOp64, c, y);
+    case 3: return span_op_x(lds, kOp64, span_op_x(lds, kOp64, c, 0u), y);
+    case 4: return span_op_x(lds, kOp256, c, y);
+    default: return span_op_x(lds, kOp256, span_op_x(lds, kOp256, c, 0u), y);
   }
 }
 
-// Table schemes (the kernel's TP parameter), 64 KiB of LDS each:
-//   TabsS4: slice-by-4, T0..T3 x 16 replicas laid out so that every lookup is bank-conflict free.
-//     A ds_read_b32 serves its 64 lanes as two groups of 32, one bank ((a / 4) mod 32) per lane.
-//     Replica r of T_k sits at dword (k & 1) * 32 + (k >> 1) * 16 + r of each entry's 256 B: bank
-//     (k >> 1) * 16 + r.  Lanes with bit 4 clear do their four lookups in the order T3, T2, T1, T0,
-//     lanes with bit 4 set in the order T1, T0, T3, T2: in every instruction the two halves of a
-//     group read tables in opposite bank halves, each lane of a half its own replica.
-//   TabsS4w: the same tables, every lane in the order T3..T0 (replica r of T_k at bank (k & 1) * 16
-//     + r): 2-way conflicts on every lookup (diagnostics A/B).
-//   TabsS2: slice-by-2, T0, T1 x 32 replicas (two dependent lookup rounds per word; diagnostics).
+// Slice-by-4 lookups on the 8-replica layout above.
 struct LaneTabs4 {
   uint32_t t[4];  // v_perm byte 0 of the lookup address: table and replica bits
   uint32_t s[4];  // v_perm selector: which byte of the state indexes lookup i
 };
 
-template <bool kSplit>
-struct TabsS4T {
+struct TabsS4 {
   typedef LaneTabs4 LT;
-  __device__ static __forceinline__ uint32_t tbyte(uint32_t k, uint32_t r) {
-    return kSplit ? (((k & 1u) << 7) | ((k >> 1) << 6) | (r << 2)) : ((k << 6) | (r << 2));
-  }
   __device__ static __forceinline__ LT lane(uint32_t u) {
-    const uint32_t r = u & 15u;
-    const bool hi = kSplit && (u & 16u);
+    const uint32_t r = u & 7u, q = (u >> 3) & 3u;
     LT lt;
 #pragma unroll
     for (uint32_t i = 0; i < 4; ++i) {
-      const uint32_t j = hi ? ((i + 2u) & 3u) : i;  // the state byte looked up by instruction i
-      lt.t[i] = tbyte(3u - j, r);                    // byte j of the state indexes T(3 - j)
-      lt.s[i] = sel_byte(j);
+      const uint32_t k = (q + i) & 3u;  // table T_k, indexed by byte 3 - k of the state
+      lt.t[i] = (k * 8u + r) << 2;
+      lt.s[i] = sel_byte(3u - k);
     }
     return lt;
   }
@@ -104,70 +102,23 @@ struct TabsS4T {
     return xor3(xor3(lds_u32(lds, a0), lds_u32(lds, a1), lds_u32(lds, a2)), lds_u32(lds, a3), w);
   }
   __device__ static __forceinline__ void stage(char* lds, const uint32_t* __restrict__ tabs) {
-    // T0..T3 x 16 replicas: 4 x 256 entries x 4 quads of 16 B (quad q = replicas 4q..4q+3)
-    for (uint32_t i0 = 0; i0 < 4096u; i0 += 4u * blockDim.x) {
-      uint32_t v[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t i = i0 + threadIdx.x + j * blockDim.x;
-        v[j] = i < 4096u ? tabs[(i >> 2)] : 0u;  // tabs: T0[256] T1[256] T2[256] T3[256]; i >> 2 = k*256 + b
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t i = i0 + threadIdx.x + j * blockDim.x;
-        const uint32_t k = i >> 10, b = (i >> 2) & 255u, q = i & 3u;
-        if (i < 4096u) *reinterpret_cast<u32x4*>(lds + ((b << 8) | tbyte(k, 4u * q))) = u32x4{v[j], v[j], v[j], v[j]};
-      }
-    }
-  }
-};
-typedef TabsS4T<true> TabsS4;
-typedef TabsS4T<false> TabsS4w;
-
-struct LaneTabs2 {
-  uint32_t t1, t0;  // v_perm byte 0 of the lookup address: j<<7 | replica<<2
-};
-
-// shift(x, 2 bytes): x' = (x >> 16) ^ T1[x & 255] ^ T0[(x >> 8) & 255]
-__device__ __forceinline__ uint32_t half2(const char* lds, const LaneTabs2& lt, uint32_t x) {
-  const uint32_t a1 = __builtin_amdgcn_perm(lt.t1, x, sel_byte(0));
-  const uint32_t a0 = __builtin_amdgcn_perm(lt.t0, x, sel_byte(1));
-  return xor3(lds_u32(lds, a1), lds_u32(lds, a0), x >> 16);
-}
-
-struct TabsS2 {
-  typedef LaneTabs2 LT;
-  __device__ static __forceinline__ LT lane(uint32_t u) {
-    const uint32_t r = (u & 31u) << 2;
-    return LaneTabs2{(1u << 7) | r, r};
-  }
-  __device__ static __forceinline__ uint32_t step(const char* lds, const LT& lt, uint32_t x, uint32_t w) {
-    return half2(lds, lt, half2(lds, lt, x)) ^ w;
-  }
-  __device__ static __forceinline__ void stage(char* lds, const uint32_t* __restrict__ tabs) {
-    // T0, T1 x 32 replicas: 256 entries x 2 tables x 8 quads of 16 B; store i at i << 4 = b<<8 | j<<7 | q<<4
-    for (uint32_t i0 = 0; i0 < 4096u; i0 += 4u * blockDim.x) {
-      uint32_t v[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t i = i0 + threadIdx.x + j * blockDim.x;
-        v[j] = i < 4096u ? tabs[((i >> 3) & 1u) * 256u + (i >> 4)] : 0u;
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t i = i0 + threadIdx.x + j * blockDim.x;
-        if (i < 4096u) *reinterpret_cast<u32x4*>(lds + (i << 4)) = u32x4{v[j], v[j], v[j], v[j]};
-      }
+    // T0..T3 x 8 replicas: 256 entries x 4 tables x 2 quads of 16 B; quad i at b<<8 | k<<5 | h<<4
+    for (uint32_t i = threadIdx.x; i < 2048u; i += blockDim.x) {
+      const uint32_t b = i >> 3, k = (i >> 1) & 3u, h = i & 1u;
+      const uint32_t v = tabs[k * 256u + b];  // tabs: T0[256] T1[256] T2[256] T3[256]
+      *reinterpret_cast<u32x4*>(lds + ((b << 8) | (k << 5) | (h << 4))) = u32x4{v, v, v, v};
     }
   }
 };
 
 __device__ __forceinline__ void stage_ops_span(char* lds, const uint32_t* __restrict__ tabs) {
-  // operators: catalog entries 0 (16), 2 (64), 4 (256), 1 (32)
-  const u32x4* cat = reinterpret_cast<const u32x4*>(tabs + 1024);
-  for (uint32_t i = threadIdx.x; i < 4u * 256u; i += blockDim.x) {
-    const uint32_t slot = i >> 8;
-    *reinterpret_cast<u32x4*>(lds + kSpanOpBase + i * 16u) = cat[(slot == 3u ? 1u : 2u * slot) * 256u + (i & 255u)];
+  // slot s, sub-table j, entry b at b<<8 | 128 | ((4s + j + b) & 31) << 2; sources: catalog
+  // entries 0 (16), 1 (32), 2 (64), 4 (256), 6 (1024), then the record operators (132, 264, 528)
+  for (uint32_t i = threadIdx.x; i < 8u * 1024u; i += blockDim.x) {
+    const uint32_t slot = i >> 10, j = (i >> 8) & 3u, b = i & 255u;
+    const uint32_t src = slot < 5u ? 1024u + (slot < 3u ? slot : (slot == 3u ? 4u : 6u)) * 1024u
+                                   : PDB_SPANOP_OFF + (slot - 5u) * 1024u;
+    *reinterpret_cast<uint32_t*>(lds + ((b << 8) | 128u | (((b + 4u * slot + j) & 31u) << 2))) = tabs[src + j * 256u + b];
   }
 }
 
@@ -215,8 +166,7 @@ __device__ __forceinline__ uint32_t span_slow_record(const char* lds, const type
     }
     const uint32_t uz = __shfl(ureg, static_cast<uint32_t>(zl) & 15u, 64);
     const uint32_t start = (zl >= 0 && zl < 16) ? uz : 0u;
-    acc = span_op_x(lds, 2, span_op_x(lds, 2, span_op_x(lds, 2, span_op_x(lds, 2, acc, 0u), 0u), 0u),
-                    span_chain16<TP>(lds, lt, start, w));  // acc = shift1024(acc) ^ row
+    acc = span_op_x(lds, kOp1024, acc, span_chain16<TP>(lds, lt, start, w));  // acc = shift1024(acc) ^ row
   }
   // tree over 64 lanes, 16 B apart: shift 16 << k between partners at distance 2^k
   uint32_t y;
@@ -270,24 +220,26 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
   return max(max(a, b), max(c, d));
 }
 
-// k for a batch whose longest in-class record has nw words: fewest steps per record, counting the
-// records an item can hold (G, and what fits a staging region at ~4 nw + 8 bytes a record)
-template <uint32_t KMAX>
+// k for a batch whose longest in-class record has nw words: the fewest chain steps per batch,
+// items per batch x steps per item, with the records an item can hold: G = floor(64 / k), and
+// what fits a staging region at ~4 nw + 8 bytes a record
+template <uint32_t KMAX, uint32_t kUsable>
 __device__ __forceinline__ LaneSpanGeom span_pick(uint32_t nw) {
-  const float fit = static_cast<float>(kSpanUsable) * __builtin_amdgcn_rcpf(static_cast<float>(4u * nw + 8u));
+  const float fit = static_cast<float>(kUsable) * __builtin_amdgcn_rcpf(static_cast<float>(4u * nw + 8u));
   uint32_t gfit = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(fit)));
   gfit = gfit ? gfit : 1u;
   LaneSpanGeom best{1u, 64u, 65536u, kSpanLD};
-  uint32_t best_eff = 1u;
+  uint32_t best_cost = ~0u;
 #pragma unroll
   for (uint32_t k = 1; k <= KMAX; ++k) {
     const uint32_t g = 64u / k;
     const uint32_t geff = g < gfit ? g : gfit;
     const int32_t h = static_cast<int32_t>(nw) - static_cast<int32_t>((k - 1u) * kSpanPart + 3u * kSpanLC);
     const uint32_t it = h > static_cast<int32_t>(kSpanLD) ? static_cast<uint32_t>(h) : kSpanLD;
-    if (k == 1 || it * best_eff < best.iters * geff) {
+    const uint32_t items = (64u + geff - 1u) / geff;
+    if (items * it < best_cost) {
       best = LaneSpanGeom{k, g, (65536u + k - 1u) / k, it};
-      best_eff = geff;
+      best_cost = items * it;
     }
   }
   return best;
@@ -307,8 +259,10 @@ struct SpanItem {
 // whatever the region holds, without the loads; 3 neither (the per-item bookkeeping alone).  TP: the
 // table scheme.
 template <class Src, class Sink, uint32_t MAXN, int MODE = 0, class TP = TabsS4>
-__global__ __launch_bounds__(kSpanWaves * 64) void crc_lanespan_kernel(const uint32_t* __restrict__ tabs, Src src,
+__global__ __launch_bounds__(SpanStage<MAXN>::kWaves * 64) void crc_lanespan_kernel(const uint32_t* __restrict__ tabs, Src src,
                                                                        uint64_t nblk, Sink sink) {
+  constexpr uint32_t kSpanWaves = SpanStage<MAXN>::kWaves, kSpanJ = SpanStage<MAXN>::kJ;
+  constexpr uint32_t kSpanRegion = SpanStage<MAXN>::kRegion, kSpanUsable = SpanStage<MAXN>::kUsable;
   static_assert(MAXN + 32u <= kSpanUsable, "a record of the class must fit a region");
   constexpr uint32_t KMAX = (MAXN / 4u + kSpanPart) / kSpanPart;  // k parts of 33 words cover MAXN: 2, 4, 8
   static_assert(KMAX >= 1 && KMAX <= 8, "tree folds for up to 8 lanes per record");
@@ -382,7 +336,7 @@ __global__ __launch_bounds__(kSpanWaves * 64) void crc_lanespan_kernel(const uin
     const bool link_ok = bfast && fn && pn >= bp && pn <= bp + bn + 64u;
     bbroken = __builtin_amdgcn_ballot_w64(!link_ok && u < 63u);
     const uint32_t nw = wave_max_u32(bfast ? (bn + 3u) >> 2 : 0u);
-    bg = span_pick<KMAX>(nw ? nw : 1u);
+    bg = span_pick<KMAX, kSpanUsable>(nw ? nw : 1u);
     bcursor = 0;
     return true;
   };
@@ -563,23 +517,21 @@ __global__ __launch_bounds__(kSpanWaves * 64) void crc_lanespan_kernel(const uin
     const uint32_t cb = T + 8 < L ? TP::step(lds, lt, xb, 0u) : 0u;
     const uint32_t cc = T + 16 < L ? TP::step(lds, lt, xc, 0u) : 0u;
     const uint32_t cd = T + 24 < L ? TP::step(lds, lt, xd, 0u) : 0u;
-    const uint32_t lo2 = span_op_x(lds, 3, cb, ca);  // shift(B, 32) ^ A
-    const uint32_t hi2 = span_op_x(lds, 3, cd, cc);  // shift(D, 32) ^ C
-    uint32_t P = span_op_x(lds, 1, hi2, lo2);        // shift(hi2, 64) ^ lo2
-    // parts c + m (the 132 m bytes before): 132 = 64 + 64 + 4, 264 = 256 + 4 + 4, 528 = 256 + 256 + 16
+    const uint32_t lo2 = span_op_x(lds, kOp32, cb, ca);  // shift(B, 32) ^ A
+    const uint32_t hi2 = span_op_x(lds, kOp32, cd, cc);  // shift(D, 32) ^ C
+    uint32_t P = span_op_x(lds, kOp64, hi2, lo2);        // shift(hi2, 64) ^ lo2
+    // parts c + m: the 132 m bytes before
     if (k > 1u) {
       const uint32_t y = __shfl_down(P, 1, 64);
-      if ((it.c & 1u) == 0 && it.c + 1u < k)
-        P = TP::step(lds, lt, span_op_x(lds, 1, span_op_x(lds, 1, y, 0u), 0u), P);
+      if ((it.c & 1u) == 0 && it.c + 1u < k) P = span_op_x(lds, kOp132, y, P);
     }
     if (k > 2u) {
       const uint32_t y = __shfl_down(P, 2, 64);
-      if ((it.c & 3u) == 0 && it.c + 2u < k)
-        P = TP::step(lds, lt, TP::step(lds, lt, span_op_x(lds, 2, y, 0u), 0u), P);
+      if ((it.c & 3u) == 0 && it.c + 2u < k) P = span_op_x(lds, kOp264, y, P);
     }
     if (k > 4u) {
       const uint32_t y = __shfl_down(P, 4, 64);
-      if ((it.c & 7u) == 0 && it.c + 4u < k) P = span_op_x(lds, 0, span_op_x(lds, 2, span_op_x(lds, 2, y, 0u), 0u), P);
+      if ((it.c & 7u) == 0 && it.c + 4u < k) P = span_op_x(lds, kOp528, y, P);
     }
     if (it.c == 0 && act)
       SinkOps<Sink>::put(sink, (it.batch << 6) + it.r, P, BlkDesc{nullptr, 0u, 0xFFFFFFFFu}, it.pre);
@@ -600,9 +552,9 @@ __global__ __launch_bounds__(kSpanWaves * 64) void crc_lanespan_kernel(const uin
   }
 }
 
-// grid: one wave per batch of 64 records, 8 waves per workgroup, at most one workgroup per CU
-inline uint32_t grid_span(const LaunchGeom& g, uint64_t nblk) {
-  const uint64_t want = ((nblk + 63) / 64 + kSpanWaves - 1) / kSpanWaves;
+// grid: one wave per batch of 64 records, `waves` per workgroup, at most one workgroup per CU
+inline uint32_t grid_span(const LaunchGeom& g, uint64_t nblk, uint32_t waves) {
+  const uint64_t want = ((nblk + 63) / 64 + waves - 1) / waves;
   return static_cast<uint32_t>(want < g.grid ? (want ? want : 1) : g.grid);
 }
 
@@ -611,13 +563,19 @@ inline uint32_t grid_span(const LaunchGeom& g, uint64_t nblk) {
 template <class Src, class Sink, int MODE = 0, class TP = TabsS4>
 void launch_lanespan(const LaunchGeom& g, const uint32_t* d_tables, const Src& src, uint64_t nblk, uint32_t cls,
                      const Sink& sink, hipStream_t s) {
-  const dim3 grid(grid_span(g, nblk)), block(kSpanWaves * 64);
-  if (cls <= 256u)
-    hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 256, MODE, TP>), grid, block, 0, s, d_tables, src, nblk, sink);
-  else if (cls <= 512u)
-    hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 512, MODE, TP>), grid, block, 0, s, d_tables, src, nblk, sink);
-  else
-    hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 1023, MODE, TP>), grid, block, 0, s, d_tables, src, nblk, sink);
+  if (cls <= 256u) {
+    constexpr uint32_t w = SpanStage<256>::kWaves;
+    hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 256, MODE, TP>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0, s,
+                       d_tables, src, nblk, sink);
+  } else if (cls <= 512u) {
+    constexpr uint32_t w = SpanStage<512>::kWaves;
+    hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 512, MODE, TP>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0, s,
+                       d_tables, src, nblk, sink);
+  } else {
+    constexpr uint32_t w = SpanStage<1023>::kWaves;
+    hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 1023, MODE, TP>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0,
+                       s, d_tables, src, nblk, sink);
+  }
 }
 
 }  // namespace

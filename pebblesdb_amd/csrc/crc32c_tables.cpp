@@ -75,7 +75,8 @@ static uint32_t unshift_byte(const uint32_t* t0, uint32_t c1) {
 
 // Fills `out` (PDB_TABLE_WORDS u32): [T0|T1|T2|T3] then the PDB_NCAT catalog operators, each as
 // 4 sub-tables j=0..3 of 256 entries: op[j][b] = shift(b << 8j, D); then the unshifted seeds
-// U[z] = shift^-z(0xFFFFFFFF), z = 0..16 (PDB_UNSHIFT_OFF).
+// U[z] = shift^-z(0xFFFFFFFF), z = 0..16 (PDB_UNSHIFT_OFF); then the record kernel's operators
+// (PDB_SPANOP_OFF, same layout).
 void build_device_tables(uint32_t* out) {
   uint32_t t[4][256];
   build_byte_table(t[0]);
@@ -87,6 +88,12 @@ void build_device_tables(uint32_t* out) {
   for (int o = 0; o < PDB_NCAT; ++o) {
     Gf2Mat m = mat_pow(z1, kPdbCatDist[o]);
     uint32_t* op = out + 1024 + o * 1024;
+    for (int j = 0; j < 4; ++j)
+      for (uint32_t b = 0; b < 256; ++b) op[j * 256 + b] = mat_vec(m, b << (8 * j));
+  }
+  for (int o = 0; o < PDB_SPANOP_N; ++o) {
+    Gf2Mat m = mat_pow(z1, kPdbSpanOpDist[o]);
+    uint32_t* op = out + PDB_SPANOP_OFF + o * 1024;
     for (int j = 0; j < 4; ++j)
       for (uint32_t b = 0; b < 256; ++b) op[j * 256 + b] = mat_vec(m, b << (8 * j));
   }

@@ -721,15 +721,11 @@ hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tab
       break;
     case 63:  // the record kernel's loads and staging alone (no hash; results undefined)
     case 64:  // the record kernel's hash alone over stale staging (no loads; results undefined)
-    case 65:  // the record kernel on 2-way-conflict slice-by-4 tables (every lane T3..T0)
-    case 66:  // the record kernel on slice-by-2 tables (T0, T1 x 32 replicas)
     case 67:  // the record kernel's bookkeeping alone (no loads, no hash)
     {
       const uint32_t cls = (flags & PDB_CRC_SIZE_256) ? 256u : ((flags & PDB_CRC_SIZE_512) ? 512u : 1023u);
       if (v == 63) launch_lanespan<DescSrc, OutSink, 1>(g, d_tables, src, nblk, cls, sink, s);
       else if (v == 64) launch_lanespan<DescSrc, OutSink, 2>(g, d_tables, src, nblk, cls, sink, s);
-      else if (v == 65) launch_lanespan<DescSrc, OutSink, 0, TabsS4w>(g, d_tables, src, nblk, cls, sink, s);
-      else if (v == 66) launch_lanespan<DescSrc, OutSink, 0, TabsS2>(g, d_tables, src, nblk, cls, sink, s);
       else launch_lanespan<DescSrc, OutSink, 3>(g, d_tables, src, nblk, cls, sink, s);
       break;
     }
