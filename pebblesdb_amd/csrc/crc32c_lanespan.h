@@ -452,7 +452,8 @@ __global__ __launch_bounds__(SpanStage<MAXN>::kWaves * 64) void crc_lanespan_ker
     }
     // the p-word's step in chain A's numbering, then T + 8 X in chain X's, in phase-2 steps
     const int32_t T = static_cast<int32_t>(iters) - ((eA - sp) >> 2) - static_cast<int32_t>(lim);
-    // the last phase-2 step at which some lane of the item replaces a state (uniform)
+    // the last phase-2 step at which some lane of the item replaces a state (uniform; one bound for
+    // all four chains: per-chain masks cost more in branches than their selects save)
     int32_t lmax = -1;
 #pragma unroll
     for (int32_t X = 0; X < 4; ++X) {
@@ -537,18 +538,28 @@ __global__ __launch_bounds__(SpanStage<MAXN>::kWaves * 64) void crc_lanespan_ker
       SinkOps<Sink>::put(sink, (it.batch << 6) + it.r, P, BlkDesc{nullptr, 0u, 0xFFFFFFFFu}, it.pre);
   };
 
-  // ---- pipeline: the next item's loads in flight while one is hashed ------------------------------
-  // (one register array: with two, the compiler's wait counting across the loop's back edge drains
-  // both arrays at the loop head; eight waves per CU keep ~70 KiB in flight per CU)
-  u32x4 A[kSpanJ];
-  SpanItem cur = next_item(true);
-  issue(A, cur);
-  while (cur.valid) {
+  // ---- pipeline: two items in flight while one is hashed ---------------------------------------
+  // Loop head: the region holds I0, array B holds I1's loads in flight; only B's loads cross the
+  // back edge.
+  u32x4 A[kSpanJ], B[kSpanJ];
+  SpanItem I0 = next_item(true);
+  issue(A, I0);
+  SpanItem I1 = next_item(I0.valid);
+  issue(B, I1);
+  to_lds(A);
+  while (I0.valid) {
+    const SpanItem I2 = next_item(I1.valid);
+    issue(A, I2);
+    hash(I0);
+    if (!I1.valid) break;
+    to_lds(B);
+    const SpanItem I3 = next_item(I2.valid);
+    issue(B, I3);
+    hash(I1);
+    if (!I2.valid) break;
     to_lds(A);
-    const SpanItem nxt = next_item(true);
-    issue(A, nxt);
-    hash(cur);
-    cur = nxt;
+    I0 = I2;
+    I1 = I3;
   }
 }
 

@@ -23,8 +23,8 @@ for s in "$@"; do
     cold) step cold 300 python tools/cold_start.py ;;
     lanespan) step lanespan 600 python -u -m pytest tests/test_lanespan.py tests/test_sst4k.py -m gpu -x -v --timeout 200 --timeout-method thread ;;
     ab_lanespan) step ab_lanespan 600 python tools/ab_lanespan.py ;;
-    probe_wal100) step probe_wal100 900 bash tools/counters_probe.sh ${TAG}_probe100 wal100 0 64 65 67 ;;
-    probe_wal400) step probe_wal400 900 bash tools/counters_probe.sh ${TAG}_probe400 wal400 0 64 65 67 ;;
+    probe_wal100) step probe_wal100 900 bash tools/counters_probe.sh ${TAG}_probe100 wal100 0 64 67 ;;
+    probe_wal400) step probe_wal400 900 bash tools/counters_probe.sh ${TAG}_probe400 wal400 0 64 67 ;;
     counters_span) step counters_span 900 bash tools/counters_span.sh ${TAG}_span wal100 wal400 ;;
     integ) step integ 600 python -u -m pytest tests/test_integration.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
     fullsize) step fullsize 600 python -u -m pytest tests/test_full_size.py tests/test_gpu_parity.py -m gpu -x -v --timeout 300 --timeout-method thread -k "full_size or host_" ;;
