@@ -38,8 +38,10 @@ def parse():
     # 40: the first ~20-30 launches of a cold GPU run slower (clock / power settling; see
     # DESIGN.md §6), so the default warmup covers them
     ap.add_argument("--warmup", type=int, default=40)
+    ap.add_argument("--settle", type=int, default=300,
+                    help="untimed launches after the timed region before the steady-state re-timing (0: skip)")
     ap.add_argument("--workload", default="c2", choices=["c2", "c3", "sstable", "sst_verify", "sst_seal", "sst_crc",
-                                                        "wal", "wal100", "wal400"],
+                                                        "wal", "wal100", "wal400", "wal1000"],
                     help="c2 (default, the headline) / c3: BASELINE configs; sstable: the C2 blocks in "
                          "sstable layout; sst_verify / sst_seal: SURVEY §8(f) rows 1-2 on a device sstable "
                          "image of ~4.17-KiB blocks; wal: row 3, the log record CRC over 32-KiB log blocks")
@@ -221,16 +223,18 @@ def main():
         workload = {"workload": f"{args.workload}: sstable image in HBM, 1M blocks of 4166-4174 B + type + "
                                 "5-B trailer, pdb_sst_" + args.workload.split("_")[1] + "_device",
                     "blocks_per_gpu": nblk, "bytes_per_gpu": hashed}
-    elif args.workload in ("wal", "wal100", "wal400"):
+    elif args.workload in ("wal", "wal100", "wal400", "wal1000"):
         # log file image: 32-KiB log blocks of physical records [crc 4][len 2][type 1][payload]
         # (db/log_format.h:27-30); fillseq-like 1055-B logical records (1 KiB value + key + batch
         # header) fragmented at block ends; the CRC covers type || fragment (log_writer.cc:111-121)
         # wal100: db_bench's default --value_size=100 -> 131-B batches, a 1 GiB log, the <= 256-B class
         # wal400: --value_size=400 -> 431-B batches, a 2 GiB log, the 257..512-B class
+        # wal1000: --value_size=969 -> 1000-B batches, a 2 GiB log, the 513..1023-B class
         small = args.workload == "wal100"
         mid = args.workload == "wal400"
-        offs, lens = wal_layout(args.nblk * (1024 if small else (2048 if mid else 4096)),
-                                131 if small else (431 if mid else 1055))
+        big = args.workload == "wal1000"
+        offs, lens = wal_layout(args.nblk * (1024 if small else (2048 if mid or big else 4096)),
+                                131 if small else (431 if mid else (1000 if big else 1055)))
         nblk = len(offs)
         total = int(offs[-1] + lens[-1])
         data = torch.empty(total, dtype=torch.uint8, device=dev)
@@ -239,13 +243,14 @@ def main():
         L = stride = None
         hashed = int(lens.sum())
         out = torch.empty(nblk, dtype=torch.int32, device=dev)
-        hint = "256" if small else ("512" if mid else "1k")
+        hint = "256" if small else ("512" if mid else ("1023" if big else "1k"))
 
         def step():
             crc32c.batch(data, d_blk, out=out, size_hint=hint)
 
         workload = {"workload": ("wal100: 1 GiB log image, 32-KiB blocks, 131-B records" if small else
                                  "wal400: 2 GiB log image, 32-KiB blocks, 431-B records" if mid else
+                                 "wal1000: 2 GiB log image, 32-KiB blocks, 1000-B records" if big else
                                  "wal: 4 GiB log image, 32-KiB blocks, 1055-B records") +
                                 " -> type||payload fragments (descriptor list)",
                     "blocks_per_gpu": nblk, "bytes_per_gpu": hashed}
@@ -269,7 +274,7 @@ def main():
 
         workload = {"workload": "c3: Zipf 1-64 KiB blocks, packed, descriptor list (byte-balanced rank ranges)",
                     "blocks_per_gpu": nblk, "bytes_per_gpu": hashed}
-    algo_bytes = hashed + 4 * nblk + (16 * nblk if args.workload in ("c3", "wal", "wal100", "wal400") else 0)
+    algo_bytes = hashed + 4 * nblk + (16 * nblk if args.workload in ("c3", "wal", "wal100", "wal400", "wal1000") else 0)
     if args.workload == "sst_verify":  # + the 4-B stored trailer read, 16-B handle, 1-B ok written
         algo_bytes = hashed + nblk * (4 + 16 + 1)
     elif args.workload in ("sst_seal", "sst_crc"):  # + 4-B trailer / CRC written, 16-B handle
@@ -309,6 +314,25 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall_max = float(t.item())
 
+    # Steady state, AFTER the timed region and not part of `value`: the power manager lowers the
+    # clock for the first ~100 launches on a cold GPU (sclk 2.41 -> ~2.05 GHz as board power climbs,
+    # then recovers), so K launches after W = 5 warmups catch the transient.  This
+    # re-times K launches after `--settle` more untimed ones, on this rank alone.
+    steady = None
+    if args.settle > 0:
+        for _ in range(args.settle):
+            step()
+        se = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+        for s_, e_ in se:
+            s_.record(stream)
+            step()
+            e_.record(stream)
+        torch.cuda.synchronize()
+        st_ms = float(np.mean([s_.elapsed_time(e_) for s_, e_ in se]))
+        steady = {"settle_launches": args.settle, "kernel_avg_ms": round(st_ms, 4),
+                  "GiB_s_per_gpu": round(hashed / (st_ms * 1e-3) / GIB, 3),
+                  "frac": round(algo_bytes / (st_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+
     # per-rank facts (outside the timed region) gathered to rank 0: device, bytes hashed, kernel
     # time, checksum of checksums -- the SCALE record shows which GPUs RCCL actually saw
     props = torch.cuda.get_device_properties(gpu)
@@ -337,9 +361,9 @@ def main():
             extra["copy_inclusive"] = copy_inclusive(crc32c, data, L, stride, min(nblk, 1 << 18))
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            if args.workload in ("c2", "sstable", "c3", "wal", "wal100", "wal400"):
+            if args.workload in ("c2", "sstable", "c3", "wal", "wal100", "wal400", "wal1000"):
                 cpu = cpu_baseline(data, L, stride, nblk, args,
-                                   d_blk if args.workload in ("c3", "wal", "wal100", "wal400") else None)
+                                   d_blk if args.workload in ("c3", "wal", "wal100", "wal400", "wal1000") else None)
             else:  # sst_verify / sst_seal: the reference's CRC over each block's contents || type
                 cpu = cpu_baseline(data, L, stride, nblk, args, cpu_blk)
 
@@ -375,8 +399,9 @@ def main():
                 "kernel": {"c2": "crc_pack4k_kernel<1,4,nt>", "sstable": "crc_sst4k_kernel<FixedSrc,OutSink,nt>",
                            "c3": "crc_stream16_kernel<DescSrc,OutSink,dyn,nt,pack>",
                            "wal": "crc_sst1k_kernel<DescSrc,OutSink,nt>",
-                           "wal100": "crc_lanerec9_kernel<DescSrc,OutSink>",
-                           "wal400": "crc_lanerec17_kernel<DescSrc,OutSink>",
+                           "wal100": "crc_lanespan_kernel<DescSrc,OutSink,256>",
+                           "wal400": "crc_lanespan_kernel<DescSrc,OutSink,512>",
+                           "wal1000": "crc_lanespan_kernel<DescSrc,OutSink,1023>",
                            "sst_verify": "crc_sst4k_kernel<SstSrc,SstVerifySink,nt>",
                            "sst_seal": "crc_sst4k_kernel<SstSrc,SealSink,nt>",
                            "sst_crc": "crc_sst4k_kernel<SstSrc,SstCrcSink,nt>"}[args.workload],
@@ -386,6 +411,7 @@ def main():
                 "timing": args.timing,
             },
             "cpu_baseline": cpu,
+            "steady_state": steady,
             "ranks": ranks,
             "xor_of_crcs": f"{xor_all:08x}",
         }

@@ -419,6 +419,7 @@ struct FixedSrc {
   uint32_t init_raw;
   using Raw = uint64_t;
   __device__ __forceinline__ Raw load(uint64_t i) const { return i; }
+  __device__ __forceinline__ Raw load_cached(uint64_t i) const { return i; }
   __device__ __forceinline__ BlkDesc finish(Raw i) const { return {base + i * stride, len, init_raw}; }
   __device__ __forceinline__ BlkDesc get(uint64_t i) const { return finish(i); }
   __device__ __forceinline__ BlkDesc lane(Raw i) const { return finish(i); }  // per-lane fields
@@ -441,6 +442,10 @@ struct DescSrc {
   __device__ __forceinline__ Raw load(uint64_t i) const {
     // 8-B alignment is all pdb_blk guarantees: a 4-B-aligned 16-B load
     return __builtin_nontemporal_load(reinterpret_cast<const u32x4a4*>(blk + i));
+  }
+  // the same, cached (a consumer that re-reads a batch's descriptors: crc_lanespan_kernel)
+  __device__ __forceinline__ Raw load_cached(uint64_t i) const {
+    return *reinterpret_cast<const u32x4a4*>(blk + i);
   }
   __device__ __forceinline__ BlkDesc finish(const Raw& r) const {
     const uint32_t len = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(r.z));

@@ -288,7 +288,7 @@ __global__ __launch_bounds__(SpanStage<MAXN>::kWaves * 64) void crc_lanespan_ker
   };
   // the next batch's descriptors and sink words, in flight; reloaded by every next_item call (the
   // same address when no batch was opened) so no load is ever consumed right after it is issued
-  typename Src::Raw raw_next = src.load(idx(bnext));
+  typename Src::Raw raw_next = src.load_cached(idx(bnext));
   uint32_t pre_next = SinkOps<Sink>::pre(sink, idx(bnext), BlkDesc{nullptr, 0u, 0u});
   uint64_t bcur = 0;
   bool have_batch = false;
@@ -363,7 +363,7 @@ __global__ __launch_bounds__(SpanStage<MAXN>::kWaves * 64) void crc_lanespan_ker
       have_batch = true;
       rem = bfastm;
     }
-    raw_next = src.load(idx(bnext < nbat ? bnext : bcur));
+    raw_next = src.load_cached(idx(bnext < nbat ? bnext : bcur));
     pre_next = SinkOps<Sink>::pre(sink, idx(bnext < nbat ? bnext : bcur), BlkDesc{nullptr, 0u, 0u});
     it.valid = true;
     it.batch = bcur;
