@@ -43,7 +43,7 @@ constexpr uint32_t kSpanStageBase = 64u << 10;                    // tables and 
 // items hold 8..21 records on 3..8 lanes each -- more waves hide more of the hash's latency)
 template <uint32_t MAXN>
 struct SpanStage {
-  static constexpr uint32_t kWaves = MAXN <= 256u ? 10u : 12u;
+  static constexpr uint32_t kWaves = MAXN <= 256u ? 10u : 12u;  // (13 x 7 KiB for 512: slower, 128-VGPR cap)
   static constexpr uint32_t kJ = MAXN <= 256u ? 9u : 8u;
   static constexpr uint32_t kRegion = kJ * 1024u;
   static constexpr uint32_t kUsable = kRegion - 16u;  // span limit: reads stay inside

@@ -441,6 +441,38 @@ struct SinkOps<SealDwordSink> {
   }
 };
 
+// A/B variant 39: the 64 B from the trailer's 32-B sector on re-read and written back whole with the
+// trailer merged in (full-sector writes: no partial-sector read-modify-write at the memory side).
+// Diagnostics only: assumes no other trailer within 64 B (true of the bench's 4-KiB blocks).
+struct SealSectorSink {};
+
+template <>
+struct SinkOps<SealSectorSink> {
+  __device__ static __forceinline__ uint32_t pre(const SealSectorSink&, uint64_t, const BlkDesc&) { return 0u; }
+  __device__ static __forceinline__ void put(const SealSectorSink&, uint64_t, uint32_t raw, const BlkDesc& d,
+                                             uint32_t) {
+    if (d.init_raw == 0) return;
+    typedef __attribute__((address_space(1))) u32x4 g_v4;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(d.p) + d.n;
+    const uintptr_t s0 = a & ~static_cast<uintptr_t>(31);
+    const uint32_t o = static_cast<uint32_t>(a - s0), i0 = o >> 2, sh = (o & 3u) * 8u;
+    const uint32_t m = pdb_mask(~raw);
+    g_v4* w = reinterpret_cast<g_v4*>(s0);
+    u32x4 v[4] = {w[0], w[1], w[2], w[3]};
+    uint32_t x[16];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x[4 * i] = v[i].x, x[4 * i + 1] = v[i].y, x[4 * i + 2] = v[i].z, x[4 * i + 3] = v[i].w;
+    const uint32_t lo_keep = sh ? (0xFFFFFFFFu >> (32u - sh)) : 0u;  // bytes of dword i0 below the trailer
+#pragma unroll
+    for (uint32_t i = 0; i < 16; ++i) {
+      if (i == i0) x[i] = (x[i] & lo_keep) | (m << sh);
+      if (i == i0 + 1 && sh) x[i] = (x[i] & ~lo_keep) | (m >> (32u - sh));
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = u32x4{x[4 * i], x[4 * i + 1], x[4 * i + 2], x[4 * i + 3]};
+  }
+};
+
 template <>
 struct SinkOps<SealTouchSink> {
   __device__ static __forceinline__ uint32_t pre(const SealTouchSink&, uint64_t, const BlkDesc& d) {
@@ -476,6 +508,11 @@ hipError_t launch_sst_variant(int v, const LaunchGeom& g, const uint32_t* d_tabl
     else
       hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstVerifySink, true, 8>), grid, block, 0, s, d_tables, src, n,
                          SstVerifySink{ok, nbad});
+    return hipGetLastError();
+  }
+  if (v == 39 && seal) {  // full 32-B-sector rewrites around each trailer
+    hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SealSectorSink, true>), grid, block, 0, s, d_tables, src, n,
+                       SealSectorSink{});
     return hipGetLastError();
   }
   if (v == 37 && seal) {  // one dword store per trailer

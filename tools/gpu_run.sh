@@ -33,6 +33,8 @@ for s in "$@"; do
     bench) step bench 600 python bench.py --diag ;;
     prof_wal) step prof_wal100 500 bash tools/profile.sh ${TAG}_prof_wal100 wal100 && step prof_wal400 500 bash tools/profile.sh ${TAG}_prof_wal400 wal400 && step prof_wal1000 500 bash tools/profile.sh ${TAG}_prof_wal1000 wal1000 ;;
     bench_wal) step bench_wal100 300 python bench.py --workload wal100 --no-copy-inclusive && step bench_wal400 300 python bench.py --workload wal400 --no-copy-inclusive && step bench_wal1000 300 python bench.py --workload wal1000 --no-copy-inclusive ;;
+    copyinc) step copyinc 600 python tools/copy_inclusive.py ;;
+    ab_seal) step ab_seal 600 python tools/ab_sst.py 0,37,39 ;;
     bench_sst) step bench_sst 600 python bench.py --workload sstable --no-cpu-baseline --no-copy-inclusive ;;
     bench_c3) step bench_c3 600 python bench.py --workload c3 --no-copy-inclusive --steps 10 ;;
     *) echo "unknown step $s"; exit 2 ;;
