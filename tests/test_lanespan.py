@@ -43,7 +43,8 @@ def _check(crc, oracle_lib, base, offs, lens, hint, verify=True):
 
 
 @pytest.mark.parametrize("payload,hint", [(100, "256"), (131, "256"), (255, "256"), (431, "512"), (300, "512"),
-                                          (511, "512"), (700, "1023"), (1000, "1023"), (131, "1023")])
+                                          (511, "512"), (600, "1023"), (700, "1023"), (850, "1023"), (1000, "1023"),
+                                          (131, "1023")])
 def test_wal_layouts(crc, oracle_lib, payload, hint):
     """Log images as log::Writer lays them out: records + 7-byte headers, fragments at 32-KiB block
     ends, block trailers; the CRC spans are type || payload."""
@@ -94,7 +95,10 @@ def test_batch_boundaries(crc, oracle_lib, n):
         _check(crc, oracle_lib, base, offs, lens, hint, verify=n > 20)
 
 
-@pytest.mark.parametrize("length", [1, 3, 4, 5, 17, 131, 255, 256, 257, 300, 431, 512, 513, 700, 1000, 1023])
+# k (lanes per record) by length: 1..132 -> 1, 133..276 -> 2, 277..396 -> 3, 397..532 -> 4,
+# 533..664 -> 5, 665..796 -> 6, 797..924 -> 7, 925..1023 -> 8 (span_pick, 8-KiB regions)
+@pytest.mark.parametrize("length", [1, 3, 4, 5, 17, 131, 132, 133, 255, 256, 257, 300, 431, 512, 513, 600, 700, 850,
+                                    1000, 1023])
 @pytest.mark.parametrize("shift", [0, 1, 3])
 def test_fixed_strides(crc, oracle_lib, length, shift):
     """pdb_crc32c_batch_device_fixed with 1..1023-B blocks (the same kernel, FixedSrc)."""

@@ -136,3 +136,41 @@ def test_concurrent_callers(crc, oracle_lib):
     for x in th:
         x.join()
     assert not errors, errors[:3]
+
+
+def test_scalar_callers_beside_batch_seals(crc, oracle_lib):
+    """The engine's real mix (`pdb_dbbench_gpu_all`): foreground threads call the
+    scalar service per WAL record while a compaction thread runs host batches that park it.  Two
+    scalar threads x 400 calls and one thread of 12 host batches (each parks the server, which
+    the next scalar call relaunches): every scalar answer and every batch CRC exact."""
+    import oracle
+
+    pool = oracle.splitmix_bytes(70000, 777)
+    rng = np.random.default_rng(5)
+    bsizes = rng.integers(1, 9000, size=3000)
+    boffs = np.concatenate([[0], np.cumsum(bsizes)[:-1]])
+    bbuf = oracle.splitmix_bytes(int(boffs[-1] + bsizes[-1]), 778)
+    blk = crc.make_blocks(boffs, bsizes)
+    bexp = oracle_lib.batch(bbuf, blk, flags=0, nthreads=4)
+    errors = []
+
+    def scalar(t):
+        r = np.random.default_rng(t)
+        for _ in range(400):
+            off, n, init = int(r.integers(0, 1000)), int(r.integers(0, 1200)), int(r.integers(0, 1 << 32))
+            if crc.extend(init, pool[off : off + n]) != oracle_lib.extend(init, pool[off : off + n]):
+                errors.append(("scalar", t, off, n))
+
+    def batches():
+        for k in range(12):
+            if not np.array_equal(crc.batch_host(bbuf, blk), bexp):
+                errors.append(("batch", k))
+
+    th = [threading.Thread(target=scalar, args=(t,)) for t in range(2)] + [threading.Thread(target=batches)]
+    t0 = time.perf_counter()
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors[:3]
+    assert time.perf_counter() - t0 < 60
