@@ -48,6 +48,7 @@ struct Flags {
   int cache_size = -1;  // < 0: the engine's default block cache
   bool verify_checksums = false;
   bool use_existing_db = false;
+  bool paranoid_checks = false;
   std::string db = "/tmp/pdb_dbbench";
 } F;
 
@@ -117,6 +118,7 @@ leveldb::DB* Open(const leveldb::FilterPolicy* fp, leveldb::Cache* cache) {
   o.create_if_missing = !F.use_existing_db;
   o.block_cache = cache;
   o.filter_policy = fp;
+  o.paranoid_checks = F.paranoid_checks;  // compactions verify their inputs too (version_set.cc:2909)
   leveldb::DB* db = NULL;
   leveldb::Status s = leveldb::DB::Open(o, F.db, &db);
   if (!s.ok()) {
@@ -213,6 +215,7 @@ int main(int argc, char** argv) {
     else if (Arg(argv[i], "--cache_size", &v)) F.cache_size = atoi(v.c_str());
     else if (Arg(argv[i], "--verify_checksums", &v)) F.verify_checksums = atoi(v.c_str()) != 0;
     else if (Arg(argv[i], "--use_existing_db", &v)) F.use_existing_db = atoi(v.c_str()) != 0;
+    else if (Arg(argv[i], "--paranoid_checks", &v)) F.paranoid_checks = atoi(v.c_str()) != 0;
     else if (Arg(argv[i], "--db", &v)) F.db = v;
     else {
       fprintf(stderr, "invalid flag '%s'\n", argv[i]);

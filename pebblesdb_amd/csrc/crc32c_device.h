@@ -333,10 +333,154 @@ __device__ __forceinline__ uint32_t partial4k(const char* lds, const LaneTabs& l
   return shift_op_x(lds, PDB_SLOT_HORNER, xa, xb);  // shift 2048
 }
 
+// ---- lane-quarter table image: conflict-free tables AND Horner operators ---------------------
+// The 32-replica T0..T3 image above makes every table lookup conflict-free but takes 128 KiB, so
+// the shift operators live in single copies and a 64-lane operator lookup costs ~3 extra LDS cycles
+// of bank conflicts (4 random bytes -> 32 banks).  In the lane-quarter image (the record kernel's,
+// crc32c_lanespan.h) lookup instruction i sends lane quarter q = (lane >> 3) & 3 to table
+// k = (q + i) & 3, replica lane & 7: the four quarters of each 32-lane group read four tables in
+// four disjoint bank ranges, so 8 replicas are conflict-free -- 32 KiB per four tables.  An operator
+// (4 sub-tables indexed by the 4 state bytes) is looked up the same way: its sub-table 3 - k sits
+// where T_k does, so the T lookup's address byte and byte selector serve it unchanged.  64-KiB
+// images of 256 entry blocks (entry b at b << 8, the state byte placed by one v_perm):
+//   image 0 [0, 64 KiB):       T_k replica r at dword k*8 + r; shift 1024 sub-table 3-k at 32 + k*8 + r
+//   image 1 [64 KiB, 128 KiB): shift 2048 sub-table 3-k at dword k*8 + r  (dwords 32..63 unused)
+// and the tree operators (single copies, fewer lanes active per lookup) in slots 0..5 of the OPS
+// region as before.
+struct QuadTabs {
+  uint32_t t[4], s[4];  // address byte 0 (table slot, replica) and byte selector (byte 3 - k) of lookup i
+  uint32_t g[4];        // t | 0x10000: image 1 (the immediate offset of a ds_read stops at 64 KiB)
+};
+
+__device__ __forceinline__ QuadTabs quad_tabs(uint32_t u) {
+  const uint32_t r = u & 7u, q = (u >> 3) & 3u;
+  QuadTabs qt;
+#pragma unroll
+  for (uint32_t i = 0; i < 4; ++i) {
+    const uint32_t k = (q + i) & 3u, a = (k * 8u + r) << 2;
+    qt.t[i] = a;
+    qt.s[i] = sel_byte(3u - k);
+    qt.g[i] = 0x10000u | a;
+  }
+  return qt;
+}
+
+// x' = shift(x, 4 bytes) ^ wnext on the lane-quarter image (the same value as the LaneTabs form)
+__device__ __forceinline__ uint32_t step4x(const char* lds, const QuadTabs& qt, uint32_t x, uint32_t wnext) {
+  const uint32_t a0 = __builtin_amdgcn_perm(qt.t[0], x, qt.s[0]);
+  const uint32_t a1 = __builtin_amdgcn_perm(qt.t[1], x, qt.s[1]);
+  const uint32_t a2 = __builtin_amdgcn_perm(qt.t[2], x, qt.s[2]);
+  const uint32_t a3 = __builtin_amdgcn_perm(qt.t[3], x, qt.s[3]);
+  return xor3(xor3(lds_u32(lds, a0), lds_u32(lds, a1), lds_u32(lds, a2)), lds_u32(lds, a3), wnext);
+}
+
+// shift(c, D) ^ y through a replicated operator whose sub-tables sit at `base` (+ `off`)
+template <uint32_t off>
+__device__ __forceinline__ uint32_t op_q(const char* lds, const uint32_t (&base)[4], const uint32_t (&s)[4], uint32_t c,
+                                         uint32_t y) {
+  const char* l = lds + off;  // folded into the ds_read immediate offset
+  const uint32_t a0 = __builtin_amdgcn_perm(base[0], c, s[0]);
+  const uint32_t a1 = __builtin_amdgcn_perm(base[1], c, s[1]);
+  const uint32_t a2 = __builtin_amdgcn_perm(base[2], c, s[2]);
+  const uint32_t a3 = __builtin_amdgcn_perm(base[3], c, s[3]);
+  return xor3(xor3(lds_u32(l, a0), lds_u32(l, a1), lds_u32(l, a2)), lds_u32(l, a3), y);
+}
+
+// One slice-by-4 step c' = shift(c ^ w, 4) (the head words of the stream kernel)
+__device__ __forceinline__ uint32_t step4(const char* lds, const QuadTabs& qt, uint32_t c, uint32_t w) {
+  return step4x(lds, qt, c ^ w, 0u);
+}
+
+// stepk on the lane-quarter image: k = 1..3 leading bytes, every lane reading table k-1-j through
+// its own replica (a wave-uniform head: the lanes share the entry, no conflicts)
+__device__ __forceinline__ uint32_t stepk(const char* lds, const QuadTabs& qt, uint32_t c, uint32_t lb, uint32_t k) {
+  const uint32_t x = c ^ lb, r = qt.t[0] & 0x1Cu;  // (lane & 7) << 2
+  auto T = [&](uint32_t tab, uint32_t byte) { return lds_u32(lds, (((x >> (8u * byte)) & 0xFFu) << 8) | (tab << 5) | r); };
+  if (k == 1) return T(0, 0) ^ (x >> 8);
+  if (k == 2) return T(1, 0) ^ T(0, 1) ^ (x >> 16);
+  return xor3(T(2, 0), T(1, 1), T(0, 2)) ^ (x >> 24);
+}
+
+// shift(c, 1024) ^ y: the Horner fold of 16-B pieces 1 KiB apart, on either image
+__device__ __forceinline__ uint32_t horner1024(const char* lds, const LaneTabs&, uint32_t c, uint32_t y) {
+  return shift_op_x(lds, PDB_SLOT_HORNER, c, y);
+}
+__device__ __forceinline__ uint32_t horner1024(const char* lds, const QuadTabs& qt, uint32_t c, uint32_t y) {
+  return op_q<128u>(lds, qt.t, qt.s, c, y);
+}
+// shift(c, 1008): the stream kernel's round chaining (slot 6 of the 32-replica image; image 1)
+__device__ __forceinline__ uint32_t round1008(const char* lds, const LaneTabs&, uint32_t c) {
+  return shift_op(lds, PDB_SLOT_HORNER, c);
+}
+__device__ __forceinline__ uint32_t round1008(const char* lds, const QuadTabs& qt, uint32_t c) {
+  return op_q<0u>(lds, qt.g, qt.s, c, 0u);
+}
+
+// Stage image 0, image 1 (catalog operator kImg1: shift 2048 for crc_pack4k_kernel, 1008 for the
+// stream kernel's round chaining; -1: none) and the tree operators (catalog kTree .. kTree + 5 ->
+// slots 0..5), all of a thread's loads issued before its stores (launch latency matters for small
+// batches).
+template <int kTree, int kImg1>
+__device__ __forceinline__ void stage_tables_q4(char* lds, const uint32_t* __restrict__ tabs) {
+  // 16-B quads: q < kRep = replicated quads (part q >> 11: T, shift 1024, image 1; entry b, table
+  // slot k, replicas 4h..4h+3), then 1536 single-copy tree-operator quads
+  constexpr uint32_t kRep = (kImg1 >= 0 ? 3u : 2u) * 2048u, kAll = kRep + 6u * 256u;
+  const u32x4* cat = reinterpret_cast<const u32x4*>(tabs + 1024);
+  for (uint32_t i0 = 0; i0 < kAll; i0 += 8u * blockDim.x) {
+    u32x4 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t i = i0 + threadIdx.x + j * blockDim.x;
+      if (i < kRep) {
+        const uint32_t part = i >> 11, b = (i >> 3) & 255u, k = (i >> 1) & 3u;
+        // T_k, or operator sub-table 3 - k (tabs: T0..T3, then the catalog's 4 x 256 per operator)
+        const uint32_t src = part == 0 ? k * 256u + b
+                                       : 1024u + (part == 1 ? PDB_CAT_S1024 : static_cast<uint32_t>(kImg1)) * 1024u +
+                                             (3u - k) * 256u + b;
+        const uint32_t x = tabs[src];
+        v[j] = u32x4{x, x, x, x};
+      } else {
+        const uint32_t t = i - kRep;
+        v[j] = t < 6u * 256u ? cat[(kTree + (t >> 8)) * 256u + (t & 255u)] : u32x4{0, 0, 0, 0};
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t i = i0 + threadIdx.x + j * blockDim.x;
+      if (i < kRep) {
+        const uint32_t part = i >> 11, b = (i >> 3) & 255u, k = (i >> 1) & 3u, h = i & 1u;
+        const uint32_t addr = (part == 2 ? 0x10000u : 0u) | (b << 8) | (part == 1 ? 128u : 0u) | (k << 5) | (h << 4);
+        *reinterpret_cast<u32x4*>(lds + addr) = v[j];
+      } else if (i < kAll) {
+        *reinterpret_cast<u32x4*>(lds + PDB_MAIN_BYTES + (i - kRep) * 16u) = v[j];
+      }
+    }
+  }
+}
+
+// partial4k<4> on the lane-quarter image: four 4-word chains, Horner folds through the replicated
+// shift 1024 / shift 2048
+__device__ __forceinline__ uint32_t partial4k_q(const char* lds, const QuadTabs& qt, uint32_t c0, const u32x4 (&v)[4]) {
+  uint32_t x0 = c0 ^ v[0].x, x1 = v[1].x, x2 = v[2].x, x3 = v[3].x;
+  const uint32_t d0[4] = {v[0].x, v[0].y, v[0].z, v[0].w}, d1[4] = {v[1].x, v[1].y, v[1].z, v[1].w};
+  const uint32_t d2[4] = {v[2].x, v[2].y, v[2].z, v[2].w}, d3[4] = {v[3].x, v[3].y, v[3].z, v[3].w};
+#pragma unroll
+  for (int i = 1; i <= 4; ++i) {
+    x0 = step4x(lds, qt, x0, i < 4 ? d0[i] : 0u);
+    x1 = step4x(lds, qt, x1, i < 4 ? d1[i] : 0u);
+    x2 = step4x(lds, qt, x2, i < 4 ? d2[i] : 0u);
+    x3 = step4x(lds, qt, x3, i < 4 ? d3[i] : 0u);
+  }
+  const uint32_t a = horner1024(lds, qt, x0, x1);
+  const uint32_t b = horner1024(lds, qt, x2, x3);
+  return op_q<0u>(lds, qt.g, qt.s, a, b);  // shift 2048
+}
+
 // ---- fixed-stride batch, 4-KiB path (BASELINE configs 2 and 4) -------------------------------
 // len == 4096, base and stride 16-B aligned.  One wave per block; lane u owns the four 16-B pieces
 // at 16u + 1024j (j = 0..3), so each of a block's 4 load instructions reads 1 KiB contiguous,
-// issued non-temporal, and the pieces are 4 independent chains folded by partial4k<4>.  A wave
+// issued non-temporal, and the pieces are 4 independent chains folded by partial4k_q (the
+// lane-quarter image: the Horner operators conflict-free, +4-7 % over partial4k<4>).  A wave
 // hashes 4 blocks (g, g+W, g+2W, g+3W; W = waves in the grid), the next block's loads issued before
 // the current one is hashed, and folds their 4 x 64 lane partials in ONE tree4_packed.  One
 // barrier per 4-block group keeps the workgroup's 16 waves on 16 consecutive blocks (DRAM row
@@ -354,10 +498,10 @@ __global__ __launch_bounds__(kThreads) void crc_pack4k_kernel(
   const uint64_t w = wg_first + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   u32x4 buf[4];
   load4k<4, true>(buf, base, stride, w < nblk ? w : nblk - 1, u);  // overlaps the table staging
-  stage_tables<PDB_CAT_TREE16, PDB_CAT_S1024, PDB_CAT_S2048>(lds, tabs);
+  stage_tables_q4<PDB_CAT_TREE16, PDB_CAT_S2048>(lds, tabs);
   __syncthreads();
   if (wg_first >= nblk) return;  // workgroup-uniform: every wave of a live workgroup reaches each barrier
-  const LaneTabs lt = lane_tabs(u);
+  const QuadTabs qt = quad_tabs(u);
   const uint32_t init_raw = (flags & PDB_CRC_USE_INIT) ? ~init : 0xFFFFFFFFu;
   const uint32_t c0 = u == 0 ? init_raw : 0u;
   uint32_t res = 0, it = 0;
@@ -371,7 +515,7 @@ __global__ __launch_bounds__(kThreads) void crc_pack4k_kernel(
       u32x4 cur[4] = {buf[0], buf[1], buf[2], buf[3]};
       const uint64_t bn = bk + nw;
       if (bn < nblk) load4k<4, true>(buf, base, stride, bn, u);  // wave-uniform
-      p[r] = bk < nblk ? partial4k<4>(lds, lt, c0, cur) : 0u;
+      p[r] = bk < nblk ? partial4k_q(lds, qt, c0, cur) : 0u;
     }
     const uint32_t v = tree4_packed(lds, u, p[0], p[1], p[2], p[3]);
     // lane 4j+r of the 64-block window holds block (window + (4j+r)*nw): move lanes 0..3's
@@ -864,7 +1008,8 @@ __device__ __forceinline__ u32x4 ldq(const uint8_t* q) {
     return *v;
 }
 
-__device__ __forceinline__ uint32_t chain16(const char* lds, const LaneTabs& lt, uint32_t start,
+template <class LT>
+__device__ __forceinline__ uint32_t chain16(const char* lds, const LT& lt, uint32_t start,
                                             const u32x4& e, uint32_t nx, uint32_t s) {
   uint32_t w0 = e.x, w1 = e.y, w2 = e.z, w3 = e.w;
   if (s) {
@@ -880,18 +1025,31 @@ __device__ __forceinline__ uint32_t chain16(const char* lds, const LaneTabs& lt,
   return step4x(lds, lt, x, 0u);
 }
 
-template <class Src, class Sink, bool kDyn, bool kNT, bool kPack = false>
+// LT: the table image -- QuadTabs (lane-quarter: T0..T3, shift 1024 and shift 1008 conflict-free;
+// shipped) or LaneTabs (32 replicas of T0..T3, single-copy operators; A/B diagnostics).
+template <class Src, class Sink, bool kDyn, bool kNT, bool kPack = false, class LT = QuadTabs>
 __global__ __launch_bounds__(kThreads) void crc_stream16_kernel(const uint32_t* __restrict__ tabs,
                                                                  Src src, uint64_t nblk, Sink sink) {
+  constexpr bool kQuad = __is_same(LT, QuadTabs);
+  // the 32-replica image leaves no free slot: its work counter takes slot 5 (the trees then apply
+  // shift 256 twice); the lane-quarter image leaves slots 6 and 7 free
+  constexpr bool kL5Twice = kDyn && !kQuad;
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
   char* lds = reinterpret_cast<char*>(lds_words);
-  stage_tables<PDB_CAT_TREE16, PDB_CAT_H1008, PDB_CAT_S1024, kDyn>(lds, tabs);
-  uint32_t* ctr = reinterpret_cast<uint32_t*>(lds + PDB_MAIN_BYTES + 5 * 4096u);
+  if constexpr (kQuad)
+    stage_tables_q4<PDB_CAT_TREE16, PDB_CAT_H1008>(lds, tabs);
+  else
+    stage_tables<PDB_CAT_TREE16, PDB_CAT_H1008, PDB_CAT_S1024, kDyn>(lds, tabs);
+  uint32_t* ctr = reinterpret_cast<uint32_t*>(lds + PDB_MAIN_BYTES + (kQuad ? 7u : 5u) * 4096u);
   const uint64_t g_lo = nblk * blockIdx.x / gridDim.x, g_hi = nblk * (blockIdx.x + 1) / gridDim.x;
   if (kDyn && threadIdx.x == 0) *ctr = kWavesPerWg;  // next block, relative to g_lo
   __syncthreads();
   const uint32_t u = threadIdx.x & 63u;
-  const LaneTabs lt = lane_tabs(u);
+  LT lt;
+  if constexpr (kQuad)
+    lt = quad_tabs(u);
+  else
+    lt = lane_tabs(u);
   const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWavesPerWg;
   auto next_block = [&](uint64_t cur) -> uint64_t {
     if constexpr (kDyn) {
@@ -984,7 +1142,7 @@ __global__ __launch_bounds__(kThreads) void crc_stream16_kernel(const uint32_t* 
   uint64_t pid0 = 0, pid1 = 0, pid2 = 0, pid3 = 0;
   BlkDesc pd0{}, pd1{}, pd2{}, pd3{};
   auto flush = [&]() {
-    const uint32_t v = tree4_packed<kDyn>(lds, u, park0, park1, park2, park3);
+    const uint32_t v = tree4_packed<kL5Twice>(lds, u, park0, park1, park2, park3);
     if (u < npark) {
       const uint64_t id = u == 0 ? pid0 : (u == 1 ? pid1 : (u == 2 ? pid2 : pid3));
       const BlkDesc bd = u == 0 ? pd0 : (u == 1 ? pd1 : (u == 2 ? pd2 : pd3));
@@ -1044,24 +1202,31 @@ __global__ __launch_bounds__(kThreads) void crc_stream16_kernel(const uint32_t* 
     if (J) {
       // chain j runs (once, for the whole wave) only if some lane has a piece in it: a block of
       // 1 KiB needs 2 of the 5 chains, not all of them (wave-uniform conditions on rem)
-      const uint32_t start = ck ? shift_op(lds, PDB_SLOT_HORNER, acc) : acc;
+      const uint32_t start = ck ? round1008(lds, lt, acc) : acc;
       const bool full = !last_round;
       uint32_t a = chain16(lds, lt, start, e0, n0, s);
+      // shift 1024: slot 7 of the 32-replica image (its slot 6 holds 1008), image 0 of the other
+      auto fold = [&](uint32_t x, uint32_t y) {
+        if constexpr (kQuad)
+          return horner1024(lds, lt, x, y);
+        else
+          return shift_op_x(lds, 7, x, y);
+      };
       if (full || rem > 64u) {
         const uint32_t x1 = chain16(lds, lt, 0u, e1, n1, s);
-        if (J > 1) a = shift_op_x(lds, 7, a, x1);
+        if (J > 1) a = fold(a, x1);
       }
       if (full || rem > 128u) {
         const uint32_t x2 = chain16(lds, lt, 0u, e2, n2, s);
-        if (J > 2) a = shift_op_x(lds, 7, a, x2);
+        if (J > 2) a = fold(a, x2);
       }
       if (full || rem > 192u) {
         const uint32_t x3 = chain16(lds, lt, 0u, e3, n3, s);
-        if (J > 3) a = shift_op_x(lds, 7, a, x3);
+        if (J > 3) a = fold(a, x3);
       }
       if (!full && rem > 256u) {  // the last round's fifth chain
         const uint32_t x4 = chain16(lds, lt, 0u, e4, n4, s);
-        if (J > 4) a = shift_op_x(lds, 7, a, x4);
+        if (J > 4) a = fold(a, x4);
       }
       acc = a;
     }
@@ -1087,7 +1252,7 @@ __global__ __launch_bounds__(kThreads) void crc_stream16_kernel(const uint32_t* 
         if (K) {
           const uint32_t q = K & 63u;
           if (q) acc = __shfl(acc, (u + q) & 63u, 64);
-          raw = wave_tree_dpp<kDyn>(lds, u, acc);
+          raw = wave_tree_dpp<kL5Twice>(lds, u, acc);
         }
         if (u == 0) sink.put(mcur.i, raw, cd);
       }
@@ -1179,7 +1344,8 @@ __device__ __forceinline__ void issue_masked(MaskedPiece& f, uintptr_t A, uintpt
 }
 
 // The piece's raw state from `start` (0 for zero pieces: the masked bytes are zeros).
-__device__ __forceinline__ uint32_t hash_masked(const char* lds, const LaneTabs& lt, const MaskedPiece& f,
+template <class LT>
+__device__ __forceinline__ uint32_t hash_masked(const char* lds, const LT& lt, const MaskedPiece& f,
                                                 uint32_t start) {
   const uint32_t z = f.zl < 0 ? 0u : static_cast<uint32_t>(f.zl);
   uint32_t w[4];
@@ -1248,7 +1414,8 @@ __device__ __forceinline__ void slow_issue(SlowFirst& sf, uintptr_t p, uint32_t 
   for (int j = 0; j < 4; ++j) issue_masked(sf.f[j], v + 1024u * j, lo);
 }
 
-__device__ __forceinline__ uint32_t slow_finish(const char* lds, const LaneTabs& lt, uint32_t u, uint32_t ureg,
+template <class LT>
+__device__ __forceinline__ uint32_t slow_finish(const char* lds, const LT& lt, uint32_t u, uint32_t ureg,
                                                 const SlowFirst& sf, uintptr_t p, uint32_t n) {
   if (n == 0) return 0xFFFFFFFFu;
   const uint32_t nb = static_cast<uint32_t>((static_cast<uint64_t>(n) + 4095u) >> 12);
@@ -1257,7 +1424,7 @@ __device__ __forceinline__ uint32_t slow_finish(const char* lds, const LaneTabs&
 #pragma unroll
   for (int j = 0; j < 4; ++j)
     if (vbs + 1024u * (j + 1) > p)  // wave-uniform: a row holding block bytes
-      acc = shift_op_x(lds, PDB_SLOT_HORNER, acc, hash_masked(lds, lt, sf.f[j], masked_start(sf.f[j], ureg)));
+      acc = horner1024(lds, lt, acc, hash_masked(lds, lt, sf.f[j], masked_start(sf.f[j], ureg)));
   if (nb > 1) {  // full bodies, the next one loading while one is hashed
     MaskedPiece f[4], g[4];
 #pragma unroll
@@ -1267,7 +1434,7 @@ __device__ __forceinline__ uint32_t slow_finish(const char* lds, const LaneTabs&
 #pragma unroll
       for (int j = 0; j < 4; ++j) issue_masked(g[j], vbs + (static_cast<uintptr_t>(qn) << 12) + 16u * u + 1024u * j, p);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc = shift_op_x(lds, PDB_SLOT_HORNER, acc, hash_masked(lds, lt, f[j], 0u));
+      for (int j = 0; j < 4; ++j) acc = horner1024(lds, lt, acc, hash_masked(lds, lt, f[j], 0u));
 #pragma unroll
       for (int j = 0; j < 4; ++j) f[j] = g[j];
     }
@@ -1284,7 +1451,9 @@ constexpr uint32_t kSlowList = 64u;
 // kRows = body size in KiB: 4 (crc_sst4k_kernel) or 1 (crc_sst1k_kernel).
 // kBlk = blocks per group: 4 (rows of 16 lanes hash the prefixes: <= 256 B) or, for 1-KiB bodies,
 // 8 (rows of 8 lanes: prefixes <= 128 B, one packed tree per 8 blocks).
-template <class Src, class Sink, bool kNT, int kRows, bool kDiagNoFold = false, int kBlk = 4>
+// LT: the table image -- QuadTabs (lane-quarter, conflict-free shift 1024; shipped) or LaneTabs (the
+// 32-replica image with single-copy operators; A/B diagnostics)
+template <class Src, class Sink, bool kNT, int kRows, bool kDiagNoFold = false, int kBlk = 4, class LT = QuadTabs>
 __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ tabs, Src src, uint64_t nblk,
                                                   Sink sink) {
   static_assert(kRows == 0 || kRows == 1 || kRows == 4, "no body (records <= 256 B), 1-KiB or 4-KiB bodies");
@@ -1294,14 +1463,22 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
   constexpr uint32_t kBody = 1024u * kRows, kMin = kRows ? kBody : 1u, kMax = kBody + 16u * kRowLanes;
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
   char* lds = reinterpret_cast<char*>(lds_words);
-  stage_tables<PDB_CAT_TREE16, PDB_CAT_S1024>(lds, tabs);  // slots 0..5 = 16..512, 6 = 1024
+  // lane-quarter image: T0..T3 and shift 1024 conflict-free, slots 0..5 = 16..512
+  if constexpr (__is_same(LT, QuadTabs))
+    stage_tables_q4<PDB_CAT_TREE16, -1>(lds, tabs);
+  else
+    stage_tables<PDB_CAT_TREE16, PDB_CAT_S1024>(lds, tabs);  // slots 0..5 = 16..512, 6 = 1024
   uint32_t* ctr = reinterpret_cast<uint32_t*>(lds + PDB_MAIN_BYTES + 7 * 4096u);
   const uint64_t g_lo = nblk * blockIdx.x / gridDim.x, g_hi = nblk * (blockIdx.x + 1) / gridDim.x;
   if (threadIdx.x == 0) *ctr = kWavesPerWg;  // next kBlk-block group, in groups relative to g_lo
   const uint32_t u = threadIdx.x & 63u;
   const uint32_t ureg = tabs[PDB_UNSHIFT_OFF + (u & 15u)];
   __syncthreads();
-  const LaneTabs lt = lane_tabs(u);
+  LT lt;
+  if constexpr (__is_same(LT, QuadTabs))
+    lt = quad_tabs(u);
+  else
+    lt = lane_tabs(u);
   uint64_t grp = g_lo + kBlk * static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
   if (grp >= g_hi) return;
   const uintptr_t dummy = reinterpret_cast<uintptr_t>(tabs);  // >= 4 KiB + 256 B of valid bytes
@@ -1393,7 +1570,7 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
       const uint32_t x = chain16(lds, lt, 0u, e[j], nx[j], s);
       // kDiagNoFold (A/B diagnostics only, WRONG CRCs): the Horner fold replaced by a XOR, to price
       // the shift-operator lookups
-      a = kDiagNoFold ? (a ^ x) : shift_op_x(lds, PDB_SLOT_HORNER, a, x);
+      a = kDiagNoFold ? (a ^ x) : horner1024(lds, lt, a, x);
     }
     return a;
   };
@@ -1652,16 +1829,18 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
 }
 
 // kBlk = 8 (A/B): 8-block groups, prefixes <= 128 B in rows of 8 lanes, one tree8_packed.
-template <class Src, class Sink, bool kNT, int kBlk = 4>
+template <class Src, class Sink, bool kNT, int kBlk = 4, class LT = QuadTabs>
 __global__ __launch_bounds__(kThreads) void crc_sst4k_kernel(const uint32_t* __restrict__ tabs, Src src,
                                                              uint64_t nblk, Sink sink) {
-  sized_kernel_body<Src, Sink, kNT, 4, false, kBlk>(tabs, src, nblk, sink);
+  sized_kernel_body<Src, Sink, kNT, 4, false, kBlk, LT>(tabs, src, nblk, sink);
 }
 
-template <class Src, class Sink, bool kNT, int kBlk = 8>
+// (the 1-KiB body has no Horner fold: both images measure the same, +0.8 % for the lane-quarter
+// one -- diagnostics variant 42 is the 32-replica image)
+template <class Src, class Sink, bool kNT, int kBlk = 8, class LT = QuadTabs>
 __global__ __launch_bounds__(kThreads) void crc_sst1k_kernel(const uint32_t* __restrict__ tabs, Src src,
                                                              uint64_t nblk, Sink sink) {
-  sized_kernel_body<Src, Sink, kNT, 1, false, kBlk>(tabs, src, nblk, sink);
+  sized_kernel_body<Src, Sink, kNT, 1, false, kBlk, LT>(tabs, src, nblk, sink);
 }
 
 // ---- records of 1..1023 B, one lane per record -------------------------------------------------

@@ -7,7 +7,7 @@
 // (table/format.cc:96-98).  Results are bit-identical (tests/golden + oracle parity).
 //
 // Shipped launches (the kernels themselves live in crc32c_device.h):
-//   * crc_pack4k_kernel<1, 4, nt> -- fixed stride, 4-KiB, 16-B aligned blocks (BASELINE configs
+//   * crc_pack4k_kernel -- fixed stride, 4-KiB, 16-B aligned blocks (BASELINE configs
 //     2/4).  One wave per block, lane l owns four 16-B pieces (16l + 1024j, so every load
 //     instruction reads 1 KiB contiguous, non-temporal) hashed as four independent slice-by-4
 //     chains, 4 blocks per wave-iteration folded in one packed tree, one barrier per 4-block
@@ -21,9 +21,12 @@
 //     leading 0..256 B of 4 blocks hashed together as zero-padded pieces from an "unshifted"
 //     seed; other lengths in the same launch take a whole-wave slow path.
 //   * crc_server_kernel (crc32c_server.hip) -- the persistent scalar Extend service.
-// LDS image (crc32c_math.h): T0..T3 replicated 32x (128 KiB) so each lane reads its own bank +
-// 8 shift-operator slots (32 KiB): the whole 160 KiB of a CU; one 1024-thread workgroup per CU
-// stages it once and walks blocks persistently.  DESIGN.md §3-§6 has the measurements.
+// LDS image (crc32c_device.h, "lane-quarter table image"): T0..T3 and the per-lane Horner
+// operators (shift 1024, and 2048 or 1008) in 8 replicas each, every lookup bank-conflict free,
+// plus the tree operators in single-copy slots; one 1024-thread workgroup per CU stages it once
+// and walks blocks persistently.  (Round 1 replicated T0..T3 32x in 128 KiB and left the Horner
+// operators in single copies: 3 extra LDS cycles per operator lookup.)  DESIGN.md §3-§6 has the
+// measurements.
 #include "crc32c_device.h"
 #include "crc32c_lanespan.h"
 

@@ -101,6 +101,21 @@ struct TabsS4 {
     const uint32_t a3 = __builtin_amdgcn_perm(lt.t[3], x, lt.s[3]);
     return xor3(xor3(lds_u32(lds, a0), lds_u32(lds, a1), lds_u32(lds, a2)), lds_u32(lds, a3), w);
   }
+  // four independent chains stepped together: all 16 lookups are issued before the first result
+  // is consumed (left to itself the scheduler issues them in groups of 4-8 and waits for each
+  // group, one LDS round trip per group)
+  __device__ static __forceinline__ void step4(const char* lds, const LT& lt, uint32_t (&x)[4], const uint32_t (&w)[4]) {
+    uint32_t a[16], v[16];
+#pragma unroll
+    for (uint32_t c = 0; c < 4; ++c)
+#pragma unroll
+      for (uint32_t i = 0; i < 4; ++i) a[4 * c + i] = __builtin_amdgcn_perm(lt.t[i], x[c], lt.s[i]);
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j) v[j] = lds_u32(lds, a[j]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (uint32_t c = 0; c < 4; ++c) x[c] = xor3(xor3(v[4 * c], v[4 * c + 1], v[4 * c + 2]), v[4 * c + 3], w[c]);
+  }
   __device__ static __forceinline__ void stage(char* lds, const uint32_t* __restrict__ tabs) {
     // T0..T3 x 8 replicas: 256 entries x 4 tables x 2 quads of 16 B; quad i at b<<8 | k<<5 | h<<4
     for (uint32_t i = threadIdx.x; i < 2048u; i += blockDim.x) {
@@ -492,19 +507,21 @@ __global__ __launch_bounds__(SpanStage<MAXN>::kWaves * 64) void crc_lanespan_ker
     uint32_t xa = 0, xb = 0, xc = 0;
 #pragma unroll
     for (int32_t t = 1; t < static_cast<int32_t>(kSpanLD); ++t) {
-      const uint32_t ha = lds_u32(q0, 4u * (t + 1)), hb = lds_u32(q1, 4u * (t + 1));
-      const uint32_t hc = lds_u32(q2, 4u * (t + 1)), hd = lds_u32(q3, 4u * (t + 1));
+      // one base, immediate offsets (q0..q2 are q3 + 96, 64, 32)
+      const uint32_t ha = lds_u32(q3, 96u + 4u * (t + 1)), hb = lds_u32(q3, 64u + 4u * (t + 1));
+      const uint32_t hc = lds_u32(q3, 32u + 4u * (t + 1)), hd = lds_u32(q3, 4u * (t + 1));
       const uint32_t wa = __builtin_amdgcn_perm(ha, la, sel), wb = __builtin_amdgcn_perm(hb, lb, sel);
       const uint32_t wc = __builtin_amdgcn_perm(hc, lc, sel), wd = __builtin_amdgcn_perm(hd, ld, sel);
       la = ha, lb = hb, lc = hc, ld = hd;
       if (t == 1) {
         xa = wa, xb = wb, xc = wc;
+        xd = TP::step(lds, lt, xd, wd);
       } else {
-        xa = TP::step(lds, lt, xa, wa);
-        xb = TP::step(lds, lt, xb, wb);
-        xc = TP::step(lds, lt, xc, wc);
+        uint32_t x4[4] = {xa, xb, xc, xd};
+        const uint32_t w4[4] = {wa, wb, wc, wd};
+        TP::step4(lds, lt, x4, w4);
+        xa = x4[0], xb = x4[1], xc = x4[2], xd = x4[3];
       }
-      xd = TP::step(lds, lt, xd, wd);
       if (t <= G) {
         xa = T == t ? pw : xa;
         xb = T + 8 == t ? pw : xb;
@@ -514,10 +531,13 @@ __global__ __launch_bounds__(SpanStage<MAXN>::kWaves * 64) void crc_lanespan_ker
     }
     // finish; a chain whose end is at or before the p-word's start holds no byte of the record
     const int32_t L = static_cast<int32_t>(kSpanLD);
-    const uint32_t ca = T < L ? TP::step(lds, lt, xa, 0u) : 0u;
-    const uint32_t cb = T + 8 < L ? TP::step(lds, lt, xb, 0u) : 0u;
-    const uint32_t cc = T + 16 < L ? TP::step(lds, lt, xc, 0u) : 0u;
-    const uint32_t cd = T + 24 < L ? TP::step(lds, lt, xd, 0u) : 0u;
+    uint32_t x4[4] = {xa, xb, xc, xd};
+    const uint32_t z4[4] = {0u, 0u, 0u, 0u};
+    TP::step4(lds, lt, x4, z4);
+    const uint32_t ca = T < L ? x4[0] : 0u;
+    const uint32_t cb = T + 8 < L ? x4[1] : 0u;
+    const uint32_t cc = T + 16 < L ? x4[2] : 0u;
+    const uint32_t cd = T + 24 < L ? x4[3] : 0u;
     const uint32_t lo2 = span_op_x(lds, kOp32, cb, ca);  // shift(B, 32) ^ A
     const uint32_t hi2 = span_op_x(lds, kOp32, cd, cc);  // shift(D, 32) ^ C
     uint32_t P = span_op_x(lds, kOp64, hi2, lo2);        // shift(hi2, 64) ^ lo2

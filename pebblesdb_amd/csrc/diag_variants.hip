@@ -501,6 +501,15 @@ hipError_t launch_sst_variant(int v, const LaunchGeom& g, const uint32_t* d_tabl
                        SstVerifySink{ok, nullptr});  // no nbad: every block "fails"; 1M atomics would dominate
     return hipGetLastError();
   }
+  if (v == 30) {  // the round-1 table image: 32 replicas of T0..T3, single-copy shift 1024
+    if (seal)
+      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SealSink, true, 4, LaneTabs>), grid, block, 0, s, d_tables, src, n,
+                         SealSink{});
+    else
+      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstVerifySink, true, 4, LaneTabs>), grid, block, 0, s, d_tables, src,
+                         n, SstVerifySink{ok, nbad});
+    return hipGetLastError();
+  }
   if (v == 38) {  // 8-block groups (prefixes <= 128 B in rows of 8 lanes, tree8_packed)
     if (seal)
       hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SealSink, true, 8>), grid, block, 0, s, d_tables, src, n,
@@ -720,6 +729,18 @@ hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tab
       break;
     case 41:  // the 1-KiB kernel with 4-block groups (fast range 1024..1280 B)
       hipLaunchKernelGGL((crc_sst1k_kernel<DescSrc, OutSink, true, 4>), grid, block, 0, s, d_tables, src, nblk, sink);
+      break;
+    case 42:  // the 1-KiB kernel on the round-1 table image (32 replicas)
+      hipLaunchKernelGGL((crc_sst1k_kernel<DescSrc, OutSink, true, 8, LaneTabs>), grid, block, 0, s, d_tables, src, nblk,
+                         sink);
+      break;
+    case 44:  // the any-length kernel (C3 routing) on the round-1 table image
+      hipLaunchKernelGGL((crc_stream16_kernel<DescSrc, OutSink, true, true, true, LaneTabs>), grid, block, 0, s, d_tables,
+                         src, nblk, sink);
+      break;
+    case 43:  // the 4-KiB kernel on the round-1 table image (32 replicas, single-copy shift 1024)
+      hipLaunchKernelGGL((crc_sst4k_kernel<DescSrc, OutSink, true, 4, LaneTabs>), grid, block, 0, s, d_tables, src, nblk,
+                         sink);
       break;
     case 50:  // one lane per record, 32-B groups loaded one ahead (nt / default policy)
       hipLaunchKernelGGL((crc_lanerec_kernel<DescSrc, OutSink, true>), lgrid, block, 0, s, d_tables, src, nblk, sink);

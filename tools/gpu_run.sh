@@ -21,6 +21,12 @@ for s in "$@"; do
   case "$s" in
     tests) step tests 1000 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread ;;
     cold) step cold 300 python tools/cold_start.py ;;
+    cold_variants) step cold_variants 300 python tools/cold_variants.py --variants 0,-1,19,24,13,28,12 ;;
+    cold_q4) step cold_q4 300 python tools/cold_variants.py --variants 0,99,-1 ;;
+    ab_c2) step ab_c2 300 python tools/ab_fast.py 0,99 8 ;;
+    ab_q4) step ab_q4_sst 300 python tools/ab_sst.py 0,30 && step ab_q4_wal 300 python tools/ab_desc.py 0,42 wal && step ab_q4_desc4k 300 python tools/ab_desc.py 0,43 sst ;;
+    ab_q4c3) step ab_q4_c3 300 python tools/ab_desc.py 0,44 c3 ;;
+    ab_q4r) step ab_q4r_wal 300 python tools/ab_desc.py 0,42 wal && step ab_q4r_wal_rev 300 python tools/ab_desc.py 42,0 wal && step ab_q4r_desc4k 300 python tools/ab_desc.py 43,0 sst && step ab_q4r_sst 300 python tools/ab_sst.py 30,0 && step ab_q4r_c3 300 python tools/ab_desc.py 44,0 c3 ;;
     lanespan) step lanespan 600 python -u -m pytest tests/test_lanespan.py tests/test_sst4k.py -m gpu -x -v --timeout 200 --timeout-method thread ;;
     ab_lanespan) step ab_lanespan 600 python tools/ab_lanespan.py ;;
     probe_wal100) step probe_wal100 900 bash tools/counters_probe.sh ${TAG}_probe100 wal100 0 64 67 ;;
