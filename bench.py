@@ -396,15 +396,15 @@ def main():
                 "traffic": traffic,
                 "traffic_source": "profiles/pmc_traffic.json: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this "
                                   "workload (tools/profile.sh), per launch, FETCH_SIZE x2 (MI355X_MICROARCH.md)",
-                "kernel": {"c2": "crc_pack4k_kernel<1,4,nt>", "sstable": "crc_sst4k_kernel<FixedSrc,OutSink,nt>",
-                           "c3": "crc_stream16_kernel<DescSrc,OutSink,dyn,nt,pack>",
-                           "wal": "crc_sst1k_kernel<DescSrc,OutSink,nt>",
+                "kernel": {"c2": "crc_pack4k_kernel (lane-quarter tables)", "sstable": "crc_sst4k_kernel<FixedSrc,OutSink,nt,QuadTabs>",
+                           "c3": "crc_stream16_kernel<DescSrc,OutSink,dyn,nt,pack,QuadTabs>",
+                           "wal": "crc_sst1k_kernel<DescSrc,OutSink,nt,QuadTabs>",
                            "wal100": "crc_lanespan_kernel<DescSrc,OutSink,256>",
                            "wal400": "crc_lanespan_kernel<DescSrc,OutSink,512>",
                            "wal1000": "crc_lanespan_kernel<DescSrc,OutSink,1023>",
-                           "sst_verify": "crc_sst4k_kernel<SstSrc,SstVerifySink,nt>",
-                           "sst_seal": "crc_sst4k_kernel<SstSrc,SealSink,nt>",
-                           "sst_crc": "crc_sst4k_kernel<SstSrc,SstCrcSink,nt>"}[args.workload],
+                           "sst_verify": "crc_sst4k_kernel<SstSrc,SstVerifySink,nt,QuadTabs>",
+                           "sst_seal": "crc_sst4k_kernel<SstSrc,SealSink,nt,QuadTabs>",
+                           "sst_crc": "crc_sst4k_kernel<SstSrc,SstCrcSink,nt,QuadTabs>"}[args.workload],
                 "algorithmic_bytes_per_launch": algo_bytes,
                 "kernel_avg_ms": round(kern_avg_ms, 4),
                 "kernel_min_ms": round(float(np.min(kern_ms)), 4),

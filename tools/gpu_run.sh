@@ -40,7 +40,10 @@ for s in "$@"; do
     prof_wal) step prof_wal100 500 bash tools/profile.sh ${TAG}_prof_wal100 wal100 && step prof_wal400 500 bash tools/profile.sh ${TAG}_prof_wal400 wal400 && step prof_wal1000 500 bash tools/profile.sh ${TAG}_prof_wal1000 wal1000 ;;
     bench_wal) step bench_wal100 300 python bench.py --workload wal100 --no-copy-inclusive && step bench_wal400 300 python bench.py --workload wal400 --no-copy-inclusive && step bench_wal1000 300 python bench.py --workload wal1000 --no-copy-inclusive ;;
     copyinc) step copyinc 600 python tools/copy_inclusive.py ;;
+    prof_c2) step prof_c2 700 bash tools/profile.sh ${TAG}_prof_c2 c2 ;;
+    prof_rows) step prof_c3 700 bash tools/profile.sh ${TAG}_prof_c3 c3 && step prof_sst_verify 700 bash tools/profile.sh ${TAG}_prof_sst_verify sst_verify && step prof_sstable 700 bash tools/profile.sh ${TAG}_prof_sstable sstable && step prof_wal 700 bash tools/profile.sh ${TAG}_prof_wal wal ;;
     ab_seal) step ab_seal 600 python tools/ab_sst.py 0,37,39 ;;
+    bench_rows) for w in sst_verify sst_seal sst_crc wal sstable c3; do step bench_$w 300 python bench.py --workload $w --no-copy-inclusive --steps 50 || exit 1; done ;;
     bench_sst) step bench_sst 600 python bench.py --workload sstable --no-cpu-baseline --no-copy-inclusive ;;
     bench_c3) step bench_c3 600 python bench.py --workload c3 --no-copy-inclusive --steps 10 ;;
     *) echo "unknown step $s"; exit 2 ;;
