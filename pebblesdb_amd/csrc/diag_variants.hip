@@ -687,6 +687,8 @@ hipError_t launch_fixed_variant(int v, const LaunchGeom& g, const uint32_t* d_ta
     // s_setprio 2 around the next block's load issue (free-running / lock-step)
     case 30: PDB_K((crc_pack4k_ab_kernel<1, 4, true, 16, false, false, 0, true>)); break;
     case 31: PDB_K((crc_pack4k_ab_kernel<0, 4, true, 16, false, false, 0, true>)); break;
+    // 99 (and unknown ids): the round-1 shipped kernel, on the 32-replica table image with
+    // single-copy Horner operators (crc_pack4k_kernel now runs on the lane-quarter image)
     default: PDB_K((crc_pack4k_ab_kernel<1, 4, true>)); break;
   }
 #undef PDB_FAST

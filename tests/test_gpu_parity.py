@@ -189,7 +189,7 @@ def test_all_fast_variants_bit_exact(crc, oracle_lib):
     diag.fill_splitmix(d, 4242)
     exp = oracle_lib.batch(d.cpu().numpy(), crc.make_blocks(np.arange(nblk) * 4096, np.full(nblk, 4096)),
                            nthreads=8)
-    for v in range(32):
+    for v in list(range(32)) + [99]:  # 99: unknown id -> the round-1 32-replica table image
         got = _u32(diag.batch_fixed(v, d, 4096, 4096, nblk))
         assert (got == exp).all(), f"variant {v}"
 

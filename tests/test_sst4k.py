@@ -277,7 +277,8 @@ def test_host_batch_picks_size_class(crc, oracle_lib, lo, hi):
 
 def test_sized_kernels_match_generic_kernel(crc):
     """Diagnostics-library variants -- 40 ignores the hints (crc_stream16_kernel), 41 runs the 1-KiB
-    kernel with 4-block groups, 50-52 the lane-per-record kernels on every list (larger blocks on
+    kernel with 4-block groups, 42-44 the 1-KiB / 4-KiB / any-length kernels on the round-1 table
+    image (32 replicas, single-copy Horner operators), 50-52 the lane-per-record kernels on every list (larger blocks on
     their whole-wave slow path), 53 the <= 256-B class on crc_rec256_kernel, 54-58 the other
     lane-per-record A/B forms: identical CRCs on a mixed batch, for every size hint."""
     rng = np.random.Generator(np.random.PCG64(81))
@@ -288,7 +289,7 @@ def test_sized_kernels_match_generic_kernel(crc):
     d_base, d_blk = torch.from_numpy(base).cuda(), crc.blocks_to_device(blk)
     hints = (crc.SIZE_1K, crc.SIZE_4K, crc.SIZE_256, crc.SIZE_512, crc.SIZE_1023)
     ref = [crc.batch(d_base, d_blk, size_hint=h).cpu().numpy() for h in ("1k", "4k", "256", "512", "1023")]
-    for v in (0, 40, 41, 50, 51, 52, 53, 54, 55, 56, 57, 58):
+    for v in (0, 40, 41, 42, 43, 44, 50, 51, 52, 53, 54, 55, 56, 57, 58):
         for a, hint in zip(ref, hints):
             b = diag.batch_desc(v, d_base, d_blk, flags=hint).cpu().numpy()
             assert (a == b).all(), (v, hint)
