@@ -427,6 +427,39 @@ struct NtSealSink {  // A/B variant 34: the trailer as non-temporal byte stores
 // before the trailer is written, so the write lands on a valid L2 line.
 struct SealTouchSink {};
 
+// Pricing variants 94 / 95 (trailer bytes go to a SHADOW image at the same offsets, so the image
+// itself stays intact): 94 writes the 4-B trailer, 95 the trailer's whole aligned 32-B sector
+// (zeros around it).  Same kernel, same reads; only the write granularity differs.
+struct ShadowSealSink {
+  intptr_t delta;  // shadow - image
+  bool sector;
+};
+
+template <>
+struct SinkOps<ShadowSealSink> {
+  __device__ static __forceinline__ uint32_t pre(const ShadowSealSink&, uint64_t, const BlkDesc&) { return 0u; }
+  __device__ static __forceinline__ void put(const ShadowSealSink& k, uint64_t, uint32_t raw, const BlkDesc& d,
+                                             uint32_t) {
+    if (d.init_raw == 0) return;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(d.p) + d.n + k.delta;
+    const uint32_t m = pdb_mask(~raw);
+    if (!k.sector) {
+      typedef __attribute__((address_space(1))) uint32_t g_u32u __attribute__((aligned(1)));
+      *reinterpret_cast<g_u32u*>(a) = m;
+      return;
+    }
+    typedef __attribute__((address_space(1))) u32x4 g_v4;
+    const uintptr_t s0 = a & ~static_cast<uintptr_t>(31);
+    const uint32_t o = static_cast<uint32_t>(a - s0), i0 = o >> 2, sh = (o & 3u) * 8u;
+    uint32_t x[8];
+#pragma unroll
+    for (uint32_t i = 0; i < 8; ++i) x[i] = i == i0 ? (m << sh) : ((i == i0 + 1 && sh) ? (m >> (32u - sh)) : 0u);
+    g_v4* w = reinterpret_cast<g_v4*>(s0);
+    w[0] = u32x4{x[0], x[1], x[2], x[3]};
+    w[1] = u32x4{x[4], x[5], x[6], x[7]};
+  }
+};
+
 // A/B variant 37: the trailer word as ONE (possibly unaligned) dword store instead of 4 byte stores.
 struct SealDwordSink {};
 
@@ -517,6 +550,22 @@ hipError_t launch_sst_variant(int v, const LaunchGeom& g, const uint32_t* d_tabl
     else
       hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstVerifySink, true, 8>), grid, block, 0, s, d_tables, src, n,
                          SstVerifySink{ok, nbad});
+    return hipGetLastError();
+  }
+  if ((v == 94 || v == 95) && seal) {  // pricing: 4-B vs 32-B-sector trailer writes into a shadow image
+    static std::mutex mu;
+    static uint8_t* shadow = nullptr;
+    static uint64_t shadow_n = 0;
+    std::lock_guard<std::mutex> lk(mu);
+    if (shadow_n < buf_len + 64) {
+      if (shadow) (void)hipFree(shadow);
+      shadow = nullptr;
+      shadow_n = 0;
+      if (hipMalloc(&shadow, buf_len + 64) != hipSuccess) return hipErrorOutOfMemory;
+      shadow_n = buf_len + 64;
+    }
+    const ShadowSealSink k{reinterpret_cast<intptr_t>(shadow) - reinterpret_cast<intptr_t>(buf), v == 95};
+    hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ShadowSealSink, true>), grid, block, 0, s, d_tables, src, n, k);
     return hipGetLastError();
   }
   if (v == 39 && seal) {  // full 32-B-sector rewrites around each trailer
