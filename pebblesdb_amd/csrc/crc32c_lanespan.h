@@ -41,6 +41,11 @@ constexpr uint32_t kSpanStageBase = 64u << 10;                    // tables and 
 // staging geometry per class: waves per CU and 1-KiB chunks per region (10 x 9 KiB for <= 256-B
 // records: 64 records of a 100-B-value log fit a region; 12 x 8 KiB for the longer classes, whose
 // items hold 8..21 records on 3..8 lanes each -- more waves hide more of the hash's latency)
+//
+// and the part geometry (see "items" below): chains A, B, C of kLC = 8 words and chain D of kLD
+// words, kPart = 3 kLC + kLD words per lane.  33-word parts (kLD = 9) for <= 256 B (a 131-B record
+// on one lane) and 513..1023 B (up to 8 lanes); 27-word parts (kLD = 3) for 257..512 B, where 4
+// lanes of 27 words cover a 431-B record exactly instead of 4 x 33 = 132 words for its 108.
 template <uint32_t MAXN>
 struct SpanStage {
   static constexpr uint32_t kWaves = MAXN <= 256u ? 10u : 12u;  // (13 x 7 KiB for 512: slower, 128-VGPR cap)
@@ -48,9 +53,14 @@ struct SpanStage {
   static constexpr uint32_t kRegion = kJ * 1024u;
   static constexpr uint32_t kUsable = kRegion - 16u;  // span limit: reads stay inside
   static_assert((64u << 10) + kWaves * kRegion <= PDB_LDS_BYTES, "fits the 160 KiB");
+  static constexpr uint32_t kLC = 8;                                // words of chains A, B, C (the 32-B folds)
+  static constexpr uint32_t kLD = MAXN > 256u && MAXN <= 512u ? 3u : 9u;  // words of chain D (not the head)
+  static constexpr uint32_t kPart = 3 * kLC + kLD;                  // odd: a record's k lanes on k banks
+  static constexpr uint32_t kNI = kLD > kLC ? kLD : kLC;            // lock-step steps of a part
+  static constexpr uint32_t kOpSet = kLD == 9u ? 0u : 3u;           // its part operators in the table source
 };
-// operator slots
-constexpr uint32_t kOp16 = 0, kOp32 = 1, kOp64 = 2, kOp256 = 3, kOp1024 = 4, kOp132 = 5, kOp264 = 6, kOp528 = 7;
+// operator slots: 5..7 shift by 1, 2 and 4 parts of the kernel's class
+constexpr uint32_t kOp16 = 0, kOp32 = 1, kOp64 = 2, kOp256 = 3, kOp1024 = 4, kOpP1 = 5, kOpP2 = 6, kOpP4 = 7;
 
 // shift(c, D) ^ y for the operator in slot `slot` (byte j of c indexes sub-table j)
 __device__ __forceinline__ uint32_t span_op_x(const char* lds, uint32_t slot, uint32_t c, uint32_t y) {
@@ -126,13 +136,15 @@ struct TabsS4 {
   }
 };
 
+template <uint32_t kOpSet>
 __device__ __forceinline__ void stage_ops_span(char* lds, const uint32_t* __restrict__ tabs) {
   // slot s, sub-table j, entry b at b<<8 | 128 | ((4s + j + b) & 31) << 2; sources: catalog
-  // entries 0 (16), 1 (32), 2 (64), 4 (256), 6 (1024), then the record operators (132, 264, 528)
+  // entries 0 (16), 1 (32), 2 (64), 4 (256), 6 (1024), then the class's part operators (132, 264,
+  // 528 or 108, 216, 432)
   for (uint32_t i = threadIdx.x; i < 8u * 1024u; i += blockDim.x) {
     const uint32_t slot = i >> 10, j = (i >> 8) & 3u, b = i & 255u;
     const uint32_t src = slot < 5u ? 1024u + (slot < 3u ? slot : (slot == 3u ? 4u : 6u)) * 1024u
-                                   : PDB_SPANOP_OFF + (slot - 5u) * 1024u;
+                                   : PDB_SPANOP_OFF + (slot - 5u + kOpSet) * 1024u;
     *reinterpret_cast<uint32_t*>(lds + ((b << 8) | 128u | (((b + 4u * slot + j) & 31u) << 2))) = tabs[src + j * 256u + b];
   }
 }
@@ -204,24 +216,23 @@ __device__ __forceinline__ uint32_t span_slow_record(const char* lds, const type
 // A batch is 64 consecutive records (lane r of the batch registers: record 64 * batch + r).  Its
 // in-class records are hashed by items: runs of up to G = floor(64 / k) consecutive records, each
 // record on k consecutive lanes (lane u: record slot u / k, part c = u % k).  Counted from the
-// record's END, part c covers 33 words (132 B) ending 132 c bytes before the end, as four chains:
-// A its last 8 words, B and C the 8 before each, D the 9 before those; part k - 1's chain D (the
-// head) also runs on to the record's start.  Parts of 33 words put the k lanes of a record on k
-// different LDS banks at every step (128-B parts would put them all on one).  All chains of an item
-// run in lock step for `iters` = max(9, nw - 33 (k - 1) - 24) steps: the head chain alone for the
-// first iters - 9, then D for 9 and A, B, C for the last 8.  Folds: per lane P = shift(shift(D, 32)
-// ^ C, 64) ^ shift(B, 32) ^ A, then across the k lanes of a record shift(P[c + m], 132 m) ^ P[c]
-// for m = 1, 2, 4.  k per batch minimises steps per record for its longest in-class record.
+// record's END, part c covers P = kPart words ending 4 P c bytes before the end, as four chains:
+// A its last LC = 8 words, B and C the 8 before each, D the LD before those; part k - 1's chain D
+// (the head) also runs on to the record's start.  Odd parts put the k lanes of a record on k
+// different LDS banks at every step (128-B parts would put them all on one).  The chains of an
+// item run in lock step: the head chain alone for lim = max(0, nw - P (k - 1) - 3 LC - LD) steps,
+// then NI = max(LC, LD) steps in which chain X works from step NI - len(X) on (the first word of A,
+// B, C is just loaded: their states start at 0).  Folds: per lane Q = shift(shift(D, 32) ^ C, 64)
+// ^ shift(B, 32) ^ A (D ends where C starts, whatever its length), then across the k lanes of a
+// record shift(Q[c + m], 4 P m) ^ Q[c] for m = 1, 2, 4.  k per batch minimises steps per batch for
+// its longest in-class record.
 constexpr uint32_t kNoRec = 0x3FFFFFFFu;
-constexpr uint32_t kSpanLC = 8;                      // words of chains A, B, C: 32 B, the slot-3 fold
-constexpr uint32_t kSpanLD = 9;                      // words of chain D (not the head)
-constexpr uint32_t kSpanPart = 3 * kSpanLC + kSpanLD;  // words per part
 
 struct LaneSpanGeom {
   uint32_t k;      // lanes per record
   uint32_t g;      // records per item: floor(64 / k)
   uint32_t magic;  // ceil(65536 / k): u / k = (u * magic) >> 16 for u < 64
-  uint32_t iters;  // chain steps per item: max(9, nw - 33 (k - 1) - 24)
+  uint32_t iters;  // lock-step steps per item: lim + NI
 };
 
 // max over the wave of a 32-bit value; every lane must be active
@@ -238,19 +249,19 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 // k for a batch whose longest in-class record has nw words: the fewest chain steps per batch,
 // items per batch x steps per item, with the records an item can hold: G = floor(64 / k), and
 // what fits a staging region at ~4 nw + 8 bytes a record
-template <uint32_t KMAX, uint32_t kUsable>
+template <uint32_t KMAX, class ST>
 __device__ __forceinline__ LaneSpanGeom span_pick(uint32_t nw) {
-  const float fit = static_cast<float>(kUsable) * __builtin_amdgcn_rcpf(static_cast<float>(4u * nw + 8u));
+  const float fit = static_cast<float>(ST::kUsable) * __builtin_amdgcn_rcpf(static_cast<float>(4u * nw + 8u));
   uint32_t gfit = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(fit)));
   gfit = gfit ? gfit : 1u;
-  LaneSpanGeom best{1u, 64u, 65536u, kSpanLD};
+  LaneSpanGeom best{1u, 64u, 65536u, ST::kNI};
   uint32_t best_cost = ~0u;
 #pragma unroll
   for (uint32_t k = 1; k <= KMAX; ++k) {
     const uint32_t g = 64u / k;
     const uint32_t geff = g < gfit ? g : gfit;
-    const int32_t h = static_cast<int32_t>(nw) - static_cast<int32_t>((k - 1u) * kSpanPart + 3u * kSpanLC);
-    const uint32_t it = h > static_cast<int32_t>(kSpanLD) ? static_cast<uint32_t>(h) : kSpanLD;
+    const int32_t h = static_cast<int32_t>(nw) - static_cast<int32_t>((k - 1u) * ST::kPart + 3u * ST::kLC + ST::kLD);
+    const uint32_t it = ST::kNI + (h > 0 ? static_cast<uint32_t>(h) : 0u);  // lim + NI
     const uint32_t items = (64u + geff - 1u) / geff;
     if (items * it < best_cost) {
       best = LaneSpanGeom{k, g, (65536u + k - 1u) / k, it};
@@ -278,13 +289,15 @@ __global__ __launch_bounds__(SpanStage<MAXN>::kWaves * 64) void crc_lanespan_ker
                                                                        uint64_t nblk, Sink sink) {
   constexpr uint32_t kSpanWaves = SpanStage<MAXN>::kWaves, kSpanJ = SpanStage<MAXN>::kJ;
   constexpr uint32_t kSpanRegion = SpanStage<MAXN>::kRegion, kSpanUsable = SpanStage<MAXN>::kUsable;
+  typedef SpanStage<MAXN> ST;
+  constexpr uint32_t LC = ST::kLC, LD = ST::kLD, NI = ST::kNI, PART = ST::kPart;
   static_assert(MAXN + 32u <= kSpanUsable, "a record of the class must fit a region");
-  constexpr uint32_t KMAX = (MAXN / 4u + kSpanPart) / kSpanPart;  // k parts of 33 words cover MAXN: 2, 4, 8
+  constexpr uint32_t KMAX = (MAXN / 4u + PART) / PART;  // k parts cover MAXN: 2, 5, 8
   static_assert(KMAX >= 1 && KMAX <= 8, "tree folds for up to 8 lanes per record");
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
   char* lds = reinterpret_cast<char*>(lds_words);
   TP::stage(lds, tabs);
-  stage_ops_span(lds, tabs);
+  stage_ops_span<ST::kOpSet>(lds, tabs);
   const uint32_t u = threadIdx.x & 63u;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t ureg = tabs[PDB_UNSHIFT_OFF + (u & 15u)];
@@ -314,7 +327,7 @@ __global__ __launch_bounds__(SpanStage<MAXN>::kWaves * 64) void crc_lanespan_ker
   uint64_t bfastm = 0;   // in-class records
   uint64_t bbroken = 0;  // bit r: records r and r + 1 may not share an item
   uint32_t bcursor = 64;
-  LaneSpanGeom bg{1u, 64u, 65536u, kSpanLD};
+  LaneSpanGeom bg{1u, 64u, 65536u, NI};
 
   // make the prefetched batch current; records outside the class are hashed here by the whole
   // wave (rare: their loads wait behind the items in flight)
@@ -351,7 +364,7 @@ __global__ __launch_bounds__(SpanStage<MAXN>::kWaves * 64) void crc_lanespan_ker
     const bool link_ok = bfast && fn && pn >= bp && pn <= bp + bn + 64u;
     bbroken = __builtin_amdgcn_ballot_w64(!link_ok && u < 63u);
     const uint32_t nw = wave_max_u32(bfast ? (bn + 3u) >> 2 : 0u);
-    bg = span_pick<KMAX, kSpanUsable>(nw ? nw : 1u);
+    bg = span_pick<KMAX, ST>(nw ? nw : 1u);
     bcursor = 0;
     return true;
   };
@@ -446,7 +459,10 @@ __global__ __launch_bounds__(SpanStage<MAXN>::kWaves * 64) void crc_lanespan_ker
   // hash an item staged in the region
   auto hash = [&](const SpanItem& it) {
     if (it.hi == 0 || MODE == 1 || MODE == 3) return;
-    const uint32_t k = it.k, iters = it.iters, lim = iters - kSpanLD;
+    // chain X (A, B, C, D = 0..3) works from phase-2 step F[X] on; its word at step t is the one
+    // ending 4 (NI - t) bytes before the chain's end
+    constexpr int32_t FABC = static_cast<int32_t>(NI - LC), FD = static_cast<int32_t>(NI - LD);
+    const uint32_t k = it.k, lim = it.iters - NI;
     const int32_t e = static_cast<int32_t>(it.e_loc);
     const int32_t pl = static_cast<int32_t>(it.p_loc);
     const bool act = it.p_loc != kNoRec;
@@ -456,35 +472,32 @@ __global__ __launch_bounds__(SpanStage<MAXN>::kWaves * 64) void crc_lanespan_ker
     const uint32_t uz = __shfl(ureg, zp, 64);
     // The word at byte s (s = e mod 4) is the dword pair (D[s >> 2], D[(s >> 2) + 1]) through sel.
     // The p-word (at sp), masked below p with U[z] injected, replaces its chain's state at its
-    // step; a chain wholly before p yields 0.  Chain X (A, B, C, D = 0..3) ends at eA - 32 X and
-    // holds at global step t the word at its end - 4 (iters - t).
-    const int32_t eA = e - static_cast<int32_t>(4u * kSpanPart * it.c);
+    // step; a chain wholly before p yields 0.
+    const int32_t eA = e - static_cast<int32_t>(4u * PART * it.c);
     const int32_t sp = act ? pl - static_cast<int32_t>(zp) : e;  // (no record: an address in range)
     uint32_t pw;
     {
       const char* q = region + 4 * (sp >> 2);
       pw = (__builtin_amdgcn_perm(lds_u32(q, 4), lds_u32(q, 0), sel) & (0xFFFFFFFFu << (8u * zp))) ^ uz;
     }
-    // the p-word's step in chain A's numbering, then T + 8 X in chain X's, in phase-2 steps
-    const int32_t T = static_cast<int32_t>(iters) - ((eA - sp) >> 2) - static_cast<int32_t>(lim);
+    // the p-word's phase-2 step in chain A's numbering; T + LC X in chain X's
+    const int32_t T = static_cast<int32_t>(NI) - ((eA - sp) >> 2);
     // the last phase-2 step at which some lane of the item replaces a state (uniform; one bound for
     // all four chains: per-chain masks cost more in branches than their selects save)
     int32_t lmax = -1;
 #pragma unroll
     for (int32_t X = 0; X < 4; ++X) {
-      const int32_t t = T + 8 * X;
-      if (t >= (X == 3 ? 0 : 1) && t < static_cast<int32_t>(kSpanLD)) lmax = t;
+      const int32_t t = T + static_cast<int32_t>(LC) * X;
+      if (t >= (X == 3 ? FD : FABC) && t < static_cast<int32_t>(NI)) lmax = t;
     }
     const int32_t G = static_cast<int32_t>(wave_max_u32(act ? static_cast<uint32_t>(lmax + 1) : 0u)) - 1;
-    // chain base pointers: word at phase-2 step t is (q[t], q[t + 1])
-    const char* q0 = region + 4 * ((eA - 36) >> 2);  // below the region for short records: unused
-    const char* q1 = q0 - 32;
-    const char* q2 = q0 - 64;
-    const char* q3 = q0 - 96;
+    // base of the chains' words: chain X's dword i at q3 + 4 LC (3 - X) + 4 i (word at phase-2
+    // step t = dwords t, t + 1); below the region for short records (words never used)
+    const char* q3 = region + 4 * ((eA - static_cast<int32_t>(4u * NI + 12u * LC)) >> 2);
     uint32_t xd = 0, ld;
     if (lim > 0) {  // the head chain alone (junk on the other lanes, dropped)
-      const int32_t tD = T + 24 + static_cast<int32_t>(lim);  // global step of the p-word in D
-      const char* q = q3 - 4 * static_cast<int32_t>(lim);
+      const int32_t tD = T + static_cast<int32_t>(3u * LC + lim) - FD;  // the p-word's step in it
+      const char* q = q3 + 4 * (FD - static_cast<int32_t>(lim));
       ld = lds_u32(q, 0);
       for (int32_t t = 0; t < static_cast<int32_t>(lim); ++t, q += 4) {
         const uint32_t h = lds_u32(q, 4);
@@ -494,65 +507,76 @@ __global__ __launch_bounds__(SpanStage<MAXN>::kWaves * 64) void crc_lanespan_ker
       }
       xd = head ? xd : 0u;
     } else {
-      ld = lds_u32(q3, 0);
+      ld = lds_u32(q3, 4u * FD);
     }
-    {
-      const uint32_t h = lds_u32(q3, 4);
-      const uint32_t w = __builtin_amdgcn_perm(h, ld, sel);
-      ld = h;
-      xd = TP::step(lds, lt, xd, w);
-      if (G >= 0) xd = T + 24 == 0 ? pw : xd;
-    }
-    uint32_t la = lds_u32(q0, 4), lb = lds_u32(q1, 4), lc = lds_u32(q2, 4);
     uint32_t xa = 0, xb = 0, xc = 0;
+    uint32_t la = lds_u32(q3, 12u * LC + 4u * FABC), lb = lds_u32(q3, 8u * LC + 4u * FABC);
+    uint32_t lc = lds_u32(q3, 4u * LC + 4u * FABC);
 #pragma unroll
-    for (int32_t t = 1; t < static_cast<int32_t>(kSpanLD); ++t) {
-      // one base, immediate offsets (q0..q2 are q3 + 96, 64, 32)
-      const uint32_t ha = lds_u32(q3, 96u + 4u * (t + 1)), hb = lds_u32(q3, 64u + 4u * (t + 1));
-      const uint32_t hc = lds_u32(q3, 32u + 4u * (t + 1)), hd = lds_u32(q3, 4u * (t + 1));
-      const uint32_t wa = __builtin_amdgcn_perm(ha, la, sel), wb = __builtin_amdgcn_perm(hb, lb, sel);
-      const uint32_t wc = __builtin_amdgcn_perm(hc, lc, sel), wd = __builtin_amdgcn_perm(hd, ld, sel);
-      la = ha, lb = hb, lc = hc, ld = hd;
-      if (t == 1) {
+    for (int32_t t = 0; t < static_cast<int32_t>(NI); ++t) {
+      const bool abc = t >= FABC, dd = t >= FD;  // compile time
+      uint32_t wa = 0, wb = 0, wc = 0, wd = 0;
+      if (abc) {
+        const uint32_t ha = lds_u32(q3, 12u * LC + 4u * (t + 1)), hb = lds_u32(q3, 8u * LC + 4u * (t + 1));
+        const uint32_t hc = lds_u32(q3, 4u * LC + 4u * (t + 1));
+        wa = __builtin_amdgcn_perm(ha, la, sel), wb = __builtin_amdgcn_perm(hb, lb, sel);
+        wc = __builtin_amdgcn_perm(hc, lc, sel);
+        la = ha, lb = hb, lc = hc;
+      }
+      if (dd) {
+        const uint32_t hd = lds_u32(q3, 4u * (t + 1));
+        wd = __builtin_amdgcn_perm(hd, ld, sel);
+        ld = hd;
+      }
+      if (abc && t == FABC) {  // the first word: the state is 0
         xa = wa, xb = wb, xc = wc;
-        xd = TP::step(lds, lt, xd, wd);
-      } else {
+        if (dd) xd = TP::step(lds, lt, xd, wd);
+      } else if (abc && dd) {
         uint32_t x4[4] = {xa, xb, xc, xd};
         const uint32_t w4[4] = {wa, wb, wc, wd};
         TP::step4(lds, lt, x4, w4);
         xa = x4[0], xb = x4[1], xc = x4[2], xd = x4[3];
+      } else if (abc) {
+        xa = TP::step(lds, lt, xa, wa);
+        xb = TP::step(lds, lt, xb, wb);
+        xc = TP::step(lds, lt, xc, wc);
+      } else if (dd) {
+        xd = TP::step(lds, lt, xd, wd);
       }
       if (t <= G) {
-        xa = T == t ? pw : xa;
-        xb = T + 8 == t ? pw : xb;
-        xc = T + 16 == t ? pw : xc;
-        xd = T + 24 == t ? pw : xd;
+        if (abc) {
+          xa = T == t ? pw : xa;
+          xb = T + static_cast<int32_t>(LC) == t ? pw : xb;
+          xc = T + static_cast<int32_t>(2u * LC) == t ? pw : xc;
+        }
+        if (dd) xd = T + static_cast<int32_t>(3u * LC) == t ? pw : xd;
       }
     }
     // finish; a chain whose end is at or before the p-word's start holds no byte of the record
-    const int32_t L = static_cast<int32_t>(kSpanLD);
+    const int32_t L = static_cast<int32_t>(NI);
     uint32_t x4[4] = {xa, xb, xc, xd};
     const uint32_t z4[4] = {0u, 0u, 0u, 0u};
     TP::step4(lds, lt, x4, z4);
     const uint32_t ca = T < L ? x4[0] : 0u;
-    const uint32_t cb = T + 8 < L ? x4[1] : 0u;
-    const uint32_t cc = T + 16 < L ? x4[2] : 0u;
-    const uint32_t cd = T + 24 < L ? x4[3] : 0u;
+    const uint32_t cb = T + static_cast<int32_t>(LC) < L ? x4[1] : 0u;
+    const uint32_t cc = T + static_cast<int32_t>(2u * LC) < L ? x4[2] : 0u;
+    const uint32_t cd = T + static_cast<int32_t>(3u * LC) < L ? x4[3] : 0u;
+    static_assert(LC == 8, "the in-part folds use the 32- and 64-B operators");
     const uint32_t lo2 = span_op_x(lds, kOp32, cb, ca);  // shift(B, 32) ^ A
     const uint32_t hi2 = span_op_x(lds, kOp32, cd, cc);  // shift(D, 32) ^ C
     uint32_t P = span_op_x(lds, kOp64, hi2, lo2);        // shift(hi2, 64) ^ lo2
-    // parts c + m: the 132 m bytes before
+    // parts c + m: the 4 PART m bytes before
     if (k > 1u) {
       const uint32_t y = __shfl_down(P, 1, 64);
-      if ((it.c & 1u) == 0 && it.c + 1u < k) P = span_op_x(lds, kOp132, y, P);
+      if ((it.c & 1u) == 0 && it.c + 1u < k) P = span_op_x(lds, kOpP1, y, P);
     }
     if (k > 2u) {
       const uint32_t y = __shfl_down(P, 2, 64);
-      if ((it.c & 3u) == 0 && it.c + 2u < k) P = span_op_x(lds, kOp264, y, P);
+      if ((it.c & 3u) == 0 && it.c + 2u < k) P = span_op_x(lds, kOpP2, y, P);
     }
     if (k > 4u) {
       const uint32_t y = __shfl_down(P, 4, 64);
-      if ((it.c & 7u) == 0 && it.c + 4u < k) P = span_op_x(lds, kOp528, y, P);
+      if ((it.c & 7u) == 0 && it.c + 4u < k) P = span_op_x(lds, kOpP4, y, P);
     }
     if (it.c == 0 && act)
       SinkOps<Sink>::put(sink, (it.batch << 6) + it.r, P, BlkDesc{nullptr, 0u, 0xFFFFFFFFu}, it.pre);
