@@ -438,17 +438,20 @@ __global__ __launch_bounds__(SpanStage<MAXN>::kWaves * 64) void crc_lanespan_ker
     return it;
   };
 
-  // loads of one item: kSpanJ unconditional 16-B loads (1 KiB contiguous per instruction) from the
-  // item's uniform base; chunks wholly past its last byte re-read its last chunk (an empty item
-  // reads the tables' first 16 B)
+  // loads of one item: kSpanJ unconditional 16-B buffer loads (1 KiB contiguous per instruction,
+  // non-temporal) from the item's uniform base, the descriptor's range check ending at its last
+  // 16-B chunk: chunks past it read as zeros without touching memory (an empty item reads the
+  // tables' first 16 B).  32-bit lane offsets, no per-chunk address arithmetic.
   auto issue = [&](u32x4 (&A)[kSpanJ], const SpanItem& it) {
-    const uint32_t last = it.hi ? (it.hi - 1u) & ~15u : 0u;
-    const uint8_t* base = reinterpret_cast<const uint8_t*>(it.lo);
+    const uint32_t lo_l = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(it.lo));
+    const uint32_t lo_h = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(static_cast<uint64_t>(it.lo) >> 32));
+    const uint32_t nb = MODE >= 2 ? 16u : __builtin_amdgcn_readfirstlane(it.hi ? (it.hi + 15u) & ~15u : 16u);
+    void* base = reinterpret_cast<void*>((static_cast<uint64_t>(lo_h) << 32) | lo_l);
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(base, 0, static_cast<int>(nb), 0x00020000);
 #pragma unroll
-    for (uint32_t j = 0; j < kSpanJ; ++j) {
-      const uint32_t off = 1024u * j + 16u * u;
-      A[j] = gload128<true>(reinterpret_cast<uintptr_t>(base + (MODE >= 2 ? 0u : (off < last ? off : last))));
-    }
+    for (uint32_t j = 0; j < kSpanJ; ++j)
+      A[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, static_cast<int>(1024u * j + 16u * u), 0,
+                                                                              2 /* nt */));
   };
   // every chunk is written, the dummy ones too: a load whose register is never read stays
   // outstanding, and the compiler then drains the counter before the register is reloaded
