@@ -17,9 +17,11 @@
 //                                & 3) reads table (q + i) & 3, replica lane & 7: the four quarters
 //                                of each 32-lane group read four tables in four disjoint bank
 //                                ranges, every lookup bank-conflict free on 32 KiB of tables.
-//                    [128, 256)  8 shift operators (16, 32, 64, 256, 1024, 132, 264, 528 B), one
-//                                copy, sub-table j of operator s at dword 32 + ((4 s + j + b) & 31):
-//                                rotated by b so a lookup's lanes spread over the banks.
+//                    [128, 256)  8 shift operators (16, 32, 64, 256, 1024 and the class's three
+//                                part operators), one copy, sub-table j of operator s at dword
+//                                32 + (((b >> 2) ^ (4 s + j)) & 31): scrambled by b so a lookup's
+//                                lanes spread over the banks, and the address is one v_perm
+//                                ([b, b, 0, 0]) and one v_bitop3 ((x & 0xFF7C) ^ const) away.
 //   [64, 154 KiB)    10 x 9 KiB: one staging region per wave (64 records of a 100-B-value log, 138 B
 //                    each with their headers, fit one)
 // A wave handles batches of 64 consecutive records; their records are hashed by items (runs of
@@ -67,8 +69,8 @@ __device__ __forceinline__ uint32_t span_op_x(const char* lds, uint32_t slot, ui
   uint32_t v[4];
 #pragma unroll
   for (uint32_t j = 0; j < 4; ++j) {
-    const uint32_t bj = (c >> (8u * j)) & 0xffu;
-    v[j] = lds_u32(lds, (bj << 8) | 128u | (((bj + 4u * slot + j) & 31u) << 2));
+    const uint32_t bb = __builtin_amdgcn_perm(0u, c, 0x0C0C0000u | (j << 8) | j);  // [b_j, b_j, 0, 0]
+    v[j] = lds_u32(lds, (bb & 0xFF7Cu) ^ (128u | ((4u * slot + j) << 2)));
   }
   return xor3(xor3(v[0], v[1], v[2]), v[3], y);
 }
@@ -138,14 +140,14 @@ struct TabsS4 {
 
 template <uint32_t kOpSet>
 __device__ __forceinline__ void stage_ops_span(char* lds, const uint32_t* __restrict__ tabs) {
-  // slot s, sub-table j, entry b at b<<8 | 128 | ((4s + j + b) & 31) << 2; sources: catalog
+  // slot s, sub-table j, entry b at b<<8 | 128 | (((b >> 2) ^ (4s + j)) & 31) << 2; sources: catalog
   // entries 0 (16), 1 (32), 2 (64), 4 (256), 6 (1024), then the class's part operators (132, 264,
   // 528 or 108, 216, 432)
   for (uint32_t i = threadIdx.x; i < 8u * 1024u; i += blockDim.x) {
     const uint32_t slot = i >> 10, j = (i >> 8) & 3u, b = i & 255u;
     const uint32_t src = slot < 5u ? 1024u + (slot < 3u ? slot : (slot == 3u ? 4u : 6u)) * 1024u
                                    : PDB_SPANOP_OFF + (slot - 5u + kOpSet) * 1024u;
-    *reinterpret_cast<uint32_t*>(lds + ((b << 8) | 128u | (((b + 4u * slot + j) & 31u) << 2))) = tabs[src + j * 256u + b];
+    *reinterpret_cast<uint32_t*>(lds + ((b << 8) | 128u | ((((b >> 2) ^ (4u * slot + j)) & 31u) << 2))) = tabs[src + j * 256u + b];
   }
 }
 
