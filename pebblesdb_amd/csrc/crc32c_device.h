@@ -99,6 +99,14 @@ __device__ __forceinline__ uint32_t shift_op_x(const char* lds, uint32_t op, uin
   return xor3(xor3(v0, v1, v2), v3, y);
 }
 
+// Tree-level operators for the packed / row trees: level l = shift(16 << l) from the single-copy
+// slots 0..5 (QuadTree below replaces levels 0 and 1 with replicated, conflict-free copies)
+struct SlotTree {
+  __device__ __forceinline__ uint32_t op(const char* lds, uint32_t l, uint32_t c, uint32_t y) const {
+    return shift_op_x(lds, l, c, y);
+  }
+};
+
 // Same fold with the partner values moved by DPP (levels 0-3, row_shl), ds_swizzle (level 4,
 // xor 16 within 32-lane halves) and readlane (level 5): one LDS round trip fewer per level
 // than ds_bpermute.  Result valid in lane 0.
@@ -231,22 +239,22 @@ __device__ __forceinline__ void load4k(u32x4 (&v)[4], const uint8_t* base, uint6
 __device__ __forceinline__ uint32_t sel(bool c, uint32_t a, uint32_t b) { return c ? a : b; }
 
 // Returns block (lane & 3)'s raw state in lanes 0..3.
-template <bool kL5Twice = false>
+template <bool kL5Twice = false, class TO = SlotTree>
 __device__ __forceinline__ uint32_t tree4_packed(const char* lds, uint32_t u, uint32_t p0, uint32_t p1,
-                                                 uint32_t p2, uint32_t p3) {
+                                                 uint32_t p2, uint32_t p3, const TO& to = TO{}) {
   const bool odd = u & 1u;
   // level 0 (shift 32): even lane 2m -> block 0/2 pair m, odd lane 2m+1 -> block 1/3 pair m
   const uint32_t p0n = __builtin_amdgcn_update_dpp(0u, p0, 0x101, 0xF, 0xF, false);  // p0[L+1]
   const uint32_t p1p = __builtin_amdgcn_update_dpp(0u, p1, 0x111, 0xF, 0xF, false);  // p1[L-1]
-  const uint32_t r0 = shift_op_x(lds, 0, sel(odd, p1p, p0), sel(odd, p1, p0n));
+  const uint32_t r0 = to.op(lds, 0, sel(odd, p1p, p0), sel(odd, p1, p0n));
   const uint32_t p2n = __builtin_amdgcn_update_dpp(0u, p2, 0x101, 0xF, 0xF, false);
   const uint32_t p3p = __builtin_amdgcn_update_dpp(0u, p3, 0x111, 0xF, 0xF, false);
-  const uint32_t r1 = shift_op_x(lds, 0, sel(odd, p3p, p2), sel(odd, p3, p2n));
+  const uint32_t r1 = to.op(lds, 0, sel(odd, p3p, p2), sel(odd, p3, p2n));
   // level 1 (shift 64): lane 4j+r -> block r pair j.  r<2 reads r0 at L, L+2; r>=2 reads r1 at L-2, L
   const bool hi = u & 2u;
   const uint32_t r0n = __builtin_amdgcn_update_dpp(0u, r0, 0x102, 0xF, 0xF, false);  // r0[L+2]
   const uint32_t r1p = __builtin_amdgcn_update_dpp(0u, r1, 0x112, 0xF, 0xF, false);  // r1[L-2]
-  uint32_t v = shift_op_x(lds, 1, sel(hi, r1p, r0), sel(hi, r1, r0n));
+  uint32_t v = to.op(lds, 1, sel(hi, r1p, r0), sel(hi, r1, r0n));
   // levels 2..5: lane 4j+r holds block r; pair (L, L + 4*2^(k-2))
   uint32_t y = __builtin_amdgcn_update_dpp(0u, v, 0x104, 0xF, 0xF, false);  // row_shl:4
   if ((u & 4u) == 0) v = shift_op_x(lds, 2, v, y);
@@ -269,21 +277,22 @@ __device__ __forceinline__ uint32_t tree4_packed(const char* lds, uint32_t u, ui
 // level 2 interleaves the two halves so that lane 8j + b holds block b (1 op), levels 3..5 once
 // for all 8 blocks: 10 shift operations per 8 blocks instead of 14.  Block b's raw state ends in
 // lane b (b = 0..7).
-__device__ __forceinline__ uint32_t tree8_packed(const char* lds, uint32_t u, const uint32_t (&p)[8]) {
+template <class TO = SlotTree>
+__device__ __forceinline__ uint32_t tree8_packed(const char* lds, uint32_t u, const uint32_t (&p)[8], const TO& to = TO{}) {
   const bool odd = u & 1u, hi = u & 2u, h4 = u & 4u;
   uint32_t r[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {  // level 0 (shift 16): even lane 2m -> block 2k pair m, odd -> 2k+1
     const uint32_t pn = __builtin_amdgcn_update_dpp(0u, p[2 * k], 0x101, 0xF, 0xF, false);      // p[2k][L+1]
     const uint32_t pp = __builtin_amdgcn_update_dpp(0u, p[2 * k + 1], 0x111, 0xF, 0xF, false);  // p[2k+1][L-1]
-    r[k] = shift_op_x(lds, 0, sel(odd, pp, p[2 * k]), sel(odd, p[2 * k + 1], pn));
+    r[k] = to.op(lds, 0, sel(odd, pp, p[2 * k]), sel(odd, p[2 * k + 1], pn));
   }
   uint32_t v[2];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {  // level 1 (shift 32): lane 4j + q -> block 4h + q, quad j
     const uint32_t rn = __builtin_amdgcn_update_dpp(0u, r[2 * h], 0x102, 0xF, 0xF, false);      // [L+2]
     const uint32_t rp = __builtin_amdgcn_update_dpp(0u, r[2 * h + 1], 0x112, 0xF, 0xF, false);  // [L-2]
-    v[h] = shift_op_x(lds, 1, sel(hi, rp, r[2 * h]), sel(hi, r[2 * h + 1], rn));
+    v[h] = to.op(lds, 1, sel(hi, rp, r[2 * h]), sel(hi, r[2 * h + 1], rn));
   }
   // level 2 (shift 64): lane 8j + q (q < 4) from v0 at L, L+4; lane 8j + 4 + q from v1 at L-4, L
   const uint32_t vn = __builtin_amdgcn_update_dpp(0u, v[0], 0x104, 0xF, 0xF, false);  // v0[L+4]
@@ -401,6 +410,20 @@ __device__ __forceinline__ uint32_t stepk(const char* lds, const QuadTabs& qt, u
   return xor3(T(2, 0), T(1, 1), T(0, 2)) ^ (x >> 24);
 }
 
+// Tree levels 0 and 1 (shift 16 / 32, the levels every lane works in) from replicated copies in
+// image 1 at byte offset kOff0 / kOff1 of an entry block (-1: the single-copy slot)
+template <int kOff0, int kOff1>
+struct QuadTree {
+  const QuadTabs& qt;
+  __device__ __forceinline__ uint32_t op(const char* lds, uint32_t l, uint32_t c, uint32_t y) const {
+    if constexpr (kOff0 >= 0)
+      if (l == 0) return op_q<static_cast<uint32_t>(kOff0)>(lds, qt.g, qt.s, c, y);
+    if constexpr (kOff1 >= 0)
+      if (l == 1) return op_q<static_cast<uint32_t>(kOff1)>(lds, qt.g, qt.s, c, y);
+    return shift_op_x(lds, l, c, y);
+  }
+};
+
 // shift(c, 1024) ^ y: the Horner fold of 16-B pieces 1 KiB apart, on either image
 __device__ __forceinline__ uint32_t horner1024(const char* lds, const LaneTabs&, uint32_t c, uint32_t y) {
   return shift_op_x(lds, PDB_SLOT_HORNER, c, y);
@@ -416,15 +439,18 @@ __device__ __forceinline__ uint32_t round1008(const char* lds, const QuadTabs& q
   return op_q<0u>(lds, qt.g, qt.s, c, 0u);
 }
 
-// Stage image 0, image 1 (catalog operator kImg1: shift 2048 for crc_pack4k_kernel, 1008 for the
-// stream kernel's round chaining; -1: none) and the tree operators (catalog kTree .. kTree + 5 ->
-// slots 0..5), all of a thread's loads issued before its stores (launch latency matters for small
-// batches).
-template <int kTree, int kImg1>
+// Stage image 0, image 1 (catalog operators kImg1Lo in dwords 0..31 and kImg1Hi in 32..63 of its
+// entry blocks: shift 2048 / 1008 for the Horner folds of crc_pack4k_kernel / the stream kernel,
+// the tree's level-0 / level-1 operators; -1: none) and the tree operators (catalog kTree ..
+// kTree + 5 -> slots 0..5), all of a thread's loads issued before its stores (launch latency
+// matters for small batches).
+template <int kTree, int kImg1Lo, int kImg1Hi = -1>
 __device__ __forceinline__ void stage_tables_q4(char* lds, const uint32_t* __restrict__ tabs) {
-  // 16-B quads: q < kRep = replicated quads (part q >> 11: T, shift 1024, image 1; entry b, table
-  // slot k, replicas 4h..4h+3), then 1536 single-copy tree-operator quads
-  constexpr uint32_t kRep = (kImg1 >= 0 ? 3u : 2u) * 2048u, kAll = kRep + 6u * 256u;
+  // 16-B quads: q < kRep = replicated quads (part q >> 11: T, shift 1024, image 1 lo, image 1 hi,
+  // the absent ones skipped; entry b, table slot k, replicas 4h..4h+3), then 1536 single-copy
+  // tree-operator quads
+  static_assert(kImg1Lo >= 0 || kImg1Hi < 0, "image 1 fills its low half first");
+  constexpr uint32_t kRep = (2u + (kImg1Lo >= 0 ? 1u : 0u) + (kImg1Hi >= 0 ? 1u : 0u)) * 2048u, kAll = kRep + 6u * 256u;
   const u32x4* cat = reinterpret_cast<const u32x4*>(tabs + 1024);
   for (uint32_t i0 = 0; i0 < kAll; i0 += 8u * blockDim.x) {
     u32x4 v[8];
@@ -434,9 +460,8 @@ __device__ __forceinline__ void stage_tables_q4(char* lds, const uint32_t* __res
       if (i < kRep) {
         const uint32_t part = i >> 11, b = (i >> 3) & 255u, k = (i >> 1) & 3u;
         // T_k, or operator sub-table 3 - k (tabs: T0..T3, then the catalog's 4 x 256 per operator)
-        const uint32_t src = part == 0 ? k * 256u + b
-                                       : 1024u + (part == 1 ? PDB_CAT_S1024 : static_cast<uint32_t>(kImg1)) * 1024u +
-                                             (3u - k) * 256u + b;
+        const uint32_t cat_id = part == 1 ? PDB_CAT_S1024 : (part == 2 ? static_cast<uint32_t>(kImg1Lo) : static_cast<uint32_t>(kImg1Hi));
+        const uint32_t src = part == 0 ? k * 256u + b : 1024u + cat_id * 1024u + (3u - k) * 256u + b;
         const uint32_t x = tabs[src];
         v[j] = u32x4{x, x, x, x};
       } else {
@@ -449,7 +474,7 @@ __device__ __forceinline__ void stage_tables_q4(char* lds, const uint32_t* __res
       const uint32_t i = i0 + threadIdx.x + j * blockDim.x;
       if (i < kRep) {
         const uint32_t part = i >> 11, b = (i >> 3) & 255u, k = (i >> 1) & 3u, h = i & 1u;
-        const uint32_t addr = (part == 2 ? 0x10000u : 0u) | (b << 8) | (part == 1 ? 128u : 0u) | (k << 5) | (h << 4);
+        const uint32_t addr = (part >= 2 ? 0x10000u : 0u) | (b << 8) | ((part & 1u) ? 128u : 0u) | (k << 5) | (h << 4);
         *reinterpret_cast<u32x4*>(lds + addr) = v[j];
       } else if (i < kAll) {
         *reinterpret_cast<u32x4*>(lds + PDB_MAIN_BYTES + (i - kRep) * 16u) = v[j];
@@ -498,7 +523,7 @@ __global__ __launch_bounds__(kThreads) void crc_pack4k_kernel(
   const uint64_t w = wg_first + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   u32x4 buf[4];
   load4k<4, true>(buf, base, stride, w < nblk ? w : nblk - 1, u);  // overlaps the table staging
-  stage_tables_q4<PDB_CAT_TREE16, PDB_CAT_S2048>(lds, tabs);
+  stage_tables_q4<PDB_CAT_TREE16, PDB_CAT_S2048, PDB_CAT_TREE16>(lds, tabs);  // image 1 hi: tree level 0
   __syncthreads();
   if (wg_first >= nblk) return;  // workgroup-uniform: every wave of a live workgroup reaches each barrier
   const QuadTabs qt = quad_tabs(u);
@@ -517,7 +542,7 @@ __global__ __launch_bounds__(kThreads) void crc_pack4k_kernel(
       if (bn < nblk) load4k<4, true>(buf, base, stride, bn, u);  // wave-uniform
       p[r] = bk < nblk ? partial4k_q(lds, qt, c0, cur) : 0u;
     }
-    const uint32_t v = tree4_packed(lds, u, p[0], p[1], p[2], p[3]);
+    const uint32_t v = tree4_packed(lds, u, p[0], p[1], p[2], p[3], QuadTree<128, -1>{qt});
     // lane 4j+r of the 64-block window holds block (window + (4j+r)*nw): move lanes 0..3's
     // results up by 4*(group mod 16) with one bpermute, park, flush every 16 groups.
     const uint32_t slot = (it & 15u) * 4u;
@@ -1037,7 +1062,7 @@ __global__ __launch_bounds__(kThreads) void crc_stream16_kernel(const uint32_t* 
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
   char* lds = reinterpret_cast<char*>(lds_words);
   if constexpr (kQuad)
-    stage_tables_q4<PDB_CAT_TREE16, PDB_CAT_H1008>(lds, tabs);
+    stage_tables_q4<PDB_CAT_TREE16, PDB_CAT_H1008, PDB_CAT_TREE16>(lds, tabs);  // image 1 hi: tree level 0
   else
     stage_tables<PDB_CAT_TREE16, PDB_CAT_H1008, PDB_CAT_S1024, kDyn>(lds, tabs);
   uint32_t* ctr = reinterpret_cast<uint32_t*>(lds + PDB_MAIN_BYTES + (kQuad ? 7u : 5u) * 4096u);
@@ -1142,7 +1167,11 @@ __global__ __launch_bounds__(kThreads) void crc_stream16_kernel(const uint32_t* 
   uint64_t pid0 = 0, pid1 = 0, pid2 = 0, pid3 = 0;
   BlkDesc pd0{}, pd1{}, pd2{}, pd3{};
   auto flush = [&]() {
-    const uint32_t v = tree4_packed<kL5Twice>(lds, u, park0, park1, park2, park3);
+    uint32_t v;
+    if constexpr (kQuad)
+      v = tree4_packed<kL5Twice>(lds, u, park0, park1, park2, park3, QuadTree<128, -1>{lt});
+    else
+      v = tree4_packed<kL5Twice>(lds, u, park0, park1, park2, park3);
     if (u < npark) {
       const uint64_t id = u == 0 ? pid0 : (u == 1 ? pid1 : (u == 2 ? pid2 : pid3));
       const BlkDesc bd = u == 0 ? pd0 : (u == 1 ? pd1 : (u == 2 ? pd2 : pd3));
@@ -1369,15 +1398,17 @@ __device__ __forceinline__ uint32_t masked_start(const MaskedPiece& f, uint32_t 
 // Levels of the wave tree inside each row of 16 lanes, folded toward the row's LAST lane
 // (row_shr never crosses a row): lane 16r + 15 gets sum_w shift(c_w, 16 (15 - w)).  A prefix of
 // E pieces sits in the row's last E lanes, so L = ceil(log2 E) levels suffice (wave-uniform).
-__device__ __forceinline__ uint32_t row_suffix_tree(const char* lds, uint32_t lane, uint32_t c, uint32_t L) {
+template <class TO = SlotTree>
+__device__ __forceinline__ uint32_t row_suffix_tree(const char* lds, uint32_t lane, uint32_t c, uint32_t L,
+                                                    const TO& to = TO{}) {
   uint32_t y;
   if (L > 0) {
     y = __builtin_amdgcn_update_dpp(0u, c, 0x111, 0xF, 0xF, false);  // row_shr:1
-    if ((lane & 1u) == 1u) c = shift_op_x(lds, 0, y, c);
+    if ((lane & 1u) == 1u) c = to.op(lds, 0, y, c);
   }
   if (L > 1) {
     y = __builtin_amdgcn_update_dpp(0u, c, 0x112, 0xF, 0xF, false);  // row_shr:2
-    if ((lane & 3u) == 3u) c = shift_op_x(lds, 1, y, c);
+    if ((lane & 3u) == 3u) c = to.op(lds, 1, y, c);
   }
   if (L > 2) {
     y = __builtin_amdgcn_update_dpp(0u, c, 0x114, 0xF, 0xF, false);  // row_shr:4
@@ -1465,7 +1496,7 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
   char* lds = reinterpret_cast<char*>(lds_words);
   // lane-quarter image: T0..T3 and shift 1024 conflict-free, slots 0..5 = 16..512
   if constexpr (__is_same(LT, QuadTabs))
-    stage_tables_q4<PDB_CAT_TREE16, -1>(lds, tabs);
+    stage_tables_q4<PDB_CAT_TREE16, PDB_CAT_TREE16, PDB_CAT_TREE16 + 1>(lds, tabs);  // image 1: tree levels 0, 1
   else
     stage_tables<PDB_CAT_TREE16, PDB_CAT_S1024>(lds, tabs);  // slots 0..5 = 16..512, 6 = 1024
   uint32_t* ctr = reinterpret_cast<uint32_t*>(lds + PDB_MAIN_BYTES + 7 * 4096u);
@@ -1479,6 +1510,13 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
     lt = quad_tabs(u);
   else
     lt = lane_tabs(u);
+  // tree levels 0 and 1 from image 1's replicated copies (lane-quarter image), else the slots
+  auto tops = [&]() {
+    if constexpr (__is_same(LT, QuadTabs))
+      return QuadTree<0, 128>{lt};
+    else
+      return SlotTree{};
+  };
   uint64_t grp = g_lo + kBlk * static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
   if (grp >= g_hi) return;
   const uintptr_t dummy = reinterpret_cast<uintptr_t>(tabs);  // >= 4 KiB + 256 B of valid bytes
@@ -1547,7 +1585,7 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
       emax = e > emax ? e : emax;
     }
     const uint32_t L = emax <= 1 ? 0u : (emax <= 2 ? 1u : (emax <= 4 ? 2u : (emax <= 8 ? 3u : 4u)));
-    const uint32_t pref = row_suffix_tree(lds, u, hash_masked(lds, lt, pf, masked_start(pf, ureg)), L);
+    const uint32_t pref = row_suffix_tree(lds, u, hash_masked(lds, lt, pf, masked_start(pf, ureg)), L, tops());
 #pragma unroll
     for (int r = 0; r < kBlk; ++r)
       P[r] = (kRows && G.n[r] == kMin) ? 0xFFFFFFFFu : __builtin_amdgcn_readlane(pref, kRowLanes * r + kRowLanes - 1);
@@ -1636,9 +1674,9 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
         }
         uint32_t v;
         if constexpr (kBlk == 4)
-          v = tree4_packed(lds, u, part[0], part[1], part[2], part[3]);
+          v = tree4_packed(lds, u, part[0], part[1], part[2], part[3], tops());
         else
-          v = tree8_packed(lds, u, part);
+          v = tree8_packed(lds, u, part, tops());
         if (u < nv && ((fastbits >> u) & 1u)) SinkOps<Sink>::put(sink, grp + u, v, G.ld, pre);
         defer(G, fastbits, nv);
         if (ngrp >= g_hi) {
@@ -1671,7 +1709,7 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
           emax = e > emax ? e : emax;
         }
         const uint32_t L = emax <= 1 ? 0u : (emax <= 2 ? 1u : (emax <= 4 ? 2u : (emax <= 8 ? 3u : 4u)));
-        const uint32_t pref = row_suffix_tree(lds, u, hash_masked(lds, lt, cpf, masked_start(cpf, ureg)), L);
+        const uint32_t pref = row_suffix_tree(lds, u, hash_masked(lds, lt, cpf, masked_start(cpf, ureg)), L, tops());
         const uint32_t v = __shfl(pref, (u & (kBlk - 1u)) * kRowLanes + kRowLanes - 1u, 64);  // lane r: block r
         const uint32_t nv = static_cast<uint32_t>(g_hi - grp < kBlk ? g_hi - grp : kBlk);
         const uint32_t fastbits = fast_bits(G);
@@ -1719,7 +1757,7 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
         if (fastbits & 2u) part[1] = body_partial(&c1, cl1, static_cast<uint32_t>((G.p[1] + G.n[1]) & 3u), P[1]);
         if (fastbits & 4u) part[2] = body_partial(&c2, cl2, static_cast<uint32_t>((G.p[2] + G.n[2]) & 3u), P[2]);
         if (fastbits & 8u) part[3] = body_partial(&c3, cl3, static_cast<uint32_t>((G.p[3] + G.n[3]) & 3u), P[3]);
-        const uint32_t v = tree4_packed(lds, u, part[0], part[1], part[2], part[3]);
+        const uint32_t v = tree4_packed(lds, u, part[0], part[1], part[2], part[3], tops());
         if (u < nv && ((fastbits >> u) & 1u)) SinkOps<Sink>::put(sink, grp + u, v, G.ld, pre);
         defer(G, fastbits, nv);
         if (ngrp >= g_hi) {
@@ -1776,7 +1814,7 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
         if (fastbits & 32u) part[5] = body_partial(&c5, cl5, static_cast<uint32_t>((G.p[5] + G.n[5]) & 3u), P[5]);
         if (fastbits & 64u) part[6] = body_partial(&c6, cl6, static_cast<uint32_t>((G.p[6] + G.n[6]) & 3u), P[6]);
         if (fastbits & 128u) part[7] = body_partial(&c7, cl7, static_cast<uint32_t>((G.p[7] + G.n[7]) & 3u), P[7]);
-        const uint32_t v = tree8_packed(lds, u, part);
+        const uint32_t v = tree8_packed(lds, u, part, tops());
         if (u < nv && ((fastbits >> u) & 1u)) SinkOps<Sink>::put(sink, grp + u, v, G.ld, pre);
         defer(G, fastbits, nv);
         if (ngrp >= g_hi) {
