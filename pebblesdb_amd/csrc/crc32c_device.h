@@ -512,14 +512,16 @@ __device__ __forceinline__ uint32_t partial4k_q(const char* lds, const QuadTabs&
 // locality: +8 %).  Results are parked in a register and flushed as one 64-lane
 // store per 16 groups.  The A/B variants of this kernel (piece shapes, waves per CU, lock-step
 // period, XCD numbering, quad transposes) live in the diagnostics library (diag_device.h).
-__global__ __launch_bounds__(kThreads) void crc_pack4k_kernel(
+// kW: waves per workgroup (one workgroup per CU); 16 shipped, 8 / 12 A/B variants.
+template <uint32_t kW = kWavesPerWg>
+__global__ __launch_bounds__(64 * kW) void crc_pack4k_kernel(
     const uint32_t* __restrict__ tabs, const uint8_t* __restrict__ base, uint64_t stride,
     uint64_t nblk, uint32_t flags, uint32_t init, uint32_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
   char* lds = reinterpret_cast<char*>(lds_words);
   const uint32_t u = threadIdx.x & 63u;
-  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWavesPerWg;
-  const uint64_t wg_first = static_cast<uint64_t>(blockIdx.x) * kWavesPerWg;
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kW;
+  const uint64_t wg_first = static_cast<uint64_t>(blockIdx.x) * kW;
   const uint64_t w = wg_first + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   u32x4 buf[4];
   load4k<4, true>(buf, base, stride, w < nblk ? w : nblk - 1, u);  // overlaps the table staging

@@ -116,7 +116,7 @@ hipError_t launch_fixed(const LaunchGeom& g, const uint32_t* d_tables, const uin
     // 4 blocks per wave-iteration, one packed tree, workgroup lock-step per 4-block group; lane
     // pieces 4 x 16 B so every load instruction reads 1 KiB contiguous, with the nt policy
     // (A/B: profiles/r01_ab_pack4k_nt*.json, +7-10 % over 2 x 32-B pieces with default loads)
-    hipLaunchKernelGGL(crc_pack4k_kernel, grid, block, 0, s, d_tables, base, stride, nblk, flags, init, out);
+    hipLaunchKernelGGL(crc_pack4k_kernel<>, grid, block, 0, s, d_tables, base, stride, nblk, flags, init, out);
     return hipGetLastError();
   }
   const FixedSrc src{base, stride, len, (flags & PDB_CRC_USE_INIT) ? ~init : 0xFFFFFFFFu};

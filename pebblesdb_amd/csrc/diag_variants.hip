@@ -736,6 +736,11 @@ hipError_t launch_fixed_variant(int v, const LaunchGeom& g, const uint32_t* d_ta
     // s_setprio 2 around the next block's load issue (free-running / lock-step)
     case 30: PDB_K((crc_pack4k_ab_kernel<1, 4, true, 16, false, false, 0, true>)); break;
     case 31: PDB_K((crc_pack4k_ab_kernel<0, 4, true, 16, false, false, 0, true>)); break;
+    // the shipped kernel (lane-quarter image) at 8 / 12 waves per CU
+    case 45: hipLaunchKernelGGL((crc_pack4k_kernel<8>), dim3(grid_for8(g, nblk)), dim3(512), 0, s, d_tables, base, stride,
+                                nblk, flags, init, out); break;
+    case 46: hipLaunchKernelGGL((crc_pack4k_kernel<12>), dim3(grid_forw(g, nblk, 12)), dim3(768), 0, s, d_tables, base,
+                                stride, nblk, flags, init, out); break;
     // 99 (and unknown ids): the round-1 shipped kernel, on the 32-replica table image with
     // single-copy Horner operators (crc_pack4k_kernel now runs on the lane-quarter image)
     default: PDB_K((crc_pack4k_ab_kernel<1, 4, true>)); break;
