@@ -23,6 +23,7 @@ for s in "$@"; do
     cold) step cold 300 python tools/cold_start.py ;;
     cold_variants) step cold_variants 300 python tools/cold_variants.py --variants 0,-1,19,24,13,28,12 ;;
     c2_waves) step ab_c2w 300 python tools/ab_fast.py 0,45,46 8 && step cold_c2w 300 python tools/cold_variants.py --variants 0,45,46,-1 ;;
+    counters_c2) step counters_c2 600 bash tools/counters_c2.sh ${TAG}_cntc2 ;;
     cold_q4) step cold_q4 300 python tools/cold_variants.py --variants 0,99,-1 ;;
     ab_c2) step ab_c2 300 python tools/ab_fast.py 0,99 8 ;;
     ab_q4) step ab_q4_sst 300 python tools/ab_sst.py 0,30 && step ab_q4_wal 300 python tools/ab_desc.py 0,42 wal && step ab_q4_desc4k 300 python tools/ab_desc.py 0,43 sst ;;
