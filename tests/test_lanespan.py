@@ -96,7 +96,7 @@ def test_batch_boundaries(crc, oracle_lib, n):
 
 
 # k (lanes per record) by length (span_pick): <= 256 B (33-word parts) 1..132 -> 1, 133..256 -> 2;
-# 257..512 B (27-word parts) 257..324 -> 3, 325..432 -> 4, 433..512 -> 5; 513..1023 B (33-word
+# 257..512 B (27-word parts) 257..324 -> 3, 325..448 -> 4, 449..512 -> 5; 513..1023 B (33-word
 # parts) 513..532 -> 4, 533..664 -> 5, 665..796 -> 6, 797..924 -> 7, 925..1023 -> 8
 @pytest.mark.parametrize("length", [1, 3, 4, 5, 17, 131, 132, 133, 255, 256, 257, 300, 431, 512, 513, 600, 700, 850,
                                     1000, 1023])
