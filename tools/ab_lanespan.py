@@ -20,6 +20,11 @@ CASES = [("wal100", 131, 1 << 30, crc32c.SIZE_256, 60), ("wal400", 431, 2 << 30,
          ("wal700", 700, 2 << 30, crc32c.SIZE_1023, 62), ("wal1000", 1000, 2 << 30, crc32c.SIZE_1023, 62)]
 
 
+# further exact variants to time beside the shipped kernel (AB_EXTRA="68,..."; 68 = 16 waves x 6 KiB,
+# one item in flight)
+EXTRA = tuple(int(x) for x in os.environ.get("AB_EXTRA", "").split(",") if x)
+
+
 def timeit(fn, reps=5):
     s = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -46,12 +51,14 @@ def main():
         out = torch.empty(len(offs), dtype=torch.int32, device="cuda")
         algo = int(lens.sum()) + 20 * len(lens)
         ref = diag.batch_desc(old, d, d_blk, flags=hint).cpu().numpy()
-        got = diag.batch_desc(0, d, d_blk, flags=hint).cpu().numpy()
-        assert (ref == got).all(), name
+        for v in (0,) + EXTRA:
+            got = diag.batch_desc(v, d, d_blk, flags=hint).cpu().numpy()
+            assert (ref == got).all(), (name, v)
         for _ in range(20):  # warm: power management settles
             diag.batch_desc(0, d, d_blk, flags=hint, out=out)
         # 63 / 64 / 67: the record kernel's loads alone / hash alone / bookkeeping alone
         t = {0: [], old: [], 63: [], 64: [], 67: []}
+        t.update({v: [] for v in EXTRA})
         for _ in range(5):
             for v in t:
                 t[v].append(timeit(lambda: diag.batch_desc(v, d, d_blk, flags=hint, out=out)))
