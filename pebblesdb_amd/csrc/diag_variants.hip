@@ -427,12 +427,12 @@ struct NtSealSink {  // A/B variant 34: the trailer as non-temporal byte stores
 // before the trailer is written, so the write lands on a valid L2 line.
 struct SealTouchSink {};
 
-// Pricing variants 94 / 95 (trailer bytes go to a SHADOW image at the same offsets, so the image
-// itself stays intact): 94 writes the 4-B trailer, 95 the trailer's whole aligned 32-B sector
-// (zeros around it).  Same kernel, same reads; only the write granularity differs.
+// Pricing variants 94 / 95 / 96 (trailer bytes go to a SHADOW image at the same offsets, so the
+// image itself stays intact): 94 writes the 4-B trailer, 95 / 96 the trailer's whole aligned 32-B /
+// 64-B window (zeros around it).  Same kernel, same reads; only the write granularity differs.
 struct ShadowSealSink {
   intptr_t delta;  // shadow - image
-  bool sector;
+  uint32_t bytes;  // 4: the trailer; 32 / 64: its whole aligned window
 };
 
 template <>
@@ -443,20 +443,24 @@ struct SinkOps<ShadowSealSink> {
     if (d.init_raw == 0) return;
     const uintptr_t a = reinterpret_cast<uintptr_t>(d.p) + d.n + k.delta;
     const uint32_t m = pdb_mask(~raw);
-    if (!k.sector) {
+    if (k.bytes == 4u) {
       typedef __attribute__((address_space(1))) uint32_t g_u32u __attribute__((aligned(1)));
       *reinterpret_cast<g_u32u*>(a) = m;
       return;
     }
     typedef __attribute__((address_space(1))) u32x4 g_v4;
-    const uintptr_t s0 = a & ~static_cast<uintptr_t>(31);
+    const uintptr_t s0 = a & ~static_cast<uintptr_t>(k.bytes - 1u);
     const uint32_t o = static_cast<uint32_t>(a - s0), i0 = o >> 2, sh = (o & 3u) * 8u;
-    uint32_t x[8];
+    uint32_t x[16];
 #pragma unroll
-    for (uint32_t i = 0; i < 8; ++i) x[i] = i == i0 ? (m << sh) : ((i == i0 + 1 && sh) ? (m >> (32u - sh)) : 0u);
+    for (uint32_t i = 0; i < 16; ++i) x[i] = i == i0 ? (m << sh) : ((i == i0 + 1 && sh) ? (m >> (32u - sh)) : 0u);
     g_v4* w = reinterpret_cast<g_v4*>(s0);
     w[0] = u32x4{x[0], x[1], x[2], x[3]};
     w[1] = u32x4{x[4], x[5], x[6], x[7]};
+    if (k.bytes == 64u) {
+      w[2] = u32x4{x[8], x[9], x[10], x[11]};
+      w[3] = u32x4{x[12], x[13], x[14], x[15]};
+    }
   }
 };
 
@@ -552,7 +556,7 @@ hipError_t launch_sst_variant(int v, const LaunchGeom& g, const uint32_t* d_tabl
                          SstVerifySink{ok, nbad});
     return hipGetLastError();
   }
-  if ((v == 94 || v == 95) && seal) {  // pricing: 4-B vs 32-B-sector trailer writes into a shadow image
+  if ((v == 94 || v == 95 || v == 96) && seal) {  // pricing: 4-B vs 32-B / 64-B window writes into a shadow image
     static std::mutex mu;
     static uint8_t* shadow = nullptr;
     static uint64_t shadow_n = 0;
@@ -564,7 +568,8 @@ hipError_t launch_sst_variant(int v, const LaunchGeom& g, const uint32_t* d_tabl
       if (hipMalloc(&shadow, buf_len + 64) != hipSuccess) return hipErrorOutOfMemory;
       shadow_n = buf_len + 64;
     }
-    const ShadowSealSink k{reinterpret_cast<intptr_t>(shadow) - reinterpret_cast<intptr_t>(buf), v == 95};
+    const ShadowSealSink k{reinterpret_cast<intptr_t>(shadow) - reinterpret_cast<intptr_t>(buf),
+                           v == 94 ? 4u : (v == 95 ? 32u : 64u)};
     hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ShadowSealSink, true>), grid, block, 0, s, d_tables, src, n, k);
     return hipGetLastError();
   }
