@@ -46,6 +46,7 @@ for s in "$@"; do
     prof_rows) step prof_c3 700 bash tools/profile.sh ${TAG}_prof_c3 c3 && step prof_sst_verify 700 bash tools/profile.sh ${TAG}_prof_sst_verify sst_verify && step prof_sstable 700 bash tools/profile.sh ${TAG}_prof_sstable sstable && step prof_wal 700 bash tools/profile.sh ${TAG}_prof_wal wal ;;
     ab_seal) step ab_seal 600 python tools/ab_sst.py 0,37,39 ;;
     vtool) step vtool 900 bash tools/verify_tool_bench.sh ${TAG}_vtool 1000000 ;;
+    vtool10m) step vtool10m 1000 bash tools/verify_tool_bench.sh ${TAG}_vtool10m 10000000 ;;
     seal_price) step seal_price 600 python tools/seal_price.py ;;
     ab_seal_price) step ab_seal_price 600 python tools/ab_sst.py 0,94,95,96 && step ab_seal_price_rev 600 python tools/ab_sst.py 96,95,94,0 ;;
     ab_seal_orders) step ab_so1 600 python tools/ab_sst.py 0,94,95 && step ab_so2 600 python tools/ab_sst.py 95,94,0 && step ab_so3 600 python tools/ab_sst.py 94,0 ;;
