@@ -750,6 +750,38 @@ struct SinkOps<SealSink> {
   }
 };
 
+// Seal with PARKED trailers (sstable-sized kernel, 4-block groups): a wave keeps the trailers of its
+// last kRing groups in lanes (lane 4 (g mod kRing) + r: block r of the wave's g-th group) and writes
+// each one when its lane slot comes round again, i.e. kRing groups later; the rest at the end.
+// kRing = 0: the plain SealSink behaviour (write when hashed).
+template <class Sink>
+struct SinkPark {
+  static constexpr uint32_t kRing = 0;
+};
+template <uint32_t R>
+struct ParkSealSink {};
+template <uint32_t R>
+struct SinkPark<ParkSealSink<R>> {
+  static_assert(R == 1 || R == 2 || R == 4 || R == 8 || R == 16, "ring of lane slots");
+  static constexpr uint32_t kRing = R;
+};
+template <uint32_t R>
+struct SinkOps<ParkSealSink<R>> {  // the deferred (slow-path) blocks: written when hashed
+  __device__ static __forceinline__ uint32_t pre(const ParkSealSink<R>&, uint64_t, const BlkDesc&) { return 0u; }
+  __device__ static __forceinline__ void put(const ParkSealSink<R>&, uint64_t i, uint32_t raw, const BlkDesc& d,
+                                             uint32_t) {
+    SinkOps<SealSink>::put(SealSink{}, i, raw, d, 0u);
+  }
+};
+__device__ __forceinline__ void write_trailer_word(uintptr_t a, uint32_t m) {
+  typedef __attribute__((address_space(1))) uint8_t g_u8;
+  g_u8* tr = reinterpret_cast<g_u8*>(a);
+  tr[0] = static_cast<uint8_t>(m);
+  tr[1] = static_cast<uint8_t>(m >> 8);
+  tr[2] = static_cast<uint8_t>(m >> 16);
+  tr[3] = static_cast<uint8_t>(m >> 24);
+}
+
 template <>
 struct SinkOps<SstVerifySink> {
   // the stored trailer word at p + n (any alignment): the two aligned dwords holding it
@@ -1553,6 +1585,24 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
     return G;
   };
   auto fast = [](uint32_t n) { return n - kMin <= kMax - kMin; };
+  // parked trailers (SinkPark): this lane's slot, written kRing groups after it was filled
+  constexpr uint32_t kRing = SinkPark<Sink>::kRing;
+  static_assert(kRing == 0 || (kRows == 4 && kBlk == 4), "parking: the sstable-sized seal");
+  uintptr_t pk_a = 0;
+  uint32_t pk_m = 0, pk_n = 0;
+  bool pk_ok = false;
+  auto park = [&](uint32_t v, const Grp& G, uint32_t fastbits, uint32_t nv) {
+    const uint32_t r = u & 3u;  // lane u holds block r's descriptor already
+    const uint32_t m = pdb_mask(~static_cast<uint32_t>(__shfl(v, r, 64)));
+    const bool ok = r < nv && ((fastbits >> r) & 1u) && G.ld.init_raw != 0;
+    if ((u >> 2) == (pk_n & (kRing - 1u))) {
+      if (pk_ok) write_trailer_word(pk_a, pk_m);
+      pk_a = reinterpret_cast<uintptr_t>(G.ld.p) + G.ld.n;
+      pk_m = m;
+      pk_ok = ok;
+    }
+    ++pk_n;
+  };
   auto body_at = [&](const Grp& G, int r) -> uintptr_t {
     return fast(G.n[r]) ? G.p[r] + G.n[r] - kBody : dummy;
   };
@@ -1679,7 +1729,10 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
           v = tree4_packed(lds, u, part[0], part[1], part[2], part[3], tops());
         else
           v = tree8_packed(lds, u, part, tops());
-        if (u < nv && ((fastbits >> u) & 1u)) SinkOps<Sink>::put(sink, grp + u, v, G.ld, pre);
+        if constexpr (kRing != 0)
+          park(v, G, fastbits, nv);
+        else if (u < nv && ((fastbits >> u) & 1u))
+          SinkOps<Sink>::put(sink, grp + u, v, G.ld, pre);
         defer(G, fastbits, nv);
         if (ngrp >= g_hi) {
           done = true;
@@ -1866,6 +1919,8 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
     }
     if (done) break;
   }
+  if constexpr (kRing != 0)
+    if (pk_ok) write_trailer_word(pk_a, pk_m);
 }
 
 // kBlk = 8 (A/B): 8-block groups, prefixes <= 128 B in rows of 8 lanes, one tree8_packed.

@@ -427,12 +427,13 @@ struct NtSealSink {  // A/B variant 34: the trailer as non-temporal byte stores
 // before the trailer is written, so the write lands on a valid L2 line.
 struct SealTouchSink {};
 
-// Pricing variants 94 / 95 / 96 (trailer bytes go to a SHADOW image at the same offsets, so the
-// image itself stays intact): 94 writes the 4-B trailer, 95 / 96 the trailer's whole aligned 32-B /
-// 64-B window (zeros around it).  Same kernel, same reads; only the write granularity differs.
+// Pricing variants 93 / 94 / 95 / 96 (trailer bytes go to a SHADOW image at the same offsets, so the
+// image itself stays intact): 94 writes the 4-B trailer, 95 / 96 / 93 the trailer's whole aligned
+// 32-B / 64-B / 128-B window (zeros around it; 128 B = one L2 line).  Same kernel, same reads; only
+// the write granularity differs.
 struct ShadowSealSink {
   intptr_t delta;  // shadow - image
-  uint32_t bytes;  // 4: the trailer; 32 / 64: its whole aligned window
+  uint32_t bytes;  // 4: the trailer; 32 / 64 / 128: its whole aligned window
 };
 
 template <>
@@ -450,16 +451,32 @@ struct SinkOps<ShadowSealSink> {
     }
     typedef __attribute__((address_space(1))) u32x4 g_v4;
     const uintptr_t s0 = a & ~static_cast<uintptr_t>(k.bytes - 1u);
-    const uint32_t o = static_cast<uint32_t>(a - s0), i0 = o >> 2, sh = (o & 3u) * 8u;
+    const uint32_t o = static_cast<uint32_t>(a - s0), i0 = (o >> 2) & 15u, sh = (o & 3u) * 8u;
     uint32_t x[16];
 #pragma unroll
     for (uint32_t i = 0; i < 16; ++i) x[i] = i == i0 ? (m << sh) : ((i == i0 + 1 && sh) ? (m >> (32u - sh)) : 0u);
     g_v4* w = reinterpret_cast<g_v4*>(s0);
     w[0] = u32x4{x[0], x[1], x[2], x[3]};
     w[1] = u32x4{x[4], x[5], x[6], x[7]};
-    if (k.bytes == 64u) {
+    if (k.bytes >= 64u) {
       w[2] = u32x4{x[8], x[9], x[10], x[11]};
       w[3] = u32x4{x[12], x[13], x[14], x[15]};
+    }
+    if (k.bytes == 128u) {  // the trailer sits in the first 64 B of its line or in the second
+      const bool hi = o >= 64u;
+      if (hi) {
+        w[0] = u32x4{0u, 0u, 0u, 0u};
+        w[1] = u32x4{0u, 0u, 0u, 0u};
+        w[2] = u32x4{0u, 0u, 0u, 0u};
+        w[3] = u32x4{0u, 0u, 0u, 0u};
+      }
+      uint32_t y[16];
+#pragma unroll
+      for (uint32_t i = 0; i < 16; ++i) y[i] = hi ? x[i] : 0u;
+      w[4] = u32x4{y[0], y[1], y[2], y[3]};
+      w[5] = u32x4{y[4], y[5], y[6], y[7]};
+      w[6] = u32x4{y[8], y[9], y[10], y[11]};
+      w[7] = u32x4{y[12], y[13], y[14], y[15]};
     }
   }
 };
@@ -556,21 +573,96 @@ hipError_t launch_sst_variant(int v, const LaunchGeom& g, const uint32_t* d_tabl
                          SstVerifySink{ok, nbad});
     return hipGetLastError();
   }
-  if ((v == 94 || v == 95 || v == 96) && seal) {  // pricing: 4-B vs 32-B / 64-B window writes into a shadow image
-    static std::mutex mu;
-    static uint8_t* shadow = nullptr;
-    static uint64_t shadow_n = 0;
-    std::lock_guard<std::mutex> lk(mu);
-    if (shadow_n < buf_len + 64) {
+  static std::mutex shadow_mu;  // diagnostics only: one shadow image (93-96, 85/87) and CRC array (85-87)
+  static uint8_t* shadow = nullptr;
+  static uint64_t shadow_n = 0;
+  static uint32_t* crcs = nullptr;
+  static uint64_t crcs_n = 0;
+  if (v >= 85 && v <= 87 && seal) {  // scatter-pass pricing: 85 / 86 the scatter alone into the shadow /
+                                     // the image (stale CRC words), 87 compact CRCs + scatter into the shadow
+    std::lock_guard<std::mutex> lk(shadow_mu);
+    if (shadow_n < buf_len + 256) {
       if (shadow) (void)hipFree(shadow);
       shadow = nullptr;
       shadow_n = 0;
-      if (hipMalloc(&shadow, buf_len + 64) != hipSuccess) return hipErrorOutOfMemory;
-      shadow_n = buf_len + 64;
+      if (hipMalloc(&shadow, buf_len + 256) != hipSuccess) return hipErrorOutOfMemory;
+      shadow_n = buf_len + 256;
+    }
+    if (crcs_n < n) {
+      if (crcs) (void)hipFree(crcs);
+      crcs = nullptr;
+      crcs_n = 0;
+      if (hipMalloc(&crcs, n * 4) != hipSuccess) return hipErrorOutOfMemory;
+      crcs_n = n;
+    }
+    if (v == 87)
+      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, OutSink, true>), grid, block, 0, s, d_tables, src, n,
+                         OutSink{crcs, PDB_CRC_MASK_OUTPUT});
+    hipLaunchKernelGGL(trailer_scatter_kernel, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256), 0, s,
+                       v == 86 ? buf : shadow, h, crcs, n);
+    return hipGetLastError();
+  }
+  if (v >= 80 && v <= 84 && seal) {  // the shadow writes of 94 / 96 / 93 (82 / 83 / 84: 128 / 4 / 64 B) or the
+                                     // scatter pass of 85 (80: alone; 81: after the compact-CRC pass),
+                                     // into one of 3 shadows in turn, so the written lines are not
+                                     // still in the 256-MB MALL from the previous launch
+    static uint8_t* rot[3] = {nullptr, nullptr, nullptr};
+    static uint64_t rot_n = 0;
+    static uint32_t turn = 0;
+    std::lock_guard<std::mutex> lk(shadow_mu);
+    if (rot_n < buf_len + 256) {
+      for (auto& r : rot) {
+        if (r) (void)hipFree(r);
+        r = nullptr;
+      }
+      rot_n = 0;
+      for (auto& r : rot)
+        if (hipMalloc(&r, buf_len + 256) != hipSuccess) return hipErrorOutOfMemory;
+      rot_n = buf_len + 256;
+    }
+    if (crcs_n < n) {
+      if (crcs) (void)hipFree(crcs);
+      crcs = nullptr;
+      crcs_n = 0;
+      if (hipMalloc(&crcs, n * 4) != hipSuccess) return hipErrorOutOfMemory;
+      crcs_n = n;
+    }
+    uint8_t* sh = rot[turn++ % 3];
+    if (v <= 81) {
+      if (v == 81)
+        hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, OutSink, true>), grid, block, 0, s, d_tables, src, n,
+                           OutSink{crcs, PDB_CRC_MASK_OUTPUT});
+      hipLaunchKernelGGL(trailer_scatter_kernel, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256), 0, s, sh, h,
+                         crcs, n);
+    } else {
+      const ShadowSealSink k{reinterpret_cast<intptr_t>(sh) - reinterpret_cast<intptr_t>(buf),
+                             v == 83 ? 4u : (v == 84 ? 64u : 128u)};
+      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ShadowSealSink, true>), grid, block, 0, s, d_tables, src, n, k);
+    }
+    return hipGetLastError();
+  }
+  if ((v == 93 || v == 94 || v == 95 || v == 96) && seal) {  // pricing: 4-B vs 32/64/128-B window writes into a shadow image
+    std::lock_guard<std::mutex> lk(shadow_mu);
+    if (shadow_n < buf_len + 256) {
+      if (shadow) (void)hipFree(shadow);
+      shadow = nullptr;
+      shadow_n = 0;
+      if (hipMalloc(&shadow, buf_len + 256) != hipSuccess) return hipErrorOutOfMemory;
+      shadow_n = buf_len + 256;
     }
     const ShadowSealSink k{reinterpret_cast<intptr_t>(shadow) - reinterpret_cast<intptr_t>(buf),
-                           v == 94 ? 4u : (v == 95 ? 32u : 64u)};
+                           v == 94 ? 4u : (v == 95 ? 32u : (v == 96 ? 64u : 128u))};
     hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ShadowSealSink, true>), grid, block, 0, s, d_tables, src, n, k);
+    return hipGetLastError();
+  }
+  if (v >= 88 && v <= 92 && seal) {  // parked trailers: written 1 / 2 / 4 / 8 / 16 groups after the hash
+    switch (v) {
+      case 88: hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ParkSealSink<1>, true>), grid, block, 0, s, d_tables, src, n, ParkSealSink<1>{}); break;
+      case 89: hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ParkSealSink<2>, true>), grid, block, 0, s, d_tables, src, n, ParkSealSink<2>{}); break;
+      case 90: hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ParkSealSink<4>, true>), grid, block, 0, s, d_tables, src, n, ParkSealSink<4>{}); break;
+      case 91: hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ParkSealSink<8>, true>), grid, block, 0, s, d_tables, src, n, ParkSealSink<8>{}); break;
+      default: hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ParkSealSink<16>, true>), grid, block, 0, s, d_tables, src, n, ParkSealSink<16>{}); break;
+    }
     return hipGetLastError();
   }
   if (v == 39 && seal) {  // full 32-B-sector rewrites around each trailer

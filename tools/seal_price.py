@@ -1,7 +1,11 @@
 #!/usr/bin/env python3
 """Seal-write pricing, seals only (tools/ab_sst.py interleaves verifies, whose kernels differ per
 variant): the in-place seal (variant 0) against the same kernel writing each trailer into a shadow
-image as 4 B (94), its aligned 32-B window (95) or 64-B window (96).  Each variant: 30 warm
+image as 4 B (94), its aligned 32-B (95), 64-B (96) or 128-B window (93); and the in-place seal with
+parked trailers, written 1 / 2 / 4 / 8 / 16 groups after their hash (88-92; each checked to
+reproduce variant 0's sealed image); scatter passes alone (85 into the shadow, 86 into the image,
+87 after a compact-CRC pass into the shadow); 80-84 = 85 / 87 / 93 / 94 / 96 into one of three
+shadows in turn (the written lines are no longer in the MALL from the launch before).  Each variant: 30 warm
 launches, then 20 timed with one event pair; the variant order is run forward and reversed, twice.
 Prints one JSON object: GB/s of algorithmic bytes per (pass, variant)."""
 import json
@@ -36,8 +40,16 @@ def seal(v):
     diag.lib().pdb_diag_sst(v, data.data_ptr(), total, d_h.data_ptr(), nblk, 1, None, None, sp)
 
 
-for v in VARIANTS:  # allocate the shadow image up front
+seal(0)
+ref = data.clone()  # the in-place seal's image
+tpos = torch.from_numpy((offs + sizes + 1)[:, None] + np.arange(4)[None, :]).reshape(-1).cuda()
+for v in VARIANTS:  # allocate the shadow image up front; in-place variants must reproduce the seal
+    data[tpos] = 0
     seal(v)
+    torch.cuda.synchronize()
+    if not (80 <= v <= 87 or 93 <= v <= 96):
+        assert torch.equal(data, ref), f"variant {v}: sealed image differs"
+    data.copy_(ref)
 torch.cuda.synchronize()
 res = {}
 for p, order in enumerate([VARIANTS, VARIANTS[::-1], VARIANTS, VARIANTS[::-1]]):
