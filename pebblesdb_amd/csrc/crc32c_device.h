@@ -762,7 +762,7 @@ template <uint32_t R>
 struct ParkSealSink {};
 template <uint32_t R>
 struct SinkPark<ParkSealSink<R>> {
-  static_assert(R == 1 || R == 2 || R == 4 || R == 8 || R == 16, "ring of lane slots");
+  static_assert(R == 1 || R == 2 || R == 4 || R == 8 || R == 16 || R == 32 || R == 64, "ring of lane slots");
   static constexpr uint32_t kRing = R;
 };
 template <uint32_t R>
@@ -1586,21 +1586,28 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
   };
   auto fast = [](uint32_t n) { return n - kMin <= kMax - kMin; };
   // parked trailers (SinkPark): this lane's slot, written kRing groups after it was filled
+  // (rings of more than 16 groups: kRing / 16 slots per lane, slot (g / 16) mod (kRing / 16))
   constexpr uint32_t kRing = SinkPark<Sink>::kRing;
+  constexpr uint32_t kPkS = kRing > 16u ? kRing / 16u : 1u, kPkL = kRing > 16u ? 16u : (kRing ? kRing : 1u);
   static_assert(kRing == 0 || (kRows == 4 && kBlk == 4), "parking: the sstable-sized seal");
-  uintptr_t pk_a = 0;
-  uint32_t pk_m = 0, pk_n = 0;
-  bool pk_ok = false;
+  uintptr_t pk_a[kPkS];
+  uint32_t pk_m[kPkS], pk_n = 0;
+  bool pk_ok[kPkS];
+#pragma unroll
+  for (uint32_t k = 0; k < kPkS; ++k) pk_a[k] = 0, pk_m[k] = 0, pk_ok[k] = false;
   auto park = [&](uint32_t v, const Grp& G, uint32_t fastbits, uint32_t nv) {
     const uint32_t r = u & 3u;  // lane u holds block r's descriptor already
     const uint32_t m = pdb_mask(~static_cast<uint32_t>(__shfl(v, r, 64)));
     const bool ok = r < nv && ((fastbits >> r) & 1u) && G.ld.init_raw != 0;
-    if ((u >> 2) == (pk_n & (kRing - 1u))) {
-      if (pk_ok) write_trailer_word(pk_a, pk_m);
-      pk_a = reinterpret_cast<uintptr_t>(G.ld.p) + G.ld.n;
-      pk_m = m;
-      pk_ok = ok;
-    }
+    const uint32_t sub = (pk_n / kPkL) % kPkS;  // uniform
+#pragma unroll
+    for (uint32_t k = 0; k < kPkS; ++k)
+      if (k == sub && (u >> 2) == (pk_n % kPkL)) {
+        if (pk_ok[k]) write_trailer_word(pk_a[k], pk_m[k]);
+        pk_a[k] = reinterpret_cast<uintptr_t>(G.ld.p) + G.ld.n;
+        pk_m[k] = m;
+        pk_ok[k] = ok;
+      }
     ++pk_n;
   };
   auto body_at = [&](const Grp& G, int r) -> uintptr_t {
@@ -1919,8 +1926,11 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
     }
     if (done) break;
   }
-  if constexpr (kRing != 0)
-    if (pk_ok) write_trailer_word(pk_a, pk_m);
+  if constexpr (kRing != 0) {
+#pragma unroll
+    for (uint32_t k = 0; k < kPkS; ++k)
+      if (pk_ok[k]) write_trailer_word(pk_a[k], pk_m[k]);
+  }
 }
 
 // kBlk = 8 (A/B): 8-block groups, prefixes <= 128 B in rows of 8 lanes, one tree8_packed.

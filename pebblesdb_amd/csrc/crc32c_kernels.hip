@@ -202,8 +202,12 @@ hipError_t launch_sst(const LaunchGeom& g, const uint32_t* d_tables, uint8_t* bu
   // emits: contents + type), the slow path in the same launch for the rest
   // (profiles/r01_ab_sst4k.json: verify +45 %, seal +27 % over crc_stream16_kernel)
   const SstSrc src{buf, h, buf_len};  // handles outside the image are reported, never followed
+  // seal: each wave parks its trailers (4 per lane) and writes them 64 groups later or when it is
+  // done -- writing a trailer soon after its line was read costs more (DESIGN.md §6.0, f2:
+  // +4.8 % over writing each group's trailers when hashed; diagnostics variant 72 is that form)
   if (seal)
-    hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SealSink, true>), grid, block, 0, s, d_tables, src, n, SealSink{});
+    hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ParkSealSink<64>, true>), grid, block, 0, s, d_tables, src, n,
+                       ParkSealSink<64>{});
   else
     hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstVerifySink, true>), grid, block, 0, s, d_tables, src, n,
                        SstVerifySink{ok, nbad});

@@ -481,6 +481,32 @@ struct SinkOps<ShadowSealSink> {
   }
 };
 
+// Pricing variants 76 / 77 / 78: the in-place trailer as byte stores with a wider scope (76: sc1 =
+// device scope; 77: sc0 sc1 = system scope, written through; 78: system scope + nt).
+template <int kPol>
+struct ScopeSealSink {};
+template <int kPol>
+struct SinkOps<ScopeSealSink<kPol>> {
+  __device__ static __forceinline__ uint32_t pre(const ScopeSealSink<kPol>&, uint64_t, const BlkDesc&) { return 0u; }
+  __device__ static __forceinline__ void put(const ScopeSealSink<kPol>&, uint64_t, uint32_t raw, const BlkDesc& d,
+                                             uint32_t) {
+    if (d.init_raw == 0) return;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(d.p) + d.n;
+    const uint32_t m = pdb_mask(~raw);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t b = (m >> (8 * k)) & 0xFFu;
+      const uint64_t ad = a + k;
+      if constexpr (kPol == 0)
+        asm volatile("global_store_byte %0, %1, off sc1" ::"v"(ad), "v"(b) : "memory");
+      else if constexpr (kPol == 1)
+        asm volatile("global_store_byte %0, %1, off sc0 sc1" ::"v"(ad), "v"(b) : "memory");
+      else
+        asm volatile("global_store_byte %0, %1, off sc0 sc1 nt" ::"v"(ad), "v"(b) : "memory");
+    }
+  }
+};
+
 // A/B variant 37: the trailer word as ONE (possibly unaligned) dword store instead of 4 byte stores.
 struct SealDwordSink {};
 
@@ -655,8 +681,23 @@ hipError_t launch_sst_variant(int v, const LaunchGeom& g, const uint32_t* d_tabl
     hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ShadowSealSink, true>), grid, block, 0, s, d_tables, src, n, k);
     return hipGetLastError();
   }
-  if (v >= 88 && v <= 92 && seal) {  // parked trailers: written 1 / 2 / 4 / 8 / 16 groups after the hash
+  if (v == 72 && seal) {  // the round-2 product seal: each group's trailers written when hashed
+    hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SealSink, true>), grid, block, 0, s, d_tables, src, n, SealSink{});
+    return hipGetLastError();
+  }
+  if (v >= 76 && v <= 78 && seal) {  // trailer stores with device / system scope
+    if (v == 76)
+      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ScopeSealSink<0>, true>), grid, block, 0, s, d_tables, src, n, ScopeSealSink<0>{});
+    else if (v == 77)
+      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ScopeSealSink<1>, true>), grid, block, 0, s, d_tables, src, n, ScopeSealSink<1>{});
+    else
+      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ScopeSealSink<2>, true>), grid, block, 0, s, d_tables, src, n, ScopeSealSink<2>{});
+    return hipGetLastError();
+  }
+  if (v >= 73 && v <= 92 && seal && (v >= 88 || v <= 74)) {  // parked trailers: written 1 / 2 / 4 / 8 / 16 (88-92), 32 / 64 (73 / 74) groups after the hash
     switch (v) {
+      case 73: hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ParkSealSink<32>, true>), grid, block, 0, s, d_tables, src, n, ParkSealSink<32>{}); break;
+      case 74: hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ParkSealSink<64>, true>), grid, block, 0, s, d_tables, src, n, ParkSealSink<64>{}); break;
       case 88: hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ParkSealSink<1>, true>), grid, block, 0, s, d_tables, src, n, ParkSealSink<1>{}); break;
       case 89: hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ParkSealSink<2>, true>), grid, block, 0, s, d_tables, src, n, ParkSealSink<2>{}); break;
       case 90: hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ParkSealSink<4>, true>), grid, block, 0, s, d_tables, src, n, ParkSealSink<4>{}); break;

@@ -199,6 +199,38 @@ def test_new_path_matches_previous_kernel(crc):
     assert (outs[0] == outs[1]).all() and (outs[0] == outs[2]).all()
 
 
+@pytest.mark.parametrize("variant", [0, 88, 89, 90, 91, 92, 73, 74])
+def test_parked_seal_matches_plain_seal(crc, variant):
+    """The shipped seal parks each wave's trailers (ring of 64 groups, 4 per lane) and writes them
+    later; the diagnostics rings of 1..64 groups (88-92, 73, 74) too.  On 1.3 M blocks (> 64 groups
+    per wave, so every ring wraps; index-sized and tiny blocks on the slow path mixed in) the sealed
+    image must equal the one written by variant 72 (each group's trailers written when hashed)."""
+    from pebblesdb_amd import table as T
+
+    rng = np.random.Generator(np.random.PCG64(77))
+    n = 1_300_000
+    sizes = rng.integers(4166, 4175, size=n).astype(np.int64)
+    sizes[::997] = rng.integers(1, 9000, size=len(sizes[::997]))
+    offs = np.concatenate([[0], np.cumsum(sizes + 5)[:-1]])
+    total = int(offs[-1] + sizes[-1] + 5)
+    img = torch.empty(total, dtype=torch.uint8, device="cuda")
+    diag.fill_splitmix(img, 78)
+    img[torch.from_numpy(offs + sizes).cuda()] = 0
+    h = np.zeros(n, dtype=crc.HANDLE_DTYPE)
+    h["offset"], h["size"] = offs, sizes
+    d_h = T.handles_to_device(h)
+    ref = img.clone()
+    diag.sst(72, ref, d_h, seal=True)
+    got = img.clone()
+    if variant == 0:
+        T.seal_device(got, d_h)
+    else:
+        diag.sst(variant, got, d_h, seal=True)
+    assert torch.equal(got, ref), variant
+    ok, nbad = T.verify_device(got, d_h)
+    assert int(nbad.item()) == 0
+
+
 # ---- descriptor batches with a size-class hint: crc_sst1k_kernel / crc_sst4k_kernel<DescSrc> ----
 EDGE_1K = [0, 1, 2, 3, 4, 15, 16, 17, 100, 255, 256, 257, 1000, 1023, 1024, 1025, 1026, 1027, 1039, 1040,
            1041, 1055, 1056, 1100, 1136, 1137, 1151, 1152, 1153, 1168, 1264, 1265, 1279, 1280, 1281, 1282, 2048,
