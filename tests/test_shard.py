@@ -1,6 +1,7 @@
 """CPU: block-range sharding and the multi-rank index scatter, world_size 2 over
 gloo (the GPU run uses the same code over RCCL).  The per-rank CRC here is the oracle -- these
-tests check the partitioning and the checksum-of-checksums, not the kernel."""
+tests check the partitioning and the checksum-of-checksums, not the kernel.  The last test (-m gpu)
+runs bench.py's own two-rank main() on the GPU box's one GPU and checks its XOR against the oracle."""
 import os
 import socket
 
@@ -127,3 +128,54 @@ def test_gloo_world2_bench_c3_byte_balanced():
     assert [r[0] for r in rows] == [0, 1] and sum(r[3] for r in rows) == total
     assert abs(rows[0][3] - rows[1][3]) <= 2 * 64 * 1024  # byte-balanced to within a block or two
     assert abs(total - world * (64 << 20)) <= 64 * 1024
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("workload", ["c2", "c3"])
+def test_bench_main_two_ranks_on_the_gpu(oracle_lib, workload):
+    """bench.py's own multi-rank main() end to end on the GPU: torchrun with 2 ranks sharing the
+    box's one GPU (gloo process group: RCCL refuses two ranks on one device), each hashing its shard
+    through libpdb_crc32c.so.  The JSON line must carry both ranks, the per-rank byte counts of the
+    count (c2) or byte-balanced (c3) split, and an XOR of all CRCs equal to the oracle's over the
+    whole two-rank workload."""
+    import json
+    import subprocess
+    import sys
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    nblk, c3_bytes = 4096, 48 << 20
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
+           "--gpus", "2", "--steps", "3", "--warmup", "1", "--settle", "0", "--backend", "gloo",
+           "--workload", workload, "--nblk", str(nblk), "--c3-bytes", str(c3_bytes), "--no-cpu-baseline"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=root)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith('{"metric"')][-1])
+    assert line["n_gpus"] == 2 and line["world_size"] == 2 and line["steps"] == 3
+    assert [x["rank"] for x in line["ranks"]] == [0, 1]
+    import oracle
+
+    if workload == "c2":
+        assert [x["bytes"] for x in line["ranks"]] == [nblk * 4096] * 2
+        data = oracle.splitmix_bytes(2 * nblk * 4096, 301)  # rank r's shard = blocks [r n, (r+1) n)
+        blk = np.zeros(2 * nblk, dtype=oracle.BLK_DTYPE)
+        blk["off"] = np.arange(2 * nblk) * 4096
+        blk["len"] = 4096
+        exp = int(np.bitwise_xor.reduce(oracle_lib.batch(data, blk, nthreads=4)))
+    else:
+        import bench
+
+        sizes = bench.c3_plan(c3_bytes, 2)
+        (lo0, hi0), (lo1, hi1) = byte_balanced_ranges(sizes, 2)
+        assert [x["bytes"] for x in line["ranks"]] == [int(sizes[lo0:hi0].sum()), int(sizes[lo1:hi1].sum())]
+        exp = 0
+        for rank, (lo, hi) in enumerate(((lo0, hi0), (lo1, hi1))):  # rank r fills its image with seed 303 + r
+            s = sizes[lo:hi]
+            data = oracle.splitmix_bytes(int(s.sum()), 303 + rank)
+            blk = np.zeros(len(s), dtype=oracle.BLK_DTYPE)
+            blk["off"] = np.concatenate([[0], np.cumsum(s)[:-1]])
+            blk["len"] = s
+            exp ^= int(np.bitwise_xor.reduce(oracle_lib.batch(data, blk, nthreads=4)))
+    assert int(line["xor_of_crcs"], 16) == exp
