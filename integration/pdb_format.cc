@@ -26,7 +26,7 @@
 
 namespace pdb_hooks {
 namespace {
-std::atomic<uint64_t> g_counters[8];
+std::atomic<uint64_t> g_counters[12];
 }
 uint64_t NowNs() {
   timespec ts;
@@ -39,6 +39,13 @@ void AddSeal(uint64_t blocks, uint64_t bytes, uint64_t ns) {
   g_counters[2].fetch_add(bytes, std::memory_order_relaxed);
   g_counters[3].fetch_add(ns, std::memory_order_relaxed);
 }
+void AddScan(uint64_t blocks, uint64_t bytes, uint64_t ns, uint64_t bad) {
+  g_counters[8].fetch_add(1, std::memory_order_relaxed);
+  g_counters[9].fetch_add(blocks, std::memory_order_relaxed);
+  g_counters[10].fetch_add(bytes, std::memory_order_relaxed);
+  g_counters[11].fetch_add(ns, std::memory_order_relaxed);
+  if (bad) g_counters[7].fetch_add(bad, std::memory_order_relaxed);
+}
 void AddVerify(uint64_t bytes, uint64_t ns, bool failed) {
   g_counters[4].fetch_add(1, std::memory_order_relaxed);
   g_counters[5].fetch_add(bytes, std::memory_order_relaxed);
@@ -49,11 +56,11 @@ void AddVerify(uint64_t bytes, uint64_t ns, bool failed) {
 
 extern "C" void pdb_hook_stats_get(pdb_hook_stats* out) {
   uint64_t* v = reinterpret_cast<uint64_t*>(out);
-  for (int i = 0; i < 8; ++i) v[i] = pdb_hooks::g_counters[i].load(std::memory_order_relaxed);
+  for (int i = 0; i < 12; ++i) v[i] = pdb_hooks::g_counters[i].load(std::memory_order_relaxed);
 }
 
 extern "C" void pdb_hook_stats_reset(void) {
-  for (int i = 0; i < 8; ++i) pdb_hooks::g_counters[i].store(0, std::memory_order_relaxed);
+  for (int i = 0; i < 12; ++i) pdb_hooks::g_counters[i].store(0, std::memory_order_relaxed);
 }
 
 namespace leveldb {
@@ -120,28 +127,48 @@ Status ReadBlock(RandomAccessFile* file, const ReadOptions& options, const Block
       return Status::Corruption("block checksum mismatch");
     }
   }
+  if (data == buf) return pdb_hooks::BlockFromChecked(data, n, buf, true, result);
+  delete[] buf;
+  return pdb_hooks::BlockFromChecked(data, n, nullptr, true, result);
+}
+
+}  // namespace leveldb
+
+namespace pdb_hooks {
+// ReadBlock's type dispatch (format.cc:106-145) for data = [contents n B][type] whose checksum has
+// been dealt with.  owned: the heap buffer data sits in (taken over; freed on every path), else
+// nullptr with stable = true (the file's own memory, live while it is open: handed out uncachable)
+// or stable = false (a transient buffer: the contents are copied).
+leveldb::Status BlockFromChecked(const char* data, size_t n, char* owned, bool stable, leveldb::BlockContents* result) {
+  using leveldb::Slice;
+  using leveldb::Status;
   switch (data[n]) {
-    case kNoCompression:
-      if (data == buf) {
-        result->data = Slice(buf, n);
+    case leveldb::kNoCompression:
+      if (owned != nullptr) {
+        result->data = Slice(owned, n);
         result->heap_allocated = true;
         result->cachable = true;
-      } else {  // the file's own memory, live while the file is open: not ours to cache or free
-        delete[] buf;
+      } else if (stable) {
         result->data = Slice(data, n);
         result->heap_allocated = false;
         result->cachable = false;
+      } else {
+        char* copy = new char[n];
+        memcpy(copy, data, n);
+        result->data = Slice(copy, n);
+        result->heap_allocated = true;
+        result->cachable = true;
       }
       return Status::OK();
-    case kSnappyCompression: {  // Snappy stays delegated to the port layer (out of scope)
+    case leveldb::kSnappyCompression: {  // Snappy stays delegated to the port layer (out of scope)
       size_t ulen = 0;
-      if (!port::Snappy_GetUncompressedLength(data, n, &ulen)) {
-        delete[] buf;
+      if (!leveldb::port::Snappy_GetUncompressedLength(data, n, &ulen)) {
+        delete[] owned;
         return Status::Corruption("corrupted compressed block contents");
       }
       char* ubuf = new char[ulen];
-      const bool ok = port::Snappy_Uncompress(data, n, ubuf);
-      delete[] buf;
+      const bool ok = leveldb::port::Snappy_Uncompress(data, n, ubuf);
+      delete[] owned;
       if (!ok) {
         delete[] ubuf;
         return Status::Corruption("corrupted compressed block contents");
@@ -152,9 +179,8 @@ Status ReadBlock(RandomAccessFile* file, const ReadOptions& options, const Block
       return Status::OK();
     }
     default:
-      delete[] buf;
+      delete[] owned;
       return Status::Corruption("bad block type");
   }
 }
-
-}  // namespace leveldb
+}  // namespace pdb_hooks

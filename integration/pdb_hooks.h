@@ -1,9 +1,11 @@
 // integration/pdb_hooks.h -- counters of the engine-side hooks (pdb_table_builder.cc: batched
-// WriteRawBlock seals; pdb_format.cc: ReadBlock verifies), read by the db_bench-equivalent harness
-// (pdb_dbbench.cc) to report the GPU CRC's share of a run and its copy-inclusive rate.
+// WriteRawBlock seals; pdb_format.cc: ReadBlock verifies; pdb_table.cc: scan read-ahead batches),
+// read by the db_bench-equivalent harness (pdb_dbbench.cc) to report the GPU CRC's share of a run
+// and its copy-inclusive rate; and ReadBlock's block decoding, shared with pdb_table.cc.
 #ifndef PDB_INTEGRATION_HOOKS_H_
 #define PDB_INTEGRATION_HOOKS_H_
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -18,7 +20,11 @@ typedef struct pdb_hook_stats {
   uint64_t verify_calls;   // ReadBlock checksum checks on the GPU
   uint64_t verify_bytes;   // contents + type bytes checked
   uint64_t verify_ns;      // wall time inside them
-  uint64_t verify_failed;  // Corruption("block checksum mismatch") returned
+  uint64_t verify_failed;  // Corruption("block checksum mismatch") returned (or found by a scan batch)
+  uint64_t scan_batches;   // pdb_table.cc: verified read-ahead batches (pdb_sst_verify_host) of scans
+  uint64_t scan_blocks;    // data blocks checked in them
+  uint64_t scan_bytes;     // bytes read and checked
+  uint64_t scan_ns;        // wall time of the window reads + GPU checks
 } pdb_hook_stats;
 
 void pdb_hook_stats_get(pdb_hook_stats* out);
@@ -31,7 +37,16 @@ namespace pdb_hooks {
 // internal: the hooks add to the counters (thread-safe, relaxed atomics)
 void AddSeal(uint64_t blocks, uint64_t bytes, uint64_t ns);
 void AddVerify(uint64_t bytes, uint64_t ns, bool failed);
+void AddScan(uint64_t blocks, uint64_t bytes, uint64_t ns, uint64_t bad);
 uint64_t NowNs();
+}  // namespace pdb_hooks
+
+namespace leveldb {
+struct BlockContents;
+class Status;
+}  // namespace leveldb
+namespace pdb_hooks {
+leveldb::Status BlockFromChecked(const char* data, size_t n, char* owned, bool stable, leveldb::BlockContents* result);
 }  // namespace pdb_hooks
 #endif
 
