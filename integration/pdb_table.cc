@@ -6,10 +6,10 @@
 // compaction input when Options::paranoid_checks is set: version_set.cc:2907-2910) reads its data
 // blocks one ReadBlock at a time (table.cc:193-259 -> format.cc:66-104), i.e. one checksum -- here
 // one PCIe round trip to the GPU -- per ~4-KiB block.  This reader keeps the table's data-block
-// handles (decoded from the index block it already holds) and, once a reader asks for the third
-// block in a row of one table, reads the next ~1 MiB of data blocks with ONE file read and checks
-// all their trailers with ONE pdb_sst_verify_host batch; the following block reads are served from
-// that window.  Semantics are ReadBlock's: the bytes a block is built from are exactly the bytes
+// handles (decoded from the index block it already holds) and, when an iterator asks for a block,
+// reads it and the data blocks after it -- 16 KiB, then x4 per window while the iterator reads on in
+// order, up to 1 MiB -- with ONE file read and checks all their trailers with ONE
+// pdb_sst_verify_host batch; the following block reads are served from that window.  Semantics are ReadBlock's: the bytes a block is built from are exactly the bytes
 // whose checksum was checked, and a block whose check failed returns Corruption("block checksum
 // mismatch") when, and only when, it is read.  Point reads (Get) and reads without
 // verify_checksums take the reference path (ReadBlock; with verify on, pdb_format.cc's GPU check).
@@ -40,8 +40,12 @@
 namespace leveldb {
 namespace {
 
-constexpr uint64_t kWindowBytes = 1u << 20;  // data blocks per read-ahead batch: ~1 MiB
-constexpr int kRunToBatch = 2;               // sequential block reads before a batch is read ahead
+// Read-ahead windows of an iterator: 16 KiB of data blocks at its first block, then x4 per window
+// while it keeps reading on in order, up to 1 MiB (a Seek followed by a few Next()s costs one small
+// batch; a scan settles at 1-MiB batches).  Point reads (Get) never read ahead.
+constexpr uint64_t kFirstWindow = 16u << 10;
+constexpr int kMaxGrow = 3;  // 16 KiB << 2 * 3 = 1 MiB
+thread_local int t_point_read = 0;  // > 0 inside Table::InternalGet
 
 // The read-ahead state of one table (shared by every reader of it, so under a mutex).
 class ScanWindow {
@@ -50,14 +54,15 @@ class ScanWindow {
   // (not a scan) by ReadBlock.
   Status Read(RandomAccessFile* file, const Block* index, const Comparator* cmp, const ReadOptions& opt,
               const BlockHandle& h, BlockContents* out) {
-    {
+    if (t_point_read == 0) {
       MutexLock l(&mu_);
       if (!decoded_) Decode(index, cmp);
       const int64_t i = Find(h);
-      run_ = (i >= 0 && i == last_ + 1) ? run_ + 1 : 0;
+      const bool in_order = i >= 0 && i == last_ + 1;
       last_ = i;
       if (i >= 0 && i >= lo_ && i < hi_) return Serve(i, out);
-      if (i >= 0 && run_ >= kRunToBatch && Fill(file, i)) return Serve(i, out);
+      grow_ = in_order ? std::min(grow_ + 1, kMaxGrow) : 0;
+      if (i >= 0 && Fill(file, i, kFirstWindow << (2 * grow_))) return Serve(i, out);
     }
     return ReadBlock(file, opt, h, out);
   }
@@ -80,15 +85,15 @@ class ScanWindow {
     if (p == blocks_.end() || p->offset != h.offset() || p->size != h.size()) return -1;
     return p - blocks_.begin();
   }
-  // Blocks i.. that lie back to back in the file, up to kWindowBytes (at least one): one read, one
-  // GPU check.  False (no window) if the read comes back short or fails -- ReadBlock then reports
-  // it for the block asked for.
-  bool Fill(RandomAccessFile* file, int64_t i) {
+  // Blocks i.. that lie back to back in the file, up to `window` bytes (at least one): one read,
+  // one GPU check.  False (no window) if the read comes back short or fails -- ReadBlock then
+  // reports it for the block asked for.
+  bool Fill(RandomAccessFile* file, int64_t i, uint64_t window) {
     const uint64_t base = blocks_[i].offset;
     uint64_t end = base;
     int64_t j = i;
     while (j < static_cast<int64_t>(blocks_.size()) && blocks_[j].offset == end &&
-           (j == i || blocks_[j].offset + blocks_[j].size + kBlockTrailerSize - base <= kWindowBytes)) {
+           (j == i || blocks_[j].offset + blocks_[j].size + kBlockTrailerSize - base <= window)) {
       end = blocks_[j].offset + blocks_[j].size + kBlockTrailerSize;
       ++j;
     }
@@ -120,8 +125,8 @@ class ScanWindow {
   port::Mutex mu_;
   bool decoded_ = false;
   std::vector<pdb_block_handle> blocks_;  // data blocks, index order = file order
-  int64_t last_ = -2;                     // index of the block read last (any reader)
-  int run_ = 0;                           // consecutive blocks read in order
+  int64_t last_ = -2;                     // index of the block read last (any iterator)
+  int grow_ = 0;                          // windows read in order so far (size 16 KiB << 2 grow_)
   std::string buf_;
   const char* data_ = nullptr;
   uint64_t base_ = 0;
@@ -263,7 +268,9 @@ Status Table::InternalGet(const ReadOptions& options, const Slice& k, void* arg,
     const bool skip = rep_->filter != nullptr && h.DecodeFrom(&hv).ok() && !rep_->filter->KeyMayMatch(h.offset(), k);
 #endif
     if (!skip) {
+      ++t_point_read;  // one block for one key: the ReadBlock path, never a window
       Iterator* bi = BlockReader(this, options, index->value());
+      --t_point_read;
       bi->Seek(k);
       if (bi->Valid()) (*saver)(arg, bi->key(), bi->value());
       s = bi->status();
