@@ -627,7 +627,52 @@ struct DescSrc {
   __device__ __forceinline__ BlkDesc lane(const Raw& r) const {  // per-lane fields (no readfirstlane)
     return {base + ((static_cast<uint64_t>(r.y) << 32) | r.x), r.z, (flags & PDB_CRC_USE_INIT) ? ~r.w : 0xFFFFFFFFu};
   }
+  // block i's offset and length (the byte-balanced split, bal_bound)
+  __device__ __forceinline__ uint64_t off(uint64_t i) const {
+    typedef __attribute__((address_space(1))) const uint64_t g_u64_;
+    return *reinterpret_cast<g_u64_*>(reinterpret_cast<uintptr_t>(&blk[i].off));
+  }
+  __device__ __forceinline__ uint32_t len(uint64_t i) const {
+    typedef __attribute__((address_space(1))) const uint32_t g_u32_;
+    return *reinterpret_cast<g_u32_*>(reinterpret_cast<uintptr_t>(&blk[i].len));
+  }
 };
+
+// Byte-balanced workgroup boundaries for descriptor lists (C3: Zipf sizes): workgroup g's first
+// block is the first block whose offset reaches g/G of the list's span (off[0] .. off[n-1] +
+// len[n-1]), searched 64 ways per step by one wave (3 dependent loads for C3's ~4800-block
+// windows), and CLAMPED to within D - 1 blocks of the count split n g / G, D = floor(n / 2G).
+// Consecutive count splits are >= 2D - 2 apart, so the boundaries are non-decreasing in g and the
+// workgroups partition [0, n) whatever the list holds; on a packed ascending list (every C3 list)
+// each workgroup gets ~1/G of the bytes instead of 1/G of the blocks.  All 64 lanes must be
+// active; the result is wave-uniform.
+template <class Src>
+__device__ __forceinline__ uint64_t bal_bound(const Src& src, uint64_t n, uint64_t g, uint64_t G, uint32_t u) {
+  const uint64_t cs = n * g / G;
+  const uint64_t D = n / (2 * G);
+  if (g == 0 || g >= G || D < 2) return cs;
+  const uint64_t o0 = src.off(0), oe = src.off(n - 1) + src.len(n - 1);
+  if (oe <= o0) return cs;
+  const uint64_t span = oe - o0;
+  const uint64_t t = o0 + span / G * g + span % G * g / G;  // o0 + span g / G without overflow
+  uint64_t lo = cs - (D - 1), hi = cs + (D - 1);              // the boundary lies in [lo, hi]
+  while (lo < hi) {
+    const uint64_t step = (hi - lo + 63u) / 64u;
+    const uint64_t sidx = lo + u * step;
+    const bool valid = sidx < hi;
+    const uint64_t o = src.off(valid ? sidx : lo);
+    const uint64_t m = __builtin_amdgcn_ballot_w64(valid && o >= t);
+    if (m & 1ull) break;  // block lo already reaches t
+    if (m == 0) {
+      lo += ((hi - lo - 1u) / step) * step + 1u;  // past the last sample
+    } else {
+      const uint64_t k = static_cast<uint64_t>(__builtin_ctzll(m));
+      hi = lo + k * step;
+      lo += (k - 1u) * step + 1u;
+    }
+  }
+  return lo;
+}
 
 // sstable handle: CRC over contents || type (table/table_builder.cc:197-198; format.cc:98).
 // A handle whose block + 5-byte trailer does not fit the buffer (ReadBlock's "truncated block
@@ -1086,7 +1131,8 @@ __device__ __forceinline__ uint32_t chain16(const char* lds, const LT& lt, uint3
 
 // LT: the table image -- QuadTabs (lane-quarter: T0..T3, shift 1024 and shift 1008 conflict-free;
 // shipped) or LaneTabs (32 replicas of T0..T3, single-copy operators; A/B diagnostics).
-template <class Src, class Sink, bool kDyn, bool kNT, bool kPack = false, class LT = QuadTabs>
+// kBal (descriptor lists): byte-balanced workgroup ranges (bal_bound) instead of equal block counts.
+template <class Src, class Sink, bool kDyn, bool kNT, bool kPack = false, class LT = QuadTabs, bool kBal = false>
 __global__ __launch_bounds__(kThreads) void crc_stream16_kernel(const uint32_t* __restrict__ tabs,
                                                                  Src src, uint64_t nblk, Sink sink) {
   constexpr bool kQuad = __is_same(LT, QuadTabs);
@@ -1100,9 +1146,19 @@ __global__ __launch_bounds__(kThreads) void crc_stream16_kernel(const uint32_t* 
   else
     stage_tables<PDB_CAT_TREE16, PDB_CAT_H1008, PDB_CAT_S1024, kDyn>(lds, tabs);
   uint32_t* ctr = reinterpret_cast<uint32_t*>(lds + PDB_MAIN_BYTES + (kQuad ? 7u : 5u) * 4096u);
-  const uint64_t g_lo = nblk * blockIdx.x / gridDim.x, g_hi = nblk * (blockIdx.x + 1) / gridDim.x;
+  uint64_t g_lo = nblk * blockIdx.x / gridDim.x, g_hi = nblk * (blockIdx.x + 1) / gridDim.x;
+  static_assert(!kBal || (kDyn && kQuad), "byte balance: dynamic scheduling, lane-quarter image (slot 7)");
+  uint64_t* bnd = reinterpret_cast<uint64_t*>(ctr + 2);  // kBal: this workgroup's range, from wave 0
+  if constexpr (kBal) {
+    if (threadIdx.x < 64) {
+      const uint64_t lo = bal_bound(src, nblk, blockIdx.x, gridDim.x, threadIdx.x);
+      const uint64_t hi = bal_bound(src, nblk, blockIdx.x + 1, gridDim.x, threadIdx.x);
+      if (threadIdx.x == 0) bnd[0] = lo, bnd[1] = hi;
+    }
+  }
   if (kDyn && threadIdx.x == 0) *ctr = kWavesPerWg;  // next block, relative to g_lo
   __syncthreads();
+  if constexpr (kBal) g_lo = bnd[0], g_hi = bnd[1];
   const uint32_t u = threadIdx.x & 63u;
   LT lt;
   if constexpr (kQuad)

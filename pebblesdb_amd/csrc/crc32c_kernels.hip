@@ -175,9 +175,10 @@ hipError_t launch_desc_sink(const LaunchGeom& g, const uint32_t* d_tables, const
     return hipGetLastError();
   }
   // descriptor lists of any lengths (C3: Zipf sizes at byte offsets): 16-B lane pieces with nt
-  // loads, dynamic blocks, packed 4-block trees (A/B: profiles/r01_ab_c3_pack*.json)
-  hipLaunchKernelGGL((crc_stream16_kernel<DescSrc, Sink, true, true, true>), grid, block, 0, s, d_tables, src, nblk,
-                     sink);
+  // loads, dynamic blocks, packed 4-block trees (A/B: profiles/r01_ab_c3_pack*.json), byte-balanced
+  // workgroup ranges (bal_bound; diagnostics variant 71 splits by block count)
+  hipLaunchKernelGGL((crc_stream16_kernel<DescSrc, Sink, true, true, true, QuadTabs, true>), grid, block, 0, s,
+                     d_tables, src, nblk, sink);
   return hipGetLastError();
 }
 

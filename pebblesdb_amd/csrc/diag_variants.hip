@@ -916,8 +916,12 @@ hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tab
       hipLaunchKernelGGL((crc_stream_kernel<DescSrc, OutSink, 0, true, true>), grid, block, 0, s, d_tables, src, nblk,
                          sink);
       break;
-    case 16:  // 40: size hints ignored -- the any-length kernel (16-B pieces, nt, dynamic, packed trees)
-    case 40:
+    case 16:  // 40: size hints ignored -- the any-length kernel (16-B pieces, nt, dynamic, packed trees,
+    case 40:  // byte-balanced workgroup ranges: the product's C3 routing)
+      hipLaunchKernelGGL((crc_stream16_kernel<DescSrc, OutSink, true, true, true, QuadTabs, true>), grid, block, 0, s,
+                         d_tables, src, nblk, sink);
+      break;
+    case 71:  // the any-length kernel with equal block counts per workgroup (round-2 C3 routing before bal_bound)
       hipLaunchKernelGGL((crc_stream16_kernel<DescSrc, OutSink, true, true, true>), grid, block, 0, s, d_tables, src,
                          nblk, sink);
       break;

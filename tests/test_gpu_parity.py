@@ -414,3 +414,35 @@ def test_round_boundaries_all_stream_paths(crc, oracle_lib):
         assert int.from_bytes(sealed[o + sz + 1 : o + sz + 5].tobytes(), "little") == want, sz
     ok, nbad = T.verify_device(d_img, d_h)
     assert int(nbad.item()) == 0 and bool(ok.all())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("order", ["packed", "shuffled", "descending", "overlapping", "gaps"])
+def test_byte_balanced_ranges_any_list(crc, oracle_lib, order):
+    """Descriptor lists without a size hint run crc_stream16_kernel with byte-balanced workgroup
+    ranges (bal_bound: boundaries searched by offset, clamped around the count split so they
+    always partition the list).  Every block must be hashed exactly as the oracle does whatever the
+    list's order -- packed ascending (C3's shape, the balanced case), shuffled, descending,
+    overlapping (all blocks share one window) or with gaps -- and as variant 71 (count split)."""
+    rng = np.random.Generator(np.random.PCG64(91))
+    n = 60000  # > 4 x 256 workgroups: the search windows are non-trivial
+    lens = np.minimum(rng.zipf(1.3, size=n), 40).astype(np.int64) * 97 + rng.integers(0, 97, size=n)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+    if order == "shuffled":
+        p = rng.permutation(n)
+        offs, lens = offs[p], lens[p]
+    elif order == "descending":
+        offs, lens = offs[::-1].copy(), lens[::-1].copy()
+    elif order == "overlapping":
+        offs = rng.integers(0, 5000, size=n).astype(np.int64)
+    elif order == "gaps":
+        offs = offs + np.cumsum(rng.integers(0, 3000, size=n))
+    total = int((offs + lens).max()) + 16
+    d = torch.empty(total, dtype=torch.uint8, device="cuda")
+    diag.fill_splitmix(d, 92)
+    blk = crc.make_blocks(offs, lens)
+    d_blk = crc.blocks_to_device(blk)
+    got = _u32(crc.batch(d, d_blk))
+    exp = oracle_lib.batch(d.cpu().numpy(), blk, nthreads=8)
+    assert (got == exp).all(), int(np.nonzero(got != exp)[0][0])
+    assert (_u32(diag.batch_desc(71, d, d_blk)) == exp).all()
