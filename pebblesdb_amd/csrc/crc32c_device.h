@@ -1427,6 +1427,17 @@ typedef __attribute__((address_space(1))) const u32x4a4 g_u32x4;
 
 __device__ __forceinline__ uint32_t gload32(uintptr_t a) { return *reinterpret_cast<g_u32*>(a); }
 
+// 16 B at any byte address (one global_load_dwordx4: the runtime runs the shader in unaligned
+// access mode); the A/B form of the body loads without the neighbour dword (variant 70)
+typedef u32x4 u32x4a1 __attribute__((aligned(1)));
+typedef __attribute__((address_space(1))) const u32x4a1 g_u32x4u;
+template <bool kNT>
+__device__ __forceinline__ u32x4 gload128u(uintptr_t a) {
+  if constexpr (kNT)
+    return __builtin_nontemporal_load(reinterpret_cast<g_u32x4u*>(a));
+  else
+    return *reinterpret_cast<g_u32x4u*>(a);
+}
 template <bool kNT>
 __device__ __forceinline__ u32x4 gload128(uintptr_t a) {
   if constexpr (kNT)
@@ -1574,7 +1585,10 @@ constexpr uint32_t kSlowList = 64u;
 // 8 (rows of 8 lanes: prefixes <= 128 B, one packed tree per 8 blocks).
 // LT: the table image -- QuadTabs (lane-quarter, conflict-free shift 1024; shipped) or LaneTabs (the
 // 32-replica image with single-copy operators; A/B diagnostics)
-template <class Src, class Sink, bool kNT, int kRows, bool kDiagNoFold = false, int kBlk = 4, class LT = QuadTabs>
+// kUA (A/B, variant 70): body pieces loaded at their exact byte addresses (unaligned dwordx4)
+// instead of 4-B aligned + the DPP neighbour dword + v_alignbyte.
+template <class Src, class Sink, bool kNT, int kRows, bool kDiagNoFold = false, int kBlk = 4, class LT = QuadTabs,
+          bool kUA = false>
 __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ tabs, Src src, uint64_t nblk,
                                                   Sink sink) {
   static_assert(kRows == 0 || kRows == 1 || kRows == 4, "no body (records <= 256 B), 1-KiB or 4-KiB bodies");
@@ -1673,9 +1687,16 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
   auto issue_body = [&](u32x4* b, uint32_t& last, uintptr_t bs) {
     const uint32_t s = static_cast<uint32_t>(bs & 3u);
     const uintptr_t q = bs - s;
+    if constexpr (kUA) {
 #pragma unroll
-    for (int j = 0; j < kRows; ++j) b[j] = gload128<kNT>(q + 16u * u + 1024u * j);
-    last = gload32(q + (s ? kBody : kBody - 4u));
+      for (int j = 0; j < kRows; ++j) b[j] = gload128u<kNT>(bs + 16u * u + 1024u * j);
+      last = 0;
+      (void)q;
+    } else {
+#pragma unroll
+      for (int j = 0; j < kRows; ++j) b[j] = gload128<kNT>(q + 16u * u + 1024u * j);
+      last = gload32(q + (s ? kBody : kBody - 4u));
+    }
   };
   // prefix loads of a group: row r (kRowLanes lanes) takes block r, lane w the 16 B at
   // bs - 16 kRowLanes + 16w
@@ -1785,7 +1806,7 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
           }
           part[r] = 0;
           if ((fastbits >> r) & 1u)
-            part[r] = body_partial(e, cl, static_cast<uint32_t>((G.p[r] + G.n[r]) & 3u), P[r]);
+            part[r] = body_partial(e, cl, kUA ? 0u : static_cast<uint32_t>((G.p[r] + G.n[r]) & 3u), P[r]);
         }
         uint32_t v;
         if constexpr (kBlk == 4)
@@ -1990,10 +2011,10 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
 }
 
 // kBlk = 8 (A/B): 8-block groups, prefixes <= 128 B in rows of 8 lanes, one tree8_packed.
-template <class Src, class Sink, bool kNT, int kBlk = 4, class LT = QuadTabs>
+template <class Src, class Sink, bool kNT, int kBlk = 4, class LT = QuadTabs, bool kUA = false>
 __global__ __launch_bounds__(kThreads) void crc_sst4k_kernel(const uint32_t* __restrict__ tabs, Src src,
                                                              uint64_t nblk, Sink sink) {
-  sized_kernel_body<Src, Sink, kNT, 4, false, kBlk, LT>(tabs, src, nblk, sink);
+  sized_kernel_body<Src, Sink, kNT, 4, false, kBlk, LT, kUA>(tabs, src, nblk, sink);
 }
 
 // (the 1-KiB body has no Horner fold: both images measure the same, +0.8 % for the lane-quarter

@@ -681,6 +681,15 @@ hipError_t launch_sst_variant(int v, const LaunchGeom& g, const uint32_t* d_tabl
     hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ShadowSealSink, true>), grid, block, 0, s, d_tables, src, n, k);
     return hipGetLastError();
   }
+  if (v == 70) {  // body pieces as unaligned dwordx4 loads (no neighbour dword / v_alignbyte)
+    if (seal)
+      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ParkSealSink<64>, true, 4, QuadTabs, true>), grid, block, 0, s,
+                         d_tables, src, n, ParkSealSink<64>{});
+    else
+      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstVerifySink, true, 4, QuadTabs, true>), grid, block, 0, s,
+                         d_tables, src, n, SstVerifySink{ok, nbad});
+    return hipGetLastError();
+  }
   if (v == 72 && seal) {  // the round-2 product seal: each group's trailers written when hashed
     hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SealSink, true>), grid, block, 0, s, d_tables, src, n, SealSink{});
     return hipGetLastError();

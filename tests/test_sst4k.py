@@ -176,7 +176,8 @@ def test_fixed_stride_sst_range(crc, oracle_lib, length, shift):
 
 def test_new_path_matches_previous_kernel(crc):
     """Variant 30 (diagnostics library) routes the hooks through the round-1 any-length kernel, 38
-    through the 8-block-group sized kernel: the same trailers as the shipped seal."""
+    through the 8-block-group sized kernel, 70 loads the bodies as unaligned dwordx4: the same
+    trailers as the shipped seal."""
     from pebblesdb_amd import table as T
 
     rng = np.random.Generator(np.random.PCG64(41))
@@ -187,7 +188,7 @@ def test_new_path_matches_previous_kernel(crc):
     h["offset"], h["size"] = offs, sizes
     d_h = T.handles_to_device(h)
     outs = []
-    for v in (0, 30, 38):
+    for v in (0, 30, 38, 70):
         d = torch.from_numpy(img).cuda()
         if v == 0:
             T.seal_device(d, d_h)
@@ -196,7 +197,7 @@ def test_new_path_matches_previous_kernel(crc):
         outs.append(d.cpu().numpy())
         ok, nbad = T.verify_device(d, d_h)
         assert int(nbad.item()) == 0, v
-    assert (outs[0] == outs[1]).all() and (outs[0] == outs[2]).all()
+    assert all((outs[0] == o).all() for o in outs[1:])
 
 
 @pytest.mark.parametrize("variant", [0, 88, 89, 90, 91, 92, 73, 74])
