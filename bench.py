@@ -397,13 +397,13 @@ def main():
                 "traffic_source": "profiles/pmc_traffic.json: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this "
                                   "workload (tools/profile.sh), per launch, FETCH_SIZE x2 (MI355X_MICROARCH.md)",
                 "kernel": {"c2": "crc_pack4k_kernel (lane-quarter tables)", "sstable": "crc_sst4k_kernel<FixedSrc,OutSink,nt,QuadTabs>",
-                           "c3": "crc_stream16_kernel<DescSrc,OutSink,dyn,nt,pack,QuadTabs>",
+                           "c3": "crc_stream16_kernel<DescSrc,OutSink,dyn,nt,pack,QuadTabs,bal>",
                            "wal": "crc_sst1k_kernel<DescSrc,OutSink,nt,QuadTabs>",
                            "wal100": "crc_lanespan_kernel<DescSrc,OutSink,256>",
                            "wal400": "crc_lanespan_kernel<DescSrc,OutSink,512>",
                            "wal1000": "crc_lanespan_kernel<DescSrc,OutSink,1023>",
                            "sst_verify": "crc_sst4k_kernel<SstSrc,SstVerifySink,nt,QuadTabs>",
-                           "sst_seal": "crc_sst4k_kernel<SstSrc,SealSink,nt,QuadTabs>",
+                           "sst_seal": "crc_sst4k_kernel<SstSrc,ParkSealSink<64>,nt,QuadTabs>",
                            "sst_crc": "crc_sst4k_kernel<SstSrc,SstCrcSink,nt,QuadTabs>"}[args.workload],
                 "algorithmic_bytes_per_launch": algo_bytes,
                 "kernel_avg_ms": round(kern_avg_ms, 4),
