@@ -200,3 +200,36 @@ def test_scan_readahead_matches_reference_reader(gpu, tmp_path):
                 assert (m["entries"], m["hash"], m["status"]) == (r["entries"], r["hash"], r["status"]), (p, k, where)
                 assert "block checksum mismatch" in r["status"], (p, k, where, r)
     assert batches > 0  # the read-ahead windows were used
+
+
+def test_paranoid_fill_and_verified_scan_through_readahead(gpu, tmp_path):
+    """The scan read-ahead inside the engine: fillrandom with --paranoid_checks=1 (every compaction
+    input block checked, version_set.cc:2909 -- by pdb_table.cc's windows, on the compaction
+    thread while the foreground writes) and readseq / readrandom with --verify_checksums=1 on the
+    result, against the CPU build over the same database: the same entries, scans served by
+    batches, no checksum failure, and the database CRC-clean under the oracle and the GPU
+    verifiers."""
+    exe, cpu = _exe("pdb_dbbench_gpu_table"), _exe("pdb_dbbench_cpu")
+    db = str(tmp_path / "db")
+    num = 30000
+    rc, out, err = _run([exe, "--benchmarks=fillrandom,readseq,readrandom", f"--num={num}", "--value_size=1024",
+                         "--paranoid_checks=1", "--verify_checksums=1", f"--db={db}"])
+    assert rc == 0, out + err
+    res = _bench_json(out)
+    fill, rs = res["fillrandom"], res["readseq"]
+    assert fill["hook"]["verify_failed"] == 0 and rs["hook"]["verify_failed"] == 0
+    assert rs["hook"]["scan_batches"] > 0 and rs["hook"]["scan_blocks"] > 0
+    assert f"({num} of {num} found)" in out
+    v = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "verify_db_dir.py"), "--gpu", db],
+                       capture_output=True, text=True, timeout=240)
+    assert v.returncode == 0, v.stdout + v.stderr
+    chk = json.loads(v.stdout.strip().splitlines()[-1])
+    assert chk["blocks_bad_oracle"] == 0 and chk["blocks_bad_gpu"] == 0
+    # the CPU build reads the same entries back (readseq counts the distinct keys fillrandom left)
+    rc2, out2, err2 = _run([cpu, "--use_existing_db=1", "--benchmarks=readseq", f"--num={num}", "--verify_checksums=1",
+                            f"--db={db}"])
+    assert rc2 == 0, out2 + err2
+    rc3, out3, err3 = _run([exe, "--use_existing_db=1", "--benchmarks=readseq", f"--num={num}", "--verify_checksums=1",
+                            f"--db={db}"])
+    assert rc3 == 0, out3 + err3
+    assert _bench_json(out2)["readseq"]["ops"] == _bench_json(out3)["readseq"]["ops"] == rs["ops"]
