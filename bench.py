@@ -398,7 +398,7 @@ def main():
                                   "workload (tools/profile.sh), per launch, FETCH_SIZE x2 (MI355X_MICROARCH.md)",
                 "kernel": {"c2": "crc_pack4k_kernel (lane-quarter tables)", "sstable": "crc_sst4k_kernel<FixedSrc,OutSink,nt,QuadTabs>",
                            "c3": "crc_stream16_kernel<DescSrc,OutSink,dyn,nt,pack,QuadTabs,bal>",
-                           "wal": "crc_sst1k_kernel<DescSrc,OutSink,nt,QuadTabs>",
+                           "wal": "crc_lanespan_kernel<DescSrc,OutSink,1152>",
                            "wal100": "crc_lanespan_kernel<DescSrc,OutSink,256>",
                            "wal400": "crc_lanespan_kernel<DescSrc,OutSink,512>",
                            "wal1000": "crc_lanespan_kernel<DescSrc,OutSink,1023>",

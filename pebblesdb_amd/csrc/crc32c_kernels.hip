@@ -130,12 +130,9 @@ hipError_t launch_fixed(const LaunchGeom& g, const uint32_t* d_tables, const uin
       hipLaunchKernelGGL((crc_sst4k_kernel<FixedSrc, OutSink, true>), grid, block, 0, s, d_tables, src, nblk, sink);
       return hipGetLastError();
     }
-    if (len - 1024u <= 128u) {  // 1-KiB records
-      hipLaunchKernelGGL((crc_sst1k_kernel<FixedSrc, OutSink, true>), grid, block, 0, s, d_tables, src, nblk, sink);
-      return hipGetLastError();
-    }
-    if (len - 1u <= 1022u) {  // one lane per record, bytes staged through LDS (crc32c_lanespan.h)
-      launch_lanespan(g, d_tables, src, nblk, len <= 256u ? 256u : (len <= 512u ? 512u : 1023u), sink, s);
+    if (len - 1u <= 1151u) {  // records of 1..1152 B, staged through LDS, k lanes each (crc32c_lanespan.h)
+      launch_lanespan(g, d_tables, src, nblk,
+                      len <= 256u ? 256u : (len <= 512u ? 512u : (len <= 1023u ? 1023u : 1152u)), sink, s);
       return hipGetLastError();
     }
   }
@@ -165,8 +162,9 @@ hipError_t launch_desc_sink(const LaunchGeom& g, const uint32_t* d_tables, const
   const uint32_t hint =
       flags & (PDB_CRC_SIZE_1K | PDB_CRC_SIZE_4K | PDB_CRC_SIZE_256 | PDB_CRC_SIZE_512 | PDB_CRC_SIZE_1023);
   if (hint && !(flags & PDB_CRC_USE_INIT)) {
-    if (flags & PDB_CRC_SIZE_1K)  // WAL records of ~1-KiB batches: 8-block groups, 1-KiB bodies
-      hipLaunchKernelGGL((crc_sst1k_kernel<DescSrc, Sink, true>), grid, block, 0, s, d_tables, src, nblk, sink);
+    if (flags & PDB_CRC_SIZE_1K)  // WAL records of ~1-KiB batches: the record kernel's 1152 class
+      // (+4-6 % over crc_sst1k_kernel's 8-block groups, profiles/r02_wal1k/; diagnostics variant 68)
+      launch_lanespan(g, d_tables, src, nblk, 1152u, sink, s);
     else if (flags & PDB_CRC_SIZE_4K)  // sstable data blocks: 4-KiB body + batched prefix
       hipLaunchKernelGGL((crc_sst4k_kernel<DescSrc, Sink, true>), grid, block, 0, s, d_tables, src, nblk, sink);
     else  // records of 1..1023 B: one lane per record, the bytes staged through LDS by coalesced loads

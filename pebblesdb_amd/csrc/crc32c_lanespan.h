@@ -294,7 +294,9 @@ __global__ __launch_bounds__(SpanStage<MAXN>::kWaves * 64) void crc_lanespan_ker
   typedef SpanStage<MAXN> ST;
   constexpr uint32_t LC = ST::kLC, LD = ST::kLD, NI = ST::kNI, PART = ST::kPart;
   static_assert(MAXN + 32u <= kSpanUsable, "a record of the class must fit a region");
-  constexpr uint32_t KMAX = (MAXN / 4u + PART) / PART;  // k parts cover MAXN: 2, 5, 8
+  // k parts cover MAXN: 2, 5, 8 (a longer class -- diagnostics 1152 -- stays at 8 lanes and runs
+  // the head chain alone for the rest)
+  constexpr uint32_t KMAX = (MAXN / 4u + PART) / PART > 8u ? 8u : (MAXN / 4u + PART) / PART;
   static_assert(KMAX >= 1 && KMAX <= 8, "tree folds for up to 8 lanes per record");
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
   char* lds = reinterpret_cast<char*>(lds_words);
@@ -618,8 +620,8 @@ inline uint32_t grid_span(const LaunchGeom& g, uint64_t nblk, uint32_t waves) {
   return static_cast<uint32_t>(want < g.grid ? (want ? want : 1) : g.grid);
 }
 
-// Records of 1..1023 B by class (the class bounds the lanes per record: 2, 4, 8); longer ones, and
-// empty ones, take the whole-wave path.
+// Records of 1..1152 B by class (the class bounds the lanes per record: 2, 4, 8, 8); longer ones,
+// and empty ones, take the whole-wave path.
 template <class Src, class Sink, int MODE = 0, class TP = TabsS4>
 void launch_lanespan(const LaunchGeom& g, const uint32_t* d_tables, const Src& src, uint64_t nblk, uint32_t cls,
                      const Sink& sink, hipStream_t s) {
@@ -631,9 +633,13 @@ void launch_lanespan(const LaunchGeom& g, const uint32_t* d_tables, const Src& s
     constexpr uint32_t w = SpanStage<512>::kWaves;
     hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 512, MODE, TP>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0, s,
                        d_tables, src, nblk, sink);
-  } else {
+  } else if (cls <= 1023u) {
     constexpr uint32_t w = SpanStage<1023>::kWaves;
     hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 1023, MODE, TP>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0,
+                       s, d_tables, src, nblk, sink);
+  } else {  // 1024..1152 B (WAL records of ~1-KiB write batches): 8 lanes, the head chain past 1056 B
+    constexpr uint32_t w = SpanStage<1152>::kWaves;
+    hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 1152, MODE, TP>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0,
                        s, d_tables, src, nblk, sink);
   }
 }

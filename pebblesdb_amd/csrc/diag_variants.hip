@@ -984,6 +984,17 @@ hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tab
     case 62:
       launch_lanerec(g, d_tables, src, nblk, v == 60 ? 256u : (v == 61 ? 512u : 1023u), sink, s);
       break;
+    case 68:  // records of 1024..1152 B on crc_sst1k_kernel (8-block groups): the 1K-hint routing before
+              // the record kernel's 1152 class
+      hipLaunchKernelGGL((crc_sst1k_kernel<DescSrc, OutSink, true>), grid, block, 0, s, d_tables, src, nblk, sink);
+      break;
+    case 69: {  // the record kernel's 1152 class (8 lanes of 33-word parts, the head chain alone past
+                // 1056 B) for any list: the shipped 1K-hint routing
+      constexpr uint32_t w = SpanStage<1152>::kWaves;
+      hipLaunchKernelGGL((crc_lanespan_kernel<DescSrc, OutSink, 1152>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0, s,
+                         d_tables, src, nblk, sink);
+      break;
+    }
     case 63:  // the record kernel's loads and staging alone (no hash; results undefined)
     case 64:  // the record kernel's hash alone over stale staging (no loads; results undefined)
     case 67:  // the record kernel's bookkeeping alone (no loads, no hash)

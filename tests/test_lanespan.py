@@ -1,5 +1,5 @@
 """GPU parity of the LDS-staged record kernel (crc_lanespan_kernel, pebblesdb_amd/csrc/
-crc32c_lanespan.h) behind the PDB_CRC_SIZE_256 / _512 / _1023 hints and the 1..1023-B fixed strides:
+crc32c_lanespan.h) behind the PDB_CRC_SIZE_256 / _512 / _1023 / _1K hints and the 1..1152-B fixed strides:
 bit-exact against the oracle on WAL layouts (the reference's record framing, db/log_writer.cc), on
 descriptor lists it must cut into smaller groups (spread, unsorted, duplicated, overlapping,
 far apart: the staging may only read 16-B lines within 64 B of a record byte), with records outside
@@ -12,7 +12,8 @@ pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
 
-HINTS = ["256", "512", "1023"]
+HINTS = ["256", "512", "1023", "1k"]
+CLASS = {"256": 256, "512": 512, "1023": 1023, "1k": 1152}  # the 1K hint: records of 1024..1152 B
 
 
 @pytest.fixture(scope="module")
@@ -44,7 +45,8 @@ def _check(crc, oracle_lib, base, offs, lens, hint, verify=True):
 
 @pytest.mark.parametrize("payload,hint", [(100, "256"), (131, "256"), (255, "256"), (431, "512"), (300, "512"),
                                           (511, "512"), (600, "1023"), (700, "1023"), (850, "1023"), (1000, "1023"),
-                                          (131, "1023")])
+                                          (131, "1023"), (1024, "1k"), (1055, "1k"), (1056, "1k"), (1057, "1k"),
+                                          (1100, "1k"), (1152, "1k"), (1000, "1k")])
 def test_wal_layouts(crc, oracle_lib, payload, hint):
     """Log images as log::Writer lays them out: records + 7-byte headers, fragments at 32-KiB block
     ends, block trailers; the CRC spans are type || payload."""
@@ -62,7 +64,7 @@ def test_spread_unsorted_and_far_records(crc, oracle_lib, hint):
     and overlapping records, records 1 MiB apart, records outside the class among them."""
     import oracle
 
-    cls = int(hint)
+    cls = CLASS[hint]
     rng = np.random.Generator(np.random.PCG64(cls))
     n = 6000
     lens = rng.integers(1, cls + 1, size=n)
@@ -87,7 +89,7 @@ def test_spread_unsorted_and_far_records(crc, oracle_lib, hint):
 def test_batch_boundaries(crc, oracle_lib, n):
     import oracle
 
-    for hint, L in (("256", 131), ("512", 431), ("1023", 1000)):
+    for hint, L in (("256", 131), ("512", 431), ("1023", 1000), ("1k", 1055), ("1k", 1150)):
         lens = np.full(n, L)
         lens[::7] = L - 3
         offs = np.concatenate([[3], 3 + np.cumsum(lens + 7)[:-1]])
@@ -99,10 +101,10 @@ def test_batch_boundaries(crc, oracle_lib, n):
 # 257..512 B (27-word parts) 257..324 -> 3, 325..448 -> 4, 449..512 -> 5; 513..1023 B (33-word
 # parts) 513..532 -> 4, 533..664 -> 5, 665..796 -> 6, 797..924 -> 7, 925..1023 -> 8
 @pytest.mark.parametrize("length", [1, 3, 4, 5, 17, 131, 132, 133, 255, 256, 257, 300, 431, 512, 513, 600, 700, 850,
-                                    1000, 1023])
+                                    1000, 1023, 1024, 1055, 1056, 1057, 1100, 1151, 1152])
 @pytest.mark.parametrize("shift", [0, 1, 3])
 def test_fixed_strides(crc, oracle_lib, length, shift):
-    """pdb_crc32c_batch_device_fixed with 1..1023-B blocks (the same kernel, FixedSrc)."""
+    """pdb_crc32c_batch_device_fixed with 1..1152-B blocks (the same kernel, FixedSrc)."""
     from pebblesdb_amd import diag
 
     nblk = 3001
@@ -118,12 +120,14 @@ def test_fixed_strides(crc, oracle_lib, length, shift):
 
 
 def test_matches_round1_lane_kernels(crc, oracle_lib):
-    """The round-1 direct-load kernels (diagnostics variants 60-62) give the same CRCs."""
+    """The round-1 direct-load kernels (diagnostics variants 60-62) and the previous 1-KiB kernel
+    (crc_sst1k_kernel, variant 68) give the same CRCs."""
     import oracle
     from bench import wal_layout
     from pebblesdb_amd import diag
 
-    for payload, hint, v in ((131, crc.SIZE_256, 60), (431, crc.SIZE_512, 61), (700, crc.SIZE_1023, 62)):
+    for payload, hint, v in ((131, crc.SIZE_256, 60), (431, crc.SIZE_512, 61), (700, crc.SIZE_1023, 62),
+                             (1055, crc.SIZE_1K, 68)):
         offs, lens = wal_layout(2 << 20, payload)
         base = oracle.splitmix_bytes(int(offs[-1] + lens[-1]) + 64, payload + 9)
         d_base, d_blk = torch.from_numpy(base).cuda(), crc.blocks_to_device(crc.make_blocks(offs, lens))
