@@ -33,7 +33,7 @@
  *     that hold the block's bytes.  A buffer handed to a device entry point must therefore stay
  *     readable to the 16-B boundaries around every block (any hipMalloc'd or torch allocation
  *     does); the bytes outside a block never affect its CRC.  Descriptor batches with the
- *     PDB_CRC_SIZE_256 / _512 / _1023 hints (and fixed strides of 1..1023 B) also read the gaps of
+ *     PDB_CRC_SIZE_256 / _512 / _1023 / _1K hints (and fixed strides of 1..1152 B) also read the gaps of
  *     at most 64 bytes between consecutive blocks of the list (a log image's record headers and
  *     block trailers), and only those: a larger gap, or a block out of ascending order, starts a
  *     new load run.
