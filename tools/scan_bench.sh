@@ -2,7 +2,10 @@
 # tools/scan_bench.sh -- SURVEY §8(f) row 1 in the engine: verified scans and paranoid compactions
 # with the table reader's read-ahead windows (integration/pdb_table.cc) against the engine as shipped
 # (CPU checks) and the GPU hooks over the reference's table reader (one GPU round trip per block).
-#   usage: tools/scan_bench.sh TAG NUM
+#   usage: tools/scan_bench.sh TAG NUM [FILL] [PARANOID]
+#   FILL: the benchmark that writes the scanned database (fillrandom; fillseq at 10 M: the CPU
+#   build dumped core in teardown right after a 10 M fillrandom with no read phase, compactions
+#   still backed up); PARANOID=0 skips step 3.
 #   1. one database (fillrandom, 1 KiB values) written by the CPU build;
 #   2. readseq --verify_checksums=1 over it: cpu, gpu_table_noscan, gpu_table (each twice, after an
 #      untimed pass that warms the page cache);
@@ -13,6 +16,8 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG="${1:-scan}"
 NUM="${2:-1000000}"
+FILL="${3:-fillrandom}"
+PARANOID="${4:-1}"
 OUT="gpurun_out/$TAG"
 mkdir -p "$OUT"
 DBROOT="${PDB_DB_ROOT:-/tmp}/pdb_scan_$$"
@@ -29,7 +34,7 @@ step() {  # name timeout cmd...
   if [ $rc -ne 0 ]; then echo "[scan] stopping after rc=$rc" | tee -a "$OUT/steps.txt"; exit $rc; fi
 }
 db="$DBROOT/db"
-step fill_cpu 900 $B/pdb_dbbench_cpu --benchmarks=fillrandom --num="$NUM" --value_size=1024 --db="$db"
+step fill_cpu 900 $B/pdb_dbbench_cpu --benchmarks="$FILL" --num="$NUM" --value_size=1024 --db="$db"
 step warm 600 $B/pdb_dbbench_cpu --use_existing_db=1 --benchmarks=readseq --num="$NUM" --verify_checksums=0 --db="$db"
 for r in 1 2; do
   for v in cpu gpu_table_noscan gpu_table; do
@@ -38,6 +43,7 @@ for r in 1 2; do
   done
 done
 rm -rf "$db"
+[ "$PARANOID" = 1 ] || { echo "[scan] done" | tee -a "$OUT/steps.txt"; exit 0; }
 for v in cpu gpu_table_noscan gpu_table; do
   d="$DBROOT/p_$v"
   step "paranoid_fill_$v" 1100 $B/pdb_dbbench_$v --benchmarks=fillrandom --num="$NUM" --value_size=1024 \
