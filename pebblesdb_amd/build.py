@@ -29,7 +29,6 @@ ARCH = "gfx950"
 
 SOURCES = ["crc32c_kernels.hip", "crc32c_server.hip", "crc32c_capi.cpp", "crc32c_tables.cpp"]
 DIAG_SOURCES = ["diag_variants.hip", "diag_capi.cpp", "crc32c_kernels.hip", "crc32c_tables.cpp"]
-HEADERS = ["crc32c_math.h", "crc32c_internal.h", "crc32c_device.h", "diag_device.h", "diag_internal.h"]
 INCLUDES = ["pdb_crc32c.h", "pdb_crc32c_diag.h"]
 EXPORTS = os.path.join(CSRC, "pdb_exports.map")
 
@@ -41,33 +40,45 @@ def _hipcc() -> str:
     raise RuntimeError("hipcc not found: the pebblesdb_amd HIP library cannot be built")
 
 
-def _deps_mtime() -> float:
-    deps = [os.path.join(CSRC, f) for f in HEADERS] + [os.path.join(ROOT, "include", f) for f in INCLUDES]
-    deps.append(EXPORTS)
-    return max(os.path.getmtime(d) for d in deps if os.path.exists(d))
-
-
 def _obj(src: str) -> str:
     return os.path.join(OBJDIR, os.path.splitext(src)[0] + ".o")
 
 
-def _stale(target: str, srcs) -> bool:
-    if not os.path.exists(target):
+def _deps(obj: str):
+    """Every file the object was compiled from, from the compiler's own -MMD record (so a header
+    added to an #include chain is tracked without a hand-kept list).  None if there is no record."""
+    try:
+        with open(obj + ".d") as f:
+            text = f.read().replace("\\\n", " ")
+    except OSError:
+        return None
+    _, _, rest = text.partition(":")
+    return rest.split()
+
+
+def _stale(obj: str, src: str) -> bool:
+    if not os.path.exists(obj):
         return True
-    t = os.path.getmtime(target)
-    return _deps_mtime() > t or any(os.path.getmtime(os.path.join(CSRC, s)) > t for s in srcs)
+    deps = _deps(obj)
+    if deps is None:
+        return True
+    t = os.path.getmtime(obj)
+    deps = deps + [os.path.join(CSRC, src)]
+    return any(not os.path.exists(d) or os.path.getmtime(d) > t for d in deps)
 
 
 def _compile(src: str, force: bool, verbose: bool) -> str:
     o = _obj(src)
-    if not force and not _stale(o, [src]):
+    if not force and not _stale(o, src):
         return o
     cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
-           f"-I{os.path.join(ROOT, 'include')}", "-c", os.path.join(CSRC, src), "-o", o + ".tmp"]
+           f"-I{os.path.join(ROOT, 'include')}", "-MMD", "-MF", o + ".d.tmp", "-c", os.path.join(CSRC, src),
+           "-o", o + ".tmp"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd)
     os.replace(o + ".tmp", o)
+    os.replace(o + ".d.tmp", o + ".d")
     return o
 
 
@@ -87,7 +98,8 @@ def build(force: bool = False, verbose: bool = True) -> str:
     with ThreadPoolExecutor(jobs) as ex:
         list(ex.map(lambda s: _compile(s, force, verbose), srcs))
     for target, lst in ((LIB, SOURCES), (DIAG_LIB, DIAG_SOURCES)):
-        if force or not os.path.exists(target) or any(os.path.getmtime(_obj(s)) > os.path.getmtime(target) for s in lst):
+        if (force or not os.path.exists(target) or os.path.getmtime(EXPORTS) > os.path.getmtime(target)
+                or any(os.path.getmtime(_obj(s)) > os.path.getmtime(target) for s in lst)):
             _link(target, lst, verbose)
     return LIB
 

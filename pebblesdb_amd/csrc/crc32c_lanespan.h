@@ -284,8 +284,9 @@ struct SpanItem {
 };
 
 // MODE (diagnostics only): 0 the product; 1 loads and staging without the hash; 2 the hash over
-// whatever the region holds, without the loads; 3 neither (the per-item bookkeeping alone).  TP: the
-// table scheme.
+// whatever the region holds, without the loads; 3 neither (the per-item bookkeeping alone); 4 the
+// product plus per-wave timestamps (a Sink with a `stamps` array: [start, end, items, batches] per
+// wave, s_memrealtime ticks).  TP: the table scheme.
 template <class Src, class Sink, uint32_t MAXN, int MODE = 0, class TP = TabsS4>
 __global__ __launch_bounds__(SpanStage<MAXN>::kWaves * 64) void crc_lanespan_kernel(const uint32_t* __restrict__ tabs, Src src,
                                                                        uint64_t nblk, Sink sink) {
@@ -305,6 +306,9 @@ __global__ __launch_bounds__(SpanStage<MAXN>::kWaves * 64) void crc_lanespan_ker
   const uint32_t u = threadIdx.x & 63u;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t ureg = tabs[PDB_UNSHIFT_OFF + (u & 15u)];
+  uint64_t t_start = 0;
+  uint32_t n_items = 0, n_batches = 0;
+  if constexpr (MODE == 4) t_start = wall_clock64();
   __syncthreads();
   const typename TP::LT lt = TP::lane(u);
   char* region = lds + kSpanStageBase + wv * kSpanRegion;
@@ -370,6 +374,7 @@ __global__ __launch_bounds__(SpanStage<MAXN>::kWaves * 64) void crc_lanespan_ker
     const uint32_t nw = wave_max_u32(bfast ? (bn + 3u) >> 2 : 0u);
     bg = span_pick<KMAX, ST>(nw ? nw : 1u);
     bcursor = 0;
+    if constexpr (MODE == 4) ++n_batches;
     return true;
   };
 
@@ -449,7 +454,7 @@ __global__ __launch_bounds__(SpanStage<MAXN>::kWaves * 64) void crc_lanespan_ker
   auto issue = [&](u32x4 (&A)[kSpanJ], const SpanItem& it) {
     const uint32_t lo_l = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(it.lo));
     const uint32_t lo_h = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(static_cast<uint64_t>(it.lo) >> 32));
-    const uint32_t nb = MODE >= 2 ? 16u : __builtin_amdgcn_readfirstlane(it.hi ? (it.hi + 15u) & ~15u : 16u);
+    const uint32_t nb = (MODE == 2 || MODE == 3) ? 16u : __builtin_amdgcn_readfirstlane(it.hi ? (it.hi + 15u) & ~15u : 16u);
     void* base = reinterpret_cast<void*>((static_cast<uint64_t>(lo_h) << 32) | lo_l);
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(base, 0, static_cast<int>(nb), 0x00020000);
 #pragma unroll
@@ -465,6 +470,7 @@ __global__ __launch_bounds__(SpanStage<MAXN>::kWaves * 64) void crc_lanespan_ker
   };
   // hash an item staged in the region
   auto hash = [&](const SpanItem& it) {
+    if constexpr (MODE == 4) ++n_items;
     if (it.hi == 0 || MODE == 1 || MODE == 3) return;
     // chain X (A, B, C, D = 0..3) works from phase-2 step F[X] on; its word at step t is the one
     // ending 4 (NI - t) bytes before the chain's end
@@ -611,6 +617,16 @@ __global__ __launch_bounds__(SpanStage<MAXN>::kWaves * 64) void crc_lanespan_ker
     to_lds(A);
     I0 = I2;
     I1 = I3;
+  }
+  if constexpr (MODE == 4) {
+    const uint64_t t_end = wall_clock64();
+    if (u == 0) {
+      uint64_t* st = sink.stamps + 4u * (static_cast<uint64_t>(blockIdx.x) * kSpanWaves + wv);
+      st[0] = t_start;
+      st[1] = t_end;
+      st[2] = n_items;
+      st[3] = n_batches;
+    }
   }
 }
 

@@ -11,6 +11,11 @@
 namespace pdb {
 namespace {
 
+// variant 110: the record kernel with per-wave timestamps, stored after the CRCs in `out`
+struct StampOutSink : OutSink {
+  uint64_t* stamps;
+};
+
 __device__ __forceinline__ uint64_t splitmix64_at(uint64_t seed, uint64_t i) {
   uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -993,6 +998,17 @@ hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tab
       constexpr uint32_t w = SpanStage<1152>::kWaves;
       hipLaunchKernelGGL((crc_lanespan_kernel<DescSrc, OutSink, 1152>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0, s,
                          d_tables, src, nblk, sink);
+      break;
+    }
+    case 110: {  // the shipped record kernel + per-wave [start, end, items, batches] stamps (s_memrealtime)
+                 // at out + nblk rounded up to 8 B: the caller sizes `out` for 4 x 8 B per wave
+      const uint32_t cls = (flags & PDB_CRC_SIZE_256) ? 256u
+                           : (flags & PDB_CRC_SIZE_512) ? 512u : ((flags & PDB_CRC_SIZE_1K) ? 1152u : 1023u);
+      StampOutSink ss;
+      ss.out = out;
+      ss.flags = flags;
+      ss.stamps = reinterpret_cast<uint64_t*>(out + ((nblk + 1u) & ~1ull));
+      launch_lanespan<DescSrc, StampOutSink, 4>(g, d_tables, src, nblk, cls, ss, s);
       break;
     }
     case 63:  // the record kernel's loads and staging alone (no hash; results undefined)

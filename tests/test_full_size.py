@@ -75,3 +75,32 @@ def test_full_size_sst_seal_verify_vs_oracle(crc, oracle_lib):
     ok, nbad = T.verify_device(d, d_h)
     okh = ok.cpu().numpy()
     assert int(nbad.item()) == len(victims) and (np.nonzero(okh == 0)[0] == victims).all()
+
+
+def test_full_size_c4_shard_vs_oracle(crc, oracle_lib):
+    """BASELINE config 4 is 128 GiB of 4 KiB blocks over 8 GPUs: each rank hashes 4,194,304
+    blocks (16 GiB) of the one global splitmix image, starting at byte lo * 4096 (bench.py
+    --nblk 4194304 under the launcher).  Rank 7's shard -- the one furthest into the image, where
+    block offsets and the generator's byte offset pass 112 GiB -- every CRC against the oracle."""
+    import oracle
+    from pebblesdb_amd import diag
+    from pebblesdb_amd.shard import block_range
+
+    per_gpu, world, rank = 1 << 22, 8, 7
+    lo, hi = block_range(per_gpu * world, world, rank)
+    assert hi - lo == per_gpu
+    d = torch.empty(per_gpu * 4096, dtype=torch.uint8, device="cuda")
+    diag.fill_splitmix(d, 301, byte_offset=lo * 4096)
+    got = crc.batch_fixed(d, 4096, 4096, per_gpu).cpu().numpy().view(np.uint32)
+    host = d.cpu().numpy()
+    del d
+    torch.cuda.empty_cache()
+    # the device generator produced the global image's bytes at this offset
+    for k in (0, per_gpu // 2, per_gpu - 1):
+        exp_bytes = oracle.splitmix_bytes(4096, 301, (lo + k) * 4096)
+        assert (host[k * 4096:(k + 1) * 4096] == exp_bytes).all()
+    blk = np.zeros(per_gpu, dtype=oracle.BLK_DTYPE)
+    blk["off"] = np.arange(per_gpu, dtype=np.int64) * 4096
+    blk["len"] = 4096
+    exp = oracle_lib.batch(host, blk, nthreads=16)
+    assert (got == exp).all(), int(np.count_nonzero(got != exp))

@@ -130,6 +130,42 @@ def test_gloo_world2_bench_c3_byte_balanced():
     assert abs(total - world * (64 << 20)) <= 64 * 1024
 
 
+def _bench_cmd(*extra):
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    return [sys.executable, os.path.join(root, "bench.py"), *extra], root
+
+
+def test_bench_gpus2_without_launcher_runs_two_ranks():
+    """The driver's BENCH form `python bench.py --gpus N` (no torchrun): bench.py must re-launch
+    itself as N ranks, not silently measure one.  --dry-run keeps it on the CPU (gloo, no kernel)."""
+    import json
+    import subprocess
+
+    cmd, root = _bench_cmd("--gpus", "2", "--steps", "3", "--warmup", "1", "--dry-run", "--nblk", "1000")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                            "MASTER_PORT", "LOCAL_WORLD_SIZE")}
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=root, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith('{"metric"')]
+    assert len(lines) == 1  # rank 0 only
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["world_size"] == 2 and line["dry_run"] is True
+    assert [x["rank"] for x in line["ranks"]] == [0, 1]
+    assert [x["blocks"] for x in line["ranks"]] == [1000, 1000]
+
+
+@pytest.mark.parametrize("gpus,world", [(1, "2"), (8, "4")])
+def test_bench_gpus_world_size_mismatch_fails(gpus, world):
+    import subprocess
+
+    cmd, root = _bench_cmd("--gpus", str(gpus), "--dry-run")
+    env = dict(os.environ, WORLD_SIZE=world, RANK="0", LOCAL_RANK="0")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=120, cwd=root, env=env)
+    assert r.returncode == 2 and "WORLD_SIZE" in r.stderr
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("workload", ["c2", "c3"])
 def test_bench_main_two_ranks_on_the_gpu(oracle_lib, workload):
@@ -146,11 +182,15 @@ def test_bench_main_two_ranks_on_the_gpu(oracle_lib, workload):
         pytest.skip("no GPU")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     nblk, c3_bytes = 4096, 48 << 20
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
-           "--gpus", "2", "--steps", "3", "--warmup", "1", "--settle", "0", "--backend", "gloo",
-           "--workload", workload, "--nblk", str(nblk), "--c3-bytes", str(c3_bytes), "--no-cpu-baseline"]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=root)
+    # c2 under the driver's torchrun form, c3 through bench.py's own re-launch (`--gpus 2`, no launcher)
+    launcher = ([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                 "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] if workload == "c2"
+                else [sys.executable])
+    cmd = launcher + [os.path.join(root, "bench.py"),
+                      "--gpus", "2", "--steps", "3", "--warmup", "1", "--settle", "0", "--backend", "gloo",
+                      "--workload", workload, "--nblk", str(nblk), "--c3-bytes", str(c3_bytes), "--no-cpu-baseline"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=root, env=env)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith('{"metric"')][-1])
     assert line["n_gpus"] == 2 and line["world_size"] == 2 and line["steps"] == 3
