@@ -27,6 +27,9 @@ namespace log {
 static const uint64_t kBlockSize = 32768;  // log_format.h:27
 static const uint64_t kHeaderSize = 7;     // log_format.h:30: checksum (4), length (2), type (1)
 enum RecordType { kZeroType = 0, kFullType = 1, kFirstType = 2, kMiddleType = 3, kLastType = 4 };
+// log::Reader's extra return values kEof / kBadRecord (log_reader.h:78-84): a record whose type byte
+// holds one of them (CRC valid) takes that path in ReadRecord
+static const uint8_t kEofValue = 5, kBadRecordValue = 6;
 
 struct PhysicalRecord {
   uint64_t offset;  // header offset in the file
@@ -131,6 +134,8 @@ struct LogicalRecord {
 struct CorruptionReport {
   uint64_t bytes;      // what the Reporter is told
   std::string reason;  // "Corruption: <message>" (Status::ToString)
+  uint64_t before;     // logical records delivered before it: the reader reports it from inside the
+                       // ReadRecord call that returns record `before` (or the final, failing call)
 };
 
 // What log::Reader::ReadRecord (log_reader.cc:59-164; checksums on, initial offset 0) delivers from
@@ -147,7 +152,7 @@ inline void ReplayItems(const char* image, uint64_t n, const std::vector<LogItem
   uint64_t prospective = 0, pos = 0, dead_block = UINT64_MAX;
   size_t ri = 0;  // index of the next record verdict
   auto report = [&](uint64_t bytes, const std::string& why) {
-    reports->push_back(CorruptionReport{bytes, "Corruption: " + why});
+    reports->push_back(CorruptionReport{bytes, "Corruption: " + why, static_cast<uint64_t>(out->size())});
   };
   auto bad_record = [&]() {  // kBadRecord in ReadRecord (log_reader.cc:143-149)
     if (in_frag) {
@@ -207,11 +212,19 @@ inline void ReplayItems(const char* image, uint64_t n, const std::vector<LogItem
           in_frag = false;
         }
         break;
-      default:
-        report(r.length + (in_frag ? scratch.size() : 0), "unknown record type " + std::to_string(r.type));
+      case kEofValue:  // ReadRecord returns false: the reader stops here (log_reader.cc:133-141)
+        return;
+      case kBadRecordValue:  // log_reader.cc:143-149
+        bad_record();
+        break;
+      default: {
+        // header[6] is a char read into an unsigned int (log_reader.cc:212): 0x80.. print as 42949671xx
+        const unsigned t = static_cast<unsigned>(static_cast<int>(static_cast<signed char>(r.type)));
+        report(r.length + (in_frag ? scratch.size() : 0), "unknown record type " + std::to_string(t));
         in_frag = false;
         scratch.clear();
         break;
+      }
     }
   }
   (void)n;

@@ -195,6 +195,30 @@ inline bool ReadTableLayout(const char* image, uint64_t len, TableLayout* t, std
   return true;
 }
 
+// The data-block handles of a table image: footer -> index block entries, nothing else read and
+// no checksum checked -- the blocks leveldb-verify's verified iterator reads (Table::Open reads the
+// index with default ReadOptions, i.e. unchecked, table.cc:97-101, and with default Options never
+// reads the metaindex or filter, table.cc:130-133).  False + *err on a structural problem.
+inline bool ReadDataHandles(const char* image, uint64_t len, std::vector<BlockHandle>* data, std::string* err) {
+  if (len < kFooterEncodedLength) return *err = "file is too short to be an sstable", false;
+  const char* f = image + len - kFooterEncodedLength;
+  uint32_t lo, hi;
+  memcpy(&lo, f + kFooterEncodedLength - 8, 4);
+  memcpy(&hi, f + kFooterEncodedLength - 4, 4);
+  if (((static_cast<uint64_t>(hi) << 32) | lo) != kTableMagicNumber)
+    return *err = "not an sstable (bad magic number)", false;
+  const char* p = f;
+  BlockHandle metaindex, index;
+  if (!DecodeHandle(&p, f + 2 * kMaxEncodedHandleLength, &metaindex) ||
+      !DecodeHandle(&p, f + 2 * kMaxEncodedHandleLength, &index))
+    return *err = "bad block handle", false;
+  if (index.offset > len || index.size > len - index.offset || len - index.offset - index.size < kBlockTrailerSize)
+    return *err = "truncated block read", false;
+  if (image[index.offset + index.size] != 0) return *err = "compressed index block", false;
+  data->clear();
+  return BlockValues(image + index.offset, index.size, data, err);
+}
+
 // leveldb-verify for one table image: every block's checksum in one GPU batch.  Returns the
 // number of bad blocks (>= 0), a negative PDB_E* code, or -1000 with *err set when the table's
 // structure (footer / index / metaindex) is corrupt -- a corrupt index or metaindex block is

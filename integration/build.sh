@@ -15,7 +15,8 @@
 #   sstwriter_gpu          oracle/ref_sstwriter.cc over the GPU hooks (golden-table parity test)
 #   leveldb_verify_ref     the reference's own src/leveldb-verify.cc over the engine as shipped
 #   pdb_verify_gpu         integration/pdb_verify.cc: the same tool with every checksum of a file
-#                          checked in one GPU batch (pdb::VerifyTable / pdb::log::ReplayLog)
+#                          checked in one GPU batch (data blocks / pdb::log::ReplayLog), over the
+#                          engine with pdb_format.cc (a damaged table's walk checks on the GPU too)
 #   table_scan_ref / _gpu  integration/pdb_table_scan.cc: one verified scan of a table through the
 #                          reference's table reader / pdb_table.cc (parity of what a reader sees)
 set -euo pipefail
@@ -83,7 +84,8 @@ $CXX -o "$B/pdb_dbbench_gpu_table_noscan" "$B/obj_hooks/dbbench_hooks.o" $HOOKS_
 $CXX -o "$B/pdb_dbbench_gpu_all" "$B/obj_hooks/dbbench_hooks.o" $HOOKS $(objs "$B/obj_shim" $ENGINE) $GPU
 $CXX -o "$B/sstwriter_gpu" "$B/obj_hooks/sstwriter.o" $HOOKS $(objs "$B/obj_ref" $ENGINE util/crc32c.cc) $GPU
 $CXX -o "$B/leveldb_verify_ref" $(objs "$B/obj_ref" leveldb-verify.cc $ENGINE $TABLE_REF util/crc32c.cc)
-$CXX -o "$B/pdb_verify_gpu" "$B/obj_hooks/pdb_verify.o" $(objs "$B/obj_ref" $ENGINE $TABLE_REF util/crc32c.cc) $GPU
+$CXX -o "$B/pdb_verify_gpu" "$B/obj_hooks/pdb_verify.o" "$B/obj_hooks/pdb_format.o" \
+  $(objs "$B/obj_ref" $ENGINE table/table_builder.cc table/table.cc util/crc32c.cc) $GPU
 $CXX -o "$B/table_scan_ref" "$B/obj_hooks/table_scan_ref.o" $(objs "$B/obj_ref" $ENGINE $TABLE_REF util/crc32c.cc)
 $CXX -o "$B/table_scan_gpu" "$B/obj_hooks/table_scan_gpu.o" $HOOKS $(objs "$B/obj_ref" $ENGINE util/crc32c.cc) $GPU
 echo "built $B/{table_scan_ref,table_scan_gpu,pdb_dbbench_cpu,pdb_dbbench_gpu_table,pdb_dbbench_gpu_table_noscan,pdb_dbbench_gpu_all,sstwriter_gpu,leveldb_verify_ref,pdb_verify_gpu}"

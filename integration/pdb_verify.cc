@@ -3,14 +3,19 @@
 // leveldb-verify), built against the engine compiled from the reference sources in place.
 //
 // For each file on the command line, by its name (db/filename.h ParseFileName):
-//   * table (.sst / .ldb): the whole file is read, pdb::VerifyTable checks every block's trailer
-//     (index and metaindex first, then all data / meta blocks: one pdb_sst_verify_host call), and
-//     the reference tool's structural walk follows -- every key parsed as an internal key and
-//     looked up again through a second iterator (leveldb-verify.cc:142-164) -- with per-block
-//     checksums off, since every block was verified up front;
+//   * table (.sst / .ldb): Table::Open as the reference tool does it, then every data block the
+//     tool's verified iterator reads (the index block's handles) is checked in ONE
+//     pdb_sst_verify_host call, and the reference tool's walk follows -- every key parsed as an
+//     internal key and looked up again through a second iterator (leveldb-verify.cc:142-168) --
+//     with per-block checksums off when every block passed, on when one failed (so the engine's
+//     ReadBlock, checked on the GPU by pdb_format.cc, reports each bad block where the reference
+//     does).  Index, metaindex and filter blocks are not checked: the reference tool never checks
+//     them (table.cc:97-133 reads the index with default ReadOptions, the others not at all);
 //   * log / MANIFEST: pdb::ReplayLog checks every physical record in one batch and replays the
 //     logical records with the reference log::Reader's drop / report rules; each record is then
-//     decoded the way the reference tool does (a WriteBatch iterated / a VersionEdit decoded).
+//     decoded the way the reference tool does (a WriteBatch iterated / a VersionEdit decoded), each
+//     corruption report printed where the reference reader prints it (before the record whose
+//     ReadRecord call found it).
 // Output and exit status follow the reference tool: problems go to stdout / stderr in its words
 // ("corruption: N bytes; ...", "iterator error: Corruption: block checksum mismatch", ...), the
 // exit status is 1 when a file could not be handled.  --timing prints each phase's wall time.
@@ -74,11 +79,19 @@ bool VerifyLogFile(leveldb::Env* env, const std::string& fname, bool descriptor)
     fprintf(stderr, "%s: device error %lld: %s\n", fname.c_str(), static_cast<long long>(rc), pdb_last_error());
     return false;
   }
-  for (const auto& r : reports) printf("corruption: %d bytes; %s\n", static_cast<int>(r.bytes), r.reason.c_str());
+  // reports are printed where the reference reader prints them: from inside the ReadRecord call
+  // that returns record r.before, i.e. before that record's own output
   t0 = Clock::now();
   g_records += recs.size();
-  for (const auto& r : recs) {
-    const leveldb::Slice rec(r.data);
+  size_t next_report = 0;
+  auto flush_reports = [&](uint64_t upto) {
+    for (; next_report < reports.size() && reports[next_report].before <= upto; ++next_report)
+      printf("corruption: %d bytes; %s\n", static_cast<int>(reports[next_report].bytes),
+             reports[next_report].reason.c_str());
+  };
+  for (size_t i = 0; i < recs.size(); ++i) {
+    flush_reports(i);
+    const leveldb::Slice rec(recs[i].data);
     if (descriptor) {
       leveldb::VersionEdit edit;
       leveldb::Status s = edit.DecodeFrom(rec);
@@ -93,6 +106,7 @@ bool VerifyLogFile(leveldb::Env* env, const std::string& fname, bool descriptor)
       if (!s.ok()) fprintf(stderr, "error: %s\n", s.ToString().c_str());
     }
   }
+  flush_reports(UINT64_MAX);
   g_walk_s += Since(t0);
   return true;
 }
@@ -100,29 +114,8 @@ bool VerifyLogFile(leveldb::Env* env, const std::string& fname, bool descriptor)
 bool VerifyTableFile(leveldb::Env* env, const std::string& fname) {
   std::string img;
   if (!ReadWhole(env, fname, &img)) return false;
-  pdb::TableLayout layout;
-  std::vector<uint8_t> ok;
-  std::string err;
+  // Table::Open exactly as the reference tool: footer + index block, unchecked (ReadOptions())
   auto t0 = Clock::now();
-  const int64_t bad = pdb::VerifyTable(img.data(), img.size(), &layout, &ok, &err);
-  g_crc_s += Since(t0);
-  if (bad == -1000) {  // footer / index / metaindex: the reference fails in Table::Open with this status
-    const bool arg = err.rfind("file is too short", 0) == 0 || err.rfind("not an sstable", 0) == 0;
-    fprintf(stderr, "%s: %s\n", arg ? "Invalid argument" : "Corruption", err.c_str());
-    return false;
-  }
-  if (bad < 0) {
-    fprintf(stderr, "%s: device error %lld: %s\n", fname.c_str(), static_cast<long long>(bad), pdb_last_error());
-    return false;
-  }
-  g_blocks += ok.size();
-  if (bad > 0) {
-    // the reference iterator stops at the first bad data block with this status
-    fprintf(stderr, "iterator error: Corruption: block checksum mismatch\n");
-    return true;
-  }
-  // the structural walk, checksums already checked
-  t0 = Clock::now();
   leveldb::RandomAccessFile* file = nullptr;
   leveldb::Table* table = nullptr;
   leveldb::Status s = env->NewRandomAccessFile(fname, &file);
@@ -133,24 +126,49 @@ bool VerifyTableFile(leveldb::Env* env, const std::string& fname) {
     delete file;
     return false;
   }
-  leveldb::ReadOptions ro;
-  ro.verify_checksums = false;
-  leveldb::Iterator* it = table->NewIterator(ro);
-  leveldb::Iterator* again = table->NewIterator(ro);
-  for (it->SeekToFirst(); it->Valid(); it->Next()) {
-    leveldb::ParsedInternalKey k;
-    if (!leveldb::ParseInternalKey(it->key(), &k)) {
-      fprintf(stderr, "badkey '%s' => '%s'\n", leveldb::EscapeString(it->key()).c_str(),
-              leveldb::EscapeString(it->value()).c_str());
-      continue;
+  g_walk_s += Since(t0);
+  // every data block the tool's verified iterator would read, checked in ONE GPU batch
+  t0 = Clock::now();
+  std::vector<pdb::BlockHandle> data;
+  std::vector<uint8_t> ok;
+  std::string err;
+  int64_t bad = 1;  // an index the walk cannot parse: let the engine's own reads report it
+  if (pdb::ReadDataHandles(img.data(), img.size(), &data, &err)) {
+    bad = pdb::VerifyBlocks(img.data(), img.size(), data.data(), data.size(), &ok);
+    if (bad < 0) {
+      fprintf(stderr, "%s: device error %lld: %s\n", fname.c_str(), static_cast<long long>(bad), pdb_last_error());
+      delete table;
+      delete file;
+      return false;
     }
-    again->SeekToFirst();
-    again->Seek(k.user_key);
-    if (!again->status().ok()) fprintf(stderr, "bad iteration %s\n", again->status().ToString().c_str());
+    g_blocks += data.size();
   }
-  if (!it->status().ok()) fprintf(stderr, "iterator error: %s\n", it->status().ToString().c_str());
-  delete it;
-  delete again;
+  g_crc_s += Since(t0);
+  // The reference tool's walk (leveldb-verify.cc:142-168), statement for statement.  Clean table:
+  // per-block checksums off, every one was just checked.  A damaged one: checksums on, so the
+  // engine's own ReadBlock (pdb_format.cc: the check on the GPU) reports each bad block exactly
+  // where the reference's iterator does -- skipped blocks, "bad iteration" per later key, the final
+  // "iterator error".
+  t0 = Clock::now();
+  leveldb::ReadOptions ro;
+  ro.verify_checksums = bad != 0;
+  leveldb::Iterator* iter = table->NewIterator(ro);
+  leveldb::Iterator* verify = table->NewIterator(ro);
+  for (iter->SeekToFirst(); iter->Valid(); iter->Next()) {
+    if (!iter->status().ok()) fprintf(stderr, "bad iteration %s\n", iter->status().ToString().c_str());
+    leveldb::ParsedInternalKey key;
+    if (!leveldb::ParseInternalKey(iter->key(), &key))
+      fprintf(stderr, "badkey '%s' => '%s'\n", leveldb::EscapeString(iter->key()).c_str(),
+              leveldb::EscapeString(iter->value()).c_str());
+    verify->SeekToFirst();
+    if (!verify->status().ok()) fprintf(stderr, "bad iteration %s\n", verify->status().ToString().c_str());
+    verify->Seek(key.user_key);
+    if (!verify->status().ok()) fprintf(stderr, "bad iteration %s\n", verify->status().ToString().c_str());
+  }
+  s = iter->status();
+  if (!s.ok()) fprintf(stderr, "iterator error: %s\n", s.ToString().c_str());
+  delete iter;
+  delete verify;
   delete table;
   delete file;
   g_walk_s += Since(t0);

@@ -287,7 +287,9 @@ struct SpanItem {
 // whatever the region holds, without the loads; 3 neither (the per-item bookkeeping alone); 4 the
 // product plus per-wave timestamps (a Sink with a `stamps` array: [start, end, items, batches] per
 // wave, s_memrealtime ticks).  TP: the table scheme.
-template <class Src, class Sink, uint32_t MAXN, int MODE = 0, class TP = TabsS4>
+// kDyn: the workgroup owns batches [g nbat / G, (g + 1) nbat / G) and its waves take the next one
+// from an LDS counter (false: batch wave_id + k W, the round-2 static assignment -- diagnostics).
+template <class Src, class Sink, uint32_t MAXN, int MODE = 0, class TP = TabsS4, bool kDyn = true>
 __global__ __launch_bounds__(SpanStage<MAXN>::kWaves * 64) void crc_lanespan_kernel(const uint32_t* __restrict__ tabs, Src src,
                                                                        uint64_t nblk, Sink sink) {
   constexpr uint32_t kSpanWaves = SpanStage<MAXN>::kWaves, kSpanJ = SpanStage<MAXN>::kJ;
@@ -309,14 +311,23 @@ __global__ __launch_bounds__(SpanStage<MAXN>::kWaves * 64) void crc_lanespan_ker
   uint64_t t_start = 0;
   uint32_t n_items = 0, n_batches = 0;
   if constexpr (MODE == 4) t_start = wall_clock64();
+  // the work counter: the last 16 B of the last wave's region, which no item ever uses (spans end
+  // by kUsable) and to_lds skips
+  uint32_t* ctr = reinterpret_cast<uint32_t*>(lds + kSpanStageBase + kSpanWaves * kSpanRegion - 16u);
+  if (kDyn && threadIdx.x == 0) *ctr = 2u * kSpanWaves;  // tickets wv and kWaves + wv are taken below
   __syncthreads();
   const typename TP::LT lt = TP::lane(u);
   char* region = lds + kSpanStageBase + wv * kSpanRegion;
   const uintptr_t dummy = reinterpret_cast<uintptr_t>(tabs);  // >= 4 KiB + 256 B of valid bytes
   const uint64_t nbat = (nblk + 63u) >> 6;
   const uint64_t W = static_cast<uint64_t>(gridDim.x) * kSpanWaves;
-  uint64_t bnext = static_cast<uint64_t>(blockIdx.x) * kSpanWaves + wv;  // next batch to open
-  if (bnext >= nbat) return;  // wave-uniform; no barrier below
+  // kDyn: this workgroup's batches; the next batch to open and the ticket after it (taken one
+  // batch early, so the LDS atomic's latency never sits in front of a descriptor load)
+  const uint64_t g_lo = kDyn ? nbat * blockIdx.x / gridDim.x : 0;
+  const uint64_t g_end = kDyn ? nbat * (blockIdx.x + 1) / gridDim.x : nbat;
+  uint64_t bnext = kDyn ? g_lo + wv : static_cast<uint64_t>(blockIdx.x) * kSpanWaves + wv;  // next batch to open
+  uint32_t tick = kSpanWaves + wv;  // kDyn: the batch after it, relative to g_lo (lane 0's VGPR)
+  if (bnext >= g_end) return;  // wave-uniform; no barrier below
 
   auto idx = [&](uint64_t bb) -> uint64_t {
     const uint64_t i = (bb << 6) + u;
@@ -340,12 +351,17 @@ __global__ __launch_bounds__(SpanStage<MAXN>::kWaves * 64) void crc_lanespan_ker
   // make the prefetched batch current; records outside the class are hashed here by the whole
   // wave (rare: their loads wait behind the items in flight)
   auto open_batch = [&]() -> bool {
-    if (bnext >= nbat) return false;
+    if (bnext >= g_end) return false;
     keep_alive(raw_next);
     const BlkDesc d = src.lane(raw_next);
     bpre = pre_next;
     bcur = bnext;
-    bnext += W;
+    if constexpr (kDyn) {
+      bnext = g_lo + __builtin_amdgcn_readfirstlane(tick);
+      if (u == 0) tick = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else {
+      bnext += W;
+    }
     const uint64_t i = (bcur << 6) + u;
     const bool valid = i < nblk;
     bp = reinterpret_cast<uintptr_t>(d.p);
@@ -400,8 +416,8 @@ __global__ __launch_bounds__(SpanStage<MAXN>::kWaves * 64) void crc_lanespan_ker
       have_batch = true;
       rem = bfastm;
     }
-    raw_next = src.load_cached(idx(bnext < nbat ? bnext : bcur));
-    pre_next = SinkOps<Sink>::pre(sink, idx(bnext < nbat ? bnext : bcur), BlkDesc{nullptr, 0u, 0u});
+    raw_next = src.load_cached(idx(bnext < g_end ? bnext : bcur));
+    pre_next = SinkOps<Sink>::pre(sink, idx(bnext < g_end ? bnext : bcur), BlkDesc{nullptr, 0u, 0u});
     it.valid = true;
     it.batch = bcur;
     it.k = bg.k;
@@ -466,7 +482,9 @@ __global__ __launch_bounds__(SpanStage<MAXN>::kWaves * 64) void crc_lanespan_ker
   // outstanding, and the compiler then drains the counter before the register is reloaded
   auto to_lds = [&](const u32x4 (&A)[kSpanJ]) {
 #pragma unroll
-    for (uint32_t j = 0; j < kSpanJ; ++j) *reinterpret_cast<u32x4*>(region + 1024u * j + 16u * u) = A[j];
+    for (uint32_t j = 0; j + 1 < kSpanJ; ++j) *reinterpret_cast<u32x4*>(region + 1024u * j + 16u * u) = A[j];
+    if (!kDyn || wv + 1u < kSpanWaves || u != 63u)  // the last 16 B of the LDS: the work counter
+      *reinterpret_cast<u32x4*>(region + 1024u * (kSpanJ - 1u) + 16u * u) = A[kSpanJ - 1u];
   };
   // hash an item staged in the region
   auto hash = [&](const SpanItem& it) {
@@ -638,24 +656,24 @@ inline uint32_t grid_span(const LaunchGeom& g, uint64_t nblk, uint32_t waves) {
 
 // Records of 1..1152 B by class (the class bounds the lanes per record: 2, 4, 8, 8); longer ones,
 // and empty ones, take the whole-wave path.
-template <class Src, class Sink, int MODE = 0, class TP = TabsS4>
+template <class Src, class Sink, int MODE = 0, class TP = TabsS4, bool kDyn = true>
 void launch_lanespan(const LaunchGeom& g, const uint32_t* d_tables, const Src& src, uint64_t nblk, uint32_t cls,
                      const Sink& sink, hipStream_t s) {
   if (cls <= 256u) {
     constexpr uint32_t w = SpanStage<256>::kWaves;
-    hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 256, MODE, TP>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0, s,
+    hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 256, MODE, TP, kDyn>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0, s,
                        d_tables, src, nblk, sink);
   } else if (cls <= 512u) {
     constexpr uint32_t w = SpanStage<512>::kWaves;
-    hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 512, MODE, TP>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0, s,
+    hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 512, MODE, TP, kDyn>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0, s,
                        d_tables, src, nblk, sink);
   } else if (cls <= 1023u) {
     constexpr uint32_t w = SpanStage<1023>::kWaves;
-    hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 1023, MODE, TP>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0,
+    hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 1023, MODE, TP, kDyn>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0,
                        s, d_tables, src, nblk, sink);
   } else {  // 1024..1152 B (WAL records of ~1-KiB write batches): 8 lanes, the head chain past 1056 B
     constexpr uint32_t w = SpanStage<1152>::kWaves;
-    hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 1152, MODE, TP>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0,
+    hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 1152, MODE, TP, kDyn>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0,
                        s, d_tables, src, nblk, sink);
   }
 }

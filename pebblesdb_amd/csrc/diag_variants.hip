@@ -1000,15 +1000,23 @@ hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tab
                          d_tables, src, nblk, sink);
       break;
     }
-    case 110: {  // the shipped record kernel + per-wave [start, end, items, batches] stamps (s_memrealtime)
-                 // at out + nblk rounded up to 8 B: the caller sizes `out` for 4 x 8 B per wave
+    case 110:    // the shipped record kernel + per-wave [start, end, items, batches] stamps (s_memrealtime)
+    case 112: {  // at out + nblk rounded up to 8 B (the caller sizes `out` for 4 x 8 B per wave); 112:
+                 // the round-2 static batch assignment (no workgroup counter)
       const uint32_t cls = (flags & PDB_CRC_SIZE_256) ? 256u
                            : (flags & PDB_CRC_SIZE_512) ? 512u : ((flags & PDB_CRC_SIZE_1K) ? 1152u : 1023u);
       StampOutSink ss;
       ss.out = out;
       ss.flags = flags;
       ss.stamps = reinterpret_cast<uint64_t*>(out + ((nblk + 1u) & ~1ull));
-      launch_lanespan<DescSrc, StampOutSink, 4>(g, d_tables, src, nblk, cls, ss, s);
+      if (v == 110) launch_lanespan<DescSrc, StampOutSink, 4>(g, d_tables, src, nblk, cls, ss, s);
+      else launch_lanespan<DescSrc, StampOutSink, 4, TabsS4, false>(g, d_tables, src, nblk, cls, ss, s);
+      break;
+    }
+    case 111: {  // the record kernel with the round-2 static batch assignment (batch wave_id + k W)
+      const uint32_t cls = (flags & PDB_CRC_SIZE_256) ? 256u
+                           : (flags & PDB_CRC_SIZE_512) ? 512u : ((flags & PDB_CRC_SIZE_1K) ? 1152u : 1023u);
+      launch_lanespan<DescSrc, OutSink, 0, TabsS4, false>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
       break;
     }
     case 63:  // the record kernel's loads and staging alone (no hash; results undefined)

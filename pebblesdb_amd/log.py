@@ -23,6 +23,9 @@ from . import crc32c
 K_BLOCK_SIZE = 32768  # log_format.h:27
 K_HEADER_SIZE = 7  # log_format.h:30: checksum (4), length (2), type (1)
 K_ZERO, K_FULL, K_FIRST, K_MIDDLE, K_LAST = 0, 1, 2, 3, 4  # log_format.h:14-24
+# log::Reader's extra return values kEof = kMaxRecordType + 1, kBadRecord = + 2 (log_reader.h:78-84):
+# a record whose type byte holds one of them (and a valid CRC) takes that path in ReadRecord
+K_EOF_VALUE, K_BADRECORD_VALUE = 5, 6
 
 
 class LogCorruption(Exception):
@@ -187,8 +190,13 @@ def replay_log(image, checksum: bool = True, ok=None) -> LogReplay:
             else:
                 out.append((prospective, scratch + frag))
                 scratch, in_frag = b"", False
-        else:
-            reports.append((len(frag) + (len(scratch) if in_frag else 0), f"Corruption: unknown record type {t}"))
+        elif t == K_EOF_VALUE:  # a valid record whose type byte is kEof: ReadRecord returns false (stop)
+            break
+        elif t == K_BADRECORD_VALUE:  # ... or kBadRecord: 'error in middle of record' if mid-fragment
+            bad_record()
+        else:  # header[6] is a (signed) char read into an unsigned int: 0x80.. print as 42949671xx
+            tu = t | 0xFFFFFF00 if t >= 0x80 else t
+            reports.append((len(frag) + (len(scratch) if in_frag else 0), f"Corruption: unknown record type {tu}"))
             scratch, in_frag = b"", False
     return LogReplay(out, reports)
 

@@ -312,6 +312,15 @@ def _corruption_recipes(img: bytes, ref):
     r.append(("length_shrink", [("set", recs[i][0] + 4, bytes([L & 0xFF, L >> 8]).hex())]))
     i = mid[(2 * len(mid)) // 3]
     r.append(("unknown_type_valid_crc", [("set", recs[i][0] + 6, "09"), fixcrc(recs[i][0], recs[i][1], 9)]))
+    # type bytes that collide with log::Reader's own return values kEof (5) / kBadRecord (6), and
+    # type bytes >= 0x80 (a signed char read into an unsigned int), each with a valid CRC
+    i = mid[(3 * len(mid)) // 4]
+    r.append(("type_keof_valid_crc", [("set", recs[i][0] + 6, "05"), fixcrc(recs[i][0], recs[i][1], 5)]))
+    i = mid[(3 * len(mid)) // 5]
+    r.append(("type_kbadrecord_valid_crc", [("set", recs[i][0] + 6, "06"), fixcrc(recs[i][0], recs[i][1], 6)]))
+    i = mid[(4 * len(mid)) // 5]
+    r.append(("type_0x80_valid_crc", [("set", recs[i][0] + 6, "80"), fixcrc(recs[i][0], recs[i][1], 0x80)]))
+    r.append(("type_0xff_valid_crc", [("set", recs[i][0] + 6, "ff"), fixcrc(recs[i][0], recs[i][1], 0xFF)]))
     i = mid[len(mid) // 5]
     r.append(("zero_header_mid_block", [("set", recs[i][0], "00" * HDR)]))
     firsts = [k for k in range(len(recs)) if recs[k][2] == 2 and recs[k][1] > 0]
@@ -323,6 +332,9 @@ def _corruption_recipes(img: bytes, ref):
         k = tails[len(tails) // 2]
         r.append(("fragment_as_full_valid_crc", [("set", recs[k][0] + 6, "01"), fixcrc(recs[k][0], recs[k][1], 1)]))
         r.append(("fragment_as_first_valid_crc", [("set", recs[k][0] + 6, "02"), fixcrc(recs[k][0], recs[k][1], 2)]))
+        # mid-fragment: kBadRecord reports 'error in middle of record'; kEof ends the read silently
+        r.append(("fragment_as_kbadrecord_valid_crc", [("set", recs[k][0] + 6, "06"), fixcrc(recs[k][0], recs[k][1], 6)]))
+        r.append(("fragment_as_keof_valid_crc", [("set", recs[k][0] + 6, "05"), fixcrc(recs[k][0], recs[k][1], 5)]))
     fulls = [k for k in mid if recs[k][2] == 1]
     if len(fulls) > 2:
         k = fulls[len(fulls) // 2]

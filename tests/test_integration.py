@@ -117,13 +117,23 @@ def test_gpu_readblock_reports_checksum_mismatch(gpu, tmp_path):
     assert rc != 0 and "block checksum mismatch" in err, out + err
 
 
+def _flip(src, dst, pos, bit=0x01):
+    img = bytearray(open(src, "rb").read())
+    img[pos] ^= bit
+    open(dst, "wb").write(bytes(img))
+
+
 def test_leveldb_verify_batched_matches_reference_tool(gpu, tmp_path):
-    """SURVEY §8(f) row 1 in the engine: pdb_verify_gpu (integration/pdb_verify.cc: every block /
+    """SURVEY §8(f) row 1 in the engine: pdb_verify_gpu (integration/pdb_verify.cc: every data-block /
     record checksum of a file in one GPU batch, then the reference tool's key walk) against the
     reference's own leveldb-verify over every table, log and MANIFEST of a database the reference
-    engine wrote: same exit status, nothing reported on the clean files; on a copy with a data
-    byte flipped in every table, both report the checksum mismatch for every table."""
-    import shutil
+    engine wrote -- same exit status and byte-identical stdout / stderr on the clean files, and on
+    damaged copies: a byte flipped in the first, a middle and the last data block (the reference
+    iterator skips the bad block and reports every later key: 'bad iteration ...'), in a data
+    block's trailer, in the index block's trailer and the metaindex block (neither of which the
+    reference tool checks), and in a log record (the corruption report interleaved with the
+    per-record output where the reference reader prints it)."""
+    from pebblesdb_amd import table as T
 
     ref, mine, cpu = _exe("leveldb_verify_ref"), _exe("pdb_verify_gpu"), _exe("pdb_dbbench_cpu")
     db = str(tmp_path / "db")
@@ -131,29 +141,72 @@ def test_leveldb_verify_batched_matches_reference_tool(gpu, tmp_path):
     assert rc == 0, out + err
     names = sorted(os.listdir(db))
     tables = [os.path.join(db, f) for f in names if f.endswith((".sst", ".ldb"))]
-    files = tables + [os.path.join(db, f) for f in names if f.endswith(".log") or f.startswith("MANIFEST")]
-    # a table the engine left unfinished is rejected by both ("bad magic number"); judge file by file
-    for f in files:
-        r_rc, r_out, r_err = _run([ref, f])
-        m_rc, m_out, m_err = _run([mine, f])
-        assert m_rc == r_rc, (f, r_err, m_err)
-        if r_rc == 0:
-            assert m_out == r_out == "" and m_err == r_err == "", (f, r_out, r_err, m_out, m_err)
-        else:
-            assert m_err.strip() == r_err.strip(), (f, r_err, m_err)
-    bad = str(tmp_path / "bad")
-    shutil.copytree(db, bad)
+    logs = [os.path.join(db, f) for f in names if f.endswith(".log") or f.startswith("MANIFEST")]
+
+    def same(path, what):
+        r = _run([ref, path])
+        m = _run([mine, path])
+        assert m == r, (what, path, r[0], r[1][-800:], r[2][-800:], m[0], m[1][-800:], m[2][-800:])
+        return r
+
+    # a table the engine left unfinished is rejected by both ("bad magic number"): judged the same way
+    for f in tables + logs:
+        rc, o, e = same(f, "clean")
+        if rc == 0:
+            assert o == "" and e == "", f
+    damaged = 0
     for f in tables:
-        p = os.path.join(bad, os.path.basename(f))
-        img = bytearray(open(p, "rb").read())
-        img[100] ^= 0x01
-        open(p, "wb").write(bytes(img))
-        r_rc, _, r_err = _run([ref, p])
-        m_rc, _, m_err = _run([mine, p])
-        assert m_rc == r_rc, (p, r_err, m_err)
-        if "bad magic number" in r_err:
+        img = open(f, "rb").read()
+        try:
+            lay = T.table_layout(img, verify_checksums=False)
+        except Exception:
+            continue  # unfinished table: covered above
+        data = lay.data
+        q = str(tmp_path / os.path.basename(f))
+        cases = [("data0", data[0].offset + 100 % max(1, data[0].size)),
+                 ("data_mid", data[len(data) // 2].offset + data[len(data) // 2].size // 2),
+                 ("data_last", data[-1].offset + data[-1].size - 1),
+                 ("data_trailer", data[len(data) // 3].offset + data[len(data) // 3].size + 2),
+                 ("index_trailer", lay.footer.index.offset + lay.footer.index.size + 3),
+                 ("metaindex", lay.footer.metaindex.offset + lay.footer.metaindex.size // 2)]
+        for name, pos in cases:
+            _flip(f, q, pos)
+            rc, o, e = same(q, name)
+            if name.startswith("data"):
+                assert rc == 0 and "block checksum mismatch" in e, (name, e[-500:])
+            else:
+                assert rc == 0 and o == "" and e == "", (name, o, e)
+        damaged += 1
+        if damaged == 3:
+            break
+    assert damaged > 0
+    for f in logs:
+        img = open(f, "rb").read()
+        if len(img) < 1000:
             continue
-        assert "block checksum mismatch" in r_err and "block checksum mismatch" in m_err, (p, r_err, m_err)
+        q = str(tmp_path / ("x" + os.path.basename(f)))
+        for pos in (len(img) // 3, len(img) // 2 + 7):
+            _flip(f, q, pos, 0x20)
+            same(q, "log")
+
+
+def test_leveldb_verify_log_reports_interleave_like_reference_tool(gpu, tmp_path):
+    """pdb_verify_gpu vs the reference leveldb-verify on every corrupted log of
+    tests/golden/log/corruptions.json, as a WAL (000005.log: records < 12 B print 'log record length
+    N is too small' on stdout, between the reader's corruption reports) and as a MANIFEST: identical
+    exit status, stdout and stderr -- each report printed where the reference reader prints it."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from test_log import CORR, _corrupted
+
+    ref, mine = _exe("leveldb_verify_ref"), _exe("pdb_verify_gpu")
+    for i, case in enumerate(CORR):
+        name = "000005.log" if case["log"].startswith("wal") else "MANIFEST-000003"
+        d = tmp_path / f"c{i}"
+        d.mkdir()
+        p = d / name
+        p.write_bytes(_corrupted(case))
+        r, m = _run([ref, str(p)]), _run([mine, str(p)])
+        assert m == r, (case["log"], case["name"], r, m)
 
 
 def test_scan_readahead_matches_reference_reader(gpu, tmp_path):

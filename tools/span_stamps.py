@@ -1,12 +1,14 @@
 #!/usr/bin/env python3
 """tools/span_stamps.py [workload ...] -- where the record kernel's time goes between waves.
 
-Runs diagnostics variant 110 (the shipped crc_lanespan_kernel + per-wave s_memrealtime stamps:
-start, end, items hashed, batches opened) on bench.py's WAL layouts and prints, per workload, one
-JSON line: kernel span from the first wave start to the last wave end, the mean wave lifetime as a
-fraction of that span (the 'resident' share: what the SQ counters' SQ_WAVE_CYCLES / GRBM ratio
-shows), the start ramp and the end tail (percentiles of wave start / end offsets), and the spread
-of work per wave.  CRCs are checked against variant 0 (the product) on the same launch."""
+Runs diagnostics variants 110 / 112 (the shipped crc_lanespan_kernel / the round-2 static batch
+assignment, + per-wave s_memrealtime stamps: start, end, items hashed, batches opened) on bench.py's
+WAL layouts and prints, per workload, one JSON line: interleaved HIP-event timings of the product
+(variant 0) and the static form (111), and for both stamped forms the kernel span from the first
+wave start to the last wave end, the mean wave lifetime as a fraction of that span (the 'resident'
+share: what the SQ counters' SQ_WAVE_CYCLES / GRBM ratio shows), the start ramp and the end tail
+(percentiles of wave start / end offsets), and the spread of work per wave.  Every variant's CRCs
+are checked against the product's."""
 import json
 import os
 import sys
@@ -33,37 +35,44 @@ def run(wl: str, reps: int = 20) -> dict:
     nst = 4 * 8192  # 4 words x up to 8192 waves
     out = torch.zeros(((n + 1) & ~1) + 2 * nst, dtype=torch.int32, device="cuda")
     ref = diag.batch_desc(0, d, d_blk, flags=hint)
+    refh = ref.cpu().numpy()
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     times = {}
-    for v in (0, 110, 0, 110):
-        o = ref if v == 0 else out
+    scratch = torch.zeros_like(ref)
+    for v in (0, 111, 0, 111, 0, 111):  # product (workgroup counter) vs the round-2 static assignment
         for _ in range(5):
-            diag.batch_desc(v, d, d_blk, flags=hint, out=o)
+            diag.batch_desc(v, d, d_blk, flags=hint, out=scratch)
         ev[0].record()
         for _ in range(reps):
-            diag.batch_desc(v, d, d_blk, flags=hint, out=o)
+            diag.batch_desc(v, d, d_blk, flags=hint, out=scratch)
         ev[1].record()
         torch.cuda.synchronize()
-        times.setdefault(v, []).append(ev[0].elapsed_time(ev[1]) / reps)
-    got = out[:n].cpu().numpy()
-    assert (got == ref.cpu().numpy()).all(), "variant 110 CRCs differ from the product"
-    st = out[((n + 1) & ~1):].cpu().numpy().view(np.uint64).reshape(-1, 4)
-    st = st[st[:, 1] > 0].astype(np.float64)
-    t0, t1 = st[:, 0].min(), st[:, 1].max()
-    span = t1 - t0
-    life = st[:, 1] - st[:, 0]
-    pct = lambda a, q: round(float(np.percentile(a, q)) * TICK_NS / 1e3, 2)  # noqa: E731  (us)
-    return {
-        "workload": wl, "records": n, "waves": int(len(st)),
-        "kernel_ms_events": {"v0": [round(x, 4) for x in times[0]], "v110": [round(x, 4) for x in times[110]]},
-        "span_us": round(span * TICK_NS / 1e3, 2),
-        "resident_frac": round(float(life.mean() / span), 4),
-        "start_offset_us_p50_p90_max": [pct(st[:, 0] - t0, 50), pct(st[:, 0] - t0, 90), pct(st[:, 0] - t0, 100)],
-        "end_offset_us_min_p10_p50": [pct(st[:, 1] - t0, 0), pct(st[:, 1] - t0, 10), pct(st[:, 1] - t0, 50)],
-        "items_per_wave_min_mean_max": [int(st[:, 2].min()), round(float(st[:, 2].mean()), 2), int(st[:, 2].max())],
-        "batches_per_wave_min_max": [int(st[:, 3].min()), int(st[:, 3].max())],
-        "us_per_item_mean": round(float((life / np.maximum(st[:, 2], 1)).mean()) * TICK_NS / 1e3, 3),
-    }
+        times.setdefault(v, []).append(round(ev[0].elapsed_time(ev[1]) / reps, 4))
+        assert (scratch.cpu().numpy() == refh).all(), f"variant {v} CRCs differ from the product"
+    res = {"workload": wl, "records": n, "kernel_ms_events": {"v0_dyn": times[0], "v111_static": times[111]}}
+    for v, name in ((110, "dyn"), (112, "static")):
+        out.zero_()
+        for _ in range(3):
+            diag.batch_desc(v, d, d_blk, flags=hint, out=out)
+        torch.cuda.synchronize()
+        assert (out[:n].cpu().numpy() == refh).all(), f"variant {v} CRCs differ from the product"
+        st = out[((n + 1) & ~1):].cpu().numpy().view(np.uint64).reshape(-1, 4)
+        st = st[st[:, 1] > 0].astype(np.float64)
+        t0, t1 = st[:, 0].min(), st[:, 1].max()
+        span = t1 - t0
+        life = st[:, 1] - st[:, 0]
+        pct = lambda a, q: round(float(np.percentile(a, q)) * TICK_NS / 1e3, 2)  # noqa: E731  (us)
+        res[name] = {
+            "waves": int(len(st)),
+            "span_us": round(span * TICK_NS / 1e3, 2),
+            "resident_frac": round(float(life.mean() / span), 4),
+            "start_offset_us_p50_p90_max": [pct(st[:, 0] - t0, 50), pct(st[:, 0] - t0, 90), pct(st[:, 0] - t0, 100)],
+            "end_offset_us_min_p10_p50": [pct(st[:, 1] - t0, 0), pct(st[:, 1] - t0, 10), pct(st[:, 1] - t0, 50)],
+            "items_per_wave_min_mean_max": [int(st[:, 2].min()), round(float(st[:, 2].mean()), 2), int(st[:, 2].max())],
+            "batches_per_wave_min_max": [int(st[:, 3].min()), int(st[:, 3].max())],
+            "us_per_item_mean": round(float((life / np.maximum(st[:, 2], 1)).mean()) * TICK_NS / 1e3, 3),
+        }
+    return res
 
 
 def main():
