@@ -12,6 +12,8 @@
 #   pdb_dbbench_gpu_table_noscan  as gpu_table over the reference's own table.cc (A/B: no read-ahead)
 #   pdb_dbbench_gpu_all    as gpu_table, and util/crc32c.h -> include/pebblesdb_amd/crc32c.h for every
 #                          other call site (log_writer/log_reader records on the scalar GPU service)
+#   pdb_dbbench_buffered_cpu  as gpu_table (buffered emission, read-ahead windows) with every CRC on
+#                          the CPU (-DPDB_CPU_CRC=1, integration/pdb_crc_route.h): the attribution A/B
 #   sstwriter_gpu          oracle/ref_sstwriter.cc over the GPU hooks (golden-table parity test)
 #   leveldb_verify_ref     the reference's own src/leveldb-verify.cc over the engine as shipped
 #   pdb_verify_gpu         integration/pdb_verify.cc: the same tool with every checksum of a file
@@ -60,9 +62,14 @@ compile "$B/obj_ref" "$ENGINE $TABLE_REF util/crc32c.cc leveldb-verify.cc" "-I$R
 compile "$B/obj_shim" "$ENGINE" "-I$ROOT/oracle/shim_pdb -I$ROOT/include -I$REF -I$REF/include"
 # the hooks and the harness (our sources)
 HOOKI="-I$ROOT/include -I$HERE -I$REF -I$REF/include"
+mkdir -p "$B/obj_hooks_cpu"
 for f in pdb_table_builder pdb_format pdb_table; do
-  [ "$B/obj_hooks/$f.o" -nt "$HERE/$f.cc" ] && [ "$B/obj_hooks/$f.o" -nt "$HERE/pdb_hooks.h" ] ||
-    $CXX $DEFS $HOOKI -c "$HERE/$f.cc" -o "$B/obj_hooks/$f.o"
+  [ "$B/obj_hooks/$f.o" -nt "$HERE/$f.cc" ] && [ "$B/obj_hooks/$f.o" -nt "$HERE/pdb_hooks.h" ] &&
+    [ "$B/obj_hooks/$f.o" -nt "$HERE/pdb_crc_route.h" ] || $CXX $DEFS $HOOKI -c "$HERE/$f.cc" -o "$B/obj_hooks/$f.o"
+  # attribution A/B: the same hooks (buffered emission, read-ahead windows) with the CPU CRC
+  [ "$B/obj_hooks_cpu/$f.o" -nt "$HERE/$f.cc" ] && [ "$B/obj_hooks_cpu/$f.o" -nt "$HERE/pdb_hooks.h" ] &&
+    [ "$B/obj_hooks_cpu/$f.o" -nt "$HERE/pdb_crc_route.h" ] ||
+    $CXX $DEFS $HOOKI -DPDB_CPU_CRC=1 -c "$HERE/$f.cc" -o "$B/obj_hooks_cpu/$f.o"
 done
 $CXX $DEFS $HOOKI -DPDB_HOOKS=0 -c "$HERE/pdb_dbbench.cc" -o "$B/obj_hooks/dbbench_cpu.o"
 $CXX $DEFS $HOOKI -DPDB_HOOKS=1 -c "$HERE/pdb_dbbench.cc" -o "$B/obj_hooks/dbbench_hooks.o"
@@ -82,10 +89,14 @@ $CXX -o "$B/pdb_dbbench_gpu_table" "$B/obj_hooks/dbbench_hooks.o" $HOOKS \
 $CXX -o "$B/pdb_dbbench_gpu_table_noscan" "$B/obj_hooks/dbbench_hooks.o" $HOOKS_NOSCAN \
   $(objs "$B/obj_ref" $ENGINE util/crc32c.cc) $GPU
 $CXX -o "$B/pdb_dbbench_gpu_all" "$B/obj_hooks/dbbench_hooks.o" $HOOKS $(objs "$B/obj_shim" $ENGINE) $GPU
+# attribution A/B: buffered emission + read-ahead windows, every CRC on the CPU
+# (the reference's crc32c.cc); no GPU library linked
+HOOKS_CPU="$B/obj_hooks_cpu/pdb_table_builder.o $B/obj_hooks_cpu/pdb_format.o $B/obj_hooks_cpu/pdb_table.o"
+$CXX -o "$B/pdb_dbbench_buffered_cpu" "$B/obj_hooks/dbbench_hooks.o" $HOOKS_CPU $(objs "$B/obj_ref" $ENGINE util/crc32c.cc)
 $CXX -o "$B/sstwriter_gpu" "$B/obj_hooks/sstwriter.o" $HOOKS $(objs "$B/obj_ref" $ENGINE util/crc32c.cc) $GPU
 $CXX -o "$B/leveldb_verify_ref" $(objs "$B/obj_ref" leveldb-verify.cc $ENGINE $TABLE_REF util/crc32c.cc)
 $CXX -o "$B/pdb_verify_gpu" "$B/obj_hooks/pdb_verify.o" "$B/obj_hooks/pdb_format.o" \
   $(objs "$B/obj_ref" $ENGINE table/table_builder.cc table/table.cc util/crc32c.cc) $GPU
 $CXX -o "$B/table_scan_ref" "$B/obj_hooks/table_scan_ref.o" $(objs "$B/obj_ref" $ENGINE $TABLE_REF util/crc32c.cc)
 $CXX -o "$B/table_scan_gpu" "$B/obj_hooks/table_scan_gpu.o" $HOOKS $(objs "$B/obj_ref" $ENGINE util/crc32c.cc) $GPU
-echo "built $B/{table_scan_ref,table_scan_gpu,pdb_dbbench_cpu,pdb_dbbench_gpu_table,pdb_dbbench_gpu_table_noscan,pdb_dbbench_gpu_all,sstwriter_gpu,leveldb_verify_ref,pdb_verify_gpu}"
+echo "built $B/{table_scan_ref,table_scan_gpu,pdb_dbbench_cpu,pdb_dbbench_gpu_table,pdb_dbbench_gpu_table_noscan,pdb_dbbench_gpu_all,pdb_dbbench_buffered_cpu,sstwriter_gpu,leveldb_verify_ref,pdb_verify_gpu}"

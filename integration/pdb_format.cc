@@ -17,6 +17,7 @@
 #include <atomic>
 
 #include "pdb_crc32c.h"
+#include "pdb_crc_route.h"
 #include "pdb_hooks.h"
 #include "pebblesdb/env.h"
 #include "pebblesdb/options.h"
@@ -119,8 +120,8 @@ Status ReadBlock(RandomAccessFile* file, const ReadOptions& options, const Block
   if (options.verify_checksums) {
     // trailer = [type][Mask(crc32c(contents || type))]: one GPU request over n + 1 bytes
     const uint64_t t0 = pdb_hooks::NowNs();
-    const uint32_t actual = pdb_crc32c_value(data, n + 1);
-    const bool bad = pdb_crc32c_unmask(DecodeFixed32(data + n + 1)) != actual;
+    const uint32_t actual = pdb_route::Value(data, n + 1);
+    const bool bad = pdb_route::Unmask(DecodeFixed32(data + n + 1)) != actual;
     pdb_hooks::AddVerify(n + 1, pdb_hooks::NowNs() - t0, bad);
     if (bad) {
       delete[] buf;

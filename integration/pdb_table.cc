@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "pdb_crc32c.h"
+#include "pdb_crc_route.h"
 #include "pdb_hooks.h"
 #include "pebblesdb/cache.h"
 #include "pebblesdb/comparator.h"
@@ -105,9 +106,9 @@ class ScanWindow {
     std::vector<pdb_block_handle> rel(blocks_.begin() + i, blocks_.begin() + j);
     for (auto& b : rel) b.offset -= base;
     ok_.assign(rel.size(), 0);
-    const int64_t bad = pdb_sst_verify_host(got.data(), got.size(), rel.data(), rel.size(), ok_.data());
+    const int64_t bad = pdb_route::SstVerifyHost(got.data(), got.size(), rel.data(), rel.size(), ok_.data());
     if (bad < 0) {
-      fprintf(stderr, "pdb_table: GPU block check failed: %s\n", pdb_last_error());
+      fprintf(stderr, "pdb_table: GPU block check failed: %s\n", pdb_route::LastError());
       abort();
     }
     data_ = got.data();  // buf_, or the file's own (mmap) memory

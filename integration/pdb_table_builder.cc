@@ -32,6 +32,7 @@
 #include <vector>
 
 #include "pdb_crc32c.h"
+#include "pdb_crc_route.h"
 #include "pdb_hooks.h"
 #include "pebblesdb/comparator.h"
 #include "pebblesdb/env.h"
@@ -110,7 +111,7 @@ struct TableBuilder::Rep {
     const int rc = inflight_rc.get();
     pdb_hooks::AddSeal(inflight_handles.size(), inflight.size(), inflight_ns);
     if (rc != 0) {
-      if (status.ok()) status = Status::IOError("pdb_sst_seal_host", pdb_last_error());
+      if (status.ok()) status = Status::IOError("pdb_sst_seal_host", pdb_route::LastError());
     } else if (status.ok()) {
       status = file->Append(Slice(inflight));
       if (status.ok()) status = file->Flush();
@@ -134,7 +135,7 @@ struct TableBuilder::Rep {
     staged_handles.clear();
     inflight_rc = std::async(std::launch::async, [this] {
       const uint64_t t0 = pdb_hooks::NowNs();
-      const int rc = pdb_sst_seal_host(&inflight[0], inflight.size(), inflight_handles.data(), inflight_handles.size());
+      const int rc = pdb_route::SstSealHost(&inflight[0], inflight.size(), inflight_handles.data(), inflight_handles.size());
       inflight_ns = pdb_hooks::NowNs() - t0;
       return rc;
     });
@@ -148,10 +149,10 @@ struct TableBuilder::Rep {
     if (staged_handles.empty()) return;
     if (status.ok()) {
       const uint64_t t0 = pdb_hooks::NowNs();
-      const int rc = pdb_sst_seal_host(&staged[0], staged.size(), staged_handles.data(), staged_handles.size());
+      const int rc = pdb_route::SstSealHost(&staged[0], staged.size(), staged_handles.data(), staged_handles.size());
       pdb_hooks::AddSeal(staged_handles.size(), staged.size(), pdb_hooks::NowNs() - t0);
       if (rc != 0) {
-        status = Status::IOError("pdb_sst_seal_host", pdb_last_error());
+        status = Status::IOError("pdb_sst_seal_host", pdb_route::LastError());
       } else {
         status = file->Append(Slice(staged));
         if (status.ok()) status = file->Flush();

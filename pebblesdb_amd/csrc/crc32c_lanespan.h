@@ -286,7 +286,10 @@ struct SpanItem {
 // MODE (diagnostics only): 0 the product; 1 loads and staging without the hash; 2 the hash over
 // whatever the region holds, without the loads; 3 neither (the per-item bookkeeping alone); 4 the
 // product plus per-wave timestamps (a Sink with a `stamps` array: [start, end, items, batches] per
-// wave, s_memrealtime ticks).  TP: the table scheme.
+// wave, s_memrealtime ticks); pricing forms with the product's instruction stream but WRONG CRCs:
+// 5 every staging read at a lane-skewed, bank-conflict-free address, 6 that and the fold operators'
+// lookups too, 7 no p-word state replacement, 8 no cross-lane folds, 9 no in-part folds (XORs).
+// TP: the table scheme.
 // kDyn: the workgroup owns batches [g nbat / G, (g + 1) nbat / G) and its waves take the next one
 // from an LDS counter (false: batch wave_id + k W, the round-2 static assignment -- diagnostics).
 template <class Src, class Sink, uint32_t MAXN, int MODE = 0, class TP = TabsS4, bool kDyn = true>
@@ -508,7 +511,7 @@ __global__ __launch_bounds__(SpanStage<MAXN>::kWaves * 64) void crc_lanespan_ker
     const int32_t sp = act ? pl - static_cast<int32_t>(zp) : e;  // (no record: an address in range)
     uint32_t pw;
     {
-      const char* q = region + 4 * (sp >> 2);
+      const char* q = (MODE == 5 || MODE == 6) ? region + 4u * (u & 31u) : region + 4 * (sp >> 2);
       pw = (__builtin_amdgcn_perm(lds_u32(q, 4), lds_u32(q, 0), sel) & (0xFFFFFFFFu << (8u * zp))) ^ uz;
     }
     // the p-word's phase-2 step in chain A's numbering; T + LC X in chain X's
@@ -524,7 +527,8 @@ __global__ __launch_bounds__(SpanStage<MAXN>::kWaves * 64) void crc_lanespan_ker
     const int32_t G = static_cast<int32_t>(wave_max_u32(act ? static_cast<uint32_t>(lmax + 1) : 0u)) - 1;
     // base of the chains' words: chain X's dword i at q3 + 4 LC (3 - X) + 4 i (word at phase-2
     // step t = dwords t, t + 1); below the region for short records (words never used)
-    const char* q3 = region + 4 * ((eA - static_cast<int32_t>(4u * NI + 12u * LC)) >> 2);
+    const char* q3 = (MODE == 5 || MODE == 6) ? region + 4u * (u & 31u)
+                                              : region + 4 * ((eA - static_cast<int32_t>(4u * NI + 12u * LC)) >> 2);
     uint32_t xd = 0, ld;
     if (lim > 0) {  // the head chain alone (junk on the other lanes, dropped)
       const int32_t tD = T + static_cast<int32_t>(3u * LC + lim) - FD;  // the p-word's step in it
@@ -574,7 +578,7 @@ __global__ __launch_bounds__(SpanStage<MAXN>::kWaves * 64) void crc_lanespan_ker
       } else if (dd) {
         xd = TP::step(lds, lt, xd, wd);
       }
-      if (t <= G) {
+      if (MODE != 7 && t <= G) {
         if (abc) {
           xa = T == t ? pw : xa;
           xb = T + static_cast<int32_t>(LC) == t ? pw : xb;
@@ -593,21 +597,34 @@ __global__ __launch_bounds__(SpanStage<MAXN>::kWaves * 64) void crc_lanespan_ker
     const uint32_t cc = T + static_cast<int32_t>(2u * LC) < L ? x4[2] : 0u;
     const uint32_t cd = T + static_cast<int32_t>(3u * LC) < L ? x4[3] : 0u;
     static_assert(LC == 8, "the in-part folds use the 32- and 64-B operators");
-    const uint32_t lo2 = span_op_x(lds, kOp32, cb, ca);  // shift(B, 32) ^ A
-    const uint32_t hi2 = span_op_x(lds, kOp32, cd, cc);  // shift(D, 32) ^ C
-    uint32_t P = span_op_x(lds, kOp64, hi2, lo2);        // shift(hi2, 64) ^ lo2
+    auto opx = [&](uint32_t slot, uint32_t c, uint32_t y) -> uint32_t {
+      if constexpr (MODE == 6) {  // pricing: lane-skewed dwords of the operator rows (conflict-free)
+        uint32_t v[4];
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+          const uint32_t bb = __builtin_amdgcn_perm(0u, c, 0x0C0C0000u | (j << 8) | j);
+          v[j] = lds_u32(lds, (bb & 0xFF00u) ^ (128u | (((u + 8u * j + slot) & 31u) << 2)));
+        }
+        return xor3(xor3(v[0], v[1], v[2]), v[3], y);
+      } else {
+        return span_op_x(lds, slot, c, y);
+      }
+    };
+    const uint32_t lo2 = MODE == 9 ? cb ^ ca : opx(kOp32, cb, ca);  // shift(B, 32) ^ A
+    const uint32_t hi2 = MODE == 9 ? cd ^ cc : opx(kOp32, cd, cc);  // shift(D, 32) ^ C
+    uint32_t P = MODE == 9 ? hi2 ^ lo2 : opx(kOp64, hi2, lo2);      // shift(hi2, 64) ^ lo2
     // parts c + m: the 4 PART m bytes before
-    if (k > 1u) {
+    if (MODE != 8 && k > 1u) {
       const uint32_t y = __shfl_down(P, 1, 64);
-      if ((it.c & 1u) == 0 && it.c + 1u < k) P = span_op_x(lds, kOpP1, y, P);
+      if ((it.c & 1u) == 0 && it.c + 1u < k) P = opx(kOpP1, y, P);
     }
-    if (k > 2u) {
+    if (MODE != 8 && k > 2u) {
       const uint32_t y = __shfl_down(P, 2, 64);
-      if ((it.c & 3u) == 0 && it.c + 2u < k) P = span_op_x(lds, kOpP2, y, P);
+      if ((it.c & 3u) == 0 && it.c + 2u < k) P = opx(kOpP2, y, P);
     }
-    if (k > 4u) {
+    if (MODE != 8 && k > 4u) {
       const uint32_t y = __shfl_down(P, 4, 64);
-      if ((it.c & 7u) == 0 && it.c + 4u < k) P = span_op_x(lds, kOpP4, y, P);
+      if ((it.c & 7u) == 0 && it.c + 4u < k) P = opx(kOpP4, y, P);
     }
     if (it.c == 0 && act)
       SinkOps<Sink>::put(sink, (it.batch << 6) + it.r, P, BlkDesc{nullptr, 0u, 0xFFFFFFFFu}, it.pre);

@@ -1013,6 +1013,24 @@ hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tab
       else launch_lanespan<DescSrc, StampOutSink, 4, TabsS4, false>(g, d_tables, src, nblk, cls, ss, s);
       break;
     }
+    case 113:    // pricing (wrong CRCs): the record kernel with conflict-free staging reads
+    case 114: {  // ... and conflict-free fold-operator lookups
+      const uint32_t cls = (flags & PDB_CRC_SIZE_256) ? 256u
+                           : (flags & PDB_CRC_SIZE_512) ? 512u : ((flags & PDB_CRC_SIZE_1K) ? 1152u : 1023u);
+      if (v == 113) launch_lanespan<DescSrc, OutSink, 5>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
+      else launch_lanespan<DescSrc, OutSink, 6>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
+      break;
+    }
+    case 115:    // pricing (wrong CRCs): no p-word replacement selects
+    case 116:    // ... no cross-lane folds
+    case 117: {  // ... no in-part folds
+      const uint32_t cls = (flags & PDB_CRC_SIZE_256) ? 256u
+                           : (flags & PDB_CRC_SIZE_512) ? 512u : ((flags & PDB_CRC_SIZE_1K) ? 1152u : 1023u);
+      if (v == 115) launch_lanespan<DescSrc, OutSink, 7>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
+      else if (v == 116) launch_lanespan<DescSrc, OutSink, 8>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
+      else launch_lanespan<DescSrc, OutSink, 9>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
+      break;
+    }
     case 111: {  // the record kernel with the round-2 static batch assignment (batch wave_id + k W)
       const uint32_t cls = (flags & PDB_CRC_SIZE_256) ? 256u
                            : (flags & PDB_CRC_SIZE_512) ? 512u : ((flags & PDB_CRC_SIZE_1K) ? 1152u : 1023u);

@@ -1,0 +1,71 @@
+#!/usr/bin/env python3
+"""tools/ab_span.py <variants> [workloads] [rounds] -- interleaved A/B of record-kernel variants.
+
+Variants (comma list, diagnostics ids of pebblesdb_amd.diag.batch_desc; 0 = the shipped routing)
+are timed round-robin on bench.py's WAL layouts (wal100 / wal400 / wal1000 / wal), after ~200 warm
+launches (the power manager's cold transient), `rounds` rounds of 20 launches each,
+the order reversed every other round.  Exact variants are checked against variant 0; pricing
+variants (wrong CRCs by design: 113-117) are not.  GB/s = algorithmic bytes (record bytes + 16-B
+descriptor + 4-B CRC) / mean launch time.  Prints one JSON line per workload."""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import wal_layout  # noqa: E402
+from pebblesdb_amd import crc32c, diag  # noqa: E402
+
+WL = {"wal100": (131, 1 << 30, crc32c.SIZE_256), "wal400": (431, 2 << 30, crc32c.SIZE_512),
+      "wal700": (700, 2 << 30, crc32c.SIZE_1023), "wal1000": (1000, 2 << 30, crc32c.SIZE_1023),
+      "wal": (1055, 4 << 30, crc32c.SIZE_1K)}
+PRICING = {113, 114, 115, 116, 117}
+
+
+def main():
+    variants = [int(x) for x in sys.argv[1].split(",")]
+    wls = sys.argv[2].split(",") if len(sys.argv) > 2 else ["wal100", "wal400", "wal1000", "wal"]
+    rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 6
+    crc32c.init_device(0)
+    for wl in wls:
+        payload, nbytes, hint = WL[wl]
+        offs, lens = wal_layout(nbytes, payload)
+        d = torch.empty(int(offs[-1] + lens[-1]) + 64, dtype=torch.uint8, device="cuda")
+        diag.fill_splitmix(d, payload)
+        d_blk = crc32c.blocks_to_device(crc32c.make_blocks(offs, lens))
+        out = torch.empty(len(offs), dtype=torch.int32, device="cuda")
+        algo = int(lens.sum()) + 20 * len(lens)
+        ref = diag.batch_desc(0, d, d_blk, flags=hint).cpu().numpy()
+        for v in variants:
+            if v not in PRICING:
+                got = diag.batch_desc(v, d, d_blk, flags=hint, out=out).cpu().numpy()
+                assert (got == ref).all(), (wl, v, int(np.count_nonzero(got != ref)))
+        for _ in range(200):
+            diag.batch_desc(variants[0], d, d_blk, flags=hint, out=out)
+        torch.cuda.synchronize()
+        t = {v: [] for v in variants}
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for r in range(rounds):
+            for v in (variants if r % 2 == 0 else variants[::-1]):
+                for _ in range(3):
+                    diag.batch_desc(v, d, d_blk, flags=hint, out=out)
+                e0.record()
+                for _ in range(20):
+                    diag.batch_desc(v, d, d_blk, flags=hint, out=out)
+                e1.record()
+                torch.cuda.synchronize()
+                t[v].append(e0.elapsed_time(e1) / 20)
+        res = {"workload": wl, "records": len(offs), "algo_bytes": algo}
+        for v in variants:
+            ms = float(np.mean(t[v]))
+            res[str(v)] = {"ms": round(ms, 4), "ms_min": round(float(np.min(t[v])), 4),
+                           "GB/s": round(algo / (ms * 1e-3) / 1e9, 1), "frac": round(algo / (ms * 1e-3) / 8e12, 4)}
+        print(json.dumps(res), flush=True)
+        del d, d_blk, out
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
