@@ -288,8 +288,9 @@ struct SpanItem {
 // product plus per-wave timestamps (a Sink with a `stamps` array: [start, end, items, batches] per
 // wave, s_memrealtime ticks); pricing forms with the product's instruction stream but WRONG CRCs:
 // 5 every staging read at a lane-skewed, bank-conflict-free address, 6 that and the fold operators'
-// lookups too, 7 no p-word state replacement, 8 no cross-lane folds, 9 no in-part folds (XORs).
-// TP: the table scheme.
+// lookups too, 7 no p-word state replacement, 8 no cross-lane folds, 9 no in-part folds (XORs);
+// exact A/B forms: 10 the round-2 finish (a table step per chain before the folds, bpermute
+// partners), 11 the shipped finish with bpermute partners.  TP: the table scheme.
 // kDyn: the workgroup owns batches [g nbat / G, (g + 1) nbat / G) and its waves take the next one
 // from an LDS counter (false: batch wave_id + k W, the round-2 static assignment -- diagnostics).
 template <class Src, class Sink, uint32_t MAXN, int MODE = 0, class TP = TabsS4, bool kDyn = true>
@@ -587,11 +588,20 @@ __global__ __launch_bounds__(SpanStage<MAXN>::kWaves * 64) void crc_lanespan_ker
         if (dd) xd = T + static_cast<int32_t>(3u * LC) == t ? pw : xd;
       }
     }
-    // finish; a chain whose end is at or before the p-word's start holds no byte of the record
+    // Finish.  Chain X's state still holds its last word unshifted, and its bytes end 32 X bytes
+    // before the part's end, so the part's raw CRC is F(xA) ^ S32 F(xB) ^ S64 F(xC) ^ S96 F(xD)
+    // with F = the table step (shift 4) and S_n = shift n; these maps commute, so it is
+    // F(S64(S32(xD) ^ xC) ^ (S32(xB) ^ xA)), and across the k parts of a record
+    // F(sum_c S_{4 PART c}(R_c)): ONE table step after the cross-lane tree (round 2: a table step
+    // per chain before the folds, 28 lookups instead of 16 per lane; diagnostics mode 10).
+    // A chain whose end is at or before the p-word's start holds no byte of the record.
     const int32_t L = static_cast<int32_t>(NI);
+    constexpr bool kOldFold = MODE == 10;
     uint32_t x4[4] = {xa, xb, xc, xd};
-    const uint32_t z4[4] = {0u, 0u, 0u, 0u};
-    TP::step4(lds, lt, x4, z4);
+    if constexpr (kOldFold) {
+      const uint32_t z4[4] = {0u, 0u, 0u, 0u};
+      TP::step4(lds, lt, x4, z4);
+    }
     const uint32_t ca = T < L ? x4[0] : 0u;
     const uint32_t cb = T + static_cast<int32_t>(LC) < L ? x4[1] : 0u;
     const uint32_t cc = T + static_cast<int32_t>(2u * LC) < L ? x4[2] : 0u;
@@ -610,22 +620,29 @@ __global__ __launch_bounds__(SpanStage<MAXN>::kWaves * 64) void crc_lanespan_ker
         return span_op_x(lds, slot, c, y);
       }
     };
-    const uint32_t lo2 = MODE == 9 ? cb ^ ca : opx(kOp32, cb, ca);  // shift(B, 32) ^ A
-    const uint32_t hi2 = MODE == 9 ? cd ^ cc : opx(kOp32, cd, cc);  // shift(D, 32) ^ C
-    uint32_t P = MODE == 9 ? hi2 ^ lo2 : opx(kOp64, hi2, lo2);      // shift(hi2, 64) ^ lo2
-    // parts c + m: the 4 PART m bytes before
+    const uint32_t lo2 = MODE == 9 ? cb ^ ca : opx(kOp32, cb, ca);  // S32(B) ^ A
+    const uint32_t hi2 = MODE == 9 ? cd ^ cc : opx(kOp32, cd, cc);  // S32(D) ^ C
+    uint32_t P = MODE == 9 ? hi2 ^ lo2 : opx(kOp64, hi2, lo2);      // S64(hi2) ^ lo2
+    // parts c + m: the 4 PART m bytes before.  k a power of two: a record's k lanes never straddle
+    // a row of 16, so the partner's value comes by DPP row_shl (no LDS round trip); other k by
+    // bpermute.
     if (MODE != 8 && k > 1u) {
-      const uint32_t y = __shfl_down(P, 1, 64);
+      const bool dpp = MODE != 11 && !kOldFold && (k & (k - 1u)) == 0;
+      uint32_t y = dpp ? static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(P), 0x101, 0xF, 0xF, false))
+                       : __shfl_down(P, 1, 64);
       if ((it.c & 1u) == 0 && it.c + 1u < k) P = opx(kOpP1, y, P);
+      if (k > 2u) {
+        y = dpp ? static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(P), 0x102, 0xF, 0xF, false))
+                : __shfl_down(P, 2, 64);
+        if ((it.c & 3u) == 0 && it.c + 2u < k) P = opx(kOpP2, y, P);
+      }
+      if (k > 4u) {
+        y = dpp ? static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(P), 0x104, 0xF, 0xF, false))
+                : __shfl_down(P, 4, 64);
+        if ((it.c & 7u) == 0 && it.c + 4u < k) P = opx(kOpP4, y, P);
+      }
     }
-    if (MODE != 8 && k > 2u) {
-      const uint32_t y = __shfl_down(P, 2, 64);
-      if ((it.c & 3u) == 0 && it.c + 2u < k) P = opx(kOpP2, y, P);
-    }
-    if (MODE != 8 && k > 4u) {
-      const uint32_t y = __shfl_down(P, 4, 64);
-      if ((it.c & 7u) == 0 && it.c + 4u < k) P = opx(kOpP4, y, P);
-    }
+    if constexpr (!kOldFold) P = TP::step(lds, lt, P, 0u);  // F: the chains' last words
     if (it.c == 0 && act)
       SinkOps<Sink>::put(sink, (it.batch << 6) + it.r, P, BlkDesc{nullptr, 0u, 0xFFFFFFFFu}, it.pre);
   };

@@ -1021,6 +1021,14 @@ hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tab
       else launch_lanespan<DescSrc, OutSink, 6>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
       break;
     }
+    case 118:    // exact: the round-2 finish (table step per chain before the folds, bpermute partners)
+    case 119: {  // exact: the shipped finish with bpermute partners (no DPP)
+      const uint32_t cls = (flags & PDB_CRC_SIZE_256) ? 256u
+                           : (flags & PDB_CRC_SIZE_512) ? 512u : ((flags & PDB_CRC_SIZE_1K) ? 1152u : 1023u);
+      if (v == 118) launch_lanespan<DescSrc, OutSink, 10>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
+      else launch_lanespan<DescSrc, OutSink, 11>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
+      break;
+    }
     case 115:    // pricing (wrong CRCs): no p-word replacement selects
     case 116:    // ... no cross-lane folds
     case 117: {  // ... no in-part folds
