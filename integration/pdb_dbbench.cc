@@ -21,7 +21,12 @@
 #include <string.h>
 #include <time.h>
 
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "pebblesdb/cache.h"
@@ -49,6 +54,7 @@ struct Flags {
   bool verify_checksums = false;
   bool use_existing_db = false;
   bool paranoid_checks = false;
+  int threads = 1;  // readrandom / readseq: db_bench --threads (db_bench.cc:1071-1110)
   std::string db = "/tmp/pdb_dbbench";
 } F;
 
@@ -82,9 +88,11 @@ class ValuePool {  // db_bench's RandomGenerator: a 1-MiB pool of compressible p
 struct Result {
   const char* name;
   long ops;
-  double seconds;
+  double seconds;  // summed over threads (db_bench's Stats::Merge)
   long long bytes;
   std::string note;
+  double wall;  // wall time of the whole benchmark (0: = seconds)
+  int threads;  // (0: 1)
 };
 
 void Report(const Result& r) {
@@ -94,9 +102,12 @@ void Report(const Result& r) {
     printf("%-12s : %11.3f micros/op; %6.1f MB/s %s\n", r.name, us, mbs, r.note.c_str());
   else
     printf("%-12s : %11.3f micros/op; %s\n", r.name, us, r.note.c_str());
+  const double wall = r.wall > 0 ? r.wall : r.seconds;
   printf("{\"bench\": \"%s\", \"ops\": %ld, \"seconds\": %.4f, \"micros_per_op\": %.4f, \"MB_s\": %.2f, "
-         "\"verify_checksums\": %s",
-         r.name, r.ops, r.seconds, us, r.bytes > 0 ? mbs : 0.0, F.verify_checksums ? "true" : "false");
+         "\"verify_checksums\": %s, \"threads\": %d, \"wall_s\": %.4f, \"ops_per_s\": %.1f",
+         r.name, r.ops, r.seconds, us, r.bytes > 0 ? mbs : 0.0, F.verify_checksums ? "true" : "false",
+         r.threads > 0 ? r.threads : 1, wall,
+         r.ops / wall);
 #if PDB_HOOKS
   pdb_hook_stats s;
   pdb_hook_stats_get(&s);
@@ -154,28 +165,55 @@ Result Write(leveldb::DB* db, bool seq) {
   return Result{seq ? "fillseq" : "fillrandom", F.num, NowSec() - t0, bytes, ""};
 }
 
+// db_bench's RunBenchmark: `threads` threads started together, thread i drawing keys from
+// Random(1000 + i) (ThreadState(i), db_bench.cc:354-359), each doing `reads` gets; micros/op is
+// the per-thread time per op (sum of thread times / ops, db_bench.cc:292-318); the JSON line also
+// carries the aggregate rate over the wall time.
 Result ReadRandom(leveldb::DB* db) {
-  leveldb::Random rand(1000);
-  leveldb::ReadOptions ro;
-  ro.verify_checksums = F.verify_checksums;
-  std::string value;
   const int reads = F.reads < 0 ? F.num : F.reads;
-  int found = 0;
-  char key[32];
-  const double t0 = NowSec();
-  for (int i = 0; i < reads; ++i) {
-    snprintf(key, sizeof(key), "%016d", static_cast<int>(rand.Next() % F.num));
-    leveldb::Status s = db->Get(ro, key, &value);
-    if (s.ok()) {
-      ++found;
-    } else if (!s.IsNotFound()) {
-      fprintf(stderr, "get error: %s\n", s.ToString().c_str());
-      exit(1);
+  const int nt = F.threads > 0 ? F.threads : 1;
+  std::vector<int> found(nt, 0);
+  std::vector<double> secs(nt, 0.0);
+  auto body = [&](int t) {
+    leveldb::Random rand(1000 + t);
+    leveldb::ReadOptions ro;
+    ro.verify_checksums = F.verify_checksums;
+    std::string value;
+    char key[32];
+    const double t0 = NowSec();
+    for (int i = 0; i < reads; ++i) {
+      snprintf(key, sizeof(key), "%016d", static_cast<int>(rand.Next() % F.num));
+      leveldb::Status s = db->Get(ro, key, &value);
+      if (s.ok()) {
+        ++found[t];
+      } else if (!s.IsNotFound()) {
+        fprintf(stderr, "get error: %s\n", s.ToString().c_str());
+        exit(1);
+      }
     }
+    secs[t] = NowSec() - t0;
+  };
+  const double w0 = NowSec();
+  if (nt == 1) {
+    body(0);
+  } else {
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t) th.emplace_back(body, t);
+    for (auto& x : th) x.join();
   }
-  char note[80];
-  snprintf(note, sizeof(note), "(%d of %d found)", found, reads);
-  return Result{"readrandom", reads, NowSec() - t0, 0, note};
+  const double wall = NowSec() - w0;
+  int fsum = 0;
+  double ssum = 0;
+  for (int t = 0; t < nt; ++t) {
+    fsum += found[t];
+    ssum += secs[t];
+  }
+  char note[120];
+  snprintf(note, sizeof(note), "(%d of %d found)", fsum, reads * nt);
+  Result r{"readrandom", static_cast<long>(reads) * nt, ssum, 0, note};
+  r.wall = wall;
+  r.threads = nt;
+  return r;
 }
 
 Result ReadSeq(leveldb::DB* db) {
@@ -207,7 +245,22 @@ bool Arg(const char* a, const char* name, std::string* v) {
 
 }  // namespace
 
+// A fault prints the faulting thread's stack (stderr) before the default action, so a crash in the
+// engine's teardown leaves evidence in the run's log.
+void CrashHandler(int sig) {
+  void* frames[64];
+  const int n = backtrace(frames, 64);
+  const char msg[] = "pdb_dbbench: fatal signal, backtrace:\n";
+  (void)!write(2, msg, sizeof(msg) - 1);
+  backtrace_symbols_fd(frames, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+
 int main(int argc, char** argv) {
+  signal(SIGSEGV, CrashHandler);
+  signal(SIGBUS, CrashHandler);
+  signal(SIGABRT, CrashHandler);
   for (int i = 1; i < argc; ++i) {
     std::string v;
     if (Arg(argv[i], "--benchmarks", &v)) F.benchmarks = v;
@@ -219,6 +272,7 @@ int main(int argc, char** argv) {
     else if (Arg(argv[i], "--verify_checksums", &v)) F.verify_checksums = atoi(v.c_str()) != 0;
     else if (Arg(argv[i], "--use_existing_db", &v)) F.use_existing_db = atoi(v.c_str()) != 0;
     else if (Arg(argv[i], "--paranoid_checks", &v)) F.paranoid_checks = atoi(v.c_str()) != 0;
+    else if (Arg(argv[i], "--threads", &v)) F.threads = atoi(v.c_str());
     else if (Arg(argv[i], "--db", &v)) F.db = v;
     else {
       fprintf(stderr, "invalid flag '%s'\n", argv[i]);
@@ -250,8 +304,11 @@ int main(int argc, char** argv) {
       return 1;
     }
   }
-  delete db;
+  fflush(stdout);
+  const double td = NowSec();
+  delete db;  // waits for the background compaction / memtable threads (db_impl.cc:259-297)
   delete cache;
   delete fp;
+  fprintf(stderr, "teardown: %.3f s\n", NowSec() - td);
   return 0;
 }

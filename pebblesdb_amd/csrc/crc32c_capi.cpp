@@ -10,6 +10,7 @@
 #include <time.h>
 
 #include <algorithm>
+#include <atomic>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -32,18 +33,38 @@ int hip_fail(hipError_t e, const char* what) {
   return fail(PDB_EHIP, std::string(what) + ": " + hipGetErrorString(e));
 }
 
+// A host-staging context: streams, pipeline events and a device workspace.  Host batches from
+// different threads (the engine's compaction seals, scan windows, log checks) take different
+// contexts and run concurrently instead of queueing on one device mutex.
+struct HostCtx {
+  std::mutex mu;
+  hipStream_t stream = nullptr;       // kernels and result copies of the host entry points
+  hipStream_t copy_stream = nullptr;  // host -> device staging copies (overlap the previous group's kernel)
+  hipEvent_t staged[2] = {};          // group in workspace slot k copied in
+  hipEvent_t drained[2] = {};         // group in workspace slot k hashed and its results copied out
+  uint8_t* d_ws = nullptr;
+  size_t ws_cap = 0;
+};
+constexpr int kHostCtx = 4;
+
+// One scalar-service request slot (crc32c_server.hip): its request sequence number, guarded by mu
+// (a slot is shared only when more threads than slots call at once).
+struct ScalarSlot {
+  std::mutex mu;
+  uint32_t seq = 0;
+};
+
 struct DevState {
   int device = -1;
   uint32_t* d_tables = nullptr;
   uint32_t* d_pow2 = nullptr;  // 64 power-of-two shift operators (long-span combine)
   LaunchGeom geom{256, 1024};
-  hipStream_t stream = nullptr;       // kernels and result copies of the host entry points
-  hipStream_t copy_stream = nullptr;  // host -> device staging copies (overlap the previous group's kernel)
-  hipEvent_t staged[2] = {};          // group in workspace slot k copied in
-  hipEvent_t drained[2] = {};         // group in workspace slot k hashed and its results copied out
-  std::mutex mu;  // guards the host-staging workspace below
-  uint8_t* d_ws = nullptr;
-  size_t ws_cap = 0;
+  // host entry points: one CU is left to the scalar service, so a host batch never has to stop it
+  // (a batch's persistent workgroups need a whole CU each) and scalar calls keep being answered
+  // while batches run
+  LaunchGeom hgeom{255, 1024};
+  HostCtx ctx[kHostCtx];
+  std::mutex mu;  // the launch-per-call scalar modes' staging below
   // scalar Extend: pinned, device-mapped staging ([256-B result area][bytes]); the kernels read
   // the bytes across PCIe and write the CRC back into it, so a call is memcpy + launch(es) + sync
   uint8_t* h_stage = nullptr;
@@ -54,16 +75,18 @@ struct DevState {
   // kernel (crc32c_server.hip); PDB_SCALAR_WAIT=poll launches one kernel per call and spins on
   // the result, =sync waits on the stream (A/B diagnostics, tools/scalar_latency.py).
   int scalar_mode = 0;
-  ServerBox* srv_in_h = nullptr;   // request box + data area (kServerBytes), host-writable address
-  ServerBox* srv_in_d = nullptr;   // its device address
-  bool srv_in_device = false;      // request box in fine-grained device memory (large BAR)
-  ServerBox* srv_out_h = nullptr;  // response box (pinned host memory)
-  ServerBox* srv_out_d = nullptr;
+  std::mutex srv_mu;             // server allocation, launch and stop (never held across a request)
+  uint8_t* srv_in_h = nullptr;   // request area (kServerInBytes), host-writable address
+  uint8_t* srv_in_d = nullptr;   // its device address
+  bool srv_in_device = false;    // request area in fine-grained device memory (large BAR)
+  uint8_t* srv_out_h = nullptr;  // response area (kServerOutBytes, pinned host memory)
+  uint8_t* srv_out_d = nullptr;
   bool large_bar = false;
   hipStream_t srv_stream = nullptr;
-  uint32_t srv_epoch = 0;      // epoch of the most recently launched server
-  uint32_t srv_seq = 0;        // last request posted
-  bool srv_live = false;       // a server of srv_epoch may still be in its loop (guarded by mu)
+  uint32_t srv_epoch = 0;        // epoch of the most recently launched server (atomic)
+  uint64_t srv_stop = 0;         // ctl->stop value the live instance runs under (srv_mu)
+  bool srv_live = false;         // an instance of srv_epoch may still be in its loop (atomic)
+  ScalarSlot slots[kServerSlots];
 };
 
 enum ScalarMode : int { kScalarServer = 0, kScalarPoll = 1, kScalarSync = 2 };
@@ -127,14 +150,17 @@ int get_state(DevState** out) {
   s->scalar_mode = !wait ? kScalarServer
                           : strcmp(wait, "sync") == 0 ? kScalarSync
                           : strcmp(wait, "poll") == 0 ? kScalarPoll : kScalarServer;
-  e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
-  if (e != hipSuccess) return hip_fail(e, "hipStreamCreate");
-  e = hipStreamCreateWithFlags(&s->copy_stream, hipStreamNonBlocking);
-  if (e != hipSuccess) return hip_fail(e, "hipStreamCreate(copy)");
-  for (int k = 0; k < 2; ++k) {
-    if ((e = hipEventCreateWithFlags(&s->staged[k], hipEventDisableTiming)) != hipSuccess ||
-        (e = hipEventCreateWithFlags(&s->drained[k], hipEventDisableTiming)) != hipSuccess)
-      return hip_fail(e, "hipEventCreate");
+  s->hgeom.grid = s->geom.grid > 1 ? s->geom.grid - 1 : 1;
+  for (HostCtx& c : s->ctx) {
+    e = hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking);
+    if (e != hipSuccess) return hip_fail(e, "hipStreamCreate");
+    e = hipStreamCreateWithFlags(&c.copy_stream, hipStreamNonBlocking);
+    if (e != hipSuccess) return hip_fail(e, "hipStreamCreate(copy)");
+    for (int k = 0; k < 2; ++k) {
+      if ((e = hipEventCreateWithFlags(&c.staged[k], hipEventDisableTiming)) != hipSuccess ||
+          (e = hipEventCreateWithFlags(&c.drained[k], hipEventDisableTiming)) != hipSuccess)
+        return hip_fail(e, "hipEventCreate");
+    }
   }
   __atomic_store_n(&g_dev[dev], s.get(), __ATOMIC_RELEASE);
   *out = s.release();
@@ -148,21 +174,41 @@ hipStream_t pick_stream(DevState* st, void* stream) {
   return static_cast<hipStream_t>(stream);
 }
 
-int ensure_ws(DevState* st, size_t bytes) {
-  if (bytes <= st->ws_cap) return PDB_OK;
-  if (st->d_ws) {
-    (void)hipStreamSynchronize(st->copy_stream);
-    (void)hipStreamSynchronize(st->stream);
-    (void)hipFree(st->d_ws);
-    st->d_ws = nullptr;
-    st->ws_cap = 0;
+int ensure_ws(HostCtx* c, size_t bytes) {
+  if (bytes <= c->ws_cap) return PDB_OK;
+  if (c->d_ws) {
+    (void)hipStreamSynchronize(c->copy_stream);
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipFree(c->d_ws);
+    c->d_ws = nullptr;
+    c->ws_cap = 0;
   }
   size_t cap = std::max<size_t>(bytes, 1 << 20);
-  hipError_t e = hipMalloc(&st->d_ws, cap);
+  hipError_t e = hipMalloc(&c->d_ws, cap);
   if (e != hipSuccess) return fail(PDB_ENOMEM, std::string("hipMalloc(workspace): ") + hipGetErrorString(e));
-  st->ws_cap = cap;
+  c->ws_cap = cap;
   return PDB_OK;
 }
+
+// A free host context (try each once), else the one this thread hashes to.
+struct CtxLock {
+  HostCtx* c;
+  std::unique_lock<std::mutex> lk;
+  explicit CtxLock(DevState* st) : c(nullptr) {
+    for (HostCtx& x : st->ctx) {
+      std::unique_lock<std::mutex> t(x.mu, std::try_to_lock);
+      if (t.owns_lock()) {
+        c = &x;
+        lk = std::move(t);
+        return;
+      }
+    }
+    static std::atomic<uint32_t> rr{0};
+    thread_local uint32_t mine = rr.fetch_add(1, std::memory_order_relaxed);
+    c = &st->ctx[mine % kHostCtx];
+    lk = std::unique_lock<std::mutex>(c->mu);
+  }
+};
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
@@ -170,8 +216,7 @@ constexpr size_t kStageHdr = 256;  // result words ahead of the staged bytes (ke
 
 int ensure_stage(DevState* st, size_t bytes) {
   if (bytes <= st->stage_cap) return PDB_OK;
-  if (st->h_stage) {
-    (void)hipStreamSynchronize(st->stream);
+  if (st->h_stage) {  // (st->mu held: every user of the stage has synchronised its stream)
     (void)hipHostFree(st->h_stage);
     st->h_stage = st->d_stage = nullptr;
     st->stage_cap = 0;
@@ -200,31 +245,37 @@ double now_s() {
 
 uint32_t box_load(const uint32_t* p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
 
-// Post request word {init, len, seq} (st->mu held); returns its seq.  The request box may be device
-// memory written through the BAR (write-combined): the fences order the staged bytes before the
-// request word and push the word out at once.
-uint32_t server_post(DevState* st, uint32_t init, uint32_t len) {
-  const uint32_t seq = st->srv_seq = (st->srv_seq + 1) & kServerSeqMask;
-  const uint64_t w = (static_cast<uint64_t>((seq << 17) | len) << 32) | init;
+ServerCtl* srv_ctl(const DevState* st) { return reinterpret_cast<ServerCtl*>(st->srv_in_h); }
+uint64_t* srv_req(const DevState* st, uint32_t slot) {
+  return reinterpret_cast<uint64_t*>(st->srv_in_h + kReqOff) + slot;
+}
+uint8_t* srv_data(const DevState* st, uint32_t slot) { return st->srv_in_h + kSlotDataOff + slot * kSlotStride; }
+const uint64_t* srv_resp(const DevState* st, uint32_t slot) {
+  return reinterpret_cast<const uint64_t*>(st->srv_out_h + 64u * slot);
+}
+ServerExit* srv_exit(const DevState* st) { return reinterpret_cast<ServerExit*>(st->srv_out_h + kExitOff); }
+
+uint32_t live_epoch(const DevState* st) { return __atomic_load_n(&st->srv_epoch, __ATOMIC_ACQUIRE); }
+bool server_exited(const DevState* st, uint32_t epoch) { return box_load(&srv_exit(st)->exit_epoch) == epoch; }
+
+// The request box may be device memory written through the BAR (write-combined): the fences order
+// the staged bytes before the request word and push the word out at once.
+void post_word(uint64_t* p, uint64_t w) {
   __builtin_ia32_sfence();
-  __atomic_store_n(&st->srv_in_h->req, w, __ATOMIC_RELEASE);
+  __atomic_store_n(p, w, __ATOMIC_RELEASE);
   __builtin_ia32_sfence();
-  return seq;
 }
 
-bool server_exited(const DevState* st) { return box_load(&st->srv_out_h->exit_epoch) == st->srv_epoch; }
-
-uint64_t server_resp(const DevState* st) { return __atomic_load_n(&st->srv_out_h->resp, __ATOMIC_ACQUIRE); }
-
-// Ask the server of st->srv_epoch to leave and wait until it has (st->mu held).  Host memory only,
-// no HIP call, so it is safe inside stream capture.  The server answers within one poll (~2 us);
-// its lifetime bounds the wait in any case.
+// Ask the live instance to leave and wait until it has (srv_mu held).  Host memory only, no HIP
+// call, so it is safe inside stream capture.  Every wave polls ctl->stop (~2 us); the lifetime
+// bounds the wait in any case.
 int server_park(DevState* st) {
-  if (!st->srv_live) return PDB_OK;
-  if (!server_exited(st)) {
-    server_post(st, 0u, kServerStop);
+  if (!__atomic_load_n(&st->srv_live, __ATOMIC_ACQUIRE)) return PDB_OK;
+  const uint32_t epoch = live_epoch(st);
+  if (!server_exited(st, epoch)) {
+    post_word(&srv_ctl(st)->stop, ++st->srv_stop);
     const double t0 = now_s();
-    while (!server_exited(st)) {
+    while (!server_exited(st, epoch)) {
       __builtin_ia32_pause();
       if (now_s() - t0 > 2.0) return fail(PDB_EHIP, "scalar server did not stop within 2 s");
     }
@@ -233,10 +284,11 @@ int server_park(DevState* st) {
   return PDB_OK;
 }
 
-// Batch launches need every CU's full LDS: park a live server first.
+// Device-resident batches launch a workgroup on every CU: stop a live server first (host batches
+// leave it a CU instead, DevState::hgeom).
 int quiesce(DevState* st) {
   if (!__atomic_load_n(&st->srv_live, __ATOMIC_ACQUIRE)) return PDB_OK;
-  std::lock_guard<std::mutex> lk(st->mu);
+  std::lock_guard<std::mutex> lk(st->srv_mu);
   return server_park(st);
 }
 
@@ -244,15 +296,16 @@ void park_all_at_exit() {
   for (int d = 0; d < kMaxDev; ++d) {
     DevState* st = __atomic_load_n(&g_dev[d], __ATOMIC_ACQUIRE);
     if (!st || !__atomic_load_n(&st->srv_live, __ATOMIC_ACQUIRE)) continue;
-    std::unique_lock<std::mutex> lk(st->mu, std::try_to_lock);
-    if (!lk.owns_lock()) continue;  // a call in flight at exit: the idle timeout ends the server
-    if (!server_exited(st)) server_post(st, 0u, kServerStop);
+    std::unique_lock<std::mutex> lk(st->srv_mu, std::try_to_lock);
+    if (!lk.owns_lock()) continue;  // a launch in flight at exit: the idle timeout ends the server
+    const uint32_t epoch = live_epoch(st);
+    if (!server_exited(st, epoch)) post_word(&srv_ctl(st)->stop, ++st->srv_stop);
     const double t0 = now_s();
-    while (!server_exited(st) && now_s() - t0 < 0.5) __builtin_ia32_pause();
+    while (!server_exited(st, epoch) && now_s() - t0 < 0.5) __builtin_ia32_pause();
   }
 }
 
-int alloc_pinned(size_t bytes, ServerBox** h, ServerBox** d) {
+int alloc_pinned(size_t bytes, uint8_t** h, uint8_t** d) {
   void* hp = nullptr;
   hipError_t e = hipHostMalloc(&hp, bytes, hipHostMallocMapped | hipHostMallocCoherent);
   if (e != hipSuccess) return fail(PDB_ENOMEM, std::string("hipHostMalloc(server): ") + hipGetErrorString(e));
@@ -262,30 +315,32 @@ int alloc_pinned(size_t bytes, ServerBox** h, ServerBox** d) {
     (void)hipHostFree(hp);
     return hip_fail(e, "hipHostGetDevicePointer(server)");
   }
-  *h = static_cast<ServerBox*>(hp);
-  *d = static_cast<ServerBox*>(dp);
+  *h = static_cast<uint8_t*>(hp);
+  *d = static_cast<uint8_t*>(dp);
   return PDB_OK;
 }
 
+// (srv_mu held)
 int server_alloc(DevState* st) {
   hipError_t e;
   int rc;
-  // request box: fine-grained device memory written by the host through the large BAR (the server
-  // polls local HBM: ~0.37 us per poll vs ~1.2 us across PCIe, tools/server_probe.hip), else pinned
-  // host memory.  PDB_SERVER_BOX=host forces the latter (A/B).
+  // request area: fine-grained device memory written by the host through the large BAR (the
+  // server polls local HBM: ~0.37 us per poll vs ~1.2 us across PCIe, tools/server_probe.hip), else
+  // pinned host memory.  PDB_SERVER_BOX=host forces the latter (A/B).
   const char* where = getenv("PDB_SERVER_BOX");
   const bool want_dev = st->large_bar && !(where && strcmp(where, "host") == 0);
   if (want_dev) {
     void* p = nullptr;
-    e = hipExtMallocWithFlags(&p, kServerBytes, hipDeviceMallocFinegrained);
+    e = hipExtMallocWithFlags(&p, kServerInBytes, hipDeviceMallocFinegrained);
     if (e == hipSuccess) {
-      if ((e = hipMemset(p, 0, kServerBytes)) != hipSuccess) return hip_fail(e, "hipMemset(server box)");
-      st->srv_in_h = st->srv_in_d = static_cast<ServerBox*>(p);
+      if ((e = hipMemset(p, 0, kServerInBytes)) != hipSuccess) return hip_fail(e, "hipMemset(server box)");
+      if ((e = hipDeviceSynchronize()) != hipSuccess) return hip_fail(e, "hipDeviceSynchronize(server box)");
+      st->srv_in_h = st->srv_in_d = static_cast<uint8_t*>(p);
       st->srv_in_device = true;
     }
   }
-  if (!st->srv_in_h && (rc = alloc_pinned(kServerBytes, &st->srv_in_h, &st->srv_in_d))) return rc;
-  if ((rc = alloc_pinned(sizeof(ServerBox), &st->srv_out_h, &st->srv_out_d))) return rc;
+  if (!st->srv_in_h && (rc = alloc_pinned(kServerInBytes, &st->srv_in_h, &st->srv_in_d))) return rc;
+  if ((rc = alloc_pinned(kServerOutBytes, &st->srv_out_h, &st->srv_out_d))) return rc;
   if ((e = hipStreamCreateWithFlags(&st->srv_stream, hipStreamNonBlocking)) != hipSuccess)
     return hip_fail(e, "hipStreamCreate(server)");
   static std::once_flag once;
@@ -293,42 +348,62 @@ int server_alloc(DevState* st) {
   return PDB_OK;
 }
 
-// Launch a server instance (st->mu held).  `pending`: a request of seq st->srv_seq is waiting.
-int server_launch(DevState* st, bool pending) {
+// Make sure an instance is serving (or about to): launch one if none is live, or if the instance
+// `seen` (the epoch the caller observed) has left.  srv_mu serialises launches; a thread that
+// finds the epoch already bumped by another caller just goes on waiting for its answer.
+int server_ensure(DevState* st, bool relaunch_seen, uint32_t seen) {
+  std::lock_guard<std::mutex> lk(st->srv_mu);
   int rc;
   if (!st->srv_stream && (rc = server_alloc(st))) return rc;
+  const bool live = __atomic_load_n(&st->srv_live, __ATOMIC_ACQUIRE);
+  const uint32_t epoch = live_epoch(st);
+  if (live && !server_exited(st, epoch)) return PDB_OK;            // serving
+  if (relaunch_seen && live && epoch != seen) return PDB_OK;        // another caller relaunched it
   hipError_t e = hipSetDevice(st->device);
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
-  const uint32_t epoch = ++st->srv_epoch;
-  const uint32_t served0 = pending ? (st->srv_seq - 1) & kServerSeqMask : st->srv_seq;
-  e = launch_server(st->d_tables, st->srv_in_d, st->srv_out_d, epoch, served0, kServerIdleTicks, kServerLifeTicks,
+  const uint32_t next = epoch + 1;
+  e = launch_server(st->d_tables, st->srv_in_d, st->srv_out_d, next, st->srv_stop, kServerIdleTicks, kServerLifeTicks,
                     st->srv_stream);
   if (e != hipSuccess) return hip_fail(e, "launch_server");
+  __atomic_store_n(&st->srv_epoch, next, __ATOMIC_RELEASE);
   __atomic_store_n(&st->srv_live, true, __ATOMIC_RELEASE);
   return PDB_OK;
 }
 
-// One request (st->mu held, n <= kServerCap): stage the bytes, post the request word, spin on the
-// response word.  A server that left its loop without taking the request (idle / lifetime exit
-// racing the post) is relaunched; the new instance serves the pending request.
+// This thread's request slot: assigned round robin at the thread's first call.
+uint32_t my_slot() {
+  static std::atomic<uint32_t> next{0};
+  thread_local uint32_t slot = next.fetch_add(1, std::memory_order_relaxed) % kServerSlots;
+  return slot;
+}
+
+// One request (n <= kServerCap) in this thread's slot: stage the bytes, post the request word,
+// spin on the slot's response word.  No device-wide lock: other threads' requests proceed in
+// their own slots.  An instance that left without answering (idle / lifetime exit racing the
+// post) is replaced; the new one serves every pending slot.
 int server_call(DevState* st, uint32_t init, const uint8_t* data, uint64_t n, uint32_t* out) {
   int rc;
-  if (!st->srv_live || server_exited(st))
-    if ((rc = server_launch(st, false))) return rc;
-  uint8_t* area = reinterpret_cast<uint8_t*>(st->srv_in_h) + sizeof(ServerBox);
-  memcpy(area + ((0u - static_cast<uint32_t>(n)) & 15u), data, n);
-  const uint32_t seq = server_post(st, init, static_cast<uint32_t>(n));
+  const uint32_t slot = my_slot();
+  ScalarSlot& sl = st->slots[slot];
+  std::lock_guard<std::mutex> lk(sl.mu);
+  if (!__atomic_load_n(&st->srv_live, __ATOMIC_ACQUIRE) || server_exited(st, live_epoch(st)))
+    if ((rc = server_ensure(st, false, 0))) return rc;
+  memcpy(srv_data(st, slot) + ((0u - static_cast<uint32_t>(n)) & 15u), data, n);
+  const uint32_t seq = sl.seq = (sl.seq + 1) & kServerSeqMask;
+  post_word(srv_req(st, slot), (static_cast<uint64_t>((seq << 17) | static_cast<uint32_t>(n)) << 32) | init);
+  const uint64_t* resp = srv_resp(st, slot);
   double t0 = 0;
   for (uint32_t spin = 1;; ++spin) {
-    const uint64_t r = server_resp(st);
+    const uint64_t r = __atomic_load_n(resp, __ATOMIC_ACQUIRE);
     if (static_cast<uint32_t>(r >> 32) == seq) {
       *out = static_cast<uint32_t>(r);
       return PDB_OK;
     }
-    if (server_exited(st)) {
-      // re-check the answer first: the server may have answered and then left
-      if (static_cast<uint32_t>(server_resp(st) >> 32) == seq) continue;
-      if ((rc = server_launch(st, true))) return rc;
+    const uint32_t ep = live_epoch(st);
+    if (server_exited(st, ep)) {
+      // re-check the answer first: the instance may have answered and then left
+      if (static_cast<uint32_t>(__atomic_load_n(resp, __ATOMIC_ACQUIRE) >> 32) == seq) continue;
+      if ((rc = server_ensure(st, true, ep))) return rc;
     }
     __builtin_ia32_pause();
     if ((spin & 0xFFFFu) == 0) {
@@ -364,8 +439,8 @@ struct HostGroup {
 // both streams, so an early error return never leaves a copy in flight from host memory that is
 // about to be freed.
 struct SlotPipe {
-  DevState* st;
-  explicit SlotPipe(DevState* s) : st(s) {}
+  HostCtx* st;
+  explicit SlotPipe(HostCtx* s) : st(s) {}
   ~SlotPipe() {
     (void)hipStreamSynchronize(st->copy_stream);
     (void)hipStreamSynchronize(st->stream);
@@ -441,12 +516,12 @@ int host_desc(const uint8_t* base, uint64_t base_len, const pdb_blk* blk, uint64
   const size_t off_ok = align_up(off_exp + (mode == kModeVerify ? max_count * 4 : 0), 256);
   const size_t slot_bytes = align_up(off_ok + (mode == kModeVerify ? max_count : 0), 256);
   const size_t nslots = groups.size() > 1 ? 2 : 1;
-  DevState* st;
-  int rc = get_state(&st);
+  DevState* dev;
+  int rc = get_state(&dev);
   if (rc) return rc;
-  std::lock_guard<std::mutex> lk(st->mu);
-  if ((rc = server_park(st))) return rc;
-  hipError_t e = hipSetDevice(st->device);
+  CtxLock cl(dev);
+  HostCtx* st = cl.c;
+  hipError_t e = hipSetDevice(dev->device);
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
   if ((rc = ensure_ws(st, nslots * slot_bytes + 256))) return rc;
   hipStream_t s = st->stream, cs = st->copy_stream;
@@ -473,7 +548,7 @@ int host_desc(const uint8_t* base, uint64_t base_len, const pdb_blk* blk, uint64
           (e = hipMemcpyAsync(ws + off_exp, expected + x.first, x.count * 4, hipMemcpyHostToDevice, cs)) != hipSuccess)
         return hip_fail(e, "hipMemcpyAsync(expected)");
       if ((e = pipe.end_copies(k)) != hipSuccess) return hip_fail(e, "hipEventRecord(staged)");
-      e = launch_desc(st->geom, st->d_tables, ws, reinterpret_cast<const pdb_blk*>(ws + off_desc), x.count, flags,
+      e = launch_desc(dev->hgeom, dev->d_tables, ws, reinterpret_cast<const pdb_blk*>(ws + off_desc), x.count, flags,
                       mode, reinterpret_cast<const uint32_t*>(ws + off_exp), reinterpret_cast<uint32_t*>(ws + off_out),
                       ws + off_ok, d_nbad, s);
       if (e != hipSuccess) return hip_fail(e, "launch_desc");
@@ -507,23 +582,24 @@ int host_scalar(uint32_t init, const uint8_t* data, uint64_t n, uint32_t* out) {
   DevState* st;
   int rc = get_state(&st);
   if (rc) return rc;
-  std::lock_guard<std::mutex> lk(st->mu);
   if (st->scalar_mode == kScalarServer && n <= kServerCap) return server_call(st, init, data, n, out);
+  // launch per call (> 64 KiB, or the A/B modes): the pinned stage (st->mu) and a host context
+  std::lock_guard<std::mutex> lk(st->mu);
+  CtxLock cl(st);
   hipError_t e = hipSetDevice(st->device);
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
-  if ((rc = server_park(st))) return rc;
   if ((rc = ensure_stage(st, kStageHdr + align_up(n, 256)))) return rc;
   memcpy(st->h_stage + kStageHdr, data, n);
   uint32_t* d_res = reinterpret_cast<uint32_t*>(st->d_stage);
   volatile uint32_t* h_res = reinterpret_cast<volatile uint32_t*>(st->h_stage);
-  hipStream_t s = st->stream;
+  hipStream_t s = cl.c->stream;
   if (n < kScalarOneLeaf) {
     // The kernel's only host write is the result, after its last read of the staged bytes, so
     // seeing it change means the call is complete: spin on it instead of waiting for the
     // end-of-kernel signal.  A CRC equal to the sentinel just falls through to the stream sync.
     const uint32_t sentinel = st->seq++ * 0x9E3779B9u ^ 0x5A5A5A5Au;
     *h_res = sentinel;
-    e = launch_fixed(st->geom, st->d_tables, st->d_stage + kStageHdr, 0, static_cast<uint32_t>(n), 1,
+    e = launch_fixed(st->hgeom, st->d_tables, st->d_stage + kStageHdr, 0, static_cast<uint32_t>(n), 1,
                      PDB_CRC_USE_INIT, init, d_res, s);
     if (e != hipSuccess) return hip_fail(e, "launch_fixed(scalar)");
     if (st->scalar_mode == kScalarPoll) {
@@ -537,9 +613,9 @@ int host_scalar(uint32_t init, const uint8_t* data, uint64_t n, uint32_t* out) {
       }
     }
   } else {
-    if ((rc = ensure_ws(st, span_scratch_words(n) * 4 + 256))) return rc;
-    e = launch_span(st->geom, st->d_tables, st->d_pow2, init, st->d_stage + kStageHdr, n,
-                    reinterpret_cast<uint32_t*>(st->d_ws), d_res, s);
+    if ((rc = ensure_ws(cl.c, span_scratch_words(n) * 4 + 256))) return rc;
+    e = launch_span(st->hgeom, st->d_tables, st->d_pow2, init, st->d_stage + kStageHdr, n,
+                    reinterpret_cast<uint32_t*>(cl.c->d_ws), d_res, s);
     if (e != hipSuccess) return hip_fail(e, "launch_span(scalar)");
   }
   if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
@@ -550,12 +626,12 @@ int host_scalar(uint32_t init, const uint8_t* data, uint64_t n, uint32_t* out) {
 // Scalar Extend over a long host span: H2D, parallel segments + tree combine, 4-byte D2H.
 int host_span(uint32_t init, const uint8_t* data, uint64_t n, uint32_t* out) {
   if (n > kSpanMaxBytes) return fail(PDB_ERANGE, "span longer than 2^45 bytes");
-  DevState* st;
-  int rc = get_state(&st);
+  DevState* dev;
+  int rc = get_state(&dev);
   if (rc) return rc;
-  std::lock_guard<std::mutex> lk(st->mu);
-  if ((rc = server_park(st))) return rc;
-  hipError_t e = hipSetDevice(st->device);
+  CtxLock cl(dev);
+  HostCtx* st = cl.c;
+  hipError_t e = hipSetDevice(dev->device);
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
   const size_t off_scr = align_up(n + 16, 256);
   const size_t off_out = align_up(off_scr + span_scratch_words(n) * 4, 256);
@@ -565,7 +641,7 @@ int host_span(uint32_t init, const uint8_t* data, uint64_t n, uint32_t* out) {
   uint8_t* ws = st->d_ws;
   if ((e = hipMemcpyAsync(ws, data, n, hipMemcpyHostToDevice, s)) != hipSuccess)
     return hip_fail(e, "hipMemcpyAsync(span)");
-  e = launch_span(st->geom, st->d_tables, st->d_pow2, init, ws, n, reinterpret_cast<uint32_t*>(ws + off_scr),
+  e = launch_span(dev->hgeom, dev->d_tables, dev->d_pow2, init, ws, n, reinterpret_cast<uint32_t*>(ws + off_scr),
                   reinterpret_cast<uint32_t*>(ws + off_out), s);
   if (e != hipSuccess) return hip_fail(e, "launch_span");
   if ((e = hipMemcpyAsync(out, ws + off_out, 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
@@ -612,12 +688,12 @@ int host_sst(uint8_t* buf, uint64_t buf_len, const pdb_block_handle* h, uint64_t
   const size_t off_ok = align_up(off_h + max_count * sizeof(pdb_block_handle), 256);
   const size_t slot_bytes = align_up(off_ok + 4 * max_count, 256);  // ok bytes (verify) or masked CRCs (seal)
   const size_t nslots = groups.size() > 1 ? 2 : 1;
-  DevState* st;
-  int rc = get_state(&st);
+  DevState* dev;
+  int rc = get_state(&dev);
   if (rc) return rc;
-  std::lock_guard<std::mutex> lk(st->mu);
-  if ((rc = server_park(st))) return rc;
-  hipError_t e = hipSetDevice(st->device);
+  CtxLock cl(dev);
+  HostCtx* st = cl.c;
+  hipError_t e = hipSetDevice(dev->device);
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
   if ((rc = ensure_ws(st, nslots * slot_bytes + 256))) return rc;
   hipStream_t s = st->stream, cs = st->copy_stream;
@@ -647,12 +723,12 @@ int host_sst(uint8_t* buf, uint64_t buf_len, const pdb_block_handle* h, uint64_t
       const pdb_block_handle* d_h = reinterpret_cast<const pdb_block_handle*>(ws + off_h);
       if (seal) {
         uint32_t* d_crc = reinterpret_cast<uint32_t*>(ws + off_ok);
-        if ((e = launch_sst_masked(st->geom, st->d_tables, ws, x.hi - x.lo, d_h, x.count, d_crc, s)) != hipSuccess)
+        if ((e = launch_sst_masked(dev->hgeom, dev->d_tables, ws, x.hi - x.lo, d_h, x.count, d_crc, s)) != hipSuccess)
           return hip_fail(e, "launch_sst_masked");
         if ((e = hipMemcpyAsync(crc.data() + x.first, d_crc, x.count * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
           return hip_fail(e, "hipMemcpyAsync(crcs)");
       } else {
-        if ((e = launch_sst(st->geom, st->d_tables, ws, x.hi - x.lo, d_h, x.count, false, ws + off_ok, d_nbad, s)) !=
+        if ((e = launch_sst(dev->hgeom, dev->d_tables, ws, x.hi - x.lo, d_h, x.count, false, ws + off_ok, d_nbad, s)) !=
             hipSuccess)
           return hip_fail(e, "launch_sst");
         if (ok && (e = hipMemcpyAsync(ok + x.first, ws + off_ok, x.count, hipMemcpyDeviceToHost, s)) != hipSuccess)

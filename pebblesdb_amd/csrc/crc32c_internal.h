@@ -48,35 +48,47 @@ hipError_t launch_span(const LaunchGeom& g, const uint32_t* d_tables, const uint
                        uint32_t init, const uint8_t* data, uint64_t n, uint32_t* scratch, uint32_t* out,
                        hipStream_t s);
 
-// crc32c_server.hip -- the scalar Extend service (persistent one-workgroup kernel).  Two boxes:
-// the request box `in` (request word + the caller's bytes, placed so that they end on a 16-B
-// boundary: data = in + sizeof(ServerBox) + ((-n) & 15)) lives in fine-grained device memory the
-// host writes through the large BAR (the GPU then polls and reads local HBM), or in pinned host
-// memory when the BAR is small; the response box `out` (resp word, exit_epoch) is pinned host
-// memory the GPU writes across PCIe.
-//   req  (host -> device, one 64-bit word, so one poll reads a whole request):
-//        bits 0..31 init (the Extend seed), 32..48 len (<= kServerCap, or kServerStop),
-//        49..63 seq (15 bits, bumped per request)
-//   resp (device -> host, one 64-bit word): bits 0..31 crc, 32..46 seq of the answered request
-//   exit_epoch: epoch of the last server instance that has left its loop
-struct ServerBox {
-  uint64_t req;
-  uint64_t pad0[7];
-  uint64_t resp;
-  uint32_t exit_epoch;
-  uint32_t pad1[13];
-  // written at exit (diagnostics): requests served, ticks (10 ns) from seeing a request to
-  // issuing its answer, polls, lifetime ticks
-  uint64_t stat_requests, stat_serve_ticks, stat_polls, stat_life_ticks;
-  uint64_t pad2[12];
-};
-static_assert(sizeof(ServerBox) == 256, "mailbox is 4 cache lines");
-constexpr uint32_t kServerCap = 64u << 10;  // largest request the server takes
-constexpr uint32_t kServerStop = 0x1FFFFu;  // len value of a stop request
+// crc32c_server.hip -- the scalar Extend service: ONE persistent workgroup of kServerWaves waves
+// serving kServerSlots request slots, so concurrent callers (the engine's writer, memtable,
+// compaction and reader threads: db/db_impl.cc:235-239) each post into their own slot without a
+// global lock, and up to kServerWaves requests are hashed at once.
+//   request area `in` (host -> device; fine-grained device memory the host writes through the
+//   large BAR, else pinned host memory):
+//     [0, 256)           ServerCtl: `stop`, bumped by the host to make the instance leave
+//     [256, 768)         req word of slot s at 256 + 8 s: bits 0..31 init (the Extend seed),
+//                        32..48 len (<= kServerCap), 49..63 seq (15 bits, bumped per request)
+//     [1024, ...)        slot s's bytes in kSlotStride-byte areas, placed so that they END on a
+//                        16-B boundary: data = in + kSlotDataOff + s kSlotStride + ((-n) & 15)
+//   response area `out` (device -> host, pinned host memory):
+//     resp word of slot s at 64 s (own cache line): bits 0..31 crc, 32..46 seq answered
+//     ServerExit at kExitOff: the epoch of the last instance that has left, and its counters
+// A request is pending while its slot's req seq differs from the resp seq, so an instance starts
+// by reading the resp words: requests an earlier instance left behind are served at once.
+constexpr uint32_t kServerSlots = 64;
+constexpr uint32_t kServerWaves = 16;        // wave w polls slots w, w + 16, w + 32, w + 48
+constexpr uint32_t kServerCap = 64u << 10;   // largest request the service takes
 constexpr uint32_t kServerSeqMask = 0x7FFFu;
-constexpr size_t kServerBytes = sizeof(ServerBox) + kServerCap + 16;
-// served0: the seq the new instance treats as already answered.
-hipError_t launch_server(const uint32_t* d_tables, ServerBox* d_in, ServerBox* d_out, uint32_t epoch,
-                         uint32_t served0, uint64_t idle_ticks, uint64_t life_ticks, hipStream_t s);
+constexpr size_t kSlotStride = kServerCap + 256;
+constexpr size_t kReqOff = 256;
+constexpr size_t kSlotDataOff = 1024;
+constexpr size_t kServerInBytes = kSlotDataOff + kServerSlots * kSlotStride;
+struct ServerCtl {
+  uint64_t stop;
+  uint64_t pad[31];
+};
+struct ServerExit {
+  uint32_t exit_epoch;
+  uint32_t pad0;
+  // diagnostics, written at exit: requests served, ticks (10 ns) from seeing a request to issuing
+  // its answer, polls (all waves), lifetime ticks
+  uint64_t stat_requests, stat_serve_ticks, stat_polls, stat_life_ticks;
+  uint64_t pad1[27];
+};
+static_assert(sizeof(ServerCtl) == 256 && sizeof(ServerExit) == 256, "mailbox records are 4 cache lines");
+constexpr size_t kExitOff = kServerSlots * 64;
+constexpr size_t kServerOutBytes = kExitOff + sizeof(ServerExit);
+// stop0: the ctl->stop value this instance runs under (it leaves when the word changes)
+hipError_t launch_server(const uint32_t* d_tables, uint8_t* d_in, uint8_t* d_out, uint32_t epoch, uint64_t stop0,
+                         uint64_t idle_ticks, uint64_t life_ticks, hipStream_t s);
 
 }  // namespace pdb

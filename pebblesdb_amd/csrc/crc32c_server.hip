@@ -1,28 +1,32 @@
 // crc32c_server.hip -- the scalar Extend service: a persistent one-workgroup kernel that serves
 // leveldb::crc32c::Extend calls (util/crc32c.h:17; called per WAL record by log_writer.cc:121,
-// per sstable block by table_builder.cc:197-199 and format.cc:97) from a pinned host mailbox.
+// per sstable block by table_builder.cc:197-199 and format.cc:97) from request slots in a mailbox.
 //
 // Why: a synchronous scalar call is latency-bound.  Launching a kernel per call costs ~10 us
 // (dispatch, wave launch, staging the 160-KiB LDS image, PCIe reads, result write;
 // profiles/r01_scalar_latency_poll.json).  The server pays dispatch and LDS staging once per
-// lifetime and then only polls its mailbox across PCIe, reads the caller's bytes, hashes them
-// with one wave and posts the CRC back into the same mapping.
+// lifetime and then only polls its mailbox, reads the caller's bytes, hashes them with one wave
+// and posts the CRC back across PCIe.
 //
-// Protocol (ServerBox, crc32c_internal.h): the host writes the bytes (placed so that they END on
-// a 16-B boundary), then ONE 64-bit request word {init, len, seq}; the server polls that word
-// (one PCIe read carries the whole request), reads the bytes (one more round trip per 16 KiB)
-// and answers with ONE 64-bit word {crc, seq}.  The server exits on a stop request (len =
-// kServerStop), after `idle_ticks` without a request, or after `life_ticks` in total
-// (s_memrealtime, 100 MHz), and writes exit_epoch = its epoch as its last act, so the host can
-// tell a live server from a finished one without a HIP call.  Every wave reaches the exit: waves 1..3 leave after staging,
-// wave 0's loop is bounded by the lifetime.
+// Protocol (crc32c_internal.h): kServerSlots request slots, each with its own request word
+// {init, len, seq} and data area; a caller thread owns a slot (no global lock on the host), writes
+// its bytes (placed so that they END on a 16-B boundary) and then the request word, and spins on
+// its slot's response word {crc, seq}.  The workgroup's kServerWaves waves each poll a quarter of
+// the slots with ONE vector load (lane l: slot w + 16 l) and serve the lowest pending one, so up
+// to kServerWaves requests are hashed at once.  A request is pending while its req seq differs
+// from its resp seq: an instance initialises its view from the resp words, so requests posted
+// while no instance was polling are served by the next one.  The instance leaves when ctl->stop
+// changes, after `idle_ticks` without a request in ANY slot, or after `life_ticks` in total
+// (s_memrealtime, 100 MHz): the first wave to see the condition sets a closing flag in LDS, every
+// wave leaves at its next poll without serving, and the last one out writes exit_epoch = its
+// epoch, so the host can tell a live server from a finished one without a HIP call.
 //
-// Per request, wave 0 hashes n bytes with the geometry of crc_stream16_kernel (16-B lane pieces,
+// Per request, a wave hashes n bytes with the geometry of crc_stream16_kernel (16-B lane pieces,
 // rounds of 4 KiB: piece c = 256r + 64j + u on lane u, chain j; 4 chains folded with shift 1024,
 // rounds chained with shift 1008, rotation by K mod 64, 6-level DPP tree over 16 << k), with every
 // piece 16-B aligned by the host's placement; the t = n mod 16 head bytes are hashed from the
 // seed on broadcast words.  Loads of up to 4 rounds (16 KiB) are issued together so a request
-// pays about one PCIe round trip per 16 KiB.
+// pays about one memory round trip per 16 KiB.
 #include "crc32c_device.h"
 
 namespace pdb {
@@ -103,64 +107,112 @@ __device__ __forceinline__ uint32_t server_hash(const char* lds, const LaneTabs&
   if (K == 0) return h;
   const uint32_t q = K & 63u;
   if (q) acc = __shfl(acc, (u + q) & 63u, 64);
-  return wave_tree_dpp<false>(lds, u, acc);
+  return wave_tree_dpp<true>(lds, u, acc);  // slot 5 holds the workgroup state
 }
 
-__global__ __launch_bounds__(256) void crc_server_kernel(const uint32_t* __restrict__ tabs, ServerBox* in,
-                                                          ServerBox* out, uint32_t epoch, uint32_t served0,
-                                                          uint64_t idle_ticks, uint64_t life_ticks) {
+__global__ __launch_bounds__(64 * kServerWaves) void crc_server_kernel(const uint32_t* __restrict__ tabs,
+                                                                        uint8_t* in, uint8_t* out, uint32_t epoch,
+                                                                        uint64_t stop0, uint64_t idle_ticks,
+                                                                        uint64_t life_ticks) {
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
   char* lds = reinterpret_cast<char*>(lds_words);
-  stage_tables<PDB_CAT_TREE16, PDB_CAT_H1008, PDB_CAT_S1024>(lds, tabs);
+  // operator slot 5 stays free (tree level 5 = shift 256 twice) and holds the workgroup's state
+  stage_tables<PDB_CAT_TREE16, PDB_CAT_H1008, PDB_CAT_S1024, /*kSkipSlot5=*/true>(lds, tabs);
+  uint32_t* wg = reinterpret_cast<uint32_t*>(lds + PDB_MAIN_BYTES + 5u * 4096u);
+  // wg[0] closing, wg[1] waves out, wg[2] requests, wg[3] polls (low 32 bits), wg[4..5] last
+  // request tick, wg[6..7] serve ticks
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) {
+    wg[0] = 0u;
+    wg[1] = 0u;
+    wg[2] = 0u;
+    wg[3] = 0u;
+    *reinterpret_cast<uint64_t*>(wg + 4) = t0;
+    *reinterpret_cast<uint64_t*>(wg + 6) = 0u;
+  }
   __syncthreads();
-  if (threadIdx.x >= 64) return;
-  const uint32_t u = threadIdx.x;
+  const uint32_t u = threadIdx.x & 63u;
+  const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const LaneTabs lt = lane_tabs(u);
   const __amdgpu_buffer_rsrc_t rin =
-      __builtin_amdgcn_make_buffer_rsrc(in, 0, static_cast<int>(kServerBytes), 0x00020000);
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  uint64_t t_last = t0;
-  uint32_t served = served0;
-  uint64_t n_req = 0, n_poll = 0, serve_ticks = 0;
+      __builtin_amdgcn_make_buffer_rsrc(in, 0, static_cast<int>(kServerInBytes), 0x00020000);
+  constexpr uint32_t kPer = kServerSlots / kServerWaves;  // slots per wave
+  const uint32_t slot = w + kServerWaves * (u < kPer ? u : 0u);
+  const uint64_t* req = reinterpret_cast<const uint64_t*>(in + kReqOff);
+  // the seq each slot last had answered, from the response words (pinned host memory)
+  uint32_t served = static_cast<uint32_t>(sys_load64(reinterpret_cast<const uint64_t*>(out + 64u * slot)) >> 32) &
+                    kServerSeqMask;
+  const ServerCtl* ctl = reinterpret_cast<const ServerCtl*>(in);
+  uint64_t t_last = t0, serve_ticks = 0;
+  uint32_t n_req = 0, n_poll = 0;
   for (;;) {
-    const uint64_t rq = sys_load64(&in->req);
+    const uint64_t rq = sys_load64(req + slot);
+    const uint64_t stop = sys_load64(&ctl->stop);
     ++n_poll;
-    const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(rq >> 32));
-    const uint32_t seq = hi >> 17, n = hi & 0x1FFFFu;
+    const uint32_t seq_l = static_cast<uint32_t>(rq >> 49);
+    const uint64_t pend = __builtin_amdgcn_ballot_w64(u < kPer && seq_l != served);
+    const bool closing = __hip_atomic_load(wg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0u;
+    if (closing || __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(stop)) != static_cast<uint32_t>(stop0) ||
+        __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(stop >> 32)) != static_cast<uint32_t>(stop0 >> 32))
+      break;
     const uint64_t now = __builtin_amdgcn_s_memrealtime();
-    if (seq != served) {
-      served = seq;
-      if (n > kServerCap) break;  // stop request
+    if (pend) {
       // no acquire fence: every load of the request bytes is system-coherent (sc0 sc1) and is
       // issued only after this poll returned (control dependency), so it sees the bytes the host
       // wrote before the request word (x86 store order + sfence, PCIe posted-write order)
-      const uint32_t init = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(rq));
-      const uint32_t crc =
-          ~server_hash(lds, lt, u, rin, static_cast<uint32_t>(sizeof(ServerBox)) + ((0u - n) & 15u), n, ~init);
-      if (u == 0) sys_store64(&out->resp, (static_cast<uint64_t>(seq) << 32) | crc);
+      const uint32_t l = static_cast<uint32_t>(__builtin_ctzll(pend));
+      const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(rq >> 32), l);
+      const uint32_t init = __builtin_amdgcn_readlane(static_cast<uint32_t>(rq), l);
+      const uint32_t sq = hi >> 17, n = hi & 0x1FFFFu;
+      const uint32_t s_srv = w + kServerWaves * l;
+      uint32_t crc = 0;
+      if (n <= kServerCap) {  // (a malformed length is answered with 0 rather than read out of range)
+        const uint32_t data_off = static_cast<uint32_t>(kSlotDataOff + s_srv * kSlotStride) + ((0u - n) & 15u);
+        crc = ~server_hash(lds, lt, u, rin, data_off, n, ~init);
+      }
+      if (u == 0) sys_store64(reinterpret_cast<uint64_t*>(out + 64u * s_srv), (static_cast<uint64_t>(sq) << 32) | crc);
+      if (u == l) served = sq;
       t_last = now;
+      if (u == 0) *reinterpret_cast<uint64_t*>(wg + 4) = now;  // any wave's request keeps all alive
       ++n_req;
       serve_ticks += __builtin_amdgcn_s_memrealtime() - now;
       continue;
     }
-    if (now - t_last > idle_ticks || now - t0 > life_ticks) break;
+    const uint64_t last = *reinterpret_cast<volatile uint64_t*>(wg + 4);
+    const uint64_t seen = last > t_last ? last : t_last;
+    if (now - seen > idle_ticks || now - t0 > life_ticks) {
+      if (u == 0) __hip_atomic_store(wg, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      break;
+    }
     __builtin_amdgcn_s_sleep(2);
   }
+  // the last wave out publishes the exit (and the counters)
+  uint32_t out_before = 0;
   if (u == 0) {
-    sys_store64(&out->stat_requests, n_req);
-    sys_store64(&out->stat_serve_ticks, serve_ticks);
-    sys_store64(&out->stat_polls, n_poll);
-    sys_store64(&out->stat_life_ticks, __builtin_amdgcn_s_memrealtime() - t0);
+    __hip_atomic_fetch_add(wg + 2, n_req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_add(wg + 3, n_poll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(wg + 6), static_cast<unsigned long long>(serve_ticks),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    out_before = __hip_atomic_fetch_add(wg + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  out_before = __builtin_amdgcn_readfirstlane(out_before);
+  if (out_before + 1u == kServerWaves && u == 0) {
+    ServerExit* ex = reinterpret_cast<ServerExit*>(out + kExitOff);
+    sys_store64(&ex->stat_requests, __hip_atomic_load(wg + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+    sys_store64(&ex->stat_serve_ticks, __hip_atomic_load(reinterpret_cast<unsigned long long*>(wg + 6),
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+    sys_store64(&ex->stat_polls, __hip_atomic_load(wg + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+    sys_store64(&ex->stat_life_ticks, __builtin_amdgcn_s_memrealtime() - t0);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    sys_store32(&out->exit_epoch, epoch);
+    sys_store32(&ex->exit_epoch, epoch);
   }
 }
 
 }  // namespace
 
-hipError_t launch_server(const uint32_t* d_tables, ServerBox* d_in, ServerBox* d_out, uint32_t epoch,
-                         uint32_t served0, uint64_t idle_ticks, uint64_t life_ticks, hipStream_t s) {
-  hipLaunchKernelGGL(crc_server_kernel, dim3(1), dim3(256), 0, s, d_tables, d_in, d_out, epoch, served0,
+hipError_t launch_server(const uint32_t* d_tables, uint8_t* d_in, uint8_t* d_out, uint32_t epoch, uint64_t stop0,
+                         uint64_t idle_ticks, uint64_t life_ticks, hipStream_t s) {
+  hipLaunchKernelGGL(crc_server_kernel, dim3(1), dim3(64 * kServerWaves), 0, s, d_tables, d_in, d_out, epoch, stop0,
                      idle_ticks, life_ticks);
   return hipGetLastError();
 }
