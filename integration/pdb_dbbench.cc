@@ -55,6 +55,7 @@ struct Flags {
   bool use_existing_db = false;
   bool paranoid_checks = false;
   int threads = 1;  // readrandom / readseq: db_bench --threads (db_bench.cc:1071-1110)
+  bool hash = false;  // readseq: FNV-1a-64 of every key and value (parity checks between builds)
   std::string db = "/tmp/pdb_dbbench";
 } F;
 
@@ -223,9 +224,17 @@ Result ReadSeq(leveldb::DB* db) {
   long n = 0;
   long long bytes = 0;
   const int reads = F.reads < 0 ? F.num : F.reads;
+  uint64_t h = 1469598103934665603ull;
+  auto fnv = [&h](const leveldb::Slice& x) {
+    for (size_t i = 0; i < x.size(); ++i) h = (h ^ static_cast<unsigned char>(x[i])) * 1099511628211ull;
+  };
   const double t0 = NowSec();
   for (it->SeekToFirst(); n < reads && it->Valid(); it->Next()) {
     bytes += it->key().size() + it->value().size();
+    if (F.hash) {
+      fnv(it->key());
+      fnv(it->value());
+    }
     ++n;
   }
   if (!it->status().ok()) {
@@ -233,7 +242,9 @@ Result ReadSeq(leveldb::DB* db) {
     exit(1);
   }
   delete it;
-  return Result{"readseq", n, NowSec() - t0, bytes, ""};
+  char note[64] = "";
+  if (F.hash) snprintf(note, sizeof(note), "(hash %016llx)", static_cast<unsigned long long>(h));
+  return Result{"readseq", n, NowSec() - t0, bytes, note};
 }
 
 bool Arg(const char* a, const char* name, std::string* v) {
@@ -273,6 +284,7 @@ int main(int argc, char** argv) {
     else if (Arg(argv[i], "--use_existing_db", &v)) F.use_existing_db = atoi(v.c_str()) != 0;
     else if (Arg(argv[i], "--paranoid_checks", &v)) F.paranoid_checks = atoi(v.c_str()) != 0;
     else if (Arg(argv[i], "--threads", &v)) F.threads = atoi(v.c_str());
+    else if (Arg(argv[i], "--hash", &v)) F.hash = atoi(v.c_str()) != 0;
     else if (Arg(argv[i], "--db", &v)) F.db = v;
     else {
       fprintf(stderr, "invalid flag '%s'\n", argv[i]);
@@ -281,9 +293,25 @@ int main(int argc, char** argv) {
   }
   const leveldb::FilterPolicy* fp = F.bloom_bits >= 0 ? leveldb::NewBloomFilterPolicy(F.bloom_bits) : NULL;
   leveldb::Cache* cache = F.cache_size >= 0 ? leveldb::NewLRUCache(F.cache_size) : NULL;
+  if (F.benchmarks.compare(0, 6, "repair") == 0) F.use_existing_db = true;  // repairs the given database
   if (!F.use_existing_db) leveldb::DestroyDB(F.db, leveldb::Options());
   printf("Keys:       16 bytes each\nValues:     %d bytes each\nEntries:    %d\nverify_checksums: %d\n", F.value_size,
          F.num, F.verify_checksums ? 1 : 0);
+  // "repair" first in --benchmarks: leveldb::RepairDB on the closed database (db/repair.cc), with
+  // --paranoid_checks every table is scanned with verify_checksums (repair.cc:262-267) and a table
+  // that fails is rewritten through a TableBuilder (repair.cc:339-391)
+  if (F.benchmarks.compare(0, 6, "repair") == 0) {
+    leveldb::Options o;
+    o.filter_policy = fp;
+    o.block_cache = cache;
+    o.paranoid_checks = F.paranoid_checks;
+    const double t0 = NowSec();
+    leveldb::Status s = leveldb::RepairDB(F.db, o);
+    Report(Result{"repair", 1, NowSec() - t0, 0, "(" + s.ToString() + ")"});  // + the hook counters
+    if (!s.ok()) return 1;
+    F.benchmarks = F.benchmarks.size() > 7 ? F.benchmarks.substr(7) : std::string();
+    F.use_existing_db = true;
+  }
   leveldb::DB* db = Open(fp, cache);
   size_t pos = 0;
   while (pos <= F.benchmarks.size()) {

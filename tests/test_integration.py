@@ -286,3 +286,23 @@ def test_paranoid_fill_and_verified_scan_through_readahead(gpu, tmp_path):
                             f"--db={db}"])
     assert rc3 == 0, out3 + err3
     assert _bench_json(out2)["readseq"]["ops"] == _bench_json(out3)["readseq"]["ops"] == rs["ops"]
+
+
+def test_repairdb_paranoid_gpu_matches_reference(gpu, tmp_path):
+    """RepairDB with paranoid_checks (db/repair.cc:262-267: every table scanned with
+    verify_checksums; a table that fails is rewritten through a TableBuilder, :339-391) through the
+    GPU hooks -- integration/pdb_table.cc's verified read-ahead windows and the batched
+    TableBuilder seals -- on a database the reference engine wrote and one byte of which was then
+    damaged: the same per-table / per-log repair reports as the reference build, and the same
+    recovered entries (count and FNV hash of every key and value)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from test_attribution import _damaged_db, repair_and_scan
+
+    cpu, mine = _exe("pdb_dbbench_cpu"), _exe("pdb_dbbench_gpu_table")
+    src, big = _damaged_db(tmp_path, cpu)
+    ref_log, ref_seq, _ = repair_and_scan(cpu, src, str(tmp_path / "ref"))
+    my_log, my_seq, hook = repair_and_scan(mine, src, str(tmp_path / "mine"))
+    assert any("Corruption: block checksum mismatch" in l for l in ref_log), ref_log
+    assert any("entries repaired" in l for l in ref_log), ref_log
+    assert my_log == ref_log and my_seq == ref_seq
+    assert hook["scan_batches"] > 0 and hook["seal_blocks"] > 0 and hook["verify_failed"] > 0
