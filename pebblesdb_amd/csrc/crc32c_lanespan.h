@@ -128,6 +128,20 @@ struct TabsS4 {
 #pragma unroll
     for (uint32_t c = 0; c < 4; ++c) x[c] = xor3(xor3(v[4 * c], v[4 * c + 1], v[4 * c + 2]), v[4 * c + 3], w[c]);
   }
+  // three chains stepped together (the 27-word parts' steps before chain D starts): all 12
+  // lookups issued before the first result is consumed, as in step4
+  __device__ static __forceinline__ void step3(const char* lds, const LT& lt, uint32_t (&x)[3], const uint32_t (&w)[3]) {
+    uint32_t a[12], v[12];
+#pragma unroll
+    for (uint32_t c = 0; c < 3; ++c)
+#pragma unroll
+      for (uint32_t i = 0; i < 4; ++i) a[4 * c + i] = __builtin_amdgcn_perm(lt.t[i], x[c], lt.s[i]);
+#pragma unroll
+    for (uint32_t j = 0; j < 12; ++j) v[j] = lds_u32(lds, a[j]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (uint32_t c = 0; c < 3; ++c) x[c] = xor3(xor3(v[4 * c], v[4 * c + 1], v[4 * c + 2]), v[4 * c + 3], w[c]);
+  }
   __device__ static __forceinline__ void stage(char* lds, const uint32_t* __restrict__ tabs) {
     // T0..T3 x 8 replicas: 256 entries x 4 tables x 2 quads of 16 B; quad i at b<<8 | k<<5 | h<<4
     for (uint32_t i = threadIdx.x; i < 2048u; i += blockDim.x) {
@@ -290,7 +304,8 @@ struct SpanItem {
 // 5 every staging read at a lane-skewed, bank-conflict-free address, 6 that and the fold operators'
 // lookups too, 7 no p-word state replacement, 8 no cross-lane folds, 9 no in-part folds (XORs);
 // exact A/B forms: 10 the round-2 finish (a table step per chain before the folds, bpermute
-// partners), 11 the shipped finish with bpermute partners.  TP: the table scheme.
+// partners), 11 the shipped finish with bpermute partners, 13 the A, B, C steps issued one chain
+// at a time (round 2).  TP: the table scheme.
 // kDyn: the workgroup owns batches [g nbat / G, (g + 1) nbat / G) and its waves take the next one
 // from an LDS counter (false: batch wave_id + k W, the round-2 static assignment -- diagnostics).
 template <class Src, class Sink, uint32_t MAXN, int MODE = 0, class TP = TabsS4, bool kDyn = true>
@@ -573,9 +588,16 @@ __global__ __launch_bounds__(SpanStage<MAXN>::kWaves * 64) void crc_lanespan_ker
         TP::step4(lds, lt, x4, w4);
         xa = x4[0], xb = x4[1], xc = x4[2], xd = x4[3];
       } else if (abc) {
-        xa = TP::step(lds, lt, xa, wa);
-        xb = TP::step(lds, lt, xb, wb);
-        xc = TP::step(lds, lt, xc, wc);
+        if constexpr (MODE == 13) {  // A/B: three separate steps (round 2)
+          xa = TP::step(lds, lt, xa, wa);
+          xb = TP::step(lds, lt, xb, wb);
+          xc = TP::step(lds, lt, xc, wc);
+        } else {
+          uint32_t x3[3] = {xa, xb, xc};
+          const uint32_t w3[3] = {wa, wb, wc};
+          TP::step3(lds, lt, x3, w3);
+          xa = x3[0], xb = x3[1], xc = x3[2];
+        }
       } else if (dd) {
         xd = TP::step(lds, lt, xd, wd);
       }

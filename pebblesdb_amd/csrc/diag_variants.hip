@@ -1022,11 +1022,13 @@ hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tab
       break;
     }
     case 118:    // exact: the round-2 finish (table step per chain before the folds, bpermute partners)
-    case 119: {  // exact: the shipped finish with bpermute partners (no DPP)
+    case 119:    // exact: the shipped finish with bpermute partners (no DPP)
+    case 121: {  // exact: the A, B, C chain steps issued one chain at a time (round 2)
       const uint32_t cls = (flags & PDB_CRC_SIZE_256) ? 256u
                            : (flags & PDB_CRC_SIZE_512) ? 512u : ((flags & PDB_CRC_SIZE_1K) ? 1152u : 1023u);
       if (v == 118) launch_lanespan<DescSrc, OutSink, 10>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
-      else launch_lanespan<DescSrc, OutSink, 11>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
+      else if (v == 119) launch_lanespan<DescSrc, OutSink, 11>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
+      else launch_lanespan<DescSrc, OutSink, 13>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
       break;
     }
     case 115:    // pricing (wrong CRCs): no p-word replacement selects
