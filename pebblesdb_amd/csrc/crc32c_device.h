@@ -484,13 +484,17 @@ __device__ __forceinline__ void stage_tables_q4(char* lds, const uint32_t* __res
 }
 
 // partial4k<4> on the lane-quarter image: four 4-word chains, Horner folds through the replicated
-// shift 1024 / shift 2048
+// shift 1024 / shift 2048.  kDeferF: the chains stop with their last word still unshifted (3 table
+// steps instead of 4): the final table step F (shift 4) commutes with every shift operator of the
+// folds and the tree, so the caller applies it ONCE to the tree's result -- 1 step per 4 blocks
+// instead of 16 per lane per block (-18 % LDS lookups, -15 % VALU per block).
+template <bool kDeferF = true>
 __device__ __forceinline__ uint32_t partial4k_q(const char* lds, const QuadTabs& qt, uint32_t c0, const u32x4 (&v)[4]) {
   uint32_t x0 = c0 ^ v[0].x, x1 = v[1].x, x2 = v[2].x, x3 = v[3].x;
   const uint32_t d0[4] = {v[0].x, v[0].y, v[0].z, v[0].w}, d1[4] = {v[1].x, v[1].y, v[1].z, v[1].w};
   const uint32_t d2[4] = {v[2].x, v[2].y, v[2].z, v[2].w}, d3[4] = {v[3].x, v[3].y, v[3].z, v[3].w};
 #pragma unroll
-  for (int i = 1; i <= 4; ++i) {
+  for (int i = 1; i <= (kDeferF ? 3 : 4); ++i) {
     x0 = step4x(lds, qt, x0, i < 4 ? d0[i] : 0u);
     x1 = step4x(lds, qt, x1, i < 4 ? d1[i] : 0u);
     x2 = step4x(lds, qt, x2, i < 4 ? d2[i] : 0u);
@@ -512,8 +516,9 @@ __device__ __forceinline__ uint32_t partial4k_q(const char* lds, const QuadTabs&
 // locality: +8 %).  Results are parked in a register and flushed as one 64-lane
 // store per 16 groups.  The A/B variants of this kernel (piece shapes, waves per CU, lock-step
 // period, XCD numbering, quad transposes) live in the diagnostics library (diag_device.h).
-// kW: waves per workgroup (one workgroup per CU); 16 shipped, 8 / 12 A/B variants.
-template <uint32_t kW = kWavesPerWg>
+// kW: waves per workgroup (one workgroup per CU); 16 shipped, 8 / 12 A/B variants.  kDeferF: one
+// table step per 4 blocks after the tree (partial4k_q); false = the round-2 form (A/B).
+template <uint32_t kW = kWavesPerWg, bool kDeferF = true>
 __global__ __launch_bounds__(64 * kW) void crc_pack4k_kernel(
     const uint32_t* __restrict__ tabs, const uint8_t* __restrict__ base, uint64_t stride,
     uint64_t nblk, uint32_t flags, uint32_t init, uint32_t* __restrict__ out) {
@@ -542,9 +547,10 @@ __global__ __launch_bounds__(64 * kW) void crc_pack4k_kernel(
       u32x4 cur[4] = {buf[0], buf[1], buf[2], buf[3]};
       const uint64_t bn = bk + nw;
       if (bn < nblk) load4k<4, true>(buf, base, stride, bn, u);  // wave-uniform
-      p[r] = bk < nblk ? partial4k_q(lds, qt, c0, cur) : 0u;
+      p[r] = bk < nblk ? partial4k_q<kDeferF>(lds, qt, c0, cur) : 0u;
     }
-    const uint32_t v = tree4_packed(lds, u, p[0], p[1], p[2], p[3], QuadTree<128, -1>{qt});
+    uint32_t v = tree4_packed(lds, u, p[0], p[1], p[2], p[3], QuadTree<128, -1>{qt});
+    if constexpr (kDeferF) v = step4x(lds, qt, v, 0u);  // F: the chains' last words
     // lane 4j+r of the 64-block window holds block (window + (4j+r)*nw): move lanes 0..3's
     // results up by 4*(group mod 16) with one bpermute, park, flush every 16 groups.
     const uint32_t slot = (it & 15u) * 4u;
@@ -1129,6 +1135,24 @@ __device__ __forceinline__ uint32_t chain16(const char* lds, const LT& lt, uint3
   return step4x(lds, lt, x, 0u);
 }
 
+// chain16 with its last word still unshifted (the final table step deferred to after the folds,
+// as in partial4k_q)
+template <class LT>
+__device__ __forceinline__ uint32_t chain16p(const char* lds, const LT& lt, uint32_t start, const u32x4& e, uint32_t nx,
+                                             uint32_t s) {
+  uint32_t w0 = e.x, w1 = e.y, w2 = e.z, w3 = e.w;
+  if (s) {
+    w0 = __builtin_amdgcn_alignbyte(e.y, e.x, s);
+    w1 = __builtin_amdgcn_alignbyte(e.z, e.y, s);
+    w2 = __builtin_amdgcn_alignbyte(e.w, e.z, s);
+    w3 = __builtin_amdgcn_alignbyte(nx, e.w, s);
+  }
+  uint32_t x = start ^ w0;
+  x = step4x(lds, lt, x, w1);
+  x = step4x(lds, lt, x, w2);
+  return step4x(lds, lt, x, w3);
+}
+
 // LT: the table image -- QuadTabs (lane-quarter: T0..T3, shift 1024 and shift 1008 conflict-free;
 // shipped) or LaneTabs (32 replicas of T0..T3, single-copy operators; A/B diagnostics).
 // kBal (descriptor lists): byte-balanced workgroup ranges (bal_bound) instead of equal block counts.
@@ -1587,8 +1611,10 @@ constexpr uint32_t kSlowList = 64u;
 // 32-replica image with single-copy operators; A/B diagnostics)
 // kUA (A/B, variant 70): body pieces loaded at their exact byte addresses (unaligned dwordx4)
 // instead of 4-B aligned + the DPP neighbour dword + v_alignbyte.
+// kDeferF: the body chains stop with their last word unshifted and ONE table step follows the tree
+// (chain16p; false = every chain finished before the folds, round 2 -- A/B).
 template <class Src, class Sink, bool kNT, int kRows, bool kDiagNoFold = false, int kBlk = 4, class LT = QuadTabs,
-          bool kUA = false>
+          bool kUA = false, bool kDeferF = true>
 __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ tabs, Src src, uint64_t nblk,
                                                   Sink sink) {
   static_assert(kRows == 0 || kRows == 1 || kRows == 4, "no body (records <= 256 B), 1-KiB or 4-KiB bodies");
@@ -1738,10 +1764,10 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
         nx[j] = __builtin_amdgcn_update_dpp(j + 1 < kRows ? __builtin_amdgcn_readlane(e[j + 1 < kRows ? j + 1 : j].x, 0) : cl,
                                             e[j].x, 0x130, 0xF, 0xF, false);
     }
-    uint32_t a = chain16(lds, lt, u == 0 ? P : 0u, e[0], nx[0], s);
+    uint32_t a = kDeferF ? chain16p(lds, lt, u == 0 ? P : 0u, e[0], nx[0], s) : chain16(lds, lt, u == 0 ? P : 0u, e[0], nx[0], s);
 #pragma unroll
     for (int j = 1; j < kRows; ++j) {
-      const uint32_t x = chain16(lds, lt, 0u, e[j], nx[j], s);
+      const uint32_t x = kDeferF ? chain16p(lds, lt, 0u, e[j], nx[j], s) : chain16(lds, lt, 0u, e[j], nx[j], s);
       // kDiagNoFold (A/B diagnostics only, WRONG CRCs): the Horner fold replaced by a XOR, to price
       // the shift-operator lookups
       a = kDiagNoFold ? (a ^ x) : horner1024(lds, lt, a, x);
@@ -1813,6 +1839,7 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
           v = tree4_packed(lds, u, part[0], part[1], part[2], part[3], tops());
         else
           v = tree8_packed(lds, u, part, tops());
+        if constexpr (kDeferF) v = step4x(lds, lt, v, 0u);  // F: the body chains' last words
         if constexpr (kRing != 0)
           park(v, G, fastbits, nv);
         else if (u < nv && ((fastbits >> u) & 1u))
@@ -1896,7 +1923,8 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
         if (fastbits & 2u) part[1] = body_partial(&c1, cl1, static_cast<uint32_t>((G.p[1] + G.n[1]) & 3u), P[1]);
         if (fastbits & 4u) part[2] = body_partial(&c2, cl2, static_cast<uint32_t>((G.p[2] + G.n[2]) & 3u), P[2]);
         if (fastbits & 8u) part[3] = body_partial(&c3, cl3, static_cast<uint32_t>((G.p[3] + G.n[3]) & 3u), P[3]);
-        const uint32_t v = tree4_packed(lds, u, part[0], part[1], part[2], part[3], tops());
+        uint32_t v = tree4_packed(lds, u, part[0], part[1], part[2], part[3], tops());
+        if constexpr (kDeferF) v = step4x(lds, lt, v, 0u);  // F: the body chains' last words
         if (u < nv && ((fastbits >> u) & 1u)) SinkOps<Sink>::put(sink, grp + u, v, G.ld, pre);
         defer(G, fastbits, nv);
         if (ngrp >= g_hi) {
@@ -1953,7 +1981,8 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
         if (fastbits & 32u) part[5] = body_partial(&c5, cl5, static_cast<uint32_t>((G.p[5] + G.n[5]) & 3u), P[5]);
         if (fastbits & 64u) part[6] = body_partial(&c6, cl6, static_cast<uint32_t>((G.p[6] + G.n[6]) & 3u), P[6]);
         if (fastbits & 128u) part[7] = body_partial(&c7, cl7, static_cast<uint32_t>((G.p[7] + G.n[7]) & 3u), P[7]);
-        const uint32_t v = tree8_packed(lds, u, part, tops());
+        uint32_t v = tree8_packed(lds, u, part, tops());
+        if constexpr (kDeferF) v = step4x(lds, lt, v, 0u);  // F: the body chains' last words
         if (u < nv && ((fastbits >> u) & 1u)) SinkOps<Sink>::put(sink, grp + u, v, G.ld, pre);
         defer(G, fastbits, nv);
         if (ngrp >= g_hi) {
@@ -2011,10 +2040,10 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
 }
 
 // kBlk = 8 (A/B): 8-block groups, prefixes <= 128 B in rows of 8 lanes, one tree8_packed.
-template <class Src, class Sink, bool kNT, int kBlk = 4, class LT = QuadTabs, bool kUA = false>
+template <class Src, class Sink, bool kNT, int kBlk = 4, class LT = QuadTabs, bool kUA = false, bool kDeferF = true>
 __global__ __launch_bounds__(kThreads) void crc_sst4k_kernel(const uint32_t* __restrict__ tabs, Src src,
                                                              uint64_t nblk, Sink sink) {
-  sized_kernel_body<Src, Sink, kNT, 4, false, kBlk, LT, kUA>(tabs, src, nblk, sink);
+  sized_kernel_body<Src, Sink, kNT, 4, false, kBlk, LT, kUA, kDeferF>(tabs, src, nblk, sink);
 }
 
 // (the 1-KiB body has no Horner fold: both images measure the same, +0.8 % for the lane-quarter

@@ -595,6 +595,15 @@ hipError_t launch_sst_variant(int v, const LaunchGeom& g, const uint32_t* d_tabl
                          n, SstVerifySink{ok, nbad});
     return hipGetLastError();
   }
+  if (v == 48) {  // every body chain finished before the folds (round 2; the shipped kernel defers it)
+    if (seal)
+      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ParkSealSink<64>, true, 4, QuadTabs, false, false>), grid, block, 0, s,
+                         d_tables, src, n, ParkSealSink<64>{});
+    else
+      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstVerifySink, true, 4, QuadTabs, false, false>), grid, block, 0, s,
+                         d_tables, src, n, SstVerifySink{ok, nbad});
+    return hipGetLastError();
+  }
   if (v == 38) {  // 8-block groups (prefixes <= 128 B in rows of 8 lanes, tree8_packed)
     if (seal)
       hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SealSink, true, 8>), grid, block, 0, s, d_tables, src, n,
@@ -893,6 +902,8 @@ hipError_t launch_fixed_variant(int v, const LaunchGeom& g, const uint32_t* d_ta
                                 nblk, flags, init, out); break;
     case 46: hipLaunchKernelGGL((crc_pack4k_kernel<12>), dim3(grid_forw(g, nblk, 12)), dim3(768), 0, s, d_tables, base,
                                 stride, nblk, flags, init, out); break;
+    // the shipped kernel with every chain finished before the folds (round 2)
+    case 47: PDB_K((crc_pack4k_kernel<16, false>)); break;
     // 99 (and unknown ids): the round-1 shipped kernel, on the 32-replica table image with
     // single-copy Horner operators (crc_pack4k_kernel now runs on the lane-quarter image)
     default: PDB_K((crc_pack4k_ab_kernel<1, 4, true>)); break;
