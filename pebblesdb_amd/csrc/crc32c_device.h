@@ -1156,7 +1156,11 @@ __device__ __forceinline__ uint32_t chain16p(const char* lds, const LT& lt, uint
 // LT: the table image -- QuadTabs (lane-quarter: T0..T3, shift 1024 and shift 1008 conflict-free;
 // shipped) or LaneTabs (32 replicas of T0..T3, single-copy operators; A/B diagnostics).
 // kBal (descriptor lists): byte-balanced workgroup ranges (bal_bound) instead of equal block counts.
-template <class Src, class Sink, bool kDyn, bool kNT, bool kPack = false, class LT = QuadTabs, bool kBal = false>
+// kDeferF: every chain stops with its last word unshifted (chain16p); the lane accumulator is
+// finished by ONE table step where a round hands it on (before shift 1008) and after the final
+// tree, instead of one step per chain (false: round 2 -- A/B).
+template <class Src, class Sink, bool kDyn, bool kNT, bool kPack = false, class LT = QuadTabs, bool kBal = false,
+          bool kDeferF = true>
 __global__ __launch_bounds__(kThreads) void crc_stream16_kernel(const uint32_t* __restrict__ tabs,
                                                                  Src src, uint64_t nblk, Sink sink) {
   constexpr bool kQuad = __is_same(LT, QuadTabs);
@@ -1278,6 +1282,7 @@ __global__ __launch_bounds__(kThreads) void crc_stream16_kernel(const uint32_t* 
   issue(B, mB.d, 0);
   uint32_t acc = 0;
   uint32_t park0 = 0, park1 = 0, park2 = 0, park3 = 0, npark = 0;
+  uint32_t pfin = 0;  // kDeferF: bit r = parked block r is a head-only block (its part is a full state)
   uint64_t pid0 = 0, pid1 = 0, pid2 = 0, pid3 = 0;
   BlkDesc pd0{}, pd1{}, pd2{}, pd3{};
   auto flush = [&]() {
@@ -1286,6 +1291,11 @@ __global__ __launch_bounds__(kThreads) void crc_stream16_kernel(const uint32_t* 
       v = tree4_packed<kL5Twice>(lds, u, park0, park1, park2, park3, QuadTree<128, -1>{lt});
     else
       v = tree4_packed<kL5Twice>(lds, u, park0, park1, park2, park3);
+    if constexpr (kDeferF) {  // F: the chains' last words (lane r holds block r)
+      const uint32_t f = step4x(lds, lt, v, 0u);
+      v = ((pfin >> (u & 3u)) & 1u) ? v : f;
+      pfin = 0;
+    }
     if (u < npark) {
       const uint64_t id = u == 0 ? pid0 : (u == 1 ? pid1 : (u == 2 ? pid2 : pid3));
       const BlkDesc bd = u == 0 ? pd0 : (u == 1 ? pd1 : (u == 2 ? pd2 : pd3));
@@ -1345,9 +1355,13 @@ __global__ __launch_bounds__(kThreads) void crc_stream16_kernel(const uint32_t* 
     if (J) {
       // chain j runs (once, for the whole wave) only if some lane has a piece in it: a block of
       // 1 KiB needs 2 of the 5 chains, not all of them (wave-uniform conditions on rem)
-      const uint32_t start = ck ? round1008(lds, lt, acc) : acc;
+      // (kDeferF: the accumulator of the rounds before is finished first)
+      const uint32_t start = ck ? round1008(lds, lt, kDeferF ? step4x(lds, lt, acc, 0u) : acc) : acc;
       const bool full = !last_round;
-      uint32_t a = chain16(lds, lt, start, e0, n0, s);
+      auto ch = [&](uint32_t st0, const u32x4& e, uint32_t nx) {
+        return kDeferF ? chain16p(lds, lt, st0, e, nx, s) : chain16(lds, lt, st0, e, nx, s);
+      };
+      uint32_t a = ch(start, e0, n0);
       // shift 1024: slot 7 of the 32-replica image (its slot 6 holds 1008), image 0 of the other
       auto fold = [&](uint32_t x, uint32_t y) {
         if constexpr (kQuad)
@@ -1356,19 +1370,19 @@ __global__ __launch_bounds__(kThreads) void crc_stream16_kernel(const uint32_t* 
           return shift_op_x(lds, 7, x, y);
       };
       if (full || rem > 64u) {
-        const uint32_t x1 = chain16(lds, lt, 0u, e1, n1, s);
+        const uint32_t x1 = ch(0u, e1, n1);
         if (J > 1) a = fold(a, x1);
       }
       if (full || rem > 128u) {
-        const uint32_t x2 = chain16(lds, lt, 0u, e2, n2, s);
+        const uint32_t x2 = ch(0u, e2, n2);
         if (J > 2) a = fold(a, x2);
       }
       if (full || rem > 192u) {
-        const uint32_t x3 = chain16(lds, lt, 0u, e3, n3, s);
+        const uint32_t x3 = ch(0u, e3, n3);
         if (J > 3) a = fold(a, x3);
       }
       if (!full && rem > 256u) {  // the last round's fifth chain
-        const uint32_t x4 = chain16(lds, lt, 0u, e4, n4, s);
+        const uint32_t x4 = ch(0u, e4, n4);
         if (J > 4) a = fold(a, x4);
       }
       acc = a;
@@ -1383,6 +1397,7 @@ __global__ __launch_bounds__(kThreads) void crc_stream16_kernel(const uint32_t* 
           part = __builtin_amdgcn_readfirstlane(acc);  // head state (lane 0)
           part = u == 63u ? part : 0u;
         }
+        if (kDeferF && !K) pfin |= 1u << npark;  // wave-uniform
         switch (npark) {  // wave-uniform
           case 0: park0 = part; pid0 = mcur.i; pd0 = cd; break;
           case 1: park1 = part; pid1 = mcur.i; pd1 = cd; break;
@@ -1396,6 +1411,7 @@ __global__ __launch_bounds__(kThreads) void crc_stream16_kernel(const uint32_t* 
           const uint32_t q = K & 63u;
           if (q) acc = __shfl(acc, (u + q) & 63u, 64);
           raw = wave_tree_dpp<kL5Twice>(lds, u, acc);
+          if constexpr (kDeferF) raw = step4x(lds, lt, raw, 0u);
         }
         if (u == 0) sink.put(mcur.i, raw, cd);
       }

@@ -946,6 +946,10 @@ hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tab
       hipLaunchKernelGGL((crc_stream16_kernel<DescSrc, OutSink, true, true, true, QuadTabs, true>), grid, block, 0, s,
                          d_tables, src, nblk, sink);
       break;
+    case 49:  // the C3 routing with every chain finished before the folds (round 2)
+      hipLaunchKernelGGL((crc_stream16_kernel<DescSrc, OutSink, true, true, true, QuadTabs, true, false>), grid, block, 0,
+                         s, d_tables, src, nblk, sink);
+      break;
     case 71:  // the any-length kernel with equal block counts per workgroup (round-2 C3 routing before bal_bound)
       hipLaunchKernelGGL((crc_stream16_kernel<DescSrc, OutSink, true, true, true>), grid, block, 0, s, d_tables, src,
                          nblk, sink);
