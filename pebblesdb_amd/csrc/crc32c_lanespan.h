@@ -305,7 +305,9 @@ struct SpanItem {
 // lookups too, 7 no p-word state replacement, 8 no cross-lane folds, 9 no in-part folds (XORs);
 // exact A/B forms: 10 the round-2 finish (a table step per chain before the folds, bpermute
 // partners), 11 the shipped finish with bpermute partners, 13 the A, B, C steps issued one chain
-// at a time (round 2).  TP: the table scheme.
+// at a time (round 2), 14 no bank-spread choice of the halves (records 0-7 | 8-15 always), 15 the
+// first row's choice for the whole batch.
+// TP: the table scheme.
 // kDyn: the workgroup owns batches [g nbat / G, (g + 1) nbat / G) and its waves take the next one
 // from an LDS counter (false: batch wave_id + k W, the round-2 static assignment -- diagnostics).
 template <class Src, class Sink, uint32_t MAXN, int MODE = 0, class TP = TabsS4, bool kDyn = true>
@@ -364,6 +366,7 @@ __global__ __launch_bounds__(SpanStage<MAXN>::kWaves * 64) void crc_lanespan_ker
   uint32_t bpre = 0;     // per lane: the sink's word
   uint64_t bfastm = 0;   // in-class records
   uint64_t bbroken = 0;  // bit r: records r and r + 1 may not share an item
+  uint64_t bswap = 0;    // k = 4: bit 16 r + 15 = row r's item splits its records into halves as C (next_item)
   uint32_t bcursor = 64;
   LaneSpanGeom bg{1u, 64u, 65536u, NI};
 
@@ -409,6 +412,31 @@ __global__ __launch_bounds__(SpanStage<MAXN>::kWaves * 64) void crc_lanespan_ker
     const uint32_t nw = wave_max_u32(bfast ? (bn + 3u) >> 2 : 0u);
     bg = span_pick<KMAX, ST>(nw ? nw : 1u);
     bcursor = 0;
+    // Bank spread of the staging reads (k = 4: 4 lanes per record, 8 records per 32-lane half).
+    // Every lane reads its words at (part end) / 4 + t, so the LDS banks of a read instruction are
+    // the half's 32 part-end dword residues mod 32, the same at every step; equal-sized records can
+    // pile onto a few banks (431-B records: 4-way conflicts on every staging read).  For each row
+    // of 16 records (one full item), count the distinct banks of the two ways of splitting it into
+    // halves -- records 0-7 | 8-15 (A) or 0-3, 8-11 | 4-7, 12-15 (C) -- and keep the better (bit
+    // 16 r + 15 of bswap: row r takes C).
+    bswap = 0;
+    if (MODE != 14 && bg.k == 4u) {
+      // the lane's 4 part-end residues: ew, ew - P, ew - 2P, ew - 3P (mod 32) = a rotation of one
+      // constant mask; quad-OR, then per row the two splits' distinct-bank counts by DPP in lane
+      // 16 r + 15 (row_shr 4: quads 0|1 and 2|3; row_shr 8: quads 0|2 and 1|3)
+      constexpr uint32_t kM0 = (1u << 0) | (1u << ((32u - ST::kPart % 32u) % 32u)) |
+                               (1u << ((64u - 2u * ST::kPart % 32u) % 32u)) | (1u << ((96u - 3u * ST::kPart % 32u) % 32u));
+      const uint32_t ew = ((plo + bn) >> 2) & 31u;
+      uint32_t msk = bfast ? __builtin_amdgcn_alignbit(kM0, kM0, (32u - ew) & 31u) : 0u;
+      msk |= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(msk), 0x111, 0xF, 0xF, false));
+      msk |= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(msk), 0x112, 0xF, 0xF, false));
+      const uint32_t pa = __builtin_popcount(msk | static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(msk), 0x114, 0xF, 0xF, false)));
+      const uint32_t pc = __builtin_popcount(msk | static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(msk), 0x118, 0xF, 0xF, false)));
+      const uint32_t da = pa + static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(pa), 0x118, 0xF, 0xF, false));
+      const uint32_t dc = pc + static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(pc), 0x114, 0xF, 0xF, false));
+      bswap = __builtin_amdgcn_ballot_w64((u & 15u) == 15u && dc > da);
+      if constexpr (MODE == 15) bswap = (bswap & 0x8000ull) ? 0x8000800080008000ull : 0ull;  // row 0 decides for the batch
+    }
     if constexpr (MODE == 4) ++n_batches;
     return true;
   };
@@ -466,12 +494,18 @@ __global__ __launch_bounds__(SpanStage<MAXN>::kWaves * 64) void crc_lanespan_ker
       it.p_loc = act ? plo - lo32 : kNoRec;
       it.e_loc = act ? plo + bn - lo32 : 0u;
     } else {
-      const uint32_t slot = (u * bg.magic) >> 16;
+      uint32_t slot = (u * bg.magic) >> 16;
       const uint32_t c = u - slot * bg.k;
-      const bool act = slot < m;
-      const uint32_t rl = act ? g0 + slot : u;
-      const uint32_t pr = __shfl(plo, rl, 64);
-      const uint32_t nr = __shfl(bn, rl, 64);
+      bool act;
+      uint32_t rl, pr = 0, nr = 0;
+      // k = 4, an item of 16 records aligned on a row of the batch: open_batch chose how to split
+      // them into the two 32-lane halves (bswap)
+      if (MODE != 14 && bg.k == 4u && (g0 & 15u) == 0 && m == 16u && ((bswap >> (g0 | 15u)) & 1u))
+        slot = (slot & 3u) | ((slot & 4u) << 1) | ((slot & 8u) >> 1);  // slot bits 2 and 3 exchanged
+      act = slot < m;
+      rl = act ? g0 + slot : u;
+      pr = __shfl(plo, rl, 64);
+      nr = __shfl(bn, rl, 64);
       it.pre = __shfl(bpre, rl, 64);
       it.r = rl;
       it.c = c;

@@ -20,7 +20,20 @@ from pebblesdb_amd import crc32c, diag  # noqa: E402
 
 WL = {"wal100": (131, 1 << 30, crc32c.SIZE_256), "wal400": (431, 2 << 30, crc32c.SIZE_512),
       "wal700": (700, 2 << 30, crc32c.SIZE_1023), "wal1000": (1000, 2 << 30, crc32c.SIZE_1023),
-      "wal": (1055, 4 << 30, crc32c.SIZE_1K)}
+      "wal": (1055, 4 << 30, crc32c.SIZE_1K),
+      # records of random sizes (uniform in [lo, hi) B incl. the type byte, 7-B headers between)
+      "rand300_500": ((300, 500), 2 << 30, crc32c.SIZE_512), "rand64_1000": ((64, 1000), 2 << 30, crc32c.SIZE_1023),
+      "wal419": (419, 2 << 30, crc32c.SIZE_512), "wal463": (463, 2 << 30, crc32c.SIZE_512),
+      "wal443": (443, 2 << 30, crc32c.SIZE_512)}
+
+
+def layout(payload, nbytes):
+    if isinstance(payload, tuple):
+        rng = np.random.default_rng(7)
+        lens = rng.integers(payload[0], payload[1], size=int(nbytes / (sum(payload) / 2 + 7)))
+        offs = np.concatenate([[0], np.cumsum(lens + 7)[:-1]]) + 6
+        return offs.astype(np.int64), lens.astype(np.int64)
+    return wal_layout(nbytes, payload)
 PRICING = {113, 114, 115, 116, 117}
 
 
@@ -31,9 +44,9 @@ def main():
     crc32c.init_device(0)
     for wl in wls:
         payload, nbytes, hint = WL[wl]
-        offs, lens = wal_layout(nbytes, payload)
+        offs, lens = layout(payload, nbytes)
         d = torch.empty(int(offs[-1] + lens[-1]) + 64, dtype=torch.uint8, device="cuda")
-        diag.fill_splitmix(d, payload)
+        diag.fill_splitmix(d, payload if isinstance(payload, int) else 7 * payload[0] + payload[1])
         d_blk = crc32c.blocks_to_device(crc32c.make_blocks(offs, lens))
         out = torch.empty(len(offs), dtype=torch.int32, device="cuda")
         algo = int(lens.sum()) + 20 * len(lens)
