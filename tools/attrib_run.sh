@@ -29,8 +29,19 @@ step() {  # name timeout cmd...
   timeout -k 10 "$to" "$@" > "$OUT/$name.log" 2>&1 || rc=$?
   echo "[attrib] $name rc=$rc wall_ms=$(( ($(date +%s%N) - t0) / 1000000 ))" | tee -a "$OUT/steps.txt"
   grep -a "micros/op\|teardown" "$OUT/$name.log" | tee -a "$OUT/steps.txt" || true
+  local lines=0
+  lines=$(grep -ac '^{"bench"' "$OUT/$name.log") || true
   grep -a '^{"bench"' "$OUT/$name.log" >> "$OUT/bench_lines.jsonl" || true
-  if [ $rc -ne 0 ]; then echo "[attrib] stopping after rc=$rc" | tee -a "$OUT/steps.txt"; exit $rc; fi
+  # a fault after every benchmark of the step reported (the engine's shutdown race)
+  # is logged with its backtrace and the next step reopens the database (WAL recovery); a step that
+  # did not finish its benchmarks, or a time limit, stops the script
+  if [ $rc -ne 0 ] && { [ "$lines" -eq 0 ] || [ $rc -eq 124 ] || [ $rc -eq 137 ]; }; then
+    echo "[attrib] stopping after rc=$rc" | tee -a "$OUT/steps.txt"; exit $rc
+  fi
+  if [ $rc -ne 0 ]; then
+    echo "[attrib] $name: rc=$rc after its benchmarks reported (teardown); backtrace:" | tee -a "$OUT/steps.txt"
+    grep -a -A 24 "fatal signal" "$OUT/$name.log" >> "$OUT/steps.txt" || true
+  fi
 }
 for v in $VARIANTS; do
   db="$DBROOT/$v"
