@@ -48,10 +48,15 @@ constexpr uint32_t kSpanStageBase = 64u << 10;                    // tables and 
 // words, kPart = 3 kLC + kLD words per lane.  33-word parts (kLD = 9) for <= 256 B (a 131-B record
 // on one lane) and 513..1023 B (up to 8 lanes); 27-word parts (kLD = 3) for 257..512 B, where 4
 // lanes of 27 words cover a 431-B record exactly instead of 4 x 33 = 132 words for its 108.
-template <uint32_t MAXN>
+// The 1024..1152-B class takes 10 x 9 KiB too: eight 1062-B records (1055-B fragments + headers)
+// do not fit 8 KiB, so 8-KiB items held 7 records on 56 of the 64 lanes (+2.5 % with 9 KiB,
+// −4..−9 % for the 512 and 1023 classes, whose 8 records fit 8 KiB; profiles/r03_wide/).
+// kWide (diagnostics MODE 16): 10 x 9 KiB for every class.
+template <uint32_t MAXN, bool kWide = false>
 struct SpanStage {
-  static constexpr uint32_t kWaves = MAXN <= 256u ? 10u : 12u;  // (13 x 7 KiB for 512: slower, 128-VGPR cap)
-  static constexpr uint32_t kJ = MAXN <= 256u ? 9u : 8u;
+  static constexpr bool k9 = MAXN <= 256u || MAXN > 1023u || kWide;
+  static constexpr uint32_t kWaves = k9 ? 10u : 12u;  // (13 x 7 KiB for 512: slower, 128-VGPR cap)
+  static constexpr uint32_t kJ = k9 ? 9u : 8u;
   static constexpr uint32_t kRegion = kJ * 1024u;
   static constexpr uint32_t kUsable = kRegion - 16u;  // span limit: reads stay inside
   static_assert((64u << 10) + kWaves * kRegion <= PDB_LDS_BYTES, "fits the 160 KiB");
@@ -306,16 +311,16 @@ struct SpanItem {
 // exact A/B forms: 10 the round-2 finish (a table step per chain before the folds, bpermute
 // partners), 11 the shipped finish with bpermute partners, 13 the A, B, C steps issued one chain
 // at a time (round 2), 14 no bank-spread choice of the halves (records 0-7 | 8-15 always), 15 the
-// first row's choice for the whole batch.
+// first row's choice for the whole batch, 16 10 waves x 9-KiB regions for every class.
 // TP: the table scheme.
 // kDyn: the workgroup owns batches [g nbat / G, (g + 1) nbat / G) and its waves take the next one
 // from an LDS counter (false: batch wave_id + k W, the round-2 static assignment -- diagnostics).
 template <class Src, class Sink, uint32_t MAXN, int MODE = 0, class TP = TabsS4, bool kDyn = true>
-__global__ __launch_bounds__(SpanStage<MAXN>::kWaves * 64) void crc_lanespan_kernel(const uint32_t* __restrict__ tabs, Src src,
+__global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void crc_lanespan_kernel(const uint32_t* __restrict__ tabs, Src src,
                                                                        uint64_t nblk, Sink sink) {
-  constexpr uint32_t kSpanWaves = SpanStage<MAXN>::kWaves, kSpanJ = SpanStage<MAXN>::kJ;
-  constexpr uint32_t kSpanRegion = SpanStage<MAXN>::kRegion, kSpanUsable = SpanStage<MAXN>::kUsable;
-  typedef SpanStage<MAXN> ST;
+  constexpr uint32_t kSpanWaves = SpanStage<MAXN, MODE == 16>::kWaves, kSpanJ = SpanStage<MAXN, MODE == 16>::kJ;
+  constexpr uint32_t kSpanRegion = SpanStage<MAXN, MODE == 16>::kRegion, kSpanUsable = SpanStage<MAXN, MODE == 16>::kUsable;
+  typedef SpanStage<MAXN, MODE == 16> ST;
   constexpr uint32_t LC = ST::kLC, LD = ST::kLD, NI = ST::kNI, PART = ST::kPart;
   static_assert(MAXN + 32u <= kSpanUsable, "a record of the class must fit a region");
   // k parts cover MAXN: 2, 5, 8 (a longer class -- diagnostics 1152 -- stays at 8 lanes and runs
@@ -750,19 +755,19 @@ template <class Src, class Sink, int MODE = 0, class TP = TabsS4, bool kDyn = tr
 void launch_lanespan(const LaunchGeom& g, const uint32_t* d_tables, const Src& src, uint64_t nblk, uint32_t cls,
                      const Sink& sink, hipStream_t s) {
   if (cls <= 256u) {
-    constexpr uint32_t w = SpanStage<256>::kWaves;
+    constexpr uint32_t w = SpanStage<256, MODE == 16>::kWaves;
     hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 256, MODE, TP, kDyn>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0, s,
                        d_tables, src, nblk, sink);
   } else if (cls <= 512u) {
-    constexpr uint32_t w = SpanStage<512>::kWaves;
+    constexpr uint32_t w = SpanStage<512, MODE == 16>::kWaves;
     hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 512, MODE, TP, kDyn>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0, s,
                        d_tables, src, nblk, sink);
   } else if (cls <= 1023u) {
-    constexpr uint32_t w = SpanStage<1023>::kWaves;
+    constexpr uint32_t w = SpanStage<1023, MODE == 16>::kWaves;
     hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 1023, MODE, TP, kDyn>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0,
                        s, d_tables, src, nblk, sink);
   } else {  // 1024..1152 B (WAL records of ~1-KiB write batches): 8 lanes, the head chain past 1056 B
-    constexpr uint32_t w = SpanStage<1152>::kWaves;
+    constexpr uint32_t w = SpanStage<1152, MODE == 16>::kWaves;
     hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 1152, MODE, TP, kDyn>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0,
                        s, d_tables, src, nblk, sink);
   }

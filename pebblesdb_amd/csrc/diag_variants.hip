@@ -1040,14 +1040,16 @@ hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tab
     case 119:    // exact: the shipped finish with bpermute partners (no DPP)
     case 121:    // exact: the A, B, C chain steps issued one chain at a time (round 2)
     case 122:    // exact: halves always records 0-7 | 8-15 (no bank-spread choice)
-    case 123: {  // exact: the first row's bank-spread choice taken for the whole batch
+    case 123:    // exact: the first row's bank-spread choice taken for the whole batch
+    case 124: {  // exact: 10 waves x 9-KiB regions for every class
       const uint32_t cls = (flags & PDB_CRC_SIZE_256) ? 256u
                            : (flags & PDB_CRC_SIZE_512) ? 512u : ((flags & PDB_CRC_SIZE_1K) ? 1152u : 1023u);
       if (v == 118) launch_lanespan<DescSrc, OutSink, 10>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
       else if (v == 119) launch_lanespan<DescSrc, OutSink, 11>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
       else if (v == 121) launch_lanespan<DescSrc, OutSink, 13>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
       else if (v == 122) launch_lanespan<DescSrc, OutSink, 14>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
-      else launch_lanespan<DescSrc, OutSink, 15>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
+      else if (v == 123) launch_lanespan<DescSrc, OutSink, 15>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
+      else launch_lanespan<DescSrc, OutSink, 16>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
       break;
     }
     case 115:    // pricing (wrong CRCs): no p-word replacement selects
