@@ -78,6 +78,11 @@ typedef struct pdb_block_handle {
 #define PDB_CRC_SIZE_256 0x10u /* most blocks 1..256 B: small WAL / MANIFEST records */
 #define PDB_CRC_SIZE_512 0x20u /* most blocks 257..512 B: WAL records of ~400-B values */
 #define PDB_CRC_SIZE_1023 0x40u /* most blocks 513..1023 B: WAL records of ~500..990-B values */
+/* With PDB_CRC_SIZE_512 / _1023: the lengths vary within the class (records of varied values), so
+ * each record is hashed on as many lanes as its own length needs instead of the batch's longest
+ * record's (+10..50 % on such logs; about -2 % on logs of equal records, so it is a hint).  Host
+ * batch entries set it themselves from the lengths. */
+#define PDB_CRC_SIZE_MIXED 0x80u
 
 /* error codes */
 #define PDB_OK 0

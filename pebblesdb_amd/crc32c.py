@@ -32,7 +32,9 @@ SIZE_4K = 0x8  # PDB_CRC_SIZE_4K: most blocks 4096..4352 B (sstable data blocks)
 SIZE_256 = 0x10  # PDB_CRC_SIZE_256: most blocks 1..256 B (small WAL / MANIFEST records)
 SIZE_512 = 0x20  # PDB_CRC_SIZE_512: most blocks 257..512 B (WAL records of ~400-B values)
 SIZE_1023 = 0x40  # PDB_CRC_SIZE_1023: most blocks 513..1023 B
-_SIZE_HINT = {None: 0, "1k": SIZE_1K, "4k": SIZE_4K, "256": SIZE_256, "512": SIZE_512, "1023": SIZE_1023}
+SIZE_MIXED = 0x80  # PDB_CRC_SIZE_MIXED: with 512 / 1023, lengths varying within the class (per-record lanes)
+_SIZE_HINT = {None: 0, "1k": SIZE_1K, "4k": SIZE_4K, "256": SIZE_256, "512": SIZE_512, "1023": SIZE_1023,
+              "512m": SIZE_512 | SIZE_MIXED, "1023m": SIZE_1023 | SIZE_MIXED}
 K_MASK_DELTA = 0xA282EAD8  # util/crc32c.h:24
 
 BLK_DTYPE = np.dtype([("off", "<u8"), ("len", "<u4"), ("init", "<u4")])  # == pdb_blk (16 B)

@@ -431,6 +431,31 @@ uint64_t host_chunk_bytes() {
   return v;
 }
 
+// PDB_CRC_SIZE_MIXED for the 512 / 1023 record classes: the record kernel's per-record lanes
+// (crc32c_lanespan.h, open_batch) pay when a batch of 64 consecutive records needs fewer items with
+// them than with every record on the longest one's lane count; set when a quarter of the batches do
+// (a log of equal records with its block-end fragments never does).
+static bool mixed_lengths(const pdb_blk* blk, uint64_t nblk, uint32_t cls) {
+  const uint32_t part_words = cls == 512u ? 27u : 33u, kmax = cls == 512u ? 5u : 8u;
+  uint64_t nb = 0, win = 0;
+  for (uint64_t b = 0; b < nblk; b += 64) {
+    uint32_t kmx = 0, sumk = 0, nf = 0;
+    for (uint64_t i = b; i < nblk && i < b + 64; ++i) {
+      const uint32_t len = blk[i].len;
+      if (len - 1u > cls - 1u) continue;  // outside the class: the whole-wave path
+      const uint32_t k = std::min(kmax, ((len + 3u) / 4u + part_words - 1u) / part_words);
+      sumk += k;
+      kmx = std::max(kmx, k);
+      ++nf;
+    }
+    if (!nf) continue;
+    ++nb;
+    const uint32_t g = 64u / kmx;
+    if ((sumk + 63u) / 64u < (nf + g - 1u) / g) ++win;
+  }
+  return nb && 4 * win >= nb;
+}
+
 struct HostGroup {
   uint64_t first, count, lo, hi;
 };
@@ -501,6 +526,8 @@ int host_desc(const uint8_t* base, uint64_t base_len, const pdb_blk* blk, uint64
     else if (4 * n256 >= 3 * nblk) flags |= PDB_CRC_SIZE_256;
     else if (4 * (n256 + n512) >= 3 * nblk) flags |= PDB_CRC_SIZE_512;  // the 17-group window takes 1..512 B
     else if (4 * (n256 + n512 + n1023) >= 3 * nblk) flags |= PDB_CRC_SIZE_1023;  // 33 groups: 1..1024 B
+    if ((flags & (PDB_CRC_SIZE_512 | PDB_CRC_SIZE_1023)) && mixed_lengths(blk, nblk, (flags & PDB_CRC_SIZE_512) ? 512u : 1023u))
+      flags |= PDB_CRC_SIZE_MIXED;
   }
   // lo keeps the source's 16-B phase so the kernels' fast loads stay aligned
   size_t need = 0;

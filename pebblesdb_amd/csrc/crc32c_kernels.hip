@@ -169,7 +169,8 @@ hipError_t launch_desc_sink(const LaunchGeom& g, const uint32_t* d_tables, const
       hipLaunchKernelGGL((crc_sst4k_kernel<DescSrc, Sink, true>), grid, block, 0, s, d_tables, src, nblk, sink);
     else  // records of 1..1023 B: one lane per record, the bytes staged through LDS by coalesced loads
       launch_lanespan(g, d_tables, src, nblk,
-                      (flags & PDB_CRC_SIZE_256) ? 256u : ((flags & PDB_CRC_SIZE_512) ? 512u : 1023u), sink, s);
+                      (flags & PDB_CRC_SIZE_256) ? 256u : ((flags & PDB_CRC_SIZE_512) ? 512u : 1023u), sink, s,
+                      (flags & PDB_CRC_SIZE_MIXED) != 0);
     return hipGetLastError();
   }
   // descriptor lists of any lengths (C3: Zipf sizes at byte offsets): 16-B lane pieces with nt

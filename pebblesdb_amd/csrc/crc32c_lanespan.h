@@ -267,6 +267,28 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
   return max(max(a, b), max(c, d));
 }
 
+// OR over the wave of a 32-bit value; every lane must be active
+__device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
+  v |= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0xB1, 0xF, 0xF, false));
+  v |= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x4E, 0xF, 0xF, false));
+  v |= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x141, 0xF, 0xF, false));
+  v |= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x140, 0xF, 0xF, false));
+  return (__builtin_amdgcn_readlane(v, 0) | __builtin_amdgcn_readlane(v, 16)) |
+         (__builtin_amdgcn_readlane(v, 32) | __builtin_amdgcn_readlane(v, 48));
+}
+
+// inclusive prefix sum over the wave's lanes (lane u: v_0 + .. + v_u); every lane must be active
+__device__ __forceinline__ uint32_t wave_incl_add_u32(uint32_t v, uint32_t u) {
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x111, 0xF, 0xF, false));  // row_shr:1
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x112, 0xF, 0xF, false));  // row_shr:2
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x114, 0xF, 0xF, false));  // row_shr:4
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x118, 0xF, 0xF, false));  // row_shr:8
+  const uint32_t r0 = __builtin_amdgcn_readlane(v, 15), r1 = __builtin_amdgcn_readlane(v, 31);
+  const uint32_t r2 = __builtin_amdgcn_readlane(v, 47);
+  const uint32_t row = u >> 4;
+  return v + (row >= 1u ? r0 : 0u) + (row >= 2u ? r1 : 0u) + (row >= 3u ? r2 : 0u);
+}
+
 // k for a batch whose longest in-class record has nw words: the fewest chain steps per batch,
 // items per batch x steps per item, with the records an item can hold: G = floor(64 / k), and
 // what fits a staging region at ~4 nw + 8 bytes a record
@@ -296,9 +318,13 @@ struct SpanItem {
   uint64_t batch;   // records 64 * batch + r
   uintptr_t lo;     // 16-B aligned global address of region byte 0
   uint32_t hi;      // local end: max over the item's records (0: nothing to hash)
-  uint32_t k, iters;
+  uint32_t k, iters;            // k: lanes per record (var: the most any record of the item takes)
   bool valid;
-  uint32_t r, c;               // per lane: record slot in the batch, part
+  bool var;                     // per-record lane counts (mixed sizes; open_batch)
+  uint32_t r;                   // per lane: record slot in the batch
+  uint32_t cw;                  // per lane: part c; kVar classes pack (one VGPR per item in flight)
+                                // c (bits 0-3) and the record's parts after it, kl - 1 - c (4-7),
+                                // + the item's records (8-14) and first record (16-21) in MODE 18
   uint32_t p_loc, e_loc, pre;  // per lane: local start (kNoRec: no record), local end, sink word
 };
 
@@ -311,11 +337,14 @@ struct SpanItem {
 // exact A/B forms: 10 the round-2 finish (a table step per chain before the folds, bpermute
 // partners), 11 the shipped finish with bpermute partners, 13 the A, B, C steps issued one chain
 // at a time (round 2), 14 no bank-spread choice of the halves (records 0-7 | 8-15 always), 15 the
-// first row's choice for the whole batch, 16 10 waves x 9-KiB regions for every class.
+// first row's choice for the whole batch, 16 10 waves x 9-KiB regions for every class, 17 the
+// batch-uniform k only (no per-record lanes for mixed sizes), 18 the item geometry instead of the CRC
+// (first record << 24 | records << 16 | lane << 8 | lanes << 4 | per-record mode; diagnostics).
 // TP: the table scheme.
 // kDyn: the workgroup owns batches [g nbat / G, (g + 1) nbat / G) and its waves take the next one
 // from an LDS counter (false: batch wave_id + k W, the round-2 static assignment -- diagnostics).
-template <class Src, class Sink, uint32_t MAXN, int MODE = 0, class TP = TabsS4, bool kDyn = true>
+// kMixed (PDB_CRC_SIZE_MIXED): per-record lane counts where a batch's records vary (open_batch).
+template <class Src, class Sink, uint32_t MAXN, int MODE = 0, class TP = TabsS4, bool kDyn = true, bool kMixed = false>
 __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void crc_lanespan_kernel(const uint32_t* __restrict__ tabs, Src src,
                                                                        uint64_t nblk, Sink sink) {
   constexpr uint32_t kSpanWaves = SpanStage<MAXN, MODE == 16>::kWaves, kSpanJ = SpanStage<MAXN, MODE == 16>::kJ;
@@ -327,6 +356,11 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void cr
   // the head chain alone for the rest)
   constexpr uint32_t KMAX = (MAXN / 4u + PART) / PART > 8u ? 8u : (MAXN / 4u + PART) / PART;
   static_assert(KMAX >= 1 && KMAX <= 8, "tree folds for up to 8 lanes per record");
+  // per-record lanes for mixed sizes (open_batch): the 257..512- and 513..1023-B classes, whose
+  // records take 3..5 and 4..8 lanes; the 9-KiB-region classes (<= 256 B: 1-2 lanes; 1024..1152 B:
+  // always 8) have no registers to spare for it (their 2 x 9 staging chunks in flight), nor has the
+  // verify form (an expected word per item in flight: it spilled 24-28 B per lane with it)
+  constexpr bool kVar = kMixed && MODE != 17 && (MAXN == 512u || MAXN == 1023u) && !__is_same(Sink, VerifySink);
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
   char* lds = reinterpret_cast<char*>(lds_words);
   TP::stage(lds, tabs);
@@ -372,6 +406,10 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void cr
   uint64_t bfastm = 0;   // in-class records
   uint64_t bbroken = 0;  // bit r: records r and r + 1 may not share an item
   uint64_t bswap = 0;    // k = 4: bit 16 r + 15 = row r's item splits its records into halves as C (next_item)
+  bool bvar = false;     // mixed sizes: record r on bkr lanes (not the batch-uniform k)
+  uint32_t bkw = 0;      // per lane: the record's lanes kr = ceil(words / PART) <= KMAX (bits 0-3; 0: not in
+                         // the class) | the inclusive prefix sum of kr over the batch (bits 4..)
+  uint32_t bkmax = 1, biters_v = NI;
   uint32_t bcursor = 64;
   LaneSpanGeom bg{1u, 64u, 65536u, NI};
 
@@ -417,6 +455,43 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void cr
     const uint32_t nw = wave_max_u32(bfast ? (bn + 3u) >> 2 : 0u);
     bg = span_pick<KMAX, ST>(nw ? nw : 1u);
     bcursor = 0;
+    // Mixed sizes: the batch-uniform k is set by the longest record, so a short record's lanes
+    // would hash padding.  Per-record lanes instead: record r on kr = ceil(words / PART) lanes
+    // (<= KMAX; the head chain runs on past KMAX parts), an item's records on consecutive lane
+    // ranges (exclusive prefix sums of kr); taken when the item-count model says it pays:
+    // items x (steps + 4), items bounded by the lanes (sum kr / 64) and the staging span.
+    bvar = false;
+    if constexpr (kVar) {
+      const uint32_t nwr = (bn + 3u) >> 2;
+      const uint32_t kq = (nwr + PART - 1u) / PART;
+      const uint32_t bkr = bfast ? (kq < KMAX ? (kq ? kq : 1u) : KMAX) : 0u;
+      bkw = bkr;
+      // the longest record's lanes from the batch's longest record (nw, above); records on fewer
+      // lanes save at most kmx - 1 each: fewer than 32 lanes saved cannot drop an item (a log of
+      // equal records with its block-end fragments) -- no scan, no extra cost on such batches
+      const uint32_t kq1 = (nw + PART - 1u) / PART;
+      const uint32_t kmx = kq1 < KMAX ? (kq1 ? kq1 : 1u) : KMAX;
+      const uint32_t nsmall = static_cast<uint32_t>(__builtin_popcountll(__builtin_amdgcn_ballot_w64(bfast && bkr < kmx)));
+      if (nsmall * (kmx - 1u) >= 32u) {
+        const uint32_t bks = wave_incl_add_u32(bkr, u);
+        bkw = bkr | (bks << 4);
+        const uint32_t sumk = __builtin_amdgcn_readlane(bks, 63);
+        const uint32_t limr = bfast && nwr > bkr * PART ? nwr - bkr * PART : 0u;
+        const uint32_t iv = NI + wave_max_u32(limr);
+        const uint32_t f0 = static_cast<uint32_t>(__builtin_ctzll(bfastm)), f1 = 63u - static_cast<uint32_t>(__builtin_clzll(bfastm));
+        const uint32_t span = (__builtin_amdgcn_readlane(plo, f1) + __builtin_amdgcn_readlane(bn, f1)) -
+                              (__builtin_amdgcn_readlane(plo, f0) & ~15u);
+        const uint32_t by_span = (span + kSpanUsable - 1u) / kSpanUsable;
+        const uint32_t nfast = static_cast<uint32_t>(__builtin_popcountll(bfastm));
+        const uint32_t iu = max((nfast + bg.g - 1u) / bg.g, by_span);
+        const uint32_t ivn = max((sumk + 63u) >> 6, by_span);
+        if (ivn * (iv + 4u) < iu * (bg.iters + 4u)) {
+          bvar = true;
+          bkmax = kmx;
+          biters_v = iv;
+        }
+      }
+    }
     // Bank spread of the staging reads (k = 4: 4 lanes per record, 8 records per 32-lane half).
     // Every lane reads its words at (part end) / 4 + t, so the LDS banks of a read instruction are
     // the half's 32 part-end dword residues mod 32, the same at every step; equal-sized records can
@@ -425,7 +500,7 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void cr
     // halves -- records 0-7 | 8-15 (A) or 0-3, 8-11 | 4-7, 12-15 (C) -- and keep the better (bit
     // 16 r + 15 of bswap: row r takes C).
     bswap = 0;
-    if (MODE != 14 && bg.k == 4u) {
+    if (MODE != 14 && bg.k == 4u && !bvar) {
       // the lane's 4 part-end residues: ew, ew - P, ew - 2P, ew - 3P (mod 32) = a rotation of one
       // constant mask; quad-OR, then per row the two splits' distinct-bank counts by DPP in lane
       // 16 r + 15 (row_shr 4: quads 0|1 and 2|3; row_shr 8: quads 0|2 and 1|3)
@@ -456,8 +531,9 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void cr
     it.hi = 0;
     it.k = bg.k;
     it.iters = bg.iters;
+    it.var = false;
     it.r = u;
-    it.c = 0;
+    it.cw = 0;
     it.p_loc = kNoRec;
     it.e_loc = 0;
     it.pre = 0;
@@ -472,8 +548,9 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void cr
     pre_next = SinkOps<Sink>::pre(sink, idx(bnext < g_end ? bnext : bcur), BlkDesc{nullptr, 0u, 0u});
     it.valid = true;
     it.batch = bcur;
-    it.k = bg.k;
-    it.iters = bg.iters;
+    it.k = bvar ? bkmax : bg.k;
+    it.iters = bvar ? biters_v : bg.iters;
+    it.var = bvar;
     if (rem == 0) {  // every record of the batch was outside the class: an empty item
       bcursor = 64;
       return it;
@@ -488,13 +565,47 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void cr
     // within a linked run the records ascend from lo: 32-bit offsets (lanes outside it are cut by m1)
     const uint64_t over = __builtin_amdgcn_ballot_w64(bfast && u >= g0 && plo + bn - lo32 > kSpanUsable) >> g0;
     const uint32_t m2 = over ? static_cast<uint32_t>(__builtin_ctzll(over)) : 64u;
+    if (kVar && bvar) {
+      // records g0.. on consecutive lane ranges: lanes of record r = [S(r) - kr - base, S(r) - base)
+      const uint32_t bkr = bkw & 15u, bks = bkw >> 4;
+      const uint32_t base = __builtin_amdgcn_readlane(bks, g0) - __builtin_amdgcn_readlane(bkr, g0);
+      const uint64_t fit = ~(__builtin_amdgcn_ballot_w64(u >= g0 && bks - base <= 64u) >> g0);
+      const uint32_t m3 = fit ? static_cast<uint32_t>(__builtin_ctzll(fit)) : 64u - g0;
+      const uint32_t m = min(min(m1, m2), m3);
+      bcursor = g0 + m;
+      it.lo = lo;
+      // the start lanes of the item's records as one 64-bit mask; lane u's record is the last
+      // start at or below u
+      const bool inr = u >= g0 && u < g0 + m;
+      const uint32_t st = bks - bkr - base;  // (lanes in range: < 64)
+      const uint32_t mlo = wave_or_u32(inr && st < 32u ? 1u << (st & 31u) : 0u);
+      const uint32_t mhi = wave_or_u32(inr && st >= 32u ? 1u << (st & 31u) : 0u);
+      const uint64_t M = (static_cast<uint64_t>(mhi) << 32) | mlo;
+      const uint32_t used = __builtin_amdgcn_readlane(bks, g0 + m - 1u) - base;
+      const uint64_t below = M & (u == 63u ? ~0ull : ((2ull << u) - 1ull));
+      const bool act = u < used && below != 0;
+      const uint32_t rel = static_cast<uint32_t>(__builtin_popcountll(below)) - 1u;
+      const uint32_t s0 = 63u - static_cast<uint32_t>(__builtin_clzll(below | 1ull));
+      const uint32_t rl = act ? g0 + rel : u;
+      // (every bpermute with all lanes active: a source lane outside EXEC reads as 0)
+      const uint32_t pr = __shfl(plo, rl, 64), nr = __shfl(bn, rl, 64);
+      const uint32_t kr = static_cast<uint32_t>(__shfl(static_cast<int>(bkr), static_cast<int>(rl), 64));
+      it.pre = __shfl(bpre, rl, 64);
+      const uint32_t c = act ? u - s0 : 0u;
+      it.cw = c | ((act ? kr - 1u - c : 0u) << 4) | (MODE == 18 ? (m << 8) | (g0 << 16) : 0u);
+      it.r = rl;
+      it.p_loc = act ? pr - lo32 : kNoRec;
+      it.e_loc = act ? pr + nr - lo32 : 0u;
+      it.hi = wave_max_u32(it.e_loc);
+      return it;
+    }
     const uint32_t m = min(min(bg.g, m1), m2);
     bcursor = g0 + m;
     it.lo = lo;
     if (bg.k == 1u && g0 == 0u) {  // the common case: lane u hashes record u
       const bool act = u < m;
       it.r = u;
-      it.c = 0;
+      it.cw = (kVar && MODE == 18) ? (m << 8) | (g0 << 16) : 0u;
       it.pre = bpre;
       it.p_loc = act ? plo - lo32 : kNoRec;
       it.e_loc = act ? plo + bn - lo32 : 0u;
@@ -513,7 +624,7 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void cr
       nr = __shfl(bn, rl, 64);
       it.pre = __shfl(bpre, rl, 64);
       it.r = rl;
-      it.c = c;
+      it.cw = kVar ? c | ((bg.k - 1u - c) << 4) | (MODE == 18 ? (m << 8) | (g0 << 16) : 0u) : c;
       it.p_loc = act ? pr - lo32 : kNoRec;
       it.e_loc = act ? pr + nr - lo32 : 0u;
     }
@@ -555,14 +666,16 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void cr
     const int32_t e = static_cast<int32_t>(it.e_loc);
     const int32_t pl = static_cast<int32_t>(it.p_loc);
     const bool act = it.p_loc != kNoRec;
-    const bool head = it.c == k - 1u;
+    // part, parts of the record after it (kVar: packed per lane; else from the uniform k)
+    const uint32_t pc = kVar ? it.cw & 15u : it.cw, pafter = kVar ? (it.cw >> 4) & 15u : k - 1u - pc;
+    const bool head = pafter == 0u;
     const uint32_t sel = static_cast<uint32_t>(e & 3) * 0x01010101u + 0x03020100u;
     const uint32_t zp = static_cast<uint32_t>(pl - e) & 3u;  // bytes of the p-word before p
     const uint32_t uz = __shfl(ureg, zp, 64);
     // The word at byte s (s = e mod 4) is the dword pair (D[s >> 2], D[(s >> 2) + 1]) through sel.
     // The p-word (at sp), masked below p with U[z] injected, replaces its chain's state at its
     // step; a chain wholly before p yields 0.
-    const int32_t eA = e - static_cast<int32_t>(4u * PART * it.c);
+    const int32_t eA = e - static_cast<int32_t>(4u * PART * pc);
     const int32_t sp = act ? pl - static_cast<int32_t>(zp) : e;  // (no record: an address in range)
     uint32_t pw;
     {
@@ -688,23 +801,25 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void cr
     // a row of 16, so the partner's value comes by DPP row_shl (no LDS round trip); other k by
     // bpermute.
     if (MODE != 8 && k > 1u) {
-      const bool dpp = MODE != 11 && !kOldFold && (k & (k - 1u)) == 0;
+      const bool dpp = MODE != 11 && !kOldFold && (k & (k - 1u)) == 0 && !it.var;
       uint32_t y = dpp ? static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(P), 0x101, 0xF, 0xF, false))
                        : __shfl_down(P, 1, 64);
-      if ((it.c & 1u) == 0 && it.c + 1u < k) P = opx(kOpP1, y, P);
+      if ((pc & 1u) == 0 && pafter >= 1u) P = opx(kOpP1, y, P);
       if (k > 2u) {
         y = dpp ? static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(P), 0x102, 0xF, 0xF, false))
                 : __shfl_down(P, 2, 64);
-        if ((it.c & 3u) == 0 && it.c + 2u < k) P = opx(kOpP2, y, P);
+        if ((pc & 3u) == 0 && pafter >= 2u) P = opx(kOpP2, y, P);
       }
       if (k > 4u) {
         y = dpp ? static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(P), 0x104, 0xF, 0xF, false))
                 : __shfl_down(P, 4, 64);
-        if ((it.c & 7u) == 0 && it.c + 4u < k) P = opx(kOpP4, y, P);
+        if ((pc & 7u) == 0 && pafter >= 4u) P = opx(kOpP4, y, P);
       }
     }
     if constexpr (!kOldFold) P = TP::step(lds, lt, P, 0u);  // F: the chains' last words
-    if (it.c == 0 && act)
+    if constexpr (MODE == 18)  // diagnostics: the item's first record, records, lane, lanes, mode
+      P = ~(((it.cw >> 16) << 24) | (((it.cw >> 8) & 127u) << 16) | (u << 8) | ((pc + pafter + 1u) << 4) | (it.var ? 1u : 0u));
+    if (pc == 0 && act)
       SinkOps<Sink>::put(sink, (it.batch << 6) + it.r, P, BlkDesc{nullptr, 0u, 0xFFFFFFFFu}, it.pre);
   };
 
@@ -753,19 +868,27 @@ inline uint32_t grid_span(const LaunchGeom& g, uint64_t nblk, uint32_t waves) {
 // and empty ones, take the whole-wave path.
 template <class Src, class Sink, int MODE = 0, class TP = TabsS4, bool kDyn = true>
 void launch_lanespan(const LaunchGeom& g, const uint32_t* d_tables, const Src& src, uint64_t nblk, uint32_t cls,
-                     const Sink& sink, hipStream_t s) {
+                     const Sink& sink, hipStream_t s, bool mixed = false) {
   if (cls <= 256u) {
     constexpr uint32_t w = SpanStage<256, MODE == 16>::kWaves;
     hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 256, MODE, TP, kDyn>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0, s,
                        d_tables, src, nblk, sink);
   } else if (cls <= 512u) {
     constexpr uint32_t w = SpanStage<512, MODE == 16>::kWaves;
-    hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 512, MODE, TP, kDyn>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0, s,
-                       d_tables, src, nblk, sink);
+    if (mixed && !__is_same(Sink, VerifySink))
+      hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 512, MODE, TP, kDyn, true>), dim3(grid_span(g, nblk, w)), dim3(w * 64),
+                         0, s, d_tables, src, nblk, sink);
+    else
+      hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 512, MODE, TP, kDyn>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0, s,
+                         d_tables, src, nblk, sink);
   } else if (cls <= 1023u) {
     constexpr uint32_t w = SpanStage<1023, MODE == 16>::kWaves;
-    hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 1023, MODE, TP, kDyn>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0,
-                       s, d_tables, src, nblk, sink);
+    if (mixed && !__is_same(Sink, VerifySink))
+      hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 1023, MODE, TP, kDyn, true>), dim3(grid_span(g, nblk, w)), dim3(w * 64),
+                         0, s, d_tables, src, nblk, sink);
+    else
+      hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 1023, MODE, TP, kDyn>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0,
+                         s, d_tables, src, nblk, sink);
   } else {  // 1024..1152 B (WAL records of ~1-KiB write batches): 8 lanes, the head chain past 1056 B
     constexpr uint32_t w = SpanStage<1152, MODE == 16>::kWaves;
     hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 1152, MODE, TP, kDyn>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0,

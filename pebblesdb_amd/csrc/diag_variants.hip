@@ -418,6 +418,133 @@ __global__ __launch_bounds__(256) void trailer_scatter_kernel(uint8_t* __restric
   tr[3] = static_cast<uint8_t>(m >> 24);
 }
 
+// Seal-pattern calibration (variants 140-142; no CRC work, trailers written with WRONG values by
+// design): the in-place seal's memory pattern without its hash -- every block's bytes [offset,
+// offset + size + 5) read as 1-KiB-contiguous 16-B nt loads by the wave owning its 4-block group,
+// groups in workgroup lock-step over the workgroup's contiguous range (the sst kernel's
+// scheduling), handles a group ahead -- with kWrite 0: no stores (the pattern's read ceiling);
+// 1: each group's 4 trailers stored (4 byte stores, like SealSink) once its loads returned;
+// 2: trailers parked 64 groups like ParkSealSink<64>, the rest written when the wave is done.
+// kAux >= 0: the loads as range-checked buffer loads with that cache policy (bit 0 sc0, bit 1 nt,
+// bit 4 sc1: 18 = device scope + nt, so the lines need not allocate in the XCD's L2).
+template <int kWrite, int kAux = -1>
+__global__ __launch_bounds__(kThreads) void seal_pattern_kernel(uint8_t* __restrict__ buf,
+                                                                const pdb_block_handle* __restrict__ h,
+                                                                uint64_t n, uint32_t* __restrict__ out,
+                                                                intptr_t shadow_delta) {
+  typedef __attribute__((address_space(1))) uint8_t g_u8;
+  const uint32_t u = threadIdx.x & 63u;
+  const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t G = gridDim.x;
+  const uint64_t lo = n * blockIdx.x / G, hi = n * (blockIdx.x + 1) / G;
+  if (lo >= hi) return;
+  uint32_t acc = 0;
+  uint32_t pv[4] = {0, 0, 0, 0};
+  uintptr_t pa[4] = {0, 0, 0, 0};
+  auto hload = [&](uint64_t b0) -> u32x4 {  // lane r < 4: block b0 + r's handle (clamped)
+    const uint64_t b = b0 + (u & 3u);
+    return gload128<false>(reinterpret_cast<uintptr_t>(h + (b < hi ? b : hi - 1)));
+  };
+  u32x4 hn = hload(lo + 4u * w);
+  for (uint64_t t = 0; lo + 64u * t < hi; ++t) {
+    __syncthreads();
+    const uint64_t b0 = lo + 4u * (16u * t + w);
+    const u32x4 hc = hn;
+    keep_alive(hc);
+    hn = hload(b0 + 64u);
+    if constexpr (kWrite == 7) {
+      if (u < 4u && b0 + u < hi) {
+        g_u8* tr = reinterpret_cast<g_u8*>(reinterpret_cast<uintptr_t>(buf) +
+                                           ((static_cast<uint64_t>(hc.y) << 32) | hc.x) + hc.z + 1u);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) tr[k] = static_cast<uint8_t>(acc >> (8 * k));
+      }
+    }
+    u32x4 x = {0, 0, 0, 0};
+    uintptr_t ta = 0;  // lane r < 4: block r's trailer word address
+#pragma unroll
+    for (uint32_t r = 0; r < 4; ++r) {
+      const uint64_t off = uniform64(__builtin_amdgcn_readlane(hc.x, r), __builtin_amdgcn_readlane(hc.y, r));
+      const uint32_t sz = __builtin_amdgcn_readlane(hc.z, r);
+      const uintptr_t a0 = (reinterpret_cast<uintptr_t>(buf) + off) & ~static_cast<uintptr_t>(15);
+      const uintptr_t e = reinterpret_cast<uintptr_t>(buf) + off + sz + 5u;
+      const uint32_t last = static_cast<uint32_t>((e - 1u - a0) >> 4);
+      if constexpr (kAux < 0) {
+#pragma unroll
+        for (uint32_t j = 0; j < 5; ++j) {
+          const uint32_t c = 64u * j + u;
+          x ^= gload128<true>(a0 + 16u * (c < last ? c : last));
+        }
+      } else {
+        const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(a0), 0,
+                                                                              static_cast<int>(16u * (last + 1u)), 0x00020000);
+#pragma unroll
+        for (uint32_t j = 0; j < 5; ++j) {
+          const uint32_t c = 64u * j + u;
+          x ^= __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, static_cast<int>(16u * (c < last ? c : last)),
+                                                                                0, kAux));
+        }
+      }
+      if (u == r) ta = reinterpret_cast<uintptr_t>(buf) + off + sz + 1u;
+    }
+    const uint32_t m = x.x ^ x.y ^ x.z ^ x.w;
+    acc ^= m;
+    const bool mine = u < 4u && b0 + u < hi;
+    if constexpr (kWrite == 1 || kWrite == 3) {  // 3: into a shadow image at the same offsets
+      if (mine) {
+        g_u8* tr = reinterpret_cast<g_u8*>(ta + (kWrite == 3 ? shadow_delta : 0));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) tr[k] = static_cast<uint8_t>(m >> (8 * k));
+      }
+    } else if constexpr (kWrite == 4) {  // the aligned 16 B holding the trailer's first byte, one store
+      typedef __attribute__((address_space(1))) u32x4 g_q;
+      if (mine) *reinterpret_cast<g_q*>(ta & ~static_cast<uintptr_t>(15)) = x;
+    } else if constexpr (kWrite == 5 || kWrite == 6) {  // the aligned 128-B (6: 64-B) line holding it
+      typedef __attribute__((address_space(1))) u32x4 g_q;
+      constexpr uint32_t kL = kWrite == 5 ? 128u : 64u, kQ = kL / 16u;
+      const uint32_t r = u / kQ, q = u % kQ;
+      const uint32_t alo = static_cast<uint32_t>(__shfl(static_cast<int>(static_cast<uint32_t>(ta)), static_cast<int>(r), 64));
+      const uint32_t ahi = static_cast<uint32_t>(__shfl(static_cast<int>(static_cast<uint32_t>(ta >> 32)), static_cast<int>(r), 64));
+      const uintptr_t a = (((static_cast<uintptr_t>(ahi) << 32) | alo) & ~static_cast<uintptr_t>(kL - 1u)) + 16u * q;
+      if (r < 4u && b0 + r < hi) *reinterpret_cast<g_q*>(a) = x;
+    } else if constexpr (kWrite == 7) {  // trailers of the group stored BEFORE its loads are issued
+      // (handled above the loads; nothing here)
+    } else if constexpr (kWrite == 2) {  // group g = t of this wave: lane 4 (t mod 16) + r, slot (t / 16) mod 4
+      const uint32_t src_lane = u & 3u;
+      const uint32_t mv = __shfl(m, src_lane, 64);
+      const uint32_t alo = static_cast<uint32_t>(__shfl(static_cast<int>(static_cast<uint32_t>(ta)), src_lane, 64));
+      const uint32_t ahi = static_cast<uint32_t>(__shfl(static_cast<int>(static_cast<uint32_t>(ta >> 32)), src_lane, 64));
+      const uintptr_t av = (static_cast<uintptr_t>(ahi) << 32) | alo;
+      const bool ok = __shfl(static_cast<int>(mine), src_lane, 64) != 0;
+      const uint32_t s = static_cast<uint32_t>((t >> 4) & 3u);
+      if ((u >> 2) == (t & 15u) && ok) {
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k)
+          if (k == s) {
+            if (pa[k]) {
+              g_u8* tr = reinterpret_cast<g_u8*>(pa[k]);
+#pragma unroll
+              for (int q = 0; q < 4; ++q) tr[q] = static_cast<uint8_t>(pv[k] >> (8 * q));
+            }
+            pa[k] = av;
+            pv[k] = mv;
+          }
+      }
+    }
+  }
+  if constexpr (kWrite == 2) {
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k)
+      if (pa[k]) {
+        g_u8* tr = reinterpret_cast<g_u8*>(pa[k]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) tr[q] = static_cast<uint8_t>(pv[k] >> (8 * q));
+      }
+  }
+  for (int k = 32; k; k >>= 1) acc ^= __shfl_xor(acc, k, 64);
+  if (u == 0 && out) atomicXor(out, acc);
+}
+
 struct NtSealSink {  // A/B variant 34: the trailer as non-temporal byte stores
   __device__ __forceinline__ void put(uint64_t, uint32_t raw, const BlkDesc& d) const {
     typedef __attribute__((address_space(1))) uint8_t g_u8;
@@ -580,6 +707,39 @@ hipError_t launch_sst_variant(int v, const LaunchGeom& g, const uint32_t* d_tabl
                               hipStream_t s) {
   if (v == 0) return launch_sst(g, d_tables, buf, buf_len, h, n, seal, ok, nbad, s);
   const dim3 grid(grid_for(g, n)), block(kThreads);
+  if (v >= 140 && v <= 151 && seal) {  // seal-pattern calibration (seal_pattern_kernel<v - 140>)
+    uint32_t* xo = nbad;  // XOR of everything read (keeps the loads live); may be null
+    static uint8_t* cal_shadow = nullptr;  // diagnostics only: 143's shadow image
+    static uint64_t cal_shadow_n = 0;
+    intptr_t delta = 0;
+    if (v == 143) {
+      static std::mutex mu;
+      std::lock_guard<std::mutex> lk(mu);
+      if (cal_shadow_n < buf_len + 256) {
+        if (cal_shadow) (void)hipFree(cal_shadow);
+        cal_shadow = nullptr;
+        cal_shadow_n = 0;
+        if (hipMalloc(&cal_shadow, buf_len + 256) != hipSuccess) return hipErrorOutOfMemory;
+        cal_shadow_n = buf_len + 256;
+      }
+      delta = reinterpret_cast<intptr_t>(cal_shadow) - reinterpret_cast<intptr_t>(buf);
+    }
+    switch (v) {
+      case 140: hipLaunchKernelGGL(seal_pattern_kernel<0>, grid, block, 0, s, buf, h, n, xo, delta); break;
+      case 141: hipLaunchKernelGGL(seal_pattern_kernel<1>, grid, block, 0, s, buf, h, n, xo, delta); break;
+      case 142: hipLaunchKernelGGL(seal_pattern_kernel<2>, grid, block, 0, s, buf, h, n, xo, delta); break;
+      case 143: hipLaunchKernelGGL(seal_pattern_kernel<3>, grid, block, 0, s, buf, h, n, xo, delta); break;
+      case 144: hipLaunchKernelGGL(seal_pattern_kernel<4>, grid, block, 0, s, buf, h, n, xo, delta); break;
+      case 145: hipLaunchKernelGGL(seal_pattern_kernel<5>, grid, block, 0, s, buf, h, n, xo, delta); break;
+      case 146: hipLaunchKernelGGL(seal_pattern_kernel<6>, grid, block, 0, s, buf, h, n, xo, delta); break;
+      case 147: hipLaunchKernelGGL(seal_pattern_kernel<7>, grid, block, 0, s, buf, h, n, xo, delta); break;
+      case 148: hipLaunchKernelGGL((seal_pattern_kernel<1, 18>), grid, block, 0, s, buf, h, n, xo, delta); break;  // sc1 nt loads + stores
+      case 149: hipLaunchKernelGGL((seal_pattern_kernel<1, 19>), grid, block, 0, s, buf, h, n, xo, delta); break;  // sc0 sc1 nt loads + stores
+      case 150: hipLaunchKernelGGL((seal_pattern_kernel<0, 18>), grid, block, 0, s, buf, h, n, xo, delta); break;  // sc1 nt loads only
+      default: hipLaunchKernelGGL((seal_pattern_kernel<1, 2>), grid, block, 0, s, buf, h, n, xo, delta); break;      // nt buffer loads + stores
+    }
+    return hipGetLastError();
+  }
   const SstSrc src{buf, h, buf_len};
   if (v == 97 && !seal) {  // WRONG CRCs by design: verify without the Horner folds (prices them)
     hipLaunchKernelGGL((crc_sst4k_nofold_kernel<SstSrc, SstVerifySink, true>), grid, block, 0, s, d_tables, src, n,
@@ -1041,7 +1201,9 @@ hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tab
     case 121:    // exact: the A, B, C chain steps issued one chain at a time (round 2)
     case 122:    // exact: halves always records 0-7 | 8-15 (no bank-spread choice)
     case 123:    // exact: the first row's bank-spread choice taken for the whole batch
-    case 124: {  // exact: 10 waves x 9-KiB regions for every class
+    case 124:    // exact: 10 waves x 9-KiB regions for every class
+    case 125:    // exact: the batch-uniform k only (no per-record lanes for mixed sizes; round 3 before)
+    case 126: {  // the item geometry per record instead of its CRC (MODE 18)
       const uint32_t cls = (flags & PDB_CRC_SIZE_256) ? 256u
                            : (flags & PDB_CRC_SIZE_512) ? 512u : ((flags & PDB_CRC_SIZE_1K) ? 1152u : 1023u);
       if (v == 118) launch_lanespan<DescSrc, OutSink, 10>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
@@ -1049,7 +1211,9 @@ hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tab
       else if (v == 121) launch_lanespan<DescSrc, OutSink, 13>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
       else if (v == 122) launch_lanespan<DescSrc, OutSink, 14>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
       else if (v == 123) launch_lanespan<DescSrc, OutSink, 15>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
-      else launch_lanespan<DescSrc, OutSink, 16>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
+      else if (v == 124) launch_lanespan<DescSrc, OutSink, 16>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
+      else if (v == 125) launch_lanespan<DescSrc, OutSink, 17>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
+      else launch_lanespan<DescSrc, OutSink, 18>(g, d_tables, src, nblk, cls, OutSink{out, 0u}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
       break;
     }
     case 115:    // pricing (wrong CRCs): no p-word replacement selects

@@ -134,3 +134,60 @@ def test_matches_round1_lane_kernels(crc, oracle_lib):
         a = diag.batch_desc(0, d_base, d_blk, flags=hint).cpu().numpy()
         b = diag.batch_desc(v, d_base, d_blk, flags=hint).cpu().numpy()
         assert (a == b).all()
+
+
+@pytest.mark.parametrize("lo,hi,hint", [(1, 257, "256"), (64, 257, "256"), (257, 513, "512m"), (300, 500, "512m"),
+                                        (1, 513, "512m"), (64, 1000, "1023m"), (513, 1024, "1023m"), (1, 1024, "1023m"),
+                                        (300, 500, "512"), (64, 1000, "1023"), (1024, 1153, "1k"), (1, 1153, "1k")])
+def test_mixed_sizes_per_record_lanes(crc, oracle_lib, lo, hi, hint):
+    """Logs of records of random sizes, packed with 7-byte headers (a write-heavy WAL with varied
+    values): with PDB_CRC_SIZE_MIXED ("512m" / "1023m") a batch's records take their own lane counts
+    (ceil(words / part) each, on consecutive lane ranges) -- against the oracle, against the
+    batch-uniform-k kernel (diagnostics variant 125), and through the host batch entry, which sets
+    the hint itself from the lengths."""
+    import oracle
+    from pebblesdb_amd import diag
+
+    rng = np.random.Generator(np.random.PCG64(lo * 7 + hi))
+    n = 20000
+    lens = rng.integers(lo, hi, size=n)
+    lens[rng.random(n) < 0.02] = rng.integers(1, 16, size=1)[0]  # a few tiny fragments among them
+    offs = np.concatenate([[6], 6 + np.cumsum(lens + 7)[:-1]])
+    base = oracle.splitmix_bytes(int(offs[-1] + lens[-1]) + 64, lo + hi)
+    _check(crc, oracle_lib, base, offs, lens, hint)
+    flags = crc._SIZE_HINT[hint]
+    d_base, d_blk = torch.from_numpy(base).cuda(), crc.blocks_to_device(crc.make_blocks(offs, lens))
+    a = diag.batch_desc(0, d_base, d_blk, flags=flags).cpu().numpy()
+    b = diag.batch_desc(125, d_base, d_blk, flags=flags).cpu().numpy()
+    assert (a == b).all()
+    blk = crc.make_blocks(offs, lens)
+    got = crc.batch_host(base, blk, masked=True).view(np.uint32)
+    assert (got == oracle_lib.batch(base, blk, flags=1, nthreads=8)).all()
+
+
+def test_mixed_geometry_items():
+    """The per-record item geometry (diagnostics variant 126: first record, records, lane, lanes per
+    record) on a batch of 300-B records with two block-end fragments: records on consecutive lane
+    ranges of ceil(words / 27) lanes, at most 64 lanes an item."""
+    from pebblesdb_amd import crc32c, diag
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    lens = np.full(64 * 40, 431)
+    rng = np.random.Generator(np.random.PCG64(5))
+    lens[:] = rng.integers(100, 500, size=lens.size)
+    offs = np.concatenate([[6], 6 + np.cumsum(lens + 7)[:-1]])
+    d = torch.zeros(int(offs[-1] + lens[-1]) + 64, dtype=torch.uint8, device="cuda")
+    d_blk = crc32c.blocks_to_device(crc32c.make_blocks(offs, lens))
+    geo = diag.batch_desc(126, d, d_blk, flags=crc32c.SIZE_512 | crc32c.SIZE_MIXED).cpu().numpy().view(np.uint32)
+    k = np.minimum(5, ((lens + 3) // 4 + 26) // 27)
+    for b in range(40):
+        g = geo[64 * b:64 * b + 64]
+        if not (g & 1).all():
+            continue  # this batch kept the uniform k
+        first, cnt, lane, kl = g >> 24, (g >> 16) & 127, (g >> 8) & 255, (g >> 4) & 15
+        assert (kl == k[64 * b:64 * b + 64]).all()
+        for r in range(64):
+            i0 = int(first[r])
+            assert i0 <= r < i0 + int(cnt[r])
+            assert lane[r] == int(k[64 * b + i0:64 * b + r].sum()) and lane[r] + kl[r] <= 64

@@ -22,7 +22,10 @@ WL = {"wal100": (131, 1 << 30, crc32c.SIZE_256), "wal400": (431, 2 << 30, crc32c
       "wal700": (700, 2 << 30, crc32c.SIZE_1023), "wal1000": (1000, 2 << 30, crc32c.SIZE_1023),
       "wal": (1055, 4 << 30, crc32c.SIZE_1K),
       # records of random sizes (uniform in [lo, hi) B incl. the type byte, 7-B headers between)
-      "rand300_500": ((300, 500), 2 << 30, crc32c.SIZE_512), "rand64_1000": ((64, 1000), 2 << 30, crc32c.SIZE_1023),
+      "rand300_500": ((300, 500), 2 << 30, crc32c.SIZE_512 | crc32c.SIZE_MIXED),
+      "rand64_1000": ((64, 1000), 2 << 30, crc32c.SIZE_1023 | crc32c.SIZE_MIXED),
+      "rand32_256": ((32, 256), 1 << 30, crc32c.SIZE_256), "rand1_512": ((1, 512), 2 << 30, crc32c.SIZE_512 | crc32c.SIZE_MIXED),
+      "rand1000_1152": ((1000, 1152), 4 << 30, crc32c.SIZE_1K),
       "wal419": (419, 2 << 30, crc32c.SIZE_512), "wal463": (463, 2 << 30, crc32c.SIZE_512),
       "wal443": (443, 2 << 30, crc32c.SIZE_512)}
 

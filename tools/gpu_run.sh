@@ -49,6 +49,11 @@ for s in "$@"; do
     vtool) step vtool 900 bash tools/verify_tool_bench.sh ${TAG}_vtool 1000000 ;;
     vtool10m) step vtool10m 1000 bash tools/verify_tool_bench.sh ${TAG}_vtool10m 10000000 ;;
     seal_price) step seal_price 600 python tools/seal_price.py ;;
+    lanespan_var) step lanespan_var 600 python -u -m pytest tests/test_lanespan.py -m gpu -x -q --timeout 200 --timeout-method thread ;;
+    ab_var) step ab_var 900 python tools/ab_span.py 0,125 rand300_500,rand64_1000,rand32_256,rand1_512,rand1000_1152,wal100,wal400,wal1000,wal 4 ;;
+    seal_cal) step seal_cal 600 python tools/seal_price.py 0,140,141,142,33 ;;
+    seal_cal2) step seal_cal2 600 python tools/seal_price.py 0,140,141,143,144,145,146,147 ;;
+    seal_cal3) step seal_cal3 600 python tools/seal_price.py 0,140,141,148,149,150,151 ;;
     ab_seal_price) step ab_seal_price 600 python tools/ab_sst.py 0,94,95,96 && step ab_seal_price_rev 600 python tools/ab_sst.py 96,95,94,0 ;;
     ab_seal_orders) step ab_so1 600 python tools/ab_sst.py 0,94,95 && step ab_so2 600 python tools/ab_sst.py 95,94,0 && step ab_so3 600 python tools/ab_sst.py 94,0 ;;
     bench_rows) for w in sst_verify sst_seal sst_crc wal sstable c3; do step bench_$w 300 python bench.py --workload $w --no-copy-inclusive --steps 50 || exit 1; done ;;

@@ -47,7 +47,7 @@ for v in VARIANTS:  # allocate the shadow image up front; in-place variants must
     data[tpos] = 0
     seal(v)
     torch.cuda.synchronize()
-    if not (80 <= v <= 87 or 93 <= v <= 96 or v == 33):
+    if not (80 <= v <= 87 or 93 <= v <= 96 or v == 33 or 140 <= v <= 151):
         assert torch.equal(data, ref), f"variant {v}: sealed image differs"
     data.copy_(ref)
 torch.cuda.synchronize()
