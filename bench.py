@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-copy-inclusive", action="store_true")
     ap.add_argument("--diag", action="store_true", help="also time the read-stream calibration kernels")
+    ap.add_argument("--no-ceiling", action="store_true",
+                    help="skip the hash-free pattern-ceiling kernels timed after the timed region (pattern_ceiling)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--timing", default="region", choices=["per-launch", "region"],
                     help="HIP events around every launch (per-launch kernel times) or one pair around "
@@ -446,6 +448,13 @@ def main():
     if rank == 0:
         if args.diag:
             extra["diag"] = read_ceiling(torch, dev, data, stream)
+        if world == 1 and not args.no_ceiling:
+            ceil = pattern_ceiling(torch, args.workload, data, stream, algo_bytes, nblk,
+                                   d_h=d_h if args.workload.startswith("sst_") else None,
+                                   d_blk=d_blk if args.workload.startswith("wal") else None,
+                                   hint=hint if args.workload.startswith("wal") else None, reseal=step)
+            if ceil:
+                extra["pattern_ceiling"] = ceil
         # the copy-inclusive rate is a one-GPU figure (like the CPU baseline): multi-rank runs skip it,
         # so no rank sits in the process-group teardown while rank 0 copies for seconds
         if not args.no_copy_inclusive and world == 1 and args.workload in ("c2", "sstable"):
@@ -510,6 +519,50 @@ def main():
         print(json.dumps(line), flush=True)
     if distributed:
         dist.destroy_process_group()
+
+
+def pattern_ceiling(torch, workload, data, stream, algo_bytes, nblk, d_h=None, d_blk=None, hint=None, reseal=None):
+    """The measured kernel's memory pattern with NO hash (diagnostics library, after the timed
+    region): the ceiling the kernel's own loads and stores allow on this box, priced against the
+    same algorithmic bytes.  c2: read_pattern4k variant 21 (the 4-KiB path's 1-KiB-contiguous nt
+    loads, 4 blocks per wave between barriers); sst_*: seal_pattern_kernel (variant 140 loads only,
+    141 loads + the 1 M trailer stores -- the in-place seal's pattern; the image is re-sealed after);
+    wal*: the record kernel's loads and LDS staging alone (variant 63).  DESIGN.md §6 / §6.0."""
+    from pebblesdb_amd import crc32c, diag
+
+    runs = []
+    if workload == "c2":
+        o = torch.zeros(1, dtype=torch.int32, device=data.device)
+        runs.append(("read_pattern4k variant 21 (loads only)", lambda: diag.read_pattern4k(data, nblk, 21, o, stream)))
+    elif workload in ("sst_verify", "sst_crc", "sst_seal"):
+        runs.append(("seal_pattern_kernel<0> (variant 140: loads only)",
+                     lambda: diag.sst(140, data, d_h, seal=True, stream=stream)))
+        if workload == "sst_seal":
+            runs.append(("seal_pattern_kernel<1> (variant 141: loads + in-place trailer stores)",
+                         lambda: diag.sst(141, data, d_h, seal=True, stream=stream)))
+    elif workload.startswith("wal"):
+        o = torch.empty(nblk, dtype=torch.int32, device=data.device)
+        flags = crc32c._SIZE_HINT[hint]
+        runs.append(("crc_lanespan_kernel MODE 1 (variant 63: loads + LDS staging, no hash)",
+                     lambda: diag.batch_desc(63, data, d_blk, flags=flags, out=o, stream=stream)))
+    res = {}
+    for name, fn in runs:
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record(stream)
+        for _ in range(10):
+            fn()
+        e.record(stream)
+        torch.cuda.synchronize()
+        ms = s.elapsed_time(e) / 10
+        gbs = algo_bytes / (ms * 1e-3) / 1e9
+        res[name] = {"ms": round(ms, 4), "GB/s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
+    if workload == "sst_seal" and reseal is not None:  # the calibration wrote wrong trailers
+        reseal()
+        torch.cuda.synchronize()
+    return res
 
 
 def read_ceiling(torch, dev, data, stream):

@@ -1236,7 +1236,8 @@ hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tab
     case 64:  // the record kernel's hash alone over stale staging (no loads; results undefined)
     case 67:  // the record kernel's bookkeeping alone (no loads, no hash)
     {
-      const uint32_t cls = (flags & PDB_CRC_SIZE_256) ? 256u : ((flags & PDB_CRC_SIZE_512) ? 512u : 1023u);
+      const uint32_t cls = (flags & PDB_CRC_SIZE_256) ? 256u
+                           : (flags & PDB_CRC_SIZE_512) ? 512u : ((flags & PDB_CRC_SIZE_1K) ? 1152u : 1023u);
       if (v == 63) launch_lanespan<DescSrc, OutSink, 1>(g, d_tables, src, nblk, cls, sink, s);
       else if (v == 64) launch_lanespan<DescSrc, OutSink, 2>(g, d_tables, src, nblk, cls, sink, s);
       else launch_lanespan<DescSrc, OutSink, 3>(g, d_tables, src, nblk, cls, sink, s);
