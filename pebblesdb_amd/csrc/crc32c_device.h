@@ -1630,7 +1630,7 @@ constexpr uint32_t kSlowList = 64u;
 // kDeferF: the body chains stop with their last word unshifted and ONE table step follows the tree
 // (chain16p; false = every chain finished before the folds, round 2 -- A/B).
 template <class Src, class Sink, bool kNT, int kRows, bool kDiagNoFold = false, int kBlk = 4, class LT = QuadTabs,
-          bool kUA = false, bool kDeferF = true>
+          bool kUA = false, bool kDeferF = true, uint32_t kW = kWavesPerWg>
 __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ tabs, Src src, uint64_t nblk,
                                                   Sink sink) {
   static_assert(kRows == 0 || kRows == 1 || kRows == 4, "no body (records <= 256 B), 1-KiB or 4-KiB bodies");
@@ -1647,7 +1647,7 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
     stage_tables<PDB_CAT_TREE16, PDB_CAT_S1024>(lds, tabs);  // slots 0..5 = 16..512, 6 = 1024
   uint32_t* ctr = reinterpret_cast<uint32_t*>(lds + PDB_MAIN_BYTES + 7 * 4096u);
   const uint64_t g_lo = nblk * blockIdx.x / gridDim.x, g_hi = nblk * (blockIdx.x + 1) / gridDim.x;
-  if (threadIdx.x == 0) *ctr = kWavesPerWg;  // next kBlk-block group, in groups relative to g_lo
+  if (threadIdx.x == 0) *ctr = kW;  // next kBlk-block group, in groups relative to g_lo
   const uint32_t u = threadIdx.x & 63u;
   const uint32_t ureg = tabs[PDB_UNSHIFT_OFF + (u & 15u)];
   __syncthreads();
@@ -2056,10 +2056,12 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
 }
 
 // kBlk = 8 (A/B): 8-block groups, prefixes <= 128 B in rows of 8 lanes, one tree8_packed.
-template <class Src, class Sink, bool kNT, int kBlk = 4, class LT = QuadTabs, bool kUA = false, bool kDeferF = true>
-__global__ __launch_bounds__(kThreads) void crc_sst4k_kernel(const uint32_t* __restrict__ tabs, Src src,
-                                                             uint64_t nblk, Sink sink) {
-  sized_kernel_body<Src, Sink, kNT, 4, false, kBlk, LT, kUA, kDeferF>(tabs, src, nblk, sink);
+// kW: waves per workgroup (16 = 1024 threads, 128 VGPRs a lane; A/B diagnostics 12 / 8 waves).
+template <class Src, class Sink, bool kNT, int kBlk = 4, class LT = QuadTabs, bool kUA = false, bool kDeferF = true,
+          uint32_t kW = kWavesPerWg>
+__global__ __launch_bounds__(kW * 64) void crc_sst4k_kernel(const uint32_t* __restrict__ tabs, Src src,
+                                                            uint64_t nblk, Sink sink) {
+  sized_kernel_body<Src, Sink, kNT, 4, false, kBlk, LT, kUA, kDeferF, kW>(tabs, src, nblk, sink);
 }
 
 // (the 1-KiB body has no Horner fold: both images measure the same, +0.8 % for the lane-quarter

@@ -707,6 +707,26 @@ hipError_t launch_sst_variant(int v, const LaunchGeom& g, const uint32_t* d_tabl
                               hipStream_t s) {
   if (v == 0) return launch_sst(g, d_tables, buf, buf_len, h, n, seal, ok, nbad, s);
   const dim3 grid(grid_for(g, n)), block(kThreads);
+  if (v == 127 || v == 128) {  // 12 / 8 waves per workgroup (168 / 256 VGPRs a lane: no spills)
+    const dim3 blk(v == 127 ? 768u : 512u);
+    const SstSrc src{buf, h, buf_len};
+    if (seal) {
+      if (v == 127)
+        hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ParkSealSink<64>, true, 4, QuadTabs, false, true, 12>), grid, blk, 0, s,
+                           d_tables, src, n, ParkSealSink<64>{});
+      else
+        hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ParkSealSink<64>, true, 4, QuadTabs, false, true, 8>), grid, blk, 0, s,
+                           d_tables, src, n, ParkSealSink<64>{});
+    } else {
+      if (v == 127)
+        hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstVerifySink, true, 4, QuadTabs, false, true, 12>), grid, blk, 0, s,
+                           d_tables, src, n, SstVerifySink{ok, nbad});
+      else
+        hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstVerifySink, true, 4, QuadTabs, false, true, 8>), grid, blk, 0, s,
+                           d_tables, src, n, SstVerifySink{ok, nbad});
+    }
+    return hipGetLastError();
+  }
   if (v >= 140 && v <= 151 && seal) {  // seal-pattern calibration (seal_pattern_kernel<v - 140>)
     uint32_t* xo = nbad;  // XOR of everything read (keeps the loads live); may be null
     static uint8_t* cal_shadow = nullptr;  // diagnostics only: 143's shadow image
