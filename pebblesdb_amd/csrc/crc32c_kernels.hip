@@ -208,9 +208,10 @@ hipError_t launch_sst(const LaunchGeom& g, const uint32_t* d_tables, uint8_t* bu
   if (seal)
     hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ParkSealSink<64>, true>), grid, block, 0, s, d_tables, src, n,
                        ParkSealSink<64>{});
-  else
-    hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstVerifySink, true>), grid, block, 0, s, d_tables, src, n,
-                       SstVerifySink{ok, nbad});
+  else  // verify: 12 waves (168 VGPRs a lane: 32 B of spills instead of 124 at 16 waves), +1.2-1.7 % in
+        // A/B both orders (profiles/r03_waves/; diagnostics 127 / 128 / 129 = 12 / 8 / 16 waves)
+    hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstVerifySink, true, 4, QuadTabs, false, true, 12>), grid, dim3(768), 0,
+                       s, d_tables, src, n, SstVerifySink{ok, nbad});
   return hipGetLastError();
 }
 

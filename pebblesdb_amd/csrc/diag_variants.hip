@@ -707,7 +707,13 @@ hipError_t launch_sst_variant(int v, const LaunchGeom& g, const uint32_t* d_tabl
                               hipStream_t s) {
   if (v == 0) return launch_sst(g, d_tables, buf, buf_len, h, n, seal, ok, nbad, s);
   const dim3 grid(grid_for(g, n)), block(kThreads);
-  if (v == 127 || v == 128) {  // 12 / 8 waves per workgroup (168 / 256 VGPRs a lane: no spills)
+  if (v == 129 && !seal) {  // verify with 16 waves (the product until late round 3)
+    const SstSrc src{buf, h, buf_len};
+    hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstVerifySink, true>), grid, block, 0, s, d_tables, src, n,
+                       SstVerifySink{ok, nbad});
+    return hipGetLastError();
+  }
+  if (v == 127 || v == 128) {  // 12 / 8 waves per workgroup (168 / 256 VGPRs a lane; spills 32 / 0 B)
     const dim3 blk(v == 127 ? 768u : 512u);
     const SstSrc src{buf, h, buf_len};
     if (seal) {
