@@ -707,6 +707,17 @@ hipError_t launch_sst_variant(int v, const LaunchGeom& g, const uint32_t* d_tabl
                               hipStream_t s) {
   if (v == 0) return launch_sst(g, d_tables, buf, buf_len, h, n, seal, ok, nbad, s);
   const dim3 grid(grid_for(g, n)), block(kThreads);
+  if ((v == 131 || v == 132) && seal) {  // the compact form (pdb_sst_crc_device): masked CRCs into
+                                         // (uint32_t*) ok -- 131: 16 waves (product), 132: 12 waves
+    const SstSrc src{buf, h, buf_len};
+    uint32_t* co = reinterpret_cast<uint32_t*>(ok);
+    if (v == 131)
+      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstCrcSink, true>), grid, block, 0, s, d_tables, src, n, SstCrcSink{co});
+    else
+      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstCrcSink, true, 4, QuadTabs, false, true, 12>), grid, dim3(768), 0, s,
+                         d_tables, src, n, SstCrcSink{co});
+    return hipGetLastError();
+  }
   if (v == 129 && !seal) {  // verify with 16 waves (the product until late round 3)
     const SstSrc src{buf, h, buf_len};
     hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstVerifySink, true>), grid, block, 0, s, d_tables, src, n,
@@ -990,6 +1001,12 @@ hipError_t launch_fixed_variant(int v, const LaunchGeom& g, const uint32_t* d_ta
                                 uint32_t* out, hipStream_t s) {
   if (v == 0) return launch_fixed(g, d_tables, base, stride, len, nblk, flags, init, out, s);
   const dim3 grid(grid_for(g, nblk)), block(kThreads);
+  if (v == 130 && len - 4096u <= 256u && !(flags & PDB_CRC_USE_INIT)) {  // sstable-sized, 12 waves
+    const FixedSrc src{base, stride, len, 0xFFFFFFFFu};
+    hipLaunchKernelGGL((crc_sst4k_kernel<FixedSrc, OutSink, true, 4, QuadTabs, false, true, 12>), grid, dim3(768), 0, s,
+                       d_tables, src, nblk, OutSink{out, flags});
+    return hipGetLastError();
+  }
   const bool fast = len == 4096u && (reinterpret_cast<uintptr_t>(base) & 15u) == 0 &&
                     (stride & 15u) == 0;
   if (!fast) {
