@@ -127,7 +127,9 @@ hipError_t launch_fixed(const LaunchGeom& g, const uint32_t* d_tables, const uin
     if (len - kSstMin <= kSstMax - kSstMin) {
       // sstable-sized blocks (4096..4352 B, any alignment): exact 4-KiB body + batched prefix
       // (profiles/r01_ab_sst4k.json)
-      hipLaunchKernelGGL((crc_sst4k_kernel<FixedSrc, OutSink, true>), grid, block, 0, s, d_tables, src, nblk, sink);
+      // (12 waves: fewer spills, +1.3 % in A/B, profiles/r03_waves/ab_waves2.log; diagnostics 130)
+      hipLaunchKernelGGL((crc_sst4k_kernel<FixedSrc, OutSink, true, 4, QuadTabs, false, true, 12>), grid, dim3(768), 0, s,
+                         d_tables, src, nblk, sink);
       return hipGetLastError();
     }
     if (len - 1u <= 1151u) {  // records of 1..1152 B, staged through LDS, k lanes each (crc32c_lanespan.h)
@@ -221,8 +223,9 @@ hipError_t launch_sst_masked(const LaunchGeom& g, const uint32_t* d_tables, uint
   // the seal's masked CRCs into a compact array (pdb_sst_crc_device; the host seal brings back 4 B
   // per block across PCIe, not the span)
   const SstSrc src{buf, h, buf_len};
-  hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstCrcSink, true>), dim3(grid_for(g, n)), dim3(kThreads), 0, s,
-                     d_tables, src, n, SstCrcSink{out});
+  // (12 waves: fewer spills, +0.7 % in A/B, profiles/r03_waves/ab_waves2.log; diagnostics 131 / 132)
+  hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstCrcSink, true, 4, QuadTabs, false, true, 12>), dim3(grid_for(g, n)),
+                     dim3(768), 0, s, d_tables, src, n, SstCrcSink{out});
   return hipGetLastError();
 }
 

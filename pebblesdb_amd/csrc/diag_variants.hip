@@ -708,7 +708,7 @@ hipError_t launch_sst_variant(int v, const LaunchGeom& g, const uint32_t* d_tabl
   if (v == 0) return launch_sst(g, d_tables, buf, buf_len, h, n, seal, ok, nbad, s);
   const dim3 grid(grid_for(g, n)), block(kThreads);
   if ((v == 131 || v == 132) && seal) {  // the compact form (pdb_sst_crc_device): masked CRCs into
-                                         // (uint32_t*) ok -- 131: 16 waves (product), 132: 12 waves
+                                         // (uint32_t*) ok -- 131: 16 waves, 132: 12 waves (the product)
     const SstSrc src{buf, h, buf_len};
     uint32_t* co = reinterpret_cast<uint32_t*>(ok);
     if (v == 131)

@@ -3,7 +3,8 @@
 sstable layout (4096 B + type at stride 4101; diagnostics batch_fixed 0 vs 130) and the compact
 trailer words (pdb_sst_crc_device; pdb_diag_sst 131 = 16 waves vs 132 = 12 waves) on bench.py's
 images.  Interleaved, both orders, 6 rounds of 20 launches after 100 warm ones; results checked
-equal.  Prints one JSON object (GB/s of algorithmic bytes)."""
+equal.  Prints one JSON object (GB/s of algorithmic bytes).  (Run before the product switched to 12
+waves: "fixed16" is batch_fixed variant 0 only in that run; since then variant 0 is the 12-wave kernel.)"""
 import json
 import os
 import sys
