@@ -74,10 +74,13 @@ def test_flag_constants_match_the_python_mirror():
     """Every PDB_CRC_* flag in the header has the same value in pebblesdb_amd.crc32c."""
     src = open(HEADER).read()
     flags = {k: int(v, 16) for k, v in re.findall(r"#define PDB_CRC_(\w+) (0x[0-9a-fA-F]+)u", src)}
-    assert {"MASK_OUTPUT", "USE_INIT", "SIZE_1K", "SIZE_4K", "SIZE_256", "SIZE_512", "SIZE_1023"} <= set(flags)
+    assert {"MASK_OUTPUT", "USE_INIT", "SIZE_1K", "SIZE_4K", "SIZE_256", "SIZE_512", "SIZE_1023", "SIZE_MIXED"} <= set(flags)
     for k, v in flags.items():
         assert getattr(crc32c, k) == v, k
     assert len(set(flags.values())) == len(flags)  # distinct bits
+    # the mixed-size hint only exists with the two classes that take per-record lane counts
+    assert crc32c._SIZE_HINT["512m"] == flags["SIZE_512"] | flags["SIZE_MIXED"]
+    assert crc32c._SIZE_HINT["1023m"] == flags["SIZE_1023"] | flags["SIZE_MIXED"]
 
 
 def test_library_is_gfx950_code(lib):
