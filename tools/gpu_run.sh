@@ -47,6 +47,7 @@ for s in "$@"; do
     prof_list) for w in ${PROF_WL:-c2}; do step prof_$w 700 bash tools/profile.sh ${TAG}_prof_$w $w || exit 1; done ;;
     ab_seal) step ab_seal 600 python tools/ab_sst.py 0,37,39 ;;
     ab_waves2) step ab_waves2 600 python tools/ab_waves.py ;;
+    ab_hints) step ab_hints 600 python tools/ab_hints.py ;;
     ab_waves) step ab_waves 600 python tools/ab_sst.py 0,127,128 && step ab_waves_rev 600 python tools/ab_sst.py 128,127,0 ;;
     vtool) step vtool 900 bash tools/verify_tool_bench.sh ${TAG}_vtool 1000000 ;;
     vtool10m) step vtool10m 1000 bash tools/verify_tool_bench.sh ${TAG}_vtool10m 10000000 ;;
