@@ -456,6 +456,35 @@ static bool mixed_lengths(const pdb_blk* blk, uint64_t nblk, uint32_t cls) {
   return nb && 4 * win >= nb;
 }
 
+// Records of <= 256 B: the 256 class hashes 33-word parts (k = 1..2 lanes a record, 9 steps an
+// item, 10 waves x 9-KiB regions), the 512 class 27-word parts (k = 1..5, 8 steps, 12 waves x 8 KiB).
+// Records of 133..216 B need two parts in either and the 512 class then runs faster (+17 % on random
+// 1-200-B records, tools/ab_hints.py); up to 132 B the 256 class takes one lane a record (wal100),
+// past 216 B the 512 class needs three.  A per-batch item count of both decides.
+static bool small_records_prefer_512(const pdb_blk* blk, uint64_t nblk) {
+  double c256 = 0, c512 = 0;
+  for (uint64_t b = 0; b < nblk; b += 64) {
+    uint32_t nw = 0, n = 0;
+    uint64_t lo = UINT64_MAX, hi = 0;
+    for (uint64_t i = b; i < nblk && i < b + 64; ++i) {
+      const uint32_t len = blk[i].len;
+      if (len - 1u > 255u) continue;
+      nw = std::max(nw, (len + 3u) / 4u);
+      lo = std::min(lo, blk[i].off);
+      hi = std::max(hi, blk[i].off + len);
+      ++n;
+    }
+    if (!n) continue;
+    const uint64_t span = hi - lo;
+    const uint32_t k256 = nw <= 33u ? 1u : 2u, k512 = (nw + 26u) / 27u;
+    const uint64_t i256 = std::max<uint64_t>((n + 64u / k256 - 1u) / (64u / k256), (span + 9199u) / 9200u);
+    const uint64_t i512 = std::max<uint64_t>((n + 64u / k512 - 1u) / (64u / k512), (span + 8175u) / 8176u);
+    c256 += static_cast<double>(i256) * (9 + 4) / 10.0;  // items x (steps + 4) / waves
+    c512 += static_cast<double>(i512) * (8 + 4) / 12.0;
+  }
+  return c512 < 0.95 * c256;
+}
+
 struct HostGroup {
   uint64_t first, count, lo, hi;
 };
@@ -523,7 +552,7 @@ int host_desc(const uint8_t* base, uint64_t base_len, const pdb_blk* blk, uint64
   if (!(flags & (PDB_CRC_USE_INIT | PDB_CRC_SIZE_1K | PDB_CRC_SIZE_4K | PDB_CRC_SIZE_256 | PDB_CRC_SIZE_512 | PDB_CRC_SIZE_1023))) {
     if (4 * n1k >= 3 * nblk) flags |= PDB_CRC_SIZE_1K;
     else if (4 * n4k >= 3 * nblk) flags |= PDB_CRC_SIZE_4K;
-    else if (4 * n256 >= 3 * nblk) flags |= PDB_CRC_SIZE_256;
+    else if (4 * n256 >= 3 * nblk) flags |= small_records_prefer_512(blk, nblk) ? PDB_CRC_SIZE_512 : PDB_CRC_SIZE_256;
     else if (4 * (n256 + n512) >= 3 * nblk) flags |= PDB_CRC_SIZE_512;  // the 17-group window takes 1..512 B
     else if (4 * (n256 + n512 + n1023) >= 3 * nblk) flags |= PDB_CRC_SIZE_1023;  // 33 groups: 1..1024 B
     if ((flags & (PDB_CRC_SIZE_512 | PDB_CRC_SIZE_1023)) && mixed_lengths(blk, nblk, (flags & PDB_CRC_SIZE_512) ? 512u : 1023u))

@@ -136,7 +136,8 @@ def test_matches_round1_lane_kernels(crc, oracle_lib):
         assert (a == b).all()
 
 
-@pytest.mark.parametrize("lo,hi,hint", [(1, 257, "256"), (64, 257, "256"), (257, 513, "512m"), (300, 500, "512m"),
+@pytest.mark.parametrize("lo,hi,hint", [(1, 257, "256"), (64, 257, "256"), (1, 200, "256"), (120, 216, "512"),
+                                        (257, 513, "512m"), (300, 500, "512m"),
                                         (1, 513, "512m"), (64, 1000, "1023m"), (513, 1024, "1023m"), (1, 1024, "1023m"),
                                         (300, 500, "512"), (64, 1000, "1023"), (1024, 1153, "1k"), (1, 1153, "1k")])
 def test_mixed_sizes_per_record_lanes(crc, oracle_lib, lo, hi, hint):
@@ -144,7 +145,8 @@ def test_mixed_sizes_per_record_lanes(crc, oracle_lib, lo, hi, hint):
     values): with PDB_CRC_SIZE_MIXED ("512m" / "1023m") a batch's records take their own lane counts
     (ceil(words / part) each, on consecutive lane ranges) -- against the oracle, against the
     batch-uniform-k kernel (diagnostics variant 125), and through the host batch entry, which sets
-    the hint itself from the lengths."""
+    the hint itself from the lengths (varied records of 133..216 B: the 512 class, which hashes them
+    on two 27-word parts in fewer steps than the 256 class's two 33-word ones)."""
     import oracle
     from pebblesdb_amd import diag
 
