@@ -550,7 +550,7 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void cr
     it.batch = bcur;
     it.k = bvar ? bkmax : bg.k;
     it.iters = bvar ? biters_v : bg.iters;
-    it.var = bvar;
+    it.var = kVar && bvar;
     if (rem == 0) {  // every record of the batch was outside the class: an empty item
       bcursor = 64;
       return it;
@@ -667,8 +667,11 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void cr
     const int32_t pl = static_cast<int32_t>(it.p_loc);
     const bool act = it.p_loc != kNoRec;
     // part, parts of the record after it (kVar: packed per lane; else from the uniform k)
-    const uint32_t pc = kVar ? it.cw & 15u : it.cw, pafter = kVar ? (it.cw >> 4) & 15u : k - 1u - pc;
-    const bool head = pafter == 0u;
+    const uint32_t pc = kVar ? it.cw & 15u : it.cw;
+    // the record's parts after this one: >= m (kVar: packed per lane; else from the uniform k, the
+    // exact round-3 form of the uniform kernels)
+    auto more = [&](uint32_t m) -> bool { return kVar ? ((it.cw >> 4) & 15u) >= m : pc + m < k; };
+    const bool head = kVar ? ((it.cw >> 4) & 15u) == 0u : pc == k - 1u;
     const uint32_t sel = static_cast<uint32_t>(e & 3) * 0x01010101u + 0x03020100u;
     const uint32_t zp = static_cast<uint32_t>(pl - e) & 3u;  // bytes of the p-word before p
     const uint32_t uz = __shfl(ureg, zp, 64);
@@ -801,24 +804,24 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void cr
     // a row of 16, so the partner's value comes by DPP row_shl (no LDS round trip); other k by
     // bpermute.
     if (MODE != 8 && k > 1u) {
-      const bool dpp = MODE != 11 && !kOldFold && (k & (k - 1u)) == 0 && !it.var;
+      const bool dpp = MODE != 11 && !kOldFold && (k & (k - 1u)) == 0 && !(kVar && it.var);
       uint32_t y = dpp ? static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(P), 0x101, 0xF, 0xF, false))
                        : __shfl_down(P, 1, 64);
-      if ((pc & 1u) == 0 && pafter >= 1u) P = opx(kOpP1, y, P);
+      if ((pc & 1u) == 0 && more(1u)) P = opx(kOpP1, y, P);
       if (k > 2u) {
         y = dpp ? static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(P), 0x102, 0xF, 0xF, false))
                 : __shfl_down(P, 2, 64);
-        if ((pc & 3u) == 0 && pafter >= 2u) P = opx(kOpP2, y, P);
+        if ((pc & 3u) == 0 && more(2u)) P = opx(kOpP2, y, P);
       }
       if (k > 4u) {
         y = dpp ? static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(P), 0x104, 0xF, 0xF, false))
                 : __shfl_down(P, 4, 64);
-        if ((pc & 7u) == 0 && pafter >= 4u) P = opx(kOpP4, y, P);
+        if ((pc & 7u) == 0 && more(4u)) P = opx(kOpP4, y, P);
       }
     }
     if constexpr (!kOldFold) P = TP::step(lds, lt, P, 0u);  // F: the chains' last words
     if constexpr (MODE == 18)  // diagnostics: the item's first record, records, lane, lanes, mode
-      P = ~(((it.cw >> 16) << 24) | (((it.cw >> 8) & 127u) << 16) | (u << 8) | ((pc + pafter + 1u) << 4) | (it.var ? 1u : 0u));
+      P = ~(((it.cw >> 16) << 24) | (((it.cw >> 8) & 127u) << 16) | (u << 8) | ((kVar ? pc + ((it.cw >> 4) & 15u) + 1u : k) << 4) | (it.var ? 1u : 0u));
     if (pc == 0 && act)
       SinkOps<Sink>::put(sink, (it.batch << 6) + it.r, P, BlkDesc{nullptr, 0u, 0xFFFFFFFFu}, it.pre);
   };
