@@ -27,6 +27,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 GIB = float(1 << 30)
+C2_BLOCKS = 1 << 20        # BASELINE config 2: 1 M x 4 KiB on one GPU
+C4_BLOCKS_PER_GPU = 4194304  # BASELINE config 4: 128 GiB of 4 KiB blocks over 8 GPUs = 16 GiB per GPU
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 METRIC = "GiB/s CRC32C over batched 4 KiB sstable blocks (device-resident); % HBM peak"
 
@@ -45,7 +47,9 @@ def parse():
                     help="c2 (default, the headline) / c3: BASELINE configs; sstable: the C2 blocks in "
                          "sstable layout; sst_verify / sst_seal: SURVEY §8(f) rows 1-2 on a device sstable "
                          "image of ~4.17-KiB blocks; wal: row 3, the log record CRC over 32-KiB log blocks")
-    ap.add_argument("--nblk", type=int, default=1 << 20, help="blocks per GPU (c2/sstable)")
+    ap.add_argument("--nblk", type=int, default=None,
+                    help="blocks per GPU (c2/sstable); default 1M (C2) on one GPU and, for c2 with --gpus N > 1, "
+                         "BASELINE config 4's 4 194 304 (16 GiB per GPU: 128 GiB over 8 GPUs)")
     ap.add_argument("--c3-bytes", type=int, default=16 << 30, help="bytes per GPU for c3 (Zipf)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-copy-inclusive", action="store_true")
@@ -59,6 +63,9 @@ def parse():
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend (nccl = RCCL over xGMI; gloo only to rehearse the "
                          "multi-rank flow with ranks sharing one GPU)")
+    ap.add_argument("--process-group", action="store_true",
+                    help="create the process group and run every collective even at world size 1 (the RCCL "
+                         "branch on one GPU: tests/test_shard.py)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / rank plumbing only, on the CPU (gloo): no device, no kernel, value null "
                          "(tests/test_shard.py)")
@@ -107,6 +114,19 @@ def launch_ranks(args) -> None:
     sys.exit(subprocess.call(cmd, env=env))
 
 
+def resolve_nblk(args, world: int) -> bool:
+    """--nblk's default: C2's 1 M blocks on one GPU; with N > 1 ranks and the c2 workload, config 4's
+    4 194 304 blocks per rank, so N = 8 hashes exactly BASELINE config 4's 128 GiB (weak scaling:
+    N = 2 / 4 keep the same 16 GiB per GPU).  Returns True when the C4 shard size was chosen."""
+    if args.nblk is not None:
+        return False
+    if world > 1 and args.workload == "c2":
+        args.nblk = C4_BLOCKS_PER_GPU
+        return True
+    args.nblk = C2_BLOCKS
+    return False
+
+
 def dry_run_main(args, world: int, rank: int) -> None:
     """The multi-rank plumbing of main() with no device: gloo process group, rank 0's index
     scatter, barrier-bracketed (empty) timed region with max-over-ranks time, per-rank row
@@ -118,7 +138,8 @@ def dry_run_main(args, world: int, rank: int) -> None:
     from pebblesdb_amd.shard import scatter_block_ranges
 
     cpu = torch.device("cpu")
-    distributed = world > 1
+    c4 = resolve_nblk(args, world)
+    distributed = world > 1 or args.process_group
     if distributed:
         dist.init_process_group("gloo")
     lo, hi = scatter_block_ranges(args.nblk * world, world, rank, cpu, dist if distributed else None)
@@ -134,7 +155,8 @@ def dry_run_main(args, world: int, rank: int) -> None:
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": None, "unit": "GiB/s", "n_gpus": world, "world_size": world,
                           "steps": args.steps, "warmup": args.warmup, "dry_run": True,
-                          "config": {"workload": "dry run (launcher plumbing only, no device)",
+                          "config": {"workload": "dry run (launcher plumbing only, no device)" +
+                                                 (" of the c4 shards" if c4 else ""),
                                      "blocks_per_gpu": args.nblk},
                           "ranks": [{"rank": r[0], "blocks": r[3] // 4096} for r in rows],
                           "region_s_max": float(t.item())}), flush=True)
@@ -193,7 +215,7 @@ def gather_rank_rows(row, world: int, cdev, dist=None) -> list:
     import torch
 
     mine = torch.tensor([int(x) for x in row], dtype=torch.int64, device=cdev)
-    if dist is None or world == 1:
+    if dist is None:
         return [[int(x) for x in mine.cpu().tolist()]]
     allr = [torch.zeros_like(mine) for _ in range(world)]
     dist.all_gather(allr, mine)
@@ -209,6 +231,7 @@ def main():
     if args.dry_run:
         dry_run_main(args, world, rank)
         return
+    c4 = resolve_nblk(args, world)
     import torch
     import torch.distributed as dist
 
@@ -225,7 +248,7 @@ def main():
         sys.exit(2)
     gpu = local % ndev if args.backend == "gloo" else local  # gloo rehearsal may share a GPU
     torch.cuda.set_device(gpu)
-    distributed = world > 1
+    distributed = world > 1 or args.process_group
     if distributed:
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
@@ -259,7 +282,9 @@ def main():
         def step():
             crc32c.batch_fixed(data, stride, L, nblk, out=out)
 
-        workload = {"workload": "c2: 1M x 4 KiB blocks per GPU, stride 4096, device-resident",
+        workload = {"workload": (f"c4: {world} x 4M x 4 KiB blocks = {world * 16} GiB ({world} x 16 GiB shards; "
+                                 "BASELINE config 4 at 8 GPUs), stride 4096, device-resident" if c4 else
+                                 "c2: 1M x 4 KiB blocks per GPU, stride 4096, device-resident"),
                     "block_bytes": L, "blocks_per_gpu": nblk, "bytes_per_gpu": hashed}
     elif args.workload == "sstable":
         # sstable layout: contents 4096 B + type byte under the CRC, trailer 5 B -> stride 4101
@@ -484,8 +509,10 @@ def main():
             "dtype": "u8",
             "data": "synthetic (splitmix64 seed 301, generated on device)",
             "config": dict(workload, parallelism=f"block-range shards x{world}",
-                           collectives="index broadcast + checksum all-gather (" +
-                                       ("RCCL" if args.backend == "nccl" else "gloo") + "), none on the data path"),
+                           collectives=("index scatter + checksum all-gather + region-time MAX all-reduce (" +
+                                        ("RCCL" if args.backend == "nccl" else "gloo") + "), none on the data path")
+                           if distributed else "none (one rank, no process group)"),
+            "process_group": (args.backend if distributed else None),
             "hbm_frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
             "roofline": {
                 "bound": "hbm",

@@ -198,7 +198,8 @@ inline bool ReadTableLayout(const char* image, uint64_t len, TableLayout* t, std
 // The data-block handles of a table image: footer -> index block entries, nothing else read and
 // no checksum checked -- the blocks leveldb-verify's verified iterator reads (Table::Open reads the
 // index with default ReadOptions, i.e. unchecked, table.cc:97-101, and with default Options never
-// reads the metaindex or filter, table.cc:130-133).  False + *err on a structural problem.
+// reads the metaindex or filter, table.cc:130-133).  False + *err on a structural problem,
+// including a data handle that does not fit the image.
 inline bool ReadDataHandles(const char* image, uint64_t len, std::vector<BlockHandle>* data, std::string* err) {
   if (len < kFooterEncodedLength) return *err = "file is too short to be an sstable", false;
   const char* f = image + len - kFooterEncodedLength;
@@ -216,7 +217,15 @@ inline bool ReadDataHandles(const char* image, uint64_t len, std::vector<BlockHa
     return *err = "truncated block read", false;
   if (image[index.offset + index.size] != 0) return *err = "compressed index block", false;
   data->clear();
-  return BlockValues(image + index.offset, index.size, data, err);
+  if (!BlockValues(image + index.offset, index.size, data, err)) return false;
+  // A damaged index entry can decode to a handle past the end of the file.  ReadBlock reports such
+  // a block as "truncated block read" when the iterator reaches it (format.cc:84-87); one handle
+  // out of range must not fail the whole GPU batch (pdb_sst_verify_host's PDB_ERANGE), so the
+  // caller gets false and lets the engine's own reads report it.
+  for (const BlockHandle& h : *data)
+    if (h.offset > len || h.size > len - h.offset || len - h.offset - h.size < kBlockTrailerSize)
+      return *err = "truncated block read", false;
+  return true;
 }
 
 // leveldb-verify for one table image: every block's checksum in one GPU batch.  Returns the

@@ -71,6 +71,11 @@ struct DevState {
   uint8_t* d_stage = nullptr;  // device alias of h_stage
   size_t stage_cap = 0;
   uint32_t seq = 0;          // scalar-call sentinel sequence
+  // kScalarPoll returns when the result word lands, before its kernel has ended (and the next call
+  // may take another context's stream): an event after every such launch, waited on before the
+  // stage is freed or regrown
+  hipEvent_t stage_done = nullptr;
+  bool stage_pending = false;
   // Scalar calls <= kServerCap: kScalarServer (default) posts them to the persistent server
   // kernel (crc32c_server.hip); PDB_SCALAR_WAIT=poll launches one kernel per call and spins on
   // the result, =sync waits on the stream (A/B diagnostics, tools/scalar_latency.py).
@@ -216,7 +221,12 @@ constexpr size_t kStageHdr = 256;  // result words ahead of the staged bytes (ke
 
 int ensure_stage(DevState* st, size_t bytes) {
   if (bytes <= st->stage_cap) return PDB_OK;
-  if (st->h_stage) {  // (st->mu held: every user of the stage has synchronised its stream)
+  if (st->h_stage) {  // (st->mu held: every user of the stage has synchronised its stream, or --
+                      // a poll-mode call that returned early -- recorded stage_done after its kernel)
+    if (st->stage_pending) {
+      (void)hipEventSynchronize(st->stage_done);
+      st->stage_pending = false;
+    }
     (void)hipHostFree(st->h_stage);
     st->h_stage = st->d_stage = nullptr;
     st->stage_cap = 0;
@@ -341,7 +351,15 @@ int server_alloc(DevState* st) {
   }
   if (!st->srv_in_h && (rc = alloc_pinned(kServerInBytes, &st->srv_in_h, &st->srv_in_d))) return rc;
   if ((rc = alloc_pinned(kServerOutBytes, &st->srv_out_h, &st->srv_out_d))) return rc;
-  if ((e = hipStreamCreateWithFlags(&st->srv_stream, hipStreamNonBlocking)) != hipSuccess)
+  // The server's stream gets the greatest priority: the runtime keeps a separate hardware-queue
+  // pool per priority, so no host-context stream (normal priority; 8 of them over
+  // GPU_MAX_HW_QUEUES = 4 queues) shares the server's queue.  On a shared queue a host batch's
+  // kernel would sit behind the persistent server for up to its 200-ms lifetime (ADVICE r03;
+  // tests/test_scalar_server.py::test_scalar_callers_beside_batch_seals times every batch).
+  int prio_least = 0, prio_greatest = 0;
+  if ((e = hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest)) != hipSuccess)
+    return hip_fail(e, "hipDeviceGetStreamPriorityRange");
+  if ((e = hipStreamCreateWithPriority(&st->srv_stream, hipStreamNonBlocking, prio_greatest)) != hipSuccess)
     return hip_fail(e, "hipStreamCreate(server)");
   static std::once_flag once;
   std::call_once(once, [] { atexit(park_all_at_exit); });
@@ -659,6 +677,10 @@ int host_scalar(uint32_t init, const uint8_t* data, uint64_t n, uint32_t* out) {
                      PDB_CRC_USE_INIT, init, d_res, s);
     if (e != hipSuccess) return hip_fail(e, "launch_fixed(scalar)");
     if (st->scalar_mode == kScalarPoll) {
+      if (!st->stage_done && (e = hipEventCreateWithFlags(&st->stage_done, hipEventDisableTiming)) != hipSuccess)
+        return hip_fail(e, "hipEventCreate(stage)");
+      if ((e = hipEventRecord(st->stage_done, s)) != hipSuccess) return hip_fail(e, "hipEventRecord(stage)");
+      st->stage_pending = true;
       for (uint32_t spin = 0; spin < (1u << 22); ++spin) {
         const uint32_t v = *h_res;
         if (v != sentinel) {

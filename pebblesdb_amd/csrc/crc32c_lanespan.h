@@ -39,6 +39,8 @@
 namespace pdb {
 namespace {
 
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
 constexpr uint32_t kSpanStageBase = 64u << 10;                    // tables and operators below
 // staging geometry per class: waves per CU and 1-KiB chunks per region (10 x 9 KiB for <= 256-B
 // records: 64 records of a 100-B-value log fit a region; 12 x 8 KiB for the longer classes, whose
@@ -339,7 +341,8 @@ struct SpanItem {
 // at a time (round 2), 14 no bank-spread choice of the halves (records 0-7 | 8-15 always), 15 the
 // first row's choice for the whole batch, 16 10 waves x 9-KiB regions for every class, 17 the
 // batch-uniform k only (no per-record lanes for mixed sizes), 18 the item geometry instead of the CRC
-// (first record << 24 | records << 16 | lane << 8 | lanes << 4 | per-record mode; diagnostics).
+// (first record << 24 | records << 16 | lane << 8 | lanes << 4 | per-record mode; diagnostics), 19 the
+// round-3 staging reads (one ds_read_b32 per word instead of aligned b64 pairs).
 // TP: the table scheme.
 // kDyn: the workgroup owns batches [g nbat / G, (g + 1) nbat / G) and its waves take the next one
 // from an LDS counter (false: batch wave_id + k W, the round-2 static assignment -- diagnostics).
@@ -700,7 +703,7 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void cr
     // step t = dwords t, t + 1); below the region for short records (words never used)
     const char* q3 = (MODE == 5 || MODE == 6) ? region + 4u * (u & 31u)
                                               : region + 4 * ((eA - static_cast<int32_t>(4u * NI + 12u * LC)) >> 2);
-    uint32_t xd = 0, ld;
+    uint32_t xd = 0, ld = 0;
     if (lim > 0) {  // the head chain alone (junk on the other lanes, dropped)
       const int32_t tD = T + static_cast<int32_t>(3u * LC + lim) - FD;  // the p-word's step in it
       const char* q = q3 + 4 * (FD - static_cast<int32_t>(lim));
@@ -712,25 +715,87 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void cr
         xd = t == tD ? pw : TP::step(lds, lt, xd, w);
       }
       xd = head ? xd : 0u;
-    } else {
+    } else if constexpr (MODE == 19 || MODE == 5 || MODE == 6) {  // (kPairs: read below)
       ld = lds_u32(q3, 4u * FD);
     }
     uint32_t xa = 0, xb = 0, xc = 0;
-    uint32_t la = lds_u32(q3, 12u * LC + 4u * FABC), lb = lds_u32(q3, 8u * LC + 4u * FABC);
-    uint32_t lc = lds_u32(q3, 4u * LC + 4u * FABC);
+    // The chains' words.  kPairs (the product since round 4): every chain's dwords come as 8-B
+    // aligned ds_read_b64 pairs from q3e (q3 rounded down to 8 B; par = q3's dword parity), one pair
+    // every two steps, and dword i of a chain is pair dword i + par (one v_cndmask).  An aligned
+    // b64 read costs the LDS ~2.5 cycles against ~2.2 for a b32 (tools/lds_probe.hip,
+    // profiles/r04_lds_probe.log: a 4-B aligned b64 / b128 costs ~27-29), so the staging reads
+    // take ~40 % of the LDS cycles of one b32 per word.  MODE 19: one ds_read_b32 per word (round 3).
+    constexpr bool kPairs = MODE != 19 && MODE != 5 && MODE != 6;
+    const int32_t qd = (eA - static_cast<int32_t>(4u * NI + 12u * LC)) >> 2;  // q3's dword (region-relative)
+    const bool par = (qd & 1) != 0;
+    // chain X's pairs: pair j = dwords 2 j, 2 j + 1 above qb[X] (8-B aligned; chains A, B, C, D at
+    // 3 LC, 2 LC, LC, 0 words above q3).  Each chain keeps the last two pairs read (P newest, Q);
+    // the base offsets are made opaque so the compiler keeps one ds_read_b64 per pair: merged into
+    // a ds_read2_b64 (two 8-B accesses, 8 LDS cycles) they would cost more than the dword reads.
+    uint32_t qb[4];
+    u32x2 Pp[4], Qp[4];
+#pragma unroll
+    for (uint32_t X = 0; X < 4; ++X) {
+      qb[X] = static_cast<uint32_t>(region - lds) + static_cast<uint32_t>(8 * (qd >> 1)) + 32u * (3u - X);
+      if constexpr (kPairs) asm volatile("" : "+v"(qb[X]));
+      Pp[X] = u32x2{0u, 0u}, Qp[X] = u32x2{0u, 0u};
+    }
+    auto pair_in = [&](uint32_t X, uint32_t j) {
+      Qp[X] = Pp[X];
+      Pp[X] = *reinterpret_cast<const u32x2*>(lds + qb[X] + 8u * j);
+    };
+    uint32_t la = 0, lb = 0, lc = 0;
+    if constexpr (kPairs) {
+      // dword F (+ par) of each chain: F even: pair F / 2; F odd: pairs (F - 1) / 2 and (F + 1) / 2
+      uint32_t d0[4];
+#pragma unroll
+      for (uint32_t X = 0; X < 4; ++X) {
+        const uint32_t F = X == 3 ? static_cast<uint32_t>(FD) : static_cast<uint32_t>(FABC);
+        if ((F & 1u) == 0) {
+          pair_in(X, F >> 1);
+          d0[X] = par ? Pp[X].y : Pp[X].x;
+        } else {
+          pair_in(X, F >> 1);
+          pair_in(X, (F + 1u) >> 1);
+          d0[X] = par ? Pp[X].x : Qp[X].y;
+        }
+      }
+      la = d0[0], lb = d0[1], lc = d0[2], ld = d0[3];
+    } else {
+      la = lds_u32(q3, 12u * LC + 4u * FABC), lb = lds_u32(q3, 8u * LC + 4u * FABC);
+      lc = lds_u32(q3, 4u * LC + 4u * FABC);
+    }
+    // dword t + 1 (+ par) of chain X at step t: even t reads pair t / 2 + 1 first
+    auto next_dw = [&](uint32_t X, int32_t t) -> uint32_t {
+      if ((t & 1) == 0) {
+        pair_in(X, static_cast<uint32_t>(t + 2) >> 1);
+        return par ? Pp[X].x : Qp[X].y;
+      }
+      return par ? Pp[X].y : Pp[X].x;
+    };
 #pragma unroll
     for (int32_t t = 0; t < static_cast<int32_t>(NI); ++t) {
       const bool abc = t >= FABC, dd = t >= FD;  // compile time
       uint32_t wa = 0, wb = 0, wc = 0, wd = 0;
       if (abc) {
-        const uint32_t ha = lds_u32(q3, 12u * LC + 4u * (t + 1)), hb = lds_u32(q3, 8u * LC + 4u * (t + 1));
-        const uint32_t hc = lds_u32(q3, 4u * LC + 4u * (t + 1));
+        uint32_t ha, hb, hc;
+        if constexpr (kPairs) {
+          ha = next_dw(0, t), hb = next_dw(1, t), hc = next_dw(2, t);
+        } else {
+          ha = lds_u32(q3, 12u * LC + 4u * (t + 1)), hb = lds_u32(q3, 8u * LC + 4u * (t + 1));
+          hc = lds_u32(q3, 4u * LC + 4u * (t + 1));
+        }
         wa = __builtin_amdgcn_perm(ha, la, sel), wb = __builtin_amdgcn_perm(hb, lb, sel);
         wc = __builtin_amdgcn_perm(hc, lc, sel);
         la = ha, lb = hb, lc = hc;
       }
       if (dd) {
-        const uint32_t hd = lds_u32(q3, 4u * (t + 1));
+        uint32_t hd;
+        if constexpr (kPairs) {
+          hd = next_dw(3, t);
+        } else {
+          hd = lds_u32(q3, 4u * (t + 1));
+        }
         wd = __builtin_amdgcn_perm(hd, ld, sel);
         ld = hd;
       }

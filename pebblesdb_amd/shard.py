@@ -36,15 +36,22 @@ def byte_balanced_ranges(lens, world: int) -> list[tuple[int, int]]:
 def scatter_block_ranges(n_total: int, world: int, rank: int, device, dist=None,
                          lens=None) -> tuple[int, int]:
     """Rank 0 computes every rank's [lo, hi) (by count, or by bytes when `lens` is given) and
-    broadcasts the small index over the process group -- the only collective on this path
-    (RCCL over xGMI on GPUs, gloo in the CPU tests).  Returns this rank's range."""
+    scatters them over the process group: each rank receives its own 16-B range -- the only
+    collective on this path (RCCL over xGMI on GPUs, gloo in the CPU tests).  With `dist` given the
+    scatter runs at any world size, 1 included (bench.py --process-group exercises the RCCL branch on
+    one GPU).  Returns this rank's range."""
     import torch
 
-    idx = torch.zeros(world, 2, dtype=torch.int64, device=device)
+    mine = torch.zeros(2, dtype=torch.int64, device=device)
+    parts = None
     if rank == 0:
         rngs = (byte_balanced_ranges(lens, world) if lens is not None
                 else [block_range(n_total, world, r) for r in range(world)])
-        idx.copy_(torch.tensor(rngs, dtype=torch.int64))
-    if dist is not None and world > 1:
-        dist.broadcast(idx, src=0)
-    return int(idx[rank, 0]), int(idx[rank, 1])
+        parts = [torch.tensor(r, dtype=torch.int64, device=device) for r in rngs]
+    if dist is not None:
+        dist.scatter(mine, scatter_list=parts, src=0)
+    else:
+        if world != 1:
+            raise ValueError("scatter_block_ranges: world > 1 needs a process group")
+        mine.copy_(parts[0])
+    return int(mine[0]), int(mine[1])

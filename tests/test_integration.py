@@ -155,6 +155,7 @@ def test_leveldb_verify_batched_matches_reference_tool(gpu, tmp_path):
         if rc == 0:
             assert o == "" and e == "", f
     damaged = 0
+    index_cases = []
     for f in tables:
         img = open(f, "rb").read()
         try:
@@ -176,10 +177,27 @@ def test_leveldb_verify_batched_matches_reference_tool(gpu, tmp_path):
                 assert rc == 0 and "block checksum mismatch" in e, (name, e[-500:])
             else:
                 assert rc == 0 and o == "" and e == "", (name, o, e)
+        # a damaged index ENTRY: the last data handle's offset varint maxed out at its
+        # encoded length, so the handle points past the end of the file.  The batch must not fail
+        # as a whole (device error, exit 1): the reference reports the block as the iterator
+        # reaches it ("truncated block read"), and so must the batched tool.
+        idx = lay.footer.index
+        contents = img[idx.offset: idx.offset + idx.size]
+        enc = data[-1].encode()
+        at = contents.rfind(enc)
+        olen = len(T.encode_varint64(data[-1].offset))
+        if at >= 0 and (1 << (7 * olen)) - 1 > len(img):
+            patched = bytearray(img)
+            patched[idx.offset + at: idx.offset + at + olen] = bytes([0xFF] * (olen - 1) + [0x7F])
+            with open(q, "wb") as fh:
+                fh.write(bytes(patched))
+            rc, o, e = same(q, "index_handle_past_eof")
+            assert rc == 0 and "truncated block read" in e, e[-500:]
+            index_cases.append(f)
         damaged += 1
         if damaged == 3:
             break
-    assert damaged > 0
+    assert damaged > 0 and index_cases, (damaged, index_cases)
     for f in logs:
         img = open(f, "rb").read()
         if len(img) < 1000:

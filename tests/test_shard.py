@@ -156,6 +156,42 @@ def test_bench_gpus2_without_launcher_runs_two_ranks():
     assert [x["blocks"] for x in line["ranks"]] == [1000, 1000]
 
 
+def test_bench_gpus2_default_is_c4_shards():
+    """Without --nblk, `--gpus N > 1` runs BASELINE config 4's shard size: 4 194 304 x 4 KiB = 16 GiB
+    per rank (128 GiB at N = 8); one GPU stays C2 (1 M blocks).  --dry-run: no device."""
+    import json
+    import subprocess
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                            "MASTER_PORT", "LOCAL_WORLD_SIZE")}
+    for gpus, blocks, c4 in ((2, 4194304, True), (1, 1 << 20, False)):
+        cmd, root = _bench_cmd("--gpus", str(gpus), "--steps", "2", "--warmup", "1", "--dry-run")
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=root, env=env)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith('{"metric"')][-1])
+        assert [x["blocks"] for x in line["ranks"]] == [blocks] * gpus
+        assert line["config"]["blocks_per_gpu"] == blocks
+        assert ("c4" in line["config"]["workload"]) == c4
+
+
+def test_bench_process_group_world1_dry_run():
+    """--process-group at world size 1: the index scatter, the rows all_gather and the MAX
+    all_reduce all run through a (gloo) process group of one rank."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
+           "--gpus", "1", "--steps", "2", "--dry-run", "--process-group", "--nblk", "777"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=root, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith('{"metric"')][-1])
+    assert line["world_size"] == 1 and [x["blocks"] for x in line["ranks"]] == [777]
+
+
 @pytest.mark.parametrize("gpus,world", [(1, "2"), (8, "4")])
 def test_bench_gpus_world_size_mismatch_fails(gpus, world):
     import subprocess
@@ -219,3 +255,37 @@ def test_bench_main_two_ranks_on_the_gpu(oracle_lib, workload):
             blk["len"] = s
             exp ^= int(np.bitwise_xor.reduce(oracle_lib.batch(data, blk, nthreads=4)))
     assert int(line["xor_of_crcs"], 16) == exp
+
+
+@pytest.mark.gpu
+def test_bench_rccl_branch_world1_on_the_gpu(oracle_lib):
+    """The RCCL branch of bench.py, which only the driver's 8-GPU run takes otherwise: torchrun with
+    one rank and --process-group, so `init_process_group("nccl", device_id=...)`, the index scatter
+    (shard.scatter_block_ranges), the per-rank rows all_gather and the MAX all_reduce of the region
+    time all run on device tensors over RCCL -- exactly the calls an N-rank run makes.  The JSON line's
+    XOR of all CRCs must equal the oracle's."""
+    import json
+    import subprocess
+    import sys
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    nblk = 8192
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
+           "--gpus", "1", "--steps", "3", "--warmup", "1", "--settle", "0", "--backend", "nccl",
+           "--process-group", "--nblk", str(nblk), "--no-cpu-baseline", "--no-copy-inclusive", "--no-ceiling"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=root, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith('{"metric"')][-1])
+    assert line["world_size"] == 1 and line["process_group"] == "nccl"
+    assert [x["bytes"] for x in line["ranks"]] == [nblk * 4096]
+    import oracle
+
+    data = oracle.splitmix_bytes(nblk * 4096, 301)
+    blk = np.zeros(nblk, dtype=oracle.BLK_DTYPE)
+    blk["off"] = np.arange(nblk) * 4096
+    blk["len"] = 4096
+    assert int(line["xor_of_crcs"], 16) == int(np.bitwise_xor.reduce(oracle_lib.batch(data, blk, nthreads=4)))
