@@ -42,7 +42,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=40)
     ap.add_argument("--settle", type=int, default=300,
                     help="untimed launches after the timed region before the steady-state re-timing (0: skip)")
-    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "sstable", "sst_verify", "sst_seal", "sst_crc",
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "sstable", "sst_verify", "sst_seal", "sst_seal2", "sst_crc",
                                                         "wal", "wal100", "wal400", "wal1000"],
                     help="c2 (default, the headline) / c3: BASELINE configs; sstable: the C2 blocks in "
                          "sstable layout; sst_verify / sst_seal: SURVEY §8(f) rows 1-2 on a device sstable "
@@ -301,7 +301,7 @@ def main():
 
         workload = {"workload": "sstable layout: 4096 B contents + type byte, stride 4101 (unaligned)",
                     "block_bytes": L, "blocks_per_gpu": nblk, "bytes_per_gpu": hashed}
-    elif args.workload in ("sst_verify", "sst_seal", "sst_crc"):
+    elif args.workload in ("sst_verify", "sst_seal", "sst_seal2", "sst_crc"):
         # sstable image: contents of 4166..4174 B (db_bench data blocks flush just past the 4-KiB
         # block_size: 4171-4175 B with the type byte), type 0, 5-B trailer
         from pebblesdb_amd import table as T
@@ -334,12 +334,20 @@ def main():
 
             def step():
                 check(lib().pdb_sst_crc_device(data.data_ptr(), total, d_h.data_ptr(), nblk, out.data_ptr(), sp))
+        elif args.workload == "sst_seal2":  # the two-launch seal: compact words, then the trailer scatter
+            scratch = torch.empty(nblk, dtype=torch.int32, device=dev)
+
+            def step():
+                check(lib().pdb_sst_seal_device_scratch(data.data_ptr(), total, d_h.data_ptr(), nblk,
+                                                        scratch.data_ptr(), nblk, sp))
         else:
             def step():
                 check(lib().pdb_sst_seal_device(data.data_ptr(), total, d_h.data_ptr(), nblk, sp))
 
         workload = {"workload": f"{args.workload}: sstable image in HBM, 1M blocks of 4166-4174 B + type + "
-                                "5-B trailer, pdb_sst_" + args.workload.split("_")[1] + "_device",
+                                "5-B trailer, " + {"sst_verify": "pdb_sst_verify_device", "sst_seal": "pdb_sst_seal_device",
+                                                   "sst_seal2": "pdb_sst_seal_device_scratch (two launches)",
+                                                   "sst_crc": "pdb_sst_crc_device"}[args.workload],
                     "blocks_per_gpu": nblk, "bytes_per_gpu": hashed}
     elif args.workload in ("wal", "wal100", "wal400", "wal1000"):
         # log file image: 32-KiB log blocks of physical records [crc 4][len 2][type 1][payload]
@@ -395,7 +403,7 @@ def main():
     algo_bytes = hashed + 4 * nblk + (16 * nblk if args.workload in ("c3", "wal", "wal100", "wal400", "wal1000") else 0)
     if args.workload == "sst_verify":  # + the 4-B stored trailer read, 16-B handle, 1-B ok written
         algo_bytes = hashed + nblk * (4 + 16 + 1)
-    elif args.workload in ("sst_seal", "sst_crc"):  # + 4-B trailer / CRC written, 16-B handle
+    elif args.workload in ("sst_seal", "sst_seal2", "sst_crc"):  # + 4-B trailer / CRC written, 16-B handle
         algo_bytes = hashed + nblk * (4 + 16)
 
     # ---- warmup + timed region -------------------------------------------------------------
@@ -476,7 +484,7 @@ def main():
         if world == 1 and not args.no_ceiling:
             ceil = pattern_ceiling(torch, args.workload, data, stream, algo_bytes, nblk,
                                    d_h=d_h if args.workload.startswith("sst_") else None,
-                                   d_blk=d_blk if args.workload.startswith("wal") else None,
+                                   d_blk=d_blk if args.workload.startswith("wal") or args.workload == "c3" else None,
                                    hint=hint if args.workload.startswith("wal") else None, reseal=step)
             if ceil:
                 extra["pattern_ceiling"] = ceil
@@ -531,6 +539,8 @@ def main():
                            "wal1000": "crc_lanespan_kernel<DescSrc,OutSink,1023>",
                            "sst_verify": "crc_sst4k_kernel<SstSrc,SstVerifySink,nt,QuadTabs>",
                            "sst_seal": "crc_sst4k_kernel<SstSrc,ParkSealSink<64>,nt,QuadTabs>",
+                           "sst_seal2": "crc_sst4k_kernel<SstSrc,SstCrcSink,nt,QuadTabs,12 waves> + sst_trailer_scatter_kernel "
+                                        "(two launches per step)",
                            "sst_crc": "crc_sst4k_kernel<SstSrc,SstCrcSink,nt,QuadTabs>"}[args.workload],
                 "algorithmic_bytes_per_launch": algo_bytes,
                 "kernel_avg_ms": round(kern_avg_ms, 4),
@@ -561,10 +571,26 @@ def pattern_ceiling(torch, workload, data, stream, algo_bytes, nblk, d_h=None, d
     if workload == "c2":
         o = torch.zeros(1, dtype=torch.int32, device=data.device)
         runs.append(("read_pattern4k variant 21 (loads only)", lambda: diag.read_pattern4k(data, nblk, 21, o, stream)))
-    elif workload in ("sst_verify", "sst_crc", "sst_seal"):
+    elif workload == "c3":
+        o = torch.empty(nblk, dtype=torch.int32, device=data.device)
+        runs.append(("crc_stream16_kernel kLoadsOnly (variant 161: the C3 routing's loads, scheduling and "
+                     "byte-balanced ranges, no hash)", lambda: diag.batch_desc(161, data, d_blk, flags=0, out=o,
+                                                                             stream=stream)))
+    elif workload == "sstable":
+        # the stride-4101 blocks as sstable handles (offset i * 4101, 4096 B contents + type + trailer):
+        # seal_pattern_kernel<0> reads each block's 4101 B with the sst kernel's 1-KiB-contiguous nt
+        # loads in 4-block groups (the 4 trailer bytes past the 4097 hashed: +0.1 % of the bytes)
+        from pebblesdb_amd import table as T
+
+        hs = np.zeros(nblk, dtype=crc32c.HANDLE_DTYPE)
+        hs["offset"], hs["size"] = np.arange(nblk, dtype=np.int64) * 4101, 4096
+        d_hs = T.handles_to_device(hs, data.device)
+        runs.append(("seal_pattern_kernel<0> (variant 140: loads only) over the stride-4101 blocks",
+                     lambda: diag.sst(140, data, d_hs, seal=True, stream=stream)))
+    elif workload in ("sst_verify", "sst_crc", "sst_seal", "sst_seal2"):
         runs.append(("seal_pattern_kernel<0> (variant 140: loads only)",
                      lambda: diag.sst(140, data, d_h, seal=True, stream=stream)))
-        if workload == "sst_seal":
+        if workload in ("sst_seal", "sst_seal2"):
             runs.append(("seal_pattern_kernel<1> (variant 141: loads + in-place trailer stores)",
                          lambda: diag.sst(141, data, d_h, seal=True, stream=stream)))
     elif workload.startswith("wal"):
@@ -586,7 +612,7 @@ def pattern_ceiling(torch, workload, data, stream, algo_bytes, nblk, d_h=None, d
         ms = s.elapsed_time(e) / 10
         gbs = algo_bytes / (ms * 1e-3) / 1e9
         res[name] = {"ms": round(ms, 4), "GB/s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
-    if workload == "sst_seal" and reseal is not None:  # the calibration wrote wrong trailers
+    if workload in ("sst_seal", "sst_seal2") and reseal is not None:  # the calibration wrote wrong trailers
         reseal()
         torch.cuda.synchronize()
     return res

@@ -92,7 +92,37 @@ struct DevState {
   uint64_t srv_stop = 0;         // ctl->stop value the live instance runs under (srv_mu)
   bool srv_live = false;         // an instance of srv_epoch may still be in its loop (atomic)
   ScalarSlot slots[kServerSlots];
+  // PDB_SERVER_STAMPS=<path> (diagnostics, tools/scalar_phases.py): every scalar call records its host
+  // clock at entry, after posting and on seeing the answer, and the server's poll / hash-done ticks;
+  // the rows are written to <path> at exit
+  bool stamps = false;
 };
+
+struct PhaseStamp {
+  uint64_t n, h0, h1, h2, g_seen, g_done;  // bytes; host CLOCK_MONOTONIC ns; s_memrealtime ticks
+};
+std::mutex g_stamp_mu;
+std::vector<PhaseStamp> g_stamps;
+
+uint64_t mono_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return static_cast<uint64_t>(ts.tv_sec) * 1000000000ull + static_cast<uint64_t>(ts.tv_nsec);
+}
+
+void write_stamps_at_exit() {
+  const char* path = getenv("PDB_SERVER_STAMPS");
+  if (!path) return;
+  std::lock_guard<std::mutex> lk(g_stamp_mu);
+  FILE* f = fopen(path, "w");
+  if (!f) return;
+  fprintf(f, "n,h0_ns,h1_ns,h2_ns,g_seen_tick,g_done_tick\n");
+  for (const PhaseStamp& p : g_stamps)
+    fprintf(f, "%llu,%llu,%llu,%llu,%llu,%llu\n", (unsigned long long)p.n, (unsigned long long)p.h0,
+            (unsigned long long)p.h1, (unsigned long long)p.h2, (unsigned long long)p.g_seen,
+            (unsigned long long)p.g_done);
+  fclose(f);
+}
 
 enum ScalarMode : int { kScalarServer = 0, kScalarPoll = 1, kScalarSync = 2 };
 // Server lifetime (s_memrealtime ticks, 100 MHz): it leaves after 20 ms without a request or
@@ -156,6 +186,11 @@ int get_state(DevState** out) {
                           : strcmp(wait, "sync") == 0 ? kScalarSync
                           : strcmp(wait, "poll") == 0 ? kScalarPoll : kScalarServer;
   s->hgeom.grid = s->geom.grid > 1 ? s->geom.grid - 1 : 1;
+  s->stamps = getenv("PDB_SERVER_STAMPS") != nullptr;
+  if (s->stamps) {
+    static std::once_flag once;
+    std::call_once(once, [] { atexit(write_stamps_at_exit); });
+  }
   for (HostCtx& c : s->ctx) {
     e = hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking);
     if (e != hipSuccess) return hip_fail(e, "hipStreamCreate");
@@ -381,7 +416,7 @@ int server_ensure(DevState* st, bool relaunch_seen, uint32_t seen) {
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
   const uint32_t next = epoch + 1;
   e = launch_server(st->d_tables, st->srv_in_d, st->srv_out_d, next, st->srv_stop, kServerIdleTicks, kServerLifeTicks,
-                    st->srv_stream);
+                    st->stamps ? 1u : 0u, st->srv_stream);
   if (e != hipSuccess) return hip_fail(e, "launch_server");
   __atomic_store_n(&st->srv_epoch, next, __ATOMIC_RELEASE);
   __atomic_store_n(&st->srv_live, true, __ATOMIC_RELEASE);
@@ -406,15 +441,23 @@ int server_call(DevState* st, uint32_t init, const uint8_t* data, uint64_t n, ui
   std::lock_guard<std::mutex> lk(sl.mu);
   if (!__atomic_load_n(&st->srv_live, __ATOMIC_ACQUIRE) || server_exited(st, live_epoch(st)))
     if ((rc = server_ensure(st, false, 0))) return rc;
+  const uint64_t h0 = st->stamps ? mono_ns() : 0;
   memcpy(srv_data(st, slot) + ((0u - static_cast<uint32_t>(n)) & 15u), data, n);
   const uint32_t seq = sl.seq = (sl.seq + 1) & kServerSeqMask;
   post_word(srv_req(st, slot), (static_cast<uint64_t>((seq << 17) | static_cast<uint32_t>(n)) << 32) | init);
+  const uint64_t h1 = st->stamps ? mono_ns() : 0;
   const uint64_t* resp = srv_resp(st, slot);
   double t0 = 0;
   for (uint32_t spin = 1;; ++spin) {
     const uint64_t r = __atomic_load_n(resp, __ATOMIC_ACQUIRE);
     if (static_cast<uint32_t>(r >> 32) == seq) {
       *out = static_cast<uint32_t>(r);
+      if (st->stamps) {
+        const uint64_t h2 = mono_ns();
+        const PhaseStamp ps{n, h0, h1, h2, __atomic_load_n(resp + 1, __ATOMIC_ACQUIRE), __atomic_load_n(resp + 2, __ATOMIC_ACQUIRE)};
+        std::lock_guard<std::mutex> lk2(g_stamp_mu);
+        g_stamps.push_back(ps);
+      }
       return PDB_OK;
     }
     const uint32_t ep = live_epoch(st);
@@ -964,6 +1007,21 @@ int pdb_sst_seal_device(void* d_buf, uint64_t buf_len, const pdb_block_handle* d
   hipError_t e = launch_sst(st->geom, st->d_tables, static_cast<uint8_t*>(d_buf), buf_len, d_h, n, true,
                             nullptr, nullptr, pick_stream(st, stream));
   return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_sst(seal)");
+}
+
+int pdb_sst_seal_device_scratch(void* d_buf, uint64_t buf_len, const pdb_block_handle* d_h, uint64_t n,
+                                uint32_t* d_scratch, uint64_t scratch_words, void* stream) {
+  if (n == 0) return PDB_OK;
+  if (!d_buf || !d_h || !d_scratch) return fail(PDB_EINVAL, "null argument");
+  if (scratch_words < n) return fail(PDB_EINVAL, "scratch smaller than one word per block");
+  if (buf_len < 5) return fail(PDB_ERANGE, "buffer smaller than one block trailer");
+  DevState* st;
+  int rc = get_state(&st);
+  if (rc) return rc;
+  if ((rc = quiesce(st))) return rc;
+  hipError_t e = launch_sst_seal2(st->geom, st->d_tables, static_cast<uint8_t*>(d_buf), buf_len, d_h, n, d_scratch,
+                                  pick_stream(st, stream));
+  return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_sst_seal2");
 }
 
 int pdb_sst_verify_device(const void* d_buf, uint64_t buf_len, const pdb_block_handle* d_h,

@@ -1159,8 +1159,11 @@ __device__ __forceinline__ uint32_t chain16p(const char* lds, const LT& lt, uint
 // kDeferF: every chain stops with its last word unshifted (chain16p); the lane accumulator is
 // finished by ONE table step where a round hands it on (before shift 1008) and after the final
 // tree, instead of one step per chain (false: round 2 -- A/B).
+// kLoadsOnly (diagnostics: the C3 row's pattern ceiling, bench.py): the same scheduling, descriptor
+// lookahead and load instructions with NO hash -- every loaded word XOR-ed into the lane's
+// accumulator, lane 0's written per block (wrong CRCs by design).
 template <class Src, class Sink, bool kDyn, bool kNT, bool kPack = false, class LT = QuadTabs, bool kBal = false,
-          bool kDeferF = true>
+          bool kDeferF = true, bool kLoadsOnly = false>
 __global__ __launch_bounds__(kThreads) void crc_stream16_kernel(const uint32_t* __restrict__ tabs,
                                                                  Src src, uint64_t nblk, Sink sink) {
   constexpr bool kQuad = __is_same(LT, QuadTabs);
@@ -1316,6 +1319,12 @@ __global__ __launch_bounds__(kThreads) void crc_stream16_kernel(const uint32_t* 
     const uint32_t ck = mcur.k;
     const uint32_t K = cd.n >> 4;
     const bool last_round = ck + 1 >= rounds16(K);
+    if constexpr (kLoadsOnly) {
+      const u32x4 x = (e0 ^ e1) ^ (e2 ^ e3) ^ e4;
+      acc ^= xor3(xor3(x.x, x.y, x.z), x.w, xor3(cx, chw, chb));
+      if (last_round && u == 0) sink.put(mcur.i, acc, cd);
+      continue;
+    }
 
     if (ck == 0) {  // head: every lane hashes the same (broadcast) head bytes from the seed
       const uint32_t t = cd.n & 15u, lead = t & 3u, nh = t >> 2;

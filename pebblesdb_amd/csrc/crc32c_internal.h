@@ -40,6 +40,10 @@ hipError_t launch_sst(const LaunchGeom& g, const uint32_t* d_tables, uint8_t* bu
 // out[i] = Mask(crc32c(contents_i || type_i)) -- the trailer word a seal writes, as an array.
 hipError_t launch_sst_masked(const LaunchGeom& g, const uint32_t* d_tables, uint8_t* buf, uint64_t buf_len,
                              const pdb_block_handle* h, uint64_t n, uint32_t* out, hipStream_t s);
+// The two-launch in-place seal: launch_sst_masked into `scratch` (n words), then one scatter of
+// the trailer words into the image (pdb_sst_seal_device_scratch).
+hipError_t launch_sst_seal2(const LaunchGeom& g, const uint32_t* d_tables, uint8_t* buf, uint64_t buf_len,
+                            const pdb_block_handle* h, uint64_t n, uint32_t* scratch, hipStream_t s);
 // Long span: raw CRCs of `nseg` segments of 2^seg_log2 bytes (+ the tail) in parallel, then a
 // one-workgroup tree combine with the power-of-two operators.  `scratch` holds
 // span_scratch_words(n) u32.  *out = Extend(init, data[0..n)).
@@ -88,7 +92,9 @@ static_assert(sizeof(ServerCtl) == 256 && sizeof(ServerExit) == 256, "mailbox re
 constexpr size_t kExitOff = kServerSlots * 64;
 constexpr size_t kServerOutBytes = kExitOff + sizeof(ServerExit);
 // stop0: the ctl->stop value this instance runs under (it leaves when the word changes)
+// stamps != 0 (diagnostics, PDB_SERVER_STAMPS): each answer's response line also carries the poll
+// and hash-done ticks (s_memrealtime) in its words 1 and 2.
 hipError_t launch_server(const uint32_t* d_tables, uint8_t* d_in, uint8_t* d_out, uint32_t epoch, uint64_t stop0,
-                         uint64_t idle_ticks, uint64_t life_ticks, hipStream_t s);
+                         uint64_t idle_ticks, uint64_t life_ticks, uint32_t stamps, hipStream_t s);
 
 }  // namespace pdb

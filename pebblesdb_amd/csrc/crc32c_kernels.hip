@@ -229,4 +229,34 @@ hipError_t launch_sst_masked(const LaunchGeom& g, const uint32_t* d_tables, uint
   return hipGetLastError();
 }
 
+// The two-launch seal's second launch: trailer word i (launch 1's compact array) to
+// buf[offset_i + size_i + 1 ..+4), one lane per block, after every block has been read (stream
+// order).  A handle whose block + trailer leaves the image is skipped, as the one-launch seal skips
+// it.  The 4 bytes are unaligned: byte stores, merged in L2 before the line is written.
+__global__ __launch_bounds__(256) void sst_trailer_scatter_kernel(uint8_t* __restrict__ buf, uint64_t len,
+                                                                  const pdb_block_handle* __restrict__ h,
+                                                                  const uint32_t* __restrict__ words, uint64_t n) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t off = h[i].offset, size = h[i].size;
+  if (len < 5 || off > len - 5 || size > len - 5 - off) return;
+  uint8_t* tr = buf + off + size + 1;
+  const uint32_t m = words[i];
+  tr[0] = static_cast<uint8_t>(m);
+  tr[1] = static_cast<uint8_t>(m >> 8);
+  tr[2] = static_cast<uint8_t>(m >> 16);
+  tr[3] = static_cast<uint8_t>(m >> 24);
+}
+
+hipError_t launch_sst_seal2(const LaunchGeom& g, const uint32_t* d_tables, uint8_t* buf, uint64_t buf_len,
+                            const pdb_block_handle* h, uint64_t n, uint32_t* scratch, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipError_t e = launch_sst_masked(g, d_tables, buf, buf_len, h, n, scratch, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(sst_trailer_scatter_kernel, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256), 0, s, buf,
+                     buf_len, h, scratch, n);
+  return hipGetLastError();
+}
+
+
 }  // namespace pdb

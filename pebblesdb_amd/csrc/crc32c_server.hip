@@ -113,7 +113,7 @@ __device__ __forceinline__ uint32_t server_hash(const char* lds, const LaneTabs&
 __global__ __launch_bounds__(64 * kServerWaves) void crc_server_kernel(const uint32_t* __restrict__ tabs,
                                                                         uint8_t* in, uint8_t* out, uint32_t epoch,
                                                                         uint64_t stop0, uint64_t idle_ticks,
-                                                                        uint64_t life_ticks) {
+                                                                        uint64_t life_ticks, uint32_t stamps) {
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
   char* lds = reinterpret_cast<char*>(lds_words);
   // operator slot 5 stays free (tree level 5 = shift 256 twice) and holds the workgroup's state
@@ -170,6 +170,15 @@ __global__ __launch_bounds__(64 * kServerWaves) void crc_server_kernel(const uin
         const uint32_t data_off = static_cast<uint32_t>(kSlotDataOff + s_srv * kSlotStride) + ((0u - n) & 15u);
         crc = ~server_hash(lds, lt, u, rin, data_off, n, ~init);
       }
+      // phase stamps (PDB_SERVER_STAMPS, diagnostics: tools/scalar_phases.py): the tick at which the
+      // poll that found the request returned and the tick after the hash, in the response line's
+      // words 1 and 2, written before the response word (the host reads them once it sees it)
+      if (stamps && u == 0) {
+        uint64_t* line = reinterpret_cast<uint64_t*>(out + 64u * s_srv);
+        sys_store64(line + 1, now);
+        sys_store64(line + 2, __builtin_amdgcn_s_memrealtime());
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      }
       if (u == 0) sys_store64(reinterpret_cast<uint64_t*>(out + 64u * s_srv), (static_cast<uint64_t>(sq) << 32) | crc);
       if (u == l) served = sq;
       t_last = now;
@@ -211,9 +220,9 @@ __global__ __launch_bounds__(64 * kServerWaves) void crc_server_kernel(const uin
 }  // namespace
 
 hipError_t launch_server(const uint32_t* d_tables, uint8_t* d_in, uint8_t* d_out, uint32_t epoch, uint64_t stop0,
-                         uint64_t idle_ticks, uint64_t life_ticks, hipStream_t s) {
+                         uint64_t idle_ticks, uint64_t life_ticks, uint32_t stamps, hipStream_t s) {
   hipLaunchKernelGGL(crc_server_kernel, dim3(1), dim3(64 * kServerWaves), 0, s, d_tables, d_in, d_out, epoch, stop0,
-                     idle_ticks, life_ticks);
+                     idle_ticks, life_ticks, stamps);
   return hipGetLastError();
 }
 

@@ -1149,6 +1149,11 @@ hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tab
       hipLaunchKernelGGL((crc_stream16_kernel<DescSrc, OutSink, true, true, true, QuadTabs, true>), grid, block, 0, s,
                          d_tables, src, nblk, sink);
       break;
+    case 161:  // the C3 routing's loads, scheduling and byte-balanced ranges with NO hash (its pattern
+               // ceiling, bench.py pattern_ceiling; wrong CRCs by design)
+      hipLaunchKernelGGL((crc_stream16_kernel<DescSrc, OutSink, true, true, true, QuadTabs, true, true, true>), grid, block,
+                         0, s, d_tables, src, nblk, sink);
+      break;
     case 49:  // the C3 routing with every chain finished before the folds (round 2)
       hipLaunchKernelGGL((crc_stream16_kernel<DescSrc, OutSink, true, true, true, QuadTabs, true, false>), grid, block, 0,
                          s, d_tables, src, nblk, sink);
