@@ -68,8 +68,10 @@ struct SpanStage {
   static constexpr uint32_t kNI = kLD > kLC ? kLD : kLC;            // lock-step steps of a part
   static constexpr uint32_t kOpSet = kLD == 9u ? 0u : 3u;           // its part operators in the table source
 };
-// operator slots: 5..7 shift by 1, 2 and 4 parts of the kernel's class
-constexpr uint32_t kOp16 = 0, kOp32 = 1, kOp64 = 2, kOp256 = 3, kOp1024 = 4, kOpP1 = 5, kOpP2 = 6, kOpP4 = 7;
+// operator slots: 5..7 shift by 1, 2 and 4 parts of the kernel's class; slot 0 shift 16 -- or, with
+// the pre-shifted cross-lane fold (kPre), shift by 3 parts (the slow path's shift 16 is then four
+// table steps: it is rare, and the fold runs once per item)
+constexpr uint32_t kOp16 = 0, kOpP3 = 0, kOp32 = 1, kOp64 = 2, kOp256 = 3, kOp1024 = 4, kOpP1 = 5, kOpP2 = 6, kOpP4 = 7;
 
 // shift(c, D) ^ y for the operator in slot `slot` (byte j of c indexes sub-table j)
 __device__ __forceinline__ uint32_t span_op_x(const char* lds, uint32_t slot, uint32_t c, uint32_t y) {
@@ -82,10 +84,15 @@ __device__ __forceinline__ uint32_t span_op_x(const char* lds, uint32_t slot, ui
   return xor3(xor3(v[0], v[1], v[2]), v[3], y);
 }
 
-// shift(c, 16 << k) ^ y for k = 0..5 (16, 32, 64, 64 x 2, 256, 256 x 2)
-__device__ __forceinline__ uint32_t span_shift_x(const char* lds, uint32_t k, uint32_t c, uint32_t y) {
+// shift(c, 16 << k) ^ y for k = 0..5 (16, 32, 64, 64 x 2, 256, 256 x 2); kPre: slot 0 holds the
+// 3-part operator, so shift 16 is four table steps
+template <class TP, bool kPre>
+__device__ __forceinline__ uint32_t span_shift_x(const char* lds, const typename TP::LT& lt, uint32_t k, uint32_t c,
+                                                 uint32_t y) {
   switch (k) {
-    case 0: return span_op_x(lds, kOp16, c, y);
+    case 0:
+      if constexpr (kPre) return TP::step(lds, lt, TP::step(lds, lt, TP::step(lds, lt, TP::step(lds, lt, c, 0u), 0u), 0u), y);
+      else return span_op_x(lds, kOp16, c, y);
     case 1: return span_op_x(lds, kOp32, c, y);
     case 2: return span_op_x(lds, kOp64, c, y);
     case 3: return span_op_x(lds, kOp64, span_op_x(lds, kOp64, c, 0u), y);
@@ -159,15 +166,16 @@ struct TabsS4 {
   }
 };
 
-template <uint32_t kOpSet>
+template <uint32_t kOpSet, bool kPre = false>
 __device__ __forceinline__ void stage_ops_span(char* lds, const uint32_t* __restrict__ tabs) {
   // slot s, sub-table j, entry b at b<<8 | 128 | (((b >> 2) ^ (4s + j)) & 31) << 2; sources: catalog
   // entries 0 (16), 1 (32), 2 (64), 4 (256), 6 (1024), then the class's part operators (132, 264,
-  // 528 or 108, 216, 432)
+  // 528 or 108, 216, 432); kPre: slot 0 = the class's 3-part operator (396 or 324)
   for (uint32_t i = threadIdx.x; i < 8u * 1024u; i += blockDim.x) {
     const uint32_t slot = i >> 10, j = (i >> 8) & 3u, b = i & 255u;
-    const uint32_t src = slot < 5u ? 1024u + (slot < 3u ? slot : (slot == 3u ? 4u : 6u)) * 1024u
-                                   : PDB_SPANOP_OFF + (slot - 5u + kOpSet) * 1024u;
+    const uint32_t src = (kPre && slot == 0u) ? PDB_SPANOP_OFF + (kOpSet == 0u ? 6u : 7u) * 1024u
+                         : slot < 5u ? 1024u + (slot < 3u ? slot : (slot == 3u ? 4u : 6u)) * 1024u
+                                     : PDB_SPANOP_OFF + (slot - 5u + kOpSet) * 1024u;
     *reinterpret_cast<uint32_t*>(lds + ((b << 8) | 128u | ((((b >> 2) ^ (4u * slot + j)) & 31u) << 2))) = tabs[src + j * 256u + b];
   }
 }
@@ -186,7 +194,7 @@ __device__ __forceinline__ uint32_t span_chain16(const char* lds, const typename
   return TP::step(lds, lt, x, 0u);
 }
 
-template <class TP>
+template <class TP, bool kPre = false>
 __device__ __forceinline__ uint32_t span_slow_record(const char* lds, const typename TP::LT& lt, uint32_t u, uint32_t ureg,
                                                      uintptr_t p, uint32_t n) {
   if (n == 0) return 0xFFFFFFFFu;
@@ -221,17 +229,17 @@ __device__ __forceinline__ uint32_t span_slow_record(const char* lds, const type
   // tree over 64 lanes, 16 B apart: shift 16 << k between partners at distance 2^k
   uint32_t y;
   y = __builtin_amdgcn_update_dpp(0u, acc, 0x101, 0xF, 0xF, false);  // row_shl:1
-  if ((u & 1u) == 0) acc = span_shift_x(lds, 0, acc, y);
+  if ((u & 1u) == 0) acc = span_shift_x<TP, kPre>(lds, lt, 0, acc, y);
   y = __builtin_amdgcn_update_dpp(0u, acc, 0x102, 0xF, 0xF, false);
-  if ((u & 3u) == 0) acc = span_shift_x(lds, 1, acc, y);
+  if ((u & 3u) == 0) acc = span_shift_x<TP, kPre>(lds, lt, 1, acc, y);
   y = __builtin_amdgcn_update_dpp(0u, acc, 0x104, 0xF, 0xF, false);
-  if ((u & 7u) == 0) acc = span_shift_x(lds, 2, acc, y);
+  if ((u & 7u) == 0) acc = span_shift_x<TP, kPre>(lds, lt, 2, acc, y);
   y = __builtin_amdgcn_update_dpp(0u, acc, 0x108, 0xF, 0xF, false);
-  if ((u & 15u) == 0) acc = span_shift_x(lds, 3, acc, y);
+  if ((u & 15u) == 0) acc = span_shift_x<TP, kPre>(lds, lt, 3, acc, y);
   y = __builtin_amdgcn_ds_swizzle(acc, 0x401F);  // lane ^ 16
-  if ((u & 31u) == 0) acc = span_shift_x(lds, 4, acc, y);
+  if ((u & 31u) == 0) acc = span_shift_x<TP, kPre>(lds, lt, 4, acc, y);
   y = __builtin_amdgcn_readlane(acc, 32);
-  if (u == 0) acc = span_shift_x(lds, 5, acc, y);
+  if (u == 0) acc = span_shift_x<TP, kPre>(lds, lt, 5, acc, y);
   return __builtin_amdgcn_readfirstlane(acc);
 }
 
@@ -364,10 +372,14 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void cr
   // always 8) have no registers to spare for it (their 2 x 9 staging chunks in flight), nor has the
   // verify form (an expected word per item in flight: it spilled 24-28 B per lane with it)
   constexpr bool kVar = kMixed && MODE != 17 && (MAXN == 512u || MAXN == 1023u) && !__is_same(Sink, VerifySink);
+  // kPre: the cross-lane fold pre-shifted per lane (lane c: shift by (c mod 4) parts, slots P1 / P2 / P3,
+  // then XORs within its quad; one P4 level for records of > 4 parts) instead of the tree of
+  // operator levels P1, P2, P4 (MODE 21 for now: A/B)
+  constexpr bool kPre = MODE == 21;
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
   char* lds = reinterpret_cast<char*>(lds_words);
   TP::stage(lds, tabs);
-  stage_ops_span<ST::kOpSet>(lds, tabs);
+  stage_ops_span<ST::kOpSet, kPre>(lds, tabs);
   const uint32_t u = threadIdx.x & 63u;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t ureg = tabs[PDB_UNSHIFT_OFF + (u & 15u)];
@@ -442,7 +454,7 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void cr
       sb &= sb - 1;
       const uintptr_t sp = static_cast<uintptr_t>(uniform64(__builtin_amdgcn_readlane(plo, k), __builtin_amdgcn_readlane(phi, k)));
       const uint32_t sn = __builtin_amdgcn_readlane(bn, k);
-      const uint32_t rs = span_slow_record<TP>(lds, lt, u, ureg, sp, sn);
+      const uint32_t rs = span_slow_record<TP, kPre>(lds, lt, u, ureg, sp, sn);
       if (u == 0)
         SinkOps<Sink>::put(sink, (bcur << 6) + k, rs, BlkDesc{reinterpret_cast<const uint8_t*>(sp), sn, 0xFFFFFFFFu},
                            __builtin_amdgcn_readlane(bpre, k));
@@ -868,7 +880,35 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void cr
     // parts c + m: the 4 PART m bytes before.  k a power of two: a record's k lanes never straddle
     // a row of 16, so the partner's value comes by DPP row_shl (no LDS round trip); other k by
     // bpermute.
-    if (MODE != 8 && k > 1u) {
+    if (kPre && k > 1u) {
+      // lane c: P = shift(R_c, 4 PART (c mod 4)) (slots P1, P2, P3 chosen per lane), XOR-reduced within
+      // the record's quad; a record of > 4 parts: the upper quad's sum shifted by 4 parts (P4) onto
+      // the lower's -- one operator level for k <= 4 (two for k <= 8) instead of log2(k)
+      const bool dpp = (k & (k - 1u)) == 0 && !(kVar && it.var);
+      const uint32_t l = pc & 3u;
+      const uint32_t slot = l == 1u ? kOpP1 : (l == 2u ? kOpP2 : kOpP3);
+      uint32_t v[4];
+#pragma unroll
+      for (uint32_t j = 0; j < 4; ++j) {
+        const uint32_t bb = __builtin_amdgcn_perm(0u, P, 0x0C0C0000u | (j << 8) | j);
+        v[j] = lds_u32(lds, (bb & 0xFF7Cu) ^ (128u | ((4u * slot + j) << 2)));
+      }
+      const uint32_t Ps = xor3(xor3(v[0], v[1], v[2]), v[3], 0u);
+      P = l ? Ps : P;
+      uint32_t y = dpp ? static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(P), 0x101, 0xF, 0xF, false))
+                       : __shfl_down(P, 1, 64);
+      if ((pc & 1u) == 0 && more(1u)) P ^= y;
+      if (k > 2u) {
+        y = dpp ? static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(P), 0x102, 0xF, 0xF, false))
+                : __shfl_down(P, 2, 64);
+        if ((pc & 3u) == 0 && more(2u)) P ^= y;
+      }
+      if (k > 4u) {
+        y = dpp ? static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(P), 0x104, 0xF, 0xF, false))
+                : __shfl_down(P, 4, 64);
+        if ((pc & 7u) == 0 && more(4u)) P = opx(kOpP4, y, P);
+      }
+    } else if (MODE != 8 && k > 1u) {
       const bool dpp = MODE != 11 && !kOldFold && (k & (k - 1u)) == 0 && !(kVar && it.var);
       uint32_t y = dpp ? static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(P), 0x101, 0xF, 0xF, false))
                        : __shfl_down(P, 1, 64);

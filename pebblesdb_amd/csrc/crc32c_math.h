@@ -76,11 +76,11 @@ static const unsigned long long kPdbCatDist[PDB_NCAT] = {16,   32,   64,   128, 
 #define PDB_UNSHIFT_OFF (1024u + PDB_NCAT * 1024u)
 #define PDB_UNSHIFT_WORDS 64u
 /* Record-kernel operators (crc32c_lanespan.h): shifts by 1, 2 and 4 parts -- 132, 264, 528 bytes
- * for its 33-word parts, 108, 216, 432 for the 27-word parts of the 257..512-B class -- 4 x 256
- * entries each. */
+ * for its 33-word parts, 108, 216, 432 for the 27-word parts of the 257..512-B class -- and by 3
+ * parts (396 / 324 B: the per-lane pre-shift of the cross-lane fold), 4 x 256 entries each. */
 #define PDB_SPANOP_OFF (PDB_UNSHIFT_OFF + PDB_UNSHIFT_WORDS)
-#define PDB_SPANOP_N 6
-static const unsigned long long kPdbSpanOpDist[PDB_SPANOP_N] = {132, 264, 528, 108, 216, 432};
+#define PDB_SPANOP_N 8
+static const unsigned long long kPdbSpanOpDist[PDB_SPANOP_N] = {132, 264, 528, 108, 216, 432, 396, 324};
 /* Device table source: T0..T3 (1024 u32), the catalog (PDB_NCAT * 1024 u32), the unshifted
  * seeds (64 u32, 17 used), the record-kernel operators (PDB_SPANOP_N * 1024 u32). */
 #define PDB_TABLE_WORDS (PDB_SPANOP_OFF + PDB_SPANOP_N * 1024u)
