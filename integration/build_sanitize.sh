@@ -1,13 +1,13 @@
 #!/usr/bin/env bash
-# integration/build_sanitize.sh <thread|address> -- the two CPU-only engine harnesses of
+# integration/build_sanitize.sh <thread|address|debug> -- the two CPU-only engine harnesses of
 # integration/build.sh (pdb_dbbench_cpu: the engine as shipped; pdb_dbbench_buffered_cpu: this repo's
 # table hooks with the reference CRC, no GPU library) compiled with a sanitizer, frame pointers and no
 # sibling-call optimisation, so a fault's stack names every caller (the teardown
-# abort).  Sources compiled IN PLACE from /root/reference (never copied or modified); outputs only
+# abort); `debug`: the same flags with no sanitizer (to run under gdb at full speed).  Sources compiled IN PLACE from /root/reference (never copied or modified); outputs only
 # under integration/_build_san_<kind>/ (git-ignored, CPU diagnostics: never run on the GPU box).
 set -euo pipefail
 KIND="${1:-thread}"
-case "$KIND" in thread|address) ;; *) echo "usage: $0 thread|address" >&2; exit 2 ;; esac
+case "$KIND" in thread|address|debug) ;; *) echo "usage: $0 thread|address|debug" >&2; exit 2 ;; esac
 HERE="$(cd "$(dirname "$0")" && pwd)"
 ROOT="$(dirname "$HERE")"
 REF="${PDB_REFERENCE_ROOT:-/root/reference}/src"
@@ -25,7 +25,8 @@ ENGINE="db/builder.cc db/db_impl.cc db/db_iter.cc db/dbformat.cc db/filename.cc 
 TABLE_REF="table/table_builder.cc table/format.cc table/table.cc"
 DEFS="-DLEVELDB_PLATFORM_POSIX -DOS_LINUX -DHAVE_FFLUSH_UNLOCKED -DHAVE_FREAD_UNLOCKED"
 DEFS="$DEFS -DHAVE_FWRITE_UNLOCKED -DHAVE_FDATASYNC -DHAVE_DECL_FDATASYNC=1 -DNDEBUG"
-SAN="-fsanitize=$KIND -fno-omit-frame-pointer -fno-optimize-sibling-calls -g"
+SAN="-fno-omit-frame-pointer -fno-optimize-sibling-calls -g"
+[ "$KIND" = debug ] || SAN="-fsanitize=$KIND $SAN"
 CXX="g++ -O1 -std=c++11 -w -pthread $SAN"
 JOBS="${PDB_BUILD_JOBS:-8}"
 for f in $ENGINE $TABLE_REF util/crc32c.cc; do echo "$f"; done | xargs -P "$JOBS" -I{} sh -c \
@@ -40,4 +41,4 @@ objs() { local od="$1" f; shift; for f in $*; do printf '%s ' "$od/$(echo "$f" |
 $CXX -o "$B/pdb_dbbench_cpu" "$B/obj_hooks/dbbench_cpu.o" $(objs "$B/obj_ref" $ENGINE $TABLE_REF util/crc32c.cc)
 $CXX -o "$B/pdb_dbbench_buffered_cpu" "$B/obj_hooks/dbbench_hooks.o" "$B/obj_hooks/pdb_table_builder.o" \
   "$B/obj_hooks/pdb_format.o" "$B/obj_hooks/pdb_table.o" $(objs "$B/obj_ref" $ENGINE util/crc32c.cc)
-echo "built $B/{pdb_dbbench_cpu,pdb_dbbench_buffered_cpu} (-fsanitize=$KIND)"
+echo "built $B/{pdb_dbbench_cpu,pdb_dbbench_buffered_cpu} ($SAN)"

@@ -375,7 +375,9 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void cr
   // kPre: the cross-lane fold pre-shifted per lane (lane c: shift by (c mod 4) parts, slots P1 / P2 / P3,
   // then XORs within its quad; one P4 level for records of > 4 parts) instead of the tree of
   // operator levels P1, P2, P4 (MODE 21 for now: A/B)
-  constexpr bool kPre = MODE == 21;
+  constexpr bool kPre = MODE == 21 || MODE == 22;
+  // kSparse: p-word selects only at the (chain, step) pairs some lane needs (MODE 22, with kPre: A/B)
+  constexpr bool kSparse = MODE == 22;
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
   char* lds = reinterpret_cast<char*>(lds_words);
   TP::stage(lds, tabs);
@@ -711,6 +713,22 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void cr
       if (t >= (X == 3 ? FD : FABC) && t < static_cast<int32_t>(NI)) lmax = t;
     }
     const int32_t G = static_cast<int32_t>(wave_max_u32(act ? static_cast<uint32_t>(lmax + 1) : 0u)) - 1;
+    // kSparse (MODE 22): the (chain, step) pairs at which some lane of the item replaces a state, as
+    // one wave-uniform mask (bit 16 X + t), so the selects run only where one is due (equal-sized
+    // records: one or two pairs per item instead of every chain up to step G)
+    uint64_t selm = 0;
+    if constexpr (kSparse) {
+      uint32_t mlo = 0, mhi = 0;
+#pragma unroll
+      for (int32_t X = 0; X < 4; ++X) {
+        const int32_t t = T + static_cast<int32_t>(LC) * X;
+        if (act && t >= (X == 3 ? FD : FABC) && t < static_cast<int32_t>(NI)) {
+          if (X < 2) mlo |= 1u << (16 * X + t);
+          else mhi |= 1u << (16 * (X - 2) + t);
+        }
+      }
+      selm = (static_cast<uint64_t>(wave_or_u32(mhi)) << 32) | wave_or_u32(mlo);
+    }
     // base of the chains' words: chain X's dword i at q3 + 4 LC (3 - X) + 4 i (word at phase-2
     // step t = dwords t, t + 1); below the region for short records (words never used)
     const char* q3 = (MODE == 5 || MODE == 6) ? region + 4u * (u & 31u)
@@ -833,7 +851,14 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void cr
       } else if (dd) {
         xd = TP::step(lds, lt, xd, wd);
       }
-      if (MODE != 7 && t <= G) {
+      if constexpr (kSparse) {
+        if (abc) {
+          if ((selm >> t) & 1u) xa = T == t ? pw : xa;
+          if ((selm >> (16 + t)) & 1u) xb = T + static_cast<int32_t>(LC) == t ? pw : xb;
+          if ((selm >> (32 + t)) & 1u) xc = T + static_cast<int32_t>(2u * LC) == t ? pw : xc;
+        }
+        if (dd && ((selm >> (48 + t)) & 1u)) xd = T + static_cast<int32_t>(3u * LC) == t ? pw : xd;
+      } else if (MODE != 7 && t <= G) {
         if (abc) {
           xa = T == t ? pw : xa;
           xb = T + static_cast<int32_t>(LC) == t ? pw : xb;

@@ -10,7 +10,7 @@ tail -2 $O/tests_seal.log
 timeout -k 10 300 $T tests/test_scalar_server.py > $O/tests_server.log 2>&1; echo server_rc=$?; tail -3 $O/tests_server.log
 timeout -k 10 300 $T tests/test_integration.py -k "leveldb_verify_batched" > $O/tests_verify.log 2>&1; echo verify_rc=$?; tail -3 $O/tests_verify.log
 timeout -k 10 300 $T tests/test_shard.py -k "rccl" > $O/tests_rccl.log 2>&1; echo rccl_rc=$?; tail -3 $O/tests_rccl.log
-timeout -k 10 500 python -u tools/ab_span.py 0,160,162 wal400,wal1000,wal,wal100,rand300_500,rand64_1000 4 > $O/ab_pairs.log 2>&1; echo ab_rc=$?; cat $O/ab_pairs.log
+timeout -k 10 500 python -u tools/ab_span.py 0,160,162,163 wal400,wal1000,wal,wal100,rand300_500,rand64_1000 4 > $O/ab_pairs.log 2>&1; echo ab_rc=$?; cat $O/ab_pairs.log
 for w in sst_seal sst_seal2 c3 sstable; do
   timeout -k 10 300 python -u bench.py --workload $w --steps 50 --warmup 20 --no-cpu-baseline --no-copy-inclusive > $O/bench_$w.log 2>&1; echo "bench $w rc=$?"
   python - $O/bench_$w.log <<'PY'
