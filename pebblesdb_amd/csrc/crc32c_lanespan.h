@@ -350,7 +350,9 @@ struct SpanItem {
 // first row's choice for the whole batch, 16 10 waves x 9-KiB regions for every class, 17 the
 // batch-uniform k only (no per-record lanes for mixed sizes), 18 the item geometry instead of the CRC
 // (first record << 24 | records << 16 | lane << 8 | lanes << 4 | per-record mode; diagnostics), 19 the
-// round-3 staging reads (one ds_read_b32 per word instead of aligned b64 pairs).
+// staging reads as aligned ds_read_b64 pairs (round 4: slower), 21 the round-3 cross-lane tree (no
+// pre-shift), 22 sparse p-word selects (slower), 24 the staging reads from an opaque base, 25 from one
+// opaque base per chain.
 // TP: the table scheme.
 // kDyn: the workgroup owns batches [g nbat / G, (g + 1) nbat / G) and its waves take the next one
 // from an LDS counter (false: batch wave_id + k W, the round-2 static assignment -- diagnostics).
@@ -372,11 +374,13 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void cr
   // always 8) have no registers to spare for it (their 2 x 9 staging chunks in flight), nor has the
   // verify form (an expected word per item in flight: it spilled 24-28 B per lane with it)
   constexpr bool kVar = kMixed && MODE != 17 && (MAXN == 512u || MAXN == 1023u) && !__is_same(Sink, VerifySink);
-  // kPre: the cross-lane fold pre-shifted per lane (lane c: shift by (c mod 4) parts, slots P1 / P2 / P3,
-  // then XORs within its quad; one P4 level for records of > 4 parts) instead of the tree of
-  // operator levels P1, P2, P4 (MODE 21 for now: A/B)
-  constexpr bool kPre = MODE == 21 || MODE == 22;
-  // kSparse: p-word selects only at the (chain, step) pairs some lane needs (MODE 22, with kPre: A/B)
+  // kPre (the product since round 4): the cross-lane fold pre-shifted per lane -- lane c: shift by
+  // (c mod 4) parts (slots P1 / P2 / P3), XORs within its quad, one P4 level for records of > 4
+  // parts -- instead of the round-3 tree of operator levels P1, P2, P4 (MODE 21; +0.2-1.7 % on the
+  // WAL rows in A/B, profiles/r04/ab_variants.log)
+  constexpr bool kPre = MODE != 8 && MODE != 10 && MODE != 11 && MODE != 21;
+  constexpr bool kOpaqueBase = MODE == 24 || MODE == 25;
+  // kSparse: p-word selects only at the (chain, step) pairs some lane needs (MODE 22: slower)
   constexpr bool kSparse = MODE == 22;
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
   char* lds = reinterpret_cast<char*>(lds_words);
@@ -733,6 +737,28 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void cr
     // step t = dwords t, t + 1); below the region for short records (words never used)
     const char* q3 = (MODE == 5 || MODE == 6) ? region + 4u * (u & 31u)
                                               : region + 4 * ((eA - static_cast<int32_t>(4u * NI + 12u * LC)) >> 2);
+    // kOpaqueBase (MODE 24): the chains' reads addressed as lds + qo + constant with qo opaque to the
+    // compiler, so every read takes its constant in the instruction's offset field (left to itself
+    // the compiler re-bases them on the highest address and computes each negative offset with a VALU)
+    // (MODE 25: one opaque base per chain, so no two chains' reads merge into a ds_read2_b32 whose
+    // result the compiler then waits for before the step's lookups)
+    uint32_t qo[4] = {0u, 0u, 0u, 0u};
+    if constexpr (kOpaqueBase) {
+      const uint32_t q0 = static_cast<uint32_t>(region - lds) +
+                          static_cast<uint32_t>(4 * ((eA - static_cast<int32_t>(4u * NI + 12u * LC)) >> 2));
+#pragma unroll
+      for (uint32_t X = 0; X < 4; ++X) {
+        qo[X] = q0 + (MODE == 25 ? 4u * LC * (3u - X) : 0u);
+        if (MODE == 25 || X == 0) asm volatile("" : "+v"(qo[X]));
+      }
+    }
+    // chain X's dword at byte offset `off` from q3 (off includes the chain's 4 LC (3 - X))
+    auto sread = [&](uint32_t X, uint32_t off) -> uint32_t {
+      if constexpr (kOpaqueBase)
+        return MODE == 25 ? lds_u32(lds, qo[X] + off - 4u * LC * (3u - X)) : lds_u32(lds, qo[0] + off);
+      else
+        return lds_u32(q3, off);
+    };
     uint32_t xd = 0, ld = 0;
     if (lim > 0) {  // the head chain alone (junk on the other lanes, dropped)
       const int32_t tD = T + static_cast<int32_t>(3u * LC + lim) - FD;  // the p-word's step in it
@@ -745,17 +771,19 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void cr
         xd = t == tD ? pw : TP::step(lds, lt, xd, w);
       }
       xd = head ? xd : 0u;
-    } else if constexpr (MODE == 19 || MODE == 5 || MODE == 6) {  // (kPairs: read below)
-      ld = lds_u32(q3, 4u * FD);
+    } else if constexpr (MODE != 19) {  // (kPairs: read below)
+      ld = sread(3, 4u * FD);
     }
     uint32_t xa = 0, xb = 0, xc = 0;
-    // The chains' words.  kPairs (the product since round 4): every chain's dwords come as 8-B
-    // aligned ds_read_b64 pairs from q3e (q3 rounded down to 8 B; par = q3's dword parity), one pair
-    // every two steps, and dword i of a chain is pair dword i + par (one v_cndmask).  An aligned
-    // b64 read costs the LDS ~2.5 cycles against ~2.2 for a b32 (tools/lds_probe.hip,
-    // profiles/r04_lds_probe.log: a 4-B aligned b64 / b128 costs ~27-29), so the staging reads
-    // take ~40 % of the LDS cycles of one b32 per word.  MODE 19: one ds_read_b32 per word (round 3).
-    constexpr bool kPairs = MODE != 19 && MODE != 5 && MODE != 6;
+    // The chains' words: one ds_read_b32 per word and chain (the dword after the previous one).
+    // kPairs (MODE 19, diagnostics): every chain's dwords as 8-B aligned ds_read_b64 pairs from
+    // q3e (q3 rounded down to 8 B; par = q3's dword parity), one pair every two steps, dword i =
+    // pair dword i + par (one v_cndmask).  An aligned b64 costs the LDS ~2.5 cycles against ~2.2
+    // for a b32 (tools/lds_probe.hip, profiles/r04/lds_probe.log; a 4-B aligned b64 / b128 ~27-29),
+    // but in the kernel the pairs measured 2.5-9 % SLOWER on every WAL row (profiles/r04/
+    // ab_pairs.log: the extra live pair registers and selects; 168 VGPRs and spills in the 9-KiB
+    // classes), so the product keeps the dword reads.
+    constexpr bool kPairs = MODE == 19;
     const int32_t qd = (eA - static_cast<int32_t>(4u * NI + 12u * LC)) >> 2;  // q3's dword (region-relative)
     const bool par = (qd & 1) != 0;
     // chain X's pairs: pair j = dwords 2 j, 2 j + 1 above qb[X] (8-B aligned; chains A, B, C, D at
@@ -792,8 +820,8 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void cr
       }
       la = d0[0], lb = d0[1], lc = d0[2], ld = d0[3];
     } else {
-      la = lds_u32(q3, 12u * LC + 4u * FABC), lb = lds_u32(q3, 8u * LC + 4u * FABC);
-      lc = lds_u32(q3, 4u * LC + 4u * FABC);
+      la = sread(0, 12u * LC + 4u * FABC), lb = sread(1, 8u * LC + 4u * FABC);
+      lc = sread(2, 4u * LC + 4u * FABC);
     }
     // dword t + 1 (+ par) of chain X at step t: even t reads pair t / 2 + 1 first
     auto next_dw = [&](uint32_t X, int32_t t) -> uint32_t {
@@ -812,8 +840,8 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void cr
         if constexpr (kPairs) {
           ha = next_dw(0, t), hb = next_dw(1, t), hc = next_dw(2, t);
         } else {
-          ha = lds_u32(q3, 12u * LC + 4u * (t + 1)), hb = lds_u32(q3, 8u * LC + 4u * (t + 1));
-          hc = lds_u32(q3, 4u * LC + 4u * (t + 1));
+          ha = sread(0, 12u * LC + 4u * (t + 1)), hb = sread(1, 8u * LC + 4u * (t + 1));
+          hc = sread(2, 4u * LC + 4u * (t + 1));
         }
         wa = __builtin_amdgcn_perm(ha, la, sel), wb = __builtin_amdgcn_perm(hb, lb, sel);
         wc = __builtin_amdgcn_perm(hc, lc, sel);
@@ -824,7 +852,7 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void cr
         if constexpr (kPairs) {
           hd = next_dw(3, t);
         } else {
-          hd = lds_u32(q3, 4u * (t + 1));
+          hd = sread(3, 4u * (t + 1));
         }
         wd = __builtin_amdgcn_perm(hd, ld, sel);
         ld = hd;

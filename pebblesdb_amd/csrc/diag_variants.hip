@@ -1252,9 +1252,11 @@ hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tab
     case 124:    // exact: 10 waves x 9-KiB regions for every class
     case 125:    // exact: the batch-uniform k only (no per-record lanes for mixed sizes; round 3 before)
     case 126:    // the item geometry per record instead of its CRC (MODE 18)
-    case 160:    // exact: the round-3 staging reads (one ds_read_b32 per word; MODE 19)
-    case 162:    // exact: the cross-lane fold pre-shifted per lane (MODE 21)
-    case 163: {  // exact: 162 + p-word selects only where some lane replaces (MODE 22)
+    case 160:    // exact: the staging reads as aligned ds_read_b64 pairs (MODE 19; round 4, slower)
+    case 162:    // exact: the round-3 cross-lane tree of operator levels (no per-lane pre-shift; MODE 21)
+    case 163:    // exact: p-word selects only where some lane replaces (MODE 22)
+    case 165:    // exact: the staging reads addressed from an opaque base (MODE 24)
+    case 166: {  // exact: ... from one opaque base per chain (MODE 25)
       const uint32_t cls = (flags & PDB_CRC_SIZE_256) ? 256u
                            : (flags & PDB_CRC_SIZE_512) ? 512u : ((flags & PDB_CRC_SIZE_1K) ? 1152u : 1023u);
       if (v == 118) launch_lanespan<DescSrc, OutSink, 10>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
@@ -1267,6 +1269,8 @@ hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tab
       else if (v == 160) launch_lanespan<DescSrc, OutSink, 19>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
       else if (v == 162) launch_lanespan<DescSrc, OutSink, 21>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
       else if (v == 163) launch_lanespan<DescSrc, OutSink, 22>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
+      else if (v == 165) launch_lanespan<DescSrc, OutSink, 24>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
+      else if (v == 166) launch_lanespan<DescSrc, OutSink, 25>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
       else launch_lanespan<DescSrc, OutSink, 18>(g, d_tables, src, nblk, cls, OutSink{out, 0u}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
       break;
     }
