@@ -835,13 +835,15 @@ __device__ __forceinline__ void write_trailer_word(uintptr_t a, uint32_t m) {
 
 template <>
 struct SinkOps<SstVerifySink> {
-  // the stored trailer word at p + n (any alignment): the two aligned dwords holding it
+  // the stored trailer word at p + n (any alignment): ONE dword load at its own byte address (the
+  // runtime runs shaders in unaligned access mode: the memory pipeline splits it when it crosses a
+  // dword, and this is one load per block, off the hashing path).  Round 3 loaded the two aligned
+  // dwords and merged them with v_alignbyte: one more register live per block in flight, which in
+  // the 12-wave verify (168 VGPRs a lane) spilled -- 6.45 MB of scratch writes per 1 M-block
+  // launch against 1.05 MB of `ok` bytes.
   __device__ static __forceinline__ uint32_t pre(const SstVerifySink&, uint64_t, const BlkDesc& d) {
-    typedef __attribute__((address_space(1))) const uint32_t g_u32_;
-    const uintptr_t a = reinterpret_cast<uintptr_t>(d.p) + d.n;
-    const uint32_t s = static_cast<uint32_t>(a & 3u);
-    const uint32_t lo = *reinterpret_cast<g_u32_*>(a - s), hi = *reinterpret_cast<g_u32_*>(a - s + (s ? 4u : 0u));
-    return __builtin_amdgcn_alignbyte(hi, lo, s);
+    typedef __attribute__((address_space(1), aligned(1))) const uint32_t g_u32u_;
+    return *reinterpret_cast<g_u32u_*>(reinterpret_cast<uintptr_t>(d.p) + d.n);
   }
   __device__ static __forceinline__ void put(const SstVerifySink& k, uint64_t i, uint32_t raw, const BlkDesc& d,
                                              uint32_t stored) {
