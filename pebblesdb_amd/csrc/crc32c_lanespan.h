@@ -351,8 +351,8 @@ struct SpanItem {
 // batch-uniform k only (no per-record lanes for mixed sizes), 18 the item geometry instead of the CRC
 // (first record << 24 | records << 16 | lane << 8 | lanes << 4 | per-record mode; diagnostics), 19 the
 // staging reads as aligned ds_read_b64 pairs (round 4: slower), 21 the round-3 cross-lane tree (no
-// pre-shift), 22 sparse p-word selects (slower), 24 the staging reads from an opaque base, 25 from one
-// opaque base per chain.
+// pre-shift), 22 sparse p-word selects (slower), 25 the staging reads from one opaque base per chain,
+// 26 one compare per step for the p-word selects, 27 the round-3 staging-read addressing.
 // TP: the table scheme.
 // kDyn: the workgroup owns batches [g nbat / G, (g + 1) nbat / G) and its waves take the next one
 // from an LDS counter (false: batch wave_id + k W, the round-2 static assignment -- diagnostics).
@@ -379,7 +379,11 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void cr
   // parts -- instead of the round-3 tree of operator levels P1, P2, P4 (MODE 21; +0.2-1.7 % on the
   // WAL rows in A/B, profiles/r04/ab_variants.log)
   constexpr bool kPre = MODE != 8 && MODE != 10 && MODE != 11 && MODE != 21;
-  constexpr bool kOpaqueBase = MODE == 24 || MODE == 25;
+  // kOpaqueBase (the product since round 4): the staging reads addressed from one opaque base
+  // (offset fields, some ds_read2_b32; +1.9-2.1 % on wal400 / wal1000 / wal in A/B,
+  // profiles/r04/ab_variants_r04d.log; MODE 27 = the round-3 addressing)
+  constexpr bool kOpaqueBase = MODE != 27 && MODE != 5 && MODE != 6 && MODE != 19;
+  constexpr bool kOneCmp = MODE == 26;
   // kSparse: p-word selects only at the (chain, step) pairs some lane needs (MODE 22: slower)
   constexpr bool kSparse = MODE == 22;
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
@@ -720,6 +724,17 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void cr
     // kSparse (MODE 22): the (chain, step) pairs at which some lane of the item replaces a state, as
     // one wave-uniform mask (bit 16 X + t), so the selects run only where one is due (equal-sized
     // records: one or two pairs per item instead of every chain up to step G)
+    // kOneCmp (MODE 26): a lane replaces at most one (chain, step) pair (Xp, tp): one compare per
+    // step (tp == t) and-ed with per-item lane masks (Xp == X), instead of one compare per chain and step
+    int32_t tp = -1, xp = -1;
+    if constexpr (kOneCmp) {
+#pragma unroll
+      for (int32_t X = 0; X < 4; ++X) {
+        const int32_t t = T + static_cast<int32_t>(LC) * X;
+        if (t >= (X == 3 ? FD : FABC) && t < static_cast<int32_t>(NI)) tp = t, xp = X;
+      }
+    }
+    const bool pA = xp == 0, pB = xp == 1, pC = xp == 2, pD = xp == 3;
     uint64_t selm = 0;
     if constexpr (kSparse) {
       uint32_t mlo = 0, mhi = 0;
@@ -886,6 +901,14 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void cr
           if ((selm >> (32 + t)) & 1u) xc = T + static_cast<int32_t>(2u * LC) == t ? pw : xc;
         }
         if (dd && ((selm >> (48 + t)) & 1u)) xd = T + static_cast<int32_t>(3u * LC) == t ? pw : xd;
+      } else if (kOneCmp && t <= G) {
+        const bool hit = tp == t;
+        if (abc) {
+          xa = hit && pA ? pw : xa;
+          xb = hit && pB ? pw : xb;
+          xc = hit && pC ? pw : xc;
+        }
+        if (dd) xd = hit && pD ? pw : xd;
       } else if (MODE != 7 && t <= G) {
         if (abc) {
           xa = T == t ? pw : xa;

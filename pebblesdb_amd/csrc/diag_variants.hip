@@ -1255,8 +1255,9 @@ hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tab
     case 160:    // exact: the staging reads as aligned ds_read_b64 pairs (MODE 19; round 4, slower)
     case 162:    // exact: the round-3 cross-lane tree of operator levels (no per-lane pre-shift; MODE 21)
     case 163:    // exact: p-word selects only where some lane replaces (MODE 22)
-    case 165:    // exact: the staging reads addressed from an opaque base (MODE 24)
-    case 166: {  // exact: ... from one opaque base per chain (MODE 25)
+    case 165:    // exact: the round-3 staging-read addressing (no opaque base; MODE 27)
+    case 166:    // exact: the staging reads from one opaque base per chain (MODE 25)
+    case 167: {  // exact: one compare per step for the p-word selects (MODE 26)
       const uint32_t cls = (flags & PDB_CRC_SIZE_256) ? 256u
                            : (flags & PDB_CRC_SIZE_512) ? 512u : ((flags & PDB_CRC_SIZE_1K) ? 1152u : 1023u);
       if (v == 118) launch_lanespan<DescSrc, OutSink, 10>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
@@ -1269,7 +1270,8 @@ hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tab
       else if (v == 160) launch_lanespan<DescSrc, OutSink, 19>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
       else if (v == 162) launch_lanespan<DescSrc, OutSink, 21>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
       else if (v == 163) launch_lanespan<DescSrc, OutSink, 22>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
-      else if (v == 165) launch_lanespan<DescSrc, OutSink, 24>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
+      else if (v == 165) launch_lanespan<DescSrc, OutSink, 27>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
+      else if (v == 167) launch_lanespan<DescSrc, OutSink, 26>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
       else if (v == 166) launch_lanespan<DescSrc, OutSink, 25>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
       else launch_lanespan<DescSrc, OutSink, 18>(g, d_tables, src, nblk, cls, OutSink{out, 0u}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
       break;
