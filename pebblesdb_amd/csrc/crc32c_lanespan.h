@@ -166,14 +166,19 @@ struct TabsS4 {
   }
 };
 
-template <uint32_t kOpSet, bool kPre = false>
+template <uint32_t kOpSet, bool kPre = false, bool kPreF = false>
 __device__ __forceinline__ void stage_ops_span(char* lds, const uint32_t* __restrict__ tabs) {
   // slot s, sub-table j, entry b at b<<8 | 128 | (((b >> 2) ^ (4s + j)) & 31) << 2; sources: catalog
   // entries 0 (16), 1 (32), 2 (64), 4 (256), 6 (1024), then the class's part operators (132, 264,
   // 528 or 108, 216, 432); kPre: slot 0 = the class's 3-part operator (396 or 324)
   for (uint32_t i = threadIdx.x; i < 8u * 1024u; i += blockDim.x) {
     const uint32_t slot = i >> 10, j = (i >> 8) & 3u, b = i & 255u;
-    const uint32_t src = (kPre && slot == 0u) ? PDB_SPANOP_OFF + (kOpSet == 0u ? 6u : 7u) * 1024u
+    // kPreF: slots 5, 6, 0 = 1, 2, 3 parts + 4 B (catalog 8..10 / 11..13); slot 7 stays 4 parts
+    const uint32_t f = kOpSet == 0u ? 8u : 11u;
+    const uint32_t src = (kPreF && slot == 0u)   ? PDB_SPANOP_OFF + (f + 2u) * 1024u
+                         : (kPreF && slot == 5u) ? PDB_SPANOP_OFF + f * 1024u
+                         : (kPreF && slot == 6u) ? PDB_SPANOP_OFF + (f + 1u) * 1024u
+                         : (kPre && slot == 0u)  ? PDB_SPANOP_OFF + (kOpSet == 0u ? 6u : 7u) * 1024u
                          : slot < 5u ? 1024u + (slot < 3u ? slot : (slot == 3u ? 4u : 6u)) * 1024u
                                      : PDB_SPANOP_OFF + (slot - 5u + kOpSet) * 1024u;
     *reinterpret_cast<uint32_t*>(lds + ((b << 8) | 128u | ((((b >> 2) ^ (4u * slot + j)) & 31u) << 2))) = tabs[src + j * 256u + b];
@@ -352,7 +357,8 @@ struct SpanItem {
 // (first record << 24 | records << 16 | lane << 8 | lanes << 4 | per-record mode; diagnostics), 19 the
 // staging reads as aligned ds_read_b64 pairs (round 4: slower), 21 the round-3 cross-lane tree (no
 // pre-shift), 22 sparse p-word selects (slower), 25 the staging reads from one opaque base per chain,
-// 26 one compare per step for the p-word selects, 27 the round-3 staging-read addressing.
+// 26 one compare per step for the p-word selects, 27 the round-3 staging-read addressing, 28 the
+// finishing step folded into the pre-shift.
 // TP: the table scheme.
 // kDyn: the workgroup owns batches [g nbat / G, (g + 1) nbat / G) and its waves take the next one
 // from an LDS counter (false: batch wave_id + k W, the round-2 static assignment -- diagnostics).
@@ -379,6 +385,10 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void cr
   // parts -- instead of the round-3 tree of operator levels P1, P2, P4 (MODE 21; +0.2-1.7 % on the
   // WAL rows in A/B, profiles/r04/ab_variants.log)
   constexpr bool kPre = MODE != 8 && MODE != 10 && MODE != 11 && MODE != 21;
+  // kPreF (MODE 28): the pre-shift operators carry the finishing table step F too (1, 2, 3 parts
+  // + 4 B), and the lanes of part 0 mod 4 apply F through the replicated T tables in the same
+  // lookup instructions -- the separate F level after the fold disappears (records of > 1 part)
+  constexpr bool kPreF = kPre && MODE == 28;
   // kOpaqueBase (the product since round 4): the staging reads addressed from one opaque base
   // (offset fields, some ds_read2_b32; +1.9-2.1 % on wal400 / wal1000 / wal in A/B,
   // profiles/r04/ab_variants_r04d.log; MODE 27 = the round-3 addressing)
@@ -389,7 +399,7 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void cr
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
   char* lds = reinterpret_cast<char*>(lds_words);
   TP::stage(lds, tabs);
-  stage_ops_span<ST::kOpSet, kPre>(lds, tabs);
+  stage_ops_span<ST::kOpSet, kPre, kPreF>(lds, tabs);
   const uint32_t u = threadIdx.x & 63u;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t ureg = tabs[PDB_UNSHIFT_OFF + (u & 15u)];
@@ -964,13 +974,29 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void cr
       const uint32_t l = pc & 3u;
       const uint32_t slot = l == 1u ? kOpP1 : (l == 2u ? kOpP2 : kOpP3);
       uint32_t v[4];
+      if constexpr (kPreF) {
+        // instruction i: byte jb = 3 - k of P, k = (quarter + i) & 3 (the T step's lane-quarter
+        // order); lanes of part 0 mod 4 read T_k (replica lane & 7), the others sub-table jb of
+        // their slot -- every lane's four lookups cover its four bytes
+        const uint32_t q = (u >> 3) & 3u;
 #pragma unroll
-      for (uint32_t j = 0; j < 4; ++j) {
-        const uint32_t bb = __builtin_amdgcn_perm(0u, P, 0x0C0C0000u | (j << 8) | j);
-        v[j] = lds_u32(lds, (bb & 0xFF7Cu) ^ (128u | ((4u * slot + j) << 2)));
+        for (uint32_t i = 0; i < 4; ++i) {
+          const uint32_t kk = (q + i) & 3u, jb = 3u - kk;
+          const uint32_t aT = __builtin_amdgcn_perm(lt.t[i], P, lt.s[i]);
+          const uint32_t bb = __builtin_amdgcn_perm(0u, P, 0x0C0C0000u | (jb << 8) | jb);
+          const uint32_t aO = (bb & 0xFF7Cu) ^ (128u | ((4u * slot + jb) << 2));
+          v[i] = lds_u32(lds, l ? aO : aT);
+        }
+        P = xor3(xor3(v[0], v[1], v[2]), v[3], 0u);
+      } else {
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+          const uint32_t bb = __builtin_amdgcn_perm(0u, P, 0x0C0C0000u | (j << 8) | j);
+          v[j] = lds_u32(lds, (bb & 0xFF7Cu) ^ (128u | ((4u * slot + j) << 2)));
+        }
+        const uint32_t Ps = xor3(xor3(v[0], v[1], v[2]), v[3], 0u);
+        P = l ? Ps : P;
       }
-      const uint32_t Ps = xor3(xor3(v[0], v[1], v[2]), v[3], 0u);
-      P = l ? Ps : P;
       uint32_t y = dpp ? static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(P), 0x101, 0xF, 0xF, false))
                        : __shfl_down(P, 1, 64);
       if ((pc & 1u) == 0 && more(1u)) P ^= y;
@@ -1000,7 +1026,7 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void cr
         if ((pc & 7u) == 0 && more(4u)) P = opx(kOpP4, y, P);
       }
     }
-    if constexpr (!kOldFold) P = TP::step(lds, lt, P, 0u);  // F: the chains' last words
+    if (!kOldFold && !(kPreF && k > 1u)) P = TP::step(lds, lt, P, 0u);  // F: the chains' last words
     if constexpr (MODE == 18)  // diagnostics: the item's first record, records, lane, lanes, mode
       P = ~(((it.cw >> 16) << 24) | (((it.cw >> 8) & 127u) << 16) | (u << 8) | ((kVar ? pc + ((it.cw >> 4) & 15u) + 1u : k) << 4) | (it.var ? 1u : 0u));
     if (pc == 0 && act)

@@ -76,11 +76,14 @@ static const unsigned long long kPdbCatDist[PDB_NCAT] = {16,   32,   64,   128, 
 #define PDB_UNSHIFT_OFF (1024u + PDB_NCAT * 1024u)
 #define PDB_UNSHIFT_WORDS 64u
 /* Record-kernel operators (crc32c_lanespan.h): shifts by 1, 2 and 4 parts -- 132, 264, 528 bytes
- * for its 33-word parts, 108, 216, 432 for the 27-word parts of the 257..512-B class -- and by 3
- * parts (396 / 324 B: the per-lane pre-shift of the cross-lane fold), 4 x 256 entries each. */
+ * for its 33-word parts, 108, 216, 432 for the 27-word parts of the 257..512-B class -- by 3
+ * parts (396 / 324 B: the per-lane pre-shift of the cross-lane fold), and by 1, 2, 3 parts + 4 B
+ * (136, 268, 400 / 112, 220, 328: the pre-shift with the finishing table step folded in), 4 x 256
+ * entries each. */
 #define PDB_SPANOP_OFF (PDB_UNSHIFT_OFF + PDB_UNSHIFT_WORDS)
-#define PDB_SPANOP_N 8
-static const unsigned long long kPdbSpanOpDist[PDB_SPANOP_N] = {132, 264, 528, 108, 216, 432, 396, 324};
+#define PDB_SPANOP_N 14
+static const unsigned long long kPdbSpanOpDist[PDB_SPANOP_N] = {132, 264, 528, 108, 216, 432, 396, 324,
+                                                                136, 268, 400, 112, 220, 328};
 /* Device table source: T0..T3 (1024 u32), the catalog (PDB_NCAT * 1024 u32), the unshifted
  * seeds (64 u32, 17 used), the record-kernel operators (PDB_SPANOP_N * 1024 u32). */
 #define PDB_TABLE_WORDS (PDB_SPANOP_OFF + PDB_SPANOP_N * 1024u)
