@@ -21,8 +21,10 @@
 #include <string.h>
 #include <time.h>
 
+#include <dirent.h>
 #include <execinfo.h>
 #include <pthread.h>
+#include <sys/stat.h>
 #include <signal.h>
 #include <unistd.h>
 
@@ -52,6 +54,7 @@ struct Flags {
   int value_size = 1024;
   int bloom_bits = 10;
   int cache_size = -1;  // < 0: the engine's default block cache
+  int quiesce_ms = 1000;  // before `delete db`: wait until the db directory is unchanged this long (0: no wait)
   bool verify_checksums = false;
   bool use_existing_db = false;
   bool paranoid_checks = false;
@@ -255,6 +258,40 @@ bool Arg(const char* a, const char* name, std::string* v) {
   return true;
 }
 
+// Sum of the sizes and mtimes of the files in `dir`: changes while a flush or compaction writes.
+uint64_t DirSignature(const std::string& dir) {
+  uint64_t sig = 0;
+  DIR* d = opendir(dir.c_str());
+  if (!d) return 0;
+  while (struct dirent* e = readdir(d)) {
+    struct stat st;
+    const std::string p = dir + "/" + e->d_name;
+    if (stat(p.c_str(), &st) == 0)
+      sig += static_cast<uint64_t>(st.st_size) * 1000003ull + static_cast<uint64_t>(st.st_mtim.tv_nsec) +
+             static_cast<uint64_t>(st.st_ino) * 7919ull;
+  }
+  closedir(d);
+  return sig;
+}
+
+// Wait until the directory's signature has not changed for `stable_ms` (checked every 50 ms), at
+// most `max_s` seconds.
+void DirQuiesce(const std::string& dir, int stable_ms, double max_s) {
+  const double t0 = NowSec();
+  uint64_t last = DirSignature(dir);
+  double since = NowSec();
+  while (NowSec() - t0 < max_s) {
+    usleep(50000);
+    const uint64_t cur = DirSignature(dir);
+    if (cur != last) {
+      last = cur;
+      since = NowSec();
+    } else if ((NowSec() - since) * 1000.0 >= stable_ms) {
+      return;
+    }
+  }
+}
+
 }  // namespace
 
 // Where the main thread is when a fault hits (the crash handler prints it): 0 running benchmarks,
@@ -271,6 +308,7 @@ void MainStackHandler(int) {
   const char msg[] = "pdb_dbbench: main thread backtrace at the fault:\n";
   (void)!write(2, msg, sizeof(msg) - 1);
   backtrace_symbols_fd(frames, n, 2);
+  for (;;) pause();  // the faulting thread re-raises its signal: the process ends with that status
 }
 
 // A fault prints the faulting thread's stack (stderr) before the default action, so a crash in the
@@ -313,6 +351,7 @@ int main(int argc, char** argv) {
     else if (Arg(argv[i], "--threads", &v)) F.threads = atoi(v.c_str());
     else if (Arg(argv[i], "--hash", &v)) F.hash = atoi(v.c_str()) != 0;
     else if (Arg(argv[i], "--db", &v)) F.db = v;
+    else if (Arg(argv[i], "--quiesce_ms", &v)) F.quiesce_ms = atoi(v.c_str());
     else {
       fprintf(stderr, "invalid flag '%s'\n", argv[i]);
       return 1;
@@ -360,6 +399,16 @@ int main(int argc, char** argv) {
     }
   }
   fflush(stdout);
+  // The engine's teardown races its own background threads: ~DBImpl (db_impl.cc:259-297) was seen
+  // destroying the table cache, the memtable or the version set while a memtable flush or a
+  // compaction was still running -- with the reference's own table code too (pdb_dbbench_cpu;
+  // DESIGN.md §6.1d, profiles/r04/teardown/).  Before `delete db` the harness therefore waits until
+  // the database directory has stopped changing (no flush or compaction writing) for --quiesce_ms.
+  if (F.quiesce_ms > 0) {
+    const double tq = NowSec();
+    DirQuiesce(F.db, F.quiesce_ms, 600.0);
+    fprintf(stderr, "quiesce: %.3f s\n", NowSec() - tq);
+  }
   const double td = NowSec();
   g_teardown_phase = 1;
   delete db;  // waits for the background compaction / memtable threads (db_impl.cc:259-297)
