@@ -66,6 +66,22 @@ def test_fillrandom_only_run_exits_cleanly(tmp_path):
         assert rc == 0, (name, out[-500:], err[-500:])
 
 
+def test_backed_up_fill_quiesces_before_delete(tmp_path):
+    """The teardown fault: the reference engine's destructor can free the table
+    cache while a flush or compaction still runs (the engine's own CPU build faults the same way,
+    profiles/r04/teardown/).  The harness waits until the database directory has stopped changing
+    (--quiesce_ms) before `delete db`: a fill large enough to leave compactions backed up at the
+    end exits 0 on both CPU builds and reports the wait."""
+    for name in ("pdb_dbbench_cpu", "pdb_dbbench_buffered_cpu"):
+        exe = _exe(name)
+        db = str(tmp_path / name)
+        rc, out, err = _run([exe, "--benchmarks=fillrandom", "--num=300000", "--value_size=1024",
+                             "--quiesce_ms=500", f"--db={db}"], timeout=600)
+        assert rc == 0, (name, out[-500:], err[-800:])
+        q = [l for l in err.splitlines() if l.startswith("quiesce: ")]
+        assert len(q) == 1 and float(q[0].split()[1]) >= 0.5, err[-800:]
+
+
 def _damaged_db(tmp_path, cpu):
     """A database the reference engine wrote, with one byte flipped in the middle data block of its
     largest table; returns (path, table name)."""
