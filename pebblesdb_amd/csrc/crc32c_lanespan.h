@@ -396,6 +396,10 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void cr
   constexpr bool kOneCmp = MODE == 26;
   // kSparse: p-word selects only at the (chain, step) pairs some lane needs (MODE 22: slower)
   constexpr bool kSparse = MODE == 22;
+  // kRot (MODE 29; the 33-word-part classes): the lock-step staging reads rotated over four chain
+  // slots per lane so that the lanes of one bank class (dword mod 8) read different banks (see hash)
+  constexpr bool kRot = MODE == 29 && LD == 9u && LC == 8u;
+  static_assert(!kRot || NI == 9u, "kRot: chain D's step 0 alone, then 8 steps of all four chains");
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
   char* lds = reinterpret_cast<char*>(lds_words);
   TP::stage(lds, tabs);
@@ -785,6 +789,86 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void cr
         return lds_u32(q3, off);
     };
     uint32_t xd = 0, ld = 0;
+    uint32_t xa = 0, xb = 0, xc = 0;
+    const int32_t qd = (eA - static_cast<int32_t>(4u * NI + 12u * LC)) >> 2;  // q3's dword (region-relative)
+    if constexpr (kRot) {
+      // the head chain alone for lim steps (junk on the other lanes, dropped), then chain D's step 0
+      // on every lane; chain D's dword i at q3 + 4 i (FD = 0)
+      const char* qh = q3 - 4 * static_cast<int32_t>(lim);
+      ld = lds_u32(qh, 0);
+      if (lim > 0) {
+        const int32_t tD = T + static_cast<int32_t>(3u * LC + lim);  // the p-word's step in it
+        for (int32_t t = 0; t < static_cast<int32_t>(lim); ++t, qh += 4) {
+          const uint32_t h = lds_u32(qh, 4);
+          const uint32_t w = __builtin_amdgcn_perm(h, ld, sel);
+          ld = h;
+          xd = t == tD ? pw : TP::step(lds, lt, xd, w);
+        }
+        xd = head ? xd : 0u;
+      }
+      xd = TP::step(lds, lt, xd, __builtin_amdgcn_perm(lds_u32(qh, 4), ld, sel));
+      xd = T + static_cast<int32_t>(3u * LC) == 0 ? pw : xd;
+      // steps 1 .. NI - 1: all four chains, in slots.  Slot i of this lane holds chain
+      // X_i = (i + rho) & 3, whose dword at step t is q3's dword + 8 (3 - X_i) + t + 1: bank
+      // (q3's dword mod 8) + 8 ((rank - i) mod 4) + t + 1 mod 32 with rank = a + 3 - rho (a = bits
+      // 3-4 of q3's dword).  rank = this lane's place among the lanes of its class (q3's dword mod 8),
+      // so up to four lanes of a class read four different banks in every slot.
+      const uint32_t qdw = (static_cast<uint32_t>(region - lds) >> 2) + static_cast<uint32_t>(qd);
+      // (records of >= 4 parts: a record's lanes are in different classes -- parts 33 words = 1 mod 8
+      // apart -- so the record's slot in the batch ranks it; fewer parts: ranked by ballots)
+      const uint32_t cls = qdw & 7u, a = (qdw >> 3) & 3u;
+      uint32_t rank = it.r;
+      if (k < 4u) {
+        const uint64_t m0 = __ballot((cls & 1u) != 0), m1 = __ballot((cls & 2u) != 0), m2 = __ballot((cls & 4u) != 0);
+        const uint64_t same = ((cls & 1u) ? m0 : ~m0) & ((cls & 2u) ? m1 : ~m1) & ((cls & 4u) ? m2 : ~m2);
+        rank = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(same >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(same), 0u));
+      }
+      const uint32_t rho = (a + 3u - rank) & 3u;
+      // a lane replaces at most one (chain, step): chain xr at step tr (-1: none), in slot ir
+      int32_t tr = -1, xr = 0;
+#pragma unroll
+      for (int32_t X = 0; X < 4; ++X) {
+        const int32_t t = T + static_cast<int32_t>(LC) * X;
+        if (t >= 1 && t < static_cast<int32_t>(NI)) tr = t, xr = X;
+      }
+      const uint32_t ir = (static_cast<uint32_t>(xr) - rho) & 3u, iD = (3u - rho) & 3u;
+      uint32_t xs[4], ls[4], qs[4];
+      int32_t tri[4];  // slot i's replacement step (-1: none)
+#pragma unroll
+      for (uint32_t i = 0; i < 4; ++i) {
+        tri[i] = ir == i ? tr : -1;
+        qs[i] = 4u * qdw + 32u * (3u - ((i + rho) & 3u));
+        asm volatile("" : "+v"(qs[i]));
+        ls[i] = lds_u32(lds, qs[i] + 4u);
+      }
+      const uint32_t TD = TP::step(lds, lt, xd, 0u);  // chain D's state stepped (its word added at step 1)
+#pragma unroll
+      for (int32_t t = 1; t < static_cast<int32_t>(NI); ++t) {
+        uint32_t ws[4];
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i) {
+          const uint32_t h = lds_u32(lds, qs[i] + 4u * static_cast<uint32_t>(t + 1));
+          ws[i] = __builtin_amdgcn_perm(h, ls[i], sel);
+          ls[i] = h;
+        }
+        if (t == 1) {
+#pragma unroll
+          for (uint32_t i = 0; i < 4; ++i) xs[i] = ws[i] ^ (iD == i ? TD : 0u);
+        } else {
+          TP::step4(lds, lt, xs, ws);
+        }
+        if (t <= G) {
+#pragma unroll
+          for (uint32_t i = 0; i < 4; ++i) xs[i] = tri[i] == t ? pw : xs[i];
+        }
+      }
+      // chain X is in slot (X - rho) & 3
+      auto pick = [&](uint32_t X) -> uint32_t {
+        const uint32_t i = (X - rho) & 3u;
+        return i == 0u ? xs[0] : (i == 1u ? xs[1] : (i == 2u ? xs[2] : xs[3]));
+      };
+      xa = pick(0u), xb = pick(1u), xc = pick(2u), xd = pick(3u);
+    } else {
     if (lim > 0) {  // the head chain alone (junk on the other lanes, dropped)
       const int32_t tD = T + static_cast<int32_t>(3u * LC + lim) - FD;  // the p-word's step in it
       const char* q = q3 + 4 * (FD - static_cast<int32_t>(lim));
@@ -799,7 +883,6 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void cr
     } else if constexpr (MODE != 19) {  // (kPairs: read below)
       ld = sread(3, 4u * FD);
     }
-    uint32_t xa = 0, xb = 0, xc = 0;
     // The chains' words: one ds_read_b32 per word and chain (the dword after the previous one).
     // kPairs (MODE 19, diagnostics): every chain's dwords as 8-B aligned ds_read_b64 pairs from
     // q3e (q3 rounded down to 8 B; par = q3's dword parity), one pair every two steps, dword i =
@@ -809,7 +892,6 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void cr
     // ab_pairs.log: the extra live pair registers and selects; 168 VGPRs and spills in the 9-KiB
     // classes), so the product keeps the dword reads.
     constexpr bool kPairs = MODE == 19;
-    const int32_t qd = (eA - static_cast<int32_t>(4u * NI + 12u * LC)) >> 2;  // q3's dword (region-relative)
     const bool par = (qd & 1) != 0;
     // chain X's pairs: pair j = dwords 2 j, 2 j + 1 above qb[X] (8-B aligned; chains A, B, C, D at
     // 3 LC, 2 LC, LC, 0 words above q3).  Each chain keeps the last two pairs read (P newest, Q);
@@ -928,6 +1010,7 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void cr
         if (dd) xd = T + static_cast<int32_t>(3u * LC) == t ? pw : xd;
       }
     }
+    }  // !kRot
     // Finish.  Chain X's state still holds its last word unshifted, and its bytes end 32 X bytes
     // before the part's end, so the part's raw CRC is F(xA) ^ S32 F(xB) ^ S64 F(xC) ^ S96 F(xD)
     // with F = the table step (shift 4) and S_n = shift n; these maps commute, so it is

@@ -37,7 +37,7 @@ def layout(payload, nbytes):
         offs = np.concatenate([[0], np.cumsum(lens + 7)[:-1]]) + 6
         return offs.astype(np.int64), lens.astype(np.int64)
     return wal_layout(nbytes, payload)
-PRICING = {113, 114, 115, 116, 117}
+PRICING = {63, 64, 67, 113, 114, 115, 116, 117}
 
 
 def main():
