@@ -413,9 +413,12 @@ int main(int argc, char** argv) {
   g_teardown_phase = 1;
   delete db;  // waits for the background compaction / memtable threads (db_impl.cc:259-297)
   g_teardown_phase = 2;
-  delete cache;
+  // The block cache and the filter policy stay allocated until the process exits: an engine thread
+  // was seen still running after ~DBImpl returned (profiles/r04/teardown/pF_3.log: the fault came
+  // after the harness had deleted both), so the harness frees nothing such a thread may still use.
+  (void)cache;
+  (void)fp;
   g_teardown_phase = 3;
-  delete fp;
   fprintf(stderr, "teardown: %.3f s\n", NowSec() - td);
   return 0;
 }
