@@ -54,11 +54,12 @@ constexpr uint32_t kSpanStageBase = 64u << 10;                    // tables and 
 // do not fit 8 KiB, so 8-KiB items held 7 records on 56 of the 64 lanes (+2.5 % with 9 KiB,
 // −4..−9 % for the 512 and 1023 classes, whose 8 records fit 8 KiB; profiles/r03_wide/).
 // kWide (diagnostics MODE 16): 10 x 9 KiB for every class.
-template <uint32_t MAXN, bool kWide = false>
+// k13 (diagnostics MODE 31, with the one-deep pipeline): 13 x 7 KiB.
+template <uint32_t MAXN, bool kWide = false, bool k13 = false>
 struct SpanStage {
-  static constexpr bool k9 = MAXN <= 256u || MAXN > 1023u || kWide;
-  static constexpr uint32_t kWaves = k9 ? 10u : 12u;  // (13 x 7 KiB for 512: slower, 128-VGPR cap)
-  static constexpr uint32_t kJ = k9 ? 9u : 8u;
+  static constexpr bool k9 = (MAXN <= 256u || MAXN > 1023u || kWide) && !k13;
+  static constexpr uint32_t kWaves = k13 ? 13u : (k9 ? 10u : 12u);  // (13 x 7 KiB with A/B staging: slower, 128-VGPR cap)
+  static constexpr uint32_t kJ = k13 ? 7u : (k9 ? 9u : 8u);
   static constexpr uint32_t kRegion = kJ * 1024u;
   static constexpr uint32_t kUsable = kRegion - 16u;  // span limit: reads stay inside
   static_assert((64u << 10) + kWaves * kRegion <= PDB_LDS_BYTES, "fits the 160 KiB");
@@ -364,11 +365,11 @@ struct SpanItem {
 // from an LDS counter (false: batch wave_id + k W, the round-2 static assignment -- diagnostics).
 // kMixed (PDB_CRC_SIZE_MIXED): per-record lane counts where a batch's records vary (open_batch).
 template <class Src, class Sink, uint32_t MAXN, int MODE = 0, class TP = TabsS4, bool kDyn = true, bool kMixed = false>
-__global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void crc_lanespan_kernel(const uint32_t* __restrict__ tabs, Src src,
+__global__ __launch_bounds__((SpanStage<MAXN, MODE == 16, MODE == 31>::kWaves * 64)) void crc_lanespan_kernel(const uint32_t* __restrict__ tabs, Src src,
                                                                        uint64_t nblk, Sink sink) {
-  constexpr uint32_t kSpanWaves = SpanStage<MAXN, MODE == 16>::kWaves, kSpanJ = SpanStage<MAXN, MODE == 16>::kJ;
-  constexpr uint32_t kSpanRegion = SpanStage<MAXN, MODE == 16>::kRegion, kSpanUsable = SpanStage<MAXN, MODE == 16>::kUsable;
-  typedef SpanStage<MAXN, MODE == 16> ST;
+  constexpr uint32_t kSpanWaves = SpanStage<MAXN, MODE == 16, MODE == 31>::kWaves, kSpanJ = SpanStage<MAXN, MODE == 16, MODE == 31>::kJ;
+  constexpr uint32_t kSpanRegion = SpanStage<MAXN, MODE == 16, MODE == 31>::kRegion, kSpanUsable = SpanStage<MAXN, MODE == 16, MODE == 31>::kUsable;
+  typedef SpanStage<MAXN, MODE == 16, MODE == 31> ST;
   constexpr uint32_t LC = ST::kLC, LD = ST::kLD, NI = ST::kNI, PART = ST::kPart;
   static_assert(MAXN + 32u <= kSpanUsable, "a record of the class must fit a region");
   // k parts cover MAXN: 2, 5, 8 (a longer class -- diagnostics 1152 -- stays at 8 lanes and runs
@@ -1119,6 +1120,23 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void cr
   // ---- pipeline: two items in flight while one is hashed ---------------------------------------
   // Loop head: the region holds I0, array B holds I1's loads in flight; only B's loads cross the
   // back edge.
+  // kOneDeep (diagnostics MODE 30 / 31): one item's loads in flight while one is hashed (half the
+  // staging registers), the loop: issue(next) -> hash(cur) -> to_lds(next)
+  constexpr bool kOneDeep = MODE == 30 || MODE == 31;
+  if constexpr (kOneDeep) {
+    u32x4 A[kSpanJ];
+    SpanItem I0 = next_item(true);
+    issue(A, I0);
+    to_lds(A);
+    while (I0.valid) {
+      const SpanItem I1 = next_item(true);
+      issue(A, I1);
+      hash(I0);
+      if (!I1.valid) break;
+      to_lds(A);
+      I0 = I1;
+    }
+  } else {
   u32x4 A[kSpanJ], B[kSpanJ];
   SpanItem I0 = next_item(true);
   issue(A, I0);
@@ -1139,6 +1157,7 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16>::kWaves * 64)) void cr
     I0 = I2;
     I1 = I3;
   }
+  }  // !kOneDeep
   if constexpr (MODE == 4) {
     const uint64_t t_end = wall_clock64();
     if (u == 0) {
@@ -1163,11 +1182,11 @@ template <class Src, class Sink, int MODE = 0, class TP = TabsS4, bool kDyn = tr
 void launch_lanespan(const LaunchGeom& g, const uint32_t* d_tables, const Src& src, uint64_t nblk, uint32_t cls,
                      const Sink& sink, hipStream_t s, bool mixed = false) {
   if (cls <= 256u) {
-    constexpr uint32_t w = SpanStage<256, MODE == 16>::kWaves;
+    constexpr uint32_t w = SpanStage<256, MODE == 16, MODE == 31>::kWaves;
     hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 256, MODE, TP, kDyn>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0, s,
                        d_tables, src, nblk, sink);
   } else if (cls <= 512u) {
-    constexpr uint32_t w = SpanStage<512, MODE == 16>::kWaves;
+    constexpr uint32_t w = SpanStage<512, MODE == 16, MODE == 31>::kWaves;
     if (mixed && !__is_same(Sink, VerifySink))
       hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 512, MODE, TP, kDyn, true>), dim3(grid_span(g, nblk, w)), dim3(w * 64),
                          0, s, d_tables, src, nblk, sink);
@@ -1175,7 +1194,7 @@ void launch_lanespan(const LaunchGeom& g, const uint32_t* d_tables, const Src& s
       hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 512, MODE, TP, kDyn>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0, s,
                          d_tables, src, nblk, sink);
   } else if (cls <= 1023u) {
-    constexpr uint32_t w = SpanStage<1023, MODE == 16>::kWaves;
+    constexpr uint32_t w = SpanStage<1023, MODE == 16, MODE == 31>::kWaves;
     if (mixed && !__is_same(Sink, VerifySink))
       hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 1023, MODE, TP, kDyn, true>), dim3(grid_span(g, nblk, w)), dim3(w * 64),
                          0, s, d_tables, src, nblk, sink);
@@ -1183,7 +1202,7 @@ void launch_lanespan(const LaunchGeom& g, const uint32_t* d_tables, const Src& s
       hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 1023, MODE, TP, kDyn>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0,
                          s, d_tables, src, nblk, sink);
   } else {  // 1024..1152 B (WAL records of ~1-KiB write batches): 8 lanes, the head chain past 1056 B
-    constexpr uint32_t w = SpanStage<1152, MODE == 16>::kWaves;
+    constexpr uint32_t w = SpanStage<1152, MODE == 16, MODE == 31>::kWaves;
     hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 1152, MODE, TP, kDyn>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0,
                        s, d_tables, src, nblk, sink);
   }
