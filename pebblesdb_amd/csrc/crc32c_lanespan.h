@@ -394,7 +394,11 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16, MODE == 31>::kWaves * 
   // (offset fields, some ds_read2_b32; +1.9-2.1 % on wal400 / wal1000 / wal in A/B,
   // profiles/r04/ab_variants_r04d.log; MODE 27 = the round-3 addressing)
   constexpr bool kOpaqueBase = MODE != 27 && MODE != 5 && MODE != 6 && MODE != 19;
-  constexpr bool kOneCmp = MODE == 26;
+  constexpr bool kOneCmp = MODE == 26 || MODE == 32;
+  // kMaskSel (MODE 32): the p-word selects as wave masks -- per item one ballot per chain of the lanes
+  // replacing in it, per step one ballot of the lanes replacing at that step; each select is then an
+  // SALU and of the two masks and one v_cndmask (inverse ballot), 5 VALU per step instead of 8
+  constexpr bool kMaskSel = MODE == 32;
   // kSparse: p-word selects only at the (chain, step) pairs some lane needs (MODE 22: slower)
   constexpr bool kSparse = MODE == 22;
   // kRot (MODE 29; the 33-word-part classes): the lock-step staging reads rotated over four chain
@@ -750,6 +754,10 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16, MODE == 31>::kWaves * 
       }
     }
     const bool pA = xp == 0, pB = xp == 1, pC = xp == 2, pD = xp == 3;
+    uint64_t mA = 0, mB = 0, mC = 0, mD = 0;
+    if constexpr (kMaskSel) {
+      mA = __ballot(pA), mB = __ballot(pB), mC = __ballot(pC), mD = __ballot(pD);
+    }
     uint64_t selm = 0;
     if constexpr (kSparse) {
       uint32_t mlo = 0, mhi = 0;
@@ -994,6 +1002,14 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16, MODE == 31>::kWaves * 
           if ((selm >> (32 + t)) & 1u) xc = T + static_cast<int32_t>(2u * LC) == t ? pw : xc;
         }
         if (dd && ((selm >> (48 + t)) & 1u)) xd = T + static_cast<int32_t>(3u * LC) == t ? pw : xd;
+      } else if (kMaskSel && t <= G) {
+        const uint64_t hm = __ballot(tp == t);
+        if (abc) {
+          xa = __builtin_amdgcn_inverse_ballot_w64(hm & mA) ? pw : xa;
+          xb = __builtin_amdgcn_inverse_ballot_w64(hm & mB) ? pw : xb;
+          xc = __builtin_amdgcn_inverse_ballot_w64(hm & mC) ? pw : xc;
+        }
+        if (dd) xd = __builtin_amdgcn_inverse_ballot_w64(hm & mD) ? pw : xd;
       } else if (kOneCmp && t <= G) {
         const bool hit = tp == t;
         if (abc) {

@@ -1261,7 +1261,8 @@ hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tab
     case 168:    // exact: the finishing step folded into the pre-shifted cross-lane fold (MODE 28)
     case 169:    // exact: the lock-step staging reads rotated over chain slots by bank class (MODE 29)
     case 170:    // exact: one item's loads in flight instead of two (MODE 30)
-    case 171: {  // exact: ... and 13 waves x 7-KiB regions (MODE 31)
+    case 171:    // exact: ... and 13 waves x 7-KiB regions (MODE 31)
+    case 172: {  // exact: the p-word selects as wave masks (inverse ballot; MODE 32)
       const uint32_t cls = (flags & PDB_CRC_SIZE_256) ? 256u
                            : (flags & PDB_CRC_SIZE_512) ? 512u : ((flags & PDB_CRC_SIZE_1K) ? 1152u : 1023u);
       if (v == 118) launch_lanespan<DescSrc, OutSink, 10>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
@@ -1279,6 +1280,7 @@ hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tab
       else if (v == 168) launch_lanespan<DescSrc, OutSink, 28>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
       else if (v == 170) launch_lanespan<DescSrc, OutSink, 30>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
       else if (v == 171) launch_lanespan<DescSrc, OutSink, 31>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
+      else if (v == 172) launch_lanespan<DescSrc, OutSink, 32>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
       else if (v == 169) launch_lanespan<DescSrc, OutSink, 29>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
       else if (v == 166) launch_lanespan<DescSrc, OutSink, 25>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
       else launch_lanespan<DescSrc, OutSink, 18>(g, d_tables, src, nblk, cls, OutSink{out, 0u}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);

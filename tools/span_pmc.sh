@@ -1,14 +1,15 @@
 #!/usr/bin/env bash
 # tools/span_pmc.sh <tag> <variants> <workloads> -- SQ LDS counters per record-kernel MODE under
 # tools/ab_span.py (one --pmc pass per workload; per-launch means in millions, grouped by the kernel's
-# MODE template argument).  Prints one JSON object (the last line).
+# MODE template argument; PMC="<counters>" overrides the default set).  Prints one JSON object (the
+# last line).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 TAG="$1"; VARS="$2"; WLS="$3"
 OUT="gpurun_out/$TAG"; mkdir -p "$OUT"
 for wl in ${WLS//,/ }; do
-  timeout -s KILL 300 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_VALU GRBM_GUI_ACTIVE \
+  timeout -s KILL 300 rocprofv3 --pmc ${PMC:-SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_VALU GRBM_GUI_ACTIVE} \
     -f csv -d "$OUT/$wl" -- python3 tools/ab_span.py "$VARS" "$wl" 1 > "$OUT/$wl.log" 2>&1
   rc=$?; echo "$wl rc=$rc"; [ $rc -eq 0 ] || { tail -5 "$OUT/$wl.log"; exit $rc; }
 done
