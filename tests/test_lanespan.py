@@ -193,3 +193,37 @@ def test_mixed_geometry_items():
             i0 = int(first[r])
             assert i0 <= r < i0 + int(cnt[r])
             assert lane[r] == int(k[64 * b + i0:64 * b + r].sum()) and lane[r] + kl[r] <= 64
+
+
+# round-4 diagnostics forms of the record kernel: 160 aligned b64 staging
+# pairs (MODE 19), 162 round-3 cross-lane tree (21), 163 sparse selects (22), 165 round-3 staging
+# addressing (27), 166 opaque base per chain (25), 167 one-compare selects (26), 168 finishing step in
+# the pre-shift (28), 169 bank-class slot rotation (29), 170 one-deep staging (30), 171 13 x 7-KiB
+# waves (31), 172 wave-mask selects (32)
+ROUND4_VARIANTS = [160, 162, 163, 165, 166, 167, 168, 169, 170, 171, 172]
+
+
+@pytest.mark.parametrize("hint", ["256", "512", "512m", "1023", "1023m", "1k"])
+def test_round4_record_variants_exact(crc, oracle_lib, hint):
+    """Every A/B form measured in round 4 is exact: spread, unsorted, duplicated and far records with
+    records outside the class among them (the slow path), against the oracle."""
+    import oracle
+    from pebblesdb_amd import diag
+
+    cls = CLASS[hint.rstrip("m")]
+    rng = np.random.Generator(np.random.PCG64(cls * 3 + len(hint)))
+    n = 3000
+    lens = rng.integers(1, cls + 1, size=n)
+    gaps = np.where(rng.random(n) < 0.8, 7, rng.integers(0, 3000, size=n))
+    offs = np.concatenate([[5], 5 + np.cumsum(lens + gaps)[:-1]])
+    out = rng.choice(n, size=40, replace=False)
+    lens[out] = rng.choice([0, cls + 1, 2000], size=40)
+    base = oracle.splitmix_bytes(int((offs + lens).max()) + 64, cls + 5)
+    blk = crc.make_blocks(offs, lens)
+    exp = oracle_lib.batch(base, blk, flags=1, nthreads=8)
+    d_base, d_blk = torch.from_numpy(base).cuda(), crc.blocks_to_device(blk)
+    flags = crc._SIZE_HINT[hint] | 1  # masked output, as crc.batch(masked=True)
+    for v in ROUND4_VARIANTS:
+        got = diag.batch_desc(v, d_base, d_blk, flags=flags).cpu().numpy().view(np.uint32)
+        bad = np.nonzero(got != exp)[0]
+        assert bad.size == 0, (hint, v, bad.size, int(lens[bad[0]]))
