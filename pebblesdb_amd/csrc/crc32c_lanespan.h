@@ -394,11 +394,15 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16, MODE == 31>::kWaves * 
   // (offset fields, some ds_read2_b32; +1.9-2.1 % on wal400 / wal1000 / wal in A/B,
   // profiles/r04/ab_variants_r04d.log; MODE 27 = the round-3 addressing)
   constexpr bool kOpaqueBase = MODE != 27 && MODE != 5 && MODE != 6 && MODE != 19;
-  constexpr bool kOneCmp = MODE == 26 || MODE == 32;
+  constexpr bool kOneCmp = MODE == 26 || MODE == 32 || MODE == 34;
   // kMaskSel (MODE 32): the p-word selects as wave masks -- per item one ballot per chain of the lanes
   // replacing in it, per step one ballot of the lanes replacing at that step; each select is then an
   // SALU and of the two masks and one v_cndmask (inverse ballot), 5 VALU per step instead of 8
-  constexpr bool kMaskSel = MODE == 32;
+  constexpr bool kMaskSel = MODE == 32 || MODE == 34;
+  // kNoG (the product since late round 4): the p-word selects on every lock-step step, branch-free,
+  // instead of only up to the item's last replacement step G behind a wave-uniform branch per step
+  // (+0.1-3 % in A/B, profiles/r04/ab/ab_nog.log; MODE 36 = the G-bounded form; 26 / 32 keep it too)
+  constexpr bool kNoG = MODE != 36 && MODE != 26 && MODE != 32;
   // kSparse: p-word selects only at the (chain, step) pairs some lane needs (MODE 22: slower)
   constexpr bool kSparse = MODE == 22;
   // kRot (MODE 29; the 33-word-part classes): the lock-step staging reads rotated over four chain
@@ -1002,7 +1006,7 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16, MODE == 31>::kWaves * 
           if ((selm >> (32 + t)) & 1u) xc = T + static_cast<int32_t>(2u * LC) == t ? pw : xc;
         }
         if (dd && ((selm >> (48 + t)) & 1u)) xd = T + static_cast<int32_t>(3u * LC) == t ? pw : xd;
-      } else if (kMaskSel && t <= G) {
+      } else if (kMaskSel && (kNoG || t <= G)) {
         const uint64_t hm = __ballot(tp == t);
         if (abc) {
           xa = __builtin_amdgcn_inverse_ballot_w64(hm & mA) ? pw : xa;
@@ -1018,7 +1022,7 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16, MODE == 31>::kWaves * 
           xc = hit && pC ? pw : xc;
         }
         if (dd) xd = hit && pD ? pw : xd;
-      } else if (MODE != 7 && t <= G) {
+      } else if (MODE != 7 && (kNoG || t <= G)) {
         if (abc) {
           xa = T == t ? pw : xa;
           xb = T + static_cast<int32_t>(LC) == t ? pw : xb;

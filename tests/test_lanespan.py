@@ -199,8 +199,9 @@ def test_mixed_geometry_items():
 # pairs (MODE 19), 162 round-3 cross-lane tree (21), 163 sparse selects (22), 165 round-3 staging
 # addressing (27), 166 opaque base per chain (25), 167 one-compare selects (26), 168 finishing step in
 # the pre-shift (28), 169 bank-class slot rotation (29), 170 one-deep staging (30), 171 13 x 7-KiB
-# waves (31), 172 wave-mask selects (32)
-ROUND4_VARIANTS = [160, 162, 163, 165, 166, 167, 168, 169, 170, 171, 172]
+# waves (31), 172 wave-mask selects (32), 174 / 175 branch-free selects (34 / 35), 176 the selects
+# bounded by the item's last replacement step (36, the product before late round 4)
+ROUND4_VARIANTS = [160, 162, 163, 165, 166, 167, 168, 169, 170, 171, 172, 174, 175, 176]
 
 
 @pytest.mark.parametrize("hint", ["256", "512", "512m", "1023", "1023m", "1k"])
