@@ -684,6 +684,11 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16, MODE == 31>::kWaves * 
   // non-temporal) from the item's uniform base, the descriptor's range check ending at its last
   // 16-B chunk: chunks past it read as zeros without touching memory (an empty item reads the
   // tables' first 16 B).  32-bit lane offsets, no per-chunk address arithmetic.
+  // kSkipWrites (the product since late round 4; MODE 39 = every chunk staged, before): the 1-KiB
+  // chunks wholly past the item's span + 64 B are not written to the region (the hash never reads
+  // them): +0.8 % on wal400, +2 % on random 300-500-B records, ±0.5 % elsewhere in A/B
+  // (profiles/r04/ab/ab_skiptail.log).  MODE 37 also skips their loads (no gain).
+  constexpr bool kSkipLoads = MODE == 37, kSkipWrites = MODE != 39;
   auto issue = [&](u32x4 (&A)[kSpanJ], const SpanItem& it) {
     const uint32_t lo_l = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(it.lo));
     const uint32_t lo_h = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(static_cast<uint64_t>(it.lo) >> 32));
@@ -692,16 +697,20 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16, MODE == 31>::kWaves * 
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(base, 0, static_cast<int>(nb), 0x00020000);
 #pragma unroll
     for (uint32_t j = 0; j < kSpanJ; ++j)
-      A[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, static_cast<int>(1024u * j + 16u * u), 0,
-                                                                              2 /* nt */));
+      if (!kSkipLoads || j == 0 || 1024u * j < nb + 64u)
+        A[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, static_cast<int>(1024u * j + 16u * u), 0,
+                                                                                2 /* nt */));
   };
   // every chunk is written, the dummy ones too: a load whose register is never read stays
   // outstanding, and the compiler then drains the counter before the register is reloaded
-  auto to_lds = [&](const u32x4 (&A)[kSpanJ]) {
+  auto to_lds = [&](const u32x4 (&A)[kSpanJ], const SpanItem& it) {
+    const uint32_t nw = __builtin_amdgcn_readfirstlane(it.hi) + 64u;  // (kSkipWrites: bytes the hash may read)
 #pragma unroll
-    for (uint32_t j = 0; j + 1 < kSpanJ; ++j) *reinterpret_cast<u32x4*>(region + 1024u * j + 16u * u) = A[j];
-    if (!kDyn || wv + 1u < kSpanWaves || u != 63u)  // the last 16 B of the LDS: the work counter
-      *reinterpret_cast<u32x4*>(region + 1024u * (kSpanJ - 1u) + 16u * u) = A[kSpanJ - 1u];
+    for (uint32_t j = 0; j + 1 < kSpanJ; ++j)
+      if (!kSkipWrites || j == 0 || 1024u * j < nw) *reinterpret_cast<u32x4*>(region + 1024u * j + 16u * u) = A[j];
+    if (!kSkipWrites || 1024u * (kSpanJ - 1u) < nw)
+      if (!kDyn || wv + 1u < kSpanWaves || u != 63u)  // the last 16 B of the LDS: the work counter
+        *reinterpret_cast<u32x4*>(region + 1024u * (kSpanJ - 1u) + 16u * u) = A[kSpanJ - 1u];
   };
   // hash an item staged in the region
   auto hash = [&](const SpanItem& it) {
@@ -1147,13 +1156,13 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16, MODE == 31>::kWaves * 
     u32x4 A[kSpanJ];
     SpanItem I0 = next_item(true);
     issue(A, I0);
-    to_lds(A);
+    to_lds(A, I0);
     while (I0.valid) {
       const SpanItem I1 = next_item(true);
       issue(A, I1);
       hash(I0);
       if (!I1.valid) break;
-      to_lds(A);
+      to_lds(A, I1);
       I0 = I1;
     }
   } else {
@@ -1162,18 +1171,18 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16, MODE == 31>::kWaves * 
   issue(A, I0);
   SpanItem I1 = next_item(I0.valid);
   issue(B, I1);
-  to_lds(A);
+  to_lds(A, I0);
   while (I0.valid) {
     const SpanItem I2 = next_item(I1.valid);
     issue(A, I2);
     hash(I0);
     if (!I1.valid) break;
-    to_lds(B);
+    to_lds(B, I1);
     const SpanItem I3 = next_item(I2.valid);
     issue(B, I3);
     hash(I1);
     if (!I2.valid) break;
-    to_lds(A);
+    to_lds(A, I2);
     I0 = I2;
     I1 = I3;
   }

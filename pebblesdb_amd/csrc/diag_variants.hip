@@ -1265,7 +1265,10 @@ hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tab
     case 172:    // exact: the p-word selects as wave masks (inverse ballot; MODE 32)
     case 174:    // exact: ... on every step, branch-free (MODE 34)
     case 175:    // exact: the plain selects on every step, branch-free (MODE 35; the product since late round 4)
-    case 176: {  // exact: the p-word selects only up to the item's last replacement step (MODE 36; before)
+    case 176:    // exact: the p-word selects only up to the item's last replacement step (MODE 36; before)
+    case 177:    // exact: chunks past the item's span neither loaded nor staged (MODE 37)
+    case 178:    // exact: ... not staged (MODE 38; the product since late round 4)
+    case 179: {  // exact: every chunk staged (MODE 39; before)
       const uint32_t cls = (flags & PDB_CRC_SIZE_256) ? 256u
                            : (flags & PDB_CRC_SIZE_512) ? 512u : ((flags & PDB_CRC_SIZE_1K) ? 1152u : 1023u);
       if (v == 118) launch_lanespan<DescSrc, OutSink, 10>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
@@ -1287,6 +1290,9 @@ hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tab
       else if (v == 174) launch_lanespan<DescSrc, OutSink, 34>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
       else if (v == 175) launch_lanespan<DescSrc, OutSink, 35>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
       else if (v == 176) launch_lanespan<DescSrc, OutSink, 36>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
+      else if (v == 177) launch_lanespan<DescSrc, OutSink, 37>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
+      else if (v == 178) launch_lanespan<DescSrc, OutSink, 38>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
+      else if (v == 179) launch_lanespan<DescSrc, OutSink, 39>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
       else if (v == 169) launch_lanespan<DescSrc, OutSink, 29>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
       else if (v == 166) launch_lanespan<DescSrc, OutSink, 25>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
       else launch_lanespan<DescSrc, OutSink, 18>(g, d_tables, src, nblk, cls, OutSink{out, 0u}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);

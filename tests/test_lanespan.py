@@ -200,8 +200,10 @@ def test_mixed_geometry_items():
 # addressing (27), 166 opaque base per chain (25), 167 one-compare selects (26), 168 finishing step in
 # the pre-shift (28), 169 bank-class slot rotation (29), 170 one-deep staging (30), 171 13 x 7-KiB
 # waves (31), 172 wave-mask selects (32), 174 / 175 branch-free selects (34 / 35), 176 the selects
-# bounded by the item's last replacement step (36, the product before late round 4)
-ROUND4_VARIANTS = [160, 162, 163, 165, 166, 167, 168, 169, 170, 171, 172, 174, 175, 176]
+# bounded by the item's last replacement step (36, the product before late round 4), 177 / 178 chunks
+# past the item's span not loaded and / or not staged (37 / 38, the latter the product since late
+# round 4), 179 every chunk staged (39)
+ROUND4_VARIANTS = [160, 162, 163, 165, 166, 167, 168, 169, 170, 171, 172, 174, 175, 176, 177, 178, 179]
 
 
 @pytest.mark.parametrize("hint", ["256", "512", "512m", "1023", "1023m", "1k"])
