@@ -57,21 +57,25 @@ def test_buffered_cpu_database_is_the_reference_format(tmp_path, oracle_lib):
 
 def test_fillrandom_only_run_exits_cleanly(tmp_path):
     """The teardown path of the harness: a fill-only run whose compactions are
-    still backed up when the benchmark ends -- `delete db` waits for the background threads --
-    exits 0 on both the CPU build and the buffered build."""
+    still backed up when the benchmark ends exits 0 on both the CPU build and the buffered build,
+    with the database closed (`--close_db=1`: `delete db` waits for the background threads) and left
+    open (the default)."""
     for name in ("pdb_dbbench_cpu", "pdb_dbbench_buffered_cpu"):
         exe = _exe(name)
         db = str(tmp_path / name)
-        rc, out, err = _run([exe, "--benchmarks=fillrandom", "--num=60000", "--value_size=1024", f"--db={db}"])
-        assert rc == 0, (name, out[-500:], err[-500:])
+        for close in (1, 0):
+            rc, out, err = _run([exe, "--benchmarks=fillrandom", "--num=60000", "--value_size=1024",
+                                 f"--close_db={close}", f"--db={db}_{close}"])
+            assert rc == 0, (name, close, out[-500:], err[-500:])
 
 
 def test_backed_up_fill_quiesces_before_delete(tmp_path):
     """The teardown fault: the reference engine's destructor can free the table
     cache while a flush or compaction still runs (the engine's own CPU build faults the same way,
     profiles/r04/teardown/).  The harness waits until the database directory has stopped changing
-    (--quiesce_ms) before `delete db`: a fill large enough to leave compactions backed up at the
-    end exits 0 on both CPU builds and reports the wait."""
+    (--quiesce_ms) and then, by default, exits with the database left open (crash-consistent): a
+    fill large enough to leave compactions backed up at the end exits 0 on both CPU builds, reports
+    the wait, and the engine as shipped reopens it (WAL replay) and finds every key."""
     for name in ("pdb_dbbench_cpu", "pdb_dbbench_buffered_cpu"):
         exe = _exe(name)
         db = str(tmp_path / name)
@@ -80,6 +84,12 @@ def test_backed_up_fill_quiesces_before_delete(tmp_path):
         assert rc == 0, (name, out[-500:], err[-800:])
         q = [l for l in err.splitlines() if l.startswith("quiesce: ")]
         assert len(q) == 1 and float(q[0].split()[1]) >= 0.5, err[-800:]
+        assert "teardown: skipped" in err, err[-800:]
+    cpu = _exe("pdb_dbbench_cpu")
+    rc, out, err = _run([cpu, "--use_existing_db=1", "--benchmarks=readrandom", "--num=300000", "--reads=20000",
+                         "--verify_checksums=1", f"--db={tmp_path / 'pdb_dbbench_buffered_cpu'}"],
+                        timeout=600)
+    assert rc == 0 and "(20000 of 20000 found)" in out, out[-500:] + err[-800:]
 
 
 def _damaged_db(tmp_path, cpu):
