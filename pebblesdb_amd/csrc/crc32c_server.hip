@@ -145,16 +145,19 @@ __global__ __launch_bounds__(64 * kServerWaves) void crc_server_kernel(const uin
   const ServerCtl* ctl = reinterpret_cast<const ServerCtl*>(in);
   uint64_t t_last = t0, serve_ticks = 0;
   uint32_t n_req = 0, n_poll = 0;
-  for (;;) {
-    const uint64_t rq = sys_load64(req + slot);
-    const uint64_t stop = sys_load64(&ctl->stop);
+  // Two polls in flight: the next poll's loads are issued before the current one is examined (the
+  // loop is unrolled over two register sets, so no copy of a result in flight forces a wait), and a
+  // request is seen about half a memory round trip sooner (a poll of fine-grained device memory is a
+  // full round trip).  A poll issued before an answer was posted still shows the answered seq, so it
+  // is never mistaken for a new request.
+  auto poll_step = [&](const uint64_t rq, const uint64_t stop) -> bool {  // true: leave
     ++n_poll;
     const uint32_t seq_l = static_cast<uint32_t>(rq >> 49);
     const uint64_t pend = __builtin_amdgcn_ballot_w64(u < kPer && seq_l != served);
     const bool closing = __hip_atomic_load(wg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0u;
     if (closing || __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(stop)) != static_cast<uint32_t>(stop0) ||
         __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(stop >> 32)) != static_cast<uint32_t>(stop0 >> 32))
-      break;
+      return true;
     const uint64_t now = __builtin_amdgcn_s_memrealtime();
     if (pend) {
       // no acquire fence: every load of the request bytes is system-coherent (sc0 sc1) and is
@@ -185,15 +188,29 @@ __global__ __launch_bounds__(64 * kServerWaves) void crc_server_kernel(const uin
       if (u == 0) *reinterpret_cast<uint64_t*>(wg + 4) = now;  // any wave's request keeps all alive
       ++n_req;
       serve_ticks += __builtin_amdgcn_s_memrealtime() - now;
-      continue;
+      return false;
     }
-    const uint64_t last = *reinterpret_cast<volatile uint64_t*>(wg + 4);
-    const uint64_t seen = last > t_last ? last : t_last;
-    if (now - seen > idle_ticks || now - t0 > life_ticks) {
-      if (u == 0) __hip_atomic_store(wg, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      break;
+    // idle: the workgroup's last-request tick is read only once this wave's own is older than the
+    // idle limit (a read of it on every poll made the compiler drain the polls in flight)
+    if (now - t_last > idle_ticks || now - t0 > life_ticks) {
+      const uint64_t last = __hip_atomic_load(reinterpret_cast<uint64_t*>(wg + 4), __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (last > t_last) t_last = last;  // another wave served since
+      if (now - t_last > idle_ticks || now - t0 > life_ticks) {
+        if (u == 0) __hip_atomic_store(wg, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return true;
+      }
     }
     __builtin_amdgcn_s_sleep(2);
+    return false;
+  };
+  uint64_t rqA = sys_load64(req + slot), stA = sys_load64(&ctl->stop);
+  for (;;) {
+    const uint64_t rqB = sys_load64(req + slot), stB = sys_load64(&ctl->stop);
+    if (poll_step(rqA, stA)) break;
+    rqA = sys_load64(req + slot);
+    stA = sys_load64(&ctl->stop);
+    if (poll_step(rqB, stB)) break;
   }
   // the last wave out publishes the exit (and the counters)
   uint32_t out_before = 0;
