@@ -42,7 +42,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=40)
     ap.add_argument("--settle", type=int, default=300,
                     help="untimed launches after the timed region before the steady-state re-timing (0: skip)")
-    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "sstable", "sst_verify", "sst_seal", "sst_seal2", "sst_crc",
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "sstable", "sst_verify", "sst_seal", "sst_crc",
                                                         "wal", "wal100", "wal400", "wal1000"],
                     help="c2 (default, the headline) / c3: BASELINE configs; sstable: the C2 blocks in "
                          "sstable layout; sst_verify / sst_seal: SURVEY §8(f) rows 1-2 on a device sstable "
@@ -53,6 +53,9 @@ def parse():
     ap.add_argument("--c3-bytes", type=int, default=16 << 30, help="bytes per GPU for c3 (Zipf)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-copy-inclusive", action="store_true")
+    ap.add_argument("--no-c4-shard", action="store_true",
+                    help="skip the N = 1 line's c4_shard key (one 16 GiB config-4 shard, the 1 -> 8 GPU curve's "
+                         "equal-shard anchor)")
     ap.add_argument("--diag", action="store_true", help="also time the read-stream calibration kernels")
     ap.add_argument("--no-ceiling", action="store_true",
                     help="skip the hash-free pattern-ceiling kernels timed after the timed region (pattern_ceiling)")
@@ -127,6 +130,11 @@ def resolve_nblk(args, world: int) -> bool:
     return False
 
 
+def wants_c4_shard(args, world: int, c4: bool) -> bool:
+    """The N = 1 default line (c2, C2 size) carries the c4_shard anchor; N > 1 lines are c4 shards."""
+    return world == 1 and args.workload == "c2" and not c4 and not args.no_c4_shard
+
+
 def dry_run_main(args, world: int, rank: int) -> None:
     """The multi-rank plumbing of main() with no device: gloo process group, rank 0's index
     scatter, barrier-bracketed (empty) timed region with max-over-ranks time, per-rank row
@@ -151,15 +159,18 @@ def dry_run_main(args, world: int, rank: int) -> None:
     t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
     if distributed:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    rows = gather_rank_rows([rank, -1, -1, (hi - lo) * 4096, 0, 0], world, cpu, dist if distributed else None)
+    rows = gather_rank_rows([rank, -1, -1, (hi - lo) * 4096, 0, 0, -1], world, cpu, dist if distributed else None)
     if rank == 0:
-        print(json.dumps({"metric": METRIC, "value": None, "unit": "GiB/s", "n_gpus": world, "world_size": world,
-                          "steps": args.steps, "warmup": args.warmup, "dry_run": True,
-                          "config": {"workload": "dry run (launcher plumbing only, no device)" +
-                                                 (" of the c4 shards" if c4 else ""),
-                                     "blocks_per_gpu": args.nblk},
-                          "ranks": [{"rank": r[0], "blocks": r[3] // 4096} for r in rows],
-                          "region_s_max": float(t.item())}), flush=True)
+        line = {"metric": METRIC, "value": None, "unit": "GiB/s", "n_gpus": world, "world_size": world,
+                "steps": args.steps, "warmup": args.warmup, "dry_run": True,
+                "config": {"workload": "dry run (launcher plumbing only, no device)" + (" of the c4 shards" if c4 else ""),
+                           "blocks_per_gpu": args.nblk},
+                "ranks": [{"rank": r[0], "blocks": r[3] // 4096, "steady_kernel_avg_ms": None} for r in rows],
+                "steady_state": ({"over_ranks": {"ranks": len(rows)}} if world > 1 and args.settle > 0 else None),
+                "region_s_max": float(t.item())}
+        if wants_c4_shard(args, world, c4):
+            line["c4_shard"] = {"blocks": C4_BLOCKS_PER_GPU, "bytes": C4_BLOCKS_PER_GPU * 4096, "dry_run": True}
+        print(json.dumps(line), flush=True)
     if distributed:
         dist.destroy_process_group()
 
@@ -236,7 +247,7 @@ def main():
     import torch.distributed as dist
 
     from pebblesdb_amd import crc32c, diag
-    from pebblesdb_amd.shard import scatter_block_ranges
+    from pebblesdb_amd.shard import scatter_block_lens, scatter_block_ranges
 
     ndev = torch.cuda.device_count()  # counting devices does not initialise HIP
     if ndev < 1:
@@ -262,10 +273,11 @@ def main():
     # ---- the rank's shard index: scattered from rank 0 over RCCL (the only collective) -------
     c3_sizes = None
     if args.workload == "c3":
-        # ONE Zipf 1-64 KiB list of world x c3_bytes (seed 301), split into contiguous ranges of
-        # ~equal BYTES by rank 0 (shard.byte_balanced_ranges) and broadcast: weak scaling by bytes
-        c3_sizes = c3_plan(args.c3_bytes, world)
-        lo, hi = scatter_block_ranges(len(c3_sizes), world, rank, cdev, dist if distributed else None, lens=c3_sizes)
+        # ONE Zipf 1-64 KiB list of world x c3_bytes (seed 301), built by rank 0 alone and split into
+        # contiguous ranges of ~equal BYTES (shard.byte_balanced_ranges); each rank receives its range
+        # and its own block lengths by scatter: weak scaling by bytes
+        lo, hi, c3_sizes = scatter_block_lens(c3_plan(args.c3_bytes, world) if rank == 0 else None, world, rank, cdev,
+                                              dist if distributed else None)
     else:
         lo, hi = scatter_block_ranges(args.nblk * world, world, rank, cdev, dist if distributed else None)
 
@@ -301,7 +313,7 @@ def main():
 
         workload = {"workload": "sstable layout: 4096 B contents + type byte, stride 4101 (unaligned)",
                     "block_bytes": L, "blocks_per_gpu": nblk, "bytes_per_gpu": hashed}
-    elif args.workload in ("sst_verify", "sst_seal", "sst_seal2", "sst_crc"):
+    elif args.workload in ("sst_verify", "sst_seal", "sst_crc"):
         # sstable image: contents of 4166..4174 B (db_bench data blocks flush just past the 4-KiB
         # block_size: 4171-4175 B with the type byte), type 0, 5-B trailer
         from pebblesdb_amd import table as T
@@ -334,19 +346,12 @@ def main():
 
             def step():
                 check(lib().pdb_sst_crc_device(data.data_ptr(), total, d_h.data_ptr(), nblk, out.data_ptr(), sp))
-        elif args.workload == "sst_seal2":  # the two-launch seal: compact words, then the trailer scatter
-            scratch = torch.empty(nblk, dtype=torch.int32, device=dev)
-
-            def step():
-                check(lib().pdb_sst_seal_device_scratch(data.data_ptr(), total, d_h.data_ptr(), nblk,
-                                                        scratch.data_ptr(), nblk, sp))
         else:
             def step():
                 check(lib().pdb_sst_seal_device(data.data_ptr(), total, d_h.data_ptr(), nblk, sp))
 
         workload = {"workload": f"{args.workload}: sstable image in HBM, 1M blocks of 4166-4174 B + type + "
                                 "5-B trailer, " + {"sst_verify": "pdb_sst_verify_device", "sst_seal": "pdb_sst_seal_device",
-                                                   "sst_seal2": "pdb_sst_seal_device_scratch (two launches)",
                                                    "sst_crc": "pdb_sst_crc_device"}[args.workload],
                     "blocks_per_gpu": nblk, "bytes_per_gpu": hashed}
     elif args.workload in ("wal", "wal100", "wal400", "wal1000"):
@@ -382,7 +387,7 @@ def main():
                     "blocks_per_gpu": nblk, "bytes_per_gpu": hashed}
     else:
         # c3: Zipf 1..64 KiB blocks packed back to back, this rank's byte-balanced range of the list
-        sizes = c3_sizes[lo:hi]
+        sizes = c3_sizes
         n = len(sizes)
         offs = np.concatenate([[0], np.cumsum(sizes)[:-1]])
         total = int(sizes.sum())
@@ -403,7 +408,7 @@ def main():
     algo_bytes = hashed + 4 * nblk + (16 * nblk if args.workload in ("c3", "wal", "wal100", "wal400", "wal1000") else 0)
     if args.workload == "sst_verify":  # + the 4-B stored trailer read, 16-B handle, 1-B ok written
         algo_bytes = hashed + nblk * (4 + 16 + 1)
-    elif args.workload in ("sst_seal", "sst_seal2", "sst_crc"):  # + 4-B trailer / CRC written, 16-B handle
+    elif args.workload in ("sst_seal", "sst_crc"):  # + 4-B trailer / CRC written, 16-B handle
         algo_bytes = hashed + nblk * (4 + 16)
 
     # ---- warmup + timed region -------------------------------------------------------------
@@ -444,33 +449,36 @@ def main():
     # clock for the first ~100 launches on a cold GPU (sclk 2.41 -> ~2.05 GHz as board power climbs,
     # then recovers), so K launches after W = 5 warmups catch the transient.  This
     # re-times K launches after `--settle` more untimed ones, on this rank alone.
+    # Every rank measures its own steady state; the N > 1 line reports the min and max over ranks.
     steady = None
-    if args.settle > 0:
-        for _ in range(args.settle):
-            step()
-        se = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-        for s_, e_ in se:
-            s_.record(stream)
-            step()
-            e_.record(stream)
-        torch.cuda.synchronize()
-        st_ms = float(np.mean([s_.elapsed_time(e_) for s_, e_ in se]))
-        steady = {"settle_launches": args.settle, "kernel_avg_ms": round(st_ms, 4),
-                  "GiB_s_per_gpu": round(hashed / (st_ms * 1e-3) / GIB, 3),
-                  "frac": round(algo_bytes / (st_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    st_ms = steady_ms(torch, step, stream, args.settle, args.steps) if args.settle > 0 else None
 
     # per-rank facts (outside the timed region) gathered to rank 0: device, bytes hashed, kernel
-    # time, checksum of checksums -- the SCALE record shows which GPUs RCCL actually saw
+    # time, checksum of checksums, steady-state kernel time -- the SCALE record shows which GPUs
+    # RCCL actually saw
     props = torch.cuda.get_device_properties(gpu)
     pci = int(getattr(props, "pci_bus_id", -1))
     xor_local = int(np.bitwise_xor.reduce(out.cpu().numpy().view(np.uint32)))
-    rows = gather_rank_rows([rank, gpu, pci, hashed, int(kern_avg_ms * 1e6), xor_local], world, cdev,
+    rows = gather_rank_rows([rank, gpu, pci, hashed, int(kern_avg_ms * 1e6), xor_local,
+                             int(st_ms * 1e6) if st_ms is not None else -1], world, cdev,
                             dist if distributed else None)
     xor_all = 0
     for r in rows:
         xor_all ^= r[5]
-    ranks = [{"rank": r[0], "device": r[1], "pci_bus_id": r[2], "bytes": r[3], "kernel_avg_ms": round(r[4] / 1e6, 4)}
-             for r in rows]
+    ranks = [{"rank": r[0], "device": r[1], "pci_bus_id": r[2], "bytes": r[3], "kernel_avg_ms": round(r[4] / 1e6, 4),
+              "steady_kernel_avg_ms": round(r[6] / 1e6, 4) if r[6] >= 0 else None} for r in rows]
+    if st_ms is not None:
+        steady = {"settle_launches": args.settle, "kernel_avg_ms": round(st_ms, 4),
+                  "GiB_s_per_gpu": round(hashed / (st_ms * 1e-3) / GIB, 3),
+                  "frac": round(algo_bytes / (st_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+        if world > 1:  # every rank's steady state: the slowest and fastest GPU of the node
+            per = [(r[3], r[6] / 1e6) for r in rows]
+            fr = [algo_bytes * (b / hashed) / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS for b, ms in per]
+            steady["over_ranks"] = {"kernel_avg_ms_min": round(min(ms for _, ms in per), 4),
+                                    "kernel_avg_ms_max": round(max(ms for _, ms in per), 4),
+                                    "frac_min": round(min(fr), 4), "frac_max": round(max(fr), 4),
+                                    "GiB_s_total_at_slowest": round(sum(b for b, _ in per) / (max(ms for _, ms in per) * 1e-3)
+                                                                    / GIB, 3)}
 
     total_bytes = sum(r[3] for r in rows) * args.steps  # weak scaling: every rank hashes its own shard
     value = total_bytes / wall_max / GIB
@@ -499,6 +507,8 @@ def main():
                                    d_blk if args.workload in ("c3", "wal", "wal100", "wal400", "wal1000") else None)
             else:  # sst_verify / sst_seal: the reference's CRC over each block's contents || type
                 cpu = cpu_baseline(data, L, stride, nblk, args, cpu_blk)
+        if wants_c4_shard(args, world, c4):
+            extra["c4_shard"] = c4_shard(torch, crc32c, diag, dev, stream, args)
 
     if rank == 0:
         traffic = pmc_traffic(args.workload)
@@ -539,8 +549,6 @@ def main():
                            "wal1000": "crc_lanespan_kernel<DescSrc,OutSink,1023>",
                            "sst_verify": "crc_sst4k_kernel<SstSrc,SstVerifySink,nt,QuadTabs>",
                            "sst_seal": "crc_sst4k_kernel<SstSrc,ParkSealSink<64>,nt,QuadTabs>",
-                           "sst_seal2": "crc_sst4k_kernel<SstSrc,SstCrcSink,nt,QuadTabs,12 waves> + sst_trailer_scatter_kernel "
-                                        "(two launches per step)",
                            "sst_crc": "crc_sst4k_kernel<SstSrc,SstCrcSink,nt,QuadTabs>"}[args.workload],
                 "algorithmic_bytes_per_launch": algo_bytes,
                 "kernel_avg_ms": round(kern_avg_ms, 4),
@@ -556,6 +564,68 @@ def main():
         print(json.dumps(line), flush=True)
     if distributed:
         dist.destroy_process_group()
+
+
+def steady_ms(torch, step, stream, settle: int, steps: int) -> float:
+    """Mean per-launch kernel time (HIP events around every launch) of `steps` launches after
+    `settle` untimed ones: the rate a sustained stream of batches gets."""
+    for _ in range(settle):
+        step()
+    se = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    for s_, e_ in se:
+        s_.record(stream)
+        step()
+        e_.record(stream)
+    torch.cuda.synchronize()
+    return float(np.mean([s_.elapsed_time(e_) for s_, e_ in se]))
+
+
+C4_IDLE_S = 3.0
+
+
+def c4_shard(torch, crc32c, diag, dev, stream, args) -> dict:
+    """The equal-shard anchor of the 1 -> 8 GPU curve, at N = 1 and outside `value`: one 16 GiB
+    shard of BASELINE config 4 (rank 0's 4 194 304 x 4 KiB blocks of the global splitmix image, what
+    every rank of an N > 1 run hashes), timed exactly as the N > 1 runs time theirs -- W warmups,
+    then K launches in one event pair -- after C4_IDLE_S s of idle GPU, so it starts from the same
+    cold power state as a fresh N > 1 process, then its own steady state."""
+    nblk = C4_BLOCKS_PER_GPU
+    data = torch.empty(nblk * 4096, dtype=torch.uint8, device=dev)
+    diag.fill_splitmix(data, 301, byte_offset=0)
+    out = torch.empty(nblk, dtype=torch.int32, device=dev)
+
+    def step():
+        crc32c.batch_fixed(data, 4096, 4096, nblk, out=out)
+
+    torch.cuda.synchronize()
+    time.sleep(C4_IDLE_S)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(args.steps):
+        step()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    kern = e0.elapsed_time(e1) / args.steps
+    xor = int(np.bitwise_xor.reduce(out.cpu().numpy().view(np.uint32)))
+    algo = nblk * 4100
+    res = {"workload": "c4 shard: 4M x 4 KiB blocks = 16 GiB (rank 0's shard of BASELINE config 4), stride 4096, "
+                       "device-resident, after %.0f s idle" % C4_IDLE_S,
+           "blocks": nblk, "bytes": nblk * 4096, "steps": args.steps, "warmup": args.warmup,
+           "GiB_s": round(nblk * 4096 * args.steps / wall / GIB, 3), "ms_per_step": round(wall / args.steps * 1e3, 4),
+           "kernel_avg_ms": round(kern, 4), "frac": round(algo / (kern * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "xor_of_crcs": f"{xor:08x}"}
+    if args.settle > 0:
+        st = steady_ms(torch, step, stream, args.settle, args.steps)
+        res["steady_state"] = {"settle_launches": args.settle, "kernel_avg_ms": round(st, 4),
+                               "frac": round(algo / (st * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    del data, out
+    torch.cuda.empty_cache()
+    return res
 
 
 def pattern_ceiling(torch, workload, data, stream, algo_bytes, nblk, d_h=None, d_blk=None, hint=None, reseal=None):
@@ -587,10 +657,10 @@ def pattern_ceiling(torch, workload, data, stream, algo_bytes, nblk, d_h=None, d
         d_hs = T.handles_to_device(hs, data.device)
         runs.append(("seal_pattern_kernel<0> (variant 140: loads only) over the stride-4101 blocks",
                      lambda: diag.sst(140, data, d_hs, seal=True, stream=stream)))
-    elif workload in ("sst_verify", "sst_crc", "sst_seal", "sst_seal2"):
+    elif workload in ("sst_verify", "sst_crc", "sst_seal"):
         runs.append(("seal_pattern_kernel<0> (variant 140: loads only)",
                      lambda: diag.sst(140, data, d_h, seal=True, stream=stream)))
-        if workload in ("sst_seal", "sst_seal2"):
+        if workload == "sst_seal":
             runs.append(("seal_pattern_kernel<1> (variant 141: loads + in-place trailer stores)",
                          lambda: diag.sst(141, data, d_h, seal=True, stream=stream)))
     elif workload.startswith("wal"):
@@ -612,7 +682,7 @@ def pattern_ceiling(torch, workload, data, stream, algo_bytes, nblk, d_h=None, d
         ms = s.elapsed_time(e) / 10
         gbs = algo_bytes / (ms * 1e-3) / 1e9
         res[name] = {"ms": round(ms, 4), "GB/s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
-    if workload in ("sst_seal", "sst_seal2") and reseal is not None:  # the calibration wrote wrong trailers
+    if workload == "sst_seal" and reseal is not None:  # the calibration wrote wrong trailers
         reseal()
         torch.cuda.synchronize()
     return res

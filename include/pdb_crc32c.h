@@ -146,13 +146,6 @@ int64_t pdb_crc32c_verify_host(const void* base, uint64_t base_len, const pdb_bl
 int pdb_sst_seal_device(void* d_buf, uint64_t buf_len, const pdb_block_handle* d_h, uint64_t n,
                         void* stream);
 int pdb_sst_seal_host(void* buf, uint64_t buf_len, const pdb_block_handle* h, uint64_t n);
-/* The same seal in two launches, for a caller that lends n words of device scratch (the device API
- * allocates nothing): launch 1 writes the trailer words into d_scratch (pdb_sst_crc_device's
- * kernel, no stores into the image while it streams it), launch 2 scatters them into the trailers
- * once every block has been read.  Same image as pdb_sst_seal_device, byte for byte.
- * scratch_words >= n. */
-int pdb_sst_seal_device_scratch(void* d_buf, uint64_t buf_len, const pdb_block_handle* d_h, uint64_t n,
-                                uint32_t* d_scratch, uint64_t scratch_words, void* stream);
 /* The seal's trailer words without writing them: d_out[i] = Mask(crc32c(contents||type)) (the
  * value WriteRawBlock encodes at offset+size+1), for an engine that writes the trailer while it
  * copies blocks out -- the in-place seal pays for scattered 4-B writes, this form does not.  A

@@ -58,7 +58,6 @@ SIGNATURES = {
     "pdb_sst_verify_host": (ctypes.c_int64, [_V, _U64, _V, _U64, _V]),
     "pdb_sst_verify_device": (_I, [_V, _U64, _V, _U64, _V, _V, _V]),
     "pdb_sst_crc_device": (_I, [_V, _U64, _V, _U64, _V, _V]),
-    "pdb_sst_seal_device_scratch": (_I, [_V, _U64, _V, _U64, _V, _U64, _V]),
 }
 
 

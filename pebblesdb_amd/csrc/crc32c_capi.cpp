@@ -44,8 +44,11 @@ struct HostCtx {
   hipEvent_t drained[2] = {};         // group in workspace slot k hashed and its results copied out
   uint8_t* d_ws = nullptr;
   size_t ws_cap = 0;
+  uint32_t* wq = nullptr;  // the record kernel's work-queue words for `stream` (kWqBytes, zeroed)
 };
 constexpr int kHostCtx = 4;
+// crc_lanespan_kernel's work queues: 8 queue words + the exit count, each on its own 128-B line
+constexpr size_t kWqBytes = 9 * 128;
 
 // One scalar-service request slot (crc32c_server.hip): its request sequence number, guarded by mu
 // (a slot is shared only when more threads than slots call at once).
@@ -64,6 +67,10 @@ struct DevState {
   // while batches run
   LaunchGeom hgeom{255, 1024};
   HostCtx ctx[kHostCtx];
+  // the device entry points' work-queue words, one set per caller stream (geom_on): launches on one
+  // stream are ordered, so each set is zero again when its next launch starts
+  std::mutex wq_mu;
+  std::vector<std::pair<hipStream_t, uint32_t*>> wqs;
   std::mutex mu;  // the launch-per-call scalar modes' staging below
   // scalar Extend: pinned, device-mapped staging ([256-B result area][bytes]); the kernels read
   // the bytes across PCIe and write the CRC back into it, so a call is memcpy + launch(es) + sync
@@ -194,6 +201,8 @@ int get_state(DevState** out) {
   for (HostCtx& c : s->ctx) {
     e = hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking);
     if (e != hipSuccess) return hip_fail(e, "hipStreamCreate");
+    if ((e = hipMalloc(&c.wq, kWqBytes)) != hipSuccess) return hip_fail(e, "hipMalloc(work queues)");
+    if ((e = hipMemset(c.wq, 0, kWqBytes)) != hipSuccess) return hip_fail(e, "hipMemset(work queues)");
     e = hipStreamCreateWithFlags(&c.copy_stream, hipStreamNonBlocking);
     if (e != hipSuccess) return hip_fail(e, "hipStreamCreate(copy)");
     for (int k = 0; k < 2; ++k) {
@@ -212,6 +221,26 @@ int get_state(DevState** out) {
 hipStream_t pick_stream(DevState* st, void* stream) {
   (void)st;
   return static_cast<hipStream_t>(stream);
+}
+
+// The launch geometry for a device entry point on stream `s`: st->geom with that stream's
+// work-queue words (allocated and zeroed on the stream's first call; launches on one stream are
+// ordered, and every record-kernel launch leaves its words zero).
+int geom_on(DevState* st, hipStream_t s, LaunchGeom* g) {
+  *g = st->geom;
+  std::lock_guard<std::mutex> lk(st->wq_mu);
+  for (auto& w : st->wqs)
+    if (w.first == s) {
+      g->wq = w.second;
+      return PDB_OK;
+    }
+  uint32_t* wq = nullptr;
+  hipError_t e = hipMalloc(&wq, kWqBytes);
+  if (e != hipSuccess) return hip_fail(e, "hipMalloc(work queues)");
+  if ((e = hipMemset(wq, 0, kWqBytes)) != hipSuccess) return hip_fail(e, "hipMemset(work queues)");
+  st->wqs.emplace_back(s, wq);
+  g->wq = wq;
+  return PDB_OK;
 }
 
 int ensure_ws(HostCtx* c, size_t bytes) {
@@ -638,6 +667,8 @@ int host_desc(const uint8_t* base, uint64_t base_len, const pdb_blk* blk, uint64
   if (rc) return rc;
   CtxLock cl(dev);
   HostCtx* st = cl.c;
+  LaunchGeom hgeom = dev->hgeom;
+  hgeom.wq = st->wq;
   hipError_t e = hipSetDevice(dev->device);
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
   if ((rc = ensure_ws(st, nslots * slot_bytes + 256))) return rc;
@@ -665,7 +696,7 @@ int host_desc(const uint8_t* base, uint64_t base_len, const pdb_blk* blk, uint64
           (e = hipMemcpyAsync(ws + off_exp, expected + x.first, x.count * 4, hipMemcpyHostToDevice, cs)) != hipSuccess)
         return hip_fail(e, "hipMemcpyAsync(expected)");
       if ((e = pipe.end_copies(k)) != hipSuccess) return hip_fail(e, "hipEventRecord(staged)");
-      e = launch_desc(dev->hgeom, dev->d_tables, ws, reinterpret_cast<const pdb_blk*>(ws + off_desc), x.count, flags,
+      e = launch_desc(hgeom, dev->d_tables, ws, reinterpret_cast<const pdb_blk*>(ws + off_desc), x.count, flags,
                       mode, reinterpret_cast<const uint32_t*>(ws + off_exp), reinterpret_cast<uint32_t*>(ws + off_out),
                       ws + off_ok, d_nbad, s);
       if (e != hipSuccess) return hip_fail(e, "launch_desc");
@@ -716,7 +747,9 @@ int host_scalar(uint32_t init, const uint8_t* data, uint64_t n, uint32_t* out) {
     // end-of-kernel signal.  A CRC equal to the sentinel just falls through to the stream sync.
     const uint32_t sentinel = st->seq++ * 0x9E3779B9u ^ 0x5A5A5A5Au;
     *h_res = sentinel;
-    e = launch_fixed(st->hgeom, st->d_tables, st->d_stage + kStageHdr, 0, static_cast<uint32_t>(n), 1,
+    LaunchGeom hgeom = st->hgeom;
+    hgeom.wq = cl.c->wq;
+    e = launch_fixed(hgeom, st->d_tables, st->d_stage + kStageHdr, 0, static_cast<uint32_t>(n), 1,
                      PDB_CRC_USE_INIT, init, d_res, s);
     if (e != hipSuccess) return hip_fail(e, "launch_fixed(scalar)");
     if (st->scalar_mode == kScalarPoll) {
@@ -814,6 +847,8 @@ int host_sst(uint8_t* buf, uint64_t buf_len, const pdb_block_handle* h, uint64_t
   if (rc) return rc;
   CtxLock cl(dev);
   HostCtx* st = cl.c;
+  LaunchGeom hgeom = dev->hgeom;
+  hgeom.wq = st->wq;
   hipError_t e = hipSetDevice(dev->device);
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
   if ((rc = ensure_ws(st, nslots * slot_bytes + 256))) return rc;
@@ -844,12 +879,12 @@ int host_sst(uint8_t* buf, uint64_t buf_len, const pdb_block_handle* h, uint64_t
       const pdb_block_handle* d_h = reinterpret_cast<const pdb_block_handle*>(ws + off_h);
       if (seal) {
         uint32_t* d_crc = reinterpret_cast<uint32_t*>(ws + off_ok);
-        if ((e = launch_sst_masked(dev->hgeom, dev->d_tables, ws, x.hi - x.lo, d_h, x.count, d_crc, s)) != hipSuccess)
+        if ((e = launch_sst_masked(hgeom, dev->d_tables, ws, x.hi - x.lo, d_h, x.count, d_crc, s)) != hipSuccess)
           return hip_fail(e, "launch_sst_masked");
         if ((e = hipMemcpyAsync(crc.data() + x.first, d_crc, x.count * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
           return hip_fail(e, "hipMemcpyAsync(crcs)");
       } else {
-        if ((e = launch_sst(dev->hgeom, dev->d_tables, ws, x.hi - x.lo, d_h, x.count, false, ws + off_ok, d_nbad, s)) !=
+        if ((e = launch_sst(hgeom, dev->d_tables, ws, x.hi - x.lo, d_h, x.count, false, ws + off_ok, d_nbad, s)) !=
             hipSuccess)
           return hip_fail(e, "launch_sst");
         if (ok && (e = hipMemcpyAsync(ok + x.first, ws + off_ok, x.count, hipMemcpyDeviceToHost, s)) != hipSuccess)
@@ -944,7 +979,9 @@ int pdb_crc32c_batch_device_fixed(const void* d_base, uint64_t stride, uint32_t 
   int rc = get_state(&st);
   if (rc) return rc;
   if ((rc = quiesce(st))) return rc;
-  hipError_t e = launch_fixed(st->geom, st->d_tables, static_cast<const uint8_t*>(d_base), stride, len,
+  LaunchGeom g;
+  if ((rc = geom_on(st, pick_stream(st, stream), &g))) return rc;
+  hipError_t e = launch_fixed(g, st->d_tables, static_cast<const uint8_t*>(d_base), stride, len,
                               nblk, flags, init, d_out, pick_stream(st, stream));
   return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_fixed");
 }
@@ -957,7 +994,9 @@ int pdb_crc32c_batch_device(const void* d_base, const pdb_blk* d_blk, uint64_t n
   int rc = get_state(&st);
   if (rc) return rc;
   if ((rc = quiesce(st))) return rc;
-  hipError_t e = launch_desc(st->geom, st->d_tables, static_cast<const uint8_t*>(d_base), d_blk, nblk,
+  LaunchGeom g;
+  if ((rc = geom_on(st, pick_stream(st, stream), &g))) return rc;
+  hipError_t e = launch_desc(g, st->d_tables, static_cast<const uint8_t*>(d_base), d_blk, nblk,
                              flags, kModeOut, nullptr, d_out, nullptr, nullptr, pick_stream(st, stream));
   return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_desc");
 }
@@ -971,7 +1010,9 @@ int pdb_crc32c_verify_device(const void* d_base, const pdb_blk* d_blk, uint64_t 
   int rc = get_state(&st);
   if (rc) return rc;
   if ((rc = quiesce(st))) return rc;
-  hipError_t e = launch_desc(st->geom, st->d_tables, static_cast<const uint8_t*>(d_base), d_blk, nblk,
+  LaunchGeom g;
+  if ((rc = geom_on(st, pick_stream(st, stream), &g))) return rc;
+  hipError_t e = launch_desc(g, st->d_tables, static_cast<const uint8_t*>(d_base), d_blk, nblk,
                              flags, kModeVerify, d_expected, nullptr, d_ok, d_nbad,
                              pick_stream(st, stream));
   return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_desc(verify)");
@@ -1007,21 +1048,6 @@ int pdb_sst_seal_device(void* d_buf, uint64_t buf_len, const pdb_block_handle* d
   hipError_t e = launch_sst(st->geom, st->d_tables, static_cast<uint8_t*>(d_buf), buf_len, d_h, n, true,
                             nullptr, nullptr, pick_stream(st, stream));
   return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_sst(seal)");
-}
-
-int pdb_sst_seal_device_scratch(void* d_buf, uint64_t buf_len, const pdb_block_handle* d_h, uint64_t n,
-                                uint32_t* d_scratch, uint64_t scratch_words, void* stream) {
-  if (n == 0) return PDB_OK;
-  if (!d_buf || !d_h || !d_scratch) return fail(PDB_EINVAL, "null argument");
-  if (scratch_words < n) return fail(PDB_EINVAL, "scratch smaller than one word per block");
-  if (buf_len < 5) return fail(PDB_ERANGE, "buffer smaller than one block trailer");
-  DevState* st;
-  int rc = get_state(&st);
-  if (rc) return rc;
-  if ((rc = quiesce(st))) return rc;
-  hipError_t e = launch_sst_seal2(st->geom, st->d_tables, static_cast<uint8_t*>(d_buf), buf_len, d_h, n, d_scratch,
-                                  pick_stream(st, stream));
-  return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_sst_seal2");
 }
 
 int pdb_sst_verify_device(const void* d_buf, uint64_t buf_len, const pdb_block_handle* d_h,

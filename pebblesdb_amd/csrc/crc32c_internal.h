@@ -24,6 +24,9 @@ enum DescMode : int {
 struct LaunchGeom {
   uint32_t grid;   // workgroups (one per CU: the LDS image is ~156 KiB)
   uint32_t block;  // threads per workgroup
+  // the launch stream's work-queue words (crc_lanespan_kernel: 9 words on 128-B lines, zero between
+  // launches; DevState::wq_for) -- null where the caller has none (no record-kernel launch then)
+  uint32_t* wq = nullptr;
 };
 
 // crc32c_kernels.hip -- all launches are asynchronous on `s`.
@@ -40,10 +43,6 @@ hipError_t launch_sst(const LaunchGeom& g, const uint32_t* d_tables, uint8_t* bu
 // out[i] = Mask(crc32c(contents_i || type_i)) -- the trailer word a seal writes, as an array.
 hipError_t launch_sst_masked(const LaunchGeom& g, const uint32_t* d_tables, uint8_t* buf, uint64_t buf_len,
                              const pdb_block_handle* h, uint64_t n, uint32_t* out, hipStream_t s);
-// The two-launch in-place seal: launch_sst_masked into `scratch` (n words), then one scatter of
-// the trailer words into the image (pdb_sst_seal_device_scratch).
-hipError_t launch_sst_seal2(const LaunchGeom& g, const uint32_t* d_tables, uint8_t* buf, uint64_t buf_len,
-                            const pdb_block_handle* h, uint64_t n, uint32_t* scratch, hipStream_t s);
 // Long span: raw CRCs of `nseg` segments of 2^seg_log2 bytes (+ the tail) in parallel, then a
 // one-workgroup tree combine with the power-of-two operators.  `scratch` holds
 // span_scratch_words(n) u32.  *out = Extend(init, data[0..n)).

@@ -133,9 +133,8 @@ hipError_t launch_fixed(const LaunchGeom& g, const uint32_t* d_tables, const uin
       return hipGetLastError();
     }
     if (len - 1u <= 1151u) {  // records of 1..1152 B, staged through LDS, k lanes each (crc32c_lanespan.h)
-      launch_lanespan(g, d_tables, src, nblk,
-                      len <= 256u ? 256u : (len <= 512u ? 512u : (len <= 1023u ? 1023u : 1152u)), sink, s);
-      return hipGetLastError();
+      return launch_lanespan(g, d_tables, src, nblk,
+                             len <= 256u ? 256u : (len <= 512u ? 512u : (len <= 1023u ? 1023u : 1152u)), sink, s);
     }
   }
   // any other length / seed: stream kernels with workgroup-local dynamic blocks and packed 4-block
@@ -166,14 +165,15 @@ hipError_t launch_desc_sink(const LaunchGeom& g, const uint32_t* d_tables, const
   if (hint && !(flags & PDB_CRC_USE_INIT)) {
     if (flags & PDB_CRC_SIZE_1K)  // WAL records of ~1-KiB batches: the record kernel's 1152 class
       // (+4-6 % over crc_sst1k_kernel's 8-block groups, profiles/r02_wal1k/; diagnostics variant 68)
-      launch_lanespan(g, d_tables, src, nblk, 1152u, sink, s);
-    else if (flags & PDB_CRC_SIZE_4K)  // sstable data blocks: 4-KiB body + batched prefix
+      return launch_lanespan(g, d_tables, src, nblk, 1152u, sink, s);
+    if (flags & PDB_CRC_SIZE_4K) {  // sstable data blocks: 4-KiB body + batched prefix
       hipLaunchKernelGGL((crc_sst4k_kernel<DescSrc, Sink, true>), grid, block, 0, s, d_tables, src, nblk, sink);
-    else  // records of 1..1023 B: one lane per record, the bytes staged through LDS by coalesced loads
-      launch_lanespan(g, d_tables, src, nblk,
-                      (flags & PDB_CRC_SIZE_256) ? 256u : ((flags & PDB_CRC_SIZE_512) ? 512u : 1023u), sink, s,
-                      (flags & PDB_CRC_SIZE_MIXED) != 0);
-    return hipGetLastError();
+      return hipGetLastError();
+    }
+    // records of 1..1023 B: k lanes per record, the bytes staged through LDS by coalesced loads
+    return launch_lanespan(g, d_tables, src, nblk,
+                           (flags & PDB_CRC_SIZE_256) ? 256u : ((flags & PDB_CRC_SIZE_512) ? 512u : 1023u), sink, s,
+                           (flags & PDB_CRC_SIZE_MIXED) != 0);
   }
   // descriptor lists of any lengths (C3: Zipf sizes at byte offsets): 16-B lane pieces with nt
   // loads, dynamic blocks, packed 4-block trees (A/B: profiles/r01_ab_c3_pack*.json), byte-balanced
@@ -229,34 +229,6 @@ hipError_t launch_sst_masked(const LaunchGeom& g, const uint32_t* d_tables, uint
   return hipGetLastError();
 }
 
-// The two-launch seal's second launch: trailer word i (launch 1's compact array) to
-// buf[offset_i + size_i + 1 ..+4), one lane per block, after every block has been read (stream
-// order).  A handle whose block + trailer leaves the image is skipped, as the one-launch seal skips
-// it.  The 4 bytes are unaligned: byte stores, merged in L2 before the line is written.
-__global__ __launch_bounds__(256) void sst_trailer_scatter_kernel(uint8_t* __restrict__ buf, uint64_t len,
-                                                                  const pdb_block_handle* __restrict__ h,
-                                                                  const uint32_t* __restrict__ words, uint64_t n) {
-  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint64_t off = h[i].offset, size = h[i].size;
-  if (len < 5 || off > len - 5 || size > len - 5 - off) return;
-  uint8_t* tr = buf + off + size + 1;
-  const uint32_t m = words[i];
-  tr[0] = static_cast<uint8_t>(m);
-  tr[1] = static_cast<uint8_t>(m >> 8);
-  tr[2] = static_cast<uint8_t>(m >> 16);
-  tr[3] = static_cast<uint8_t>(m >> 24);
-}
-
-hipError_t launch_sst_seal2(const LaunchGeom& g, const uint32_t* d_tables, uint8_t* buf, uint64_t buf_len,
-                            const pdb_block_handle* h, uint64_t n, uint32_t* scratch, hipStream_t s) {
-  if (n == 0) return hipSuccess;
-  hipError_t e = launch_sst_masked(g, d_tables, buf, buf_len, h, n, scratch, s);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(sst_trailer_scatter_kernel, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256), 0, s, buf,
-                     buf_len, h, scratch, n);
-  return hipGetLastError();
-}
 
 
 }  // namespace pdb

@@ -331,7 +331,7 @@ __device__ __forceinline__ LaneSpanGeom span_pick(uint32_t nw) {
 }
 
 struct SpanItem {
-  uint64_t batch;   // records 64 * batch + r
+  uint64_t r0;      // records r0 + r (the unit's first record)
   uintptr_t lo;     // 16-B aligned global address of region byte 0
   uint32_t hi;      // local end: max over the item's records (0: nothing to hash)
   uint32_t k, iters;            // k: lanes per record (var: the most any record of the item takes)
@@ -366,7 +366,7 @@ struct SpanItem {
 // kMixed (PDB_CRC_SIZE_MIXED): per-record lane counts where a batch's records vary (open_batch).
 template <class Src, class Sink, uint32_t MAXN, int MODE = 0, class TP = TabsS4, bool kDyn = true, bool kMixed = false>
 __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16, MODE == 31>::kWaves * 64)) void crc_lanespan_kernel(const uint32_t* __restrict__ tabs, Src src,
-                                                                       uint64_t nblk, Sink sink) {
+                                                                       uint64_t nblk, Sink sink, uint32_t* wq) {
   constexpr uint32_t kSpanWaves = SpanStage<MAXN, MODE == 16, MODE == 31>::kWaves, kSpanJ = SpanStage<MAXN, MODE == 16, MODE == 31>::kJ;
   constexpr uint32_t kSpanRegion = SpanStage<MAXN, MODE == 16, MODE == 31>::kRegion, kSpanUsable = SpanStage<MAXN, MODE == 16, MODE == 31>::kUsable;
   typedef SpanStage<MAXN, MODE == 16, MODE == 31> ST;
@@ -418,34 +418,103 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16, MODE == 31>::kWaves * 
   const uint32_t ureg = tabs[PDB_UNSHIFT_OFF + (u & 15u)];
   uint64_t t_start = 0;
   uint32_t n_items = 0, n_batches = 0;
-  if constexpr (MODE == 4) t_start = wall_clock64();
-  // the work counter: the last 16 B of the last wave's region, which no item ever uses (spans end
-  // by kUsable) and to_lds skips
+  uint64_t c_start = 0;
+  constexpr bool kClk = MODE >= 40 && MODE <= 42;  // diagnostics: shader-clock stamps (tools/span_clock.py)
+  if constexpr (MODE == 4 || kClk) t_start = wall_clock64();
+  if constexpr (kClk) c_start = clock64();
+  // kGQ (the product since round 5): work units from 8 device-wide queues (wq), one per XCD;
+  // MODE 44 = the round-2..4 scheme (each workgroup a fixed range of batches, its waves taking
+  // them from an LDS counter); kDyn false = static batches wv + k W (diagnostics)
+  constexpr bool kGQ = kDyn && MODE != 44;
+  // the workgroup's batch counter (MODE 44): the last 16 B of the last wave's region, which no item
+  // ever uses (spans end by kUsable) and to_lds skips
   uint32_t* ctr = reinterpret_cast<uint32_t*>(lds + kSpanStageBase + kSpanWaves * kSpanRegion - 16u);
-  if (kDyn && threadIdx.x == 0) *ctr = 2u * kSpanWaves;  // tickets wv and kWaves + wv are taken below
+  if (kDyn && !kGQ && threadIdx.x == 0) *ctr = kSpanWaves;  // ticket wv is each wave's first
   __syncthreads();
   const typename TP::LT lt = TP::lane(u);
   char* region = lds + kSpanStageBase + wv * kSpanRegion;
   const uintptr_t dummy = reinterpret_cast<uintptr_t>(tabs);  // >= 4 KiB + 256 B of valid bytes
   const uint64_t nbat = (nblk + 63u) >> 6;
-  const uint64_t W = static_cast<uint64_t>(gridDim.x) * kSpanWaves;
-  // kDyn: this workgroup's batches; the next batch to open and the ticket after it (taken one
-  // batch early, so the LDS atomic's latency never sits in front of a descriptor load)
-  const uint64_t g_lo = kDyn ? nbat * blockIdx.x / gridDim.x : 0;
-  const uint64_t g_end = kDyn ? nbat * (blockIdx.x + 1) / gridDim.x : nbat;
-  uint64_t bnext = kDyn ? g_lo + wv : static_cast<uint64_t>(blockIdx.x) * kSpanWaves + wv;  // next batch to open
-  uint32_t tick = kSpanWaves + wv;  // kDyn: the batch after it, relative to g_lo (lane 0's VGPR)
-  if (bnext >= g_end) return;  // wave-uniform; no barrier below
+  const uint32_t nwaves = gridDim.x * kSpanWaves;
+  const uint64_t W = nwaves;
 
-  auto idx = [&](uint64_t bb) -> uint64_t {
-    const uint64_t i = (bb << 6) + u;
-    return i < nblk ? i : nblk - 1;
+  // ---- work units: (first record r0, records cnt <= 64), a batch or part of one ----------------
+  // kGQ: queue x (word wq[32 x], its own 128-B line) owns batches [nbat x / 8, nbat (x + 1) / 8):
+  // its tickets are first whole batches, then -- for its last ceil(waves / 8) batches -- quarter
+  // batches (16 records: one item of the 512 class, two of the 1023 / 1152 classes; the <= 256
+  // class keeps whole batches, one or two items each), so the chip's waves run out of work within
+  // about an item of each other instead of a batch (~40 us on 1000-B records: DESIGN.md §4).  A
+  // workgroup starts on queue blockIdx.x mod 8 (its XCD's, under round-robin dispatch) and moves
+  // on to the next queue when one runs out, so a slower XCD's batches are finished by the others.
+  // Each wave holds one ticket in flight (the unit after the one whose descriptors are in flight),
+  // so the device-scope atomic's latency (~1-3 us) never waits in front of a load.  The last wave
+  // out resets the 9 words (8 queues + the exit count), so every launch starts from zeros; one set
+  // per stream (the C-ABI), so launches that may overlap never share one.
+  constexpr uint32_t kS = MAXN <= 256u ? 1u : 4u;  // units per split batch
+  uint32_t qx = blockIdx.x & 7u, qn = 0;
+  uint32_t tick = wv;  // lane 0: the ticket in flight (MODE 44: the LDS counter's value)
+  uint64_t sbat = static_cast<uint64_t>(blockIdx.x) * kSpanWaves + wv;  // kDyn false: the next batch
+  const uint64_t g_lo = (kDyn && !kGQ) ? nbat * blockIdx.x / gridDim.x : 0;
+  const uint64_t g_end = (kDyn && !kGQ) ? nbat * (blockIdx.x + 1) / gridDim.x : nbat;
+  const uint64_t qsplit = kS > 1u ? (nwaves + 7u) / 8u : 0u;  // split batches per queue
+  auto unit_of_batch = [&](uint64_t b, uint64_t& r0, uint32_t& cnt) {
+    r0 = b << 6;
+    cnt = static_cast<uint32_t>(nblk - r0 < 64u ? nblk - r0 : 64u);
   };
-  // the next batch's descriptors and sink words, in flight; reloaded by every next_item call (the
-  // same address when no batch was opened) so no load is ever consumed right after it is issued
-  typename Src::Raw raw_next = src.load_cached(idx(bnext));
-  uint32_t pre_next = SinkOps<Sink>::pre(sink, idx(bnext), BlkDesc{nullptr, 0u, 0u});
-  uint64_t bcur = 0;
+  // queue x's ticket t: false when the queue is exhausted; cnt 0 = an empty quarter past nblk
+  auto decode = [&](uint32_t x, uint32_t t, uint64_t& r0, uint32_t& cnt) -> bool {
+    const uint64_t lo = nbat * x / 8u, n = nbat * (x + 1u) / 8u - lo;
+    const uint64_t R = n < qsplit ? n : qsplit, F = n - R;
+    if (t < F) {
+      unit_of_batch(lo + t, r0, cnt);
+      return true;
+    }
+    const uint64_t q = t - F;
+    if (q >= kS * R) return false;
+    r0 = ((lo + F + q / kS) << 6) + (q % kS) * (64u / kS);
+    cnt = r0 >= nblk ? 0u : static_cast<uint32_t>(nblk - r0 < 64u / kS ? nblk - r0 : 64u / kS);
+    return true;
+  };
+  // the next unit (false: no work left): decode the ticket in flight, put the following one in flight
+  auto acquire = [&](uint64_t& r0, uint32_t& cnt) -> bool {
+    if constexpr (!kDyn) {
+      if (sbat >= nbat) return false;
+      unit_of_batch(sbat, r0, cnt);
+      sbat += W;
+      return true;
+    } else if constexpr (!kGQ) {
+      const uint64_t b = g_lo + __builtin_amdgcn_readfirstlane(tick);
+      if (b >= g_end) return false;
+      if (u == 0) tick = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      unit_of_batch(b, r0, cnt);
+      return true;
+    } else {
+      for (;;) {
+        const uint32_t t = __builtin_amdgcn_readfirstlane(tick);
+        if (decode(qx, t, r0, cnt)) {
+          if (u == 0) tick = __hip_atomic_fetch_add(wq + 32u * qx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (cnt) return true;
+          continue;  // an empty quarter (the last batch's): the next ticket
+        }
+        if (++qn == 8u) return false;
+        qx = (qx + 1u) & 7u;
+        if (u == 0) tick = __hip_atomic_fetch_add(wq + 32u * qx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  };
+  if constexpr (kGQ) {
+    if (u == 0) tick = __hip_atomic_fetch_add(wq + 32u * qx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  uint64_t nx_r0 = 0;  // the next unit (its descriptors in flight)
+  uint32_t nx_cnt = 0;
+  bool nx_ok = acquire(nx_r0, nx_cnt);
+  auto idx = [&](uint64_t r0, uint32_t cnt) -> uint64_t { return r0 + (u < cnt ? u : cnt - 1u); };
+  // the next unit's descriptors and sink words, in flight; reloaded by every next_item call (the
+  // same address when no unit was opened) so no load is ever consumed right after it is issued
+  typename Src::Raw raw_next = src.load_cached(idx(nx_r0, nx_ok ? nx_cnt : 1u));
+  uint32_t pre_next = SinkOps<Sink>::pre(sink, idx(nx_r0, nx_ok ? nx_cnt : 1u), BlkDesc{nullptr, 0u, 0u});
+  uint64_t b_r0 = 0;  // the current unit
+  uint32_t b_cnt = 0;
   bool have_batch = false;
   uintptr_t bp = 0;      // per lane: record start
   uint32_t bn = 0;       // per lane: record length
@@ -464,19 +533,14 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16, MODE == 31>::kWaves * 
   // make the prefetched batch current; records outside the class are hashed here by the whole
   // wave (rare: their loads wait behind the items in flight)
   auto open_batch = [&]() -> bool {
-    if (bnext >= g_end) return false;
+    if (!nx_ok) return false;
     keep_alive(raw_next);
     const BlkDesc d = src.lane(raw_next);
     bpre = pre_next;
-    bcur = bnext;
-    if constexpr (kDyn) {
-      bnext = g_lo + __builtin_amdgcn_readfirstlane(tick);
-      if (u == 0) tick = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    } else {
-      bnext += W;
-    }
-    const uint64_t i = (bcur << 6) + u;
-    const bool valid = i < nblk;
+    b_r0 = nx_r0;
+    b_cnt = nx_cnt;
+    nx_ok = acquire(nx_r0, nx_cnt);
+    const bool valid = u < b_cnt;
     bp = reinterpret_cast<uintptr_t>(d.p);
     bn = d.n;
     bfast = valid && (d.n - 1u) <= MAXN - 1u && d.init_raw == 0xFFFFFFFFu;
@@ -489,7 +553,7 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16, MODE == 31>::kWaves * 
       const uint32_t sn = __builtin_amdgcn_readlane(bn, k);
       const uint32_t rs = span_slow_record<TP, kPre>(lds, lt, u, ureg, sp, sn);
       if (u == 0)
-        SinkOps<Sink>::put(sink, (bcur << 6) + k, rs, BlkDesc{reinterpret_cast<const uint8_t*>(sp), sn, 0xFFFFFFFFu},
+        SinkOps<Sink>::put(sink, b_r0 + k, rs, BlkDesc{reinterpret_cast<const uint8_t*>(sp), sn, 0xFFFFFFFFu},
                            __builtin_amdgcn_readlane(bpre, k));
     }
     bfastm = __builtin_amdgcn_ballot_w64(bfast);
@@ -574,7 +638,7 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16, MODE == 31>::kWaves * 
   auto next_item = [&](bool want) -> SpanItem {
     SpanItem it;
     it.valid = false;
-    it.batch = bcur;
+    it.r0 = b_r0;
     it.lo = dummy;
     it.hi = 0;
     it.k = bg.k;
@@ -592,10 +656,10 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16, MODE == 31>::kWaves * 
       have_batch = true;
       rem = bfastm;
     }
-    raw_next = src.load_cached(idx(bnext < g_end ? bnext : bcur));
-    pre_next = SinkOps<Sink>::pre(sink, idx(bnext < g_end ? bnext : bcur), BlkDesc{nullptr, 0u, 0u});
+    raw_next = src.load_cached(nx_ok ? idx(nx_r0, nx_cnt) : idx(b_r0, b_cnt));
+    pre_next = SinkOps<Sink>::pre(sink, nx_ok ? idx(nx_r0, nx_cnt) : idx(b_r0, b_cnt), BlkDesc{nullptr, 0u, 0u});
     it.valid = true;
-    it.batch = bcur;
+    it.r0 = b_r0;
     it.k = bvar ? bkmax : bg.k;
     it.iters = bvar ? biters_v : bg.iters;
     it.var = kVar && bvar;
@@ -692,7 +756,7 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16, MODE == 31>::kWaves * 
   auto issue = [&](u32x4 (&A)[kSpanJ], const SpanItem& it) {
     const uint32_t lo_l = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(it.lo));
     const uint32_t lo_h = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(static_cast<uint64_t>(it.lo) >> 32));
-    const uint32_t nb = (MODE == 2 || MODE == 3) ? 16u : __builtin_amdgcn_readfirstlane(it.hi ? (it.hi + 15u) & ~15u : 16u);
+    const uint32_t nb = (MODE == 2 || MODE == 3 || MODE == 42) ? 16u : __builtin_amdgcn_readfirstlane(it.hi ? (it.hi + 15u) & ~15u : 16u);
     void* base = reinterpret_cast<void*>((static_cast<uint64_t>(lo_h) << 32) | lo_l);
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(base, 0, static_cast<int>(nb), 0x00020000);
 #pragma unroll
@@ -715,7 +779,7 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16, MODE == 31>::kWaves * 
   // hash an item staged in the region
   auto hash = [&](const SpanItem& it) {
     if constexpr (MODE == 4) ++n_items;
-    if (it.hi == 0 || MODE == 1 || MODE == 3) return;
+    if (it.hi == 0 || MODE == 1 || MODE == 3 || MODE == 41) return;
     // chain X (A, B, C, D = 0..3) works from phase-2 step F[X] on; its word at step t is the one
     // ending 4 (NI - t) bytes before the chain's end
     constexpr int32_t FABC = static_cast<int32_t>(NI - LC), FD = static_cast<int32_t>(NI - LD);
@@ -1143,7 +1207,7 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16, MODE == 31>::kWaves * 
     if constexpr (MODE == 18)  // diagnostics: the item's first record, records, lane, lanes, mode
       P = ~(((it.cw >> 16) << 24) | (((it.cw >> 8) & 127u) << 16) | (u << 8) | ((kVar ? pc + ((it.cw >> 4) & 15u) + 1u : k) << 4) | (it.var ? 1u : 0u));
     if (pc == 0 && act)
-      SinkOps<Sink>::put(sink, (it.batch << 6) + it.r, P, BlkDesc{nullptr, 0u, 0xFFFFFFFFu}, it.pre);
+      SinkOps<Sink>::put(sink, it.r0 + it.r, P, BlkDesc{nullptr, 0u, 0xFFFFFFFFu}, it.pre);
   };
 
   // ---- pipeline: two items in flight while one is hashed ---------------------------------------
@@ -1152,7 +1216,9 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16, MODE == 31>::kWaves * 
   // kOneDeep (diagnostics MODE 30 / 31): one item's loads in flight while one is hashed (half the
   // staging registers), the loop: issue(next) -> hash(cur) -> to_lds(next)
   constexpr bool kOneDeep = MODE == 30 || MODE == 31;
-  if constexpr (kOneDeep) {
+  if (!nx_ok) {
+    // no unit for this wave: straight to the exit count
+  } else if constexpr (kOneDeep) {
     u32x4 A[kSpanJ];
     SpanItem I0 = next_item(true);
     issue(A, I0);
@@ -1187,14 +1253,28 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16, MODE == 31>::kWaves * 
     I1 = I3;
   }
   }  // !kOneDeep
-  if constexpr (MODE == 4) {
+  if constexpr (kGQ) {
+    // the last wave out (every wave counts itself once, after its last ticket came back) resets the
+    // queue words for the next launch on this stream
+    if (u == 0) {
+      const uint32_t done = __hip_atomic_fetch_add(wq + 32u * 8u, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (done == nwaves - 1u) {
+#pragma unroll
+        for (uint32_t x = 0; x <= 8u; ++x) __hip_atomic_store(wq + 32u * x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+  if constexpr (MODE == 4 || kClk) {
+    // MODE 40 / 41 / 42 (the product / loads alone / hash alone): [start, end] s_memrealtime (100 MHz)
+    // and [start, end] s_memtime (shader clock): the wave's mean clock over its lifetime
     const uint64_t t_end = wall_clock64();
+    const uint64_t c_end = kClk ? clock64() : 0;
     if (u == 0) {
       uint64_t* st = sink.stamps + 4u * (static_cast<uint64_t>(blockIdx.x) * kSpanWaves + wv);
       st[0] = t_start;
       st[1] = t_end;
-      st[2] = n_items;
-      st[3] = n_batches;
+      st[2] = kClk ? c_start : n_items;
+      st[3] = kClk ? c_end : n_batches;
     }
   }
 }
@@ -1207,34 +1287,39 @@ inline uint32_t grid_span(const LaunchGeom& g, uint64_t nblk, uint32_t waves) {
 
 // Records of 1..1152 B by class (the class bounds the lanes per record: 2, 4, 8, 8); longer ones,
 // and empty ones, take the whole-wave path.
+// The product form (kGQ) takes its work from the stream's queue words g.wq (9 words on 128-B lines,
+// zero between launches): no queue words, no launch.
 template <class Src, class Sink, int MODE = 0, class TP = TabsS4, bool kDyn = true>
-void launch_lanespan(const LaunchGeom& g, const uint32_t* d_tables, const Src& src, uint64_t nblk, uint32_t cls,
-                     const Sink& sink, hipStream_t s, bool mixed = false) {
+hipError_t launch_lanespan(const LaunchGeom& g, const uint32_t* d_tables, const Src& src, uint64_t nblk, uint32_t cls,
+                           const Sink& sink, hipStream_t s, bool mixed = false) {
+  uint32_t* wq = g.wq;
+  if (kDyn && MODE != 44 && wq == nullptr) return hipErrorInvalidValue;
   if (cls <= 256u) {
     constexpr uint32_t w = SpanStage<256, MODE == 16, MODE == 31>::kWaves;
     hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 256, MODE, TP, kDyn>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0, s,
-                       d_tables, src, nblk, sink);
+                       d_tables, src, nblk, sink, wq);
   } else if (cls <= 512u) {
     constexpr uint32_t w = SpanStage<512, MODE == 16, MODE == 31>::kWaves;
     if (mixed && !__is_same(Sink, VerifySink))
       hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 512, MODE, TP, kDyn, true>), dim3(grid_span(g, nblk, w)), dim3(w * 64),
-                         0, s, d_tables, src, nblk, sink);
+                         0, s, d_tables, src, nblk, sink, wq);
     else
       hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 512, MODE, TP, kDyn>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0, s,
-                         d_tables, src, nblk, sink);
+                         d_tables, src, nblk, sink, wq);
   } else if (cls <= 1023u) {
     constexpr uint32_t w = SpanStage<1023, MODE == 16, MODE == 31>::kWaves;
     if (mixed && !__is_same(Sink, VerifySink))
       hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 1023, MODE, TP, kDyn, true>), dim3(grid_span(g, nblk, w)), dim3(w * 64),
-                         0, s, d_tables, src, nblk, sink);
+                         0, s, d_tables, src, nblk, sink, wq);
     else
       hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 1023, MODE, TP, kDyn>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0,
-                         s, d_tables, src, nblk, sink);
+                         s, d_tables, src, nblk, sink, wq);
   } else {  // 1024..1152 B (WAL records of ~1-KiB write batches): 8 lanes, the head chain past 1056 B
     constexpr uint32_t w = SpanStage<1152, MODE == 16, MODE == 31>::kWaves;
     hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 1152, MODE, TP, kDyn>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0,
-                       s, d_tables, src, nblk, sink);
+                       s, d_tables, src, nblk, sink, wq);
   }
+  return hipGetLastError();
 }
 
 }  // namespace

@@ -1220,7 +1220,7 @@ hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tab
                 // 1056 B) for any list: the shipped 1K-hint routing
       constexpr uint32_t w = SpanStage<1152>::kWaves;
       hipLaunchKernelGGL((crc_lanespan_kernel<DescSrc, OutSink, 1152>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0, s,
-                         d_tables, src, nblk, sink);
+                         d_tables, src, nblk, sink, g.wq);
       break;
     }
     case 110:    // the shipped record kernel + per-wave [start, end, items, batches] stamps (s_memrealtime)
@@ -1234,6 +1234,27 @@ hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tab
       ss.stamps = reinterpret_cast<uint64_t*>(out + ((nblk + 1u) & ~1ull));
       if (v == 110) launch_lanespan<DescSrc, StampOutSink, 4>(g, d_tables, src, nblk, cls, ss, s);
       else launch_lanespan<DescSrc, StampOutSink, 4, TabsS4, false>(g, d_tables, src, nblk, cls, ss, s);
+      break;
+    }
+    case 183: {  // the record kernel with the round-2..4 work distribution (each workgroup a fixed range
+                 // of batches, its waves taking them from an LDS counter), for A/B against the queues
+      const uint32_t cls = (flags & PDB_CRC_SIZE_256) ? 256u
+                           : (flags & PDB_CRC_SIZE_512) ? 512u : ((flags & PDB_CRC_SIZE_1K) ? 1152u : 1023u);
+      launch_lanespan<DescSrc, OutSink, 44>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
+      break;
+    }
+    case 180:    // the product / loads + staging alone / hash alone, + per-wave [start, end] s_memrealtime
+    case 181:    // and [start, end] s_memtime stamps (the waves' shader clock; tools/span_clock.py)
+    case 182: {
+      const uint32_t cls = (flags & PDB_CRC_SIZE_256) ? 256u
+                           : (flags & PDB_CRC_SIZE_512) ? 512u : ((flags & PDB_CRC_SIZE_1K) ? 1152u : 1023u);
+      StampOutSink ss;
+      ss.out = out;
+      ss.flags = flags;
+      ss.stamps = reinterpret_cast<uint64_t*>(out + ((nblk + 1u) & ~1ull));
+      if (v == 180) launch_lanespan<DescSrc, StampOutSink, 40>(g, d_tables, src, nblk, cls, ss, s);
+      else if (v == 181) launch_lanespan<DescSrc, StampOutSink, 41>(g, d_tables, src, nblk, cls, ss, s);
+      else launch_lanespan<DescSrc, StampOutSink, 42>(g, d_tables, src, nblk, cls, ss, s);
       break;
     }
     case 113:    // pricing (wrong CRCs): the record kernel with conflict-free staging reads

@@ -55,3 +55,37 @@ def scatter_block_ranges(n_total: int, world: int, rank: int, device, dist=None,
             raise ValueError("scatter_block_ranges: world > 1 needs a process group")
         mine.copy_(parts[0])
     return int(mine[0]), int(mine[1])
+
+
+def scatter_block_lens(lens, world: int, rank: int, device, dist=None) -> tuple[int, int, np.ndarray]:
+    """A variable-size plan held by rank 0 only (`lens` is None on every other rank): rank 0 splits
+    it into byte-balanced ranges, scatters each rank's [lo, hi) (scatter_block_ranges), then each
+    rank's own block lengths (one scatter of equal-width int64 rows, padded to the longest range).
+    Returns (lo, hi, this rank's lengths)."""
+    import torch
+
+    rngs = byte_balanced_ranges(lens, world) if rank == 0 else None
+    width = torch.zeros(1, dtype=torch.int64, device=device)
+    if rank == 0:
+        width[0] = max((hi - lo for lo, hi in rngs), default=0)
+    if dist is not None:
+        dist.broadcast(width, src=0)
+    w = int(width.item())
+    lo, hi = scatter_block_ranges(len(lens) if rank == 0 else 0, world, rank, device, dist,
+                                  lens=lens if rank == 0 else None)
+    mine = torch.zeros(max(w, 1), dtype=torch.int64, device=device)
+    parts = None
+    if rank == 0:
+        src = torch.from_numpy(np.asarray(lens, dtype=np.int64))
+        parts = []
+        for a, b in rngs:
+            row = torch.zeros(max(w, 1), dtype=torch.int64)
+            row[: b - a] = src[a:b]
+            parts.append(row.to(device))
+    if dist is not None:
+        dist.scatter(mine, scatter_list=parts, src=0)
+    else:
+        if world != 1:
+            raise ValueError("scatter_block_lens: world > 1 needs a process group")
+        mine.copy_(parts[0])
+    return lo, hi, mine[: hi - lo].cpu().numpy()

@@ -291,19 +291,6 @@ def seal_device(d_image, d_handles, stream=None) -> None:
                                     _stream(stream)))
 
 
-def seal_device_scratch(d_image, d_handles, scratch=None, stream=None) -> None:
-    """The same seal in two launches (pdb_sst_seal_device_scratch): the trailer words into `scratch`
-    (int32, >= one per handle; allocated here if None), then one scatter into the trailers after
-    every block has been read.  Byte-identical to seal_device."""
-    import torch
-
-    n = d_handles.numel() * d_handles.element_size() // 16
-    if scratch is None:
-        scratch = torch.empty(max(n, 1), dtype=torch.int32, device=d_image.device)
-    check(lib().pdb_sst_seal_device_scratch(_dev(d_image), d_image.numel() * d_image.element_size(), _dev(d_handles),
-                                            n, _dev(scratch), scratch.numel(), _stream(stream)))
-
-
 def crc_device(d_image, d_handles, stream=None, out=None):
     """The seal's trailer words without writing them: int32 tensor of Mask(crc32c(contents||type))
     per handle (an engine writes the trailer while it copies blocks out; the in-place seal pays

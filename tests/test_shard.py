@@ -11,7 +11,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from pebblesdb_amd.shard import block_range, byte_balanced_ranges, scatter_block_ranges
+from pebblesdb_amd.shard import block_range, byte_balanced_ranges, scatter_block_lens, scatter_block_ranges
 
 
 @pytest.mark.parametrize("n,world", [(0, 1), (1, 2), (7, 8), (1 << 20, 8), (33554432, 8), (1000, 3)])
@@ -100,13 +100,15 @@ def _bench_worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import bench
 
-    sizes = bench.c3_plan(64 << 20, world)  # 64 MiB per rank (the bench default is 16 GiB)
-    lo, hi = scatter_block_ranges(len(sizes), world, rank, torch.device("cpu"), dist, lens=sizes)
-    mine = int(sizes[lo:hi].sum())
-    rows = bench.gather_rank_rows([rank, 0, -1, mine, 123456, rank * 7], world, torch.device("cpu"), dist)
+    # the plan exists on rank 0 only; every rank receives its range and its own lengths
+    sizes = bench.c3_plan(64 << 20, world) if rank == 0 else None  # 64 MiB per rank (bench default 16 GiB)
+    lo, hi, lens = scatter_block_lens(sizes, world, rank, torch.device("cpu"), dist)
+    mine = int(lens.sum())
+    rows = bench.gather_rank_rows([rank, 0, -1, mine, 123456, rank * 7, -1], world, torch.device("cpu"), dist)
     if rank == 0:
         q.put(("rows", rows, len(sizes), int(sizes.sum())))
-    q.put(("range", rank, lo, hi))
+    full = bench.c3_plan(64 << 20, world)  # (test only: the same list, to check what rank r received)
+    q.put(("range", rank, lo, hi, bool(len(lens) == hi - lo and (lens == full[lo:hi]).all())))
     dist.destroy_process_group()
 
 
@@ -124,6 +126,7 @@ def test_gloo_world2_bench_c3_byte_balanced():
     msgs = [q.get(timeout=10) for _ in range(world + 1)]
     rows, n, total = next(m[1:] for m in msgs if m[0] == "rows")
     ranges = sorted((m[1], m[2], m[3]) for m in msgs if m[0] == "range")
+    assert all(m[4] for m in msgs if m[0] == "range")  # each rank's lengths are its slice of the plan
     assert ranges[0][1] == 0 and ranges[-1][2] == n and ranges[0][2] == ranges[1][1]
     assert [r[0] for r in rows] == [0, 1] and sum(r[3] for r in rows) == total
     assert abs(rows[0][3] - rows[1][3]) <= 2 * 64 * 1024  # byte-balanced to within a block or two
@@ -172,6 +175,32 @@ def test_bench_gpus2_default_is_c4_shards():
         assert [x["blocks"] for x in line["ranks"]] == [blocks] * gpus
         assert line["config"]["blocks_per_gpu"] == blocks
         assert ("c4" in line["config"]["workload"]) == c4
+
+
+def test_bench_dry_run_curve_keys():
+    """The 1 -> 8 curve's keys (--dry-run, no device): the N = 1 default line carries the c4_shard
+    anchor (one 16 GiB config-4 shard outside `value`); an N > 1 line carries one steady-state row
+    per rank and the steady state over ranks, and no c4_shard (its ranks ARE c4 shards)."""
+    import json
+    import subprocess
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                            "MASTER_PORT", "LOCAL_WORLD_SIZE")}
+    for gpus in (1, 2):
+        cmd, root = _bench_cmd("--gpus", str(gpus), "--steps", "2", "--warmup", "1", "--dry-run")
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=root, env=env)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith('{"metric"')][-1])
+        assert [set(x) >= {"rank", "blocks", "steady_kernel_avg_ms"} for x in line["ranks"]] == [True] * gpus
+        if gpus == 1:
+            assert line["c4_shard"]["blocks"] == 4194304 and line["c4_shard"]["bytes"] == 16 << 30
+            assert line["steady_state"] is None
+        else:
+            assert "c4_shard" not in line
+            assert line["steady_state"]["over_ranks"]["ranks"] == gpus
+    cmd, root = _bench_cmd("--gpus", "1", "--steps", "2", "--dry-run", "--no-c4-shard")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=root, env=env)
+    assert r.returncode == 0 and "c4_shard" not in json.loads(r.stdout.strip().splitlines()[-1])
 
 
 def test_bench_process_group_world1_dry_run():
@@ -289,3 +318,18 @@ def test_bench_rccl_branch_world1_on_the_gpu(oracle_lib):
     blk["off"] = np.arange(nblk) * 4096
     blk["len"] = 4096
     assert int(line["xor_of_crcs"], 16) == int(np.bitwise_xor.reduce(oracle_lib.batch(data, blk, nthreads=4)))
+    # the N = 1 line's equal-shard anchor: rank 0's 16 GiB shard of config 4, every CRC folded into
+    # one XOR that must equal the oracle's over the same bytes (generated again here on the device)
+    c4 = line["c4_shard"]
+    assert c4["blocks"] == 4194304 and c4["steps"] == 3 and c4["warmup"] == 1 and c4["GiB_s"] > 0
+    from pebblesdb_amd import diag
+
+    d = torch.empty(c4["blocks"] * 4096, dtype=torch.uint8, device="cuda")
+    diag.fill_splitmix(d, 301, byte_offset=0)
+    host = d.cpu().numpy()
+    del d
+    torch.cuda.empty_cache()
+    blk = np.zeros(c4["blocks"], dtype=oracle.BLK_DTYPE)
+    blk["off"] = np.arange(c4["blocks"], dtype=np.int64) * 4096
+    blk["len"] = 4096
+    assert int(c4["xor_of_crcs"], 16) == int(np.bitwise_xor.reduce(oracle_lib.batch(host, blk, nthreads=16)))

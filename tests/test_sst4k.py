@@ -200,13 +200,12 @@ def test_new_path_matches_previous_kernel(crc):
     assert all((outs[0] == o).all() for o in outs[1:])
 
 
-@pytest.mark.parametrize("variant", [0, -1, 88, 89, 90, 91, 92, 73, 74])
+@pytest.mark.parametrize("variant", [0, 88, 89, 90, 91, 92, 73, 74])
 def test_parked_seal_matches_plain_seal(crc, variant):
     """The shipped seal parks each wave's trailers (ring of 64 groups, 4 per lane) and writes them
     later; the diagnostics rings of 1..64 groups (88-92, 73, 74) too.  On 1.3 M blocks (> 64 groups
     per wave, so every ring wraps; index-sized and tiny blocks on the slow path mixed in) the sealed
-    image must equal the one written by variant 72 (each group's trailers written when hashed).
-    Variant -1: the two-launch seal (pdb_sst_seal_device_scratch: compact words, then one scatter)."""
+    image must equal the one written by variant 72 (each group's trailers written when hashed)."""
     from pebblesdb_amd import table as T
 
     rng = np.random.Generator(np.random.PCG64(77))
@@ -226,40 +225,11 @@ def test_parked_seal_matches_plain_seal(crc, variant):
     got = img.clone()
     if variant == 0:
         T.seal_device(got, d_h)
-    elif variant == -1:
-        T.seal_device_scratch(got, d_h)
     else:
         diag.sst(variant, got, d_h, seal=True)
     assert torch.equal(got, ref), variant
     ok, nbad = T.verify_device(got, d_h)
     assert int(nbad.item()) == 0
-
-
-def test_two_launch_seal_skips_out_of_image_handles(crc):
-    """Handles whose block + trailer leave the image are skipped by the one-launch seal; the
-    two-launch form (its compact words never written for them, its scatter checking the same bound)
-    must leave the same bytes, and reject scratch smaller than one word per handle."""
-    from pebblesdb_amd import table as T
-    from pebblesdb_amd._native import PdbError
-
-    rng = np.random.Generator(np.random.PCG64(79))
-    sizes = rng.integers(1, 9000, size=3000).astype(np.int64)
-    offs = np.concatenate([[0], np.cumsum(sizes + 5)[:-1]])
-    total = int(offs[-1] + sizes[-1] + 5)
-    img = torch.empty(total, dtype=torch.uint8, device="cuda")
-    diag.fill_splitmix(img, 80)
-    img[torch.from_numpy(offs + sizes).cuda()] = 0
-    h = np.zeros(len(sizes) + 3, dtype=crc.HANDLE_DTYPE)
-    h["offset"][:-3], h["size"][:-3] = offs, sizes
-    h["offset"][-3:], h["size"][-3:] = [total - 4, total + 10, 5], [0, 1, total]  # past the end
-    d_h = T.handles_to_device(h)
-    a, b = img.clone(), img.clone()
-    T.seal_device(a, d_h)
-    T.seal_device_scratch(b, d_h)
-    assert torch.equal(a, b)
-    small = torch.empty(len(h) - 1, dtype=torch.int32, device="cuda")
-    with pytest.raises(PdbError):
-        T.seal_device_scratch(b, d_h, scratch=small)
 
 
 # ---- descriptor batches with a size-class hint: crc_sst1k_kernel / crc_sst4k_kernel<DescSrc> ----

@@ -60,7 +60,7 @@ for s in "$@"; do
     ab_seal_price) step ab_seal_price 600 python tools/ab_sst.py 0,94,95,96 && step ab_seal_price_rev 600 python tools/ab_sst.py 96,95,94,0 ;;
     ab_seal_orders) step ab_so1 600 python tools/ab_sst.py 0,94,95 && step ab_so2 600 python tools/ab_sst.py 95,94,0 && step ab_so3 600 python tools/ab_sst.py 94,0 ;;
     bench_rows) for w in sst_verify sst_seal sst_crc wal sstable c3; do step bench_$w 300 python bench.py --workload $w --no-copy-inclusive --steps 50 || exit 1; done ;;
-    bench_rows4) for w in c3 sstable sst_verify sst_seal sst_seal2 sst_crc wal wal100 wal400 wal1000; do step bench_$w 300 python bench.py --workload $w --no-copy-inclusive --steps 50 || exit 1; done ;;
+    bench_rows4) for w in c3 sstable sst_verify sst_seal sst_crc wal wal100 wal400 wal1000; do step bench_$w 300 python bench.py --workload $w --no-copy-inclusive --steps 50 || exit 1; done ;;
     bench_driver3) for i in 1 2 3; do step bench_driver_$i 300 python bench.py || exit 1; done ;;
     bench_sst3) for w in sst_verify sst_crc sstable; do step bench3_$w 300 python bench.py --workload $w --no-copy-inclusive --steps 50 || exit 1; done ;;
     bench_sst) step bench_sst 600 python bench.py --workload sstable --no-cpu-baseline --no-copy-inclusive ;;

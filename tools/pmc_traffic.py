@@ -17,7 +17,7 @@ out_dir, workload = sys.argv[1], (sys.argv[2] if len(sys.argv) > 2 else "c2")
 KERNELS = {"c2": "crc_pack4k_kernel", "sstable": "crc_sst4k_kernel", "c3": "crc_stream16_kernel",
            "wal": "crc_lanespan_kernel", "wal100": "crc_lanespan_kernel", "wal400": "crc_lanespan_kernel",
            "wal1000": "crc_lanespan_kernel", "sst_verify": "crc_sst4k_kernel", "sst_seal": "crc_sst4k_kernel",
-           "sst_crc": "crc_sst4k_kernel", "sst_seal2": "sst_trailer_scatter_kernel"}
+           "sst_crc": "crc_sst4k_kernel"}
 target = KERNELS[workload]
 
 
