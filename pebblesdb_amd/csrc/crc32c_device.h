@@ -515,7 +515,7 @@ __device__ __forceinline__ uint32_t partial4k_q(const char* lds, const QuadTabs&
 // barrier per 4-block group keeps the workgroup's 16 waves on 16 consecutive blocks (DRAM row
 // locality: +8 %).  Results are parked in a register and flushed as one 64-lane
 // store per 16 groups.  The A/B variants of this kernel (piece shapes, waves per CU, lock-step
-// period, XCD numbering, quad transposes) live in the diagnostics library (diag_device.h).
+// period, XCD numbering, quad transposes) were diagnostics-library variants until round 4.
 // kW: waves per workgroup (one workgroup per CU); 16 shipped, 8 / 12 A/B variants.  kDeferF: one
 // table step per 4 blocks after the tree (partial4k_q); false = the round-2 form (A/B).
 template <uint32_t kW = kWavesPerWg, bool kDeferF = true>

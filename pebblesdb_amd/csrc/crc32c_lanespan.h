@@ -53,13 +53,11 @@ constexpr uint32_t kSpanStageBase = 64u << 10;                    // tables and 
 // The 1024..1152-B class takes 10 x 9 KiB too: eight 1062-B records (1055-B fragments + headers)
 // do not fit 8 KiB, so 8-KiB items held 7 records on 56 of the 64 lanes (+2.5 % with 9 KiB,
 // −4..−9 % for the 512 and 1023 classes, whose 8 records fit 8 KiB; profiles/r03_wide/).
-// kWide (diagnostics MODE 16): 10 x 9 KiB for every class.
-// k13 (diagnostics MODE 31, with the one-deep pipeline): 13 x 7 KiB.
-template <uint32_t MAXN, bool kWide = false, bool k13 = false>
+template <uint32_t MAXN>
 struct SpanStage {
-  static constexpr bool k9 = (MAXN <= 256u || MAXN > 1023u || kWide) && !k13;
-  static constexpr uint32_t kWaves = k13 ? 13u : (k9 ? 10u : 12u);  // (13 x 7 KiB with A/B staging: slower, 128-VGPR cap)
-  static constexpr uint32_t kJ = k13 ? 7u : (k9 ? 9u : 8u);
+  static constexpr bool k9 = MAXN <= 256u || MAXN > 1023u;
+  static constexpr uint32_t kWaves = k9 ? 10u : 12u;
+  static constexpr uint32_t kJ = k9 ? 9u : 8u;
   static constexpr uint32_t kRegion = kJ * 1024u;
   static constexpr uint32_t kUsable = kRegion - 16u;  // span limit: reads stay inside
   static_assert((64u << 10) + kWaves * kRegion <= PDB_LDS_BYTES, "fits the 160 KiB");
@@ -69,10 +67,10 @@ struct SpanStage {
   static constexpr uint32_t kNI = kLD > kLC ? kLD : kLC;            // lock-step steps of a part
   static constexpr uint32_t kOpSet = kLD == 9u ? 0u : 3u;           // its part operators in the table source
 };
-// operator slots: 5..7 shift by 1, 2 and 4 parts of the kernel's class; slot 0 shift 16 -- or, with
-// the pre-shifted cross-lane fold (kPre), shift by 3 parts (the slow path's shift 16 is then four
-// table steps: it is rare, and the fold runs once per item)
-constexpr uint32_t kOp16 = 0, kOpP3 = 0, kOp32 = 1, kOp64 = 2, kOp256 = 3, kOp1024 = 4, kOpP1 = 5, kOpP2 = 6, kOpP4 = 7;
+// operator slots: 5..7 and 0 shift by 1, 2, 4 and 3 parts of the kernel's class (the pre-shifted
+// cross-lane fold; the slow path's shift 16 is four table steps: it is rare, and the fold runs once
+// per item)
+constexpr uint32_t kOpP3 = 0, kOp32 = 1, kOp64 = 2, kOp256 = 3, kOp1024 = 4, kOpP1 = 5, kOpP2 = 6, kOpP4 = 7;
 
 // shift(c, D) ^ y for the operator in slot `slot` (byte j of c indexes sub-table j)
 __device__ __forceinline__ uint32_t span_op_x(const char* lds, uint32_t slot, uint32_t c, uint32_t y) {
@@ -85,15 +83,14 @@ __device__ __forceinline__ uint32_t span_op_x(const char* lds, uint32_t slot, ui
   return xor3(xor3(v[0], v[1], v[2]), v[3], y);
 }
 
-// shift(c, 16 << k) ^ y for k = 0..5 (16, 32, 64, 64 x 2, 256, 256 x 2); kPre: slot 0 holds the
-// 3-part operator, so shift 16 is four table steps
-template <class TP, bool kPre>
+// shift(c, 16 << k) ^ y for k = 0..5 (16, 32, 64, 64 x 2, 256, 256 x 2); shift 16 is four table
+// steps (slot 0 holds the 3-part operator)
+template <class TP>
 __device__ __forceinline__ uint32_t span_shift_x(const char* lds, const typename TP::LT& lt, uint32_t k, uint32_t c,
                                                  uint32_t y) {
   switch (k) {
     case 0:
-      if constexpr (kPre) return TP::step(lds, lt, TP::step(lds, lt, TP::step(lds, lt, TP::step(lds, lt, c, 0u), 0u), 0u), y);
-      else return span_op_x(lds, kOp16, c, y);
+      return TP::step(lds, lt, TP::step(lds, lt, TP::step(lds, lt, TP::step(lds, lt, c, 0u), 0u), 0u), y);
     case 1: return span_op_x(lds, kOp32, c, y);
     case 2: return span_op_x(lds, kOp64, c, y);
     case 3: return span_op_x(lds, kOp64, span_op_x(lds, kOp64, c, 0u), y);
@@ -167,19 +164,14 @@ struct TabsS4 {
   }
 };
 
-template <uint32_t kOpSet, bool kPre = false, bool kPreF = false>
+template <uint32_t kOpSet>
 __device__ __forceinline__ void stage_ops_span(char* lds, const uint32_t* __restrict__ tabs) {
   // slot s, sub-table j, entry b at b<<8 | 128 | (((b >> 2) ^ (4s + j)) & 31) << 2; sources: catalog
-  // entries 0 (16), 1 (32), 2 (64), 4 (256), 6 (1024), then the class's part operators (132, 264,
-  // 528 or 108, 216, 432); kPre: slot 0 = the class's 3-part operator (396 or 324)
+  // entries 1 (32), 2 (64), 4 (256), 6 (1024), then the class's part operators (132, 264, 528 or
+  // 108, 216, 432); slot 0 = the class's 3-part operator (396 or 324)
   for (uint32_t i = threadIdx.x; i < 8u * 1024u; i += blockDim.x) {
     const uint32_t slot = i >> 10, j = (i >> 8) & 3u, b = i & 255u;
-    // kPreF: slots 5, 6, 0 = 1, 2, 3 parts + 4 B (catalog 8..10 / 11..13); slot 7 stays 4 parts
-    const uint32_t f = kOpSet == 0u ? 8u : 11u;
-    const uint32_t src = (kPreF && slot == 0u)   ? PDB_SPANOP_OFF + (f + 2u) * 1024u
-                         : (kPreF && slot == 5u) ? PDB_SPANOP_OFF + f * 1024u
-                         : (kPreF && slot == 6u) ? PDB_SPANOP_OFF + (f + 1u) * 1024u
-                         : (kPre && slot == 0u)  ? PDB_SPANOP_OFF + (kOpSet == 0u ? 6u : 7u) * 1024u
+    const uint32_t src = slot == 0u  ? PDB_SPANOP_OFF + (kOpSet == 0u ? 6u : 7u) * 1024u
                          : slot < 5u ? 1024u + (slot < 3u ? slot : (slot == 3u ? 4u : 6u)) * 1024u
                                      : PDB_SPANOP_OFF + (slot - 5u + kOpSet) * 1024u;
     *reinterpret_cast<uint32_t*>(lds + ((b << 8) | 128u | ((((b >> 2) ^ (4u * slot + j)) & 31u) << 2))) = tabs[src + j * 256u + b];
@@ -200,7 +192,7 @@ __device__ __forceinline__ uint32_t span_chain16(const char* lds, const typename
   return TP::step(lds, lt, x, 0u);
 }
 
-template <class TP, bool kPre = false>
+template <class TP>
 __device__ __forceinline__ uint32_t span_slow_record(const char* lds, const typename TP::LT& lt, uint32_t u, uint32_t ureg,
                                                      uintptr_t p, uint32_t n) {
   if (n == 0) return 0xFFFFFFFFu;
@@ -235,17 +227,17 @@ __device__ __forceinline__ uint32_t span_slow_record(const char* lds, const type
   // tree over 64 lanes, 16 B apart: shift 16 << k between partners at distance 2^k
   uint32_t y;
   y = __builtin_amdgcn_update_dpp(0u, acc, 0x101, 0xF, 0xF, false);  // row_shl:1
-  if ((u & 1u) == 0) acc = span_shift_x<TP, kPre>(lds, lt, 0, acc, y);
+  if ((u & 1u) == 0) acc = span_shift_x<TP>(lds, lt, 0, acc, y);
   y = __builtin_amdgcn_update_dpp(0u, acc, 0x102, 0xF, 0xF, false);
-  if ((u & 3u) == 0) acc = span_shift_x<TP, kPre>(lds, lt, 1, acc, y);
+  if ((u & 3u) == 0) acc = span_shift_x<TP>(lds, lt, 1, acc, y);
   y = __builtin_amdgcn_update_dpp(0u, acc, 0x104, 0xF, 0xF, false);
-  if ((u & 7u) == 0) acc = span_shift_x<TP, kPre>(lds, lt, 2, acc, y);
+  if ((u & 7u) == 0) acc = span_shift_x<TP>(lds, lt, 2, acc, y);
   y = __builtin_amdgcn_update_dpp(0u, acc, 0x108, 0xF, 0xF, false);
-  if ((u & 15u) == 0) acc = span_shift_x<TP, kPre>(lds, lt, 3, acc, y);
+  if ((u & 15u) == 0) acc = span_shift_x<TP>(lds, lt, 3, acc, y);
   y = __builtin_amdgcn_ds_swizzle(acc, 0x401F);  // lane ^ 16
-  if ((u & 31u) == 0) acc = span_shift_x<TP, kPre>(lds, lt, 4, acc, y);
+  if ((u & 31u) == 0) acc = span_shift_x<TP>(lds, lt, 4, acc, y);
   y = __builtin_amdgcn_readlane(acc, 32);
-  if (u == 0) acc = span_shift_x<TP, kPre>(lds, lt, 5, acc, y);
+  if (u == 0) acc = span_shift_x<TP>(lds, lt, 5, acc, y);
   return __builtin_amdgcn_readfirstlane(acc);
 }
 
@@ -344,32 +336,22 @@ struct SpanItem {
   uint32_t p_loc, e_loc, pre;  // per lane: local start (kNoRec: no record), local end, sink word
 };
 
-// MODE (diagnostics only): 0 the product; 1 loads and staging without the hash; 2 the hash over
-// whatever the region holds, without the loads; 3 neither (the per-item bookkeeping alone); 4 the
-// product plus per-wave timestamps (a Sink with a `stamps` array: [start, end, items, batches] per
-// wave, s_memrealtime ticks); pricing forms with the product's instruction stream but WRONG CRCs:
-// 5 every staging read at a lane-skewed, bank-conflict-free address, 6 that and the fold operators'
-// lookups too, 7 no p-word state replacement, 8 no cross-lane folds, 9 no in-part folds (XORs);
-// exact A/B forms: 10 the round-2 finish (a table step per chain before the folds, bpermute
-// partners), 11 the shipped finish with bpermute partners, 13 the A, B, C steps issued one chain
-// at a time (round 2), 14 no bank-spread choice of the halves (records 0-7 | 8-15 always), 15 the
-// first row's choice for the whole batch, 16 10 waves x 9-KiB regions for every class, 17 the
-// batch-uniform k only (no per-record lanes for mixed sizes), 18 the item geometry instead of the CRC
-// (first record << 24 | records << 16 | lane << 8 | lanes << 4 | per-record mode; diagnostics), 19 the
-// staging reads as aligned ds_read_b64 pairs (round 4: slower), 21 the round-3 cross-lane tree (no
-// pre-shift), 22 sparse p-word selects (slower), 25 the staging reads from one opaque base per chain,
-// 26 one compare per step for the p-word selects, 27 the round-3 staging-read addressing, 28 the
-// finishing step folded into the pre-shift.
+// MODE (diagnostics only, libpdb_crc32c_diag.so): 0 the product; 1 loads and staging without the
+// hash; 2 the hash over whatever the region holds, without the loads; 3 neither (the per-item
+// bookkeeping alone); 17 the batch-uniform k only (no per-record lanes for mixed sizes); 18 the
+// item geometry instead of the CRC (first record << 24 | records << 16 | lane << 8 | lanes << 4 |
+// per-record mode); 40 / 41 / 42 = 0 / 1 / 2 with per-wave clock stamps (a Sink with a `stamps`
+// array); 44 the round-2..4 work distribution (each workgroup a fixed range of batches).  The
+// round-2..4 A/B forms that lost are recorded in DESIGN.md's appendix and were removed in round 5.
 // TP: the table scheme.
-// kDyn: the workgroup owns batches [g nbat / G, (g + 1) nbat / G) and its waves take the next one
-// from an LDS counter (false: batch wave_id + k W, the round-2 static assignment -- diagnostics).
+// kDyn: false = static batches wv + k W (diagnostics).
 // kMixed (PDB_CRC_SIZE_MIXED): per-record lane counts where a batch's records vary (open_batch).
 template <class Src, class Sink, uint32_t MAXN, int MODE = 0, class TP = TabsS4, bool kDyn = true, bool kMixed = false>
-__global__ __launch_bounds__((SpanStage<MAXN, MODE == 16, MODE == 31>::kWaves * 64)) void crc_lanespan_kernel(const uint32_t* __restrict__ tabs, Src src,
+__global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_kernel(const uint32_t* __restrict__ tabs, Src src,
                                                                        uint64_t nblk, Sink sink, uint32_t* wq) {
-  constexpr uint32_t kSpanWaves = SpanStage<MAXN, MODE == 16, MODE == 31>::kWaves, kSpanJ = SpanStage<MAXN, MODE == 16, MODE == 31>::kJ;
-  constexpr uint32_t kSpanRegion = SpanStage<MAXN, MODE == 16, MODE == 31>::kRegion, kSpanUsable = SpanStage<MAXN, MODE == 16, MODE == 31>::kUsable;
-  typedef SpanStage<MAXN, MODE == 16, MODE == 31> ST;
+  constexpr uint32_t kSpanWaves = SpanStage<MAXN>::kWaves, kSpanJ = SpanStage<MAXN>::kJ;
+  constexpr uint32_t kSpanRegion = SpanStage<MAXN>::kRegion, kSpanUsable = SpanStage<MAXN>::kUsable;
+  typedef SpanStage<MAXN> ST;
   constexpr uint32_t LC = ST::kLC, LD = ST::kLD, NI = ST::kNI, PART = ST::kPart;
   static_assert(MAXN + 32u <= kSpanUsable, "a record of the class must fit a region");
   // k parts cover MAXN: 2, 5, 8 (a longer class -- diagnostics 1152 -- stays at 8 lanes and runs
@@ -381,46 +363,17 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16, MODE == 31>::kWaves * 
   // always 8) have no registers to spare for it (their 2 x 9 staging chunks in flight), nor has the
   // verify form (an expected word per item in flight: it spilled 24-28 B per lane with it)
   constexpr bool kVar = kMixed && MODE != 17 && (MAXN == 512u || MAXN == 1023u) && !__is_same(Sink, VerifySink);
-  // kPre (the product since round 4): the cross-lane fold pre-shifted per lane -- lane c: shift by
-  // (c mod 4) parts (slots P1 / P2 / P3), XORs within its quad, one P4 level for records of > 4
-  // parts -- instead of the round-3 tree of operator levels P1, P2, P4 (MODE 21; +0.2-1.7 % on the
-  // WAL rows in A/B, profiles/r04/ab_variants.log)
-  constexpr bool kPre = MODE != 8 && MODE != 10 && MODE != 11 && MODE != 21;
-  // kPreF (MODE 28): the pre-shift operators carry the finishing table step F too (1, 2, 3 parts
-  // + 4 B), and the lanes of part 0 mod 4 apply F through the replicated T tables in the same
-  // lookup instructions -- the separate F level after the fold disappears (records of > 1 part)
-  constexpr bool kPreF = kPre && MODE == 28;
-  // kOpaqueBase (the product since round 4): the staging reads addressed from one opaque base
-  // (offset fields, some ds_read2_b32; +1.9-2.1 % on wal400 / wal1000 / wal in A/B,
-  // profiles/r04/ab_variants_r04d.log; MODE 27 = the round-3 addressing)
-  constexpr bool kOpaqueBase = MODE != 27 && MODE != 5 && MODE != 6 && MODE != 19;
-  constexpr bool kOneCmp = MODE == 26 || MODE == 32 || MODE == 34;
-  // kMaskSel (MODE 32): the p-word selects as wave masks -- per item one ballot per chain of the lanes
-  // replacing in it, per step one ballot of the lanes replacing at that step; each select is then an
-  // SALU and of the two masks and one v_cndmask (inverse ballot), 5 VALU per step instead of 8
-  constexpr bool kMaskSel = MODE == 32 || MODE == 34;
-  // kNoG (the product since late round 4): the p-word selects on every lock-step step, branch-free,
-  // instead of only up to the item's last replacement step G behind a wave-uniform branch per step
-  // (+0.1-3 % in A/B, profiles/r04/ab/ab_nog.log; MODE 36 = the G-bounded form; 26 / 32 keep it too)
-  constexpr bool kNoG = MODE != 36 && MODE != 26 && MODE != 32;
-  // kSparse: p-word selects only at the (chain, step) pairs some lane needs (MODE 22: slower)
-  constexpr bool kSparse = MODE == 22;
-  // kRot (MODE 29; the 33-word-part classes): the lock-step staging reads rotated over four chain
-  // slots per lane so that the lanes of one bank class (dword mod 8) read different banks (see hash)
-  constexpr bool kRot = MODE == 29 && LD == 9u && LC == 8u;
-  static_assert(!kRot || NI == 9u, "kRot: chain D's step 0 alone, then 8 steps of all four chains");
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
   char* lds = reinterpret_cast<char*>(lds_words);
   TP::stage(lds, tabs);
-  stage_ops_span<ST::kOpSet, kPre, kPreF>(lds, tabs);
+  stage_ops_span<ST::kOpSet>(lds, tabs);
   const uint32_t u = threadIdx.x & 63u;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t ureg = tabs[PDB_UNSHIFT_OFF + (u & 15u)];
   uint64_t t_start = 0;
-  uint32_t n_items = 0, n_batches = 0;
   uint64_t c_start = 0;
   constexpr bool kClk = MODE >= 40 && MODE <= 42;  // diagnostics: shader-clock stamps (tools/span_clock.py)
-  if constexpr (MODE == 4 || kClk) t_start = wall_clock64();
+  if constexpr (kClk) t_start = wall_clock64();
   if constexpr (kClk) c_start = clock64();
   // kGQ (the product since round 5): work units from 8 device-wide queues (wq), one per XCD;
   // MODE 44 = the round-2..4 scheme (each workgroup a fixed range of batches, its waves taking
@@ -551,7 +504,7 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16, MODE == 31>::kWaves * 
       sb &= sb - 1;
       const uintptr_t sp = static_cast<uintptr_t>(uniform64(__builtin_amdgcn_readlane(plo, k), __builtin_amdgcn_readlane(phi, k)));
       const uint32_t sn = __builtin_amdgcn_readlane(bn, k);
-      const uint32_t rs = span_slow_record<TP, kPre>(lds, lt, u, ureg, sp, sn);
+      const uint32_t rs = span_slow_record<TP>(lds, lt, u, ureg, sp, sn);
       if (u == 0)
         SinkOps<Sink>::put(sink, b_r0 + k, rs, BlkDesc{reinterpret_cast<const uint8_t*>(sp), sn, 0xFFFFFFFFu},
                            __builtin_amdgcn_readlane(bpre, k));
@@ -612,7 +565,7 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16, MODE == 31>::kWaves * 
     // halves -- records 0-7 | 8-15 (A) or 0-3, 8-11 | 4-7, 12-15 (C) -- and keep the better (bit
     // 16 r + 15 of bswap: row r takes C).
     bswap = 0;
-    if (MODE != 14 && bg.k == 4u && !bvar) {
+    if (bg.k == 4u && !bvar) {
       // the lane's 4 part-end residues: ew, ew - P, ew - 2P, ew - 3P (mod 32) = a rotation of one
       // constant mask; quad-OR, then per row the two splits' distinct-bank counts by DPP in lane
       // 16 r + 15 (row_shr 4: quads 0|1 and 2|3; row_shr 8: quads 0|2 and 1|3)
@@ -627,9 +580,7 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16, MODE == 31>::kWaves * 
       const uint32_t da = pa + static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(pa), 0x118, 0xF, 0xF, false));
       const uint32_t dc = pc + static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(pc), 0x114, 0xF, 0xF, false));
       bswap = __builtin_amdgcn_ballot_w64((u & 15u) == 15u && dc > da);
-      if constexpr (MODE == 15) bswap = (bswap & 0x8000ull) ? 0x8000800080008000ull : 0ull;  // row 0 decides for the batch
     }
-    if constexpr (MODE == 4) ++n_batches;
     return true;
   };
 
@@ -728,7 +679,7 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16, MODE == 31>::kWaves * 
       uint32_t rl, pr = 0, nr = 0;
       // k = 4, an item of 16 records aligned on a row of the batch: open_batch chose how to split
       // them into the two 32-lane halves (bswap)
-      if (MODE != 14 && bg.k == 4u && (g0 & 15u) == 0 && m == 16u && ((bswap >> (g0 | 15u)) & 1u))
+      if (bg.k == 4u && (g0 & 15u) == 0 && m == 16u && ((bswap >> (g0 | 15u)) & 1u))
         slot = (slot & 3u) | ((slot & 4u) << 1) | ((slot & 8u) >> 1);  // slot bits 2 and 3 exchanged
       act = slot < m;
       rl = act ? g0 + slot : u;
@@ -748,11 +699,6 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16, MODE == 31>::kWaves * 
   // non-temporal) from the item's uniform base, the descriptor's range check ending at its last
   // 16-B chunk: chunks past it read as zeros without touching memory (an empty item reads the
   // tables' first 16 B).  32-bit lane offsets, no per-chunk address arithmetic.
-  // kSkipWrites (the product since late round 4; MODE 39 = every chunk staged, before): the 1-KiB
-  // chunks wholly past the item's span + 64 B are not written to the region (the hash never reads
-  // them): +0.8 % on wal400, +2 % on random 300-500-B records, ±0.5 % elsewhere in A/B
-  // (profiles/r04/ab/ab_skiptail.log).  MODE 37 also skips their loads (no gain).
-  constexpr bool kSkipLoads = MODE == 37, kSkipWrites = MODE != 39;
   auto issue = [&](u32x4 (&A)[kSpanJ], const SpanItem& it) {
     const uint32_t lo_l = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(it.lo));
     const uint32_t lo_h = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(static_cast<uint64_t>(it.lo) >> 32));
@@ -761,36 +707,37 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16, MODE == 31>::kWaves * 
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(base, 0, static_cast<int>(nb), 0x00020000);
 #pragma unroll
     for (uint32_t j = 0; j < kSpanJ; ++j)
-      if (!kSkipLoads || j == 0 || 1024u * j < nb + 64u)
-        A[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, static_cast<int>(1024u * j + 16u * u), 0,
-                                                                                2 /* nt */));
+      A[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, static_cast<int>(1024u * j + 16u * u), 0,
+                                                                              2 /* nt */));
   };
-  // every chunk is written, the dummy ones too: a load whose register is never read stays
-  // outstanding, and the compiler then drains the counter before the register is reloaded
+  // The region receives the chunks below the item's end + 64 B, the rest are not written (+0.8 % on
+  // wal400, +2 % on random 300-500-B records in A/B, profiles/r04/ab/ab_skiptail.log): the hash
+  // reads a record's words as dword pairs ending within 4 B past the record's end and the p-word's
+  // pair within 8 B past its start, all below hi + 8, so the 64-B margin is never read past.  (The
+  // unwritten chunks' loads still complete before their registers are reloaded by the next issue().)
+  static_assert(64u >= 8u, "the staged margin covers the hash's read window past hi");
   auto to_lds = [&](const u32x4 (&A)[kSpanJ], const SpanItem& it) {
-    const uint32_t nw = __builtin_amdgcn_readfirstlane(it.hi) + 64u;  // (kSkipWrites: bytes the hash may read)
+    const uint32_t nw = __builtin_amdgcn_readfirstlane(it.hi) + 64u;
 #pragma unroll
     for (uint32_t j = 0; j + 1 < kSpanJ; ++j)
-      if (!kSkipWrites || j == 0 || 1024u * j < nw) *reinterpret_cast<u32x4*>(region + 1024u * j + 16u * u) = A[j];
-    if (!kSkipWrites || 1024u * (kSpanJ - 1u) < nw)
-      if (!kDyn || wv + 1u < kSpanWaves || u != 63u)  // the last 16 B of the LDS: the work counter
+      if (j == 0 || 1024u * j < nw) *reinterpret_cast<u32x4*>(region + 1024u * j + 16u * u) = A[j];
+    if (1024u * (kSpanJ - 1u) < nw)
+      if (kGQ || !kDyn || wv + 1u < kSpanWaves || u != 63u)  // MODE 44: the last 16 B of the LDS hold its counter
         *reinterpret_cast<u32x4*>(region + 1024u * (kSpanJ - 1u) + 16u * u) = A[kSpanJ - 1u];
   };
   // hash an item staged in the region
   auto hash = [&](const SpanItem& it) {
-    if constexpr (MODE == 4) ++n_items;
     if (it.hi == 0 || MODE == 1 || MODE == 3 || MODE == 41) return;
-    // chain X (A, B, C, D = 0..3) works from phase-2 step F[X] on; its word at step t is the one
+    // chain X (A, B, C, D = 0..3) works from lock-step step F[X] on; its word at step t is the one
     // ending 4 (NI - t) bytes before the chain's end
     constexpr int32_t FABC = static_cast<int32_t>(NI - LC), FD = static_cast<int32_t>(NI - LD);
     const uint32_t k = it.k, lim = it.iters - NI;
     const int32_t e = static_cast<int32_t>(it.e_loc);
     const int32_t pl = static_cast<int32_t>(it.p_loc);
     const bool act = it.p_loc != kNoRec;
-    // part, parts of the record after it (kVar: packed per lane; else from the uniform k)
+    // part (kVar: packed per lane with the record's parts after it; else from the uniform k)
     const uint32_t pc = kVar ? it.cw & 15u : it.cw;
-    // the record's parts after this one: >= m (kVar: packed per lane; else from the uniform k, the
-    // exact round-3 form of the uniform kernels)
+    // the record's parts after this one: >= m
     auto more = [&](uint32_t m) -> bool { return kVar ? ((it.cw >> 4) & 15u) >= m : pc + m < k; };
     const bool head = kVar ? ((it.cw >> 4) & 15u) == 0u : pc == k - 1u;
     const uint32_t sel = static_cast<uint32_t>(e & 3) * 0x01010101u + 0x03020100u;
@@ -803,158 +750,24 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16, MODE == 31>::kWaves * 
     const int32_t sp = act ? pl - static_cast<int32_t>(zp) : e;  // (no record: an address in range)
     uint32_t pw;
     {
-      const char* q = (MODE == 5 || MODE == 6) ? region + 4u * (u & 31u) : region + 4 * (sp >> 2);
+      const char* q = region + 4 * (sp >> 2);
       pw = (__builtin_amdgcn_perm(lds_u32(q, 4), lds_u32(q, 0), sel) & (0xFFFFFFFFu << (8u * zp))) ^ uz;
     }
-    // the p-word's phase-2 step in chain A's numbering; T + LC X in chain X's
+    // the p-word's lock-step step in chain A's numbering; T + LC X in chain X's
     const int32_t T = static_cast<int32_t>(NI) - ((eA - sp) >> 2);
-    // the last phase-2 step at which some lane of the item replaces a state (uniform; one bound for
-    // all four chains: per-chain masks cost more in branches than their selects save)
-    int32_t lmax = -1;
-#pragma unroll
-    for (int32_t X = 0; X < 4; ++X) {
-      const int32_t t = T + static_cast<int32_t>(LC) * X;
-      if (t >= (X == 3 ? FD : FABC) && t < static_cast<int32_t>(NI)) lmax = t;
-    }
-    const int32_t G = static_cast<int32_t>(wave_max_u32(act ? static_cast<uint32_t>(lmax + 1) : 0u)) - 1;
-    // kSparse (MODE 22): the (chain, step) pairs at which some lane of the item replaces a state, as
-    // one wave-uniform mask (bit 16 X + t), so the selects run only where one is due (equal-sized
-    // records: one or two pairs per item instead of every chain up to step G)
-    // kOneCmp (MODE 26): a lane replaces at most one (chain, step) pair (Xp, tp): one compare per
-    // step (tp == t) and-ed with per-item lane masks (Xp == X), instead of one compare per chain and step
-    int32_t tp = -1, xp = -1;
-    if constexpr (kOneCmp) {
-#pragma unroll
-      for (int32_t X = 0; X < 4; ++X) {
-        const int32_t t = T + static_cast<int32_t>(LC) * X;
-        if (t >= (X == 3 ? FD : FABC) && t < static_cast<int32_t>(NI)) tp = t, xp = X;
-      }
-    }
-    const bool pA = xp == 0, pB = xp == 1, pC = xp == 2, pD = xp == 3;
-    uint64_t mA = 0, mB = 0, mC = 0, mD = 0;
-    if constexpr (kMaskSel) {
-      mA = __ballot(pA), mB = __ballot(pB), mC = __ballot(pC), mD = __ballot(pD);
-    }
-    uint64_t selm = 0;
-    if constexpr (kSparse) {
-      uint32_t mlo = 0, mhi = 0;
-#pragma unroll
-      for (int32_t X = 0; X < 4; ++X) {
-        const int32_t t = T + static_cast<int32_t>(LC) * X;
-        if (act && t >= (X == 3 ? FD : FABC) && t < static_cast<int32_t>(NI)) {
-          if (X < 2) mlo |= 1u << (16 * X + t);
-          else mhi |= 1u << (16 * (X - 2) + t);
-        }
-      }
-      selm = (static_cast<uint64_t>(wave_or_u32(mhi)) << 32) | wave_or_u32(mlo);
-    }
-    // base of the chains' words: chain X's dword i at q3 + 4 LC (3 - X) + 4 i (word at phase-2
-    // step t = dwords t, t + 1); below the region for short records (words never used)
-    const char* q3 = (MODE == 5 || MODE == 6) ? region + 4u * (u & 31u)
-                                              : region + 4 * ((eA - static_cast<int32_t>(4u * NI + 12u * LC)) >> 2);
-    // kOpaqueBase (MODE 24): the chains' reads addressed as lds + qo + constant with qo opaque to the
-    // compiler, so every read takes its constant in the instruction's offset field (left to itself
-    // the compiler re-bases them on the highest address and computes each negative offset with a VALU)
-    // (MODE 25: one opaque base per chain, so no two chains' reads merge into a ds_read2_b32 whose
-    // result the compiler then waits for before the step's lookups)
-    uint32_t qo[4] = {0u, 0u, 0u, 0u};
-    if constexpr (kOpaqueBase) {
-      const uint32_t q0 = static_cast<uint32_t>(region - lds) +
-                          static_cast<uint32_t>(4 * ((eA - static_cast<int32_t>(4u * NI + 12u * LC)) >> 2));
-#pragma unroll
-      for (uint32_t X = 0; X < 4; ++X) {
-        qo[X] = q0 + (MODE == 25 ? 4u * LC * (3u - X) : 0u);
-        if (MODE == 25 || X == 0) asm volatile("" : "+v"(qo[X]));
-      }
-    }
-    // chain X's dword at byte offset `off` from q3 (off includes the chain's 4 LC (3 - X))
-    auto sread = [&](uint32_t X, uint32_t off) -> uint32_t {
-      if constexpr (kOpaqueBase)
-        return MODE == 25 ? lds_u32(lds, qo[X] + off - 4u * LC * (3u - X)) : lds_u32(lds, qo[0] + off);
-      else
-        return lds_u32(q3, off);
-    };
+    // base of the chains' words: chain X's dword i at q3 + 4 LC (3 - X) + 4 i (word at step t =
+    // dwords t, t + 1); below the region for short records (words never used)
+    const int32_t qd = (eA - static_cast<int32_t>(4u * NI + 12u * LC)) >> 2;  // q3's dword (region-relative)
+    const char* q3 = region + 4 * qd;
+    // the chains' reads are addressed as lds + qo + constant with qo opaque to the compiler, so every
+    // read takes its constant in the instruction's offset field (left to itself the compiler re-bases
+    // them on the highest address and computes each negative offset with a VALU; +1.9-2.1 % on
+    // wal400 / wal1000 / wal in A/B, profiles/r04/ab_variants_r04d.log)
+    uint32_t qo = static_cast<uint32_t>(region - lds) + static_cast<uint32_t>(4 * qd);
+    asm volatile("" : "+v"(qo));
+    auto sread = [&](uint32_t off) -> uint32_t { return lds_u32(lds, qo + off); };
     uint32_t xd = 0, ld = 0;
     uint32_t xa = 0, xb = 0, xc = 0;
-    const int32_t qd = (eA - static_cast<int32_t>(4u * NI + 12u * LC)) >> 2;  // q3's dword (region-relative)
-    if constexpr (kRot) {
-      // the head chain alone for lim steps (junk on the other lanes, dropped), then chain D's step 0
-      // on every lane; chain D's dword i at q3 + 4 i (FD = 0)
-      const char* qh = q3 - 4 * static_cast<int32_t>(lim);
-      ld = lds_u32(qh, 0);
-      if (lim > 0) {
-        const int32_t tD = T + static_cast<int32_t>(3u * LC + lim);  // the p-word's step in it
-        for (int32_t t = 0; t < static_cast<int32_t>(lim); ++t, qh += 4) {
-          const uint32_t h = lds_u32(qh, 4);
-          const uint32_t w = __builtin_amdgcn_perm(h, ld, sel);
-          ld = h;
-          xd = t == tD ? pw : TP::step(lds, lt, xd, w);
-        }
-        xd = head ? xd : 0u;
-      }
-      xd = TP::step(lds, lt, xd, __builtin_amdgcn_perm(lds_u32(qh, 4), ld, sel));
-      xd = T + static_cast<int32_t>(3u * LC) == 0 ? pw : xd;
-      // steps 1 .. NI - 1: all four chains, in slots.  Slot i of this lane holds chain
-      // X_i = (i + rho) & 3, whose dword at step t is q3's dword + 8 (3 - X_i) + t + 1: bank
-      // (q3's dword mod 8) + 8 ((rank - i) mod 4) + t + 1 mod 32 with rank = a + 3 - rho (a = bits
-      // 3-4 of q3's dword).  rank = this lane's place among the lanes of its class (q3's dword mod 8),
-      // so up to four lanes of a class read four different banks in every slot.
-      const uint32_t qdw = (static_cast<uint32_t>(region - lds) >> 2) + static_cast<uint32_t>(qd);
-      // (records of >= 4 parts: a record's lanes are in different classes -- parts 33 words = 1 mod 8
-      // apart -- so the record's slot in the batch ranks it; fewer parts: ranked by ballots)
-      const uint32_t cls = qdw & 7u, a = (qdw >> 3) & 3u;
-      uint32_t rank = it.r;
-      if (k < 4u) {
-        const uint64_t m0 = __ballot((cls & 1u) != 0), m1 = __ballot((cls & 2u) != 0), m2 = __ballot((cls & 4u) != 0);
-        const uint64_t same = ((cls & 1u) ? m0 : ~m0) & ((cls & 2u) ? m1 : ~m1) & ((cls & 4u) ? m2 : ~m2);
-        rank = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(same >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(same), 0u));
-      }
-      const uint32_t rho = (a + 3u - rank) & 3u;
-      // a lane replaces at most one (chain, step): chain xr at step tr (-1: none), in slot ir
-      int32_t tr = -1, xr = 0;
-#pragma unroll
-      for (int32_t X = 0; X < 4; ++X) {
-        const int32_t t = T + static_cast<int32_t>(LC) * X;
-        if (t >= 1 && t < static_cast<int32_t>(NI)) tr = t, xr = X;
-      }
-      const uint32_t ir = (static_cast<uint32_t>(xr) - rho) & 3u, iD = (3u - rho) & 3u;
-      uint32_t xs[4], ls[4], qs[4];
-      int32_t tri[4];  // slot i's replacement step (-1: none)
-#pragma unroll
-      for (uint32_t i = 0; i < 4; ++i) {
-        tri[i] = ir == i ? tr : -1;
-        qs[i] = 4u * qdw + 32u * (3u - ((i + rho) & 3u));
-        asm volatile("" : "+v"(qs[i]));
-        ls[i] = lds_u32(lds, qs[i] + 4u);
-      }
-      const uint32_t TD = TP::step(lds, lt, xd, 0u);  // chain D's state stepped (its word added at step 1)
-#pragma unroll
-      for (int32_t t = 1; t < static_cast<int32_t>(NI); ++t) {
-        uint32_t ws[4];
-#pragma unroll
-        for (uint32_t i = 0; i < 4; ++i) {
-          const uint32_t h = lds_u32(lds, qs[i] + 4u * static_cast<uint32_t>(t + 1));
-          ws[i] = __builtin_amdgcn_perm(h, ls[i], sel);
-          ls[i] = h;
-        }
-        if (t == 1) {
-#pragma unroll
-          for (uint32_t i = 0; i < 4; ++i) xs[i] = ws[i] ^ (iD == i ? TD : 0u);
-        } else {
-          TP::step4(lds, lt, xs, ws);
-        }
-        if (t <= G) {
-#pragma unroll
-          for (uint32_t i = 0; i < 4; ++i) xs[i] = tri[i] == t ? pw : xs[i];
-        }
-      }
-      // chain X is in slot (X - rho) & 3
-      auto pick = [&](uint32_t X) -> uint32_t {
-        const uint32_t i = (X - rho) & 3u;
-        return i == 0u ? xs[0] : (i == 1u ? xs[1] : (i == 2u ? xs[2] : xs[3]));
-      };
-      xa = pick(0u), xb = pick(1u), xc = pick(2u), xd = pick(3u);
-    } else {
     if (lim > 0) {  // the head chain alone (junk on the other lanes, dropped)
       const int32_t tD = T + static_cast<int32_t>(3u * LC + lim) - FD;  // the p-word's step in it
       const char* q = q3 + 4 * (FD - static_cast<int32_t>(lim));
@@ -966,87 +779,26 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16, MODE == 31>::kWaves * 
         xd = t == tD ? pw : TP::step(lds, lt, xd, w);
       }
       xd = head ? xd : 0u;
-    } else if constexpr (MODE != 19) {  // (kPairs: read below)
-      ld = sread(3, 4u * FD);
+    } else {
+      ld = sread(4u * FD);
     }
     // The chains' words: one ds_read_b32 per word and chain (the dword after the previous one).
-    // kPairs (MODE 19, diagnostics): every chain's dwords as 8-B aligned ds_read_b64 pairs from
-    // q3e (q3 rounded down to 8 B; par = q3's dword parity), one pair every two steps, dword i =
-    // pair dword i + par (one v_cndmask).  An aligned b64 costs the LDS ~2.5 cycles against ~2.2
-    // for a b32 (tools/lds_probe.hip, profiles/r04/lds_probe.log; a 4-B aligned b64 / b128 ~27-29),
-    // but in the kernel the pairs measured 2.5-9 % SLOWER on every WAL row (profiles/r04/
-    // ab_pairs.log: the extra live pair registers and selects; 168 VGPRs and spills in the 9-KiB
-    // classes), so the product keeps the dword reads.
-    constexpr bool kPairs = MODE == 19;
-    const bool par = (qd & 1) != 0;
-    // chain X's pairs: pair j = dwords 2 j, 2 j + 1 above qb[X] (8-B aligned; chains A, B, C, D at
-    // 3 LC, 2 LC, LC, 0 words above q3).  Each chain keeps the last two pairs read (P newest, Q);
-    // the base offsets are made opaque so the compiler keeps one ds_read_b64 per pair: merged into
-    // a ds_read2_b64 (two 8-B accesses, 8 LDS cycles) they would cost more than the dword reads.
-    uint32_t qb[4];
-    u32x2 Pp[4], Qp[4];
-#pragma unroll
-    for (uint32_t X = 0; X < 4; ++X) {
-      qb[X] = static_cast<uint32_t>(region - lds) + static_cast<uint32_t>(8 * (qd >> 1)) + 32u * (3u - X);
-      if constexpr (kPairs) asm volatile("" : "+v"(qb[X]));
-      Pp[X] = u32x2{0u, 0u}, Qp[X] = u32x2{0u, 0u};
-    }
-    auto pair_in = [&](uint32_t X, uint32_t j) {
-      Qp[X] = Pp[X];
-      Pp[X] = *reinterpret_cast<const u32x2*>(lds + qb[X] + 8u * j);
-    };
-    uint32_t la = 0, lb = 0, lc = 0;
-    if constexpr (kPairs) {
-      // dword F (+ par) of each chain: F even: pair F / 2; F odd: pairs (F - 1) / 2 and (F + 1) / 2
-      uint32_t d0[4];
-#pragma unroll
-      for (uint32_t X = 0; X < 4; ++X) {
-        const uint32_t F = X == 3 ? static_cast<uint32_t>(FD) : static_cast<uint32_t>(FABC);
-        if ((F & 1u) == 0) {
-          pair_in(X, F >> 1);
-          d0[X] = par ? Pp[X].y : Pp[X].x;
-        } else {
-          pair_in(X, F >> 1);
-          pair_in(X, (F + 1u) >> 1);
-          d0[X] = par ? Pp[X].x : Qp[X].y;
-        }
-      }
-      la = d0[0], lb = d0[1], lc = d0[2], ld = d0[3];
-    } else {
-      la = sread(0, 12u * LC + 4u * FABC), lb = sread(1, 8u * LC + 4u * FABC);
-      lc = sread(2, 4u * LC + 4u * FABC);
-    }
-    // dword t + 1 (+ par) of chain X at step t: even t reads pair t / 2 + 1 first
-    auto next_dw = [&](uint32_t X, int32_t t) -> uint32_t {
-      if ((t & 1) == 0) {
-        pair_in(X, static_cast<uint32_t>(t + 2) >> 1);
-        return par ? Pp[X].x : Qp[X].y;
-      }
-      return par ? Pp[X].y : Pp[X].x;
-    };
+    // (Aligned ds_read_b64 pairs measured 2.5-9 % slower on every WAL row, profiles/r04/ab_pairs.log:
+    // the extra live pair registers and selects.)
+    uint32_t la = sread(12u * LC + 4u * FABC), lb = sread(8u * LC + 4u * FABC), lc = sread(4u * LC + 4u * FABC);
 #pragma unroll
     for (int32_t t = 0; t < static_cast<int32_t>(NI); ++t) {
       const bool abc = t >= FABC, dd = t >= FD;  // compile time
       uint32_t wa = 0, wb = 0, wc = 0, wd = 0;
       if (abc) {
-        uint32_t ha, hb, hc;
-        if constexpr (kPairs) {
-          ha = next_dw(0, t), hb = next_dw(1, t), hc = next_dw(2, t);
-        } else {
-          ha = sread(0, 12u * LC + 4u * (t + 1)), hb = sread(1, 8u * LC + 4u * (t + 1));
-          hc = sread(2, 4u * LC + 4u * (t + 1));
-        }
+        const uint32_t ha = sread(12u * LC + 4u * (t + 1)), hb = sread(8u * LC + 4u * (t + 1));
+        const uint32_t hc = sread(4u * LC + 4u * (t + 1));
         wa = __builtin_amdgcn_perm(ha, la, sel), wb = __builtin_amdgcn_perm(hb, lb, sel);
         wc = __builtin_amdgcn_perm(hc, lc, sel);
         la = ha, lb = hb, lc = hc;
       }
       if (dd) {
-        uint32_t hd;
-        if constexpr (kPairs) {
-          hd = next_dw(3, t);
-        } else {
-          hd = sread(3, 4u * (t + 1));
-        }
+        const uint32_t hd = sread(4u * (t + 1));
         wd = __builtin_amdgcn_perm(hd, ld, sel);
         ld = hd;
       }
@@ -1059,121 +811,55 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16, MODE == 31>::kWaves * 
         TP::step4(lds, lt, x4, w4);
         xa = x4[0], xb = x4[1], xc = x4[2], xd = x4[3];
       } else if (abc) {
-        if constexpr (MODE == 13) {  // A/B: three separate steps (round 2)
-          xa = TP::step(lds, lt, xa, wa);
-          xb = TP::step(lds, lt, xb, wb);
-          xc = TP::step(lds, lt, xc, wc);
-        } else {
-          uint32_t x3[3] = {xa, xb, xc};
-          const uint32_t w3[3] = {wa, wb, wc};
-          TP::step3(lds, lt, x3, w3);
-          xa = x3[0], xb = x3[1], xc = x3[2];
-        }
+        uint32_t x3[3] = {xa, xb, xc};
+        const uint32_t w3[3] = {wa, wb, wc};
+        TP::step3(lds, lt, x3, w3);
+        xa = x3[0], xb = x3[1], xc = x3[2];
       } else if (dd) {
         xd = TP::step(lds, lt, xd, wd);
       }
-      if constexpr (kSparse) {
-        if (abc) {
-          if ((selm >> t) & 1u) xa = T == t ? pw : xa;
-          if ((selm >> (16 + t)) & 1u) xb = T + static_cast<int32_t>(LC) == t ? pw : xb;
-          if ((selm >> (32 + t)) & 1u) xc = T + static_cast<int32_t>(2u * LC) == t ? pw : xc;
-        }
-        if (dd && ((selm >> (48 + t)) & 1u)) xd = T + static_cast<int32_t>(3u * LC) == t ? pw : xd;
-      } else if (kMaskSel && (kNoG || t <= G)) {
-        const uint64_t hm = __ballot(tp == t);
-        if (abc) {
-          xa = __builtin_amdgcn_inverse_ballot_w64(hm & mA) ? pw : xa;
-          xb = __builtin_amdgcn_inverse_ballot_w64(hm & mB) ? pw : xb;
-          xc = __builtin_amdgcn_inverse_ballot_w64(hm & mC) ? pw : xc;
-        }
-        if (dd) xd = __builtin_amdgcn_inverse_ballot_w64(hm & mD) ? pw : xd;
-      } else if (kOneCmp && t <= G) {
-        const bool hit = tp == t;
-        if (abc) {
-          xa = hit && pA ? pw : xa;
-          xb = hit && pB ? pw : xb;
-          xc = hit && pC ? pw : xc;
-        }
-        if (dd) xd = hit && pD ? pw : xd;
-      } else if (MODE != 7 && (kNoG || t <= G)) {
-        if (abc) {
-          xa = T == t ? pw : xa;
-          xb = T + static_cast<int32_t>(LC) == t ? pw : xb;
-          xc = T + static_cast<int32_t>(2u * LC) == t ? pw : xc;
-        }
-        if (dd) xd = T + static_cast<int32_t>(3u * LC) == t ? pw : xd;
+      // the p-word replaces its chain's state: branch-free selects on every step (+0.1-3 % over
+      // selects bounded by the item's last replacement step, profiles/r04/ab/ab_nog.log)
+      if (abc) {
+        xa = T == t ? pw : xa;
+        xb = T + static_cast<int32_t>(LC) == t ? pw : xb;
+        xc = T + static_cast<int32_t>(2u * LC) == t ? pw : xc;
       }
+      if (dd) xd = T + static_cast<int32_t>(3u * LC) == t ? pw : xd;
     }
-    }  // !kRot
     // Finish.  Chain X's state still holds its last word unshifted, and its bytes end 32 X bytes
     // before the part's end, so the part's raw CRC is F(xA) ^ S32 F(xB) ^ S64 F(xC) ^ S96 F(xD)
     // with F = the table step (shift 4) and S_n = shift n; these maps commute, so it is
     // F(S64(S32(xD) ^ xC) ^ (S32(xB) ^ xA)), and across the k parts of a record
-    // F(sum_c S_{4 PART c}(R_c)): ONE table step after the cross-lane tree (round 2: a table step
-    // per chain before the folds, 28 lookups instead of 16 per lane; diagnostics mode 10).
+    // F(sum_c S_{4 PART c}(R_c)): ONE table step after the cross-lane fold.
     // A chain whose end is at or before the p-word's start holds no byte of the record.
     const int32_t L = static_cast<int32_t>(NI);
-    constexpr bool kOldFold = MODE == 10;
-    uint32_t x4[4] = {xa, xb, xc, xd};
-    if constexpr (kOldFold) {
-      const uint32_t z4[4] = {0u, 0u, 0u, 0u};
-      TP::step4(lds, lt, x4, z4);
-    }
-    const uint32_t ca = T < L ? x4[0] : 0u;
-    const uint32_t cb = T + static_cast<int32_t>(LC) < L ? x4[1] : 0u;
-    const uint32_t cc = T + static_cast<int32_t>(2u * LC) < L ? x4[2] : 0u;
-    const uint32_t cd = T + static_cast<int32_t>(3u * LC) < L ? x4[3] : 0u;
+    const uint32_t ca = T < L ? xa : 0u;
+    const uint32_t cb = T + static_cast<int32_t>(LC) < L ? xb : 0u;
+    const uint32_t cc = T + static_cast<int32_t>(2u * LC) < L ? xc : 0u;
+    const uint32_t cd = T + static_cast<int32_t>(3u * LC) < L ? xd : 0u;
     static_assert(LC == 8, "the in-part folds use the 32- and 64-B operators");
-    auto opx = [&](uint32_t slot, uint32_t c, uint32_t y) -> uint32_t {
-      if constexpr (MODE == 6) {  // pricing: lane-skewed dwords of the operator rows (conflict-free)
-        uint32_t v[4];
-#pragma unroll
-        for (uint32_t j = 0; j < 4; ++j) {
-          const uint32_t bb = __builtin_amdgcn_perm(0u, c, 0x0C0C0000u | (j << 8) | j);
-          v[j] = lds_u32(lds, (bb & 0xFF00u) ^ (128u | (((u + 8u * j + slot) & 31u) << 2)));
-        }
-        return xor3(xor3(v[0], v[1], v[2]), v[3], y);
-      } else {
-        return span_op_x(lds, slot, c, y);
-      }
-    };
-    const uint32_t lo2 = MODE == 9 ? cb ^ ca : opx(kOp32, cb, ca);  // S32(B) ^ A
-    const uint32_t hi2 = MODE == 9 ? cd ^ cc : opx(kOp32, cd, cc);  // S32(D) ^ C
-    uint32_t P = MODE == 9 ? hi2 ^ lo2 : opx(kOp64, hi2, lo2);      // S64(hi2) ^ lo2
-    // parts c + m: the 4 PART m bytes before.  k a power of two: a record's k lanes never straddle
-    // a row of 16, so the partner's value comes by DPP row_shl (no LDS round trip); other k by
-    // bpermute.
-    if (kPre && k > 1u) {
-      // lane c: P = shift(R_c, 4 PART (c mod 4)) (slots P1, P2, P3 chosen per lane), XOR-reduced within
-      // the record's quad; a record of > 4 parts: the upper quad's sum shifted by 4 parts (P4) onto
-      // the lower's -- one operator level for k <= 4 (two for k <= 8) instead of log2(k)
+    const uint32_t lo2 = span_op_x(lds, kOp32, cb, ca);  // S32(B) ^ A
+    const uint32_t hi2 = span_op_x(lds, kOp32, cd, cc);  // S32(D) ^ C
+    uint32_t P = span_op_x(lds, kOp64, hi2, lo2);        // S64(hi2) ^ lo2
+    if (k > 1u) {
+      // the cross-lane fold, pre-shifted per lane: lane c applies shift(R_c, 4 PART (c mod 4)) (slots
+      // P1, P2, P3 chosen per lane), the record's quad XOR-reduces, and a record of > 4 parts adds
+      // the upper quad's sum shifted by 4 parts (P4) -- one operator level for k <= 4, two for k <= 8
+      // (+0.2-1.7 % over the round-3 tree of levels P1, P2, P4, profiles/r04/ab_variants.log).
+      // k a power of two: a record's k lanes never straddle a row of 16, so the partner's value
+      // comes by DPP row_shl (no LDS round trip); other k by bpermute.
       const bool dpp = (k & (k - 1u)) == 0 && !(kVar && it.var);
       const uint32_t l = pc & 3u;
       const uint32_t slot = l == 1u ? kOpP1 : (l == 2u ? kOpP2 : kOpP3);
       uint32_t v[4];
-      if constexpr (kPreF) {
-        // instruction i: byte jb = 3 - k of P, k = (quarter + i) & 3 (the T step's lane-quarter
-        // order); lanes of part 0 mod 4 read T_k (replica lane & 7), the others sub-table jb of
-        // their slot -- every lane's four lookups cover its four bytes
-        const uint32_t q = (u >> 3) & 3u;
 #pragma unroll
-        for (uint32_t i = 0; i < 4; ++i) {
-          const uint32_t kk = (q + i) & 3u, jb = 3u - kk;
-          const uint32_t aT = __builtin_amdgcn_perm(lt.t[i], P, lt.s[i]);
-          const uint32_t bb = __builtin_amdgcn_perm(0u, P, 0x0C0C0000u | (jb << 8) | jb);
-          const uint32_t aO = (bb & 0xFF7Cu) ^ (128u | ((4u * slot + jb) << 2));
-          v[i] = lds_u32(lds, l ? aO : aT);
-        }
-        P = xor3(xor3(v[0], v[1], v[2]), v[3], 0u);
-      } else {
-#pragma unroll
-        for (uint32_t j = 0; j < 4; ++j) {
-          const uint32_t bb = __builtin_amdgcn_perm(0u, P, 0x0C0C0000u | (j << 8) | j);
-          v[j] = lds_u32(lds, (bb & 0xFF7Cu) ^ (128u | ((4u * slot + j) << 2)));
-        }
-        const uint32_t Ps = xor3(xor3(v[0], v[1], v[2]), v[3], 0u);
-        P = l ? Ps : P;
+      for (uint32_t j = 0; j < 4; ++j) {
+        const uint32_t bb = __builtin_amdgcn_perm(0u, P, 0x0C0C0000u | (j << 8) | j);
+        v[j] = lds_u32(lds, (bb & 0xFF7Cu) ^ (128u | ((4u * slot + j) << 2)));
       }
+      const uint32_t Ps = xor3(xor3(v[0], v[1], v[2]), v[3], 0u);
+      P = l ? Ps : P;
       uint32_t y = dpp ? static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(P), 0x101, 0xF, 0xF, false))
                        : __shfl_down(P, 1, 64);
       if ((pc & 1u) == 0 && more(1u)) P ^= y;
@@ -1185,25 +871,10 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16, MODE == 31>::kWaves * 
       if (k > 4u) {
         y = dpp ? static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(P), 0x104, 0xF, 0xF, false))
                 : __shfl_down(P, 4, 64);
-        if ((pc & 7u) == 0 && more(4u)) P = opx(kOpP4, y, P);
-      }
-    } else if (MODE != 8 && k > 1u) {
-      const bool dpp = MODE != 11 && !kOldFold && (k & (k - 1u)) == 0 && !(kVar && it.var);
-      uint32_t y = dpp ? static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(P), 0x101, 0xF, 0xF, false))
-                       : __shfl_down(P, 1, 64);
-      if ((pc & 1u) == 0 && more(1u)) P = opx(kOpP1, y, P);
-      if (k > 2u) {
-        y = dpp ? static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(P), 0x102, 0xF, 0xF, false))
-                : __shfl_down(P, 2, 64);
-        if ((pc & 3u) == 0 && more(2u)) P = opx(kOpP2, y, P);
-      }
-      if (k > 4u) {
-        y = dpp ? static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(P), 0x104, 0xF, 0xF, false))
-                : __shfl_down(P, 4, 64);
-        if ((pc & 7u) == 0 && more(4u)) P = opx(kOpP4, y, P);
+        if ((pc & 7u) == 0 && more(4u)) P = span_op_x(lds, kOpP4, y, P);
       }
     }
-    if (!kOldFold && !(kPreF && k > 1u)) P = TP::step(lds, lt, P, 0u);  // F: the chains' last words
+    P = TP::step(lds, lt, P, 0u);  // F: the chains' last words
     if constexpr (MODE == 18)  // diagnostics: the item's first record, records, lane, lanes, mode
       P = ~(((it.cw >> 16) << 24) | (((it.cw >> 8) & 127u) << 16) | (u << 8) | ((kVar ? pc + ((it.cw >> 4) & 15u) + 1u : k) << 4) | (it.var ? 1u : 0u));
     if (pc == 0 && act)
@@ -1212,47 +883,30 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16, MODE == 31>::kWaves * 
 
   // ---- pipeline: two items in flight while one is hashed ---------------------------------------
   // Loop head: the region holds I0, array B holds I1's loads in flight; only B's loads cross the
-  // back edge.
-  // kOneDeep (diagnostics MODE 30 / 31): one item's loads in flight while one is hashed (half the
-  // staging registers), the loop: issue(next) -> hash(cur) -> to_lds(next)
-  constexpr bool kOneDeep = MODE == 30 || MODE == 31;
-  if (!nx_ok) {
-    // no unit for this wave: straight to the exit count
-  } else if constexpr (kOneDeep) {
-    u32x4 A[kSpanJ];
+  // back edge.  (One item in flight -- half the staging registers, 13 waves of 7 KiB -- measured
+  // slower, profiles/r04/ab/ab_onedeep_13waves.log.)
+  if (nx_ok) {
+    u32x4 A[kSpanJ], B[kSpanJ];
     SpanItem I0 = next_item(true);
     issue(A, I0);
+    SpanItem I1 = next_item(I0.valid);
+    issue(B, I1);
     to_lds(A, I0);
     while (I0.valid) {
-      const SpanItem I1 = next_item(true);
-      issue(A, I1);
+      const SpanItem I2 = next_item(I1.valid);
+      issue(A, I2);
       hash(I0);
       if (!I1.valid) break;
-      to_lds(A, I1);
-      I0 = I1;
+      to_lds(B, I1);
+      const SpanItem I3 = next_item(I2.valid);
+      issue(B, I3);
+      hash(I1);
+      if (!I2.valid) break;
+      to_lds(A, I2);
+      I0 = I2;
+      I1 = I3;
     }
-  } else {
-  u32x4 A[kSpanJ], B[kSpanJ];
-  SpanItem I0 = next_item(true);
-  issue(A, I0);
-  SpanItem I1 = next_item(I0.valid);
-  issue(B, I1);
-  to_lds(A, I0);
-  while (I0.valid) {
-    const SpanItem I2 = next_item(I1.valid);
-    issue(A, I2);
-    hash(I0);
-    if (!I1.valid) break;
-    to_lds(B, I1);
-    const SpanItem I3 = next_item(I2.valid);
-    issue(B, I3);
-    hash(I1);
-    if (!I2.valid) break;
-    to_lds(A, I2);
-    I0 = I2;
-    I1 = I3;
   }
-  }  // !kOneDeep
   if constexpr (kGQ) {
     // the last wave out (every wave counts itself once, after its last ticket came back) resets the
     // queue words for the next launch on this stream
@@ -1264,17 +918,17 @@ __global__ __launch_bounds__((SpanStage<MAXN, MODE == 16, MODE == 31>::kWaves * 
       }
     }
   }
-  if constexpr (MODE == 4 || kClk) {
+  if constexpr (kClk) {
     // MODE 40 / 41 / 42 (the product / loads alone / hash alone): [start, end] s_memrealtime (100 MHz)
     // and [start, end] s_memtime (shader clock): the wave's mean clock over its lifetime
     const uint64_t t_end = wall_clock64();
-    const uint64_t c_end = kClk ? clock64() : 0;
+    const uint64_t c_end = clock64();
     if (u == 0) {
       uint64_t* st = sink.stamps + 4u * (static_cast<uint64_t>(blockIdx.x) * kSpanWaves + wv);
       st[0] = t_start;
       st[1] = t_end;
-      st[2] = kClk ? c_start : n_items;
-      st[3] = kClk ? c_end : n_batches;
+      st[2] = c_start;
+      st[3] = c_end;
     }
   }
 }
@@ -1295,11 +949,11 @@ hipError_t launch_lanespan(const LaunchGeom& g, const uint32_t* d_tables, const 
   uint32_t* wq = g.wq;
   if (kDyn && MODE != 44 && wq == nullptr) return hipErrorInvalidValue;
   if (cls <= 256u) {
-    constexpr uint32_t w = SpanStage<256, MODE == 16, MODE == 31>::kWaves;
+    constexpr uint32_t w = SpanStage<256>::kWaves;
     hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 256, MODE, TP, kDyn>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0, s,
                        d_tables, src, nblk, sink, wq);
   } else if (cls <= 512u) {
-    constexpr uint32_t w = SpanStage<512, MODE == 16, MODE == 31>::kWaves;
+    constexpr uint32_t w = SpanStage<512>::kWaves;
     if (mixed && !__is_same(Sink, VerifySink))
       hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 512, MODE, TP, kDyn, true>), dim3(grid_span(g, nblk, w)), dim3(w * 64),
                          0, s, d_tables, src, nblk, sink, wq);
@@ -1307,7 +961,7 @@ hipError_t launch_lanespan(const LaunchGeom& g, const uint32_t* d_tables, const 
       hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 512, MODE, TP, kDyn>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0, s,
                          d_tables, src, nblk, sink, wq);
   } else if (cls <= 1023u) {
-    constexpr uint32_t w = SpanStage<1023, MODE == 16, MODE == 31>::kWaves;
+    constexpr uint32_t w = SpanStage<1023>::kWaves;
     if (mixed && !__is_same(Sink, VerifySink))
       hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 1023, MODE, TP, kDyn, true>), dim3(grid_span(g, nblk, w)), dim3(w * 64),
                          0, s, d_tables, src, nblk, sink, wq);
@@ -1315,7 +969,7 @@ hipError_t launch_lanespan(const LaunchGeom& g, const uint32_t* d_tables, const 
       hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 1023, MODE, TP, kDyn>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0,
                          s, d_tables, src, nblk, sink, wq);
   } else {  // 1024..1152 B (WAL records of ~1-KiB write batches): 8 lanes, the head chain past 1056 B
-    constexpr uint32_t w = SpanStage<1152, MODE == 16, MODE == 31>::kWaves;
+    constexpr uint32_t w = SpanStage<1152>::kWaves;
     hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 1152, MODE, TP, kDyn>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0,
                        s, d_tables, src, nblk, sink, wq);
   }

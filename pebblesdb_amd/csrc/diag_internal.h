@@ -10,9 +10,8 @@ hipError_t launch_fixed_variant(int v, const LaunchGeom& g, const uint32_t* d_ta
                                 uint32_t* out, hipStream_t s);
 hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tables, const uint8_t* base,
                                const pdb_blk* blk, uint64_t nblk, uint32_t flags, uint32_t* out, hipStream_t s);
-// sstable hooks: 18 = crc_stream_kernel (32-B pieces), 30 = crc_stream16_kernel (the round-1
-// default), 31-37 seal-write diagnostics, 38 8-block groups, 97 verify without the Horner folds
-// (wrong CRCs by design); other ids = the shipped kernel
+// sstable hooks: 18 = crc_stream_kernel (32-B pieces), 72 = the seal without trailer parking,
+// 140 / 141 = the seal's memory pattern without the hash; other ids = the shipped routing
 hipError_t launch_sst_variant(int v, const LaunchGeom& g, const uint32_t* d_tables, uint8_t* buf, uint64_t buf_len,
                               const pdb_block_handle* h, uint64_t n, bool seal, uint8_t* ok, uint32_t* nbad,
                               hipStream_t s);

@@ -1,17 +1,17 @@
 // diag_variants.hip -- BENCH / TEST INFRASTRUCTURE (libpdb_crc32c_diag.so, never linked into the
-// product): the A/B kernel variants measured against the shipped kernels (selected per call through
-// include/pdb_crc32c_diag.h, all parity-tested in tests/test_gpu_parity.py), the load-pattern
-// calibration kernels behind the roofline numbers in DESIGN.md §6, and the synthetic-input fill.
-#include <mutex>
-
-#include "diag_device.h"
+// product): the synthetic-input fill, the load-pattern calibration kernels behind the roofline and
+// pattern-ceiling numbers, the record kernel's part / clock / work-distribution
+// diagnostics, and the few alternative kernels the parity tests use as independent cross-checks of
+// the product's routing.  Selected per call through include/pdb_crc32c_diag.h.  (The round-1..4
+// A/B variants that lost are recorded in DESIGN.md's appendix; round 5 removed them.)
+#include "crc32c_device.h"
 #include "crc32c_lanespan.h"
 #include "diag_internal.h"
 
 namespace pdb {
 namespace {
 
-// variant 110: the record kernel with per-wave timestamps, stored after the CRCs in `out`
+// variants 180-182: the record kernel with per-wave clock stamps, stored after the CRCs in `out`
 struct StampOutSink : OutSink {
   uint64_t* stamps;
 };
@@ -44,235 +44,7 @@ __global__ __launch_bounds__(256) void fill_splitmix_kernel(uint8_t* __restrict_
   }
 }
 
-template <int kNP, int kDepth, bool kIssueFirst = false>
-__global__ __launch_bounds__(kThreads) void crc_fast4k_kernel(
-    const uint32_t* __restrict__ tabs, const uint8_t* __restrict__ base, uint64_t stride,
-    uint64_t nblk, uint32_t flags, uint32_t init, uint32_t* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
-  char* lds = reinterpret_cast<char*>(lds_words);
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWavesPerWg;
-  const uint64_t b0 = wave_id_uniform();
-  // Issue the first kDepth blocks' loads before staging the tables: the table copy then
-  // overlaps the first HBM round trip.
-  u32x4 buf[kDepth][4];
-#pragma unroll
-  for (int k = 0; k < kDepth; ++k) {
-    const uint64_t b = b0 + k * nw;
-    load4k<kNP>(buf[k], base, stride, b < nblk ? b : (nblk - 1), lane);
-  }
-  constexpr int kTree = kNP == 1 ? PDB_CAT_TREE64 : (kNP == 2 ? PDB_CAT_TREE32 : PDB_CAT_TREE16);
-  constexpr int kHorner = kNP == 1 ? PDB_CAT_TREE32 : (kNP == 2 ? PDB_CAT_S2048 : PDB_CAT_S1024);
-  stage_tables<kTree, kHorner>(lds, tabs);
-  __syncthreads();
-  const LaneTabs lt = lane_tabs(lane);
-  const uint32_t init_raw = (flags & PDB_CRC_USE_INIT) ? ~init : 0xFFFFFFFFu;
-  // Results are parked in a register (lane j holds the j-th block's CRC of the current 64-block
-  // window) and flushed with one scattered 64-lane store per window: a per-block store from
-  // lane 0 would sit in vmcnt behind the next block's loads and make every wait drain it.
-  uint32_t res = 0;
-  uint32_t it = 0;
-  uint64_t win0 = b0;  // first block of the current window
-  for (uint64_t b = b0; b < nblk; b += kDepth * nw) {
-#pragma unroll
-    for (int k = 0; k < kDepth; ++k) {
-      const uint64_t bk = b + k * nw;
-      if (bk >= nblk) break;  // wave-uniform
-      u32x4 cur[4] = {buf[k][0], buf[k][1], buf[k][2], buf[k][3]};
-      const uint64_t bn = bk + kDepth * nw;
-      load4k<kNP>(buf[k], base, stride, bn < nblk ? bn : bk, lane);  // clamp: valid block
-      if constexpr (kIssueFirst) __builtin_amdgcn_sched_barrier(0);
-      const uint32_t c = hash4k<kNP>(lds, lt, lane, lane == 0 ? init_raw : 0u, cur);
-      const uint32_t v = finalize(__builtin_amdgcn_readfirstlane(c), flags);
-      if (lane == (it & 63u)) res = v;
-      if ((++it & 63u) == 0) {
-        out[win0 + static_cast<uint64_t>(lane) * nw] = res;
-        win0 += 64 * nw;
-      }
-    }
-  }
-  if ((it & 63u) && lane < (it & 63u)) out[win0 + static_cast<uint64_t>(lane) * nw] = res;
-}
-
-// ---- fixed-stride batch, 4-KiB ping-pong path ----------------------------------------------------
-// crc_fast4k_kernel<2,1> with two named load buffers and a scheduling barrier right after each
-// load issue, so the next block's 4 KiB is in flight for the WHOLE hash of the current block
-// (hipcc otherwise sinks the loads a third of the way into the chain to reuse registers).
-__global__ __launch_bounds__(kThreads) void crc_pingpong4k_kernel(
-    const uint32_t* __restrict__ tabs, const uint8_t* __restrict__ base, uint64_t stride,
-    uint64_t nblk, uint32_t flags, uint32_t init, uint32_t* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
-  char* lds = reinterpret_cast<char*>(lds_words);
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWavesPerWg;
-  const uint64_t b0 = wave_id_uniform();
-  u32x4 A[4], B[4];
-  load4k<2>(A, base, stride, b0 < nblk ? b0 : nblk - 1, lane);
-  stage_tables<PDB_CAT_TREE32, PDB_CAT_S2048>(lds, tabs);
-  __syncthreads();
-  if (b0 >= nblk) return;
-  const LaneTabs lt = lane_tabs(lane);
-  const uint32_t init_raw = (flags & PDB_CRC_USE_INIT) ? ~init : 0xFFFFFFFFu;
-  const uint32_t c0 = lane == 0 ? init_raw : 0u;
-  uint32_t res = 0, it = 0;
-  uint64_t win0 = b0;
-  auto emit = [&](uint32_t c) {
-    const uint32_t v = finalize(__builtin_amdgcn_readfirstlane(c), flags);
-    if (lane == (it & 63u)) res = v;
-    if ((++it & 63u) == 0) {
-      out[win0 + static_cast<uint64_t>(lane) * nw] = res;
-      win0 += 64 * nw;
-    }
-  };
-  for (uint64_t b = b0; b < nblk; b += 2 * nw) {
-    const uint64_t b1 = b + nw, b2 = b + 2 * nw;
-    load4k<2>(B, base, stride, b1 < nblk ? b1 : b, lane);
-    __builtin_amdgcn_sched_barrier(0);
-    emit(hash4k<2>(lds, lt, lane, c0, A));
-    if (b1 >= nblk) break;
-    load4k<2>(A, base, stride, b2 < nblk ? b2 : b1, lane);
-    __builtin_amdgcn_sched_barrier(0);
-    emit(hash4k<2>(lds, lt, lane, c0, B));
-  }
-  if ((it & 63u) && lane < (it & 63u)) out[win0 + static_cast<uint64_t>(lane) * nw] = res;
-}
-
-// Dynamic variant of the packed kernel: workgroup g owns blocks [g*N/G, (g+1)*N/G); each wave
-// takes 4 consecutive blocks at a time from an LDS counter (operator slot 7 is unused here) and
-// writes their 4 CRCs with one 16-B store.
-__global__ __launch_bounds__(kThreads) void crc_pack4k_dyn_kernel(
-    const uint32_t* __restrict__ tabs, const uint8_t* __restrict__ base, uint64_t stride,
-    uint64_t nblk, uint32_t flags, uint32_t init, uint32_t* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
-  char* lds = reinterpret_cast<char*>(lds_words);
-  uint32_t* ctr = reinterpret_cast<uint32_t*>(lds + PDB_MAIN_BYTES + 7 * 4096u);
-  const uint32_t u = threadIdx.x & 63u;
-  const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t g_lo = nblk * blockIdx.x / gridDim.x, g_hi = nblk * (blockIdx.x + 1) / gridDim.x;
-  uint64_t grp = g_lo + 4u * wid;  // first group of this wave (static), then from the counter
-  u32x4 buf[4];
-  load4k<2>(buf, base, stride, grp < g_hi ? grp : (nblk ? nblk - 1 : 0), u);
-  stage_tables<PDB_CAT_TREE32, PDB_CAT_S2048>(lds, tabs);
-  if (threadIdx.x == 0) *ctr = kWavesPerWg;  // next group, in groups relative to g_lo
-  __syncthreads();
-  const LaneTabs lt = lane_tabs(u);
-  const uint32_t init_raw = (flags & PDB_CRC_USE_INIT) ? ~init : 0xFFFFFFFFu;
-  const uint32_t c0 = u == 0 ? init_raw : 0u;
-  while (grp < g_hi) {
-    uint32_t r0 = 0;
-    if (u == 0) r0 = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    const uint64_t ngrp = g_lo + 4u * static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(r0));
-    uint32_t p[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const uint64_t bk = grp + r;
-      u32x4 cur[4] = {buf[0], buf[1], buf[2], buf[3]};
-      const uint64_t bn = r < 3 ? bk + 1 : ngrp;
-      if (bn < g_hi) load4k<2>(buf, base, stride, bn, u);  // wave-uniform
-      p[r] = bk < g_hi ? partial4k(lds, lt, c0, cur) : 0u;
-    }
-    const uint32_t v = tree4_packed(lds, u, p[0], p[1], p[2], p[3]);
-    if (u < 4 && grp + u < g_hi) out[grp + u] = finalize(v, flags);
-    grp = ngrp;
-  }
-}
-
-// ---- fixed-stride batch, 4-KiB team path ----------------------------------------------------
-// A wave hashes T = 64/kG consecutive 4-KiB blocks at once: team t (lanes [t*kG, (t+1)*kG))
-// owns block t.  Within a team, lane u owns R = 4096/(32*kG) pieces of 32 B, piece r at
-// r*32*kG + 32*u, so every 16-B load instruction covers T blocks x kG lanes at a 32-B lane
-// stride.  Each piece is an independent 8-step chain; the R chains fold with "shift by
-// 32*kG bytes" (slot 6), then a log2(kG)-level team tree (slots 0.., shift by 32 << k) whose
-// VALU/LDS instructions serve all T blocks at once -- the per-block tree cost drops by T.
-template <int kG>
-__device__ __forceinline__ uint32_t team_tree(const char* lds, uint32_t u, uint32_t c) {
-  uint32_t y;
-  y = __builtin_amdgcn_update_dpp(0u, c, 0x101, 0xF, 0xF, false);
-  if ((u & 1u) == 0) c = shift_op_x(lds, 0, c, y);
-  y = __builtin_amdgcn_update_dpp(0u, c, 0x102, 0xF, 0xF, false);
-  if ((u & 3u) == 0) c = shift_op_x(lds, 1, c, y);
-  y = __builtin_amdgcn_update_dpp(0u, c, 0x104, 0xF, 0xF, false);
-  if ((u & 7u) == 0) c = shift_op_x(lds, 2, c, y);
-  y = __builtin_amdgcn_update_dpp(0u, c, 0x108, 0xF, 0xF, false);
-  if ((u & 15u) == 0) c = shift_op_x(lds, 3, c, y);
-  if constexpr (kG >= 32) {
-    y = __builtin_amdgcn_ds_swizzle(c, 0x401F);
-    if ((u & 31u) == 0) c = shift_op_x(lds, 4, c, y);
-  }
-  if constexpr (kG >= 64) {
-    y = __builtin_amdgcn_readlane(c, 32);
-    if (u == 0) c = shift_op_x(lds, 5, c, y);
-  }
-  return c;
-}
-
-template <int kG, int kDepth>
-__global__ __launch_bounds__(kThreads) void crc_team4k_kernel(
-    const uint32_t* __restrict__ tabs, const uint8_t* __restrict__ base, uint64_t stride,
-    uint64_t nblk, uint32_t flags, uint32_t init, uint32_t* __restrict__ out) {
-  constexpr uint32_t T = 64 / kG;             // blocks per wave-iteration
-  constexpr uint32_t R = 4096 / (32 * kG);    // 32-B pieces per lane per block
-  constexpr uint32_t ROW = 32 * kG;           // bytes between a lane's pieces
-  constexpr int kFold = kG == 32 ? PDB_CAT_S1024 : (kG == 16 ? 5 /* 512 */ : PDB_CAT_S2048);
-  __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
-  char* lds = reinterpret_cast<char*>(lds_words);
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t t = lane / kG, u = lane % kG;
-  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWavesPerWg;
-  const uint64_t ngroups = (nblk + T - 1) / T;  // wave-iterations needed in total
-  const uint64_t g0 = wave_id_uniform();
-
-  auto load = [&](u32x4 (&v)[2 * R], uint64_t g) {
-    uint64_t b = g * T + t;
-    if (b >= nblk) b = nblk - 1;  // clamp: a valid block (result discarded)
-    const uint8_t* p = base + b * stride + u * 32u;
-#pragma unroll
-    for (uint32_t r = 0; r < R; ++r) {
-      v[2 * r] = *reinterpret_cast<const u32x4*>(p + r * ROW);
-      v[2 * r + 1] = *reinterpret_cast<const u32x4*>(p + r * ROW + 16u);
-    }
-  };
-
-  u32x4 nxt[2 * R];
-  if constexpr (kDepth > 0) load(nxt, g0 < ngroups ? g0 : 0);
-  stage_tables<PDB_CAT_TREE32, kFold>(lds, tabs);
-  __syncthreads();
-  const LaneTabs lt = lane_tabs(lane);
-  const uint32_t init_raw = (flags & PDB_CRC_USE_INIT) ? ~init : 0xFFFFFFFFu;
-  for (uint64_t g = g0; g < ngroups; g += nw) {
-    u32x4 cur[2 * R];
-    if constexpr (kDepth > 0) {
-#pragma unroll
-      for (uint32_t i = 0; i < 2 * R; ++i) cur[i] = nxt[i];
-      const uint64_t gn = g + nw;
-      load(nxt, gn < ngroups ? gn : g);
-    } else {
-      load(cur, g);
-    }
-    uint32_t x[R];
-#pragma unroll
-    for (uint32_t r = 0; r < R; ++r) x[r] = cur[2 * r].x ^ ((r == 0 && u == 0) ? init_raw : 0u);
-#pragma unroll
-    for (int i = 1; i <= 8; ++i) {
-#pragma unroll
-      for (uint32_t r = 0; r < R; ++r) {
-        const u32x4& a = cur[2 * r];
-        const u32x4& bq = cur[2 * r + 1];
-        const uint32_t w = i == 1 ? a.y : i == 2 ? a.z : i == 3 ? a.w : i == 4 ? bq.x
-                         : i == 5 ? bq.y : i == 6 ? bq.z : i == 7 ? bq.w : 0u;
-        x[r] = step4x(lds, lt, x[r], w);
-      }
-    }
-    uint32_t c = x[0];
-#pragma unroll
-    for (uint32_t r = 1; r < R; ++r) c = shift_op_x(lds, PDB_SLOT_HORNER, c, x[r]);
-    c = team_tree<kG>(lds, u, c);
-    const uint64_t b = g * T + t;
-    if (u == 0 && b < nblk) out[b] = finalize(c, flags);
-  }
-}
-
-// ---- diagnostics ------------------------------------------------------------------------------
+// ---- load-pattern calibration ------------------------------------------------------------------
 __global__ __launch_bounds__(256) void read_stream_kernel(const u32x4* __restrict__ src,
                                                           uint64_t n16, uint32_t* __restrict__ out) {
   u32x4 acc = {0, 0, 0, 0};
@@ -288,150 +60,42 @@ __global__ __launch_bounds__(256) void read_stream_kernel(const u32x4* __restric
   if ((threadIdx.x & 63) == 0) atomicXor(out, r);
 }
 
-// Load-pattern calibration for 4-KiB blocks, no CRC work.
-//   kPat 0: lane l reads bytes [64l, 64l+64) of the block (the fast path's pattern)
-//   kPat 1: lane l reads 16 B at 16l + 1024j, j = 0..3 (each instruction 1 KiB contiguous)
-//   kDepth: blocks in flight per wave; kAssign 0: wave-interleaved blocks, 1: contiguous per WG
-template <int kPat, int kDepth, int kAssign, bool kSync = false, bool kNT = false, int kWaves = kWavesPerWg>
-__global__ __launch_bounds__(kWaves * 64) void read_pattern4k_kernel(const uint8_t* __restrict__ base,
-                                                                     uint64_t nblk,
-                                                                     uint32_t* __restrict__ out) {
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWaves;
-  uint32_t acc = 0;
-  uint64_t first, step, last;
-  if constexpr (kAssign == 0) {
-    first = static_cast<uint64_t>(blockIdx.x) * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    step = nw;
-    last = nblk;
-  } else {
-    const uint64_t per = (nblk + gridDim.x - 1) / gridDim.x;
-    const uint64_t lo = blockIdx.x * per;
-    first = lo + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    step = kWaves;
-    last = lo + per < nblk ? lo + per : nblk;
-  }
-  const uint64_t wg_first = static_cast<uint64_t>(blockIdx.x) * kWaves;
-  for (uint64_t b = first, bw = wg_first; (kSync ? bw : b) < last; b += step * kDepth, bw += step * kDepth) {
-    if constexpr (kSync) __syncthreads();
-    u32x4 x = {0, 0, 0, 0};
-#pragma unroll
-    for (int k = 0; k < kDepth; ++k) {
-      const uint64_t bk = b + k * step;
-      if (bk < last) {
-        const uint8_t* blk = base + bk * 4096u;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t off = kPat == 0 ? lane * 64u + j * 16u
-                             : (kPat == 1 ? lane * 16u + j * 1024u
-                                          : lane * 32u + (j >> 1) * 2048u + (j & 1) * 16u);
-          if constexpr (kNT)
-            x ^= __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(blk + off));
-          else
-            x ^= *reinterpret_cast<const u32x4*>(blk + off);
-        }
-      }
-    }
-    acc ^= x.x ^ x.y ^ x.z ^ x.w;
-  }
-  for (int k = 32; k; k >>= 1) acc ^= __shfl_xor(acc, k, 64);
-  if (lane == 0) atomicXor(out, acc);
-}
-
-// LDS-DMA calibration: each wave streams whole 4-KiB blocks into its own LDS ring with
-// global_load_lds_dwordx4 (4 instructions per block, each 1 KiB contiguous, lane-linear image),
-// kDepth blocks in flight per wave; kAux = cache policy bits (0 default, 2 = nt).  The block is then
-// read back from LDS (ds_read_b128) and folded, so the LDS round trip is paid as a CRC kernel would.
-template <int kAux, int kDepth, int kUnitKiB = 4, int kWaves = kWavesPerWg>
-__global__ __launch_bounds__(kWaves * 64) void read_glds4k_kernel(const uint8_t* __restrict__ base,
-                                                                  uint64_t nblk,
+// The 4-KiB path's loads with no CRC work (pdb_diag_read_pattern4k variant 21, the only one kept):
+// lane l reads 16 B at 16 l + 1024 j, j = 0..3 (each load instruction 1 KiB contiguous, nt policy),
+// one block per wave at a time, blocks wave-interleaved, every 16 waves of a workgroup in lock-step
+// (one __syncthreads per block step).  Also the FETCH_SIZE calibration kernel of tools/pmc_traffic.py.
+__global__ __launch_bounds__(kThreads) void read_pattern4k_kernel(const uint8_t* __restrict__ base, uint64_t nblk,
                                                                   uint32_t* __restrict__ out) {
-  constexpr uint32_t kUnit = kUnitKiB * 1024u;
-  __shared__ __attribute__((aligned(16))) uint8_t ring[kWaves * kDepth * kUnit];
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uint8_t* my = ring + wv * (kDepth * kUnit);
-  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWaves;
-  const uint64_t nunit = nblk * (4096u / kUnit);
-  const uint64_t first = static_cast<uint64_t>(blockIdx.x) * kWaves + wv;
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWavesPerWg;
   uint32_t acc = 0;
-  auto issue = [&](uint64_t u, uint32_t slot) {
-    const uint8_t* g = base + u * kUnit + lane * 16u;
-    uint8_t* l = my + slot * kUnit;
+  const uint64_t first = static_cast<uint64_t>(blockIdx.x) * kWavesPerWg + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t wg_first = static_cast<uint64_t>(blockIdx.x) * kWavesPerWg;
+  for (uint64_t b = first, bw = wg_first; bw < nblk; b += nw, bw += nw) {
+    __syncthreads();
+    u32x4 x = {0, 0, 0, 0};
+    if (b < nblk) {
+      const uint8_t* blk = base + b * 4096u;
 #pragma unroll
-    for (int j = 0; j < kUnitKiB; ++j)
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(g + j * 1024),
-                                       reinterpret_cast<__attribute__((address_space(3))) void*>(
-                                           reinterpret_cast<uintptr_t>(l + j * 1024)),
-                                       16, 0, kAux);
-  };
-  uint64_t u = first;
-#pragma unroll
-  for (int k = 0; k < kDepth - 1; ++k)
-    if (u + k * nw < nunit) issue(u + k * nw, k);
-  uint32_t slot = 0;
-  for (; u < nunit; u += nw) {
-    const uint64_t ahead = u + (kDepth - 1) * nw;
-    const uint32_t aslot = (slot + kDepth - 1) % kDepth;
-    if (ahead < nunit) {
-      issue(ahead, aslot);
-      // leave the (kDepth-1) newer units' loads in flight (kDepth 2 only; else drain)
-      if constexpr (kDepth == 2 && kUnitKiB == 4) __builtin_amdgcn_s_waitcnt(0x0F74);       // vmcnt(4)
-      else if constexpr (kDepth == 2 && kUnitKiB == 2) __builtin_amdgcn_s_waitcnt(0x0F72);  // vmcnt(2)
-      else __builtin_amdgcn_s_waitcnt(0x0F70);
-    } else {
-      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+      for (int j = 0; j < 4; ++j)
+        x ^= __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(blk + lane * 16u + j * 1024u));
     }
-    const u32x4* l = reinterpret_cast<const u32x4*>(my + slot * kUnit);
-    u32x4 x = l[lane];
-#pragma unroll
-    for (int j = 1; j < kUnitKiB; ++j) x ^= l[lane + 64 * j];
     acc ^= x.x ^ x.y ^ x.z ^ x.w;
-    slot = (slot + 1) % kDepth;
   }
   for (int k = 32; k; k >>= 1) acc ^= __shfl_xor(acc, k, 64);
   if (lane == 0) atomicXor(out, acc);
 }
 
-}  // namespace
-
-uint32_t grid_forw(const LaunchGeom& g, uint64_t nblk, uint32_t waves) {
-  const uint64_t want = (nblk + waves - 1) / waves;
-  return static_cast<uint32_t>(want < g.grid ? (want ? want : 1) : g.grid);
-}
-uint32_t grid_for8(const LaunchGeom& g, uint64_t nblk) { return grid_forw(g, nblk, 8); }
-
-namespace {
-
-// Seal's second half (A/B variant 35): trailer word i (masked CRC, from a compact array) to
-// buf + offset_i + size_i + 1, one thread per block.
-__global__ __launch_bounds__(256) void trailer_scatter_kernel(uint8_t* __restrict__ buf,
-                                                              const pdb_block_handle* __restrict__ h,
-                                                              const uint32_t* __restrict__ crc, uint64_t n) {
-  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint8_t* tr = buf + h[i].offset + h[i].size + 1;
-  const uint32_t m = crc[i];
-  tr[0] = static_cast<uint8_t>(m);
-  tr[1] = static_cast<uint8_t>(m >> 8);
-  tr[2] = static_cast<uint8_t>(m >> 16);
-  tr[3] = static_cast<uint8_t>(m >> 24);
-}
-
-// Seal-pattern calibration (variants 140-142; no CRC work, trailers written with WRONG values by
-// design): the in-place seal's memory pattern without its hash -- every block's bytes [offset,
+// Seal-pattern calibration (sst variants 140 / 141; no CRC work, trailers written with WRONG values
+// by design): the in-place seal's memory pattern without its hash -- every block's bytes [offset,
 // offset + size + 5) read as 1-KiB-contiguous 16-B nt loads by the wave owning its 4-block group,
 // groups in workgroup lock-step over the workgroup's contiguous range (the sst kernel's
 // scheduling), handles a group ahead -- with kWrite 0: no stores (the pattern's read ceiling);
-// 1: each group's 4 trailers stored (4 byte stores, like SealSink) once its loads returned;
-// 2: trailers parked 64 groups like ParkSealSink<64>, the rest written when the wave is done.
-// kAux >= 0: the loads as range-checked buffer loads with that cache policy (bit 0 sc0, bit 1 nt,
-// bit 4 sc1: 18 = device scope + nt, so the lines need not allocate in the XCD's L2).
-template <int kWrite, int kAux = -1>
+// 1: each group's 4 trailers stored (4 byte stores, like SealSink) once its loads returned.
+template <int kWrite>
 __global__ __launch_bounds__(kThreads) void seal_pattern_kernel(uint8_t* __restrict__ buf,
                                                                 const pdb_block_handle* __restrict__ h,
-                                                                uint64_t n, uint32_t* __restrict__ out,
-                                                                intptr_t shadow_delta) {
+                                                                uint64_t n, uint32_t* __restrict__ out) {
   typedef __attribute__((address_space(1))) uint8_t g_u8;
   const uint32_t u = threadIdx.x & 63u;
   const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -439,8 +103,6 @@ __global__ __launch_bounds__(kThreads) void seal_pattern_kernel(uint8_t* __restr
   const uint64_t lo = n * blockIdx.x / G, hi = n * (blockIdx.x + 1) / G;
   if (lo >= hi) return;
   uint32_t acc = 0;
-  uint32_t pv[4] = {0, 0, 0, 0};
-  uintptr_t pa[4] = {0, 0, 0, 0};
   auto hload = [&](uint64_t b0) -> u32x4 {  // lane r < 4: block b0 + r's handle (clamped)
     const uint64_t b = b0 + (u & 3u);
     return gload128<false>(reinterpret_cast<uintptr_t>(h + (b < hi ? b : hi - 1)));
@@ -452,14 +114,6 @@ __global__ __launch_bounds__(kThreads) void seal_pattern_kernel(uint8_t* __restr
     const u32x4 hc = hn;
     keep_alive(hc);
     hn = hload(b0 + 64u);
-    if constexpr (kWrite == 7) {
-      if (u < 4u && b0 + u < hi) {
-        g_u8* tr = reinterpret_cast<g_u8*>(reinterpret_cast<uintptr_t>(buf) +
-                                           ((static_cast<uint64_t>(hc.y) << 32) | hc.x) + hc.z + 1u);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) tr[k] = static_cast<uint8_t>(acc >> (8 * k));
-      }
-    }
     u32x4 x = {0, 0, 0, 0};
     uintptr_t ta = 0;  // lane r < 4: block r's trailer word address
 #pragma unroll
@@ -469,652 +123,80 @@ __global__ __launch_bounds__(kThreads) void seal_pattern_kernel(uint8_t* __restr
       const uintptr_t a0 = (reinterpret_cast<uintptr_t>(buf) + off) & ~static_cast<uintptr_t>(15);
       const uintptr_t e = reinterpret_cast<uintptr_t>(buf) + off + sz + 5u;
       const uint32_t last = static_cast<uint32_t>((e - 1u - a0) >> 4);
-      if constexpr (kAux < 0) {
 #pragma unroll
-        for (uint32_t j = 0; j < 5; ++j) {
-          const uint32_t c = 64u * j + u;
-          x ^= gload128<true>(a0 + 16u * (c < last ? c : last));
-        }
-      } else {
-        const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(a0), 0,
-                                                                              static_cast<int>(16u * (last + 1u)), 0x00020000);
-#pragma unroll
-        for (uint32_t j = 0; j < 5; ++j) {
-          const uint32_t c = 64u * j + u;
-          x ^= __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, static_cast<int>(16u * (c < last ? c : last)),
-                                                                                0, kAux));
-        }
+      for (uint32_t j = 0; j < 5; ++j) {
+        const uint32_t c = 64u * j + u;
+        x ^= gload128<true>(a0 + 16u * (c < last ? c : last));
       }
       if (u == r) ta = reinterpret_cast<uintptr_t>(buf) + off + sz + 1u;
     }
     const uint32_t m = x.x ^ x.y ^ x.z ^ x.w;
     acc ^= m;
-    const bool mine = u < 4u && b0 + u < hi;
-    if constexpr (kWrite == 1 || kWrite == 3) {  // 3: into a shadow image at the same offsets
-      if (mine) {
-        g_u8* tr = reinterpret_cast<g_u8*>(ta + (kWrite == 3 ? shadow_delta : 0));
+    if constexpr (kWrite == 1) {
+      if (u < 4u && b0 + u < hi) {
+        g_u8* tr = reinterpret_cast<g_u8*>(ta);
 #pragma unroll
         for (int k = 0; k < 4; ++k) tr[k] = static_cast<uint8_t>(m >> (8 * k));
       }
-    } else if constexpr (kWrite == 4) {  // the aligned 16 B holding the trailer's first byte, one store
-      typedef __attribute__((address_space(1))) u32x4 g_q;
-      if (mine) *reinterpret_cast<g_q*>(ta & ~static_cast<uintptr_t>(15)) = x;
-    } else if constexpr (kWrite == 5 || kWrite == 6) {  // the aligned 128-B (6: 64-B) line holding it
-      typedef __attribute__((address_space(1))) u32x4 g_q;
-      constexpr uint32_t kL = kWrite == 5 ? 128u : 64u, kQ = kL / 16u;
-      const uint32_t r = u / kQ, q = u % kQ;
-      const uint32_t alo = static_cast<uint32_t>(__shfl(static_cast<int>(static_cast<uint32_t>(ta)), static_cast<int>(r), 64));
-      const uint32_t ahi = static_cast<uint32_t>(__shfl(static_cast<int>(static_cast<uint32_t>(ta >> 32)), static_cast<int>(r), 64));
-      const uintptr_t a = (((static_cast<uintptr_t>(ahi) << 32) | alo) & ~static_cast<uintptr_t>(kL - 1u)) + 16u * q;
-      if (r < 4u && b0 + r < hi) *reinterpret_cast<g_q*>(a) = x;
-    } else if constexpr (kWrite == 7) {  // trailers of the group stored BEFORE its loads are issued
-      // (handled above the loads; nothing here)
-    } else if constexpr (kWrite == 2) {  // group g = t of this wave: lane 4 (t mod 16) + r, slot (t / 16) mod 4
-      const uint32_t src_lane = u & 3u;
-      const uint32_t mv = __shfl(m, src_lane, 64);
-      const uint32_t alo = static_cast<uint32_t>(__shfl(static_cast<int>(static_cast<uint32_t>(ta)), src_lane, 64));
-      const uint32_t ahi = static_cast<uint32_t>(__shfl(static_cast<int>(static_cast<uint32_t>(ta >> 32)), src_lane, 64));
-      const uintptr_t av = (static_cast<uintptr_t>(ahi) << 32) | alo;
-      const bool ok = __shfl(static_cast<int>(mine), src_lane, 64) != 0;
-      const uint32_t s = static_cast<uint32_t>((t >> 4) & 3u);
-      if ((u >> 2) == (t & 15u) && ok) {
-#pragma unroll
-        for (uint32_t k = 0; k < 4; ++k)
-          if (k == s) {
-            if (pa[k]) {
-              g_u8* tr = reinterpret_cast<g_u8*>(pa[k]);
-#pragma unroll
-              for (int q = 0; q < 4; ++q) tr[q] = static_cast<uint8_t>(pv[k] >> (8 * q));
-            }
-            pa[k] = av;
-            pv[k] = mv;
-          }
-      }
     }
-  }
-  if constexpr (kWrite == 2) {
-#pragma unroll
-    for (uint32_t k = 0; k < 4; ++k)
-      if (pa[k]) {
-        g_u8* tr = reinterpret_cast<g_u8*>(pa[k]);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) tr[q] = static_cast<uint8_t>(pv[k] >> (8 * q));
-      }
   }
   for (int k = 32; k; k >>= 1) acc ^= __shfl_xor(acc, k, 64);
   if (u == 0 && out) atomicXor(out, acc);
 }
 
-struct NtSealSink {  // A/B variant 34: the trailer as non-temporal byte stores
-  __device__ __forceinline__ void put(uint64_t, uint32_t raw, const BlkDesc& d) const {
-    typedef __attribute__((address_space(1))) uint8_t g_u8;
-    g_u8* tr = reinterpret_cast<g_u8*>(reinterpret_cast<uintptr_t>(d.p) + d.n);
-    const uint32_t m = pdb_mask(~raw);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) __builtin_nontemporal_store(static_cast<uint8_t>(m >> (8 * k)), tr + k);
-  }
-};
-
-// A/B variant 36: the seal, with the line holding each trailer read (default policy) a group
-// before the trailer is written, so the write lands on a valid L2 line.
-struct SealTouchSink {};
-
-// Pricing variants 93 / 94 / 95 / 96 (trailer bytes go to a SHADOW image at the same offsets, so the
-// image itself stays intact): 94 writes the 4-B trailer, 95 / 96 / 93 the trailer's whole aligned
-// 32-B / 64-B / 128-B window (zeros around it; 128 B = one L2 line).  Same kernel, same reads; only
-// the write granularity differs.
-struct ShadowSealSink {
-  intptr_t delta;  // shadow - image
-  uint32_t bytes;  // 4: the trailer; 32 / 64 / 128: its whole aligned window
-};
-
-template <>
-struct SinkOps<ShadowSealSink> {
-  __device__ static __forceinline__ uint32_t pre(const ShadowSealSink&, uint64_t, const BlkDesc&) { return 0u; }
-  __device__ static __forceinline__ void put(const ShadowSealSink& k, uint64_t, uint32_t raw, const BlkDesc& d,
-                                             uint32_t) {
-    if (d.init_raw == 0) return;
-    const uintptr_t a = reinterpret_cast<uintptr_t>(d.p) + d.n + k.delta;
-    const uint32_t m = pdb_mask(~raw);
-    if (k.bytes == 4u) {
-      typedef __attribute__((address_space(1))) uint32_t g_u32u __attribute__((aligned(1)));
-      *reinterpret_cast<g_u32u*>(a) = m;
-      return;
-    }
-    typedef __attribute__((address_space(1))) u32x4 g_v4;
-    const uintptr_t s0 = a & ~static_cast<uintptr_t>(k.bytes - 1u);
-    const uint32_t o = static_cast<uint32_t>(a - s0), i0 = (o >> 2) & 15u, sh = (o & 3u) * 8u;
-    uint32_t x[16];
-#pragma unroll
-    for (uint32_t i = 0; i < 16; ++i) x[i] = i == i0 ? (m << sh) : ((i == i0 + 1 && sh) ? (m >> (32u - sh)) : 0u);
-    g_v4* w = reinterpret_cast<g_v4*>(s0);
-    w[0] = u32x4{x[0], x[1], x[2], x[3]};
-    w[1] = u32x4{x[4], x[5], x[6], x[7]};
-    if (k.bytes >= 64u) {
-      w[2] = u32x4{x[8], x[9], x[10], x[11]};
-      w[3] = u32x4{x[12], x[13], x[14], x[15]};
-    }
-    if (k.bytes == 128u) {  // the trailer sits in the first 64 B of its line or in the second
-      const bool hi = o >= 64u;
-      if (hi) {
-        w[0] = u32x4{0u, 0u, 0u, 0u};
-        w[1] = u32x4{0u, 0u, 0u, 0u};
-        w[2] = u32x4{0u, 0u, 0u, 0u};
-        w[3] = u32x4{0u, 0u, 0u, 0u};
-      }
-      uint32_t y[16];
-#pragma unroll
-      for (uint32_t i = 0; i < 16; ++i) y[i] = hi ? x[i] : 0u;
-      w[4] = u32x4{y[0], y[1], y[2], y[3]};
-      w[5] = u32x4{y[4], y[5], y[6], y[7]};
-      w[6] = u32x4{y[8], y[9], y[10], y[11]};
-      w[7] = u32x4{y[12], y[13], y[14], y[15]};
-    }
-  }
-};
-
-// Pricing variants 76 / 77 / 78: the in-place trailer as byte stores with a wider scope (76: sc1 =
-// device scope; 77: sc0 sc1 = system scope, written through; 78: system scope + nt).
-template <int kPol>
-struct ScopeSealSink {};
-template <int kPol>
-struct SinkOps<ScopeSealSink<kPol>> {
-  __device__ static __forceinline__ uint32_t pre(const ScopeSealSink<kPol>&, uint64_t, const BlkDesc&) { return 0u; }
-  __device__ static __forceinline__ void put(const ScopeSealSink<kPol>&, uint64_t, uint32_t raw, const BlkDesc& d,
-                                             uint32_t) {
-    if (d.init_raw == 0) return;
-    const uintptr_t a = reinterpret_cast<uintptr_t>(d.p) + d.n;
-    const uint32_t m = pdb_mask(~raw);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t b = (m >> (8 * k)) & 0xFFu;
-      const uint64_t ad = a + k;
-      if constexpr (kPol == 0)
-        asm volatile("global_store_byte %0, %1, off sc1" ::"v"(ad), "v"(b) : "memory");
-      else if constexpr (kPol == 1)
-        asm volatile("global_store_byte %0, %1, off sc0 sc1" ::"v"(ad), "v"(b) : "memory");
-      else
-        asm volatile("global_store_byte %0, %1, off sc0 sc1 nt" ::"v"(ad), "v"(b) : "memory");
-    }
-  }
-};
-
-// A/B variant 37: the trailer word as ONE (possibly unaligned) dword store instead of 4 byte stores.
-struct SealDwordSink {};
-
-template <>
-struct SinkOps<SealDwordSink> {
-  __device__ static __forceinline__ uint32_t pre(const SealDwordSink&, uint64_t, const BlkDesc&) { return 0u; }
-  __device__ static __forceinline__ void put(const SealDwordSink&, uint64_t, uint32_t raw, const BlkDesc& d,
-                                             uint32_t) {
-    if (d.init_raw == 0) return;
-    typedef __attribute__((address_space(1))) uint32_t g_u32u __attribute__((aligned(1)));
-    *reinterpret_cast<g_u32u*>(reinterpret_cast<uintptr_t>(d.p) + d.n) = pdb_mask(~raw);
-  }
-};
-
-// A/B variant 39: the 64 B from the trailer's 32-B sector on re-read and written back whole with the
-// trailer merged in (full-sector writes: no partial-sector read-modify-write at the memory side).
-// Diagnostics only: assumes no other trailer within 64 B (true of the bench's 4-KiB blocks).
-struct SealSectorSink {};
-
-template <>
-struct SinkOps<SealSectorSink> {
-  __device__ static __forceinline__ uint32_t pre(const SealSectorSink&, uint64_t, const BlkDesc&) { return 0u; }
-  __device__ static __forceinline__ void put(const SealSectorSink&, uint64_t, uint32_t raw, const BlkDesc& d,
-                                             uint32_t) {
-    if (d.init_raw == 0) return;
-    typedef __attribute__((address_space(1))) u32x4 g_v4;
-    const uintptr_t a = reinterpret_cast<uintptr_t>(d.p) + d.n;
-    const uintptr_t s0 = a & ~static_cast<uintptr_t>(31);
-    const uint32_t o = static_cast<uint32_t>(a - s0), i0 = o >> 2, sh = (o & 3u) * 8u;
-    const uint32_t m = pdb_mask(~raw);
-    g_v4* w = reinterpret_cast<g_v4*>(s0);
-    u32x4 v[4] = {w[0], w[1], w[2], w[3]};
-    uint32_t x[16];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) x[4 * i] = v[i].x, x[4 * i + 1] = v[i].y, x[4 * i + 2] = v[i].z, x[4 * i + 3] = v[i].w;
-    const uint32_t lo_keep = sh ? (0xFFFFFFFFu >> (32u - sh)) : 0u;  // bytes of dword i0 below the trailer
-#pragma unroll
-    for (uint32_t i = 0; i < 16; ++i) {
-      if (i == i0) x[i] = (x[i] & lo_keep) | (m << sh);
-      if (i == i0 + 1 && sh) x[i] = (x[i] & ~lo_keep) | (m >> (32u - sh));
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) w[i] = u32x4{x[4 * i], x[4 * i + 1], x[4 * i + 2], x[4 * i + 3]};
-  }
-};
-
-template <>
-struct SinkOps<SealTouchSink> {
-  __device__ static __forceinline__ uint32_t pre(const SealTouchSink&, uint64_t, const BlkDesc& d) {
-    typedef __attribute__((address_space(1))) const uint32_t g_u32_;
-    const uintptr_t a = (reinterpret_cast<uintptr_t>(d.p) + d.n) & ~static_cast<uintptr_t>(3);
-    return *reinterpret_cast<g_u32_*>(a);
-  }
-  __device__ static __forceinline__ void put(const SealTouchSink&, uint64_t i, uint32_t raw, const BlkDesc& d,
-                                             uint32_t touched) {
-    asm volatile("" ::"v"(touched));
-    SinkOps<SealSink>::put(SealSink{}, i, raw, d, 0u);
-  }
-};
-
+uint32_t record_class(uint32_t flags) {
+  return (flags & PDB_CRC_SIZE_256) ? 256u : (flags & PDB_CRC_SIZE_512) ? 512u : ((flags & PDB_CRC_SIZE_1K) ? 1152u : 1023u);
+}
 
 }  // namespace
 
 hipError_t launch_sst_variant(int v, const LaunchGeom& g, const uint32_t* d_tables, uint8_t* buf, uint64_t buf_len,
                               const pdb_block_handle* h, uint64_t n, bool seal, uint8_t* ok, uint32_t* nbad,
                               hipStream_t s) {
-  if (v == 0) return launch_sst(g, d_tables, buf, buf_len, h, n, seal, ok, nbad, s);
   const dim3 grid(grid_for(g, n)), block(kThreads);
-  if ((v == 131 || v == 132) && seal) {  // the compact form (pdb_sst_crc_device): masked CRCs into
-                                         // (uint32_t*) ok -- 131: 16 waves, 132: 12 waves (the product)
-    const SstSrc src{buf, h, buf_len};
-    uint32_t* co = reinterpret_cast<uint32_t*>(ok);
-    if (v == 131)
-      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstCrcSink, true>), grid, block, 0, s, d_tables, src, n, SstCrcSink{co});
-    else
-      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstCrcSink, true, 4, QuadTabs, false, true, 12>), grid, dim3(768), 0, s,
-                         d_tables, src, n, SstCrcSink{co});
-    return hipGetLastError();
-  }
-  if (v == 129 && !seal) {  // verify with 16 waves (the product until late round 3)
-    const SstSrc src{buf, h, buf_len};
-    hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstVerifySink, true>), grid, block, 0, s, d_tables, src, n,
-                       SstVerifySink{ok, nbad});
-    return hipGetLastError();
-  }
-  if (v == 127 || v == 128) {  // 12 / 8 waves per workgroup (168 / 256 VGPRs a lane; spills 32 / 0 B)
-    const dim3 blk(v == 127 ? 768u : 512u);
-    const SstSrc src{buf, h, buf_len};
-    if (seal) {
-      if (v == 127)
-        hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ParkSealSink<64>, true, 4, QuadTabs, false, true, 12>), grid, blk, 0, s,
-                           d_tables, src, n, ParkSealSink<64>{});
-      else
-        hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ParkSealSink<64>, true, 4, QuadTabs, false, true, 8>), grid, blk, 0, s,
-                           d_tables, src, n, ParkSealSink<64>{});
-    } else {
-      if (v == 127)
-        hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstVerifySink, true, 4, QuadTabs, false, true, 12>), grid, blk, 0, s,
-                           d_tables, src, n, SstVerifySink{ok, nbad});
-      else
-        hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstVerifySink, true, 4, QuadTabs, false, true, 8>), grid, blk, 0, s,
-                           d_tables, src, n, SstVerifySink{ok, nbad});
-    }
-    return hipGetLastError();
-  }
-  if (v >= 140 && v <= 151 && seal) {  // seal-pattern calibration (seal_pattern_kernel<v - 140>)
-    uint32_t* xo = nbad;  // XOR of everything read (keeps the loads live); may be null
-    static uint8_t* cal_shadow = nullptr;  // diagnostics only: 143's shadow image
-    static uint64_t cal_shadow_n = 0;
-    intptr_t delta = 0;
-    if (v == 143) {
-      static std::mutex mu;
-      std::lock_guard<std::mutex> lk(mu);
-      if (cal_shadow_n < buf_len + 256) {
-        if (cal_shadow) (void)hipFree(cal_shadow);
-        cal_shadow = nullptr;
-        cal_shadow_n = 0;
-        if (hipMalloc(&cal_shadow, buf_len + 256) != hipSuccess) return hipErrorOutOfMemory;
-        cal_shadow_n = buf_len + 256;
-      }
-      delta = reinterpret_cast<intptr_t>(cal_shadow) - reinterpret_cast<intptr_t>(buf);
-    }
-    switch (v) {
-      case 140: hipLaunchKernelGGL(seal_pattern_kernel<0>, grid, block, 0, s, buf, h, n, xo, delta); break;
-      case 141: hipLaunchKernelGGL(seal_pattern_kernel<1>, grid, block, 0, s, buf, h, n, xo, delta); break;
-      case 142: hipLaunchKernelGGL(seal_pattern_kernel<2>, grid, block, 0, s, buf, h, n, xo, delta); break;
-      case 143: hipLaunchKernelGGL(seal_pattern_kernel<3>, grid, block, 0, s, buf, h, n, xo, delta); break;
-      case 144: hipLaunchKernelGGL(seal_pattern_kernel<4>, grid, block, 0, s, buf, h, n, xo, delta); break;
-      case 145: hipLaunchKernelGGL(seal_pattern_kernel<5>, grid, block, 0, s, buf, h, n, xo, delta); break;
-      case 146: hipLaunchKernelGGL(seal_pattern_kernel<6>, grid, block, 0, s, buf, h, n, xo, delta); break;
-      case 147: hipLaunchKernelGGL(seal_pattern_kernel<7>, grid, block, 0, s, buf, h, n, xo, delta); break;
-      case 148: hipLaunchKernelGGL((seal_pattern_kernel<1, 18>), grid, block, 0, s, buf, h, n, xo, delta); break;  // sc1 nt loads + stores
-      case 149: hipLaunchKernelGGL((seal_pattern_kernel<1, 19>), grid, block, 0, s, buf, h, n, xo, delta); break;  // sc0 sc1 nt loads + stores
-      case 150: hipLaunchKernelGGL((seal_pattern_kernel<0, 18>), grid, block, 0, s, buf, h, n, xo, delta); break;  // sc1 nt loads only
-      default: hipLaunchKernelGGL((seal_pattern_kernel<1, 2>), grid, block, 0, s, buf, h, n, xo, delta); break;      // nt buffer loads + stores
-    }
-    return hipGetLastError();
-  }
   const SstSrc src{buf, h, buf_len};
-  if (v == 97 && !seal) {  // WRONG CRCs by design: verify without the Horner folds (prices them)
-    hipLaunchKernelGGL((crc_sst4k_nofold_kernel<SstSrc, SstVerifySink, true>), grid, block, 0, s, d_tables, src, n,
-                       SstVerifySink{ok, nullptr});  // no nbad: every block "fails"; 1M atomics would dominate
-    return hipGetLastError();
-  }
-  if (v == 30) {  // the round-1 table image: 32 replicas of T0..T3, single-copy shift 1024
-    if (seal)
-      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SealSink, true, 4, LaneTabs>), grid, block, 0, s, d_tables, src, n,
-                         SealSink{});
-    else
-      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstVerifySink, true, 4, LaneTabs>), grid, block, 0, s, d_tables, src,
-                         n, SstVerifySink{ok, nbad});
-    return hipGetLastError();
-  }
-  if (v == 48) {  // every body chain finished before the folds (round 2; the shipped kernel defers it)
-    if (seal)
-      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ParkSealSink<64>, true, 4, QuadTabs, false, false>), grid, block, 0, s,
-                         d_tables, src, n, ParkSealSink<64>{});
-    else
-      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstVerifySink, true, 4, QuadTabs, false, false>), grid, block, 0, s,
-                         d_tables, src, n, SstVerifySink{ok, nbad});
-    return hipGetLastError();
-  }
-  if (v == 38) {  // 8-block groups (prefixes <= 128 B in rows of 8 lanes, tree8_packed)
-    if (seal)
-      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SealSink, true, 8>), grid, block, 0, s, d_tables, src, n,
-                         SealSink{});
-    else
-      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstVerifySink, true, 8>), grid, block, 0, s, d_tables, src, n,
-                         SstVerifySink{ok, nbad});
-    return hipGetLastError();
-  }
-  static std::mutex shadow_mu;  // diagnostics only: one shadow image (93-96, 85/87) and CRC array (85-87)
-  static uint8_t* shadow = nullptr;
-  static uint64_t shadow_n = 0;
-  static uint32_t* crcs = nullptr;
-  static uint64_t crcs_n = 0;
-  if (v >= 85 && v <= 87 && seal) {  // scatter-pass pricing: 85 / 86 the scatter alone into the shadow /
-                                     // the image (stale CRC words), 87 compact CRCs + scatter into the shadow
-    std::lock_guard<std::mutex> lk(shadow_mu);
-    if (shadow_n < buf_len + 256) {
-      if (shadow) (void)hipFree(shadow);
-      shadow = nullptr;
-      shadow_n = 0;
-      if (hipMalloc(&shadow, buf_len + 256) != hipSuccess) return hipErrorOutOfMemory;
-      shadow_n = buf_len + 256;
-    }
-    if (crcs_n < n) {
-      if (crcs) (void)hipFree(crcs);
-      crcs = nullptr;
-      crcs_n = 0;
-      if (hipMalloc(&crcs, n * 4) != hipSuccess) return hipErrorOutOfMemory;
-      crcs_n = n;
-    }
-    if (v == 87)
-      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, OutSink, true>), grid, block, 0, s, d_tables, src, n,
-                         OutSink{crcs, PDB_CRC_MASK_OUTPUT});
-    hipLaunchKernelGGL(trailer_scatter_kernel, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256), 0, s,
-                       v == 86 ? buf : shadow, h, crcs, n);
-    return hipGetLastError();
-  }
-  if (v >= 80 && v <= 84 && seal) {  // the shadow writes of 94 / 96 / 93 (82 / 83 / 84: 128 / 4 / 64 B) or the
-                                     // scatter pass of 85 (80: alone; 81: after the compact-CRC pass),
-                                     // into one of 3 shadows in turn, so the written lines are not
-                                     // still in the 256-MB MALL from the previous launch
-    static uint8_t* rot[3] = {nullptr, nullptr, nullptr};
-    static uint64_t rot_n = 0;
-    static uint32_t turn = 0;
-    std::lock_guard<std::mutex> lk(shadow_mu);
-    if (rot_n < buf_len + 256) {
-      for (auto& r : rot) {
-        if (r) (void)hipFree(r);
-        r = nullptr;
-      }
-      rot_n = 0;
-      for (auto& r : rot)
-        if (hipMalloc(&r, buf_len + 256) != hipSuccess) return hipErrorOutOfMemory;
-      rot_n = buf_len + 256;
-    }
-    if (crcs_n < n) {
-      if (crcs) (void)hipFree(crcs);
-      crcs = nullptr;
-      crcs_n = 0;
-      if (hipMalloc(&crcs, n * 4) != hipSuccess) return hipErrorOutOfMemory;
-      crcs_n = n;
-    }
-    uint8_t* sh = rot[turn++ % 3];
-    if (v <= 81) {
-      if (v == 81)
-        hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, OutSink, true>), grid, block, 0, s, d_tables, src, n,
-                           OutSink{crcs, PDB_CRC_MASK_OUTPUT});
-      hipLaunchKernelGGL(trailer_scatter_kernel, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256), 0, s, sh, h,
-                         crcs, n);
-    } else {
-      const ShadowSealSink k{reinterpret_cast<intptr_t>(sh) - reinterpret_cast<intptr_t>(buf),
-                             v == 83 ? 4u : (v == 84 ? 64u : 128u)};
-      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ShadowSealSink, true>), grid, block, 0, s, d_tables, src, n, k);
-    }
-    return hipGetLastError();
-  }
-  if ((v == 93 || v == 94 || v == 95 || v == 96) && seal) {  // pricing: 4-B vs 32/64/128-B window writes into a shadow image
-    std::lock_guard<std::mutex> lk(shadow_mu);
-    if (shadow_n < buf_len + 256) {
-      if (shadow) (void)hipFree(shadow);
-      shadow = nullptr;
-      shadow_n = 0;
-      if (hipMalloc(&shadow, buf_len + 256) != hipSuccess) return hipErrorOutOfMemory;
-      shadow_n = buf_len + 256;
-    }
-    const ShadowSealSink k{reinterpret_cast<intptr_t>(shadow) - reinterpret_cast<intptr_t>(buf),
-                           v == 94 ? 4u : (v == 95 ? 32u : (v == 96 ? 64u : 128u))};
-    hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ShadowSealSink, true>), grid, block, 0, s, d_tables, src, n, k);
-    return hipGetLastError();
-  }
-  if (v == 70) {  // body pieces as unaligned dwordx4 loads (no neighbour dword / v_alignbyte)
-    if (seal)
-      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ParkSealSink<64>, true, 4, QuadTabs, true>), grid, block, 0, s,
-                         d_tables, src, n, ParkSealSink<64>{});
-    else
-      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstVerifySink, true, 4, QuadTabs, true>), grid, block, 0, s,
-                         d_tables, src, n, SstVerifySink{ok, nbad});
-    return hipGetLastError();
-  }
-  if (v == 72 && seal) {  // the round-2 product seal: each group's trailers written when hashed
-    hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SealSink, true>), grid, block, 0, s, d_tables, src, n, SealSink{});
-    return hipGetLastError();
-  }
-  if (v >= 76 && v <= 78 && seal) {  // trailer stores with device / system scope
-    if (v == 76)
-      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ScopeSealSink<0>, true>), grid, block, 0, s, d_tables, src, n, ScopeSealSink<0>{});
-    else if (v == 77)
-      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ScopeSealSink<1>, true>), grid, block, 0, s, d_tables, src, n, ScopeSealSink<1>{});
-    else
-      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ScopeSealSink<2>, true>), grid, block, 0, s, d_tables, src, n, ScopeSealSink<2>{});
-    return hipGetLastError();
-  }
-  if (v >= 73 && v <= 92 && seal && (v >= 88 || v <= 74)) {  // parked trailers: written 1 / 2 / 4 / 8 / 16 (88-92), 32 / 64 (73 / 74) groups after the hash
-    switch (v) {
-      case 73: hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ParkSealSink<32>, true>), grid, block, 0, s, d_tables, src, n, ParkSealSink<32>{}); break;
-      case 74: hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ParkSealSink<64>, true>), grid, block, 0, s, d_tables, src, n, ParkSealSink<64>{}); break;
-      case 88: hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ParkSealSink<1>, true>), grid, block, 0, s, d_tables, src, n, ParkSealSink<1>{}); break;
-      case 89: hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ParkSealSink<2>, true>), grid, block, 0, s, d_tables, src, n, ParkSealSink<2>{}); break;
-      case 90: hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ParkSealSink<4>, true>), grid, block, 0, s, d_tables, src, n, ParkSealSink<4>{}); break;
-      case 91: hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ParkSealSink<8>, true>), grid, block, 0, s, d_tables, src, n, ParkSealSink<8>{}); break;
-      default: hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ParkSealSink<16>, true>), grid, block, 0, s, d_tables, src, n, ParkSealSink<16>{}); break;
-    }
-    return hipGetLastError();
-  }
-  if (v == 39 && seal) {  // full 32-B-sector rewrites around each trailer
-    hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SealSectorSink, true>), grid, block, 0, s, d_tables, src, n,
-                       SealSectorSink{});
-    return hipGetLastError();
-  }
-  if (v == 37 && seal) {  // one dword store per trailer
-    hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SealDwordSink, true>), grid, block, 0, s, d_tables, src, n,
-                       SealDwordSink{});
-    return hipGetLastError();
-  }
-  if (v == 36 && seal) {  // trailer line read a group before the write
-    hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SealTouchSink, true>), grid, block, 0, s, d_tables, src, n,
-                       SealTouchSink{});
-    return hipGetLastError();
-  }
-  if (v >= 31 && v <= 36) {  // seal-write diagnostics (verify: 31 default-policy loads, else shipped)
-    static std::mutex mu;   // diagnostics only: one scratch array for variants 32 / 35
-    static uint32_t* scratch = nullptr;
-    static uint64_t scratch_n = 0;
-    std::lock_guard<std::mutex> lk(mu);
-    if ((v == 32 || v == 35) && scratch_n < n) {
-      if (scratch) (void)hipFree(scratch);
-      scratch = nullptr;
-      scratch_n = 0;
-      if (hipMalloc(&scratch, n * 4) != hipSuccess) return hipErrorOutOfMemory;
-      scratch_n = n;
-    }
-    if (!seal) {
-      if (v == 31)
-        hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstVerifySink, false>), grid, block, 0, s, d_tables, src, n,
-                           SstVerifySink{ok, nbad});
+  switch (v) {
+    case 140:  // the seal's loads alone / loads + its in-place trailer stores (pattern ceilings;
+    case 141:  // wrong trailers by design; nbad = XOR of what was read)
+      if (!seal) return hipErrorInvalidValue;
+      if (v == 140) hipLaunchKernelGGL(seal_pattern_kernel<0>, grid, block, 0, s, buf, h, n, nbad);
+      else hipLaunchKernelGGL(seal_pattern_kernel<1>, grid, block, 0, s, buf, h, n, nbad);
+      return hipGetLastError();
+    case 72:  // the seal with each group's trailers written when hashed (no parking): the reference
+              // image of the parked-trailer product seal (tests/test_sst4k.py)
+      if (!seal) return hipErrorInvalidValue;
+      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SealSink, true>), grid, block, 0, s, d_tables, src, n, SealSink{});
+      return hipGetLastError();
+    case 18:  // the hooks on the 32-B-piece any-length stream kernel: an independent kernel for the
+              // reference-file tests (tests/test_sst_files.py)
+      if (seal)
+        hipLaunchKernelGGL((crc_stream_kernel<SstSrc, SealSink, 0, true, true>), grid, block, 0, s, d_tables, src, n,
+                           SealSink{});
       else
-        hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstVerifySink, true>), grid, block, 0, s, d_tables, src, n,
-                           SstVerifySink{ok, nbad});
-    } else if (v == 31) {  // default-policy loads
-      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SealSink, false>), grid, block, 0, s, d_tables, src, n, SealSink{});
-    } else if (v == 32 || v == 35) {  // compact 4-B output (+ 35: a separate trailer scatter pass)
-      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, OutSink, true>), grid, block, 0, s, d_tables, src, n,
-                         OutSink{scratch, PDB_CRC_MASK_OUTPUT});
-      if (v == 35)
-        hipLaunchKernelGGL(trailer_scatter_kernel, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256), 0, s, buf,
-                           h, scratch, n);
-    } else if (v == 34) {  // trailers as nt byte stores
-      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, NtSealSink, true>), grid, block, 0, s, d_tables, src, n,
-                         NtSealSink{});
-    } else {  // 33: the seal's kernel with its stores dropped (a verify with nowhere to report)
-      hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstVerifySink, true>), grid, block, 0, s, d_tables, src, n,
-                         SstVerifySink{nullptr, nullptr});
-    }
-    return hipGetLastError();
+        hipLaunchKernelGGL((crc_stream_kernel<SstSrc, SstVerifySink, 0, true, true>), grid, block, 0, s, d_tables,
+                           src, n, SstVerifySink{ok, nbad});
+      return hipGetLastError();
+    default:  // 0: the product routing
+      return launch_sst(g, d_tables, buf, buf_len, h, n, seal, ok, nbad, s);
   }
-  if (v == 18) {  // 32-B-piece stream kernel
-    if (seal)
-      hipLaunchKernelGGL((crc_stream_kernel<SstSrc, SealSink, 0, true, true>), grid, block, 0, s, d_tables, src, n,
-                         SealSink{});
-    else
-      hipLaunchKernelGGL((crc_stream_kernel<SstSrc, SstVerifySink, 0, true, true>), grid, block, 0, s, d_tables,
-                         src, n, SstVerifySink{ok, nbad});
-    return hipGetLastError();
-  }
-  // any other variant (30): the previous default, crc_stream16_kernel
-  if (seal)
-    hipLaunchKernelGGL((crc_stream16_kernel<SstSrc, SealSink, true, true, true>), grid, block, 0, s, d_tables, src, n,
-                       SealSink{});
-  else
-    hipLaunchKernelGGL((crc_stream16_kernel<SstSrc, SstVerifySink, true, true, true>), grid, block, 0, s, d_tables,
-                       src, n, SstVerifySink{ok, nbad});
-  return hipGetLastError();
 }
 
 hipError_t launch_fixed_variant(int v, const LaunchGeom& g, const uint32_t* d_tables, const uint8_t* base,
                                 uint64_t stride, uint32_t len, uint64_t nblk, uint32_t flags, uint32_t init,
                                 uint32_t* out, hipStream_t s) {
-  if (v == 0) return launch_fixed(g, d_tables, base, stride, len, nblk, flags, init, out, s);
-  const dim3 grid(grid_for(g, nblk)), block(kThreads);
-  if (v == 130 && len - 4096u <= 256u && !(flags & PDB_CRC_USE_INIT)) {  // sstable-sized, 12 waves
-    const FixedSrc src{base, stride, len, 0xFFFFFFFFu};
-    hipLaunchKernelGGL((crc_sst4k_kernel<FixedSrc, OutSink, true, 4, QuadTabs, false, true, 12>), grid, dim3(768), 0, s,
-                       d_tables, src, nblk, OutSink{out, flags});
-    return hipGetLastError();
-  }
-  const bool fast = len == 4096u && (reinterpret_cast<uintptr_t>(base) & 15u) == 0 &&
-                    (stride & 15u) == 0;
-  if (!fast) {
+  if (v == 16) {  // the any-length kernel for every length and alignment (16-B pieces, nt, packed trees)
+    const dim3 grid(grid_for(g, nblk)), block(kThreads);
     const FixedSrc src{base, stride, len, (flags & PDB_CRC_USE_INIT) ? ~init : 0xFFFFFFFFu};
-#define PDB_STREAM_FIXED(P)                                                                       \
-  hipLaunchKernelGGL((crc_stream_kernel<FixedSrc, OutSink, P>), grid, block, 0, s, d_tables, src, nblk, \
-                     OutSink{out, flags})
-    switch (v) {  // lock-step period in items (0 = free-running, static strided blocks)
-      case 8: PDB_STREAM_FIXED(0); break;
-      case 9: PDB_STREAM_FIXED(1); break;
-      case 10: PDB_STREAM_FIXED(4); break;
-      case 11: PDB_STREAM_FIXED(8); break;
-      case 12:
-        hipLaunchKernelGGL((crc_stream16_kernel<FixedSrc, OutSink, true, true>), grid, block, 0, s, d_tables,
-                           src, nblk, OutSink{out, flags});
-        break;
-      case 13:
-        hipLaunchKernelGGL((crc_stream16_kernel<FixedSrc, OutSink, true, false>), grid, block, 0, s, d_tables,
-                           src, nblk, OutSink{out, flags});
-        break;
-      case 14:
-        hipLaunchKernelGGL((crc_stream16_kernel<FixedSrc, OutSink, false, true>), grid, block, 0, s, d_tables,
-                           src, nblk, OutSink{out, flags});
-        break;
-      case 15:
-        hipLaunchKernelGGL((crc_stream_kernel<FixedSrc, OutSink, 0, true, true>), grid, block, 0, s, d_tables,
-                           src, nblk, OutSink{out, flags});
-        break;
-      case 16:
-        hipLaunchKernelGGL((crc_stream16_kernel<FixedSrc, OutSink, true, true, true>), grid, block, 0, s,
-                           d_tables, src, nblk, OutSink{out, flags});
-        break;
-      default:
-        hipLaunchKernelGGL((crc_stream_kernel<FixedSrc, OutSink, 0, true>), grid, block, 0, s, d_tables, src,
-                           nblk, OutSink{out, flags});
-        break;
-    }
-#undef PDB_STREAM_FIXED
+    const bool aligned4 = ((reinterpret_cast<uintptr_t>(base) + (len & 15u)) & 3u) == 0 && (stride & 3u) == 0;
+    if (aligned4)
+      hipLaunchKernelGGL((crc_stream16_kernel<FixedSrc, OutSink, true, true, true>), grid, block, 0, s, d_tables, src,
+                         nblk, OutSink{out, flags});
+    else
+      hipLaunchKernelGGL((crc_stream_kernel<FixedSrc, OutSink, 0, true, true>), grid, block, 0, s, d_tables, src, nblk,
+                         OutSink{out, flags});
     return hipGetLastError();
   }
-#define PDB_FAST(NP, D)                                                                       \
-  hipLaunchKernelGGL((crc_fast4k_kernel<NP, D>), grid, block, 0, s, d_tables, base, stride, nblk, \
-                     flags, init, out)
-#define PDB_TEAM(G, D)                                                                        \
-  hipLaunchKernelGGL((crc_team4k_kernel<G, D>), grid, block, 0, s, d_tables, base, stride, nblk, \
-                     flags, init, out)
-#define PDB_K(K) hipLaunchKernelGGL(K, grid, block, 0, s, d_tables, base, stride, nblk, flags, init, out)
-  switch (v) {
-    case 1: PDB_FAST(2, 1); break;  // one 64-lane tree per block, free-running
-    case 2: PDB_FAST(1, 1); break;  // 64-B lane pieces
-    case 3: PDB_FAST(4, 1); break;  // coalesced 16-B pieces, 4 chains + 3 Horner shifts
-    case 4: PDB_TEAM(32, 1); break;  // 2 blocks per wave, 32-lane teams
-    case 5: PDB_TEAM(16, 0); break;  // 4 blocks per wave, 16-lane teams
-    case 6: PDB_K(crc_pingpong4k_kernel); break;
-    case 7: PDB_K((crc_fast4k_kernel<2, 1, true>)); break;  // loads issued before the hash
-    case 8: PDB_K(crc_pack4k_ab_kernel<0>); break;  // packed tree, free-running
-    case 9: PDB_K(crc_pack4k_ab_kernel<2>); break;  // lock-step every 2 groups
-    case 10: PDB_K(crc_pack4k_ab_kernel<4>); break;
-    case 11: PDB_K(crc_pack4k_dyn_kernel); break;  // workgroup-local dynamic groups
-    // coalesced 4 x 16-B lane pieces (each load instruction 1 KiB contiguous), nt loads (13-25;
-    // the shipped default is crc_pack4k_ab_kernel<1, 4, true>)
-    case 12: PDB_K((crc_pack4k_ab_kernel<1>)); break;  // previous default: 2 x 32-B pieces, default policy
-    case 13: PDB_K((crc_pack4k_ab_kernel<0, 4, true>)); break;
-    case 14: PDB_K((crc_pack4k_ab_kernel<1, 2, true>)); break;
-    case 15: PDB_K((crc_pack4k_ab_kernel<0, 4, false>)); break;
-    case 16: PDB_K((crc_pack4k_ab_kernel<2, 4, true>)); break;
-    case 17: PDB_K((crc_pack4k_ab_kernel<4, 4, true>)); break;
-    case 18: PDB_K((crc_pack4k_ab_kernel<8, 4, true>)); break;
-    // 8 waves per CU (512-thread workgroups)
-    case 19: hipLaunchKernelGGL((crc_pack4k_ab_kernel<1, 4, true, 8>), dim3(grid_for8(g, nblk)), dim3(512), 0, s, d_tables,
-                                base, stride, nblk, flags, init, out); break;
-    case 20: hipLaunchKernelGGL((crc_pack4k_ab_kernel<0, 4, true, 8>), dim3(grid_for8(g, nblk)), dim3(512), 0, s, d_tables,
-                                base, stride, nblk, flags, init, out); break;
-    // blocks in pairs (8 chains per wave): 8 waves / 16 waves, lock-step / free
-    case 21: hipLaunchKernelGGL((crc_pack4k_ab_kernel<1, 4, true, 8, true>), dim3(grid_for8(g, nblk)), dim3(512), 0, s,
-                                d_tables, base, stride, nblk, flags, init, out); break;
-    case 22: hipLaunchKernelGGL((crc_pack4k_ab_kernel<0, 4, true, 8, true>), dim3(grid_for8(g, nblk)), dim3(512), 0, s,
-                                d_tables, base, stride, nblk, flags, init, out); break;
-    case 23: PDB_K((crc_pack4k_ab_kernel<1, 4, true, 16, true>)); break;
-    // 12 waves per CU (768-thread workgroups): 48 KiB in flight
-    case 24: hipLaunchKernelGGL((crc_pack4k_ab_kernel<1, 4, true, 12>), dim3(grid_forw(g, nblk, 12)), dim3(768), 0, s,
-                                d_tables, base, stride, nblk, flags, init, out); break;
-    case 25: hipLaunchKernelGGL((crc_pack4k_ab_kernel<2, 4, true, 12>), dim3(grid_forw(g, nblk, 12)), dim3(768), 0, s,
-                                d_tables, base, stride, nblk, flags, init, out); break;
-    // XCD-contiguous workgroup numbering (lock-step / free-running)
-    case 26: PDB_K((crc_pack4k_ab_kernel<1, 4, true, 16, false, true>)); break;
-    case 27: PDB_K((crc_pack4k_ab_kernel<0, 4, true, 16, false, true>)); break;
-    // quad-transposed lanes: 64 contiguous bytes per lane, no per-lane Horner folds
-    case 28: PDB_K((crc_pack4k_ab_kernel<1, 4, true, 16, false, false, 1>)); break;
-    case 29: PDB_K((crc_pack4k_ab_kernel<1, 4, true, 16, false, false, 2>)); break;  // 2 chains + shift 32
-    // s_setprio 2 around the next block's load issue (free-running / lock-step)
-    case 30: PDB_K((crc_pack4k_ab_kernel<1, 4, true, 16, false, false, 0, true>)); break;
-    case 31: PDB_K((crc_pack4k_ab_kernel<0, 4, true, 16, false, false, 0, true>)); break;
-    // the shipped kernel (lane-quarter image) at 8 / 12 waves per CU
-    case 45: hipLaunchKernelGGL((crc_pack4k_kernel<8>), dim3(grid_for8(g, nblk)), dim3(512), 0, s, d_tables, base, stride,
-                                nblk, flags, init, out); break;
-    case 46: hipLaunchKernelGGL((crc_pack4k_kernel<12>), dim3(grid_forw(g, nblk, 12)), dim3(768), 0, s, d_tables, base,
-                                stride, nblk, flags, init, out); break;
-    // the shipped kernel with every chain finished before the folds (round 2)
-    case 47: PDB_K((crc_pack4k_kernel<16, false>)); break;
-    // 99 (and unknown ids): the round-1 shipped kernel, on the 32-replica table image with
-    // single-copy Horner operators (crc_pack4k_kernel now runs on the lane-quarter image)
-    default: PDB_K((crc_pack4k_ab_kernel<1, 4, true>)); break;
-  }
-#undef PDB_FAST
-#undef PDB_TEAM
-#undef PDB_K
-  return hipGetLastError();
+  return launch_fixed(g, d_tables, base, stride, len, nblk, flags, init, out, s);  // 0: the product routing
 }
 
 hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tables, const uint8_t* base,
@@ -1123,233 +205,46 @@ hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tab
   const dim3 grid(grid_for(g, nblk)), block(kThreads);
   const DescSrc src{base, blk, flags};
   const OutSink sink{out, flags};
-  const dim3 lgrid(grid_for(g, (nblk + 63) / 64)), qgrid(grid_for(g, (nblk + 15) / 16));
+  const bool mixed = (flags & PDB_CRC_SIZE_MIXED) != 0;
   switch (v) {
-    case 8:  // 32-B pieces, static strided assignment (free-running)
-      hipLaunchKernelGGL((crc_stream_kernel<DescSrc, OutSink, 0, false>), grid, block, 0, s, d_tables, src, nblk, sink);
-      break;
-    case 12:  // coalesced 16-B pieces, nt loads, dynamic blocks
-      hipLaunchKernelGGL((crc_stream16_kernel<DescSrc, OutSink, true, true>), grid, block, 0, s, d_tables, src, nblk,
-                         sink);
-      break;
-    case 13:  // coalesced 16-B pieces, default-policy loads
-      hipLaunchKernelGGL((crc_stream16_kernel<DescSrc, OutSink, true, false>), grid, block, 0, s, d_tables, src, nblk,
-                         sink);
-      break;
-    case 14:  // coalesced 16-B pieces, nt loads, static strided blocks
-      hipLaunchKernelGGL((crc_stream16_kernel<DescSrc, OutSink, false, true>), grid, block, 0, s, d_tables, src, nblk,
-                         sink);
-      break;
-    case 15:  // 32-B pieces, dynamic blocks, packed 4-block trees
-      hipLaunchKernelGGL((crc_stream_kernel<DescSrc, OutSink, 0, true, true>), grid, block, 0, s, d_tables, src, nblk,
-                         sink);
-      break;
-    case 16:  // 40: size hints ignored -- the any-length kernel (16-B pieces, nt, dynamic, packed trees,
-    case 40:  // byte-balanced workgroup ranges: the product's C3 routing)
+    case 16:  // size hints ignored: the any-length kernel (the product's C3 routing) for every list
       hipLaunchKernelGGL((crc_stream16_kernel<DescSrc, OutSink, true, true, true, QuadTabs, true>), grid, block, 0, s,
                          d_tables, src, nblk, sink);
-      break;
+      return hipGetLastError();
     case 161:  // the C3 routing's loads, scheduling and byte-balanced ranges with NO hash (its pattern
                // ceiling, bench.py pattern_ceiling; wrong CRCs by design)
       hipLaunchKernelGGL((crc_stream16_kernel<DescSrc, OutSink, true, true, true, QuadTabs, true, true, true>), grid, block,
                          0, s, d_tables, src, nblk, sink);
-      break;
-    case 49:  // the C3 routing with every chain finished before the folds (round 2)
-      hipLaunchKernelGGL((crc_stream16_kernel<DescSrc, OutSink, true, true, true, QuadTabs, true, false>), grid, block, 0,
-                         s, d_tables, src, nblk, sink);
-      break;
-    case 71:  // the any-length kernel with equal block counts per workgroup (round-2 C3 routing before bal_bound)
-      hipLaunchKernelGGL((crc_stream16_kernel<DescSrc, OutSink, true, true, true>), grid, block, 0, s, d_tables, src,
-                         nblk, sink);
-      break;
-    case 41:  // the 1-KiB kernel with 4-block groups (fast range 1024..1280 B)
-      hipLaunchKernelGGL((crc_sst1k_kernel<DescSrc, OutSink, true, 4>), grid, block, 0, s, d_tables, src, nblk, sink);
-      break;
-    case 42:  // the 1-KiB kernel on the round-1 table image (32 replicas)
-      hipLaunchKernelGGL((crc_sst1k_kernel<DescSrc, OutSink, true, 8, LaneTabs>), grid, block, 0, s, d_tables, src, nblk,
-                         sink);
-      break;
-    case 44:  // the any-length kernel (C3 routing) on the round-1 table image
-      hipLaunchKernelGGL((crc_stream16_kernel<DescSrc, OutSink, true, true, true, LaneTabs>), grid, block, 0, s, d_tables,
-                         src, nblk, sink);
-      break;
-    case 43:  // the 4-KiB kernel on the round-1 table image (32 replicas, single-copy shift 1024)
-      hipLaunchKernelGGL((crc_sst4k_kernel<DescSrc, OutSink, true, 4, LaneTabs>), grid, block, 0, s, d_tables, src, nblk,
-                         sink);
-      break;
-    case 50:  // one lane per record, 32-B groups loaded one ahead (nt / default policy)
-      hipLaunchKernelGGL((crc_lanerec_kernel<DescSrc, OutSink, true>), lgrid, block, 0, s, d_tables, src, nblk, sink);
-      break;
-    case 51:
-      hipLaunchKernelGGL((crc_lanerec_kernel<DescSrc, OutSink, false>), lgrid, block, 0, s, d_tables, src, nblk, sink);
-      break;
-    case 52:  // the shipped <= 256-B window kernel, for any list
-      hipLaunchKernelGGL((crc_lanerec9_kernel<DescSrc, OutSink>), lgrid, block, 0, s, d_tables, src, nblk, sink);
-      break;
-    case 53:  // the <= 256-B class on the round-1 crc_rec256_kernel (rows of 16 lanes + row tree)
-      hipLaunchKernelGGL((crc_rec256_kernel<DescSrc, OutSink, true>), grid, block, 0, s, d_tables, src, nblk, sink);
-      break;
-    case 54:  // 257..512 B with two chains (9 + 8 groups)
-      hipLaunchKernelGGL((crc_lanerec17_kernel<DescSrc, OutSink, 2>), dim3(grid17(g, nblk)), dim3(kThreads17), 0, s,
-                         d_tables, src, nblk, sink);
-      break;
-    case 55:  // cross-batch prefetch: 9 groups at 512 threads / 17 groups at 256 threads
-      hipLaunchKernelGGL((crc_lanerec_pf_kernel<DescSrc, OutSink, 9, 512>), dim3(grid_wg(g, nblk, 512)), dim3(512), 0,
-                         s, d_tables, src, nblk, sink);
-      break;
-    case 56:
-      hipLaunchKernelGGL((crc_lanerec_pf_kernel<DescSrc, OutSink, 17, 256>), dim3(grid_wg(g, nblk, 256)), dim3(256), 0,
-                         s, d_tables, src, nblk, sink);
-      break;
-    case 57:  // four lanes per record (<= 256 B / <= 512 B)
-      hipLaunchKernelGGL((crc_quadrec_kernel<DescSrc, OutSink, 5, 256>), qgrid, block, 0, s, d_tables, src, nblk, sink);
-      break;
-    case 58:
-      hipLaunchKernelGGL((crc_quadrec_kernel<DescSrc, OutSink, 9, 512>), qgrid, block, 0, s, d_tables, src, nblk, sink);
-      break;
-    case 60:  // round-1 lane-per-record kernels (direct 16-B window loads) for the <= 256 / 512 / 1023 classes
-    case 61:
-    case 62:
-      launch_lanerec(g, d_tables, src, nblk, v == 60 ? 256u : (v == 61 ? 512u : 1023u), sink, s);
-      break;
-    case 68:  // records of 1024..1152 B on crc_sst1k_kernel (8-block groups): the 1K-hint routing before
-              // the record kernel's 1152 class
-      hipLaunchKernelGGL((crc_sst1k_kernel<DescSrc, OutSink, true>), grid, block, 0, s, d_tables, src, nblk, sink);
-      break;
-    case 69: {  // the record kernel's 1152 class (8 lanes of 33-word parts, the head chain alone past
-                // 1056 B) for any list: the shipped 1K-hint routing
-      constexpr uint32_t w = SpanStage<1152>::kWaves;
-      hipLaunchKernelGGL((crc_lanespan_kernel<DescSrc, OutSink, 1152>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0, s,
-                         d_tables, src, nblk, sink, g.wq);
-      break;
-    }
-    case 110:    // the shipped record kernel + per-wave [start, end, items, batches] stamps (s_memrealtime)
-    case 112: {  // at out + nblk rounded up to 8 B (the caller sizes `out` for 4 x 8 B per wave); 112:
-                 // the round-2 static batch assignment (no workgroup counter)
-      const uint32_t cls = (flags & PDB_CRC_SIZE_256) ? 256u
-                           : (flags & PDB_CRC_SIZE_512) ? 512u : ((flags & PDB_CRC_SIZE_1K) ? 1152u : 1023u);
-      StampOutSink ss;
-      ss.out = out;
-      ss.flags = flags;
-      ss.stamps = reinterpret_cast<uint64_t*>(out + ((nblk + 1u) & ~1ull));
-      if (v == 110) launch_lanespan<DescSrc, StampOutSink, 4>(g, d_tables, src, nblk, cls, ss, s);
-      else launch_lanespan<DescSrc, StampOutSink, 4, TabsS4, false>(g, d_tables, src, nblk, cls, ss, s);
-      break;
-    }
-    case 183: {  // the record kernel with the round-2..4 work distribution (each workgroup a fixed range
-                 // of batches, its waves taking them from an LDS counter), for A/B against the queues
-      const uint32_t cls = (flags & PDB_CRC_SIZE_256) ? 256u
-                           : (flags & PDB_CRC_SIZE_512) ? 512u : ((flags & PDB_CRC_SIZE_1K) ? 1152u : 1023u);
-      launch_lanespan<DescSrc, OutSink, 44>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
-      break;
-    }
+      return hipGetLastError();
+    // the record kernel (size-hinted lists): its parts, its cross-checks and its work distribution
+    case 63:  // loads and staging alone (no hash; results undefined)
+      return launch_lanespan<DescSrc, OutSink, 1>(g, d_tables, src, nblk, record_class(flags), sink, s, mixed);
+    case 64:  // the hash alone over stale staging (no loads; results undefined)
+      return launch_lanespan<DescSrc, OutSink, 2>(g, d_tables, src, nblk, record_class(flags), sink, s, mixed);
+    case 67:  // the bookkeeping alone (no loads, no hash)
+      return launch_lanespan<DescSrc, OutSink, 3>(g, d_tables, src, nblk, record_class(flags), sink, s, mixed);
+    case 125:  // exact: the batch-uniform k only (no per-record lanes for mixed sizes)
+      return launch_lanespan<DescSrc, OutSink, 17>(g, d_tables, src, nblk, record_class(flags), sink, s, mixed);
+    case 126:  // the item geometry per record instead of its CRC (MODE 18; tests/test_lanespan.py)
+      return launch_lanespan<DescSrc, OutSink, 18>(g, d_tables, src, nblk, record_class(flags), OutSink{out, 0u}, s,
+                                                   mixed);
+    case 183:  // exact: the round-2..4 work distribution (each workgroup a fixed range of batches, its
+               // waves taking them from an LDS counter), for A/B against the device-wide queues
+      return launch_lanespan<DescSrc, OutSink, 44>(g, d_tables, src, nblk, record_class(flags), sink, s, mixed);
     case 180:    // the product / loads + staging alone / hash alone, + per-wave [start, end] s_memrealtime
-    case 181:    // and [start, end] s_memtime stamps (the waves' shader clock; tools/span_clock.py)
-    case 182: {
-      const uint32_t cls = (flags & PDB_CRC_SIZE_256) ? 256u
-                           : (flags & PDB_CRC_SIZE_512) ? 512u : ((flags & PDB_CRC_SIZE_1K) ? 1152u : 1023u);
+    case 181:    // and [start, end] s_memtime stamps at out + nblk rounded up to 8 B (the caller sizes
+    case 182: {  // `out` for 4 x 8 B per wave; tools/span_clock.py)
       StampOutSink ss;
       ss.out = out;
       ss.flags = flags;
       ss.stamps = reinterpret_cast<uint64_t*>(out + ((nblk + 1u) & ~1ull));
-      if (v == 180) launch_lanespan<DescSrc, StampOutSink, 40>(g, d_tables, src, nblk, cls, ss, s);
-      else if (v == 181) launch_lanespan<DescSrc, StampOutSink, 41>(g, d_tables, src, nblk, cls, ss, s);
-      else launch_lanespan<DescSrc, StampOutSink, 42>(g, d_tables, src, nblk, cls, ss, s);
-      break;
-    }
-    case 113:    // pricing (wrong CRCs): the record kernel with conflict-free staging reads
-    case 114: {  // ... and conflict-free fold-operator lookups
-      const uint32_t cls = (flags & PDB_CRC_SIZE_256) ? 256u
-                           : (flags & PDB_CRC_SIZE_512) ? 512u : ((flags & PDB_CRC_SIZE_1K) ? 1152u : 1023u);
-      if (v == 113) launch_lanespan<DescSrc, OutSink, 5>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
-      else launch_lanespan<DescSrc, OutSink, 6>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
-      break;
-    }
-    case 118:    // exact: the round-2 finish (table step per chain before the folds, bpermute partners)
-    case 119:    // exact: the shipped finish with bpermute partners (no DPP)
-    case 121:    // exact: the A, B, C chain steps issued one chain at a time (round 2)
-    case 122:    // exact: halves always records 0-7 | 8-15 (no bank-spread choice)
-    case 123:    // exact: the first row's bank-spread choice taken for the whole batch
-    case 124:    // exact: 10 waves x 9-KiB regions for every class
-    case 125:    // exact: the batch-uniform k only (no per-record lanes for mixed sizes; round 3 before)
-    case 126:    // the item geometry per record instead of its CRC (MODE 18)
-    case 160:    // exact: the staging reads as aligned ds_read_b64 pairs (MODE 19; round 4, slower)
-    case 162:    // exact: the round-3 cross-lane tree of operator levels (no per-lane pre-shift; MODE 21)
-    case 163:    // exact: p-word selects only where some lane replaces (MODE 22)
-    case 165:    // exact: the round-3 staging-read addressing (no opaque base; MODE 27)
-    case 166:    // exact: the staging reads from one opaque base per chain (MODE 25)
-    case 167:    // exact: one compare per step for the p-word selects (MODE 26)
-    case 168:    // exact: the finishing step folded into the pre-shifted cross-lane fold (MODE 28)
-    case 169:    // exact: the lock-step staging reads rotated over chain slots by bank class (MODE 29)
-    case 170:    // exact: one item's loads in flight instead of two (MODE 30)
-    case 171:    // exact: ... and 13 waves x 7-KiB regions (MODE 31)
-    case 172:    // exact: the p-word selects as wave masks (inverse ballot; MODE 32)
-    case 174:    // exact: ... on every step, branch-free (MODE 34)
-    case 175:    // exact: the plain selects on every step, branch-free (MODE 35; the product since late round 4)
-    case 176:    // exact: the p-word selects only up to the item's last replacement step (MODE 36; before)
-    case 177:    // exact: chunks past the item's span neither loaded nor staged (MODE 37)
-    case 178:    // exact: ... not staged (MODE 38; the product since late round 4)
-    case 179: {  // exact: every chunk staged (MODE 39; before)
-      const uint32_t cls = (flags & PDB_CRC_SIZE_256) ? 256u
-                           : (flags & PDB_CRC_SIZE_512) ? 512u : ((flags & PDB_CRC_SIZE_1K) ? 1152u : 1023u);
-      if (v == 118) launch_lanespan<DescSrc, OutSink, 10>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
-      else if (v == 119) launch_lanespan<DescSrc, OutSink, 11>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
-      else if (v == 121) launch_lanespan<DescSrc, OutSink, 13>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
-      else if (v == 122) launch_lanespan<DescSrc, OutSink, 14>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
-      else if (v == 123) launch_lanespan<DescSrc, OutSink, 15>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
-      else if (v == 124) launch_lanespan<DescSrc, OutSink, 16>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
-      else if (v == 125) launch_lanespan<DescSrc, OutSink, 17>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
-      else if (v == 160) launch_lanespan<DescSrc, OutSink, 19>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
-      else if (v == 162) launch_lanespan<DescSrc, OutSink, 21>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
-      else if (v == 163) launch_lanespan<DescSrc, OutSink, 22>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
-      else if (v == 165) launch_lanespan<DescSrc, OutSink, 27>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
-      else if (v == 167) launch_lanespan<DescSrc, OutSink, 26>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
-      else if (v == 168) launch_lanespan<DescSrc, OutSink, 28>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
-      else if (v == 170) launch_lanespan<DescSrc, OutSink, 30>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
-      else if (v == 171) launch_lanespan<DescSrc, OutSink, 31>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
-      else if (v == 172) launch_lanespan<DescSrc, OutSink, 32>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
-      else if (v == 174) launch_lanespan<DescSrc, OutSink, 34>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
-      else if (v == 175) launch_lanespan<DescSrc, OutSink, 35>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
-      else if (v == 176) launch_lanespan<DescSrc, OutSink, 36>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
-      else if (v == 177) launch_lanespan<DescSrc, OutSink, 37>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
-      else if (v == 178) launch_lanespan<DescSrc, OutSink, 38>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
-      else if (v == 179) launch_lanespan<DescSrc, OutSink, 39>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
-      else if (v == 169) launch_lanespan<DescSrc, OutSink, 29>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
-      else if (v == 166) launch_lanespan<DescSrc, OutSink, 25>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
-      else launch_lanespan<DescSrc, OutSink, 18>(g, d_tables, src, nblk, cls, OutSink{out, 0u}, s, (flags & PDB_CRC_SIZE_MIXED) != 0);
-      break;
-    }
-    case 115:    // pricing (wrong CRCs): no p-word replacement selects
-    case 116:    // ... no cross-lane folds
-    case 117: {  // ... no in-part folds
-      const uint32_t cls = (flags & PDB_CRC_SIZE_256) ? 256u
-                           : (flags & PDB_CRC_SIZE_512) ? 512u : ((flags & PDB_CRC_SIZE_1K) ? 1152u : 1023u);
-      if (v == 115) launch_lanespan<DescSrc, OutSink, 7>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
-      else if (v == 116) launch_lanespan<DescSrc, OutSink, 8>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
-      else launch_lanespan<DescSrc, OutSink, 9>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
-      break;
-    }
-    case 111: {  // the record kernel with the round-2 static batch assignment (batch wave_id + k W)
-      const uint32_t cls = (flags & PDB_CRC_SIZE_256) ? 256u
-                           : (flags & PDB_CRC_SIZE_512) ? 512u : ((flags & PDB_CRC_SIZE_1K) ? 1152u : 1023u);
-      launch_lanespan<DescSrc, OutSink, 0, TabsS4, false>(g, d_tables, src, nblk, cls, OutSink{out, flags}, s);
-      break;
-    }
-    case 63:  // the record kernel's loads and staging alone (no hash; results undefined)
-    case 64:  // the record kernel's hash alone over stale staging (no loads; results undefined)
-    case 67:  // the record kernel's bookkeeping alone (no loads, no hash)
-    {
-      const uint32_t cls = (flags & PDB_CRC_SIZE_256) ? 256u
-                           : (flags & PDB_CRC_SIZE_512) ? 512u : ((flags & PDB_CRC_SIZE_1K) ? 1152u : 1023u);
-      if (v == 63) launch_lanespan<DescSrc, OutSink, 1>(g, d_tables, src, nblk, cls, sink, s);
-      else if (v == 64) launch_lanespan<DescSrc, OutSink, 2>(g, d_tables, src, nblk, cls, sink, s);
-      else launch_lanespan<DescSrc, OutSink, 3>(g, d_tables, src, nblk, cls, sink, s);
-      break;
+      if (v == 180) return launch_lanespan<DescSrc, StampOutSink, 40>(g, d_tables, src, nblk, record_class(flags), ss, s, mixed);
+      if (v == 181) return launch_lanespan<DescSrc, StampOutSink, 41>(g, d_tables, src, nblk, record_class(flags), ss, s, mixed);
+      return launch_lanespan<DescSrc, StampOutSink, 42>(g, d_tables, src, nblk, record_class(flags), ss, s, mixed);
     }
     default:  // 0 (and unknown ids): the shipped routing
       return launch_desc(g, d_tables, base, blk, nblk, flags, kModeOut, nullptr, out, nullptr, nullptr, s);
   }
-  return hipGetLastError();
 }
 
 hipError_t launch_read_stream(const uint8_t* base, uint64_t nbytes, uint32_t* out, hipStream_t s) {
@@ -1361,51 +256,8 @@ hipError_t launch_read_stream(const uint8_t* base, uint64_t nbytes, uint32_t* ou
 
 hipError_t launch_read_pattern4k(const LaunchGeom& g, const uint8_t* base, uint64_t nblk,
                                  int variant, uint32_t* out, hipStream_t s) {
-  const dim3 grid(g.grid), block(kThreads);
-#define PDB_RP(P, D, A) \
-  hipLaunchKernelGGL((read_pattern4k_kernel<P, D, A>), grid, block, 0, s, base, nblk, out)
-  switch (variant) {
-    case 1: PDB_RP(1, 1, 0); break;
-    case 2: PDB_RP(0, 2, 0); break;
-    case 3: PDB_RP(1, 2, 0); break;
-    case 4: PDB_RP(0, 1, 1); break;
-    case 5: PDB_RP(1, 1, 1); break;
-    case 6: PDB_RP(1, 4, 0); break;
-    case 7: PDB_RP(0, 4, 0); break;
-    case 8: PDB_RP(2, 1, 0); break;
-    case 9: PDB_RP(2, 2, 0); break;
-    // workgroup lock-step (one barrier per iteration), as in the shipped CRC kernels
-    case 10: hipLaunchKernelGGL((read_pattern4k_kernel<2, 1, 0, true>), grid, block, 0, s, base, nblk, out); break;
-    case 11: hipLaunchKernelGGL((read_pattern4k_kernel<1, 1, 0, true>), grid, block, 0, s, base, nblk, out); break;
-    case 12: hipLaunchKernelGGL((read_pattern4k_kernel<2, 4, 0, true>), grid, block, 0, s, base, nblk, out); break;
-    case 13: hipLaunchKernelGGL((read_pattern4k_kernel<1, 4, 0, true>), grid, block, 0, s, base, nblk, out); break;
-    // LDS-DMA (global_load_lds_dwordx4) into a per-wave ring: default / nt policy, depth 1-2
-    case 14: hipLaunchKernelGGL((read_glds4k_kernel<0, 1>), grid, block, 0, s, base, nblk, out); break;
-    case 15: hipLaunchKernelGGL((read_glds4k_kernel<2, 1>), grid, block, 0, s, base, nblk, out); break;
-    case 16: hipLaunchKernelGGL((read_glds4k_kernel<0, 2>), grid, block, 0, s, base, nblk, out); break;
-    case 17: hipLaunchKernelGGL((read_glds4k_kernel<2, 2>), grid, block, 0, s, base, nblk, out); break;
-    // register loads with the nt policy (__builtin_nontemporal_load)
-    case 18: hipLaunchKernelGGL((read_pattern4k_kernel<1, 1, 0, false, true>), grid, block, 0, s, base, nblk, out); break;
-    case 19: hipLaunchKernelGGL((read_pattern4k_kernel<2, 1, 0, false, true>), grid, block, 0, s, base, nblk, out); break;
-    case 20: hipLaunchKernelGGL((read_pattern4k_kernel<2, 1, 0, true, true>), grid, block, 0, s, base, nblk, out); break;
-    case 21: hipLaunchKernelGGL((read_pattern4k_kernel<1, 4, 0, true, true>), grid, block, 0, s, base, nblk, out); break;
-    // LDS-DMA nt with less LDS: 2-KiB units (32 KiB ring per CU), 8 waves x 4 KiB, 2-KiB depth 2
-    case 22: hipLaunchKernelGGL((read_glds4k_kernel<2, 1, 2>), grid, block, 0, s, base, nblk, out); break;
-    case 23: hipLaunchKernelGGL((read_glds4k_kernel<2, 1, 4, 8>), grid, dim3(512), 0, s, base, nblk, out); break;
-    case 24: hipLaunchKernelGGL((read_glds4k_kernel<2, 2, 2>), grid, block, 0, s, base, nblk, out); break;
-    case 25: hipLaunchKernelGGL((read_glds4k_kernel<2, 1, 1>), grid, block, 0, s, base, nblk, out); break;
-    // nt register loads, coalesced: depth 2 / sync period per 4 blocks
-    case 26: hipLaunchKernelGGL((read_pattern4k_kernel<1, 2, 0, false, true>), grid, block, 0, s, base, nblk, out); break;
-    case 27: hipLaunchKernelGGL((read_pattern4k_kernel<1, 1, 1, false, true>), grid, block, 0, s, base, nblk, out); break;
-    // 8 waves per CU (512-thread workgroups), nt coalesced: depth 1 / 2 / lock-step
-    case 28: hipLaunchKernelGGL((read_pattern4k_kernel<1, 1, 0, false, true, 8>), grid, dim3(512), 0, s, base, nblk, out); break;
-    case 29: hipLaunchKernelGGL((read_pattern4k_kernel<1, 2, 0, false, true, 8>), grid, dim3(512), 0, s, base, nblk, out); break;
-    case 30: hipLaunchKernelGGL((read_pattern4k_kernel<1, 1, 0, true, true, 8>), grid, dim3(512), 0, s, base, nblk, out); break;
-    case 31: hipLaunchKernelGGL((read_pattern4k_kernel<1, 1, 0, false, true, 12>), grid, dim3(768), 0, s, base, nblk, out); break;
-    case 32: hipLaunchKernelGGL((read_pattern4k_kernel<1, 1, 0, true, true, 12>), grid, dim3(768), 0, s, base, nblk, out); break;
-    default: PDB_RP(0, 1, 0); break;
-  }
-#undef PDB_RP
+  if (variant != 21) return hipErrorInvalidValue;  // the 4-KiB path's pattern (the others: round 1-2, removed)
+  hipLaunchKernelGGL(read_pattern4k_kernel, dim3(g.grid), dim3(kThreads), 0, s, base, nblk, out);
   return hipGetLastError();
 }
 

@@ -182,18 +182,6 @@ def test_fast_path_partial_groups(crc, oracle_lib, nblk):
     assert (got == exp).all()
 
 
-def test_all_fast_variants_bit_exact(crc, oracle_lib):
-    """The A/B variants of the 4-KiB path (libpdb_crc32c_diag.so) are all exact."""
-    nblk = 3 * 4096 * 4 + 7
-    d = torch.empty(nblk * 4096, dtype=torch.uint8, device="cuda")
-    diag.fill_splitmix(d, 4242)
-    exp = oracle_lib.batch(d.cpu().numpy(), crc.make_blocks(np.arange(nblk) * 4096, np.full(nblk, 4096)),
-                           nthreads=8)
-    for v in list(range(32)) + [99]:  # 99: unknown id -> the round-1 32-replica table image
-        got = _u32(diag.batch_fixed(v, d, 4096, 4096, nblk))
-        assert (got == exp).all(), f"variant {v}"
-
-
 def test_device_entry_points_capture_into_hip_graph(crc, oracle_lib):
     """Device entry points are stream-ordered and allocation-free (include/pdb_crc32c.h): a
     captured hipGraph replays them and recomputes after the input changes."""
@@ -274,11 +262,10 @@ def test_scalar_extend_zero_copy_sizes(crc, oracle_lib):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [12, 13, 14, 15, 16])
+@pytest.mark.parametrize("variant", [16])
 def test_stream_variants_exact(crc, golden, oracle_lib, variant):
-    """A/B variants of the descriptor / generic fixed paths (12-14: coalesced 16-B-piece stream
-    kernel; 15: 32-B pieces with packed 4-block trees; 16: the shipped any-length kernel): the
-    golden sweep (every alignment x every length 0..300), the golden batches, and unaligned /
+    """The shipped any-length kernel forced on every list (diagnostics variant 16, whatever the
+    sizes would route to): the golden sweep (every alignment x every length 0..300), the golden batches, and unaligned /
     multi-round fixed strides, all against the reference's vectors and the oracle."""
     sw = golden["sweep"]
     buf = _materialize(sw["input"])
@@ -445,4 +432,4 @@ def test_byte_balanced_ranges_any_list(crc, oracle_lib, order):
     got = _u32(crc.batch(d, d_blk))
     exp = oracle_lib.batch(d.cpu().numpy(), blk, nthreads=8)
     assert (got == exp).all(), int(np.nonzero(got != exp)[0][0])
-    assert (_u32(diag.batch_desc(71, d, d_blk)) == exp).all()
+    assert (_u32(diag.batch_desc(16, d, d_blk)) == exp).all()

@@ -119,23 +119,6 @@ def test_fixed_strides(crc, oracle_lib, length, shift):
         assert (got == exp).all(), (length, stride, shift)
 
 
-def test_matches_round1_lane_kernels(crc, oracle_lib):
-    """The round-1 direct-load kernels (diagnostics variants 60-62) and the previous 1-KiB kernel
-    (crc_sst1k_kernel, variant 68) give the same CRCs."""
-    import oracle
-    from bench import wal_layout
-    from pebblesdb_amd import diag
-
-    for payload, hint, v in ((131, crc.SIZE_256, 60), (431, crc.SIZE_512, 61), (700, crc.SIZE_1023, 62),
-                             (1055, crc.SIZE_1K, 68)):
-        offs, lens = wal_layout(2 << 20, payload)
-        base = oracle.splitmix_bytes(int(offs[-1] + lens[-1]) + 64, payload + 9)
-        d_base, d_blk = torch.from_numpy(base).cuda(), crc.blocks_to_device(crc.make_blocks(offs, lens))
-        a = diag.batch_desc(0, d_base, d_blk, flags=hint).cpu().numpy()
-        b = diag.batch_desc(v, d_base, d_blk, flags=hint).cpu().numpy()
-        assert (a == b).all()
-
-
 @pytest.mark.parametrize("lo,hi,hint", [(1, 257, "256"), (64, 257, "256"), (1, 200, "256"), (120, 216, "512"),
                                         (257, 513, "512m"), (300, 500, "512m"),
                                         (1, 513, "512m"), (64, 1000, "1023m"), (513, 1024, "1023m"), (1, 1024, "1023m"),
@@ -195,20 +178,14 @@ def test_mixed_geometry_items():
             assert lane[r] == int(k[64 * b + i0:64 * b + r].sum()) and lane[r] + kl[r] <= 64
 
 
-# round-4 diagnostics forms of the record kernel: 160 aligned b64 staging
-# pairs (MODE 19), 162 round-3 cross-lane tree (21), 163 sparse selects (22), 165 round-3 staging
-# addressing (27), 166 opaque base per chain (25), 167 one-compare selects (26), 168 finishing step in
-# the pre-shift (28), 169 bank-class slot rotation (29), 170 one-deep staging (30), 171 13 x 7-KiB
-# waves (31), 172 wave-mask selects (32), 174 / 175 branch-free selects (34 / 35), 176 the selects
-# bounded by the item's last replacement step (36, the product before late round 4), 177 / 178 chunks
-# past the item's span not loaded and / or not staged (37 / 38, the latter the product since late
-# round 4), 179 every chunk staged (39)
-ROUND4_VARIANTS = [160, 162, 163, 165, 166, 167, 168, 169, 170, 171, 172, 174, 175, 176, 177, 178, 179]
+# 183: the round-2..4 work distribution (each workgroup a fixed range of batches, MODE 44), against
+# which the device-wide queues of round 5 were measured; 125: the batch-uniform lane count only
+RECORD_VARIANTS = [183, 125]
 
 
 @pytest.mark.parametrize("hint", ["256", "512", "512m", "1023", "1023m", "1k"])
-def test_round4_record_variants_exact(crc, oracle_lib, hint):
-    """Every A/B form measured in round 4 is exact: spread, unsorted, duplicated and far records with
+def test_record_variants_exact(crc, oracle_lib, hint):
+    """The record kernel's diagnostics forms are exact too: spread, unsorted, duplicated and far records with
     records outside the class among them (the slow path), against the oracle."""
     import oracle
     from pebblesdb_amd import diag
@@ -226,7 +203,7 @@ def test_round4_record_variants_exact(crc, oracle_lib, hint):
     exp = oracle_lib.batch(base, blk, flags=1, nthreads=8)
     d_base, d_blk = torch.from_numpy(base).cuda(), crc.blocks_to_device(blk)
     flags = crc._SIZE_HINT[hint] | 1  # masked output, as crc.batch(masked=True)
-    for v in ROUND4_VARIANTS:
+    for v in RECORD_VARIANTS:
         got = diag.batch_desc(v, d_base, d_blk, flags=flags).cpu().numpy().view(np.uint32)
         bad = np.nonzero(got != exp)[0]
         assert bad.size == 0, (hint, v, bad.size, int(lens[bad[0]]))
