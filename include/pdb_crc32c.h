@@ -130,6 +130,15 @@ int pdb_crc32c_verify_device(const void* d_base, const pdb_blk* d_blk, uint64_t 
                              const uint32_t* d_expected, uint8_t* d_ok, uint32_t* d_nbad,
                              void* stream);
 
+/* ---- pinned host staging -----------------------------------------------------------------------
+ * Page-locked host memory for a caller that stages the blocks of host batches (pdb_sst_seal_host,
+ * pdb_sst_verify_host, pdb_crc32c_batch_host, ...): spans in it reach the device by DMA, without the
+ * runtime's pageable bounce copies (integration/pdb_table_builder.cc stages its sealed batches in
+ * it).  Any host memory stays valid for every entry point; this only changes the copy rate.
+ * *out = NULL for bytes == 0.  Free with pdb_host_free (NULL is a no-op). */
+int pdb_host_alloc(uint64_t bytes, void** out);
+int pdb_host_free(void* p);
+
 /* ---- host batches (copy-inclusive: H2D + kernel + D2H on the internal stream) ---------------
  * Staged in groups of at most 256 MiB of span, so the device workspace stays bounded. */
 int pdb_crc32c_batch_host(const void* base, uint64_t base_len, const pdb_blk* blk, uint64_t nblk,

@@ -15,12 +15,20 @@
 #include "pdb_crc32c.h"
 
 #if PDB_CPU_CRC
+#include <stdlib.h>
+
 #include "util/coding.h"
 #include "util/crc32c.h"
 
 namespace pdb_route {
 inline const char* Name() { return "cpu"; }
 inline const char* LastError() { return "cpu crc"; }
+// staging memory for the sealed batches: plain heap memory (no device to copy to)
+inline int HostAlloc(uint64_t n, void** out) {
+  *out = n ? malloc(static_cast<size_t>(n)) : nullptr;
+  return n && !*out ? PDB_ENOMEM : PDB_OK;
+}
+inline void HostFree(void* p) { free(p); }
 // WriteRawBlock's trailer math per handle: [type] is already at contents + size
 inline int SstSealHost(void* buf, uint64_t len, const pdb_block_handle* h, uint64_t n) {
   char* b = static_cast<char*>(buf);
@@ -59,6 +67,9 @@ inline uint32_t Unmask(uint32_t m) { return leveldb::crc32c::Unmask(m); }
 namespace pdb_route {
 inline const char* Name() { return "gpu"; }
 inline const char* LastError() { return pdb_last_error(); }
+// staging memory for the sealed batches: page-locked, so each batch reaches the device by DMA
+inline int HostAlloc(uint64_t n, void** out) { return pdb_host_alloc(n, out); }
+inline void HostFree(void* p) { (void)pdb_host_free(p); }
 inline int SstSealHost(void* buf, uint64_t len, const pdb_block_handle* h, uint64_t n) {
   return pdb_sst_seal_host(buf, len, h, n);
 }

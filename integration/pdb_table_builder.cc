@@ -18,7 +18,10 @@
 //     a block may still be staged in memory (Finish() always writes everything; Abandon() drops it);
 //   * a device error surfaces as Status::IOError("pdb_sst_seal_host", <message>) from the call that
 //     sealed (Add, Flush or Finish), never as a wrong trailer (there is no CPU fallback).
-// Batch size: PDB_SEAL_BATCH_BYTES (default 4 MiB of staged blocks).  PDB_SEAL_ASYNC=1 seals a
+// Batch size: PDB_SEAL_BATCH_BYTES (default 4 MiB of staged blocks).  The batches are staged in
+// page-locked memory from the checksum library (pdb_host_alloc, pdb_crc_route.h), so each seal's H2D
+// copy is one DMA instead of the runtime's pageable bounce copies (the in-engine
+// copy-inclusive seal rate).  PDB_SEAL_ASYNC=1 seals a
 // full batch asynchronously (one std::async task per batch) while the builder stages the next one;
 // the next seal, Finish() or Abandon() first waits for it and appends its bytes, so the file still
 // receives the batches in order and the GPU seal overlaps block building.
@@ -26,7 +29,9 @@
 // synchronous, profiles/r02_c5_seal_async/) -- the seals of concurrent builders serialise on the
 // device and the compaction thread is not waiting on them.
 #include <stdlib.h>
+#include <string.h>
 
+#include <algorithm>
 #include <future>
 #include <string>
 #include <vector>
@@ -55,12 +60,54 @@ size_t SealBatchBytes() {
   }();
   return v;
 }
+// A growable byte buffer in the route's staging memory (page-locked on the GPU route).  Growth
+// copies; the builder keeps two of them (staged, in flight) for its whole life, so after the first
+// batches no allocation happens.
+class StageBuf {
+ public:
+  StageBuf() = default;
+  StageBuf(const StageBuf&) = delete;
+  StageBuf& operator=(const StageBuf&) = delete;
+  ~StageBuf() { pdb_route::HostFree(p_); }
+  char* data() { return p_; }
+  size_t size() const { return n_; }
+  void clear() { n_ = 0; }
+  // false: the staging memory could not grow
+  bool append(const char* d, size_t k) {
+    if (n_ + k > cap_ && !grow(n_ + k)) return false;
+    memcpy(p_ + n_, d, k);
+    n_ += k;
+    return true;
+  }
+  void swap(StageBuf& o) {
+    std::swap(p_, o.p_);
+    std::swap(n_, o.n_);
+    std::swap(cap_, o.cap_);
+  }
+
+ private:
+  bool grow(size_t need);
+  char* p_ = nullptr;
+  size_t n_ = 0, cap_ = 0;
+};
+
 bool SealAsync() {
   static const bool v = [] {
     const char* e = getenv("PDB_SEAL_ASYNC");
     return e && e[0] == '1';
   }();
   return v;
+}
+bool StageBuf::grow(size_t need) {
+  // a batch ends just past SealBatchBytes(); one block can be larger
+  const size_t cap = std::max(need, std::max(2 * cap_, SealBatchBytes() + (SealBatchBytes() >> 2)));
+  void* q = nullptr;
+  if (pdb_route::HostAlloc(cap, &q) != 0 || !q) return false;
+  if (n_) memcpy(q, p_, n_);
+  pdb_route::HostFree(p_);
+  p_ = static_cast<char*>(q);
+  cap_ = cap;
+  return true;
 }
 }  // namespace
 
@@ -82,10 +129,10 @@ struct TableBuilder::Rep {
   BlockHandle pending_handle;
   std::string compressed_output;
   // buffered emission: blocks in file order, each [contents][type][crc placeholder]
-  std::string staged;
+  StageBuf staged;
   std::vector<pdb_block_handle> staged_handles;  // relative to staged
   // the previous batch, being sealed on the GPU by an async task (its bytes follow in the file)
-  std::string inflight;
+  StageBuf inflight;
   std::vector<pdb_block_handle> inflight_handles;
   std::future<int> inflight_rc;
   uint64_t inflight_ns = 0;
@@ -113,7 +160,7 @@ struct TableBuilder::Rep {
     if (rc != 0) {
       if (status.ok()) status = Status::IOError("pdb_sst_seal_host", pdb_route::LastError());
     } else if (status.ok()) {
-      status = file->Append(Slice(inflight));
+      status = file->Append(Slice(inflight.data(), inflight.size()));
       if (status.ok()) status = file->Flush();
     }
     inflight.clear();
@@ -135,7 +182,7 @@ struct TableBuilder::Rep {
     staged_handles.clear();
     inflight_rc = std::async(std::launch::async, [this] {
       const uint64_t t0 = pdb_hooks::NowNs();
-      const int rc = pdb_route::SstSealHost(&inflight[0], inflight.size(), inflight_handles.data(), inflight_handles.size());
+      const int rc = pdb_route::SstSealHost(inflight.data(), inflight.size(), inflight_handles.data(), inflight_handles.size());
       inflight_ns = pdb_hooks::NowNs() - t0;
       return rc;
     });
@@ -149,12 +196,12 @@ struct TableBuilder::Rep {
     if (staged_handles.empty()) return;
     if (status.ok()) {
       const uint64_t t0 = pdb_hooks::NowNs();
-      const int rc = pdb_route::SstSealHost(&staged[0], staged.size(), staged_handles.data(), staged_handles.size());
+      const int rc = pdb_route::SstSealHost(staged.data(), staged.size(), staged_handles.data(), staged_handles.size());
       pdb_hooks::AddSeal(staged_handles.size(), staged.size(), pdb_hooks::NowNs() - t0);
       if (rc != 0) {
         status = Status::IOError("pdb_sst_seal_host", pdb_route::LastError());
       } else {
-        status = file->Append(Slice(staged));
+        status = file->Append(Slice(staged.data(), staged.size()));
         if (status.ok()) status = file->Flush();
       }
     }
@@ -239,9 +286,11 @@ void TableBuilder::WriteRawBlock(const Slice& contents, CompressionType type, Bl
   handle->set_offset(r->offset);
   handle->set_size(contents.size());
   const uint64_t rel = r->staged.size();
-  r->staged.append(contents.data(), contents.size());
   const char trailer[kBlockTrailerSize] = {static_cast<char>(type), 0, 0, 0, 0};  // crc: sealed in batch
-  r->staged.append(trailer, kBlockTrailerSize);
+  if (!r->staged.append(contents.data(), contents.size()) || !r->staged.append(trailer, kBlockTrailerSize)) {
+    r->status = Status::IOError("pdb_host_alloc", "staging memory for the sealed batch");
+    return;
+  }
   r->staged_handles.push_back(pdb_block_handle{rel, contents.size()});
   r->offset += contents.size() + kBlockTrailerSize;
   if (r->staged.size() >= SealBatchBytes()) r->SealStagedAsync();

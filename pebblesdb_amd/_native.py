@@ -39,6 +39,8 @@ _I = ctypes.c_int
 # name -> (restype, argtypes): the complete exported surface of include/pdb_crc32c.h
 SIGNATURES = {
     "pdb_crc32c_abi_version": (_I, []),
+    "pdb_host_alloc": (_I, [_U64, ctypes.POINTER(ctypes.c_void_p)]),
+    "pdb_host_free": (_I, [_V]),
     "pdb_crc32c_init": (_I, [_I]),
     "pdb_last_error": (ctypes.c_char_p, []),
     "pdb_crc32c_current_device": (_I, []),

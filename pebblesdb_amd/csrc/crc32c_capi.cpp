@@ -45,6 +45,10 @@ struct HostCtx {
   uint8_t* d_ws = nullptr;
   size_t ws_cap = 0;
   uint32_t* wq = nullptr;  // the record kernel's work-queue words for `stream` (kWqBytes, zeroed)
+  // page-locked host scratch for a call's small per-block arrays (rebased handles in, trailer words
+  // / ok bytes out): DMA'd directly instead of through the runtime's pageable bounce buffers
+  uint8_t* h_pin = nullptr;
+  size_t h_pin_cap = 0;
 };
 constexpr int kHostCtx = 4;
 // crc_lanespan_kernel's work queues: 8 queue words + the exit count, each on its own 128-B line
@@ -256,6 +260,22 @@ int ensure_ws(HostCtx* c, size_t bytes) {
   hipError_t e = hipMalloc(&c->d_ws, cap);
   if (e != hipSuccess) return fail(PDB_ENOMEM, std::string("hipMalloc(workspace): ") + hipGetErrorString(e));
   c->ws_cap = cap;
+  return PDB_OK;
+}
+
+int ensure_pin(HostCtx* c, size_t bytes) {
+  if (bytes <= c->h_pin_cap) return PDB_OK;
+  if (c->h_pin) {
+    (void)hipStreamSynchronize(c->copy_stream);
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipHostFree(c->h_pin);
+    c->h_pin = nullptr;
+    c->h_pin_cap = 0;
+  }
+  size_t cap = std::max<size_t>(bytes, 1 << 16);
+  hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&c->h_pin), cap, hipHostMallocDefault);
+  if (e != hipSuccess) return fail(PDB_ENOMEM, std::string("hipHostMalloc(scratch): ") + hipGetErrorString(e));
+  c->h_pin_cap = cap;
   return PDB_OK;
 }
 
@@ -852,27 +872,31 @@ int host_sst(uint8_t* buf, uint64_t buf_len, const pdb_block_handle* h, uint64_t
   hipError_t e = hipSetDevice(dev->device);
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
   if ((rc = ensure_ws(st, nslots * slot_bytes + 256))) return rc;
+  // pinned: every group's rebased handles, then the trailer words (seal) or ok bytes (verify), then nbad
+  const size_t pin_crc = align_up(n * sizeof(pdb_block_handle), 64);
+  if ((rc = ensure_pin(st, pin_crc + align_up(4 * n, 64) + 64))) return rc;
   hipStream_t s = st->stream, cs = st->copy_stream;
   uint32_t* d_nbad = reinterpret_cast<uint32_t*>(st->d_ws + nslots * slot_bytes);
   // Seal: only the 4 CRC bytes of every trailer change, so the kernel writes the masked CRCs into
   // a compact array, 4 B per block come back across PCIe (not the span), and the host encodes
   // them little-endian at offset + size + 1 (table_builder.cc:199-200).
-  std::vector<uint32_t> crc(seal ? n : 0);
-  std::vector<std::vector<pdb_block_handle>> rhs(groups.size());  // async H2D sources
-  uint32_t nb = 0;
+  pdb_block_handle* h_rh = reinterpret_cast<pdb_block_handle*>(st->h_pin);  // async H2D sources
+  uint32_t* crc = reinterpret_cast<uint32_t*>(st->h_pin + pin_crc);
+  uint8_t* h_ok = st->h_pin + pin_crc;
+  uint32_t* h_nb = reinterpret_cast<uint32_t*>(st->h_pin + pin_crc + align_up(4 * n, 64));
+  *h_nb = 0;
   {
     SlotPipe pipe(st);
     if (!seal && (e = hipMemsetAsync(d_nbad, 0, 4, s)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
     for (size_t k = 0; k < groups.size(); ++k) {
       const HostGroup& x = groups[k];
       uint8_t* ws = st->d_ws + (k % nslots) * slot_bytes;
-      std::vector<pdb_block_handle>& rh = rhs[k];
-      rh.assign(h + x.first, h + x.first + x.count);
-      for (auto& y : rh) y.offset -= x.lo;
+      pdb_block_handle* rh = h_rh + x.first;
+      for (uint64_t i = 0; i < x.count; ++i) rh[i] = pdb_block_handle{h[x.first + i].offset - x.lo, h[x.first + i].size};
       if ((e = pipe.begin_copies(k)) != hipSuccess) return hip_fail(e, "hipStreamWaitEvent");
       if ((e = hipMemcpyAsync(ws, buf + x.lo, x.hi - x.lo, hipMemcpyHostToDevice, cs)) != hipSuccess)
         return hip_fail(e, "hipMemcpyAsync(span)");
-      if ((e = hipMemcpyAsync(ws + off_h, rh.data(), x.count * sizeof(pdb_block_handle), hipMemcpyHostToDevice,
+      if ((e = hipMemcpyAsync(ws + off_h, rh, x.count * sizeof(pdb_block_handle), hipMemcpyHostToDevice,
                               cs)) != hipSuccess)
         return hip_fail(e, "hipMemcpyAsync(handles)");
       if ((e = pipe.end_copies(k)) != hipSuccess) return hip_fail(e, "hipEventRecord(staged)");
@@ -881,29 +905,33 @@ int host_sst(uint8_t* buf, uint64_t buf_len, const pdb_block_handle* h, uint64_t
         uint32_t* d_crc = reinterpret_cast<uint32_t*>(ws + off_ok);
         if ((e = launch_sst_masked(hgeom, dev->d_tables, ws, x.hi - x.lo, d_h, x.count, d_crc, s)) != hipSuccess)
           return hip_fail(e, "launch_sst_masked");
-        if ((e = hipMemcpyAsync(crc.data() + x.first, d_crc, x.count * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
+        if ((e = hipMemcpyAsync(crc + x.first, d_crc, x.count * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
           return hip_fail(e, "hipMemcpyAsync(crcs)");
       } else {
         if ((e = launch_sst(hgeom, dev->d_tables, ws, x.hi - x.lo, d_h, x.count, false, ws + off_ok, d_nbad, s)) !=
             hipSuccess)
           return hip_fail(e, "launch_sst");
-        if (ok && (e = hipMemcpyAsync(ok + x.first, ws + off_ok, x.count, hipMemcpyDeviceToHost, s)) != hipSuccess)
+        if (ok && (e = hipMemcpyAsync(h_ok + x.first, ws + off_ok, x.count, hipMemcpyDeviceToHost, s)) != hipSuccess)
           return hip_fail(e, "hipMemcpyAsync(ok)");
       }
       if ((e = pipe.end_group(k)) != hipSuccess) return hip_fail(e, "hipEventRecord(drained)");
     }
-    if (!seal && (e = hipMemcpyAsync(&nb, d_nbad, 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
+    if (!seal && (e = hipMemcpyAsync(h_nb, d_nbad, 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
       return hip_fail(e, "hipMemcpyAsync(nbad)");
     if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
   }
-  for (uint64_t i = 0; i < crc.size(); ++i) {
-    uint8_t* tr = buf + h[i].offset + h[i].size + 1;
-    tr[0] = static_cast<uint8_t>(crc[i]);
-    tr[1] = static_cast<uint8_t>(crc[i] >> 8);
-    tr[2] = static_cast<uint8_t>(crc[i] >> 16);
-    tr[3] = static_cast<uint8_t>(crc[i] >> 24);
+  if (seal) {
+    for (uint64_t i = 0; i < n; ++i) {
+      uint8_t* tr = buf + h[i].offset + h[i].size + 1;
+      tr[0] = static_cast<uint8_t>(crc[i]);
+      tr[1] = static_cast<uint8_t>(crc[i] >> 8);
+      tr[2] = static_cast<uint8_t>(crc[i] >> 16);
+      tr[3] = static_cast<uint8_t>(crc[i] >> 24);
+    }
+  } else if (ok) {
+    memcpy(ok, h_ok, n);
   }
-  if (nbad_out) *nbad_out = nb;
+  if (nbad_out) *nbad_out = *h_nb;
   return PDB_OK;
 }
 
@@ -915,6 +943,27 @@ using namespace pdb;
 extern "C" {
 
 int pdb_crc32c_abi_version(void) { return PDB_CRC32C_ABI_VERSION; }
+
+int pdb_host_alloc(uint64_t bytes, void** out) {
+  if (!out) return fail(PDB_EINVAL, "null out");
+  *out = nullptr;
+  if (bytes == 0) return PDB_OK;
+  DevState* st;
+  int rc = get_state(&st);
+  if (rc) return rc;
+  hipError_t e = hipHostMalloc(out, bytes, hipHostMallocDefault);
+  if (e != hipSuccess) {
+    *out = nullptr;
+    return fail(PDB_ENOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e));
+  }
+  return PDB_OK;
+}
+
+int pdb_host_free(void* p) {
+  if (!p) return PDB_OK;
+  hipError_t e = hipHostFree(p);
+  return e == hipSuccess ? PDB_OK : hip_fail(e, "hipHostFree");
+}
 
 int pdb_crc32c_init(int device) {
   if (device >= 0) {
