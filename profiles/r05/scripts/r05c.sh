@@ -6,6 +6,7 @@ timeout -k 10 900 python -u -m pytest -x -q --timeout 200 --timeout-method threa
 tail -2 $O/tests.log
 timeout -k 10 400 python tools/ab_span.py 0,183 wal100,wal400,wal1000,wal 6 > $O/ab_queues.log 2>&1 || exit 1
 timeout -k 10 300 python tools/span_clock.py wal1000,wal100 3 > $O/span_clock.log 2>&1 || exit 1
+timeout -k 10 300 python tools/ab_pattern.py 21,23 6 > $O/ab_pattern.log 2>&1 || exit 1
 for w in wal100 wal400 wal1000 wal; do
   timeout -k 10 200 python bench.py --workload $w --no-copy-inclusive --no-cpu-baseline --steps 50 > $O/bench_$w.log 2>&1 || exit 1
 done
