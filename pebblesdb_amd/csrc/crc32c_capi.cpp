@@ -71,10 +71,16 @@ struct DevState {
   // while batches run
   LaunchGeom hgeom{255, 1024};
   HostCtx ctx[kHostCtx];
-  // the device entry points' work-queue words, one set per caller stream (geom_on): launches on one
-  // stream are ordered, so each set is zero again when its next launch starts
+  // the device entry points' record-kernel work-queue words (wq_take): a set belongs to one launch
+  // from the call that takes it until the event recorded after that launch completes, so launches
+  // that may run at once (other streams, other threads) never share one
+  struct WqSet {
+    uint32_t* d = nullptr;
+    hipEvent_t done = nullptr;
+    bool busy = false;
+  };
   std::mutex wq_mu;
-  std::vector<std::pair<hipStream_t, uint32_t*>> wqs;
+  std::vector<WqSet> wqs;
   std::mutex mu;  // the launch-per-call scalar modes' staging below
   // scalar Extend: pinned, device-mapped staging ([256-B result area][bytes]); the kernels read
   // the bytes across PCIe and write the CRC back into it, so a call is memcpy + launch(es) + sync
@@ -227,24 +233,56 @@ hipStream_t pick_stream(DevState* st, void* stream) {
   return static_cast<hipStream_t>(stream);
 }
 
-// The launch geometry for a device entry point on stream `s`: st->geom with that stream's
-// work-queue words (allocated and zeroed on the stream's first call; launches on one stream are
-// ordered, and every record-kernel launch leaves its words zero).
-int geom_on(DevState* st, hipStream_t s, LaunchGeom* g) {
+// The launch geometry of a device entry point on stream `s` (st->geom) and, when the launch will
+// run the record kernel (`records`), a set of its work-queue words that no other launch holds: a
+// free set (its last launch's event has completed; every record-kernel launch leaves its words
+// zero), else a new one.  While `s` is being captured into a graph nothing may be allocated or
+// waited on, and the graph may be replayed later beside any other launch: the captured launch gets
+// no set and runs the kernel's workgroup-local distribution instead (g->wq null).  *slot: the set
+// to pass to wq_done after the launch (-1: none).
+int wq_take(DevState* st, hipStream_t s, bool records, LaunchGeom* g, int* slot) {
   *g = st->geom;
+  *slot = -1;
+  if (!records) return PDB_OK;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  hipError_t e = hipStreamIsCapturing(s, &cap);
+  if (e != hipSuccess) return hip_fail(e, "hipStreamIsCapturing");
+  if (cap != hipStreamCaptureStatusNone) return PDB_OK;
   std::lock_guard<std::mutex> lk(st->wq_mu);
-  for (auto& w : st->wqs)
-    if (w.first == s) {
-      g->wq = w.second;
+  for (size_t i = 0; i < st->wqs.size(); ++i) {
+    DevState::WqSet& w = st->wqs[i];
+    if (w.busy && hipEventQuery(w.done) == hipSuccess) w.busy = false;
+    if (!w.busy) {
+      w.busy = true;
+      g->wq = w.d;
+      *slot = static_cast<int>(i);
       return PDB_OK;
     }
-  uint32_t* wq = nullptr;
-  hipError_t e = hipMalloc(&wq, kWqBytes);
-  if (e != hipSuccess) return hip_fail(e, "hipMalloc(work queues)");
-  if ((e = hipMemset(wq, 0, kWqBytes)) != hipSuccess) return hip_fail(e, "hipMemset(work queues)");
-  st->wqs.emplace_back(s, wq);
-  g->wq = wq;
+  }
+  DevState::WqSet w;
+  if ((e = hipMalloc(&w.d, kWqBytes)) != hipSuccess) return hip_fail(e, "hipMalloc(work queues)");
+  if ((e = hipMemset(w.d, 0, kWqBytes)) != hipSuccess) return hip_fail(e, "hipMemset(work queues)");
+  if ((e = hipEventCreateWithFlags(&w.done, hipEventDisableTiming)) != hipSuccess) return hip_fail(e, "hipEventCreate");
+  w.busy = true;
+  st->wqs.push_back(w);
+  g->wq = w.d;
+  *slot = static_cast<int>(st->wqs.size() - 1);
   return PDB_OK;
+}
+
+// After the launch that took `slot`: the set stays held until the launch completes (launched: an
+// event after it on `s`; not launched: free again at once).
+hipError_t wq_done(DevState* st, int slot, hipStream_t s, bool launched) {
+  if (slot < 0) return hipSuccess;
+  std::lock_guard<std::mutex> lk(st->wq_mu);
+  DevState::WqSet& w = st->wqs[static_cast<size_t>(slot)];
+  if (!launched) {
+    w.busy = false;
+    return hipSuccess;
+  }
+  hipError_t e = hipEventRecord(w.done, s);
+  if (e != hipSuccess) (void)hipStreamSynchronize(s);  // (never left held without a way to free it)
+  return e;
 }
 
 int ensure_ws(HostCtx* c, size_t bytes) {
@@ -1029,9 +1067,13 @@ int pdb_crc32c_batch_device_fixed(const void* d_base, uint64_t stride, uint32_t 
   if (rc) return rc;
   if ((rc = quiesce(st))) return rc;
   LaunchGeom g;
-  if ((rc = geom_on(st, pick_stream(st, stream), &g))) return rc;
+  int slot;
+  hipStream_t s = pick_stream(st, stream);
+  if ((rc = wq_take(st, s, fixed_runs_records(d_base, stride, len, flags), &g, &slot))) return rc;
   hipError_t e = launch_fixed(g, st->d_tables, static_cast<const uint8_t*>(d_base), stride, len,
-                              nblk, flags, init, d_out, pick_stream(st, stream));
+                              nblk, flags, init, d_out, s);
+  const hipError_t e2 = wq_done(st, slot, s, e == hipSuccess);
+  if (e == hipSuccess) e = e2;
   return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_fixed");
 }
 
@@ -1044,9 +1086,13 @@ int pdb_crc32c_batch_device(const void* d_base, const pdb_blk* d_blk, uint64_t n
   if (rc) return rc;
   if ((rc = quiesce(st))) return rc;
   LaunchGeom g;
-  if ((rc = geom_on(st, pick_stream(st, stream), &g))) return rc;
+  int slot;
+  hipStream_t s = pick_stream(st, stream);
+  if ((rc = wq_take(st, s, desc_runs_records(flags), &g, &slot))) return rc;
   hipError_t e = launch_desc(g, st->d_tables, static_cast<const uint8_t*>(d_base), d_blk, nblk,
-                             flags, kModeOut, nullptr, d_out, nullptr, nullptr, pick_stream(st, stream));
+                             flags, kModeOut, nullptr, d_out, nullptr, nullptr, s);
+  const hipError_t e2 = wq_done(st, slot, s, e == hipSuccess);
+  if (e == hipSuccess) e = e2;
   return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_desc");
 }
 
@@ -1060,10 +1106,13 @@ int pdb_crc32c_verify_device(const void* d_base, const pdb_blk* d_blk, uint64_t 
   if (rc) return rc;
   if ((rc = quiesce(st))) return rc;
   LaunchGeom g;
-  if ((rc = geom_on(st, pick_stream(st, stream), &g))) return rc;
+  int slot;
+  hipStream_t s = pick_stream(st, stream);
+  if ((rc = wq_take(st, s, desc_runs_records(flags), &g, &slot))) return rc;
   hipError_t e = launch_desc(g, st->d_tables, static_cast<const uint8_t*>(d_base), d_blk, nblk,
-                             flags, kModeVerify, d_expected, nullptr, d_ok, d_nbad,
-                             pick_stream(st, stream));
+                             flags, kModeVerify, d_expected, nullptr, d_ok, d_nbad, s);
+  const hipError_t e2 = wq_done(st, slot, s, e == hipSuccess);
+  if (e == hipSuccess) e = e2;
   return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_desc(verify)");
 }
 

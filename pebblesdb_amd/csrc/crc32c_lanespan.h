@@ -341,7 +341,7 @@ struct SpanItem {
 // bookkeeping alone); 17 the batch-uniform k only (no per-record lanes for mixed sizes); 18 the
 // item geometry instead of the CRC (first record << 24 | records << 16 | lane << 8 | lanes << 4 |
 // per-record mode); 40 / 41 / 42 = 0 / 1 / 2 with per-wave clock stamps (a Sink with a `stamps`
-// array); 44 the round-2..4 work distribution (each workgroup a fixed range of batches).  The
+// array).  The
 // round-2..4 A/B forms that lost are recorded in DESIGN.md's appendix and were removed in round 5.
 // TP: the table scheme.
 // kDyn: false = static batches wv + k W (diagnostics).
@@ -375,14 +375,26 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
   constexpr bool kClk = MODE >= 40 && MODE <= 42;  // diagnostics: shader-clock stamps (tools/span_clock.py)
   if constexpr (kClk) t_start = wall_clock64();
   if constexpr (kClk) c_start = clock64();
-  // kGQ (the product since round 5): work units from 8 device-wide queues (wq), one per XCD;
-  // MODE 44 = the round-2..4 scheme (each workgroup a fixed range of batches, its waves taking
-  // them from an LDS counter); kDyn false = static batches wv + k W (diagnostics)
-  constexpr bool kGQ = kDyn && MODE != 44;
-  // the workgroup's batch counter (MODE 44): the last 16 B of the last wave's region, which no item
-  // ever uses (spans end by kUsable) and to_lds skips
+  // Work units (first record r0, records cnt <= 64): whole batches, and at the end of each work
+  // range its last batches split in kS units of 64 / kS records (16: one item of the 512 class, two
+  // of the 1023 / 1152 classes; the <= 256 class keeps whole batches, one or two items each), so the
+  // waves run out of work within about an item of each other instead of a batch (~40 us on 1000-B
+  // records).  Each wave holds one ticket in flight (the unit after the one whose
+  // descriptors are in flight), so no atomic's latency waits in front of a load.
+  //   gq (wq != null, the C-ABI's default): 8 device-wide queues, wq[32 x] on its own 128-B line,
+  //     queue x owning batches [nbat x / 8, nbat (x + 1) / 8) with its last ceil(waves / 8) split; a
+  //     workgroup starts on queue blockIdx.x mod 8 (its XCD's under round-robin dispatch) and moves
+  //     on when one runs out, so a slower XCD's batches are finished by the others.  The last wave
+  //     out resets the 9 words (8 queues + the exit count); the C-ABI never hands one set to two
+  //     launches that may run at once.
+  //   otherwise (a launch captured into a graph, diagnostics variant 183): the workgroup's own
+  //     batches [g nbat / G, (g + 1) nbat / G) from an LDS counter, its last kWaves split.
+  //   kDyn false (diagnostics): static batches wv + k W.
+  const bool gq = kDyn && wq != nullptr;  // grid-uniform
+  // the workgroup's batch counter (!gq): the last 16 B of the last wave's region, which no item ever
+  // uses (spans end by kUsable) and to_lds skips
   uint32_t* ctr = reinterpret_cast<uint32_t*>(lds + kSpanStageBase + kSpanWaves * kSpanRegion - 16u);
-  if (kDyn && !kGQ && threadIdx.x == 0) *ctr = kSpanWaves;  // ticket wv is each wave's first
+  if (kDyn && !gq && threadIdx.x == 0) *ctr = kSpanWaves;  // ticket wv is each wave's first
   __syncthreads();
   const typename TP::LT lt = TP::lane(u);
   char* region = lds + kSpanStageBase + wv * kSpanRegion;
@@ -390,34 +402,21 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
   const uint64_t nbat = (nblk + 63u) >> 6;
   const uint32_t nwaves = gridDim.x * kSpanWaves;
   const uint64_t W = nwaves;
-
-  // ---- work units: (first record r0, records cnt <= 64), a batch or part of one ----------------
-  // kGQ: queue x (word wq[32 x], its own 128-B line) owns batches [nbat x / 8, nbat (x + 1) / 8):
-  // its tickets are first whole batches, then -- for its last ceil(waves / 8) batches -- quarter
-  // batches (16 records: one item of the 512 class, two of the 1023 / 1152 classes; the <= 256
-  // class keeps whole batches, one or two items each), so the chip's waves run out of work within
-  // about an item of each other instead of a batch (~40 us on 1000-B records: DESIGN.md §4).  A
-  // workgroup starts on queue blockIdx.x mod 8 (its XCD's, under round-robin dispatch) and moves
-  // on to the next queue when one runs out, so a slower XCD's batches are finished by the others.
-  // Each wave holds one ticket in flight (the unit after the one whose descriptors are in flight),
-  // so the device-scope atomic's latency (~1-3 us) never waits in front of a load.  The last wave
-  // out resets the 9 words (8 queues + the exit count), so every launch starts from zeros; one set
-  // per stream (the C-ABI), so launches that may overlap never share one.
   constexpr uint32_t kS = MAXN <= 256u ? 1u : 4u;  // units per split batch
   uint32_t qx = blockIdx.x & 7u, qn = 0;
-  uint32_t tick = wv;  // lane 0: the ticket in flight (MODE 44: the LDS counter's value)
+  uint32_t tick = wv;  // lane 0: the ticket in flight
   uint64_t sbat = static_cast<uint64_t>(blockIdx.x) * kSpanWaves + wv;  // kDyn false: the next batch
-  const uint64_t g_lo = (kDyn && !kGQ) ? nbat * blockIdx.x / gridDim.x : 0;
-  const uint64_t g_end = (kDyn && !kGQ) ? nbat * (blockIdx.x + 1) / gridDim.x : nbat;
-  const uint64_t qsplit = kS > 1u ? (nwaves + 7u) / 8u : 0u;  // split batches per queue
+  const uint64_t g_lo = nbat * blockIdx.x / gridDim.x, g_end = nbat * (blockIdx.x + 1) / gridDim.x;
+  const uint64_t nsplit = kS == 1u ? 0u : (gq ? (nwaves + 7u) / 8u : kSpanWaves);  // split batches per range
   auto unit_of_batch = [&](uint64_t b, uint64_t& r0, uint32_t& cnt) {
     r0 = b << 6;
     cnt = static_cast<uint32_t>(nblk - r0 < 64u ? nblk - r0 : 64u);
   };
-  // queue x's ticket t: false when the queue is exhausted; cnt 0 = an empty quarter past nblk
+  // ticket t of queue x (gq) or of the workgroup's range: false when exhausted; cnt 0 = an empty
+  // unit past nblk (the last batch's)
   auto decode = [&](uint32_t x, uint32_t t, uint64_t& r0, uint32_t& cnt) -> bool {
-    const uint64_t lo = nbat * x / 8u, n = nbat * (x + 1u) / 8u - lo;
-    const uint64_t R = n < qsplit ? n : qsplit, F = n - R;
+    const uint64_t lo = gq ? nbat * x / 8u : g_lo, n = (gq ? nbat * (x + 1u) / 8u : g_end) - lo;
+    const uint64_t R = n < nsplit ? n : nsplit, F = n - R;
     if (t < F) {
       unit_of_batch(lo + t, r0, cnt);
       return true;
@@ -428,6 +427,11 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
     cnt = r0 >= nblk ? 0u : static_cast<uint32_t>(nblk - r0 < 64u / kS ? nblk - r0 : 64u / kS);
     return true;
   };
+  auto take = [&]() -> uint32_t {  // lane 0: the next ticket of the current range
+    if (u != 0) return 0u;
+    return gq ? __hip_atomic_fetch_add(wq + 32u * qx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+              : __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  };
   // the next unit (false: no work left): decode the ticket in flight, put the following one in flight
   auto acquire = [&](uint64_t& r0, uint32_t& cnt) -> bool {
     if constexpr (!kDyn) {
@@ -435,29 +439,21 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
       unit_of_batch(sbat, r0, cnt);
       sbat += W;
       return true;
-    } else if constexpr (!kGQ) {
-      const uint64_t b = g_lo + __builtin_amdgcn_readfirstlane(tick);
-      if (b >= g_end) return false;
-      if (u == 0) tick = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      unit_of_batch(b, r0, cnt);
-      return true;
     } else {
       for (;;) {
         const uint32_t t = __builtin_amdgcn_readfirstlane(tick);
         if (decode(qx, t, r0, cnt)) {
-          if (u == 0) tick = __hip_atomic_fetch_add(wq + 32u * qx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          tick = take();
           if (cnt) return true;
-          continue;  // an empty quarter (the last batch's): the next ticket
+          continue;  // an empty unit (the last batch's): the next ticket
         }
-        if (++qn == 8u) return false;
+        if (!gq || ++qn == 8u) return false;
         qx = (qx + 1u) & 7u;
-        if (u == 0) tick = __hip_atomic_fetch_add(wq + 32u * qx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        tick = take();
       }
     }
   };
-  if constexpr (kGQ) {
-    if (u == 0) tick = __hip_atomic_fetch_add(wq + 32u * qx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  if (gq) tick = take();
   uint64_t nx_r0 = 0;  // the next unit (its descriptors in flight)
   uint32_t nx_cnt = 0;
   bool nx_ok = acquire(nx_r0, nx_cnt);
@@ -722,7 +718,7 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
     for (uint32_t j = 0; j + 1 < kSpanJ; ++j)
       if (j == 0 || 1024u * j < nw) *reinterpret_cast<u32x4*>(region + 1024u * j + 16u * u) = A[j];
     if (1024u * (kSpanJ - 1u) < nw)
-      if (kGQ || !kDyn || wv + 1u < kSpanWaves || u != 63u)  // MODE 44: the last 16 B of the LDS hold its counter
+      if (gq || !kDyn || wv + 1u < kSpanWaves || u != 63u)  // (!gq: the last 16 B of the LDS hold the counter)
         *reinterpret_cast<u32x4*>(region + 1024u * (kSpanJ - 1u) + 16u * u) = A[kSpanJ - 1u];
   };
   // hash an item staged in the region
@@ -907,9 +903,9 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
       I1 = I3;
     }
   }
-  if constexpr (kGQ) {
+  if (gq) {
     // the last wave out (every wave counts itself once, after its last ticket came back) resets the
-    // queue words for the next launch on this stream
+    // queue words for the set's next launch
     if (u == 0) {
       const uint32_t done = __hip_atomic_fetch_add(wq + 32u * 8u, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (done == nwaves - 1u) {
@@ -941,13 +937,12 @@ inline uint32_t grid_span(const LaunchGeom& g, uint64_t nblk, uint32_t waves) {
 
 // Records of 1..1152 B by class (the class bounds the lanes per record: 2, 4, 8, 8); longer ones,
 // and empty ones, take the whole-wave path.
-// The product form (kGQ) takes its work from the stream's queue words g.wq (9 words on 128-B lines,
-// zero between launches): no queue words, no launch.
+// g.wq: the launch's work-queue words (9 words on 128-B lines, zero, owned by this launch until it
+// completes), or null for the workgroup-local distribution (crc_lanespan_kernel, "work units").
 template <class Src, class Sink, int MODE = 0, class TP = TabsS4, bool kDyn = true>
 hipError_t launch_lanespan(const LaunchGeom& g, const uint32_t* d_tables, const Src& src, uint64_t nblk, uint32_t cls,
                            const Sink& sink, hipStream_t s, bool mixed = false) {
   uint32_t* wq = g.wq;
-  if (kDyn && MODE != 44 && wq == nullptr) return hipErrorInvalidValue;
   if (cls <= 256u) {
     constexpr uint32_t w = SpanStage<256>::kWaves;
     hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 256, MODE, TP, kDyn>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0, s,

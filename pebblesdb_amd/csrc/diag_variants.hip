@@ -292,9 +292,13 @@ hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tab
     case 126:  // the item geometry per record instead of its CRC (MODE 18; tests/test_lanespan.py)
       return launch_lanespan<DescSrc, OutSink, 18>(g, d_tables, src, nblk, record_class(flags), OutSink{out, 0u}, s,
                                                    mixed);
-    case 183:  // exact: the round-2..4 work distribution (each workgroup a fixed range of batches, its
-               // waves taking them from an LDS counter), for A/B against the device-wide queues
-      return launch_lanespan<DescSrc, OutSink, 44>(g, d_tables, src, nblk, record_class(flags), sink, s, mixed);
+    case 183: {  // exact: the workgroup-local distribution (each workgroup a fixed range of batches from
+                 // an LDS counter, its last batches split; what a launch captured into a graph runs),
+                 // for A/B against the device-wide queues
+      LaunchGeom g0 = g;
+      g0.wq = nullptr;
+      return launch_lanespan<DescSrc, OutSink>(g0, d_tables, src, nblk, record_class(flags), sink, s, mixed);
+    }
     case 180:    // the product / loads + staging alone / hash alone, + per-wave [start, end] s_memrealtime
     case 181:    // and [start, end] s_memtime stamps at out + nblk rounded up to 8 B (the caller sizes
     case 182: {  // `out` for 4 x 8 B per wave; tools/span_clock.py)

@@ -191,23 +191,69 @@ def test_device_entry_points_capture_into_hip_graph(crc, oracle_lib):
     blk = crc.blocks_to_device(crc.make_blocks(np.arange(nblk) * 4096 + 1, np.full(nblk, 4095)))
     out1 = torch.empty(nblk, dtype=torch.int32, device="cuda")
     out2 = torch.empty(nblk, dtype=torch.int32, device="cuda")
+    # the record kernel too (size hint 512: WAL-sized records); captured it runs its workgroup-local
+    # distribution, since a graph may be replayed beside any other launch
+    roffs, rlens = np.arange(20000) * 431 + 6, np.full(20000, 425)
+    rblk = crc.blocks_to_device(crc.make_blocks(roffs, rlens))
+    out3 = torch.empty(len(roffs), dtype=torch.int32, device="cuda")
     crc.batch_fixed(d, 4096, 4096, nblk, out=out1)  # warm (per-device state exists before capture)
     crc.batch(d, blk, out=out2)
+    crc.batch(d, rblk, out=out3, size_hint="512")
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
         crc.batch_fixed(d, 4096, 4096, nblk, out=out1)
         crc.batch(d, blk, out=out2)
+        crc.batch(d, rblk, out=out3, size_hint="512")
     for seed in (78, 79):
         diag.fill_splitmix(d, seed)
         out1.zero_()
         out2.zero_()
+        out3.zero_()
         g.replay()
+        crc.batch(d, rblk, out=out3, size_hint="512")  # a direct launch after the replay: both exact
         torch.cuda.synchronize()
         host = d.cpu().numpy()
         e1 = oracle_lib.batch(host, crc.make_blocks(np.arange(nblk) * 4096, np.full(nblk, 4096)), nthreads=8)
         e2 = oracle_lib.batch(host, crc.make_blocks(np.arange(nblk) * 4096 + 1, np.full(nblk, 4095)), nthreads=8)
-        assert (_u32(out1) == e1).all() and (_u32(out2) == e2).all()
+        e3 = oracle_lib.batch(host, crc.make_blocks(roffs, rlens), nthreads=8)
+        assert (_u32(out1) == e1).all() and (_u32(out2) == e2).all() and (_u32(out3) == e3).all()
+
+
+def test_record_batches_on_concurrent_streams(crc, oracle_lib):
+    """Record-kernel launches (the device-wide work queues) from several streams at once, each
+    launch many times back to back: every launch holds its own queue words until it completes, so
+    concurrent launches never take each other's work (a shared set would skip or repeat units)."""
+    import threading
+
+    rng = np.random.Generator(np.random.PCG64(606))
+    lens = rng.integers(300, 1000, size=60000)
+    offs = np.concatenate([[6], 6 + np.cumsum(lens + 7)[:-1]])
+    d = torch.empty(int(offs[-1] + lens[-1]) + 64, dtype=torch.uint8, device="cuda")
+    diag.fill_splitmix(d, 607)
+    blk = crc.make_blocks(offs, lens)
+    d_blk = crc.blocks_to_device(blk)
+    exp = oracle_lib.batch(d.cpu().numpy(), blk, nthreads=8)
+    torch.cuda.synchronize()
+    errors = []
+
+    def run(k):
+        st = torch.cuda.Stream()
+        outs = [torch.empty(len(lens), dtype=torch.int32, device="cuda") for _ in range(6)]
+        with torch.cuda.stream(st):
+            for o in outs:
+                crc.batch(d, d_blk, out=o, size_hint="1023", stream=st)
+        st.synchronize()
+        for o in outs:
+            if not (_u32(o) == exp).all():
+                errors.append(k)
+
+    th = [threading.Thread(target=run, args=(k,)) for k in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors
 
 
 @pytest.mark.parametrize("n", [0, 1, 65535, 65536, 65537, 3 * 65536 + 5, (64 << 20) + 13, (1 << 30) + 7])
