@@ -77,7 +77,8 @@ struct DevState {
   struct WqSet {
     uint32_t* d = nullptr;
     hipEvent_t done = nullptr;
-    bool busy = false;
+    bool busy = false;      // held by a launch
+    bool recorded = false;  // `done` follows that launch (until then it still marks an older one)
   };
   std::mutex wq_mu;
   std::vector<WqSet> wqs;
@@ -251,9 +252,10 @@ int wq_take(DevState* st, hipStream_t s, bool records, LaunchGeom* g, int* slot)
   std::lock_guard<std::mutex> lk(st->wq_mu);
   for (size_t i = 0; i < st->wqs.size(); ++i) {
     DevState::WqSet& w = st->wqs[i];
-    if (w.busy && hipEventQuery(w.done) == hipSuccess) w.busy = false;
+    if (w.busy && w.recorded && hipEventQuery(w.done) == hipSuccess) w.busy = false;
     if (!w.busy) {
       w.busy = true;
+      w.recorded = false;
       g->wq = w.d;
       *slot = static_cast<int>(i);
       return PDB_OK;
@@ -281,7 +283,12 @@ hipError_t wq_done(DevState* st, int slot, hipStream_t s, bool launched) {
     return hipSuccess;
   }
   hipError_t e = hipEventRecord(w.done, s);
-  if (e != hipSuccess) (void)hipStreamSynchronize(s);  // (never left held without a way to free it)
+  if (e != hipSuccess) {
+    (void)hipStreamSynchronize(s);  // (never left held without a way to free it)
+    w.busy = false;
+    return e;
+  }
+  w.recorded = true;
   return e;
 }
 
