@@ -332,7 +332,7 @@ struct SpanItem {
   uint32_t r;                   // per lane: record slot in the batch
   uint32_t cw;                  // per lane: part c; kVar classes pack (one VGPR per item in flight)
                                 // c (bits 0-3) and the record's parts after it, kl - 1 - c (4-7),
-                                // + the item's records (8-14) and first record (16-21) in MODE 18
+                                // + the item's records (8-14) and first record in its batch of 64 (16-21) in MODE 18
   uint32_t p_loc, e_loc, pre;  // per lane: local start (kNoRec: no record), local end, sink word
 };
 
@@ -651,7 +651,7 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
       const uint32_t kr = static_cast<uint32_t>(__shfl(static_cast<int>(bkr), static_cast<int>(rl), 64));
       it.pre = __shfl(bpre, rl, 64);
       const uint32_t c = act ? u - s0 : 0u;
-      it.cw = c | ((act ? kr - 1u - c : 0u) << 4) | (MODE == 18 ? (m << 8) | (g0 << 16) : 0u);
+      it.cw = c | ((act ? kr - 1u - c : 0u) << 4) | (MODE == 18 ? (m << 8) | ((g0 + static_cast<uint32_t>(b_r0 & 63u)) << 16) : 0u);
       it.r = rl;
       it.p_loc = act ? pr - lo32 : kNoRec;
       it.e_loc = act ? pr + nr - lo32 : 0u;
@@ -664,7 +664,7 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
     if (bg.k == 1u && g0 == 0u) {  // the common case: lane u hashes record u
       const bool act = u < m;
       it.r = u;
-      it.cw = (kVar && MODE == 18) ? (m << 8) | (g0 << 16) : 0u;
+      it.cw = (kVar && MODE == 18) ? (m << 8) | ((g0 + static_cast<uint32_t>(b_r0 & 63u)) << 16) : 0u;
       it.pre = bpre;
       it.p_loc = act ? plo - lo32 : kNoRec;
       it.e_loc = act ? plo + bn - lo32 : 0u;
@@ -683,7 +683,7 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
       nr = __shfl(bn, rl, 64);
       it.pre = __shfl(bpre, rl, 64);
       it.r = rl;
-      it.cw = kVar ? c | ((bg.k - 1u - c) << 4) | (MODE == 18 ? (m << 8) | (g0 << 16) : 0u) : c;
+      it.cw = kVar ? c | ((bg.k - 1u - c) << 4) | (MODE == 18 ? (m << 8) | ((g0 + static_cast<uint32_t>(b_r0 & 63u)) << 16) : 0u) : c;
       it.p_loc = act ? pr - lo32 : kNoRec;
       it.e_loc = act ? pr + nr - lo32 : 0u;
     }
