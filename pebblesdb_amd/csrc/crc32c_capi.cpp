@@ -51,8 +51,7 @@ struct HostCtx {
   size_t h_pin_cap = 0;
 };
 constexpr int kHostCtx = 4;
-// crc_lanespan_kernel's work queues: 8 queue words + the exit count, each on its own 128-B line
-constexpr size_t kWqBytes = 9 * 128;
+
 
 // One scalar-service request slot (crc32c_server.hip): its request sequence number, guarded by mu
 // (a slot is shared only when more threads than slots call at once).

@@ -21,10 +21,15 @@ enum DescMode : int {
   kModeVerify = 1,  // ok[i] = (crc == expected[i])
 };
 
+// crc_lanespan_kernel's device-wide work queues: PDB_SPAN_QUEUES queue words + the exit count, each
+// on its own 128-B line
+#define PDB_SPAN_QUEUES 16u
+constexpr size_t kWqBytes = (PDB_SPAN_QUEUES + 1u) * 128u;
+
 struct LaunchGeom {
   uint32_t grid;   // workgroups (one per CU: the LDS image is ~156 KiB)
   uint32_t block;  // threads per workgroup
-  // work-queue words for crc_lanespan_kernel (9 words on 128-B lines, zero, held by this launch
+  // work-queue words for crc_lanespan_kernel (kWqBytes, zero, held by this launch
   // alone until it completes: the C-ABI's wq_take / a host context's own set), or null for the
   // kernel's workgroup-local distribution
   uint32_t* wq = nullptr;

@@ -381,12 +381,15 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
   // waves run out of work within about an item of each other instead of a batch (~40 us on 1000-B
   // records).  Each wave holds one ticket in flight (the unit after the one whose
   // descriptors are in flight), so no atomic's latency waits in front of a load.
-  //   gq (wq != null, the C-ABI's default): 8 device-wide queues, wq[32 x] on its own 128-B line,
-  //     queue x owning batches [nbat x / 8, nbat (x + 1) / 8) with its last ceil(waves / 8) split; a
-  //     workgroup starts on queue blockIdx.x mod 8 (its XCD's under round-robin dispatch) and moves
-  //     on when one runs out, so a slower XCD's batches are finished by the others.  The last wave
-  //     out resets the 9 words (8 queues + the exit count); the C-ABI never hands one set to two
-  //     launches that may run at once.
+  //   gq (wq != null, the C-ABI's default): kQ = 16 device-wide queues, wq[32 x] on its own 128-B
+  //     line, queue x owning the batches b = kQ j + x (every CU keeps streaming the same region of
+  //     the image as all the others, as the static ranges do: per-queue contiguous regions measured
+  //     30 % slower even for the loads alone) with its last ceil(waves / kQ) split; a workgroup
+  //     starts on queue blockIdx.x mod kQ and moves on when one runs out, so a slower XCD's batches
+  //     are finished by the others.  16 queues keep each word below the ~88 dequeues / us one
+  //     address sustains (MI355X_MICROARCH.md) on 131-B records (~600 batches / us chip-wide).  The
+  //     last wave out resets the kQ + 1 words (queues + the exit count); the C-ABI never hands one set
+  //     to two launches that may run at once.
   //   otherwise (a launch captured into a graph, diagnostics variant 183): the workgroup's own
   //     batches [g nbat / G, (g + 1) nbat / G) from an LDS counter, its last kWaves split.
   //   kDyn false (diagnostics): static batches wv + k W.
@@ -403,27 +406,30 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
   const uint32_t nwaves = gridDim.x * kSpanWaves;
   const uint64_t W = nwaves;
   constexpr uint32_t kS = MAXN <= 256u ? 1u : 4u;  // units per split batch
-  uint32_t qx = blockIdx.x & 7u, qn = 0;
+  constexpr uint32_t kQ = PDB_SPAN_QUEUES;
+  uint32_t qx = blockIdx.x % kQ, qn = 0;
   uint32_t tick = wv;  // lane 0: the ticket in flight
   uint64_t sbat = static_cast<uint64_t>(blockIdx.x) * kSpanWaves + wv;  // kDyn false: the next batch
   const uint64_t g_lo = nbat * blockIdx.x / gridDim.x, g_end = nbat * (blockIdx.x + 1) / gridDim.x;
-  const uint64_t nsplit = kS == 1u ? 0u : (gq ? (nwaves + 7u) / 8u : kSpanWaves);  // split batches per range
+  const uint64_t nsplit = kS == 1u ? 0u : (gq ? (nwaves + kQ - 1u) / kQ : kSpanWaves);  // split batches per range
   auto unit_of_batch = [&](uint64_t b, uint64_t& r0, uint32_t& cnt) {
     r0 = b << 6;
     cnt = static_cast<uint32_t>(nblk - r0 < 64u ? nblk - r0 : 64u);
   };
   // ticket t of queue x (gq) or of the workgroup's range: false when exhausted; cnt 0 = an empty
   // unit past nblk (the last batch's)
+  // (range j-th batch: g_lo + j, or kQ j + x for queue x)
   auto decode = [&](uint32_t x, uint32_t t, uint64_t& r0, uint32_t& cnt) -> bool {
-    const uint64_t lo = gq ? nbat * x / 8u : g_lo, n = (gq ? nbat * (x + 1u) / 8u : g_end) - lo;
+    const uint64_t n = gq ? (nbat > x ? (nbat - x + kQ - 1u) / kQ : 0u) : g_end - g_lo;
+    auto batch = [&](uint64_t j) -> uint64_t { return gq ? kQ * j + x : g_lo + j; };
     const uint64_t R = n < nsplit ? n : nsplit, F = n - R;
     if (t < F) {
-      unit_of_batch(lo + t, r0, cnt);
+      unit_of_batch(batch(t), r0, cnt);
       return true;
     }
     const uint64_t q = t - F;
     if (q >= kS * R) return false;
-    r0 = ((lo + F + q / kS) << 6) + (q % kS) * (64u / kS);
+    r0 = (batch(F + q / kS) << 6) + (q % kS) * (64u / kS);
     cnt = r0 >= nblk ? 0u : static_cast<uint32_t>(nblk - r0 < 64u / kS ? nblk - r0 : 64u / kS);
     return true;
   };
@@ -447,8 +453,8 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
           if (cnt) return true;
           continue;  // an empty unit (the last batch's): the next ticket
         }
-        if (!gq || ++qn == 8u) return false;
-        qx = (qx + 1u) & 7u;
+        if (!gq || ++qn == kQ) return false;
+        qx = (qx + 1u) % kQ;
         tick = take();
       }
     }
@@ -907,10 +913,10 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
     // the last wave out (every wave counts itself once, after its last ticket came back) resets the
     // queue words for the set's next launch
     if (u == 0) {
-      const uint32_t done = __hip_atomic_fetch_add(wq + 32u * 8u, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t done = __hip_atomic_fetch_add(wq + 32u * kQ, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (done == nwaves - 1u) {
 #pragma unroll
-        for (uint32_t x = 0; x <= 8u; ++x) __hip_atomic_store(wq + 32u * x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (uint32_t x = 0; x <= kQ; ++x) __hip_atomic_store(wq + 32u * x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   }
@@ -937,7 +943,7 @@ inline uint32_t grid_span(const LaunchGeom& g, uint64_t nblk, uint32_t waves) {
 
 // Records of 1..1152 B by class (the class bounds the lanes per record: 2, 4, 8, 8); longer ones,
 // and empty ones, take the whole-wave path.
-// g.wq: the launch's work-queue words (9 words on 128-B lines, zero, owned by this launch until it
+// g.wq: the launch's work-queue words (PDB_SPAN_QUEUES + 1 words on 128-B lines, zero, owned by this launch until it
 // completes), or null for the workgroup-local distribution (crc_lanespan_kernel, "work units").
 template <class Src, class Sink, int MODE = 0, class TP = TabsS4, bool kDyn = true>
 hipError_t launch_lanespan(const LaunchGeom& g, const uint32_t* d_tables, const Src& src, uint64_t nblk, uint32_t cls,

@@ -54,9 +54,9 @@ int diag_state(const DiagDev** out) {
     // the record kernel's work-queue words (one set per device: the diagnostics tools launch on one
     // stream; crc32c_capi.cpp keeps one per stream)
     uint32_t* wq = nullptr;
-    if ((e = hipMalloc(&wq, 9 * 128)) != hipSuccess)
+    if ((e = hipMalloc(&wq, kWqBytes)) != hipSuccess)
       return dfail(PDB_ENOMEM, std::string("hipMalloc(work queues): ") + hipGetErrorString(e));
-    if ((e = hipMemset(wq, 0, 9 * 128)) != hipSuccess)
+    if ((e = hipMemset(wq, 0, kWqBytes)) != hipSuccess)
       return dfail(PDB_EHIP, std::string("hipMemset(work queues): ") + hipGetErrorString(e));
     d.geom.wq = wq;
     d.d_tables = p;

@@ -87,7 +87,8 @@ __global__ __launch_bounds__(kThreads) void read_pattern4k_kernel(const uint8_t*
 }
 
 // Variant 23: the same loads with the WORK DISTRIBUTION of the record kernel's queues (crc32c_lanespan.h,
-// kGQ) at workgroup level: chunks of 64 blocks from 8 per-XCD queue words (wq[32 x]); in a chunk,
+// gq) at workgroup level: chunks of 64 blocks from PDB_SPAN_QUEUES queue words (wq[32 x]; queue x
+// owns chunks kQ j + x, so every workgroup streams the same region as the others); in a chunk,
 // wave w loads blocks 16 r + w (r = 0..3) in lock-step, so each row of the workgroup reads 64 KiB
 // contiguous; the next chunk's ticket is taken one chunk ahead by lane 0 of wave 0 and published
 // through LDS at the barrier; a workgroup moves to the next queue when its own runs out, and the
@@ -99,18 +100,18 @@ __global__ __launch_bounds__(kThreads) void read_pattern4k_dyn_kernel(const uint
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t nchunk = (nblk + 63u) / 64u;
-  uint32_t qx = blockIdx.x & 7u, qn = 0;  // (wave 0's copy is the one that counts)
-  auto qlo = [&](uint32_t x) { return nchunk * x / 8u; };
+  constexpr uint32_t kQ = PDB_SPAN_QUEUES;
+  uint32_t qx = blockIdx.x % kQ, qn = 0;  // (wave 0's copy is the one that counts)
   auto issue = [&]() -> uint32_t {  // lane 0 of wave 0: a ticket of queue qx
     return lane == 0 ? __hip_atomic_fetch_add(wq + 32u * qx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
   };
   // the chunk of ticket tk (in flight), else the next queues' tickets (every queue exhausted: ~0)
   auto resolve = [&](uint32_t tk) -> uint64_t {
     for (;;) {
-      const uint64_t c = qlo(qx) + __builtin_amdgcn_readfirstlane(tk);
-      if (c < qlo(qx + 1u)) return c;
-      if (++qn == 8u) return ~0ull;
-      qx = (qx + 1u) & 7u;
+      const uint64_t c = static_cast<uint64_t>(kQ) * __builtin_amdgcn_readfirstlane(tk) + qx;
+      if (c < nchunk) return c;
+      if (++qn == kQ) return ~0ull;
+      qx = (qx + 1u) % kQ;
       tk = issue();
     }
   };
@@ -144,9 +145,9 @@ __global__ __launch_bounds__(kThreads) void read_pattern4k_dyn_kernel(const uint
   for (int k = 32; k; k >>= 1) acc ^= __shfl_xor(acc, k, 64);
   if (lane == 0) atomicXor(out, acc);
   if (threadIdx.x == 0) {  // the last workgroup out resets the queue words
-    const uint32_t done = __hip_atomic_fetch_add(wq + 32u * 8u, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t done = __hip_atomic_fetch_add(wq + 32u * kQ, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (done == gridDim.x - 1u)
-      for (uint32_t q = 0; q <= 8u; ++q) __hip_atomic_store(wq + 32u * q, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (uint32_t q = 0; q <= kQ; ++q) __hip_atomic_store(wq + 32u * q, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
