@@ -375,29 +375,29 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
   constexpr bool kClk = MODE >= 40 && MODE <= 42;  // diagnostics: shader-clock stamps (tools/span_clock.py)
   if constexpr (kClk) t_start = wall_clock64();
   if constexpr (kClk) c_start = clock64();
-  // Work units (first record r0, records cnt <= 64): whole batches, and at the end of each work
-  // range its last batches split in kS units of 64 / kS records (16: one item of the 512 class, two
-  // of the 1023 / 1152 classes; the <= 256 class keeps whole batches, one or two items each), so the
-  // waves run out of work within about an item of each other instead of a batch (~40 us on 1000-B
-  // records).  Each wave holds one ticket in flight (the unit after the one whose
-  // descriptors are in flight), so no atomic's latency waits in front of a load.
-  //   gq (wq != null, the C-ABI's default): kQ = 16 device-wide queues, wq[32 x] on its own 128-B
-  //     line, queue x owning the batches b = kQ j + x (every CU keeps streaming the same region of
-  //     the image as all the others, as the static ranges do: per-queue contiguous regions measured
-  //     30 % slower even for the loads alone) with its last ceil(waves / kQ) split; a workgroup
-  //     starts on queue blockIdx.x mod kQ and moves on when one runs out, so a slower XCD's batches
-  //     are finished by the others.  16 queues keep each word below the ~88 dequeues / us one
-  //     address sustains (MI355X_MICROARCH.md) on 131-B records (~600 batches / us chip-wide).  The
-  //     last wave out resets the kQ + 1 words (queues + the exit count); the C-ABI never hands one set
-  //     to two launches that may run at once.
-  //   otherwise (a launch captured into a graph, diagnostics variant 183): the workgroup's own
-  //     batches [g nbat / G, (g + 1) nbat / G) from an LDS counter, its last kWaves split.
+  // Work units (first record r0, records cnt <= 64): whole batches, and near the end split batches,
+  // kS units of 64 / kS records (16: one item of the 512 class, two of the 1023 / 1152 classes; the
+  // <= 256 class keeps whole batches, one or two items each), so the waves run out of work within
+  // about an item of each other instead of a batch (~40 us on 1000-B records).  Each
+  // wave holds one ticket in flight (the unit after the one whose descriptors are in flight), so no
+  // atomic's latency waits in front of a load.
+  //   Phase 1: the workgroup's own contiguous range of the first M batches, from an LDS counter
+  //     (every CU streams the same region of the image as the others; device-wide queues for ALL the
+  //     work measured 1-16 % slower, the atomics' traffic and order costing more than they balance:
+  //     profiles/r05/).  Without a pool (wq null: a launch captured into a graph, diagnostics 183)
+  //     M = nbat and the range's last kWaves batches are split.
+  //   Phase 2 (wq != null, the C-ABI's default): the pool, the last nbat - M batches (kPool of them per
+  //     kQ-wave slice of the grid, ~2 per wave), all split, from kQ = 16 device-wide queues -- queue x
+  //     (wq[32 x], its own 128-B line) owns pool batches M + kQ j + x -- started at queue
+  //     blockIdx.x mod kQ and moved on from when one runs out.  Whichever CUs finish their range
+  //     first (a faster XCD) take more of the pool.  The last wave out resets the kQ + 1 words
+  //     (queues + the exit count); the C-ABI never hands one set to two launches that may run at once.
   //   kDyn false (diagnostics): static batches wv + k W.
   const bool gq = kDyn && wq != nullptr;  // grid-uniform
-  // the workgroup's batch counter (!gq): the last 16 B of the last wave's region, which no item ever
-  // uses (spans end by kUsable) and to_lds skips
+  // the workgroup's batch counter (phase 1): the last 16 B of the last wave's region, which no item
+  // ever uses (spans end by kUsable) and to_lds skips
   uint32_t* ctr = reinterpret_cast<uint32_t*>(lds + kSpanStageBase + kSpanWaves * kSpanRegion - 16u);
-  if (kDyn && !gq && threadIdx.x == 0) *ctr = kSpanWaves;  // ticket wv is each wave's first
+  if (kDyn && threadIdx.x == 0) *ctr = kSpanWaves;  // ticket wv is each wave's first
   __syncthreads();
   const typename TP::LT lt = TP::lane(u);
   char* region = lds + kSpanStageBase + wv * kSpanRegion;
@@ -407,22 +407,26 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
   const uint64_t W = nwaves;
   constexpr uint32_t kS = MAXN <= 256u ? 1u : 4u;  // units per split batch
   constexpr uint32_t kQ = PDB_SPAN_QUEUES;
+  // the pool: ~kPool batches per wave of the grid (at most half the work; MODE 45 / 46: 1 / 4, A/B)
+  constexpr uint64_t kPool = MODE == 45 ? 1u : (MODE == 46 ? 4u : 2u);
+  const uint64_t npool = gq ? (kPool * nwaves < nbat / 2u ? kPool * nwaves : nbat / 2u) : 0u;
+  const uint64_t M = nbat - npool;
   uint32_t qx = blockIdx.x % kQ, qn = 0;
+  bool phase2 = false;
   uint32_t tick = wv;  // lane 0: the ticket in flight
   uint64_t sbat = static_cast<uint64_t>(blockIdx.x) * kSpanWaves + wv;  // kDyn false: the next batch
-  const uint64_t g_lo = nbat * blockIdx.x / gridDim.x, g_end = nbat * (blockIdx.x + 1) / gridDim.x;
-  const uint64_t nsplit = kS == 1u ? 0u : (gq ? (nwaves + kQ - 1u) / kQ : kSpanWaves);  // split batches per range
+  const uint64_t g_lo = M * blockIdx.x / gridDim.x, g_end = M * (blockIdx.x + 1) / gridDim.x;
   auto unit_of_batch = [&](uint64_t b, uint64_t& r0, uint32_t& cnt) {
     r0 = b << 6;
     cnt = static_cast<uint32_t>(nblk - r0 < 64u ? nblk - r0 : 64u);
   };
-  // ticket t of queue x (gq) or of the workgroup's range: false when exhausted; cnt 0 = an empty
-  // unit past nblk (the last batch's)
-  // (range j-th batch: g_lo + j, or kQ j + x for queue x)
-  auto decode = [&](uint32_t x, uint32_t t, uint64_t& r0, uint32_t& cnt) -> bool {
-    const uint64_t n = gq ? (nbat > x ? (nbat - x + kQ - 1u) / kQ : 0u) : g_end - g_lo;
-    auto batch = [&](uint64_t j) -> uint64_t { return gq ? kQ * j + x : g_lo + j; };
-    const uint64_t R = n < nsplit ? n : nsplit, F = n - R;
+  // ticket t of the workgroup's range (phase 1) or of pool queue x (phase 2): false when exhausted;
+  // cnt 0 = an empty unit past nblk (the last batch's)
+  auto decode = [&](uint32_t t, uint64_t& r0, uint32_t& cnt) -> bool {
+    const uint64_t n = phase2 ? (npool > qx ? (npool - qx + kQ - 1u) / kQ : 0u) : g_end - g_lo;
+    auto batch = [&](uint64_t j) -> uint64_t { return phase2 ? M + kQ * j + qx : g_lo + j; };
+    const uint64_t R = kS == 1u ? 0u : (phase2 ? n : (gq ? 0u : (n < kSpanWaves ? n : kSpanWaves)));
+    const uint64_t F = n - R;
     if (t < F) {
       unit_of_batch(batch(t), r0, cnt);
       return true;
@@ -435,8 +439,8 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
   };
   auto take = [&]() -> uint32_t {  // lane 0: the next ticket of the current range
     if (u != 0) return 0u;
-    return gq ? __hip_atomic_fetch_add(wq + 32u * qx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-              : __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return phase2 ? __hip_atomic_fetch_add(wq + 32u * qx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                  : __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   };
   // the next unit (false: no work left): decode the ticket in flight, put the following one in flight
   auto acquire = [&](uint64_t& r0, uint32_t& cnt) -> bool {
@@ -448,18 +452,21 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
     } else {
       for (;;) {
         const uint32_t t = __builtin_amdgcn_readfirstlane(tick);
-        if (decode(qx, t, r0, cnt)) {
+        if (decode(t, r0, cnt)) {
           tick = take();
           if (cnt) return true;
           continue;  // an empty unit (the last batch's): the next ticket
         }
-        if (!gq || ++qn == kQ) return false;
-        qx = (qx + 1u) % kQ;
+        if (!gq) return false;
+        if (phase2) {
+          if (++qn == kQ) return false;
+          qx = (qx + 1u) % kQ;
+        }
+        phase2 = true;
         tick = take();
       }
     }
   };
-  if (gq) tick = take();
   uint64_t nx_r0 = 0;  // the next unit (its descriptors in flight)
   uint32_t nx_cnt = 0;
   bool nx_ok = acquire(nx_r0, nx_cnt);
@@ -724,7 +731,7 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
     for (uint32_t j = 0; j + 1 < kSpanJ; ++j)
       if (j == 0 || 1024u * j < nw) *reinterpret_cast<u32x4*>(region + 1024u * j + 16u * u) = A[j];
     if (1024u * (kSpanJ - 1u) < nw)
-      if (gq || !kDyn || wv + 1u < kSpanWaves || u != 63u)  // (!gq: the last 16 B of the LDS hold the counter)
+      if (!kDyn || wv + 1u < kSpanWaves || u != 63u)  // the last 16 B of the LDS hold the counter
         *reinterpret_cast<u32x4*>(region + 1024u * (kSpanJ - 1u) + 16u * u) = A[kSpanJ - 1u];
   };
   // hash an item staged in the region

@@ -300,6 +300,10 @@ hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tab
       g0.wq = nullptr;
       return launch_lanespan<DescSrc, OutSink>(g0, d_tables, src, nblk, record_class(flags), sink, s, mixed);
     }
+    case 184:  // exact: the tail pool at 1 / 4 batches per wave of the grid (the product: 2)
+      return launch_lanespan<DescSrc, OutSink, 45>(g, d_tables, src, nblk, record_class(flags), sink, s, mixed);
+    case 185:
+      return launch_lanespan<DescSrc, OutSink, 46>(g, d_tables, src, nblk, record_class(flags), sink, s, mixed);
     case 180:    // the product / loads + staging alone / hash alone, + per-wave [start, end] s_memrealtime
     case 181:    // and [start, end] s_memtime stamps at out + nblk rounded up to 8 B (the caller sizes
     case 182: {  // `out` for 4 x 8 B per wave; tools/span_clock.py)
