@@ -212,7 +212,9 @@ int get_state(DevState** out) {
     e = hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking);
     if (e != hipSuccess) return hip_fail(e, "hipStreamCreate");
     if ((e = hipMalloc(&c.wq, kWqBytes)) != hipSuccess) return hip_fail(e, "hipMalloc(work queues)");
-    if ((e = hipMemset(c.wq, 0, kWqBytes)) != hipSuccess) return hip_fail(e, "hipMemset(work queues)");
+    // zeroed on the context's own stream, which its launches follow
+    if ((e = hipMemsetAsync(c.wq, 0, kWqBytes, c.stream)) != hipSuccess) return hip_fail(e, "hipMemsetAsync(work queues)");
+    if ((e = hipStreamSynchronize(c.stream)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
     e = hipStreamCreateWithFlags(&c.copy_stream, hipStreamNonBlocking);
     if (e != hipSuccess) return hip_fail(e, "hipStreamCreate(copy)");
     for (int k = 0; k < 2; ++k) {
@@ -262,7 +264,12 @@ int wq_take(DevState* st, hipStream_t s, bool records, LaunchGeom* g, int* slot)
   }
   DevState::WqSet w;
   if ((e = hipMalloc(&w.d, kWqBytes)) != hipSuccess) return hip_fail(e, "hipMalloc(work queues)");
-  if ((e = hipMemset(w.d, 0, kWqBytes)) != hipSuccess) return hip_fail(e, "hipMemset(work queues)");
+  // zeroed in order on the launch's own stream: a plain hipMemset runs on the null stream, which a
+  // non-blocking caller stream does not wait for (recycled memory is not zero)
+  if ((e = hipMemsetAsync(w.d, 0, kWqBytes, s)) != hipSuccess) {
+    (void)hipFree(w.d);
+    return hip_fail(e, "hipMemsetAsync(work queues)");
+  }
   if ((e = hipEventCreateWithFlags(&w.done, hipEventDisableTiming)) != hipSuccess) return hip_fail(e, "hipEventCreate");
   w.busy = true;
   st->wqs.push_back(w);

@@ -58,6 +58,9 @@ int diag_state(const DiagDev** out) {
       return dfail(PDB_ENOMEM, std::string("hipMalloc(work queues): ") + hipGetErrorString(e));
     if ((e = hipMemset(wq, 0, kWqBytes)) != hipSuccess)
       return dfail(PDB_EHIP, std::string("hipMemset(work queues): ") + hipGetErrorString(e));
+    // (the null-stream memset must be done before a launch on a non-blocking stream reads the words)
+    if ((e = hipDeviceSynchronize()) != hipSuccess)
+      return dfail(PDB_EHIP, std::string("hipDeviceSynchronize: ") + hipGetErrorString(e));
     d.geom.wq = wq;
     d.d_tables = p;
   }
