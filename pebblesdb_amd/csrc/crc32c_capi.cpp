@@ -44,14 +44,12 @@ struct HostCtx {
   hipEvent_t drained[2] = {};         // group in workspace slot k hashed and its results copied out
   uint8_t* d_ws = nullptr;
   size_t ws_cap = 0;
-  uint32_t* wq = nullptr;  // the record kernel's work-queue words for `stream` (kWqBytes, zeroed)
   // page-locked host scratch for a call's small per-block arrays (rebased handles in, trailer words
   // / ok bytes out): DMA'd directly instead of through the runtime's pageable bounce buffers
   uint8_t* h_pin = nullptr;
   size_t h_pin_cap = 0;
 };
 constexpr int kHostCtx = 4;
-
 
 // One scalar-service request slot (crc32c_server.hip): its request sequence number, guarded by mu
 // (a slot is shared only when more threads than slots call at once).
@@ -70,17 +68,6 @@ struct DevState {
   // while batches run
   LaunchGeom hgeom{255, 1024};
   HostCtx ctx[kHostCtx];
-  // the device entry points' record-kernel work-queue words (wq_take): a set belongs to one launch
-  // from the call that takes it until the event recorded after that launch completes, so launches
-  // that may run at once (other streams, other threads) never share one
-  struct WqSet {
-    uint32_t* d = nullptr;
-    hipEvent_t done = nullptr;
-    bool busy = false;      // held by a launch
-    bool recorded = false;  // `done` follows that launch (until then it still marks an older one)
-  };
-  std::mutex wq_mu;
-  std::vector<WqSet> wqs;
   std::mutex mu;  // the launch-per-call scalar modes' staging below
   // scalar Extend: pinned, device-mapped staging ([256-B result area][bytes]); the kernels read
   // the bytes across PCIe and write the CRC back into it, so a call is memcpy + launch(es) + sync
@@ -211,10 +198,6 @@ int get_state(DevState** out) {
   for (HostCtx& c : s->ctx) {
     e = hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking);
     if (e != hipSuccess) return hip_fail(e, "hipStreamCreate");
-    if ((e = hipMalloc(&c.wq, kWqBytes)) != hipSuccess) return hip_fail(e, "hipMalloc(work queues)");
-    // zeroed on the context's own stream, which its launches follow
-    if ((e = hipMemsetAsync(c.wq, 0, kWqBytes, c.stream)) != hipSuccess) return hip_fail(e, "hipMemsetAsync(work queues)");
-    if ((e = hipStreamSynchronize(c.stream)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
     e = hipStreamCreateWithFlags(&c.copy_stream, hipStreamNonBlocking);
     if (e != hipSuccess) return hip_fail(e, "hipStreamCreate(copy)");
     for (int k = 0; k < 2; ++k) {
@@ -233,69 +216,6 @@ int get_state(DevState** out) {
 hipStream_t pick_stream(DevState* st, void* stream) {
   (void)st;
   return static_cast<hipStream_t>(stream);
-}
-
-// The launch geometry of a device entry point on stream `s` (st->geom) and, when the launch will
-// run the record kernel (`records`), a set of its work-queue words that no other launch holds: a
-// free set (its last launch's event has completed; every record-kernel launch leaves its words
-// zero), else a new one.  While `s` is being captured into a graph nothing may be allocated or
-// waited on, and the graph may be replayed later beside any other launch: the captured launch gets
-// no set and runs the kernel's workgroup-local distribution instead (g->wq null).  *slot: the set
-// to pass to wq_done after the launch (-1: none).
-int wq_take(DevState* st, hipStream_t s, bool records, LaunchGeom* g, int* slot) {
-  *g = st->geom;
-  *slot = -1;
-  if (!records) return PDB_OK;
-  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-  hipError_t e = hipStreamIsCapturing(s, &cap);
-  if (e != hipSuccess) return hip_fail(e, "hipStreamIsCapturing");
-  if (cap != hipStreamCaptureStatusNone) return PDB_OK;
-  std::lock_guard<std::mutex> lk(st->wq_mu);
-  for (size_t i = 0; i < st->wqs.size(); ++i) {
-    DevState::WqSet& w = st->wqs[i];
-    if (w.busy && w.recorded && hipEventQuery(w.done) == hipSuccess) w.busy = false;
-    if (!w.busy) {
-      w.busy = true;
-      w.recorded = false;
-      g->wq = w.d;
-      *slot = static_cast<int>(i);
-      return PDB_OK;
-    }
-  }
-  DevState::WqSet w;
-  if ((e = hipMalloc(&w.d, kWqBytes)) != hipSuccess) return hip_fail(e, "hipMalloc(work queues)");
-  // zeroed in order on the launch's own stream: a plain hipMemset runs on the null stream, which a
-  // non-blocking caller stream does not wait for (recycled memory is not zero)
-  if ((e = hipMemsetAsync(w.d, 0, kWqBytes, s)) != hipSuccess) {
-    (void)hipFree(w.d);
-    return hip_fail(e, "hipMemsetAsync(work queues)");
-  }
-  if ((e = hipEventCreateWithFlags(&w.done, hipEventDisableTiming)) != hipSuccess) return hip_fail(e, "hipEventCreate");
-  w.busy = true;
-  st->wqs.push_back(w);
-  g->wq = w.d;
-  *slot = static_cast<int>(st->wqs.size() - 1);
-  return PDB_OK;
-}
-
-// After the launch that took `slot`: the set stays held until the launch completes (launched: an
-// event after it on `s`; not launched: free again at once).
-hipError_t wq_done(DevState* st, int slot, hipStream_t s, bool launched) {
-  if (slot < 0) return hipSuccess;
-  std::lock_guard<std::mutex> lk(st->wq_mu);
-  DevState::WqSet& w = st->wqs[static_cast<size_t>(slot)];
-  if (!launched) {
-    w.busy = false;
-    return hipSuccess;
-  }
-  hipError_t e = hipEventRecord(w.done, s);
-  if (e != hipSuccess) {
-    (void)hipStreamSynchronize(s);  // (never left held without a way to free it)
-    w.busy = false;
-    return e;
-  }
-  w.recorded = true;
-  return e;
 }
 
 int ensure_ws(HostCtx* c, size_t bytes) {
@@ -739,7 +659,6 @@ int host_desc(const uint8_t* base, uint64_t base_len, const pdb_blk* blk, uint64
   CtxLock cl(dev);
   HostCtx* st = cl.c;
   LaunchGeom hgeom = dev->hgeom;
-  hgeom.wq = st->wq;
   hipError_t e = hipSetDevice(dev->device);
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
   if ((rc = ensure_ws(st, nslots * slot_bytes + 256))) return rc;
@@ -819,7 +738,6 @@ int host_scalar(uint32_t init, const uint8_t* data, uint64_t n, uint32_t* out) {
     const uint32_t sentinel = st->seq++ * 0x9E3779B9u ^ 0x5A5A5A5Au;
     *h_res = sentinel;
     LaunchGeom hgeom = st->hgeom;
-    hgeom.wq = cl.c->wq;
     e = launch_fixed(hgeom, st->d_tables, st->d_stage + kStageHdr, 0, static_cast<uint32_t>(n), 1,
                      PDB_CRC_USE_INIT, init, d_res, s);
     if (e != hipSuccess) return hip_fail(e, "launch_fixed(scalar)");
@@ -919,7 +837,6 @@ int host_sst(uint8_t* buf, uint64_t buf_len, const pdb_block_handle* h, uint64_t
   CtxLock cl(dev);
   HostCtx* st = cl.c;
   LaunchGeom hgeom = dev->hgeom;
-  hgeom.wq = st->wq;
   hipError_t e = hipSetDevice(dev->device);
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
   if ((rc = ensure_ws(st, nslots * slot_bytes + 256))) return rc;
@@ -1079,14 +996,8 @@ int pdb_crc32c_batch_device_fixed(const void* d_base, uint64_t stride, uint32_t 
   int rc = get_state(&st);
   if (rc) return rc;
   if ((rc = quiesce(st))) return rc;
-  LaunchGeom g;
-  int slot;
-  hipStream_t s = pick_stream(st, stream);
-  if ((rc = wq_take(st, s, fixed_runs_records(d_base, stride, len, flags), &g, &slot))) return rc;
-  hipError_t e = launch_fixed(g, st->d_tables, static_cast<const uint8_t*>(d_base), stride, len,
-                              nblk, flags, init, d_out, s);
-  const hipError_t e2 = wq_done(st, slot, s, e == hipSuccess);
-  if (e == hipSuccess) e = e2;
+  hipError_t e = launch_fixed(st->geom, st->d_tables, static_cast<const uint8_t*>(d_base), stride, len,
+                              nblk, flags, init, d_out, pick_stream(st, stream));
   return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_fixed");
 }
 
@@ -1098,14 +1009,8 @@ int pdb_crc32c_batch_device(const void* d_base, const pdb_blk* d_blk, uint64_t n
   int rc = get_state(&st);
   if (rc) return rc;
   if ((rc = quiesce(st))) return rc;
-  LaunchGeom g;
-  int slot;
-  hipStream_t s = pick_stream(st, stream);
-  if ((rc = wq_take(st, s, desc_runs_records(flags), &g, &slot))) return rc;
-  hipError_t e = launch_desc(g, st->d_tables, static_cast<const uint8_t*>(d_base), d_blk, nblk,
-                             flags, kModeOut, nullptr, d_out, nullptr, nullptr, s);
-  const hipError_t e2 = wq_done(st, slot, s, e == hipSuccess);
-  if (e == hipSuccess) e = e2;
+  hipError_t e = launch_desc(st->geom, st->d_tables, static_cast<const uint8_t*>(d_base), d_blk, nblk,
+                             flags, kModeOut, nullptr, d_out, nullptr, nullptr, pick_stream(st, stream));
   return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_desc");
 }
 
@@ -1118,14 +1023,8 @@ int pdb_crc32c_verify_device(const void* d_base, const pdb_blk* d_blk, uint64_t 
   int rc = get_state(&st);
   if (rc) return rc;
   if ((rc = quiesce(st))) return rc;
-  LaunchGeom g;
-  int slot;
-  hipStream_t s = pick_stream(st, stream);
-  if ((rc = wq_take(st, s, desc_runs_records(flags), &g, &slot))) return rc;
-  hipError_t e = launch_desc(g, st->d_tables, static_cast<const uint8_t*>(d_base), d_blk, nblk,
-                             flags, kModeVerify, d_expected, nullptr, d_ok, d_nbad, s);
-  const hipError_t e2 = wq_done(st, slot, s, e == hipSuccess);
-  if (e == hipSuccess) e = e2;
+  hipError_t e = launch_desc(st->geom, st->d_tables, static_cast<const uint8_t*>(d_base), d_blk, nblk,
+                             flags, kModeVerify, d_expected, nullptr, d_ok, d_nbad, pick_stream(st, stream));
   return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_desc(verify)");
 }
 

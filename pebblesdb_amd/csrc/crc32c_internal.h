@@ -21,25 +21,12 @@ enum DescMode : int {
   kModeVerify = 1,  // ok[i] = (crc == expected[i])
 };
 
-// crc_lanespan_kernel's device-wide work queues: PDB_SPAN_QUEUES queue words + the exit count, each
-// on its own 128-B line
-#define PDB_SPAN_QUEUES 16u
-constexpr size_t kWqBytes = (PDB_SPAN_QUEUES + 1u) * 128u;
-
 struct LaunchGeom {
   uint32_t grid;   // workgroups (one per CU: the LDS image is ~156 KiB)
   uint32_t block;  // threads per workgroup
-  // work-queue words for crc_lanespan_kernel (kWqBytes, zero, held by this launch
-  // alone until it completes: the C-ABI's wq_take / a host context's own set), or null for the
-  // kernel's workgroup-local distribution
-  uint32_t* wq = nullptr;
 };
 
 // crc32c_kernels.hip -- all launches are asynchronous on `s`.
-// Whether launch_fixed / launch_desc with these arguments run the record kernel (crc_lanespan_kernel),
-// the one kernel that takes work from LaunchGeom::wq (the C-ABI only takes a queue set for those).
-bool fixed_runs_records(const void* base, uint64_t stride, uint32_t len, uint32_t flags);
-bool desc_runs_records(uint32_t flags);
 hipError_t launch_fixed(const LaunchGeom& g, const uint32_t* d_tables, const uint8_t* base,
                         uint64_t stride, uint32_t len, uint64_t nblk, uint32_t flags, uint32_t init,
                         uint32_t* out, hipStream_t s);

@@ -106,17 +106,6 @@ hipError_t launch_span(const LaunchGeom& g, const uint32_t* d_tables, const uint
   return hipGetLastError();
 }
 
-// (the routing of launch_fixed / launch_desc_sink below, kept in step with them)
-bool fixed_runs_records(const void* base, uint64_t stride, uint32_t len, uint32_t flags) {
-  const bool fast = len == 4096u && (reinterpret_cast<uintptr_t>(base) & 15u) == 0 && (stride & 15u) == 0;
-  return !fast && !(flags & PDB_CRC_USE_INIT) && !(len - kSstMin <= kSstMax - kSstMin) && len - 1u <= 1151u;
-}
-bool desc_runs_records(uint32_t flags) {
-  if (flags & PDB_CRC_USE_INIT) return false;
-  return (flags & PDB_CRC_SIZE_1K) ||
-         (!(flags & PDB_CRC_SIZE_4K) && (flags & (PDB_CRC_SIZE_256 | PDB_CRC_SIZE_512 | PDB_CRC_SIZE_1023)));
-}
-
 hipError_t launch_fixed(const LaunchGeom& g, const uint32_t* d_tables, const uint8_t* base,
                         uint64_t stride, uint32_t len, uint64_t nblk, uint32_t flags, uint32_t init,
                         uint32_t* out, hipStream_t s) {

@@ -348,7 +348,7 @@ struct SpanItem {
 // kMixed (PDB_CRC_SIZE_MIXED): per-record lane counts where a batch's records vary (open_batch).
 template <class Src, class Sink, uint32_t MAXN, int MODE = 0, class TP = TabsS4, bool kDyn = true, bool kMixed = false>
 __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_kernel(const uint32_t* __restrict__ tabs, Src src,
-                                                                       uint64_t nblk, Sink sink, uint32_t* wq) {
+                                                                       uint64_t nblk, Sink sink) {
   constexpr uint32_t kSpanWaves = SpanStage<MAXN>::kWaves, kSpanJ = SpanStage<MAXN>::kJ;
   constexpr uint32_t kSpanRegion = SpanStage<MAXN>::kRegion, kSpanUsable = SpanStage<MAXN>::kUsable;
   typedef SpanStage<MAXN> ST;
@@ -375,27 +375,17 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
   constexpr bool kClk = MODE >= 40 && MODE <= 42;  // diagnostics: shader-clock stamps (tools/span_clock.py)
   if constexpr (kClk) t_start = wall_clock64();
   if constexpr (kClk) c_start = clock64();
-  // Work units (first record r0, records cnt <= 64): whole batches, and near the end split batches,
-  // kS units of 64 / kS records (16: one item of the 512 class, two of the 1023 / 1152 classes; the
-  // <= 256 class keeps whole batches, one or two items each), so the waves run out of work within
-  // about an item of each other instead of a batch (~40 us on 1000-B records).  Each
-  // wave holds one ticket in flight (the unit after the one whose descriptors are in flight), so no
-  // atomic's latency waits in front of a load.
-  //   Phase 1: the workgroup's own contiguous range of the first M batches, from an LDS counter
-  //     (every CU streams the same region of the image as the others; device-wide queues for ALL the
-  //     work measured 1-16 % slower, the atomics' traffic and order costing more than they balance:
-  //     profiles/r05/).  Without a pool (wq null: a launch captured into a graph, diagnostics 183)
-  //     M = nbat and the range's last kWaves batches are split.
-  //   Phase 2 (wq != null, the C-ABI's default): the pool, the last nbat - M batches (kPool of them per
-  //     kQ-wave slice of the grid, ~2 per wave), all split, from kQ = 16 device-wide queues -- queue x
-  //     (wq[32 x], its own 128-B line) owns pool batches M + kQ j + x -- started at queue
-  //     blockIdx.x mod kQ and moved on from when one runs out.  Whichever CUs finish their range
-  //     first (a faster XCD) take more of the pool.  The last wave out resets the kQ + 1 words
-  //     (queues + the exit count); the C-ABI never hands one set to two launches that may run at once.
-  //   kDyn false (diagnostics): static batches wv + k W.
-  const bool gq = kDyn && wq != nullptr;  // grid-uniform
-  // the workgroup's batch counter (phase 1): the last 16 B of the last wave's region, which no item
-  // ever uses (spans end by kUsable) and to_lds skips
+  // Work units (first record r0, records cnt <= 64): the workgroup owns batches [g nbat / G,
+  // (g + 1) nbat / G) and its waves take them from an LDS counter; the range's last kWaves batches
+  // are split in kS units of 64 / kS records (16: one item of the 512 class, two of the 1023 / 1152
+  // classes; the <= 256 class keeps whole batches, one or two items each), so the waves run out of
+  // work within about an item of each other instead of a batch (~40 us on 1000-B records): +1.3-1.5 %
+  // on wal400 / wal1000 (profiles/r05/queues/).  Each wave holds one ticket in flight (the unit after
+  // the one whose descriptors are in flight), so the LDS atomic's latency never waits in front of a
+  // load.  (Device-wide queues -- for all the work, or a pool for the tail -- measured 1-16 % slower:
+  // profiles/r05/queues/README.md.)  kDyn false (diagnostics): static batches wv + k W.
+  // the counter: the last 16 B of the last wave's region, which no item ever uses (spans end by
+  // kUsable) and to_lds skips
   uint32_t* ctr = reinterpret_cast<uint32_t*>(lds + kSpanStageBase + kSpanWaves * kSpanRegion - 16u);
   if (kDyn && threadIdx.x == 0) *ctr = kSpanWaves;  // ticket wv is each wave's first
   __syncthreads();
@@ -403,44 +393,28 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
   char* region = lds + kSpanStageBase + wv * kSpanRegion;
   const uintptr_t dummy = reinterpret_cast<uintptr_t>(tabs);  // >= 4 KiB + 256 B of valid bytes
   const uint64_t nbat = (nblk + 63u) >> 6;
-  const uint32_t nwaves = gridDim.x * kSpanWaves;
-  const uint64_t W = nwaves;
+  const uint64_t W = static_cast<uint64_t>(gridDim.x) * kSpanWaves;
   constexpr uint32_t kS = MAXN <= 256u ? 1u : 4u;  // units per split batch
-  constexpr uint32_t kQ = PDB_SPAN_QUEUES;
-  // the pool: ~kPool batches per wave of the grid (at most half the work; MODE 45 / 46: 1 / 4, A/B)
-  constexpr uint64_t kPool = MODE == 45 ? 1u : (MODE == 46 ? 4u : 2u);
-  const uint64_t npool = gq ? (kPool * nwaves < nbat / 2u ? kPool * nwaves : nbat / 2u) : 0u;
-  const uint64_t M = nbat - npool;
-  uint32_t qx = blockIdx.x % kQ, qn = 0;
-  bool phase2 = false;
   uint32_t tick = wv;  // lane 0: the ticket in flight
   uint64_t sbat = static_cast<uint64_t>(blockIdx.x) * kSpanWaves + wv;  // kDyn false: the next batch
-  const uint64_t g_lo = M * blockIdx.x / gridDim.x, g_end = M * (blockIdx.x + 1) / gridDim.x;
+  const uint64_t g_lo = nbat * blockIdx.x / gridDim.x, g_end = nbat * (blockIdx.x + 1) / gridDim.x;
   auto unit_of_batch = [&](uint64_t b, uint64_t& r0, uint32_t& cnt) {
     r0 = b << 6;
     cnt = static_cast<uint32_t>(nblk - r0 < 64u ? nblk - r0 : 64u);
   };
-  // ticket t of the workgroup's range (phase 1) or of pool queue x (phase 2): false when exhausted;
-  // cnt 0 = an empty unit past nblk (the last batch's)
+  // ticket t of the workgroup's range: false when exhausted; cnt 0 = an empty unit past nblk
   auto decode = [&](uint32_t t, uint64_t& r0, uint32_t& cnt) -> bool {
-    const uint64_t n = phase2 ? (npool > qx ? (npool - qx + kQ - 1u) / kQ : 0u) : g_end - g_lo;
-    auto batch = [&](uint64_t j) -> uint64_t { return phase2 ? M + kQ * j + qx : g_lo + j; };
-    const uint64_t R = kS == 1u ? 0u : (phase2 ? n : (gq ? 0u : (n < kSpanWaves ? n : kSpanWaves)));
-    const uint64_t F = n - R;
+    const uint64_t n = g_end - g_lo;
+    const uint64_t R = kS == 1u ? 0u : (n < kSpanWaves ? n : kSpanWaves), F = n - R;
     if (t < F) {
-      unit_of_batch(batch(t), r0, cnt);
+      unit_of_batch(g_lo + t, r0, cnt);
       return true;
     }
     const uint64_t q = t - F;
     if (q >= kS * R) return false;
-    r0 = (batch(F + q / kS) << 6) + (q % kS) * (64u / kS);
+    r0 = ((g_lo + F + q / kS) << 6) + (q % kS) * (64u / kS);
     cnt = r0 >= nblk ? 0u : static_cast<uint32_t>(nblk - r0 < 64u / kS ? nblk - r0 : 64u / kS);
     return true;
-  };
-  auto take = [&]() -> uint32_t {  // lane 0: the next ticket of the current range
-    if (u != 0) return 0u;
-    return phase2 ? __hip_atomic_fetch_add(wq + 32u * qx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                  : __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   };
   // the next unit (false: no work left): decode the ticket in flight, put the following one in flight
   auto acquire = [&](uint64_t& r0, uint32_t& cnt) -> bool {
@@ -452,18 +426,9 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
     } else {
       for (;;) {
         const uint32_t t = __builtin_amdgcn_readfirstlane(tick);
-        if (decode(t, r0, cnt)) {
-          tick = take();
-          if (cnt) return true;
-          continue;  // an empty unit (the last batch's): the next ticket
-        }
-        if (!gq) return false;
-        if (phase2) {
-          if (++qn == kQ) return false;
-          qx = (qx + 1u) % kQ;
-        }
-        phase2 = true;
-        tick = take();
+        if (!decode(t, r0, cnt)) return false;
+        if (u == 0) tick = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (cnt) return true;  // (else an empty unit, the last batch's: the next ticket)
       }
     }
   };
@@ -916,17 +881,6 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
       I1 = I3;
     }
   }
-  if (gq) {
-    // the last wave out (every wave counts itself once, after its last ticket came back) resets the
-    // queue words for the set's next launch
-    if (u == 0) {
-      const uint32_t done = __hip_atomic_fetch_add(wq + 32u * kQ, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (done == nwaves - 1u) {
-#pragma unroll
-        for (uint32_t x = 0; x <= kQ; ++x) __hip_atomic_store(wq + 32u * x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-  }
   if constexpr (kClk) {
     // MODE 40 / 41 / 42 (the product / loads alone / hash alone): [start, end] s_memrealtime (100 MHz)
     // and [start, end] s_memtime (shader clock): the wave's mean clock over its lifetime
@@ -950,36 +904,33 @@ inline uint32_t grid_span(const LaunchGeom& g, uint64_t nblk, uint32_t waves) {
 
 // Records of 1..1152 B by class (the class bounds the lanes per record: 2, 4, 8, 8); longer ones,
 // and empty ones, take the whole-wave path.
-// g.wq: the launch's work-queue words (PDB_SPAN_QUEUES + 1 words on 128-B lines, zero, owned by this launch until it
-// completes), or null for the workgroup-local distribution (crc_lanespan_kernel, "work units").
 template <class Src, class Sink, int MODE = 0, class TP = TabsS4, bool kDyn = true>
 hipError_t launch_lanespan(const LaunchGeom& g, const uint32_t* d_tables, const Src& src, uint64_t nblk, uint32_t cls,
                            const Sink& sink, hipStream_t s, bool mixed = false) {
-  uint32_t* wq = g.wq;
   if (cls <= 256u) {
     constexpr uint32_t w = SpanStage<256>::kWaves;
     hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 256, MODE, TP, kDyn>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0, s,
-                       d_tables, src, nblk, sink, wq);
+                       d_tables, src, nblk, sink);
   } else if (cls <= 512u) {
     constexpr uint32_t w = SpanStage<512>::kWaves;
     if (mixed && !__is_same(Sink, VerifySink))
       hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 512, MODE, TP, kDyn, true>), dim3(grid_span(g, nblk, w)), dim3(w * 64),
-                         0, s, d_tables, src, nblk, sink, wq);
+                         0, s, d_tables, src, nblk, sink);
     else
       hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 512, MODE, TP, kDyn>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0, s,
-                         d_tables, src, nblk, sink, wq);
+                         d_tables, src, nblk, sink);
   } else if (cls <= 1023u) {
     constexpr uint32_t w = SpanStage<1023>::kWaves;
     if (mixed && !__is_same(Sink, VerifySink))
       hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 1023, MODE, TP, kDyn, true>), dim3(grid_span(g, nblk, w)), dim3(w * 64),
-                         0, s, d_tables, src, nblk, sink, wq);
+                         0, s, d_tables, src, nblk, sink);
     else
       hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 1023, MODE, TP, kDyn>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0,
-                         s, d_tables, src, nblk, sink, wq);
+                         s, d_tables, src, nblk, sink);
   } else {  // 1024..1152 B (WAL records of ~1-KiB write batches): 8 lanes, the head chain past 1056 B
     constexpr uint32_t w = SpanStage<1152>::kWaves;
     hipLaunchKernelGGL((crc_lanespan_kernel<Src, Sink, 1152, MODE, TP, kDyn>), dim3(grid_span(g, nblk, w)), dim3(w * 64), 0,
-                       s, d_tables, src, nblk, sink, wq);
+                       s, d_tables, src, nblk, sink);
   }
   return hipGetLastError();
 }

@@ -51,17 +51,6 @@ int diag_state(const DiagDev** out) {
       return dfail(PDB_ENOMEM, std::string("hipMalloc(tables): ") + hipGetErrorString(e));
     if ((e = hipMemcpy(p, tabs.data(), tabs.size() * 4, hipMemcpyHostToDevice)) != hipSuccess)
       return dfail(PDB_EHIP, std::string("hipMemcpy(tables): ") + hipGetErrorString(e));
-    // the record kernel's work-queue words (one set per device: the diagnostics tools launch on one
-    // stream; crc32c_capi.cpp keeps one per stream)
-    uint32_t* wq = nullptr;
-    if ((e = hipMalloc(&wq, kWqBytes)) != hipSuccess)
-      return dfail(PDB_ENOMEM, std::string("hipMalloc(work queues): ") + hipGetErrorString(e));
-    if ((e = hipMemset(wq, 0, kWqBytes)) != hipSuccess)
-      return dfail(PDB_EHIP, std::string("hipMemset(work queues): ") + hipGetErrorString(e));
-    // (the null-stream memset must be done before a launch on a non-blocking stream reads the words)
-    if ((e = hipDeviceSynchronize()) != hipSuccess)
-      return dfail(PDB_EHIP, std::string("hipDeviceSynchronize: ") + hipGetErrorString(e));
-    d.geom.wq = wq;
     d.d_tables = p;
   }
   *out = &d;

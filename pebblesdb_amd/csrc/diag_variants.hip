@@ -86,71 +86,6 @@ __global__ __launch_bounds__(kThreads) void read_pattern4k_kernel(const uint8_t*
   if (lane == 0) atomicXor(out, acc);
 }
 
-// Variant 23: the same loads with the WORK DISTRIBUTION of the record kernel's queues (crc32c_lanespan.h,
-// gq) at workgroup level: chunks of 64 blocks from PDB_SPAN_QUEUES queue words (wq[32 x]; queue x
-// owns chunks kQ j + x, so every workgroup streams the same region as the others); in a chunk,
-// wave w loads blocks 16 r + w (r = 0..3) in lock-step, so each row of the workgroup reads 64 KiB
-// contiguous; the next chunk's ticket is taken one chunk ahead by lane 0 of wave 0 and published
-// through LDS at the barrier; a workgroup moves to the next queue when its own runs out, and the
-// last workgroup out resets the words.  Against variant 21 it prices what balancing the chip's
-// CUs dynamically is worth for the 4-KiB kernel's own loads.
-__global__ __launch_bounds__(kThreads) void read_pattern4k_dyn_kernel(const uint8_t* __restrict__ base, uint64_t nblk,
-                                                                      uint32_t* __restrict__ out, uint32_t* wq) {
-  __shared__ uint32_t next_chunk[2];
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t nchunk = (nblk + 63u) / 64u;
-  constexpr uint32_t kQ = PDB_SPAN_QUEUES;
-  uint32_t qx = blockIdx.x % kQ, qn = 0;  // (wave 0's copy is the one that counts)
-  auto issue = [&]() -> uint32_t {  // lane 0 of wave 0: a ticket of queue qx
-    return lane == 0 ? __hip_atomic_fetch_add(wq + 32u * qx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-  };
-  // the chunk of ticket tk (in flight), else the next queues' tickets (every queue exhausted: ~0)
-  auto resolve = [&](uint32_t tk) -> uint64_t {
-    for (;;) {
-      const uint64_t c = static_cast<uint64_t>(kQ) * __builtin_amdgcn_readfirstlane(tk) + qx;
-      if (c < nchunk) return c;
-      if (++qn == kQ) return ~0ull;
-      qx = (qx + 1u) % kQ;
-      tk = issue();
-    }
-  };
-  if (w == 0) {
-    const uint64_t c = resolve(issue());
-    if (lane == 0) next_chunk[0] = static_cast<uint32_t>(c), next_chunk[1] = static_cast<uint32_t>(c >> 32);
-  }
-  __syncthreads();
-  uint64_t cur = uniform64(next_chunk[0], next_chunk[1]);
-  uint32_t acc = 0;
-  while (cur != ~0ull) {
-    const uint32_t tk = w == 0 ? issue() : 0u;  // the next chunk's ticket, in flight with the loads
-    u32x4 x = {0, 0, 0, 0};
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const uint64_t b = cur * 64u + 16u * r + w;
-      if (b < nblk) {
-        const uint8_t* blk = base + b * 4096u;
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          x ^= __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(blk + lane * 16u + j * 1024u));
-      }
-    }
-    acc ^= x.x ^ x.y ^ x.z ^ x.w;
-    const uint64_t nxt = w == 0 ? resolve(tk) : 0u;
-    __syncthreads();  // every wave has read next_chunk (previous iteration)
-    if (w == 0 && lane == 0) next_chunk[0] = static_cast<uint32_t>(nxt), next_chunk[1] = static_cast<uint32_t>(nxt >> 32);
-    __syncthreads();
-    cur = uniform64(next_chunk[0], next_chunk[1]);
-  }
-  for (int k = 32; k; k >>= 1) acc ^= __shfl_xor(acc, k, 64);
-  if (lane == 0) atomicXor(out, acc);
-  if (threadIdx.x == 0) {  // the last workgroup out resets the queue words
-    const uint32_t done = __hip_atomic_fetch_add(wq + 32u * kQ, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (done == gridDim.x - 1u)
-      for (uint32_t q = 0; q <= kQ; ++q) __hip_atomic_store(wq + 32u * q, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
 // Seal-pattern calibration (sst variants 140 / 141; no CRC work, trailers written with WRONG values
 // by design): the in-place seal's memory pattern without its hash -- every block's bytes [offset,
 // offset + size + 5) read as 1-KiB-contiguous 16-B nt loads by the wave owning its 4-block group,
@@ -293,17 +228,6 @@ hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tab
     case 126:  // the item geometry per record instead of its CRC (MODE 18; tests/test_lanespan.py)
       return launch_lanespan<DescSrc, OutSink, 18>(g, d_tables, src, nblk, record_class(flags), OutSink{out, 0u}, s,
                                                    mixed);
-    case 183: {  // exact: the workgroup-local distribution (each workgroup a fixed range of batches from
-                 // an LDS counter, its last batches split; what a launch captured into a graph runs),
-                 // for A/B against the device-wide queues
-      LaunchGeom g0 = g;
-      g0.wq = nullptr;
-      return launch_lanespan<DescSrc, OutSink>(g0, d_tables, src, nblk, record_class(flags), sink, s, mixed);
-    }
-    case 184:  // exact: the tail pool at 1 / 4 batches per wave of the grid (the product: 2)
-      return launch_lanespan<DescSrc, OutSink, 45>(g, d_tables, src, nblk, record_class(flags), sink, s, mixed);
-    case 185:
-      return launch_lanespan<DescSrc, OutSink, 46>(g, d_tables, src, nblk, record_class(flags), sink, s, mixed);
     case 180:    // the product / loads + staging alone / hash alone, + per-wave [start, end] s_memrealtime
     case 181:    // and [start, end] s_memtime stamps at out + nblk rounded up to 8 B (the caller sizes
     case 182: {  // `out` for 4 x 8 B per wave; tools/span_clock.py)
@@ -329,11 +253,6 @@ hipError_t launch_read_stream(const uint8_t* base, uint64_t nbytes, uint32_t* ou
 
 hipError_t launch_read_pattern4k(const LaunchGeom& g, const uint8_t* base, uint64_t nblk,
                                  int variant, uint32_t* out, hipStream_t s) {
-  if (variant == 23) {  // the same loads from device-wide chunk queues
-    if (!g.wq) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(read_pattern4k_dyn_kernel, dim3(g.grid), dim3(kThreads), 0, s, base, nblk, out, g.wq);
-    return hipGetLastError();
-  }
   if (variant != 21) return hipErrorInvalidValue;  // the 4-KiB path's pattern (the others: round 1-2, removed)
   hipLaunchKernelGGL(read_pattern4k_kernel, dim3(g.grid), dim3(kThreads), 0, s, base, nblk, out);
   return hipGetLastError();

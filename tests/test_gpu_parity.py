@@ -221,9 +221,9 @@ def test_device_entry_points_capture_into_hip_graph(crc, oracle_lib):
 
 
 def test_record_batches_on_concurrent_streams(crc, oracle_lib):
-    """Record-kernel launches (the device-wide work queues) from several streams at once, each
-    launch many times back to back: every launch holds its own queue words until it completes, so
-    concurrent launches never take each other's work (a shared set would skip or repeat units)."""
+    """Record-kernel launches from several streams at once, each launch many times back to back:
+    launches that run side by side share nothing (each workgroup's work counter is in its own LDS),
+    so every record is hashed exactly once by every launch."""
     import threading
 
     rng = np.random.Generator(np.random.PCG64(606))

@@ -178,9 +178,8 @@ def test_mixed_geometry_items():
             assert lane[r] == int(k[64 * b + i0:64 * b + r].sum()) and lane[r] + kl[r] <= 64
 
 
-# 183: the round-2..4 work distribution (each workgroup a fixed range of batches, MODE 44), against
-# which the device-wide queues of round 5 were measured; 125: the batch-uniform lane count only
-RECORD_VARIANTS = [183, 125]
+# 125: the batch-uniform lane count only (no per-record lanes for mixed sizes)
+RECORD_VARIANTS = [125]
 
 
 @pytest.mark.parametrize("hint", ["256", "512", "512m", "1023", "1023m", "1k"])

@@ -29,7 +29,7 @@ for s in "$@"; do
     fullsize) step fullsize 600 python -u -m pytest tests/test_full_size.py tests/test_gpu_parity.py -m gpu -x -v --timeout 300 --timeout-method thread -k "full_size or host_" ;;
     # the record kernel: 50-step bench lines, parts / distribution A/B, clocks, counters
     bench_wal) for w in wal100 wal400 wal1000 wal; do step bench_$w 300 python bench.py --workload $w --no-copy-inclusive --steps 50 || exit 1; done ;;
-    ab_span) step ab_span 600 python tools/ab_span.py 0,183,63,64,67 wal100,wal400,wal1000,wal 6 ;;
+    ab_span) step ab_span 600 python tools/ab_span.py 0,63,64,67 wal100,wal400,wal1000,wal 6 ;;
     span_clock) step span_clock 600 python tools/span_clock.py wal100,wal400,wal1000,wal 3 ;;
     counters_span) step counters_span 900 bash tools/counters_span.sh ${TAG}_span wal100 wal400 wal1000 wal ;;
     prof_wal) for w in wal100 wal400 wal1000 wal; do step prof_$w 500 bash tools/profile.sh ${TAG}_prof_$w $w || exit 1; done ;;
