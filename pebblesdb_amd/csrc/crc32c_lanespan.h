@@ -491,7 +491,10 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
     const uint32_t fn = __shfl_down(bfast ? 1u : 0u, 1, 64);
     const bool link_ok = bfast && fn && pn >= bp && pn <= bp + bn + 64u;
     bbroken = __builtin_amdgcn_ballot_w64(!link_ok && u < 63u);
-    const uint32_t nw = wave_max_u32(bfast ? (bn + 3u) >> 2 : 0u);
+    // the lanes cover a record's dwords after its p-word (the hash takes the p-word on the head lane
+    // either way): nw = dwords of [p, p + n) on the grid - 1 <= ceil(n / 4)
+    const uint32_t nwl = ((plo & 3u) + bn + 3u) >> 2;
+    const uint32_t nw = wave_max_u32(bfast ? (nwl > 1u ? nwl - 1u : 1u) : 0u);
     bg = span_pick<KMAX, ST>(nw ? nw : 1u);
     bcursor = 0;
     // Mixed sizes: the batch-uniform k is set by the longest record, so a short record's lanes
@@ -501,7 +504,7 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
     // items x (steps + 4), items bounded by the lanes (sum kr / 64) and the staging span.
     bvar = false;
     if constexpr (kVar) {
-      const uint32_t nwr = (bn + 3u) >> 2;
+      const uint32_t nwr = nwl > 1u ? nwl - 1u : 1u;
       const uint32_t kq = (nwr + PART - 1u) / PART;
       const uint32_t bkr = bfast ? (kq < KMAX ? (kq ? kq : 1u) : KMAX) : 0u;
       bkw = bkr;
@@ -545,7 +548,7 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
       // 16 r + 15 (row_shr 4: quads 0|1 and 2|3; row_shr 8: quads 0|2 and 1|3)
       constexpr uint32_t kM0 = (1u << 0) | (1u << ((32u - ST::kPart % 32u) % 32u)) |
                                (1u << ((64u - 2u * ST::kPart % 32u) % 32u)) | (1u << ((96u - 3u * ST::kPart % 32u) % 32u));
-      const uint32_t ew = ((plo + bn) >> 2) & 31u;
+      const uint32_t ew = ((plo + bn + 3u) >> 2) & 31u;
       uint32_t msk = bfast ? __builtin_amdgcn_alignbit(kM0, kM0, (32u - ew) & 31u) : 0u;
       msk |= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(msk), 0x111, 0xF, 0xF, false));
       msk |= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(msk), 0x112, 0xF, 0xF, false));
@@ -714,23 +717,26 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
     // the record's parts after this one: >= m
     auto more = [&](uint32_t m) -> bool { return kVar ? ((it.cw >> 4) & 15u) >= m : pc + m < k; };
     const bool head = kVar ? ((it.cw >> 4) & 15u) == 0u : pc == k - 1u;
-    const uint32_t sel = static_cast<uint32_t>(e & 3) * 0x01010101u + 0x03020100u;
-    const uint32_t zp = static_cast<uint32_t>(pl - e) & 3u;  // bytes of the p-word before p
+    // Words are the region's dwords (the dword grid): the record's last dword holds j = (-e) mod 4
+    // bytes past its end, masked to zero (finished by a shift of 4 - j bytes instead of F), and its
+    // first dword, the p-word, zp bytes before p, masked with U[zp] injected.  Part c ends at
+    // eg - 4 PART c, eg = e rounded up to the grid.
+    const int32_t eg = (e + 3) & ~3;
+    const uint32_t j = static_cast<uint32_t>(eg - e);
+    const uint32_t endm = 0xFFFFFFFFu >> (8u * j);  // the last dword's bytes in the record
+    const uint32_t zp = static_cast<uint32_t>(pl) & 3u;  // bytes of the p-word before p
     const uint32_t uz = __shfl(ureg, zp, 64);
-    // The word at byte s (s = e mod 4) is the dword pair (D[s >> 2], D[(s >> 2) + 1]) through sel.
     // The p-word (at sp), masked below p with U[z] injected, replaces its chain's state at its
     // step; a chain wholly before p yields 0.
-    const int32_t eA = e - static_cast<int32_t>(4u * PART * pc);
-    const int32_t sp = act ? pl - static_cast<int32_t>(zp) : e;  // (no record: an address in range)
-    uint32_t pw;
-    {
-      const char* q = region + 4 * (sp >> 2);
-      pw = (__builtin_amdgcn_perm(lds_u32(q, 4), lds_u32(q, 0), sel) & (0xFFFFFFFFu << (8u * zp))) ^ uz;
-    }
+    const int32_t eA = eg - static_cast<int32_t>(4u * PART * pc);
+    const int32_t sp = act ? pl - static_cast<int32_t>(zp) : eg - 4;  // (no record: an address in range)
+    const uint32_t pw = (lds_u32(region + sp, 0) & (0xFFFFFFFFu << (8u * zp)) & (sp == eg - 4 ? endm : 0xFFFFFFFFu)) ^ uz;
+    // the last word of chain A on part 0 (the record's last dword) keeps the record's bytes only
+    const uint32_t lastm = pc == 0 ? endm : 0xFFFFFFFFu;
     // the p-word's lock-step step in chain A's numbering; T + LC X in chain X's
     const int32_t T = static_cast<int32_t>(NI) - ((eA - sp) >> 2);
     // base of the chains' words: chain X's dword i at q3 + 4 LC (3 - X) + 4 i (word at step t =
-    // dwords t, t + 1); below the region for short records (words never used)
+    // dword t); below the region for short records (words never used)
     const int32_t qd = (eA - static_cast<int32_t>(4u * NI + 12u * LC)) >> 2;  // q3's dword (region-relative)
     const char* q3 = region + 4 * qd;
     // the chains' reads are addressed as lds + qo + constant with qo opaque to the compiler, so every
@@ -740,42 +746,34 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
     uint32_t qo = static_cast<uint32_t>(region - lds) + static_cast<uint32_t>(4 * qd);
     asm volatile("" : "+v"(qo));
     auto sread = [&](uint32_t off) -> uint32_t { return lds_u32(lds, qo + off); };
-    uint32_t xd = 0, ld = 0;
+    // The p-word may also be the dword just before the head lane's first word (the lanes cover the
+    // record's dwords after its p-word: span_pick counts those): the head chain then starts from it.
+    uint32_t xd = 0;
     uint32_t xa = 0, xb = 0, xc = 0;
     if (lim > 0) {  // the head chain alone (junk on the other lanes, dropped)
       const int32_t tD = T + static_cast<int32_t>(3u * LC + lim) - FD;  // the p-word's step in it
       const char* q = q3 + 4 * (FD - static_cast<int32_t>(lim));
-      ld = lds_u32(q, 0);
+      xd = tD == -1 ? pw : 0u;
       for (int32_t t = 0; t < static_cast<int32_t>(lim); ++t, q += 4) {
-        const uint32_t h = lds_u32(q, 4);
-        const uint32_t w = __builtin_amdgcn_perm(h, ld, sel);
-        ld = h;
+        const uint32_t w = lds_u32(q, 0);
         xd = t == tD ? pw : TP::step(lds, lt, xd, w);
       }
       xd = head ? xd : 0u;
     } else {
-      ld = sread(4u * FD);
+      xd = head && T + static_cast<int32_t>(3u * LC) == FD - 1 ? pw : 0u;
     }
-    // The chains' words: one ds_read_b32 per word and chain (the dword after the previous one).
-    // (Aligned ds_read_b64 pairs measured 2.5-9 % slower on every WAL row, profiles/r04/ab_pairs.log:
-    // the extra live pair registers and selects.)
-    uint32_t la = sread(12u * LC + 4u * FABC), lb = sread(8u * LC + 4u * FABC), lc = sread(4u * LC + 4u * FABC);
+    // The chains' words: one ds_read_b32 per word and chain.  (Aligned ds_read_b64 pairs measured
+    // 2.5-9 % slower on every WAL row, profiles/r04/ab_pairs.log: the extra live pair registers and
+    // selects.)
 #pragma unroll
     for (int32_t t = 0; t < static_cast<int32_t>(NI); ++t) {
       const bool abc = t >= FABC, dd = t >= FD;  // compile time
       uint32_t wa = 0, wb = 0, wc = 0, wd = 0;
       if (abc) {
-        const uint32_t ha = sread(12u * LC + 4u * (t + 1)), hb = sread(8u * LC + 4u * (t + 1));
-        const uint32_t hc = sread(4u * LC + 4u * (t + 1));
-        wa = __builtin_amdgcn_perm(ha, la, sel), wb = __builtin_amdgcn_perm(hb, lb, sel);
-        wc = __builtin_amdgcn_perm(hc, lc, sel);
-        la = ha, lb = hb, lc = hc;
+        wa = sread(12u * LC + 4u * t), wb = sread(8u * LC + 4u * t), wc = sread(4u * LC + 4u * t);
+        if (t == static_cast<int32_t>(NI) - 1) wa &= lastm;
       }
-      if (dd) {
-        const uint32_t hd = sread(4u * (t + 1));
-        wd = __builtin_amdgcn_perm(hd, ld, sel);
-        ld = hd;
-      }
+      if (dd) wd = sread(4u * t);
       if (abc && t == FABC) {  // the first word: the state is 0
         xa = wa, xb = wb, xc = wc;
         if (dd) xd = TP::step(lds, lt, xd, wd);
@@ -848,7 +846,8 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
         if ((pc & 7u) == 0 && more(4u)) P = span_op_x(lds, kOpP4, y, P);
       }
     }
-    P = TP::step(lds, lt, P, 0u);  // F: the chains' last words
+    // F for a last dword of 4 - j record bytes: shift(P, 4 - j bytes) = F(P << 8 j) ^ (P >> 8 (4 - j))
+    P = TP::step(lds, lt, P << (8u * j), (P >> (24u - 8u * j)) >> 8);
     if constexpr (MODE == 18)  // diagnostics: the item's first record, records, lane, lanes, mode
       P = ~(((it.cw >> 16) << 24) | (((it.cw >> 8) & 127u) << 16) | (u << 8) | ((kVar ? pc + ((it.cw >> 4) & 15u) + 1u : k) << 4) | (it.var ? 1u : 0u));
     if (pc == 0 && act)

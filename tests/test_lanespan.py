@@ -153,7 +153,7 @@ def test_mixed_sizes_per_record_lanes(crc, oracle_lib, lo, hi, hint):
 def test_mixed_geometry_items():
     """The per-record item geometry (diagnostics variant 126: first record, records, lane, lanes per
     record) on a batch of 300-B records with two block-end fragments: records on consecutive lane
-    ranges of ceil(words / 27) lanes, at most 64 lanes an item."""
+    ranges of ceil(words / 27) lanes (words: the record's dwords after its first), at most 64 lanes an item."""
     from pebblesdb_amd import crc32c, diag
 
     if not torch.cuda.is_available():
@@ -165,7 +165,9 @@ def test_mixed_geometry_items():
     d = torch.zeros(int(offs[-1] + lens[-1]) + 64, dtype=torch.uint8, device="cuda")
     d_blk = crc32c.blocks_to_device(crc32c.make_blocks(offs, lens))
     geo = diag.batch_desc(126, d, d_blk, flags=crc32c.SIZE_512 | crc32c.SIZE_MIXED).cpu().numpy().view(np.uint32)
-    k = np.minimum(5, ((lens + 3) // 4 + 26) // 27)
+    # the lanes cover a record's dwords after the one holding its first byte (the p-word)
+    words = np.maximum(1, ((offs & 3) + lens + 3) // 4 - 1)
+    k = np.minimum(5, (words + 26) // 27)
     for b in range(40):
         g = geo[64 * b:64 * b + 64]
         if not (g & 1).all():

@@ -30,6 +30,7 @@ for s in "$@"; do
     # the record kernel: 50-step bench lines, parts / distribution A/B, clocks, counters
     bench_wal) for w in wal100 wal400 wal1000 wal; do step bench_$w 300 python bench.py --workload $w --no-copy-inclusive --steps 50 || exit 1; done ;;
     ab_span) step ab_span 600 python tools/ab_span.py 0,63,64,67 wal100,wal400,wal1000,wal 6 ;;
+    ab_vs) step ab_vs 900 python tools/ab_span.py ${AB_VARIANTS:-0,wgl/0} ${AB_WL:-wal100,wal400,wal1000,wal,rand300_500,rand64_1000} ${AB_ROUNDS:-6} ;;
     span_clock) step span_clock 600 python tools/span_clock.py wal100,wal400,wal1000,wal 3 ;;
     counters_span) step counters_span 900 bash tools/counters_span.sh ${TAG}_span wal100 wal400 wal1000 wal ;;
     prof_wal) for w in wal100 wal400 wal1000 wal; do step prof_$w 500 bash tools/profile.sh ${TAG}_prof_$w $w || exit 1; done ;;
