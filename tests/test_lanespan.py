@@ -97,11 +97,13 @@ def test_batch_boundaries(crc, oracle_lib, n):
         _check(crc, oracle_lib, base, offs, lens, hint, verify=n > 20)
 
 
-# k (lanes per record) by length (span_pick): <= 256 B (33-word parts) 1..132 -> 1, 133..256 -> 2;
-# 257..512 B (27-word parts) 257..324 -> 3, 325..448 -> 4, 449..512 -> 5; 513..1023 B (33-word
-# parts) 513..532 -> 4, 533..664 -> 5, 665..796 -> 6, 797..924 -> 7, 925..1023 -> 8
-@pytest.mark.parametrize("length", [1, 3, 4, 5, 17, 131, 132, 133, 255, 256, 257, 300, 431, 512, 513, 600, 700, 850,
-                                    1000, 1023, 1024, 1055, 1056, 1057, 1100, 1151, 1152])
+# k (lanes per record) by length (span_pick; words: the record's dwords after its first, ~ length / 4):
+# <= 256 B (33-word parts) 1..132 -> 1, 133..256 -> 2; 257..512 B (27-word parts) 257..324 -> 3,
+# 325..448 -> 4, 449..512 -> 5; 513..1152 B (33-word parts) ..532 -> 4, ..664 -> 5, ..796 -> 6,
+# ..924 -> 7, beyond -> 8 (past 1056 B the head chain runs on alone)
+@pytest.mark.parametrize("length", [1, 3, 4, 5, 17, 131, 132, 133, 255, 256, 257, 300, 431, 512, 513, 576, 577, 600,
+                                    700, 720, 721, 850, 864, 865, 1000, 1001, 1008, 1009, 1023, 1024, 1055, 1056, 1057,
+                                    1100, 1151, 1152])
 @pytest.mark.parametrize("shift", [0, 1, 3])
 def test_fixed_strides(crc, oracle_lib, length, shift):
     """pdb_crc32c_batch_device_fixed with 1..1152-B blocks (the same kernel, FixedSrc)."""

@@ -1,5 +1,6 @@
 #!/usr/bin/env bash
-# tools/ab_base.sh <git-rev> <name> -- build the diagnostics library of an earlier revision's sources
+# tools/ab_base.sh <git-rev | WORKTREE> <name> -- build the diagnostics library of an earlier revision's
+# sources (or of the working tree as it is now)
 # as pebblesdb_amd/_lib/ab/libpdb_crc32c_diag_<name>.so, for in-process A/B against the working tree
 # (tools/ab_span.py variant tokens "<name>/<id>").  Run here, on the CPU, before the GPU call.
 set -euo pipefail
@@ -7,7 +8,11 @@ rev=$1 name=$2
 root=$(cd "$(dirname "$0")/.." && pwd)
 tmp=$(mktemp -d)
 trap 'rm -rf "$tmp"' EXIT
-git -C "$root" archive "$rev" pebblesdb_amd/csrc include | tar -x -C "$tmp"
+if [ "$rev" = WORKTREE ]; then
+  mkdir -p "$tmp/pebblesdb_amd" && cp -r "$root/pebblesdb_amd/csrc" "$tmp/pebblesdb_amd/" && cp -r "$root/include" "$tmp/"
+else
+  git -C "$root" archive "$rev" pebblesdb_amd/csrc include | tar -x -C "$tmp"
+fi
 mkdir -p "$root/pebblesdb_amd/_lib/ab"
 objs=() pids=()
 for s in diag_variants.hip diag_capi.cpp crc32c_kernels.hip crc32c_tables.cpp; do

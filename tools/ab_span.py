@@ -28,7 +28,8 @@ WL = {"wal100": (131, 1 << 30, crc32c.SIZE_256), "wal400": (431, 2 << 30, crc32c
       "rand32_256": ((32, 256), 1 << 30, crc32c.SIZE_256), "rand1_512": ((1, 512), 2 << 30, crc32c.SIZE_512 | crc32c.SIZE_MIXED),
       "rand1000_1152": ((1000, 1152), 4 << 30, crc32c.SIZE_1K),
       "wal419": (419, 2 << 30, crc32c.SIZE_512), "wal463": (463, 2 << 30, crc32c.SIZE_512),
-      "wal443": (443, 2 << 30, crc32c.SIZE_512)}
+      "wal443": (443, 2 << 30, crc32c.SIZE_512), "wal800": (800, 2 << 30, crc32c.SIZE_1023),
+      "wal900": (900, 2 << 30, crc32c.SIZE_1023)}
 
 
 def layout(payload, nbytes):
