@@ -131,11 +131,14 @@ int pdb_crc32c_verify_device(const void* d_base, const pdb_blk* d_blk, uint64_t 
                              void* stream);
 
 /* ---- pinned host staging -----------------------------------------------------------------------
- * Page-locked host memory for a caller that stages the blocks of host batches (pdb_sst_seal_host,
- * pdb_sst_verify_host, pdb_crc32c_batch_host, ...): spans in it reach the device by DMA, without the
- * runtime's pageable bounce copies (integration/pdb_table_builder.cc stages its sealed batches in
- * it).  Any host memory stays valid for every entry point; this only changes the copy rate.
- * *out = NULL for bytes == 0.  Free with pdb_host_free (NULL is a no-op). */
+ * Page-locked, device-mapped host memory for a caller that stages the blocks of host batches
+ * (integration/pdb_table_builder.cc stages its sealed batches in it).  pdb_sst_seal_host /
+ * pdb_sst_verify_host on a buffer inside one such allocation run zero-copy: the kernel reads the
+ * blocks (and a seal writes the trailers) through the mapping, one launch, no DMA; the other host
+ * entry points DMA from it without the runtime's pageable bounce copies.  Any host memory stays
+ * valid for every entry point; this only changes the rate.  Freed allocations are kept for reuse
+ * (a few), so staging per table does not page-lock anew.  *out = NULL for bytes == 0.  Free with
+ * pdb_host_free (NULL is a no-op; any other pointer not from pdb_host_alloc: PDB_EINVAL). */
 int pdb_host_alloc(uint64_t bytes, void** out);
 int pdb_host_free(void* p);
 

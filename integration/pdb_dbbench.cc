@@ -117,12 +117,18 @@ void Report(const Result& r) {
 #if PDB_HOOKS
   pdb_hook_stats s;
   pdb_hook_stats_get(&s);
+  // seal_copy_inclusive_MiB_s: sealed bytes per second of wall time with a seal in flight (the
+  // flush and compaction threads seal concurrently: seal_s sums the calls' times, overlaps twice);
+  // seal_per_call_MiB_s: sealed bytes / summed call time
   printf(", \"hook\": {\"seal_calls\": %llu, \"seal_blocks\": %llu, \"seal_bytes\": %llu, \"seal_s\": %.4f, "
+         "\"seal_busy_s\": %.4f, \"seal_overlap_max\": %llu, \"seal_per_call_MiB_s\": %.1f, "
          "\"seal_copy_inclusive_MiB_s\": %.1f, \"verify_calls\": %llu, \"verify_bytes\": %llu, \"verify_s\": %.4f, "
          "\"verify_us_per_call\": %.3f, \"verify_failed\": %llu, \"scan_batches\": %llu, \"scan_blocks\": %llu, "
          "\"scan_bytes\": %llu, \"scan_s\": %.4f, \"scan_copy_inclusive_MiB_s\": %.1f}",
          (unsigned long long)s.seal_calls, (unsigned long long)s.seal_blocks, (unsigned long long)s.seal_bytes,
-         s.seal_ns * 1e-9, s.seal_ns ? s.seal_bytes / 1048576.0 / (s.seal_ns * 1e-9) : 0.0,
+         s.seal_ns * 1e-9, s.seal_busy_ns * 1e-9, (unsigned long long)s.seal_overlap,
+         s.seal_ns ? s.seal_bytes / 1048576.0 / (s.seal_ns * 1e-9) : 0.0,
+         s.seal_busy_ns ? s.seal_bytes / 1048576.0 / (s.seal_busy_ns * 1e-9) : 0.0,
          (unsigned long long)s.verify_calls, (unsigned long long)s.verify_bytes, s.verify_ns * 1e-9,
          s.verify_calls ? s.verify_ns * 1e-3 / s.verify_calls : 0.0, (unsigned long long)s.verify_failed,
          (unsigned long long)s.scan_batches, (unsigned long long)s.scan_blocks, (unsigned long long)s.scan_bytes,

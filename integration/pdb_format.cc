@@ -15,6 +15,7 @@
 #include <time.h>
 
 #include <atomic>
+#include <mutex>
 
 #include "pdb_crc32c.h"
 #include "pdb_crc_route.h"
@@ -27,7 +28,11 @@
 
 namespace pdb_hooks {
 namespace {
-std::atomic<uint64_t> g_counters[12];
+constexpr int kCounters = 14;
+std::atomic<uint64_t> g_counters[kCounters];
+std::mutex g_seal_mu;
+int g_seal_active = 0;
+uint64_t g_seal_t0 = 0;
 }
 uint64_t NowNs() {
   timespec ts;
@@ -39,6 +44,16 @@ void AddSeal(uint64_t blocks, uint64_t bytes, uint64_t ns) {
   g_counters[1].fetch_add(blocks, std::memory_order_relaxed);
   g_counters[2].fetch_add(bytes, std::memory_order_relaxed);
   g_counters[3].fetch_add(ns, std::memory_order_relaxed);
+}
+void SealBegin() {
+  std::lock_guard<std::mutex> lk(g_seal_mu);
+  if (g_seal_active++ == 0) g_seal_t0 = NowNs();
+  if (static_cast<uint64_t>(g_seal_active) > g_counters[13].load(std::memory_order_relaxed))
+    g_counters[13].store(static_cast<uint64_t>(g_seal_active), std::memory_order_relaxed);
+}
+void SealEnd() {
+  std::lock_guard<std::mutex> lk(g_seal_mu);
+  if (--g_seal_active == 0) g_counters[12].fetch_add(NowNs() - g_seal_t0, std::memory_order_relaxed);
 }
 void AddScan(uint64_t blocks, uint64_t bytes, uint64_t ns, uint64_t bad) {
   g_counters[8].fetch_add(1, std::memory_order_relaxed);
@@ -57,11 +72,11 @@ void AddVerify(uint64_t bytes, uint64_t ns, bool failed) {
 
 extern "C" void pdb_hook_stats_get(pdb_hook_stats* out) {
   uint64_t* v = reinterpret_cast<uint64_t*>(out);
-  for (int i = 0; i < 12; ++i) v[i] = pdb_hooks::g_counters[i].load(std::memory_order_relaxed);
+  for (int i = 0; i < pdb_hooks::kCounters; ++i) v[i] = pdb_hooks::g_counters[i].load(std::memory_order_relaxed);
 }
 
 extern "C" void pdb_hook_stats_reset(void) {
-  for (int i = 0; i < 12; ++i) pdb_hooks::g_counters[i].store(0, std::memory_order_relaxed);
+  for (int i = 0; i < pdb_hooks::kCounters; ++i) pdb_hooks::g_counters[i].store(0, std::memory_order_relaxed);
 }
 
 namespace leveldb {

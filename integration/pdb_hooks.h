@@ -25,6 +25,8 @@ typedef struct pdb_hook_stats {
   uint64_t scan_blocks;    // data blocks checked in them
   uint64_t scan_bytes;     // bytes read and checked
   uint64_t scan_ns;        // wall time of the window reads + GPU checks
+  uint64_t seal_busy_ns;   // wall time with at least one seal call in flight (builders seal concurrently)
+  uint64_t seal_overlap;   // most seal calls in flight at once
 } pdb_hook_stats;
 
 void pdb_hook_stats_get(pdb_hook_stats* out);
@@ -36,6 +38,9 @@ void pdb_hook_stats_reset(void);
 namespace pdb_hooks {
 // internal: the hooks add to the counters (thread-safe, relaxed atomics)
 void AddSeal(uint64_t blocks, uint64_t bytes, uint64_t ns);
+// around every seal call: the union of the calls' intervals (seal_busy_ns) and their overlap
+void SealBegin();
+void SealEnd();
 void AddVerify(uint64_t bytes, uint64_t ns, bool failed);
 void AddScan(uint64_t blocks, uint64_t bytes, uint64_t ns, uint64_t bad);
 uint64_t NowNs();

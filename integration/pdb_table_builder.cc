@@ -181,9 +181,11 @@ struct TableBuilder::Rep {
     staged.clear();
     staged_handles.clear();
     inflight_rc = std::async(std::launch::async, [this] {
+      pdb_hooks::SealBegin();
       const uint64_t t0 = pdb_hooks::NowNs();
       const int rc = pdb_route::SstSealHost(inflight.data(), inflight.size(), inflight_handles.data(), inflight_handles.size());
       inflight_ns = pdb_hooks::NowNs() - t0;
+      pdb_hooks::SealEnd();
       return rc;
     });
     has_inflight = true;
@@ -195,9 +197,11 @@ struct TableBuilder::Rep {
     WaitInflight();
     if (staged_handles.empty()) return;
     if (status.ok()) {
+      pdb_hooks::SealBegin();
       const uint64_t t0 = pdb_hooks::NowNs();
       const int rc = pdb_route::SstSealHost(staged.data(), staged.size(), staged_handles.data(), staged_handles.size());
       pdb_hooks::AddSeal(staged_handles.size(), staged.size(), pdb_hooks::NowNs() - t0);
+      pdb_hooks::SealEnd();
       if (rc != 0) {
         status = Status::IOError("pdb_sst_seal_host", pdb_route::LastError());
       } else {

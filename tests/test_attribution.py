@@ -42,6 +42,8 @@ def test_buffered_cpu_database_is_the_reference_format(tmp_path, oracle_lib):
     assert rc == 0, out + err
     res = {d["bench"]: d for d in (json.loads(l) for l in out.splitlines() if l.startswith('{"bench"'))}
     assert res["fillrandom"]["hook"]["seal_blocks"] > 0  # the batched (buffered) seals ran
+    h = res["fillrandom"]["hook"]  # the union of the seal calls' intervals is within their sum
+    assert 0 < h["seal_busy_s"] <= h["seal_s"] + 1e-3 and h["seal_overlap_max"] >= 1
     assert res["readseq"]["hook"]["scan_batches"] > 0 and res["readseq"]["hook"]["verify_failed"] == 0
     assert f"({num} of {num} found)" in out
     v = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "verify_db_dir.py"), db],

@@ -98,3 +98,56 @@ def test_verify_and_read_blocks(dev, oracle_lib):
     # truncated read (format.cc:84-87)
     with pytest.raises(T.Corruption, match="truncated block read"):
         T.read_block(img[: hs[-1].offset + 10], hs[-1])
+
+
+@gpu
+def test_pinned_staging_zero_copy_seal_and_verify(dev, oracle_lib):
+    """pdb_sst_seal_host / pdb_sst_verify_host on a buffer from pdb_host_alloc run zero-copy (the
+    kernel reads the blocks and writes the trailers through the device mapping): the sealed image is
+    byte for byte the pageable path's, the verify's ok bytes and bad count agree, a batch that only
+    partly lies in the allocation takes the DMA path, and freed allocations are reused."""
+    import ctypes
+
+    import oracle
+    from pebblesdb_amd import crc32c
+    from pebblesdb_amd._native import check, lib
+
+    rng = np.random.Generator(np.random.PCG64(31))
+    sizes = np.concatenate([rng.integers(4166, 4175, size=900), rng.integers(0, 9000, size=60), [0, 1, 70000]])
+    offs = np.concatenate([[3], 3 + np.cumsum(sizes + 5)[:-1]]).astype(np.int64)
+    total = int(offs[-1] + sizes[-1] + 5) + 11
+    img = oracle.splitmix_bytes(total, 77).copy()
+    img[offs + sizes] = rng.integers(0, 2, size=len(sizes))  # type bytes
+    h = np.zeros(len(sizes), dtype=crc32c.HANDLE_DTYPE)
+    h["offset"], h["size"] = offs, sizes
+    ref = img.copy()
+    check(lib().pdb_sst_seal_host(ref.ctypes.data, total, h.ctypes.data, len(h)))
+    for i in (0, 1, 900, len(h) - 1):  # the pageable path against the oracle
+        body = ref[offs[i] : offs[i] + sizes[i] + 1].tobytes()
+        assert int.from_bytes(ref[offs[i] + sizes[i] + 1 : offs[i] + sizes[i] + 5].tobytes(), "little") == \
+            oracle_lib.mask(oracle_lib.value(body))
+    p = ctypes.c_void_p()
+    check(lib().pdb_host_alloc(total + 64, ctypes.byref(p)))
+    pin = np.ctypeslib.as_array((ctypes.c_uint8 * (total + 64)).from_address(p.value))
+    pin[:total] = img
+    check(lib().pdb_sst_seal_host(p.value, total, h.ctypes.data, len(h)))
+    assert (pin[:total] == ref).all()
+    ok = np.zeros(len(h), dtype=np.uint8)
+    assert lib().pdb_sst_verify_host(p.value, total, h.ctypes.data, len(h), ok.ctypes.data) == 0 and ok.all()
+    pin[offs[5] + 9] ^= 0x10
+    pin[offs[-1] + sizes[-1]] ^= 0x01  # a type byte
+    ok[:] = 1
+    assert lib().pdb_sst_verify_host(p.value, total, h.ctypes.data, len(h), ok.ctypes.data) == 2
+    assert ok.sum() == len(h) - 2 and ok[5] == 0 and ok[-1] == 0
+    # a span reaching past the allocation is still served (by DMA), with the same answer
+    big = np.zeros(total + 4096, dtype=np.uint8)
+    big[:total] = pin[:total]
+    assert lib().pdb_sst_verify_host(big.ctypes.data, total + 4096, h.ctypes.data, len(h), ok.ctypes.data) == 2
+    # a freed allocation comes back for a request of about its size; foreign / double frees are errors
+    check(lib().pdb_host_free(p))
+    q = ctypes.c_void_p()
+    check(lib().pdb_host_alloc(total, ctypes.byref(q)))
+    assert q.value == p.value
+    check(lib().pdb_host_free(q))
+    assert lib().pdb_host_free(q) == -3
+    assert lib().pdb_host_free(ctypes.c_void_p(big.ctypes.data)) == -3

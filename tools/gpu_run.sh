@@ -39,6 +39,7 @@ for s in "$@"; do
     prof_c2) step prof_c2 700 bash tools/profile.sh ${TAG}_prof_c2 c2 ;;
     prof_list) for w in ${PROF_WL:-c2}; do step prof_$w 700 bash tools/profile.sh ${TAG}_prof_$w $w || exit 1; done ;;
     copyinc) step copyinc 600 python tools/copy_inclusive.py ;;
+    sealb) step sealb 300 python tools/seal_batches.py ${SEAL_MIB:-4,16,32} ;;
     ab_sst) step ab_sst 600 python tools/ab_sst.py 0,72 ;;
     # the engine (BASELINE configs 1 / 5, §8(f) row 1)
     vtool) step vtool 900 bash tools/verify_tool_bench.sh ${TAG}_vtool 1000000 ;;

@@ -1,0 +1,105 @@
+#!/usr/bin/env python3
+"""tools/seal_batches.py [MiB,...] -- the engine's seal call (pdb_sst_seal_host) on sstable batches of
+4 / 16 / 32 MiB (the TableBuilder's PDB_SEAL_BATCH_BYTES), against the bare H2D copy of the same
+bytes, from page-locked staging (pdb_host_alloc, what integration/pdb_table_builder.cc stages in) and
+from pageable memory; and the zero-copy form: the device seal kernel run directly on the page-locked
+batch through its device mapping (hipHostGetDevicePointer), the trailers written in place across
+PCIe, no DMA.  Every form's image must equal the host seal's.  One JSON line per batch size."""
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import sst_layout  # noqa: E402
+from pebblesdb_amd import crc32c  # noqa: E402
+from pebblesdb_amd._native import check, lib  # noqa: E402
+
+GIB = float(1 << 30)
+hip = ctypes.CDLL("libamdhip64.so")
+
+
+def pinned(nbytes: int):
+    p = ctypes.c_void_p()
+    check(lib().pdb_host_alloc(nbytes, ctypes.byref(p)))
+    return p.value, np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(p.value))
+
+
+def dev_ptr(host_ptr: int) -> int:
+    d = ctypes.c_void_p()
+    rc = hip.hipHostGetDevicePointer(ctypes.byref(d), ctypes.c_void_p(host_ptr), 0)
+    if rc != 0:
+        raise RuntimeError(f"hipHostGetDevicePointer rc={rc}")
+    return d.value
+
+
+def per_call(fn, reps: int) -> float:
+    fn()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    return (time.perf_counter() - t0) / reps
+
+
+def main():
+    sizes_mib = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "4,16,32").split(",")]
+    crc32c.init_device(0)
+    stream = torch.cuda.Stream()
+    sp = int(stream.cuda_stream)
+    for mib in sizes_mib:
+        nblk = max(1, (mib << 20) // 4175)
+        sizes, offs, total = sst_layout(nblk, 401 + mib)
+        rng = np.random.Generator(np.random.PCG64(mib))
+        img = rng.integers(0, 256, size=total, dtype=np.uint8)
+        img[offs + sizes] = 0  # kNoCompression type bytes
+        h = np.zeros(nblk, dtype=crc32c.HANDLE_DTYPE)
+        h["offset"], h["size"] = offs, sizes
+        ref = img.copy()
+        check(lib().pdb_sst_seal_host(ref.ctypes.data, total, h.ctypes.data, nblk))
+        p_img, pin = pinned(total)
+        p_h, pin_h = pinned(h.nbytes)
+        pin_h[:] = h.view(np.uint8)
+        res = {"batch_MiB": mib, "blocks": nblk, "bytes": total}
+        reps = max(20, 2000 // mib)
+
+        def host_seal(arr):
+            return lambda: check(lib().pdb_sst_seal_host(arr.ctypes.data, total, h.ctypes.data, nblk))
+
+        for name, arr in (("seal_host_pinned", pin), ("seal_host_pageable", img.copy())):
+            arr[:] = img
+            dt = per_call(host_seal(arr), reps)
+            assert (arr == ref).all(), name
+            res[name] = {"us_per_call": round(dt * 1e6, 1), "GiB_s": round(total / dt / GIB, 2)}
+        # zero-copy: the seal kernel reads the batch and writes its trailers through the mapping
+        d_img, d_h = dev_ptr(p_img), dev_ptr(p_h)
+        pin[:] = img
+
+        def zero_copy():
+            check(lib().pdb_sst_seal_device(ctypes.c_void_p(d_img), total, ctypes.c_void_p(d_h), nblk, ctypes.c_void_p(sp)))
+            stream.synchronize()
+
+        dt = per_call(zero_copy, reps)
+        assert (pin == ref).all(), "zero-copy seal differs from the host seal"
+        res["seal_zero_copy"] = {"us_per_call": round(dt * 1e6, 1), "GiB_s": round(total / dt / GIB, 2)}
+        # the bare copy of the same bytes (pinned -> device), the DMA ceiling of the host form
+        d = torch.empty(total, dtype=torch.uint8, device="cuda")
+        src = torch.from_numpy(pin)
+
+        def h2d():
+            with torch.cuda.stream(stream):
+                d.copy_(src, non_blocking=True)
+            stream.synchronize()
+
+        dt = per_call(h2d, reps)
+        res["h2d_pinned"] = {"us_per_call": round(dt * 1e6, 1), "GiB_s": round(total / dt / GIB, 2)}
+        print(json.dumps(res), flush=True)
+        check(lib().pdb_host_free(ctypes.c_void_p(p_img)))
+        check(lib().pdb_host_free(ctypes.c_void_p(p_h)))
+
+
+if __name__ == "__main__":
+    main()
