@@ -37,9 +37,13 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
-    # 40: the first ~20-30 launches of a cold GPU run slower (clock / power settling; see
-    # DESIGN.md §6), so the default warmup covers them
-    ap.add_argument("--warmup", type=int, default=40)
+    # default: 40 for c2 (the first ~20-30 launches of a cold GPU run slower: clock / power
+    # settling); the other workloads warm up for at least --warmup-s seconds of
+    # launches too (their kernels are 0.2-0.8 ms: 40 of them end inside the ~0.15 s power transient).
+    # An explicit --warmup W is exactly W launches (the driver's --warmup 5).
+    ap.add_argument("--warmup", type=int, default=None)
+    ap.add_argument("--warmup-s", type=float, default=0.3,
+                    help="non-c2 workloads without --warmup: warm up until this many seconds have passed")
     ap.add_argument("--settle", type=int, default=300,
                     help="untimed launches after the timed region before the steady-state re-timing (0: skip)")
     ap.add_argument("--workload", default="c2", choices=["c2", "c3", "sstable", "sst_verify", "sst_seal", "sst_crc",
@@ -72,7 +76,11 @@ def parse():
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / rank plumbing only, on the CPU (gloo): no device, no kernel, value null "
                          "(tests/test_shard.py)")
-    return ap.parse_args()
+    args = ap.parse_args()
+    args.warmup_timed = args.warmup is None and args.workload != "c2"
+    if args.warmup is None:
+        args.warmup = 40
+    return args
 
 
 def _free_port() -> int:
@@ -412,9 +420,17 @@ def main():
         algo_bytes = hashed + nblk * (4 + 16)
 
     # ---- warmup + timed region -------------------------------------------------------------
+    warm_t0 = time.perf_counter()
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    if args.warmup_timed:  # (per rank; the barrier below lines the ranks up)
+        while time.perf_counter() - warm_t0 < args.warmup_s:
+            for _ in range(10):
+                step()
+            args.warmup += 10
+            torch.cuda.synchronize()
+    warm_s = time.perf_counter() - warm_t0
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
@@ -520,6 +536,7 @@ def main():
             "world_size": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "warmup_s": round(warm_s, 3),
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
             "scaling": "weak",

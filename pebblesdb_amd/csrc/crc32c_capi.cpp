@@ -832,7 +832,7 @@ int host_sst_mapped(uint8_t* d_buf, uint64_t buf_len, const pdb_block_handle* h,
   HostCtx* st = cl.c;
   hipError_t e = hipSetDevice(dev->device);
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
-  const size_t pin_ok = align_up(n * sizeof(pdb_block_handle), 64);
+  const size_t pin_ok = align_up(n * sizeof(pdb_block_handle), 128);  // (the verify stores 128-B lines of ok bytes)
   if ((rc = ensure_pin(st, pin_ok + align_up(n, 64) + 64))) return rc;
   if (!st->d_pin) return fail(PDB_EHIP, "pinned scratch has no device mapping");
   if ((rc = ensure_ws(st, 256))) return rc;

@@ -851,6 +851,23 @@ struct SinkOps<SstVerifySink> {
     if (k.ok) k.ok[i] = good ? 1 : 0;
     if (!good && k.nbad) atomicAdd(k.nbad, 1u);
   }
+  // the ok byte alone (crc_sst4k_kernel's LDS ring of ok bytes, OkRing below)
+  __device__ static __forceinline__ uint8_t verdict(const SstVerifySink& k, uint32_t raw, const BlkDesc& d, uint32_t stored) {
+    const bool good = d.init_raw != 0 && pdb_unmask(stored) == ~raw;
+    if (!good && k.nbad) atomicAdd(k.nbad, 1u);
+    return good ? 1 : 0;
+  }
+};
+
+// Sinks whose per-block byte crc_sst4k_kernel gathers in an LDS ring of 64-block lines and stores
+// as one 64-lane byte store per line (OkRing): the verify's ok flags.
+template <class Sink>
+struct SinkRing {
+  static constexpr bool kOn = false;
+};
+template <>
+struct SinkRing<SstVerifySink> {
+  static constexpr bool kOn = true;
 };
 
 // Rounds of a block of K 32-B pieces: 128 pieces (4 KiB) per round, and the block's last round
@@ -1659,6 +1676,26 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
   uint32_t* ctr = reinterpret_cast<uint32_t*>(lds + PDB_MAIN_BYTES + 7 * 4096u);
   const uint64_t g_lo = nblk * blockIdx.x / gridDim.x, g_hi = nblk * (blockIdx.x + 1) / gridDim.x;
   if (threadIdx.x == 0) *ctr = kW;  // next kBlk-block group, in groups relative to g_lo
+  // OkRing (SinkRing<Sink>::kOn, the verify's ok bytes): the waves take groups out of order, so a
+  // wave's own ok bytes are 4-B pieces scattered over the array (4.15 MB of partial-line writes per
+  // 1 M blocks for 1.05 MB of flags).  Instead every block's byte goes to a ring of 16 lines of 128
+  // blocks (one 128-B cache line of flags; 64-B lines still cost two write-backs of each 128-B line)
+  // in operator slot 6 (free in this image), each line with a count of its blocks done and the line
+  // that owns its slot; the wave whose count completes a line stores it as ONE 64-lane 2-byte store
+  // (128 contiguous bytes) and hands the slot to line + 16.  A wave whose line's slot still holds line
+  // - 16 waits for it (its blocks are all taken, by waves that never wait on a later line: no cycle).
+  // A deferred (slow-path) block marks its byte 0xFF, which the line store skips: it is stored
+  // directly when hashed.
+  constexpr bool kOkRing = SinkRing<Sink>::kOn && kRows == 4 && kBlk == 4;
+  uint8_t* ok_ring = reinterpret_cast<uint8_t*>(lds + PDB_MAIN_BYTES + 6 * 4096u);
+  uint32_t* ok_cnt = reinterpret_cast<uint32_t*>(lds + PDB_MAIN_BYTES + 6 * 4096u + 2048u);
+  uint32_t* ok_tag = reinterpret_cast<uint32_t*>(lds + PDB_MAIN_BYTES + 6 * 4096u + 2112u);
+  if constexpr (kOkRing) {
+    if (threadIdx.x < 16u) {  // relative lines 0..15 own slots 0..15
+      ok_cnt[threadIdx.x] = 0;
+      ok_tag[threadIdx.x] = threadIdx.x;
+    }
+  }
   const uint32_t u = threadIdx.x & 63u;
   const uint32_t ureg = tabs[PDB_UNSHIFT_OFF + (u & 15u)];
   __syncthreads();
@@ -1732,6 +1769,54 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
         pk_ok[k] = ok;
       }
     ++pk_n;
+  };
+  // the group's ok bytes into the ring (lane u < nv: block grp + u), then the lines they complete
+  // stored (see OkRing above)
+  auto ok_ring_put = [&](uint32_t v, const Grp& G, uint32_t fastbits, uint32_t nv, uint32_t stored) {
+    if constexpr (kOkRing) {
+      // 32-bit, relative to the range: block r = grp - g_lo + u, line Lr = (r + lo7) / 128 (lines
+      // of the flag array's 128-B grid, lo7 = g_lo mod 128), tags hold relative lines
+      const bool mine = u < nv;
+      const uint32_t lo7 = static_cast<uint32_t>(g_lo) & 127u, nrel = static_cast<uint32_t>(g_hi - g_lo);
+      const uint32_t r = static_cast<uint32_t>(grp - g_lo) + u, rl = r + lo7;
+      const uint32_t L = rl >> 7, slot = L & 15u;
+      uint8_t b = 0xFFu;  // deferred: stored by the slow path
+      if (mine && ((fastbits >> u) & 1u)) b = SinkOps<Sink>::verdict(sink, v, G.ld, stored);
+      // wait until every lane's slot belongs to its line
+      while (__builtin_amdgcn_ballot_w64(mine && __hip_atomic_load(ok_tag + slot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != L))
+        __builtin_amdgcn_s_sleep(1);
+      bool done = false;
+      if (mine) {
+        ok_ring[slot * 128u + (rl & 127u)] = b;
+        const uint32_t lb = L << 7;  // (in rl units)
+        const uint32_t want = min(nrel + lo7, lb + 128u) - max(lo7, lb);
+        done = __hip_atomic_fetch_add(ok_cnt + slot, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) + 1u == want;
+      }
+      uint64_t fin = __builtin_amdgcn_ballot_w64(done);
+      while (fin) {  // at most two lines: a group straddles at most one line boundary
+        const uint32_t k = static_cast<uint32_t>(__builtin_ctzll(fin));
+        fin &= fin - 1;
+        const uint32_t Lc = __builtin_amdgcn_readlane(L, k), sc = Lc & 15u;
+        // lane u: blocks 2u, 2u + 1 of the line (rl units; the range is [lo7, nrel + lo7))
+        const uint32_t j = (Lc << 7) + 2u * u;
+        const uint32_t pair = *reinterpret_cast<const uint16_t*>(ok_ring + sc * 128u + 2u * u);
+        const bool v0 = j >= lo7 && j < nrel + lo7 && (pair & 0xFFu) != 0xFFu;
+        const bool v1 = j + 1u >= lo7 && j + 1u < nrel + lo7 && (pair >> 8) != 0xFFu;
+        uint8_t* dst = sink.ok + (g_lo - lo7) + j;
+        if (sink.ok) {
+          if (v0 && v1)
+            *reinterpret_cast<uint16_t*>(dst) = static_cast<uint16_t>(pair);
+          else if (v0)
+            dst[0] = static_cast<uint8_t>(pair);
+          else if (v1)
+            dst[1] = static_cast<uint8_t>(pair >> 8);
+        }
+        if (u == 0) {
+          ok_cnt[sc] = 0;
+          __hip_atomic_store(ok_tag + sc, Lc + 16u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      }
+    }
   };
   auto body_at = [&](const Grp& G, int r) -> uintptr_t {
     return fast(G.n[r]) ? G.p[r] + G.n[r] - kBody : dummy;
@@ -1836,6 +1921,10 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
       for (;;) {
         uint32_t P[kBlk];
         prefix_states(pf, G, P);
+        // what the sink reads for this group (the verify's stored trailers), issued here and used
+        // after the group's four bodies: one such register live, not this group's and the next's
+        // (a second one spilled the 12-wave verify)
+        if constexpr (kOkRing) pre = SinkOps<Sink>::pre(sink, lane_idx(grp), G.ld);
         Grp NG = G;
         uint32_t npre = pre;
         MaskedPiece npf = pf;
@@ -1853,7 +1942,7 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
             NG = finish(nraw);
             issue_body(buf, blast, body_at(NG, 0));
             issue_prefix(npf, NG);
-            npre = SinkOps<Sink>::pre(sink, lane_idx(ngrp), NG.ld);
+            if constexpr (!kOkRing) npre = SinkOps<Sink>::pre(sink, lane_idx(ngrp), NG.ld);
             if (ngrp < g_hi) nngrp = next_group();
             nraw = load_desc(nngrp < g_hi ? nngrp : ngrp);
           }
@@ -1869,6 +1958,8 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
         if constexpr (kDeferF) v = step4x(lds, lt, v, 0u);  // F: the body chains' last words
         if constexpr (kRing != 0)
           park(v, G, fastbits, nv);
+        else if constexpr (kOkRing)
+          ok_ring_put(v, G, fastbits, nv, pre);
         else if (u < nv && ((fastbits >> u) & 1u))
           SinkOps<Sink>::put(sink, grp + u, v, G.ld, pre);
         defer(G, fastbits, nv);

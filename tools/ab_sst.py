@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Interleaved A/B of the sstable hooks (pdb_sst_seal_device / pdb_sst_verify_device) across
 diagnostics-library variants (pdb_diag_sst) on bench.py's sst image (1 M blocks of 4166-4174 B + type + trailer).
-argv[1] = variants (e.g. 0,18).  Prints one JSON object (GB/s of algorithmic bytes, median)."""
+argv[1] = variants (e.g. 0,18; "<name>/<id>" = id in pebblesdb_amd/_lib/ab/libpdb_crc32c_diag_<name>.so, an
+earlier revision built by tools/ab_base.sh).  Prints one JSON object (GB/s of algorithmic bytes, median)."""
+import ctypes
 import json
 import os
 import sys
@@ -15,7 +17,27 @@ from pebblesdb_amd import table as T  # noqa: E402
 from pebblesdb_amd import diag  # noqa: E402
 from pebblesdb_amd._native import lib  # noqa: E402
 
-variants = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "0,18").split(",")]
+variants = (sys.argv[1] if len(sys.argv) > 1 else "0,18").split(",")
+_libs = {}
+
+
+def sst_fn(tok):
+    """(pdb_diag_sst of the token's library, variant id)"""
+    if "/" not in tok:
+        return diag.lib().pdb_diag_sst, int(tok)
+    name, v = tok.split("/")
+    if name not in _libs:
+        L = ctypes.CDLL(os.path.join(os.path.dirname(diag.DIAG_LIB), "ab", f"libpdb_crc32c_diag_{name}.so"))
+        L.pdb_diag_sst.restype, L.pdb_diag_sst.argtypes = diag.SIGNATURES["pdb_diag_sst"]
+        _libs[name] = L
+    return _libs[name].pdb_diag_sst, int(v)
+
+
+def run(tok, seal, ok=None, nbad=None, sp=None):
+    f, v = sst_fn(tok)
+    diag.check(f(v, data.data_ptr(), total, d_h.data_ptr(), nblk, 1 if seal else 0,
+                 ok.data_ptr() if ok is not None else None, nbad.data_ptr() if nbad is not None else None,
+                 sp if sp is not None else int(torch.cuda.current_stream().cuda_stream)))
 nblk = 1 << 20
 crc32c.init_device(0)
 rng = np.random.Generator(np.random.PCG64(301))
@@ -35,19 +57,19 @@ for _ in range(20):
 res = {"seal": {}, "verify": {}}
 times = {(m, v): [] for m in res for v in variants}
 for v in variants:  # every variant seals the same bytes and verifies them all
-    diag.sst(v, data, d_h, seal=True)
-    ok = torch.empty(nblk, dtype=torch.uint8, device="cuda")
+    run(v, True)
+    ok = torch.zeros(nblk, dtype=torch.uint8, device="cuda")
     nbad = torch.zeros(1, dtype=torch.int32, device="cuda")
-    diag.sst(v, data, d_h, seal=False, ok=ok, nbad=nbad)
+    run(v, False, ok, nbad)
     torch.cuda.synchronize()
-    assert torch.equal(data, ref) and (int(nbad.item()) == 0 or v >= 90), v  # >= 90: wrong by design
+    vid = int(v.split("/")[-1])
+    assert torch.equal(data, ref) and ((int(nbad.item()) == 0 and bool(ok.all())) or vid >= 90), v  # >= 90: wrong by design
 ok = torch.empty(nblk, dtype=torch.uint8, device="cuda")
 nbad = torch.zeros(1, dtype=torch.int32, device="cuda")
 sp = int(torch.cuda.current_stream().cuda_stream)
 # past the power manager's cold transient (~40 launches) before anything is timed
 for _ in range(60):
-    diag.lib().pdb_diag_sst(variants[0], data.data_ptr(), total, d_h.data_ptr(), nblk, 0, ok.data_ptr(),
-                            nbad.data_ptr(), sp)
+    run(variants[0], False, ok, nbad, sp)
 torch.cuda.synchronize()
 for _ in range(8):
     for v in variants:
@@ -56,10 +78,9 @@ for _ in range(8):
             e0.record()
             for _ in range(3):
                 if m == "seal":
-                    diag.lib().pdb_diag_sst(v, data.data_ptr(), total, d_h.data_ptr(), nblk, 1, None, None, sp)
+                    run(v, True, sp=sp)
                 else:
-                    diag.lib().pdb_diag_sst(v, data.data_ptr(), total, d_h.data_ptr(), nblk, 0, ok.data_ptr(),
-                                            nbad.data_ptr(), sp)
+                    run(v, False, ok, nbad, sp)
             e1.record()
             torch.cuda.synchronize()
             times[(m, v)].append(e0.elapsed_time(e1) / 3)
