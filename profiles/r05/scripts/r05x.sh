@@ -1,0 +1,8 @@
+# round 5: the engine's seal kernels under rocprofv3 --kernel-trace (GPU time per seal vs the call's time)
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/r05x; mkdir -p $O
+DB=/tmp/pdb_r05x_$$; mkdir -p $DB; trap 'rm -rf $DB' EXIT
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d $O/prof -- integration/_build/pdb_dbbench_gpu_table \
+  --benchmarks=fillrandom --num=10000000 --value_size=1024 --db=$DB/x > $O/fill.log 2>&1 || exit 1
+grep -a '^{' $O/fill.log | cut -c1-500

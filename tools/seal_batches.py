@@ -4,7 +4,10 @@
 bytes, from page-locked staging (pdb_host_alloc, what integration/pdb_table_builder.cc stages in) and
 from pageable memory; and the zero-copy form: the device seal kernel run directly on the page-locked
 batch through its device mapping (hipHostGetDevicePointer), the trailers written in place across
-PCIe, no DMA.  Every form's image must equal the host seal's.  One JSON line per batch size."""
+PCIe, no DMA.  Also the conditions of the engine's seals: the batch freshly written by the CPU,
+8 batches in rotation, a new allocation per batch, 1 / 5 / 20 ms of idle GPU between seals.  argv[2]:
+run on that NUMA node's CPUs.  Every form's image must equal the host seal's.  One JSON line per
+batch size."""
 import ctypes
 import json
 import os
@@ -45,9 +48,21 @@ def per_call(fn, reps: int) -> float:
     return (time.perf_counter() - t0) / reps
 
 
+def node_cpus(node: int):
+    out = set()
+    for part in open(f"/sys/devices/system/node/node{node}/cpulist").read().strip().split(","):
+        lo, _, hi = part.partition("-")
+        out.update(range(int(lo), int(hi or lo) + 1))
+    return out
+
+
 def main():
     sizes_mib = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "4,16,32").split(",")]
+    node = int(sys.argv[2]) if len(sys.argv) > 2 else -1  # run (and page-lock) on this NUMA node's CPUs
+    if node >= 0:
+        os.sched_setaffinity(0, node_cpus(node) & os.sched_getaffinity(0) or node_cpus(node))
     crc32c.init_device(0)
+    bus = torch.cuda.get_device_properties(0).pci_bus_id if hasattr(torch.cuda.get_device_properties(0), "pci_bus_id") else -1
     stream = torch.cuda.Stream()
     sp = int(stream.cuda_stream)
     for mib in sizes_mib:
@@ -63,7 +78,7 @@ def main():
         p_img, pin = pinned(total)
         p_h, pin_h = pinned(h.nbytes)
         pin_h[:] = h.view(np.uint8)
-        res = {"batch_MiB": mib, "blocks": nblk, "bytes": total}
+        res = {"batch_MiB": mib, "blocks": nblk, "bytes": total, "cpu_node": node, "gpu_pci_bus": bus}
         reps = max(20, 2000 // mib)
 
         def host_seal(arr):
@@ -85,6 +100,54 @@ def main():
         dt = per_call(zero_copy, reps)
         assert (pin == ref).all(), "zero-copy seal differs from the host seal"
         res["seal_zero_copy"] = {"us_per_call": round(dt * 1e6, 1), "GiB_s": round(total / dt / GIB, 2)}
+        # the engine's case: the batch was just written by the CPU (its lines dirty in the CPU caches)
+        tot = 0.0
+        for _ in range(reps):
+            pin[:] = img
+            t0 = time.perf_counter()
+            zero_copy()
+            tot += time.perf_counter() - t0
+        assert (pin == ref).all()
+        res["seal_zero_copy_fresh"] = {"us_per_call": round(tot / reps * 1e6, 1), "GiB_s": round(total * reps / tot / GIB, 2)}
+        tot = 0.0
+        for _ in range(reps):
+            pin[:] = img
+            t0 = time.perf_counter()
+            check(lib().pdb_sst_seal_host(pin.ctypes.data, total, h.ctypes.data, nblk))
+            tot += time.perf_counter() - t0
+        res["seal_host_pinned_fresh"] = {"us_per_call": round(tot / reps * 1e6, 1), "GiB_s": round(total * reps / tot / GIB, 2)}
+        # rotating over 8 page-locked batches (a builder per table, the allocations kept for reuse)
+        bufs = [pinned(total) for _ in range(8)]
+        for _, b_ in bufs:
+            b_[:] = img
+        tot = 0.0
+        for k in range(reps):
+            p_, b_ = bufs[k % 8]
+            b_[:] = img
+            t0 = time.perf_counter()
+            check(lib().pdb_sst_seal_host(p_, total, h.ctypes.data, nblk))
+            tot += time.perf_counter() - t0
+        res["seal_host_pinned_rot8"] = {"us_per_call": round(tot / reps * 1e6, 1), "GiB_s": round(total * reps / tot / GIB, 2)}
+        # the engine's cadence: one seal every few milliseconds, the GPU idle in between
+        for gap_ms in (1, 5, 20):
+            tot = 0.0
+            for k in range(min(reps, 40)):
+                time.sleep(gap_ms * 1e-3)
+                t0 = time.perf_counter()
+                check(lib().pdb_sst_seal_host(p_img, total, h.ctypes.data, nblk))
+                tot += time.perf_counter() - t0
+            res[f"seal_host_pinned_gap{gap_ms}ms"] = {"us_per_call": round(tot / min(reps, 40) * 1e6, 1),
+                                                     "GiB_s": round(total * min(reps, 40) / tot / GIB, 2)}
+        # a new page-locked allocation per batch
+        tot = 0.0
+        for k in range(min(reps, 20)):
+            p_, b_ = pinned(total + 4096 * (k + 1))  # (never a kept allocation)
+            b_[:total] = img
+            t0 = time.perf_counter()
+            check(lib().pdb_sst_seal_host(p_, total, h.ctypes.data, nblk))
+            tot += time.perf_counter() - t0
+        res["seal_host_pinned_new"] = {"us_per_call": round(tot / min(reps, 20) * 1e6, 1),
+                                       "GiB_s": round(total * min(reps, 20) / tot / GIB, 2)}
         # the bare copy of the same bytes (pinned -> device), the DMA ceiling of the host form
         d = torch.empty(total, dtype=torch.uint8, device="cuda")
         src = torch.from_numpy(pin)
