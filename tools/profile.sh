@@ -11,7 +11,7 @@ TAG="${1:-prof}"
 WL="${2:-c2}"
 OUT="gpurun_out/${TAG}"
 mkdir -p "$OUT"
-ARGS="bench.py --workload $WL --no-cpu-baseline --no-copy-inclusive --diag"
+ARGS="bench.py --workload $WL --no-cpu-baseline --no-copy-inclusive --no-c4-shard --diag"
 run() {  # run <name> <rocprof args...>
   local name=$1; shift
   echo "== $name"
