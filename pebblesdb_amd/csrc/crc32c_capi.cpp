@@ -563,7 +563,7 @@ static bool mixed_lengths(const pdb_blk* blk, uint64_t nblk, uint32_t cls) {
 }
 
 // Records of <= 256 B: the 256 class hashes 33-word parts (k = 1..2 lanes a record, 9 steps an
-// item, 10 waves x 9-KiB regions), the 512 class 27-word parts (k = 1..5, 8 steps, 12 waves x 8 KiB).
+// item, 11 waves x 8928-B regions), the 512 class 27-word parts (k = 1..5, 8 steps, 12 waves x 8 KiB).
 // Records of 133..216 B need two parts in either and the 512 class then runs faster (+17 % on random
 // 1-200-B records, tools/ab_hints.py); up to 132 B the 256 class takes one lane a record (wal100),
 // past 216 B the 512 class needs three.  A per-batch item count of both decides.
@@ -583,9 +583,9 @@ static bool small_records_prefer_512(const pdb_blk* blk, uint64_t nblk) {
     if (!n) continue;
     const uint64_t span = hi - lo;
     const uint32_t k256 = nw <= 33u ? 1u : 2u, k512 = (nw + 26u) / 27u;
-    const uint64_t i256 = std::max<uint64_t>((n + 64u / k256 - 1u) / (64u / k256), (span + 9199u) / 9200u);
+    const uint64_t i256 = std::max<uint64_t>((n + 64u / k256 - 1u) / (64u / k256), (span + 8911u) / 8912u);
     const uint64_t i512 = std::max<uint64_t>((n + 64u / k512 - 1u) / (64u / k512), (span + 8175u) / 8176u);
-    c256 += static_cast<double>(i256) * (9 + 4) / 10.0;  // items x (steps + 4) / waves
+    c256 += static_cast<double>(i256) * (9 + 4) / 11.0;  // items x (steps + 4) / waves
     c512 += static_cast<double>(i512) * (8 + 4) / 12.0;
   }
   return c512 < 0.95 * c256;

@@ -9,7 +9,7 @@
 // instruction 1 KiB contiguous), written to the wave's LDS region, and every lane then reads its
 // own record from LDS.
 //
-// LDS image (154 of 160 KiB, one 640-thread workgroup = 10 waves per CU):
+// LDS image (160 KiB, one 704-thread workgroup = 11 waves per CU, for the <= 256-B class):
 //   [0, 64 KiB)      256 entry blocks of 256 B, block b at b << 8 (v_perm puts a state byte in
 //                    address bits 8..15 in one instruction):
 //                    [0, 128)    T0..T3 x 8 replicas: T_k replica r at dword k * 8 + r, bank
@@ -22,15 +22,16 @@
 //                                32 + (((b >> 2) ^ (4 s + j)) & 31): scrambled by b so a lookup's
 //                                lanes spread over the banks, and the address is one v_perm
 //                                ([b, b, 0, 0]) and one v_bitop3 ((x & 0xFF7C) ^ const) away.
-//   [64, 154 KiB)    10 x 9 KiB: one staging region per wave (64 records of a 100-B-value log, 138 B
+//   [64, 160 KiB)    11 x 8928 B: one staging region per wave (64 records of a 100-B-value log, 138 B
 //                    each with their headers, fit one)
 // A wave handles batches of 64 consecutive records; their records are hashed by items (runs of
 // consecutive records whose span fits a region, each record on k lanes: see "items" below).  The
-// next item's loads are in flight while one is hashed.  Per lane, a record part is END-aligned on a
-// grid of 4-byte words built by one v_perm from two LDS dwords and hashed as four interleaved
-// slice-by-4 chains; the word holding the record's first byte p is masked below p and injects U[z]
-// (z masked bytes: the state entering the record is Value()'s 0xFFFFFFFF), and it REPLACES the
-// state of its chain, so no word before it needs masking.  Records outside the class (0 B, > MAXN)
+// next item's loads are in flight while one is hashed.  Per lane, a record part is a run of the
+// region's dwords counted from the record's last one (whose bytes past the record are masked; the
+// finishing step then shifts by the record bytes it holds) and hashed as four interleaved slice-by-4
+// chains; the dword holding the record's first byte p is masked below p and injects U[z] (z masked
+// bytes: the state entering the record is Value()'s 0xFFFFFFFF), and it REPLACES the state of its
+// chain, so no word before it needs masking.  Records outside the class (0 B, > MAXN)
 // are hashed by the whole wave when their batch is opened (slow path: global loads, the same
 // operators; rare, so their loads may wait behind the item in flight).
 #pragma once
@@ -42,23 +43,27 @@ namespace {
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 constexpr uint32_t kSpanStageBase = 64u << 10;                    // tables and operators below
-// staging geometry per class: waves per CU and 1-KiB chunks per region (10 x 9 KiB for <= 256-B
-// records: 64 records of a 100-B-value log fit a region; 12 x 8 KiB for the longer classes, whose
-// items hold 8..21 records on 3..8 lanes each -- more waves hide more of the hash's latency)
+// staging geometry per class: waves per CU, 1-KiB load chunks per item and the region size (11 x
+// 8928 B for <= 256-B records: 64 records of a 100-B-value log, 8832 B, fit a region, whose last
+// chunk is staged by its first 46 lanes only; 12 x 8 KiB for the longer classes, whose items hold
+// 8..21 records on 3..8 lanes each -- more waves hide more of the hash's latency)
 //
 // and the part geometry (see "items" below): chains A, B, C of kLC = 8 words and chain D of kLD
 // words, kPart = 3 kLC + kLD words per lane.  33-word parts (kLD = 9) for <= 256 B (a 131-B record
 // on one lane) and 513..1023 B (up to 8 lanes); 27-word parts (kLD = 3) for 257..512 B, where 4
 // lanes of 27 words cover a 431-B record exactly instead of 4 x 33 = 132 words for its 108.
-// The 1024..1152-B class takes 10 x 9 KiB too: eight 1062-B records (1055-B fragments + headers)
+// The 1024..1152-B class takes 11 x 8928 B too: eight 1062-B records (1055-B fragments + headers)
 // do not fit 8 KiB, so 8-KiB items held 7 records on 56 of the 64 lanes (+2.5 % with 9 KiB,
-// −4..−9 % for the 512 and 1023 classes, whose 8 records fit 8 KiB; profiles/r03_wide/).
+// −4..−9 % for the 512 and 1023 classes, whose 8 records fit 8 KiB; profiles/r03_wide/).  11 waves
+// of 8928 B instead of 10 of 9 KiB (round 5): profiles/r05/ab/ab_11waves.log.
 template <uint32_t MAXN>
 struct SpanStage {
   static constexpr bool k9 = MAXN <= 256u || MAXN > 1023u;
-  static constexpr uint32_t kWaves = k9 ? 10u : 12u;
+  static constexpr uint32_t kWaves = k9 ? 11u : 12u;
   static constexpr uint32_t kJ = k9 ? 9u : 8u;
-  static constexpr uint32_t kRegion = kJ * 1024u;
+  static constexpr uint32_t kRegion = k9 ? 8928u : 8192u;  // (a multiple of 16 B)
+  static constexpr uint32_t kLastLanes = (kRegion - 1024u * (kJ - 1u)) / 16u;  // lanes staging the last chunk
+  static_assert(kRegion % 16u == 0 && kLastLanes >= 1u && kLastLanes <= 64u, "the last chunk ends the region");
   static constexpr uint32_t kUsable = kRegion - 16u;  // span limit: reads stay inside
   static_assert((64u << 10) + kWaves * kRegion <= PDB_LDS_BYTES, "fits the 160 KiB");
   static constexpr uint32_t kLC = 8;                                // words of chains A, B, C (the 32-B folds)
@@ -698,8 +703,11 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
 #pragma unroll
     for (uint32_t j = 0; j + 1 < kSpanJ; ++j)
       if (j == 0 || 1024u * j < nw) *reinterpret_cast<u32x4*>(region + 1024u * j + 16u * u) = A[j];
+    // the last chunk: its lanes that fall inside the region (all of them for 8-KiB regions), but not
+    // the last 16 B of the last region, which hold the counter
+    constexpr uint32_t kLast = SpanStage<MAXN>::kLastLanes;
     if (1024u * (kSpanJ - 1u) < nw)
-      if (!kDyn || wv + 1u < kSpanWaves || u != 63u)  // the last 16 B of the LDS hold the counter
+      if (u < kLast && (!kDyn || wv + 1u < kSpanWaves || u != kLast - 1u))
         *reinterpret_cast<u32x4*>(region + 1024u * (kSpanJ - 1u) + 16u * u) = A[kSpanJ - 1u];
   };
   // hash an item staged in the region
