@@ -1,3 +1,3 @@
-# round 5 final library: GPU suite, smoke, the driver's bench line, every row's 50-step line, C2's rocprof
+# round 5 final library: GPU suite, smoke, the driver's bench line, every row's 50-step line
 set -o pipefail
-bash tools/gpu_run.sh r05q tests smoke bench_driver bench_rows prof_c2
+bash tools/gpu_run.sh r05q tests smoke bench_driver bench_rows
