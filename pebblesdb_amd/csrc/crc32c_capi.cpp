@@ -881,7 +881,14 @@ int host_sst(uint8_t* buf, uint64_t buf_len, const pdb_block_handle* h, uint64_t
     }
   }
   groups.push_back(g);
-  if (uint8_t* d_buf = pin_mapping(buf, buf_len)) return host_sst_mapped(d_buf, buf_len, h, n, seal, ok, nbad_out);
+  // PDB_HOST_MAPPED=0 (read once per process): pinned buffers take the DMA route below as well
+  // (experiments: the engine's seals by DMA against zero-copy, profiles/r05/engine/)
+  static const bool mapped = [] {
+    const char* e = getenv("PDB_HOST_MAPPED");
+    return !(e && e[0] == '0');
+  }();
+  if (mapped)
+    if (uint8_t* d_buf = pin_mapping(buf, buf_len)) return host_sst_mapped(d_buf, buf_len, h, n, seal, ok, nbad_out);
   size_t need = 0;
   uint64_t max_count = 0;
   for (const auto& x : groups) {

@@ -700,6 +700,13 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
   static_assert(64u >= 8u, "the staged margin covers the hash's read window past hi");
   auto to_lds = [&](const u32x4 (&A)[kSpanJ], const SpanItem& it) {
     const uint32_t nw = __builtin_amdgcn_readfirstlane(it.hi) + 64u;
+    if constexpr (MODE == 47) {  // pricing: one store of the chunks' XOR (wrong CRCs by design)
+      u32x4 x = A[0];
+#pragma unroll
+      for (uint32_t j = 1; j < kSpanJ; ++j) x ^= A[j];
+      *reinterpret_cast<u32x4*>(region + 16u * u) = x;
+      return;
+    }
 #pragma unroll
     for (uint32_t j = 0; j + 1 < kSpanJ; ++j)
       if (j == 0 || 1024u * j < nw) *reinterpret_cast<u32x4*>(region + 1024u * j + 16u * u) = A[j];
@@ -819,9 +826,19 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
     const uint32_t cc = T + static_cast<int32_t>(2u * LC) < L ? xc : 0u;
     const uint32_t cd = T + static_cast<int32_t>(3u * LC) < L ? xd : 0u;
     static_assert(LC == 8, "the in-part folds use the 32- and 64-B operators");
-    const uint32_t lo2 = span_op_x(lds, kOp32, cb, ca);  // S32(B) ^ A
-    const uint32_t hi2 = span_op_x(lds, kOp32, cd, cc);  // S32(D) ^ C
-    uint32_t P = span_op_x(lds, kOp64, hi2, lo2);        // S64(hi2) ^ lo2
+    // (diagnostics, wrong CRCs by design: MODE 43 prices the folds' operator lookups as free, MODE 44
+    // as 8 conflict-free lookups each, MODE 45 with no dependence between them (each indexed by
+    // chain states, `alt`), MODE 46 the cross-lane operators alone as free)
+    auto fold_op = [&](uint32_t slot, uint32_t c, uint32_t y, uint32_t alt) -> uint32_t {
+      if constexpr (MODE == 43) return c ^ y;
+      if constexpr (MODE == 44) return TP::step(lds, lt, TP::step(lds, lt, c, 0u), y);
+      if constexpr (MODE == 45) return span_op_x(lds, slot, alt, y ^ c);
+      if constexpr (MODE == 46) if (slot != kOp32 && slot != kOp64) return c ^ y;
+      return span_op_x(lds, slot, c, y);
+    };
+    const uint32_t lo2 = fold_op(kOp32, cb, ca, cb);  // S32(B) ^ A
+    const uint32_t hi2 = fold_op(kOp32, cd, cc, cd);  // S32(D) ^ C
+    uint32_t P = fold_op(kOp64, hi2, lo2, ca ^ cc);  // S64(hi2) ^ lo2
     if (k > 1u) {
       // the cross-lane fold, pre-shifted per lane: lane c applies shift(R_c, 4 PART (c mod 4)) (slots
       // P1, P2, P3 chosen per lane), the record's quad XOR-reduces, and a record of > 4 parts adds
@@ -832,13 +849,18 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
       const bool dpp = (k & (k - 1u)) == 0 && !(kVar && it.var);
       const uint32_t l = pc & 3u;
       const uint32_t slot = l == 1u ? kOpP1 : (l == 2u ? kOpP2 : kOpP3);
-      uint32_t v[4];
+      uint32_t Ps;
+      if constexpr (MODE >= 43 && MODE <= 46) {
+        Ps = fold_op(slot, P, 0u, cb ^ cc);
+      } else {
+        uint32_t v[4];
 #pragma unroll
-      for (uint32_t j = 0; j < 4; ++j) {
-        const uint32_t bb = __builtin_amdgcn_perm(0u, P, 0x0C0C0000u | (j << 8) | j);
-        v[j] = lds_u32(lds, (bb & 0xFF7Cu) ^ (128u | ((4u * slot + j) << 2)));
+        for (uint32_t j = 0; j < 4; ++j) {
+          const uint32_t bb = __builtin_amdgcn_perm(0u, P, 0x0C0C0000u | (j << 8) | j);
+          v[j] = lds_u32(lds, (bb & 0xFF7Cu) ^ (128u | ((4u * slot + j) << 2)));
+        }
+        Ps = xor3(xor3(v[0], v[1], v[2]), v[3], 0u);
       }
-      const uint32_t Ps = xor3(xor3(v[0], v[1], v[2]), v[3], 0u);
       P = l ? Ps : P;
       uint32_t y = dpp ? static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(P), 0x101, 0xF, 0xF, false))
                        : __shfl_down(P, 1, 64);
@@ -851,7 +873,7 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
       if (k > 4u) {
         y = dpp ? static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(P), 0x104, 0xF, 0xF, false))
                 : __shfl_down(P, 4, 64);
-        if ((pc & 7u) == 0 && more(4u)) P = span_op_x(lds, kOpP4, y, P);
+        if ((pc & 7u) == 0 && more(4u)) P = fold_op(kOpP4, y, P, ca ^ cd);
       }
     }
     // F for a last dword of 4 - j record bytes: shift(P, 4 - j bytes) = F(P << 8 j) ^ (P >> 8 (4 - j))

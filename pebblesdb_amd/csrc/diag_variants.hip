@@ -223,6 +223,16 @@ hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tab
       return launch_lanespan<DescSrc, OutSink, 2>(g, d_tables, src, nblk, record_class(flags), sink, s, mixed);
     case 67:  // the bookkeeping alone (no loads, no hash)
       return launch_lanespan<DescSrc, OutSink, 3>(g, d_tables, src, nblk, record_class(flags), sink, s, mixed);
+    case 127:  // pricing: the hash's fold operators as plain XORs (no lookups)
+      return launch_lanespan<DescSrc, OutSink, 43>(g, d_tables, src, nblk, record_class(flags), sink, s, mixed);
+    case 128:  // pricing: each fold operator as 8 conflict-free table lookups
+      return launch_lanespan<DescSrc, OutSink, 44>(g, d_tables, src, nblk, record_class(flags), sink, s, mixed);
+    case 129:  // pricing: the fold operators' lookups with no dependence between them
+      return launch_lanespan<DescSrc, OutSink, 45>(g, d_tables, src, nblk, record_class(flags), sink, s, mixed);
+    case 130:  // pricing: the cross-lane fold operators as plain XORs
+      return launch_lanespan<DescSrc, OutSink, 46>(g, d_tables, src, nblk, record_class(flags), sink, s, mixed);
+    case 131:  // pricing: the staging stores as one 16-B store per lane and item
+      return launch_lanespan<DescSrc, OutSink, 47>(g, d_tables, src, nblk, record_class(flags), sink, s, mixed);
     case 125:  // exact: the batch-uniform k only (no per-record lanes for mixed sizes)
       return launch_lanespan<DescSrc, OutSink, 17>(g, d_tables, src, nblk, record_class(flags), sink, s, mixed);
     case 126:  // the item geometry per record instead of its CRC (MODE 18; tests/test_lanespan.py)
