@@ -780,15 +780,33 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
     // The chains' words: one ds_read_b32 per word and chain.  (Aligned ds_read_b64 pairs measured
     // 2.5-9 % slower on every WAL row, profiles/r04/ab_pairs.log: the extra live pair registers and
     // selects.)
+    // (diagnostics, wrong CRCs by design: MODE 48 prices the chains' words as 16-B reads, one per
+    // four words of a chain, at the 16-B-aligned addresses below them)
+    const uint32_t qo16 = qo & ~15u;
+    u32x4 qa4{}, qb4{}, qc4{}, qd4{};
+    auto sread4 = [&](uint32_t off) -> u32x4 { return *reinterpret_cast<const u32x4*>(lds + qo16 + off); };
 #pragma unroll
     for (int32_t t = 0; t < static_cast<int32_t>(NI); ++t) {
       const bool abc = t >= FABC, dd = t >= FD;  // compile time
       uint32_t wa = 0, wb = 0, wc = 0, wd = 0;
-      if (abc) {
-        wa = sread(12u * LC + 4u * t), wb = sread(8u * LC + 4u * t), wc = sread(4u * LC + 4u * t);
-        if (t == static_cast<int32_t>(NI) - 1) wa &= lastm;
+      if constexpr (MODE == 48) {
+        if (abc) {
+          const uint32_t r = static_cast<uint32_t>(t - FABC);
+          if ((r & 3u) == 0) qa4 = sread4(12u * LC + 4u * r), qb4 = sread4(8u * LC + 4u * r), qc4 = sread4(4u * LC + 4u * r);
+          wa = qa4[r & 3u], wb = qb4[r & 3u], wc = qc4[r & 3u];
+        }
+        if (dd) {
+          const uint32_t r = static_cast<uint32_t>(t - FD);
+          if ((r & 3u) == 0) qd4 = sread4(4u * r);
+          wd = qd4[r & 3u];
+        }
+      } else {
+        if (abc) {
+          wa = sread(12u * LC + 4u * t), wb = sread(8u * LC + 4u * t), wc = sread(4u * LC + 4u * t);
+          if (t == static_cast<int32_t>(NI) - 1) wa &= lastm;
+        }
+        if (dd) wd = sread(4u * t);
       }
-      if (dd) wd = sread(4u * t);
       if (abc && t == FABC) {  // the first word: the state is 0
         xa = wa, xb = wb, xc = wc;
         if (dd) xd = TP::step(lds, lt, xd, wd);

@@ -233,6 +233,8 @@ hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tab
       return launch_lanespan<DescSrc, OutSink, 46>(g, d_tables, src, nblk, record_class(flags), sink, s, mixed);
     case 131:  // pricing: the staging stores as one 16-B store per lane and item
       return launch_lanespan<DescSrc, OutSink, 47>(g, d_tables, src, nblk, record_class(flags), sink, s, mixed);
+    case 132:  // pricing: the chains' words as 16-B LDS reads
+      return launch_lanespan<DescSrc, OutSink, 48>(g, d_tables, src, nblk, record_class(flags), sink, s, mixed);
     case 125:  // exact: the batch-uniform k only (no per-record lanes for mixed sizes)
       return launch_lanespan<DescSrc, OutSink, 17>(g, d_tables, src, nblk, record_class(flags), sink, s, mixed);
     case 126:  // the item geometry per record instead of its CRC (MODE 18; tests/test_lanespan.py)

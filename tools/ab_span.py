@@ -39,7 +39,7 @@ def layout(payload, nbytes):
         offs = np.concatenate([[0], np.cumsum(lens + 7)[:-1]]) + 6
         return offs.astype(np.int64), lens.astype(np.int64)
     return wal_layout(nbytes, payload)
-PRICING = {63, 64, 67, 113, 114, 115, 116, 117, 127, 128, 129, 130, 131}
+PRICING = {63, 64, 67, 113, 114, 115, 116, 117, 127, 128, 129, 130, 131, 132}
 _ALT = {}
 
 
