@@ -133,6 +133,15 @@ void Report(const Result& r) {
          s.verify_calls ? s.verify_ns * 1e-3 / s.verify_calls : 0.0, (unsigned long long)s.verify_failed,
          (unsigned long long)s.scan_batches, (unsigned long long)s.scan_blocks, (unsigned long long)s.scan_bytes,
          s.scan_ns * 1e-9, s.scan_ns ? s.scan_bytes / 1048576.0 / (s.scan_ns * 1e-9) : 0.0);
+  // the seal calls by batch size: calls, mean MiB, MiB/s per call (bytes / summed call time)
+  static const char* kSizeLabel[5] = {"<1", "1-4", "4-8", "8-15", ">=15"};
+  printf(", \"seal_by_batch_MiB\": {");
+  for (int b = 0; b < 5; ++b)
+    printf("%s\"%s\": {\"calls\": %llu, \"mean_MiB\": %.2f, \"MiB_s\": %.1f}", b ? ", " : "", kSizeLabel[b],
+           (unsigned long long)s.seal_size_calls[b],
+           s.seal_size_calls[b] ? s.seal_size_bytes[b] / 1048576.0 / s.seal_size_calls[b] : 0.0,
+           s.seal_size_ns[b] ? s.seal_size_bytes[b] / 1048576.0 / (s.seal_size_ns[b] * 1e-9) : 0.0);
+  printf("}");
   pdb_hook_stats_reset();
 #endif
   printf("}\n");

@@ -28,7 +28,7 @@
 
 namespace pdb_hooks {
 namespace {
-constexpr int kCounters = 14;
+constexpr int kCounters = 29;
 std::atomic<uint64_t> g_counters[kCounters];
 std::mutex g_seal_mu;
 int g_seal_active = 0;
@@ -44,6 +44,11 @@ void AddSeal(uint64_t blocks, uint64_t bytes, uint64_t ns) {
   g_counters[1].fetch_add(blocks, std::memory_order_relaxed);
   g_counters[2].fetch_add(bytes, std::memory_order_relaxed);
   g_counters[3].fetch_add(ns, std::memory_order_relaxed);
+  const uint64_t mib = bytes >> 20;
+  const int b = mib < 1 ? 0 : (mib < 4 ? 1 : (mib < 8 ? 2 : (mib < 15 ? 3 : 4)));
+  g_counters[14 + b].fetch_add(1, std::memory_order_relaxed);
+  g_counters[19 + b].fetch_add(bytes, std::memory_order_relaxed);
+  g_counters[24 + b].fetch_add(ns, std::memory_order_relaxed);
 }
 void SealBegin() {
   std::lock_guard<std::mutex> lk(g_seal_mu);

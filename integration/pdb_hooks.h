@@ -27,6 +27,10 @@ typedef struct pdb_hook_stats {
   uint64_t scan_ns;        // wall time of the window reads + GPU checks
   uint64_t seal_busy_ns;   // wall time with at least one seal call in flight (builders seal concurrently)
   uint64_t seal_overlap;   // most seal calls in flight at once
+  // the seal calls by batch size (< 1, 1-4, 4-8, 8-15, >= 15 MiB): calls, bytes, call time (ns)
+  uint64_t seal_size_calls[5];
+  uint64_t seal_size_bytes[5];
+  uint64_t seal_size_ns[5];
 } pdb_hook_stats;
 
 void pdb_hook_stats_get(pdb_hook_stats* out);

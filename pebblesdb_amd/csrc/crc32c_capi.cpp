@@ -109,6 +109,38 @@ struct PhaseStamp {
 std::mutex g_stamp_mu;
 std::vector<PhaseStamp> g_stamps;
 
+// PDB_SEAL_STAMPS=<path> (diagnostics): every zero-copy host seal / verify records its bytes, its
+// host clock at entry, with its context locked, after the launch and after the synchronisation,
+// and the kernel's own time (events around it); the rows are written to <path> at exit
+struct SealStamp {
+  uint64_t n, t0, t1, t2, t3, allocs, nblk, maxblk;  // allocs: pdb_host_alloc page-locking calls so far
+  float kern_ms;
+};
+std::atomic<uint64_t> g_pin_allocs{0};
+std::mutex g_seal_stamp_mu;
+std::vector<SealStamp> g_seal_stamps;
+void write_seal_stamps_at_exit() {
+  const char* path = getenv("PDB_SEAL_STAMPS");
+  if (!path) return;
+  std::lock_guard<std::mutex> lk(g_seal_stamp_mu);
+  FILE* f = fopen(path, "w");
+  if (!f) return;
+  fprintf(f, "bytes,entry_ns,locked_ns,launched_ns,synced_ns,kernel_ms,allocs,blocks,max_block\n");
+  for (const SealStamp& p : g_seal_stamps)
+    fprintf(f, "%llu,%llu,%llu,%llu,%llu,%.4f,%llu,%llu,%llu\n", (unsigned long long)p.n, (unsigned long long)p.t0,
+            (unsigned long long)p.t1, (unsigned long long)p.t2, (unsigned long long)p.t3, p.kern_ms,
+            (unsigned long long)p.allocs, (unsigned long long)p.nblk, (unsigned long long)p.maxblk);
+  fclose(f);
+}
+bool seal_stamps_on() {
+  static const bool v = [] {
+    if (!getenv("PDB_SEAL_STAMPS")) return false;
+    atexit(write_seal_stamps_at_exit);
+    return true;
+  }();
+  return v;
+}
+
 uint64_t mono_ns() {
   timespec ts;
   clock_gettime(CLOCK_MONOTONIC, &ts);
@@ -823,33 +855,125 @@ int host_span(uint32_t init, const uint8_t* data, uint64_t n, uint32_t* out) {
 // the same way (the device seal's own kernel, crc_sst4k_kernel<SstSrc, ParkSealSink>), the handles
 // and the verify's ok bytes in the context's pinned scratch; one launch and one synchronisation
 // (tools/seal_batches.py: 4-MiB batches 31 -> 40.5 GiB/s, 16 MiB 43 -> 46, the bare H2D copy 44 / 51).
-int host_sst_mapped(uint8_t* d_buf, uint64_t buf_len, const pdb_block_handle* h, uint64_t n, bool seal, uint8_t* ok,
-                    int64_t* nbad_out) {
+// Blocks longer than kLongBlock (a table's index and filter blocks: 16 KiB .. 1.3 MiB in the engine)
+// are left out of that kernel, whose slow path hashes a block on one wave -- a round trip across
+// PCIe per 16 KiB, 0.3-1.3 ms for the last batch of a large table (profiles/r05/engine/long_blocks/)
+// -- and hashed by launch_span in 4-KiB segments on as many waves instead, on the same stream; the
+// host writes their trailers (seal) or checks them (verify) after the synchronisation.
+constexpr uint64_t kLongBlock = 16u << 10;
+int host_sst_mapped(uint8_t* h_buf, uint8_t* d_buf, uint64_t buf_len, const pdb_block_handle* h, uint64_t n, bool seal,
+                    uint8_t* ok, int64_t* nbad_out) {
+  const bool stamp = seal_stamps_on();
+  SealStamp ss{buf_len, stamp ? mono_ns() : 0, 0, 0, 0, g_pin_allocs.load(std::memory_order_relaxed), n, 0, 0.f};
+  if (stamp)
+    for (uint64_t i = 0; i < n; ++i) ss.maxblk = std::max<uint64_t>(ss.maxblk, h[i].size);
+  // the long blocks (their handle indices) and the scratch their span launches share
+  std::vector<uint64_t> longs;
+  uint64_t scratch_words = 0;
+  for (uint64_t i = 0; i < n; ++i)
+    if (h[i].size >= kLongBlock) {
+      longs.push_back(i);
+      scratch_words = std::max<uint64_t>(scratch_words, span_scratch_words(h[i].size + 1, 12));
+    }
+  const uint64_t nl = longs.size(), m = n - nl;  // m: blocks the sst kernel takes
   DevState* dev;
   int rc = get_state(&dev);
   if (rc) return rc;
   CtxLock cl(dev);
   HostCtx* st = cl.c;
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  if (stamp) {
+    ss.t1 = mono_ns();
+    if (hipEventCreate(&ev[0]) != hipSuccess || hipEventCreate(&ev[1]) != hipSuccess) return fail(PDB_EHIP, "hipEventCreate(stamps)");
+  }
   hipError_t e = hipSetDevice(dev->device);
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+  // pinned: [the kernel's handles][ok bytes, 128-B lines][nbad][the long blocks' CRCs]
   const size_t pin_ok = align_up(n * sizeof(pdb_block_handle), 128);  // (the verify stores 128-B lines of ok bytes)
-  if ((rc = ensure_pin(st, pin_ok + align_up(n, 64) + 64))) return rc;
+  const size_t pin_nb = pin_ok + align_up(n, 64), pin_long = pin_nb + 64;
+  if ((rc = ensure_pin(st, pin_long + align_up(4 * nl, 64)))) return rc;
   if (!st->d_pin) return fail(PDB_EHIP, "pinned scratch has no device mapping");
-  if ((rc = ensure_ws(st, 256))) return rc;
-  memcpy(st->h_pin, h, n * sizeof(pdb_block_handle));
+  // device workspace: [nbad][the long blocks' CRCs][span scratch]
+  const size_t ws_out = 256, ws_scr = ws_out + align_up(4 * nl, 256);
+  if ((rc = ensure_ws(st, ws_scr + scratch_words * 4 + 256))) return rc;
+  pdb_block_handle* hk = reinterpret_cast<pdb_block_handle*>(st->h_pin);
+  if (nl == 0) {
+    memcpy(hk, h, n * sizeof(pdb_block_handle));
+  } else {
+    for (uint64_t i = 0, j = 0; i < n; ++i)
+      if (h[i].size < kLongBlock) hk[j++] = h[i];
+  }
   hipStream_t s = st->stream;
   uint32_t* d_nbad = reinterpret_cast<uint32_t*>(st->d_ws);
-  uint32_t* h_nb = reinterpret_cast<uint32_t*>(st->h_pin + pin_ok + align_up(n, 64));
+  uint32_t* d_long = reinterpret_cast<uint32_t*>(st->d_ws + ws_out);
+  uint32_t* d_scr = reinterpret_cast<uint32_t*>(st->d_ws + ws_scr);
+  uint32_t* h_nb = reinterpret_cast<uint32_t*>(st->h_pin + pin_nb);
+  uint32_t* h_long = reinterpret_cast<uint32_t*>(st->h_pin + pin_long);
   *h_nb = 0;
   if (!seal && (e = hipMemsetAsync(d_nbad, 0, 4, s)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
-  e = launch_sst(dev->hgeom, dev->d_tables, d_buf, buf_len, reinterpret_cast<const pdb_block_handle*>(st->d_pin), n, seal,
+  if (stamp) (void)hipEventRecord(ev[0], s);
+  e = launch_sst(dev->hgeom, dev->d_tables, d_buf, buf_len, reinterpret_cast<const pdb_block_handle*>(st->d_pin), m, seal,
                  seal ? nullptr : st->d_pin + pin_ok, seal ? nullptr : d_nbad, s);
   if (e != hipSuccess) return hip_fail(e, seal ? "launch_sst(seal, mapped)" : "launch_sst(verify, mapped)");
+  for (uint64_t k = 0; k < nl; ++k) {  // Value(contents || type) of each long block
+    const pdb_block_handle& b = h[longs[k]];
+    e = launch_span(dev->hgeom, dev->d_tables, dev->d_pow2, 0u, d_buf + b.offset, b.size + 1, d_scr, d_long + k, s, 12);
+    if (e != hipSuccess) return hip_fail(e, "launch_span(long block, mapped)");
+  }
+  if (stamp) {
+    (void)hipEventRecord(ev[1], s);
+    ss.t2 = mono_ns();
+  }
   if (!seal && (e = hipMemcpyAsync(h_nb, d_nbad, 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
     return hip_fail(e, "hipMemcpyAsync(nbad)");
+  if (nl && (e = hipMemcpyAsync(h_long, d_long, 4 * nl, hipMemcpyDeviceToHost, s)) != hipSuccess)
+    return hip_fail(e, "hipMemcpyAsync(long blocks)");
   if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
-  if (!seal && ok) memcpy(ok, st->h_pin + pin_ok, n);
-  if (nbad_out) *nbad_out = seal ? 0 : *h_nb;
+  if (stamp) {
+    ss.t3 = mono_ns();
+    (void)hipEventElapsedTime(&ss.kern_ms, ev[0], ev[1]);
+    (void)hipEventDestroy(ev[0]);
+    (void)hipEventDestroy(ev[1]);
+    std::lock_guard<std::mutex> lk(g_seal_stamp_mu);
+    g_seal_stamps.push_back(ss);
+  }
+  // the long blocks' trailers: [type][Mask(crc)] little-endian at offset + size (table_builder.cc:197-200)
+  uint64_t nbad = seal ? 0 : *h_nb;
+  const uint8_t* okk = st->h_pin + pin_ok;  // the kernel's ok bytes, in the order of its handles
+  for (uint64_t k = 0; k < nl; ++k) {
+    const pdb_block_handle& b = h[longs[k]];
+    uint8_t* tr = h_buf + b.offset + b.size + 1;
+    if (seal) {
+      const uint32_t w = pdb_mask(h_long[k]);
+      tr[0] = static_cast<uint8_t>(w);
+      tr[1] = static_cast<uint8_t>(w >> 8);
+      tr[2] = static_cast<uint8_t>(w >> 16);
+      tr[3] = static_cast<uint8_t>(w >> 24);
+    } else {
+      const uint32_t w = static_cast<uint32_t>(tr[0]) | (static_cast<uint32_t>(tr[1]) << 8) |
+                         (static_cast<uint32_t>(tr[2]) << 16) | (static_cast<uint32_t>(tr[3]) << 24);
+      nbad += pdb_unmask(w) != h_long[k];
+    }
+  }
+  if (!seal && ok) {
+    if (nl == 0) {
+      memcpy(ok, okk, n);
+    } else {
+      for (uint64_t i = 0, j = 0, k = 0; i < n; ++i) {
+        if (k < nl && longs[k] == i) {
+          const pdb_block_handle& b = h[i];
+          const uint8_t* tr = h_buf + b.offset + b.size + 1;
+          const uint32_t w = static_cast<uint32_t>(tr[0]) | (static_cast<uint32_t>(tr[1]) << 8) |
+                             (static_cast<uint32_t>(tr[2]) << 16) | (static_cast<uint32_t>(tr[3]) << 24);
+          ok[i] = pdb_unmask(w) == h_long[k] ? 1u : 0u;
+          ++k;
+        } else {
+          ok[i] = okk[j++];
+        }
+      }
+    }
+  }
+  if (nbad_out) *nbad_out = static_cast<int64_t>(nbad);
   return PDB_OK;
 }
 
@@ -888,7 +1012,7 @@ int host_sst(uint8_t* buf, uint64_t buf_len, const pdb_block_handle* h, uint64_t
     return !(e && e[0] == '0');
   }();
   if (mapped)
-    if (uint8_t* d_buf = pin_mapping(buf, buf_len)) return host_sst_mapped(d_buf, buf_len, h, n, seal, ok, nbad_out);
+    if (uint8_t* d_buf = pin_mapping(buf, buf_len)) return host_sst_mapped(buf, d_buf, buf_len, h, n, seal, ok, nbad_out);
   size_t need = 0;
   uint64_t max_count = 0;
   for (const auto& x : groups) {
@@ -996,6 +1120,7 @@ int pdb_host_alloc(uint64_t bytes, void** out) {
     *out = best->h;
     return PDB_OK;
   }
+  g_pin_allocs.fetch_add(1, std::memory_order_relaxed);
   hipError_t e = hipHostMalloc(out, bytes, hipHostMallocDefault);
   if (e != hipSuccess) {
     *out = nullptr;

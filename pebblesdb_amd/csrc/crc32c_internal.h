@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include "../../include/pdb_crc32c.h"
+#include "crc32c_math.h"
 
 namespace pdb {
 
@@ -42,11 +43,12 @@ hipError_t launch_sst_masked(const LaunchGeom& g, const uint32_t* d_tables, uint
                              const pdb_block_handle* h, uint64_t n, uint32_t* out, hipStream_t s);
 // Long span: raw CRCs of `nseg` segments of 2^seg_log2 bytes (+ the tail) in parallel, then a
 // one-workgroup tree combine with the power-of-two operators.  `scratch` holds
-// span_scratch_words(n) u32.  *out = Extend(init, data[0..n)).
-uint64_t span_scratch_words(uint64_t n);
+// span_scratch_words(n) u32.  *out = Extend(init, data[0..n)).  Segments of at least
+// 2^min_seg_log2 bytes (4 KiB for a block read across PCIe: one round trip per wave).
+uint64_t span_scratch_words(uint64_t n, uint32_t min_seg_log2 = PDB_SPAN_MIN_SEG_LOG2);
 hipError_t launch_span(const LaunchGeom& g, const uint32_t* d_tables, const uint32_t* d_pow2,
                        uint32_t init, const uint8_t* data, uint64_t n, uint32_t* scratch, uint32_t* out,
-                       hipStream_t s);
+                       hipStream_t s, uint32_t min_seg_log2 = PDB_SPAN_MIN_SEG_LOG2);
 
 // crc32c_server.hip -- the scalar Extend service: ONE persistent workgroup of kServerWaves waves
 // serving kServerSlots request slots, so concurrent callers (the engine's writer, memtable,

@@ -46,9 +46,9 @@ struct SpanGeom {
   uint64_t nf, head;
 };
 
-__host__ __device__ inline SpanGeom span_geom(uint64_t n) {
+__host__ __device__ inline SpanGeom span_geom(uint64_t n, uint32_t min_seg_log2 = PDB_SPAN_MIN_SEG_LOG2) {
   SpanGeom g;
-  g.seg_log2 = PDB_SPAN_MIN_SEG_LOG2;
+  g.seg_log2 = min_seg_log2;
   while ((n >> g.seg_log2) + 1 > (1ull << PDB_SPAN_MAX_SEGS_LOG2)) ++g.seg_log2;
   g.nf = n >> g.seg_log2;
   g.head = n & ((1ull << g.seg_log2) - 1);
@@ -85,12 +85,12 @@ __global__ __launch_bounds__(1024) void span_combine_kernel(const uint32_t* __re
 
 }  // namespace
 
-uint64_t span_scratch_words(uint64_t n) { return span_geom(n).nf + 1; }
+uint64_t span_scratch_words(uint64_t n, uint32_t min_seg_log2) { return span_geom(n, min_seg_log2).nf + 1; }
 
 hipError_t launch_span(const LaunchGeom& g, const uint32_t* d_tables, const uint32_t* d_pow2,
                        uint32_t init, const uint8_t* data, uint64_t n, uint32_t* scratch, uint32_t* out,
-                       hipStream_t s) {
-  const SpanGeom sg = span_geom(n);
+                       hipStream_t s, uint32_t min_seg_log2) {
+  const SpanGeom sg = span_geom(n, min_seg_log2);
   // head leaf from the Extend seed (n mod S bytes, possibly empty), then the full segments
   hipError_t e = launch_fixed(g, d_tables, data, 0, static_cast<uint32_t>(sg.head), 1, PDB_CRC_USE_INIT,
                               init, scratch, s);

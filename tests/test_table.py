@@ -151,3 +151,55 @@ def test_pinned_staging_zero_copy_seal_and_verify(dev, oracle_lib):
     check(lib().pdb_host_free(q))
     assert lib().pdb_host_free(q) == -3
     assert lib().pdb_host_free(ctypes.c_void_p(big.ctypes.data)) == -3
+
+
+@gpu
+def test_pinned_staging_long_blocks(dev, oracle_lib):
+    """A zero-copy seal / verify batch with index- and filter-sized blocks: blocks of 16 KiB and more
+    leave the sst kernel for 4-KiB-segment span launches (crc32c_capi.cpp kLongBlock) and the host
+    writes / checks their trailers.  Every trailer is checked against the oracle, including the
+    sizes either side of the threshold and a 1.3-MiB block; ok bytes keep the handles' order."""
+    import ctypes
+
+    import oracle
+    from pebblesdb_amd import crc32c
+    from pebblesdb_amd._native import check, lib
+
+    rng = np.random.Generator(np.random.PCG64(47))
+    longs = [16383, 16384, 16385, 65535, 65543, 4096 * 37 + 3, 1363149, 20000]
+    sizes = rng.integers(4166, 4175, size=300).tolist()
+    for i, z in enumerate(longs):  # spread through the batch, the last block long
+        sizes.insert(20 + 37 * i, z)
+    sizes += [0, 7, 300001]
+    sizes = np.array(sizes, dtype=np.int64)
+    offs = np.concatenate([[5], 5 + np.cumsum(sizes + 5)[:-1]]).astype(np.int64)
+    total = int(offs[-1] + sizes[-1] + 5) + 3
+    img = oracle.splitmix_bytes(total, 91).copy()
+    img[offs + sizes] = rng.integers(0, 2, size=len(sizes))
+    h = np.zeros(len(sizes), dtype=crc32c.HANDLE_DTYPE)
+    h["offset"], h["size"] = offs, sizes
+    p = ctypes.c_void_p()
+    check(lib().pdb_host_alloc(total, ctypes.byref(p)))
+    try:
+        pin = np.ctypeslib.as_array((ctypes.c_uint8 * total).from_address(p.value))
+        pin[:] = img
+        check(lib().pdb_sst_seal_host(p.value, total, h.ctypes.data, len(h)))
+        for o, z in zip(offs.tolist(), sizes.tolist()):
+            word = int.from_bytes(pin[o + z + 1 : o + z + 5].tobytes(), "little")
+            assert word == oracle_lib.mask(oracle_lib.value(pin[o : o + z + 1].tobytes())), (o, z)
+        mask = np.ones(total, dtype=bool)
+        for o, z in zip(offs.tolist(), sizes.tolist()):
+            mask[o + z + 1 : o + z + 5] = False
+        assert (pin[mask] == img[mask]).all()  # nothing but the trailers written
+        ok = np.zeros(len(h), dtype=np.uint8)
+        assert lib().pdb_sst_verify_host(p.value, total, h.ctypes.data, len(h), ok.ctypes.data) == 0 and ok.all()
+        bad = [int(np.flatnonzero(sizes == 16384)[0]), int(np.flatnonzero(sizes == 1363149)[0]), 3, len(h) - 1]
+        pin[offs[bad[0]] + 16000] ^= 0x04
+        pin[offs[bad[1]] + sizes[bad[1]]] ^= 0x01  # a type byte
+        pin[offs[bad[2]] + 100] ^= 0x80
+        pin[offs[bad[3]] + sizes[bad[3]] + 2] ^= 0x10  # a trailer byte
+        ok[:] = 1
+        assert lib().pdb_sst_verify_host(p.value, total, h.ctypes.data, len(h), ok.ctypes.data) == 4
+        assert sorted(np.flatnonzero(ok == 0).tolist()) == sorted(bad)
+    finally:
+        check(lib().pdb_host_free(p))

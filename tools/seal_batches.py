@@ -7,7 +7,9 @@ batch through its device mapping (hipHostGetDevicePointer), the trailers written
 PCIe, no DMA.  Also the conditions of the engine's seals: the batch freshly written by the CPU,
 8 batches in rotation, a new allocation per batch, 1 / 5 / 20 ms of idle GPU between seals.  argv[2]:
 run on that NUMA node's CPUs.  Every form's image must equal the host seal's.  One JSON line per
-batch size."""
+batch size.  argv[3] (e.g. "0,2,4,8"): the seal of the pinned batch again with that many host
+threads copying 256-MiB arrays in the background (the engine's compaction and page-cache traffic as
+host-memory load)."""
 import ctypes
 import json
 import os
@@ -53,6 +55,37 @@ def node_cpus(node: int):
     for part in open(f"/sys/devices/system/node/node{node}/cpulist").read().strip().split(","):
         lo, _, hi = part.partition("-")
         out.update(range(int(lo), int(hi or lo) + 1))
+    return out
+
+
+def copy_load_rates(total: int, p_img: int, h, nblk: int, counts):
+    """Seals of one pinned batch while `n` host threads copy 256-MiB arrays (numpy releases the GIL)."""
+    import threading
+    out = {}
+    for n in counts:
+        stop = threading.Event()
+        copied = [0] * n
+
+        def worker(i):
+            a = np.ones(256 << 20, dtype=np.uint8)
+            b = np.empty_like(a)
+            while not stop.is_set():
+                np.copyto(b, a)
+                copied[i] += a.nbytes
+        ths = [threading.Thread(target=worker, args=(i,)) for i in range(n)]
+        for t in ths:
+            t.start()
+        time.sleep(0.5 if n else 0.0)
+        c0, t0 = sum(copied), time.perf_counter()
+        reps = 200
+        for _ in range(reps):
+            check(lib().pdb_sst_seal_host(p_img, total, h.ctypes.data, nblk))
+        dt = time.perf_counter() - t0
+        c1 = sum(copied)
+        stop.set()
+        for t in ths:
+            t.join()
+        out[n] = {"seal_GiB_s": round(total * reps / dt / GIB, 2), "host_copy_GiB_s": round((c1 - c0) / dt / GIB, 1)}
     return out
 
 
@@ -159,6 +192,8 @@ def main():
 
         dt = per_call(h2d, reps)
         res["h2d_pinned"] = {"us_per_call": round(dt * 1e6, 1), "GiB_s": round(total / dt / GIB, 2)}
+        if len(sys.argv) > 3:
+            res["under_host_copies"] = copy_load_rates(total, p_img, h, nblk, [int(x) for x in sys.argv[3].split(",")])
         print(json.dumps(res), flush=True)
         check(lib().pdb_host_free(ctypes.c_void_p(p_img)))
         check(lib().pdb_host_free(ctypes.c_void_p(p_h)))
