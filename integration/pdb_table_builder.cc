@@ -23,7 +23,8 @@
 // (pdb_host_alloc, pdb_crc_route.h), so each seal runs zero-copy: the kernel reads the blocks and
 // writes the trailers through the mapping, one launch, no DMA (the in-engine
 // copy-inclusive seal rate; 16-MiB batches 29 013 vs 24 769 MiB/s for 4 MiB, fillrandom 10 M 5.27 vs
-// 5.40 us/op, profiles/r05/engine/).  PDB_SEAL_ASYNC=1 seals a
+// 5.40 us/op, profiles/r05/engine/; with a table's index and filter blocks hashed by span launches
+// beside the seal kernel, 35 777 MiB/s and 5.25 us/op, profiles/r05/c5b/).  PDB_SEAL_ASYNC=1 seals a
 // full batch asynchronously (one std::async task per batch) while the builder stages the next one;
 // the next seal, Finish() or Abandon() first waits for it and appends its bytes, so the file still
 // receives the batches in order and the GPU seal overlaps block building.
