@@ -861,6 +861,16 @@ int host_span(uint32_t init, const uint8_t* data, uint64_t n, uint32_t* out) {
 // -- and hashed by launch_span in 4-KiB segments on as many waves instead, on the same stream; the
 // host writes their trailers (seal) or checks them (verify) after the synchronisation.
 constexpr uint64_t kLongBlock = 16u << 10;
+// PDB_LONG_BLOCK=<bytes> (read once; 0: never) moves the threshold, for A/B runs
+uint64_t long_block_bytes() {
+  static const uint64_t v = [] {
+    const char* e = getenv("PDB_LONG_BLOCK");
+    if (!e) return kLongBlock;
+    const unsigned long long x = strtoull(e, nullptr, 10);
+    return x ? static_cast<uint64_t>(x) : UINT64_MAX;
+  }();
+  return v;
+}
 int host_sst_mapped(uint8_t* h_buf, uint8_t* d_buf, uint64_t buf_len, const pdb_block_handle* h, uint64_t n, bool seal,
                     uint8_t* ok, int64_t* nbad_out) {
   const bool stamp = seal_stamps_on();
@@ -870,8 +880,9 @@ int host_sst_mapped(uint8_t* h_buf, uint8_t* d_buf, uint64_t buf_len, const pdb_
   // the long blocks (their handle indices) and the scratch their span launches share
   std::vector<uint64_t> longs;
   uint64_t scratch_words = 0;
+  const uint64_t long_block = long_block_bytes();
   for (uint64_t i = 0; i < n; ++i)
-    if (h[i].size >= kLongBlock) {
+    if (h[i].size >= long_block) {
       longs.push_back(i);
       scratch_words = std::max<uint64_t>(scratch_words, span_scratch_words(h[i].size + 1, 12));
     }
@@ -901,7 +912,7 @@ int host_sst_mapped(uint8_t* h_buf, uint8_t* d_buf, uint64_t buf_len, const pdb_
     memcpy(hk, h, n * sizeof(pdb_block_handle));
   } else {
     for (uint64_t i = 0, j = 0; i < n; ++i)
-      if (h[i].size < kLongBlock) hk[j++] = h[i];
+      if (h[i].size < long_block) hk[j++] = h[i];
   }
   hipStream_t s = st->stream;
   uint32_t* d_nbad = reinterpret_cast<uint32_t*>(st->d_ws);
