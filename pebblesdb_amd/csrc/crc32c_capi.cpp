@@ -878,13 +878,22 @@ int host_sst_mapped(uint8_t* h_buf, uint8_t* d_buf, uint64_t buf_len, const pdb_
   if (stamp)
     for (uint64_t i = 0; i < n; ++i) ss.maxblk = std::max<uint64_t>(ss.maxblk, h[i].size);
   // the long blocks (their handle indices) and the scratch their span launches share
+  // Long blocks of up to 2^14 pieces of 4 KiB (64 MiB) go together: one descriptor launch over all
+  // their pieces, one combine launch; longer ones each take launch_span (its scratch).
+  constexpr uint64_t kPiece = 4096, kMaxPieces = 1ull << PDB_SPAN_MAX_SEGS_LOG2;
   std::vector<uint64_t> longs;
-  uint64_t scratch_words = 0;
+  uint64_t scratch_words = 0, npieces = 0, nmany = 0;
   const uint64_t long_block = long_block_bytes();
   for (uint64_t i = 0; i < n; ++i)
     if (h[i].size >= long_block) {
       longs.push_back(i);
-      scratch_words = std::max<uint64_t>(scratch_words, span_scratch_words(h[i].size + 1, 12));
+      const uint64_t pieces = (h[i].size + 1 + kPiece - 1) / kPiece;
+      if (pieces <= kMaxPieces) {
+        npieces += pieces;
+        ++nmany;
+      } else {
+        scratch_words = std::max<uint64_t>(scratch_words, span_scratch_words(h[i].size + 1, 12));
+      }
     }
   const uint64_t nl = longs.size(), m = n - nl;  // m: blocks the sst kernel takes
   DevState* dev;
@@ -899,14 +908,16 @@ int host_sst_mapped(uint8_t* h_buf, uint8_t* d_buf, uint64_t buf_len, const pdb_
   }
   hipError_t e = hipSetDevice(dev->device);
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
-  // pinned: [the kernel's handles][ok bytes, 128-B lines][nbad][the long blocks' CRCs]
+  // pinned: [the kernel's handles][ok bytes, 128-B lines][nbad][the long blocks' CRCs][their pieces][their parts]
   const size_t pin_ok = align_up(n * sizeof(pdb_block_handle), 128);  // (the verify stores 128-B lines of ok bytes)
   const size_t pin_nb = pin_ok + align_up(n, 64), pin_long = pin_nb + 64;
-  if ((rc = ensure_pin(st, pin_long + align_up(4 * nl, 64)))) return rc;
+  const size_t pin_pieces = pin_long + align_up(4 * nl, 64), pin_parts = pin_pieces + npieces * sizeof(pdb_blk);
+  if ((rc = ensure_pin(st, pin_parts + nmany * sizeof(SpanPart)))) return rc;
   if (!st->d_pin) return fail(PDB_EHIP, "pinned scratch has no device mapping");
-  // device workspace: [nbad][the long blocks' CRCs][span scratch]
+  // device workspace: [nbad][the long blocks' CRCs][span scratch][the pieces' leaves]
   const size_t ws_out = 256, ws_scr = ws_out + align_up(4 * nl, 256);
-  if ((rc = ensure_ws(st, ws_scr + scratch_words * 4 + 256))) return rc;
+  const size_t ws_leaves = ws_scr + align_up(scratch_words * 4, 256);
+  if ((rc = ensure_ws(st, ws_leaves + npieces * 4 + 256))) return rc;
   pdb_block_handle* hk = reinterpret_cast<pdb_block_handle*>(st->h_pin);
   if (nl == 0) {
     memcpy(hk, h, n * sizeof(pdb_block_handle));
@@ -926,11 +937,43 @@ int host_sst_mapped(uint8_t* h_buf, uint8_t* d_buf, uint64_t buf_len, const pdb_
   e = launch_sst(dev->hgeom, dev->d_tables, d_buf, buf_len, reinterpret_cast<const pdb_block_handle*>(st->d_pin), m, seal,
                  seal ? nullptr : st->d_pin + pin_ok, seal ? nullptr : d_nbad, s);
   if (e != hipSuccess) return hip_fail(e, seal ? "launch_sst(seal, mapped)" : "launch_sst(verify, mapped)");
-  for (uint64_t k = 0; k < nl; ++k) {  // Value(contents || type) of each long block
-    const pdb_block_handle& b = h[longs[k]];
-    e = launch_span(dev->hgeom, dev->d_tables, dev->d_pow2, 0u, d_buf + b.offset, b.size + 1, d_scr, d_long + k, s, 12);
-    if (e != hipSuccess) return hip_fail(e, "launch_span(long block, mapped)");
+  // Value(contents || type) of each long block: the ones of <= 2^14 pieces first (their CRCs at
+  // d_long[0, nmany)), then the rest (d_long[nmany, nl)); `order` maps back to longs[]
+  std::vector<uint64_t> order;
+  order.reserve(nl);
+  if (nmany) {
+    pdb_blk* pc = reinterpret_cast<pdb_blk*>(st->h_pin + pin_pieces);
+    SpanPart* parts = reinterpret_cast<SpanPart*>(st->h_pin + pin_parts);
+    uint64_t q = 0, b = 0;
+    for (uint64_t k = 0; k < nl; ++k) {
+      const pdb_block_handle& hb = h[longs[k]];
+      const uint64_t L = hb.size + 1, pieces = (L + kPiece - 1) / kPiece;
+      if (pieces > kMaxPieces) continue;
+      // the first piece takes the Value seed and the bytes that are not a whole piece
+      const uint64_t first = L - (pieces - 1) * kPiece;
+      uint32_t ml = 0;
+      while ((1ull << ml) < pieces) ++ml;
+      parts[b++] = SpanPart{static_cast<uint32_t>(q), static_cast<uint32_t>(pieces), ml, 0u};
+      pc[q++] = pdb_blk{hb.offset, static_cast<uint32_t>(first), 0u};
+      for (uint64_t j = 1; j < pieces; ++j)
+        pc[q++] = pdb_blk{hb.offset + first + (j - 1) * kPiece, static_cast<uint32_t>(kPiece), 0xFFFFFFFFu};
+      order.push_back(k);
+    }
+    e = launch_span_many(dev->hgeom, dev->d_tables, dev->d_pow2, d_buf, reinterpret_cast<const pdb_blk*>(st->d_pin + pin_pieces),
+                         npieces, reinterpret_cast<const SpanPart*>(st->d_pin + pin_parts), static_cast<uint32_t>(nmany), 12,
+                         reinterpret_cast<uint32_t*>(st->d_ws + ws_leaves), d_long, s);
+    if (e != hipSuccess) return hip_fail(e, "launch_span_many(long blocks, mapped)");
   }
+  for (uint64_t k = 0; k < nl; ++k) {
+    const pdb_block_handle& b = h[longs[k]];
+    if ((b.size + 1 + kPiece - 1) / kPiece <= kMaxPieces) continue;
+    e = launch_span(dev->hgeom, dev->d_tables, dev->d_pow2, 0u, d_buf + b.offset, b.size + 1, d_scr,
+                    d_long + order.size(), s, 12);
+    if (e != hipSuccess) return hip_fail(e, "launch_span(long block, mapped)");
+    order.push_back(k);
+  }
+  // h_long[r] is the CRC of longs[order[r]]: crc_of[k] for longs[k]
+  std::vector<uint32_t> crc_of(nl);
   if (stamp) {
     (void)hipEventRecord(ev[1], s);
     ss.t2 = mono_ns();
@@ -948,6 +991,7 @@ int host_sst_mapped(uint8_t* h_buf, uint8_t* d_buf, uint64_t buf_len, const pdb_
     std::lock_guard<std::mutex> lk(g_seal_stamp_mu);
     g_seal_stamps.push_back(ss);
   }
+  for (uint64_t r = 0; r < nl; ++r) crc_of[order[r]] = h_long[r];
   // the long blocks' trailers: [type][Mask(crc)] little-endian at offset + size (table_builder.cc:197-200)
   uint64_t nbad = seal ? 0 : *h_nb;
   const uint8_t* okk = st->h_pin + pin_ok;  // the kernel's ok bytes, in the order of its handles
@@ -955,7 +999,7 @@ int host_sst_mapped(uint8_t* h_buf, uint8_t* d_buf, uint64_t buf_len, const pdb_
     const pdb_block_handle& b = h[longs[k]];
     uint8_t* tr = h_buf + b.offset + b.size + 1;
     if (seal) {
-      const uint32_t w = pdb_mask(h_long[k]);
+      const uint32_t w = pdb_mask(crc_of[k]);
       tr[0] = static_cast<uint8_t>(w);
       tr[1] = static_cast<uint8_t>(w >> 8);
       tr[2] = static_cast<uint8_t>(w >> 16);
@@ -963,7 +1007,7 @@ int host_sst_mapped(uint8_t* h_buf, uint8_t* d_buf, uint64_t buf_len, const pdb_
     } else {
       const uint32_t w = static_cast<uint32_t>(tr[0]) | (static_cast<uint32_t>(tr[1]) << 8) |
                          (static_cast<uint32_t>(tr[2]) << 16) | (static_cast<uint32_t>(tr[3]) << 24);
-      nbad += pdb_unmask(w) != h_long[k];
+      nbad += pdb_unmask(w) != crc_of[k];
     }
   }
   if (!seal && ok) {
@@ -976,7 +1020,7 @@ int host_sst_mapped(uint8_t* h_buf, uint8_t* d_buf, uint64_t buf_len, const pdb_
           const uint8_t* tr = h_buf + b.offset + b.size + 1;
           const uint32_t w = static_cast<uint32_t>(tr[0]) | (static_cast<uint32_t>(tr[1]) << 8) |
                              (static_cast<uint32_t>(tr[2]) << 16) | (static_cast<uint32_t>(tr[3]) << 24);
-          ok[i] = pdb_unmask(w) == h_long[k] ? 1u : 0u;
+          ok[i] = pdb_unmask(w) == crc_of[k] ? 1u : 0u;
           ++k;
         } else {
           ok[i] = okk[j++];

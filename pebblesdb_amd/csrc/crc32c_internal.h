@@ -49,6 +49,17 @@ uint64_t span_scratch_words(uint64_t n, uint32_t min_seg_log2 = PDB_SPAN_MIN_SEG
 hipError_t launch_span(const LaunchGeom& g, const uint32_t* d_tables, const uint32_t* d_pow2,
                        uint32_t init, const uint8_t* data, uint64_t n, uint32_t* scratch, uint32_t* out,
                        hipStream_t s, uint32_t min_seg_log2 = PDB_SPAN_MIN_SEG_LOG2);
+// Many spans in two launches: `pieces` (npieces descriptors over `base`, PDB_CRC_USE_INIT) are
+// every span's leaves in order -- its first piece with init 0 (the Value seed), then pieces of
+// exactly 2^seg_log2 bytes with init 0xFFFFFFFF (raw state 0) -- and parts[b] = {span b's first
+// leaf, its leaves (<= 2^PDB_SPAN_MAX_SEGS_LOG2), ceil(log2(leaves))}; out[b] = Value(span b).
+// `leaves` holds npieces u32.
+struct SpanPart {
+  uint32_t leaf0, nleaves, m_log2, pad;
+};
+hipError_t launch_span_many(const LaunchGeom& g, const uint32_t* d_tables, const uint32_t* d_pow2, const uint8_t* base,
+                            const pdb_blk* pieces, uint64_t npieces, const SpanPart* parts, uint32_t nparts,
+                            uint32_t seg_log2, uint32_t* leaves, uint32_t* out, hipStream_t s);
 
 // crc32c_server.hip -- the scalar Extend service: ONE persistent workgroup of kServerWaves waves
 // serving kServerSlots request slots, so concurrent callers (the engine's writer, memtable,

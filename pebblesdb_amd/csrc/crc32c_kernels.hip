@@ -83,7 +83,47 @@ __global__ __launch_bounds__(1024) void span_combine_kernel(const uint32_t* __re
   if (threadIdx.x == 0) out[0] = ~sw[0];
 }
 
+// Many spans at once (launch_span_many): workgroup b folds span b's leaves, parts[b] = {first
+// leaf, leaves, tree levels}; the same tree as span_combine_kernel with segments of 2^seg_log2 B.
+__global__ __launch_bounds__(1024) void span_combine_many_kernel(const uint32_t* __restrict__ pow2,
+                                                                 const uint32_t* __restrict__ leaves,
+                                                                 const SpanPart* __restrict__ parts, uint32_t seg_log2,
+                                                                 uint32_t* __restrict__ out) {
+  __shared__ uint32_t sw[1u << PDB_SPAN_MAX_SEGS_LOG2];
+  __shared__ uint32_t ops[PDB_SPAN_MAX_SEGS_LOG2][1024];
+  const SpanPart p = parts[blockIdx.x];
+  const uint32_t M = 1u << p.m_log2;
+  for (uint32_t i = threadIdx.x; i < p.m_log2 * 1024u; i += blockDim.x)
+    ops[i >> 10][i & 1023u] = pow2[(seg_log2 + (i >> 10)) * 1024u + (i & 1023u)];
+  const uint32_t pad = M - p.nleaves;
+  for (uint32_t i = threadIdx.x; i < M; i += blockDim.x) sw[i] = i < pad ? 0u : ~leaves[p.leaf0 + i - pad];
+  __syncthreads();
+  for (uint32_t k = 0; k < p.m_log2; ++k) {
+    const uint32_t half = 1u << k, pairs = M >> (k + 1);
+    for (uint32_t j = threadIdx.x; j < pairs; j += blockDim.x) {
+      const uint32_t i = j << (k + 1);
+      const uint32_t c = sw[i];
+      const uint32_t* op = ops[k];
+      sw[i] = op[c & 0xffu] ^ op[256u + ((c >> 8) & 0xffu)] ^ op[512u + ((c >> 16) & 0xffu)] ^
+              op[768u + (c >> 24)] ^ sw[i + half];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[blockIdx.x] = ~sw[0];
+}
+
 }  // namespace
+
+hipError_t launch_span_many(const LaunchGeom& g, const uint32_t* d_tables, const uint32_t* d_pow2, const uint8_t* base,
+                            const pdb_blk* pieces, uint64_t npieces, const SpanPart* parts, uint32_t nparts,
+                            uint32_t seg_log2, uint32_t* leaves, uint32_t* out, hipStream_t s) {
+  if (nparts == 0) return hipSuccess;
+  hipError_t e = launch_desc(g, d_tables, base, pieces, npieces, PDB_CRC_USE_INIT, kModeOut, nullptr, leaves, nullptr,
+                             nullptr, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(span_combine_many_kernel, dim3(nparts), dim3(1024), 0, s, d_pow2, leaves, parts, seg_log2, out);
+  return hipGetLastError();
+}
 
 uint64_t span_scratch_words(uint64_t n, uint32_t min_seg_log2) { return span_geom(n, min_seg_log2).nf + 1; }
 
