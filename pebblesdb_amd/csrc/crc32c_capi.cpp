@@ -858,8 +858,9 @@ int host_span(uint32_t init, const uint8_t* data, uint64_t n, uint32_t* out) {
 // Blocks longer than kLongBlock (a table's index and filter blocks: 16 KiB .. 1.3 MiB in the engine)
 // are left out of that kernel, whose slow path hashes a block on one wave -- a round trip across
 // PCIe per 16 KiB, 0.3-1.3 ms for the last batch of a large table (profiles/r05/engine/long_blocks/)
-// -- and hashed by launch_span in 4-KiB segments on as many waves instead, on the same stream; the
-// host writes their trailers (seal) or checks them (verify) after the synchronisation.
+// -- and hashed in 4-KiB pieces on as many waves instead: one descriptor launch over all of the
+// batch's long blocks and one combine launch (launch_span_many), on the same stream; the host writes
+// their trailers (seal) or checks them (verify) after the synchronisation.
 constexpr uint64_t kLongBlock = 16u << 10;
 // PDB_LONG_BLOCK=<bytes> (read once; 0: never) moves the threshold, for A/B runs
 uint64_t long_block_bytes() {
