@@ -2,7 +2,7 @@
 
 Run with PDB_HOST_CHUNK_BYTES set (the product reads it once per process): the host batch, verify,
 seal and sstable-verify entry points must give the reference's answers however small the staging
-groups are.  Checked against the golden vectors (generated from the reference's util/crc32c.cc)
+groups are, long (index / filter sized) blocks included.  Checked against the golden vectors (generated from the reference's util/crc32c.cc)
 and the sstable files the reference's TableBuilder wrote.  Prints "host staging ok".
 """
 import json
@@ -62,8 +62,45 @@ def reference_tables():
         assert [i for i in range(len(hs)) if not ok[i]] == victims, name
 
 
+def long_blocks():
+    """Index- and filter-sized blocks (16 KiB .. 1.3 MiB) among 4-KiB ones, from pageable memory
+    (the DMA route: 0-byte stand-ins in the sst kernel, the blocks by span launches), every trailer
+    against the oracle, then verify with corrupted long and short blocks."""
+    import ctypes
+
+    from pebblesdb_amd._native import check, lib
+    orc = oracle.Oracle()
+    rng = np.random.Generator(np.random.PCG64(53))
+    sizes = rng.integers(4166, 4175, size=120).tolist()
+    for i, z in enumerate([16384, 16383, 70001, 1363149, 4096 * 9]):
+        sizes.insert(7 + 23 * i, z)
+    sizes = np.array(sizes, dtype=np.int64)
+    offs = np.concatenate([[9], 9 + np.cumsum(sizes + 5)[:-1]]).astype(np.int64)
+    total = int(offs[-1] + sizes[-1] + 5) + 7
+    img = oracle.splitmix_bytes(total, 29).copy()
+    img[offs + sizes] = rng.integers(0, 2, size=len(sizes))
+    h = np.zeros(len(sizes), dtype=crc.HANDLE_DTYPE)
+    h["offset"], h["size"] = offs, sizes
+    check(lib().pdb_sst_seal_host(img.ctypes.data, total, h.ctypes.data, len(h)))
+    for o, z in zip(offs.tolist(), sizes.tolist()):
+        word = int.from_bytes(img[o + z + 1 : o + z + 5].tobytes(), "little")
+        assert word == orc.mask(orc.value(img[o : o + z + 1].tobytes())), (o, z)
+    ok = np.zeros(len(h), dtype=np.uint8)
+    assert lib().pdb_sst_verify_host(img.ctypes.data, total, h.ctypes.data, len(h), ok.ctypes.data) == 0 and ok.all()
+    assert lib().pdb_sst_verify_host(img.ctypes.data, total, h.ctypes.data, len(h), None) == 0
+    bad = [int(np.flatnonzero(sizes == 1363149)[0]), int(np.flatnonzero(sizes == 16384)[0]), 2]
+    img[offs[bad[0]] + 1000000] ^= 0x20
+    img[offs[bad[1]] + sizes[bad[1]] + 3] ^= 0x01  # a trailer byte
+    img[offs[bad[2]] + 17] ^= 0x02
+    ok[:] = 1
+    assert lib().pdb_sst_verify_host(img.ctypes.data, total, h.ctypes.data, len(h), ok.ctypes.data) == 3
+    assert sorted(np.flatnonzero(ok == 0).tolist()) == sorted(bad)
+    assert lib().pdb_sst_verify_host(img.ctypes.data, total, h.ctypes.data, len(h), None) == 3
+
+
 if __name__ == "__main__":
     crc.init_device(0)
     golden_batches()
     reference_tables()
+    long_blocks()
     print("host staging ok (PDB_HOST_CHUNK_BYTES=%s)" % os.environ.get("PDB_HOST_CHUNK_BYTES"))

@@ -158,7 +158,8 @@ def test_pinned_staging_long_blocks(dev, oracle_lib):
     """A zero-copy seal / verify batch with index- and filter-sized blocks: blocks of 16 KiB and more
     leave the sst kernel for 4-KiB-segment span launches (crc32c_capi.cpp kLongBlock) and the host
     writes / checks their trailers.  Every trailer is checked against the oracle, including the
-    sizes either side of the threshold and a 1.3-MiB block; ok bytes keep the handles' order."""
+    sizes either side of the threshold and a 1.3-MiB block; ok bytes keep the handles' order.  The
+    pageable route (DMA; 0-byte stand-ins in the sst kernel) gives the same image and verdicts."""
     import ctypes
 
     import oracle
@@ -201,5 +202,19 @@ def test_pinned_staging_long_blocks(dev, oracle_lib):
         ok[:] = 1
         assert lib().pdb_sst_verify_host(p.value, total, h.ctypes.data, len(h), ok.ctypes.data) == 4
         assert sorted(np.flatnonzero(ok == 0).tolist()) == sorted(bad)
+        # the same batch from pageable memory (the DMA route: 0-byte stand-ins for the long blocks)
+        page = img.copy()
+        check(lib().pdb_sst_seal_host(page.ctypes.data, total, h.ctypes.data, len(h)))
+        pin[offs[bad[0]] + 16000] ^= 0x04  # (undo the corruptions: the sealed image again)
+        pin[offs[bad[1]] + sizes[bad[1]]] ^= 0x01
+        pin[offs[bad[2]] + 100] ^= 0x80
+        pin[offs[bad[3]] + sizes[bad[3]] + 2] ^= 0x10
+        assert (page == pin).all()
+        ok[:] = 0
+        assert lib().pdb_sst_verify_host(page.ctypes.data, total, h.ctypes.data, len(h), ok.ctypes.data) == 0 and ok.all()
+        page[offs[bad[0]] + 16000] ^= 0x04
+        page[offs[bad[3]] + sizes[bad[3]] + 2] ^= 0x10
+        assert lib().pdb_sst_verify_host(page.ctypes.data, total, h.ctypes.data, len(h), ok.ctypes.data) == 2
+        assert sorted(np.flatnonzero(ok == 0).tolist()) == sorted([bad[0], bad[3]])
     finally:
         check(lib().pdb_host_free(p))
