@@ -902,7 +902,14 @@ int host_sst_mapped(uint8_t* h_buf, uint8_t* d_buf, uint64_t buf_len, const pdb_
   if (rc) return rc;
   CtxLock cl(dev);
   HostCtx* st = cl.c;
-  hipEvent_t ev[2] = {nullptr, nullptr};
+  struct StampEvents {  // (destroyed on every return)
+    hipEvent_t e[2] = {nullptr, nullptr};
+    ~StampEvents() {
+      for (hipEvent_t x : e)
+        if (x) (void)hipEventDestroy(x);
+    }
+  } sev;
+  hipEvent_t* ev = sev.e;
   if (stamp) {
     ss.t1 = mono_ns();
     if (hipEventCreate(&ev[0]) != hipSuccess || hipEventCreate(&ev[1]) != hipSuccess) return fail(PDB_EHIP, "hipEventCreate(stamps)");
@@ -987,8 +994,6 @@ int host_sst_mapped(uint8_t* h_buf, uint8_t* d_buf, uint64_t buf_len, const pdb_
   if (stamp) {
     ss.t3 = mono_ns();
     (void)hipEventElapsedTime(&ss.kern_ms, ev[0], ev[1]);
-    (void)hipEventDestroy(ev[0]);
-    (void)hipEventDestroy(ev[1]);
     std::lock_guard<std::mutex> lk(g_seal_stamp_mu);
     g_seal_stamps.push_back(ss);
   }
