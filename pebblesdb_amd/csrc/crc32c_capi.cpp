@@ -922,8 +922,8 @@ int host_sst_mapped(uint8_t* h_buf, uint8_t* d_buf, uint64_t buf_len, const pdb_
   const size_t pin_pieces = pin_long + align_up(4 * nl, 64), pin_parts = pin_pieces + npieces * sizeof(pdb_blk);
   if ((rc = ensure_pin(st, pin_parts + nmany * sizeof(SpanPart)))) return rc;
   if (!st->d_pin) return fail(PDB_EHIP, "pinned scratch has no device mapping");
-  // device workspace: [nbad][the long blocks' CRCs][span scratch][the pieces' leaves]
-  const size_t ws_out = 256, ws_scr = ws_out + align_up(4 * nl, 256);
+  // device workspace: [nbad][span scratch][the pieces' leaves] (the long blocks' CRCs: pinned)
+  const size_t ws_scr = 256;
   const size_t ws_leaves = ws_scr + align_up(scratch_words * 4, 256);
   if ((rc = ensure_ws(st, ws_leaves + npieces * 4 + 256))) return rc;
   pdb_block_handle* hk = reinterpret_cast<pdb_block_handle*>(st->h_pin);
@@ -935,7 +935,7 @@ int host_sst_mapped(uint8_t* h_buf, uint8_t* d_buf, uint64_t buf_len, const pdb_
   }
   hipStream_t s = st->stream;
   uint32_t* d_nbad = reinterpret_cast<uint32_t*>(st->d_ws);
-  uint32_t* d_long = reinterpret_cast<uint32_t*>(st->d_ws + ws_out);
+  uint32_t* d_long = reinterpret_cast<uint32_t*>(st->d_pin + pin_long);  // (written across PCIe: no copy back)
   uint32_t* d_scr = reinterpret_cast<uint32_t*>(st->d_ws + ws_scr);
   uint32_t* h_nb = reinterpret_cast<uint32_t*>(st->h_pin + pin_nb);
   uint32_t* h_long = reinterpret_cast<uint32_t*>(st->h_pin + pin_long);
@@ -988,8 +988,6 @@ int host_sst_mapped(uint8_t* h_buf, uint8_t* d_buf, uint64_t buf_len, const pdb_
   }
   if (!seal && (e = hipMemcpyAsync(h_nb, d_nbad, 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
     return hip_fail(e, "hipMemcpyAsync(nbad)");
-  if (nl && (e = hipMemcpyAsync(h_long, d_long, 4 * nl, hipMemcpyDeviceToHost, s)) != hipSuccess)
-    return hip_fail(e, "hipMemcpyAsync(long blocks)");
   if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
   if (stamp) {
     ss.t3 = mono_ns();
@@ -1095,18 +1093,16 @@ int host_sst(uint8_t* buf, uint64_t buf_len, const pdb_block_handle* h, uint64_t
     return b.size >= long_block && (b.size + 1 + kPiece - 1) / kPiece <= kMaxPieces;
   };
   std::vector<uint64_t> longs;  // handle indices, ascending (so by group)
-  uint64_t npieces = 0, max_gpieces = 0, max_glong = 0;
+  uint64_t npieces = 0, max_gpieces = 0;
   for (const auto& x : groups) {
-    uint64_t gp = 0, gl = 0;
+    uint64_t gp = 0;
     for (uint64_t i = x.first; i < x.first + x.count; ++i)
       if (is_long(h[i])) {
         longs.push_back(i);
         gp += (h[i].size + 1 + kPiece - 1) / kPiece;
-        ++gl;
       }
     npieces += gp;
     max_gpieces = std::max(max_gpieces, gp);
-    max_glong = std::max(max_glong, gl);
   }
   const uint64_t nl = longs.size();
   DevState* dev;
@@ -1117,9 +1113,9 @@ int host_sst(uint8_t* buf, uint64_t buf_len, const pdb_block_handle* h, uint64_t
   LaunchGeom hgeom = dev->hgeom;
   hipError_t e = hipSetDevice(dev->device);
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
-  // device: the slots, nbad, then the long blocks' leaves and CRCs (one group's at a time: stream s)
-  const size_t ws_leaves = nslots * slot_bytes + 256, ws_lcrc = ws_leaves + align_up(4 * max_gpieces, 256);
-  if ((rc = ensure_ws(st, ws_lcrc + align_up(4 * max_glong, 256)))) return rc;
+  // device: the slots, nbad, then the long blocks' leaves (one group's at a time: stream s)
+  const size_t ws_leaves = nslots * slot_bytes + 256;
+  if ((rc = ensure_ws(st, ws_leaves + align_up(4 * max_gpieces, 256)))) return rc;
   // pinned: every group's rebased handles, then the trailer words (seal) or ok bytes (verify), then
   // nbad, then the long blocks' CRCs, pieces and parts (every group's, side by side)
   const size_t pin_crc = align_up(n * sizeof(pdb_block_handle), 64);
@@ -1186,13 +1182,11 @@ int host_sst(uint8_t* buf, uint64_t buf_len, const pdb_block_handle* h, uint64_t
           pc[lp++] = pdb_blk{o + first + (j - 1) * kPiece, static_cast<uint32_t>(kPiece), 0xFFFFFFFFu};
       }
       if (lq > lq0) {
-        uint32_t* d_lcrc = reinterpret_cast<uint32_t*>(st->d_ws + ws_lcrc);
+        uint32_t* d_lcrc = reinterpret_cast<uint32_t*>(st->d_pin + pin_lcrc) + lq0;  // (written across PCIe)
         e = launch_span_many(hgeom, dev->d_tables, dev->d_pow2, ws, reinterpret_cast<const pdb_blk*>(st->d_pin + pin_pieces) + lp0,
                              lp - lp0, reinterpret_cast<const SpanPart*>(st->d_pin + pin_parts) + lq0,
                              static_cast<uint32_t>(lq - lq0), 12, reinterpret_cast<uint32_t*>(st->d_ws + ws_leaves), d_lcrc, s);
         if (e != hipSuccess) return hip_fail(e, "launch_span_many(long blocks)");
-        if ((e = hipMemcpyAsync(h_lcrc + lq0, d_lcrc, 4 * (lq - lq0), hipMemcpyDeviceToHost, s)) != hipSuccess)
-          return hip_fail(e, "hipMemcpyAsync(long blocks)");
       }
       if ((e = pipe.end_group(k)) != hipSuccess) return hip_fail(e, "hipEventRecord(drained)");
     }
