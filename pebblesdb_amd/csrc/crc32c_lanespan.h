@@ -870,6 +870,17 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
       uint32_t Ps;
       if constexpr (MODE >= 43 && MODE <= 46) {
         Ps = fold_op(slot, P, 0u, cb ^ cc);
+      } else if constexpr (MODE == 49) {  // (diagnostics: the lookups on the lanes that use them only)
+        Ps = P;
+        if (l) {
+          uint32_t v[4];
+#pragma unroll
+          for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t bb = __builtin_amdgcn_perm(0u, P, 0x0C0C0000u | (j << 8) | j);
+            v[j] = lds_u32(lds, (bb & 0xFF7Cu) ^ (128u | ((4u * slot + j) << 2)));
+          }
+          Ps = xor3(xor3(v[0], v[1], v[2]), v[3], 0u);
+        }
       } else {
         uint32_t v[4];
 #pragma unroll
