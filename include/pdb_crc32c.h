@@ -21,9 +21,17 @@
  *     usable device the call fails (PDB_ENODEV) and pdb_last_error() says why.
  *   - Scalar Extend/Value cannot report errors (the reference contract, util/crc32c.h:17); on a
  *     device failure they abort() with a message instead of returning a wrong value.
- *   - Caller owns every buffer.  Device-resident entry points allocate nothing and are
- *     stream-ordered (capturable into a hipGraph).  Host entry points stage through a cached
+ *   - Caller owns every buffer.  Device-resident entry points are stream-ordered and capturable
+ *     into a hipGraph; the only memory they own is the long-block lane's scratch (~42 MiB per
+ *     caller stream, made at the stream's first call outside a capture or by
+ *     pdb_crc32c_prepare_stream, kept for the process).  Host entry points stage through a cached
  *     per-device workspace that only grows.
+ *   - Long blocks (the long-block lane): a block of >= 16 KiB in a descriptor or sstable batch
+ *     (> 64 KiB in a descriptor batch without a size hint) is not hashed by the wave that meets it;
+ *     it is split into 4-KiB pieces hashed on the whole GPU after the batch kernel and folded with
+ *     shift operators, on the same stream.  Results are identical either way: a stream without a
+ *     lane (captured before it was prepared), or a call whose long blocks exceed the scratch (8 GiB
+ *     of them, or 65536 blocks), hashes them on one wave each -- only the time differs.
  *   - Per-block length in batches is < 2^32 bytes (the reference narrows to uint32_t:
  *     util/crc32c.cc:19-23,589); a single span (pdb_crc32c_extend*) may be longer.
  *   - Thread-safe: host entry points serialise per device; device entry points are pure launches.
@@ -52,7 +60,8 @@
 extern "C" {
 #endif
 
-#define PDB_CRC32C_ABI_VERSION 1
+/* 2: pdb_crc32c_prepare_stream added; pdb_sst_seal_device_scratch (version 1) removed */
+#define PDB_CRC32C_ABI_VERSION 2
 
 /* One block of a batch: bytes [base+off, base+off+len), optional Extend seed. 16 bytes. */
 typedef struct pdb_blk {
@@ -98,6 +107,10 @@ int pdb_crc32c_abi_version(void);
  * stream.  Called implicitly by every entry point; explicit calls are idempotent. */
 int pdb_crc32c_init(int device);
 const char* pdb_last_error(void); /* thread-local message of the last failure */
+/* Make the long-block lane's scratch for device-resident calls on `stream` now (it is otherwise made
+ * at the stream's first call): call it before capturing device entry points on a stream into a
+ * hipGraph.  PDB_EINVAL while the stream is capturing. */
+int pdb_crc32c_prepare_stream(void* stream);
 /* Device the calling thread uses (HIP current device). */
 int pdb_crc32c_current_device(void);
 

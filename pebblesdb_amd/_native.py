@@ -11,6 +11,8 @@ import threading
 
 from .build import LIB
 
+ABI_VERSION = 2  # include/pdb_crc32c.h PDB_CRC32C_ABI_VERSION this binding is written against
+
 _lock = threading.Lock()
 _lib = None
 
@@ -42,6 +44,7 @@ SIGNATURES = {
     "pdb_host_alloc": (_I, [_U64, ctypes.POINTER(ctypes.c_void_p)]),
     "pdb_host_free": (_I, [_V]),
     "pdb_crc32c_init": (_I, [_I]),
+    "pdb_crc32c_prepare_stream": (_I, [_V]),
     "pdb_last_error": (ctypes.c_char_p, []),
     "pdb_crc32c_current_device": (_I, []),
     "pdb_crc32c_extend": (_U32, [_U32, _V, ctypes.c_size_t]),
@@ -81,6 +84,9 @@ def lib():
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
+        if L.pdb_crc32c_abi_version() != ABI_VERSION:
+            raise ImportError(f"{LIB}: ABI version {L.pdb_crc32c_abi_version()}, this binding expects {ABI_VERSION} "
+                              "(rebuild with `python -m pebblesdb_amd.build`)")
         _lib = L
     return _lib
 

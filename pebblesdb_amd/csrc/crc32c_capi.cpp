@@ -20,6 +20,20 @@
 #include "crc32c_math.h"
 
 namespace pdb {
+
+LongLane long_lane_at(uint8_t* d, const uint32_t* d_pow2) {
+  LongLane ll{};
+  if (!d) return ll;
+  ll.hdr = reinterpret_cast<unsigned long long*>(d);
+  ll.rec = reinterpret_cast<LongRec*>(d + kLongRecOff);
+  ll.piece = reinterpret_cast<LongPiece*>(d + kLongPieceOff);
+  ll.leaf = reinterpret_cast<uint32_t*>(d + kLongLeafOff);
+  ll.pow2 = d_pow2;
+  ll.rec_cap = kLongRecCap;
+  ll.piece_cap = kLongPieceCap;
+  return ll;
+}
+
 namespace {
 
 thread_local std::string g_err;
@@ -49,6 +63,7 @@ struct HostCtx {
   uint8_t* h_pin = nullptr;
   uint8_t* d_pin = nullptr;  // its device mapping (the zero-copy sst path's handles and ok bytes)
   size_t h_pin_cap = 0;
+  uint8_t* d_lane = nullptr;  // long-block lane scratch (long_scratch_bytes(), made at the first long block)
 };
 constexpr int kHostCtx = 4;
 
@@ -101,7 +116,12 @@ struct DevState {
   // clock at entry, after posting and on seeing the answer, and the server's poll / hash-done ticks;
   // the rows are written to <path> at exit
   bool stamps = false;
+  // the long-block lane of device-resident calls, one scratch per caller stream (made at the stream's
+  // first call outside a capture, or by pdb_crc32c_prepare_stream; kept for the process)
+  std::mutex lane_mu;
+  std::vector<std::pair<hipStream_t, uint8_t*>> lanes;
 };
+constexpr size_t kMaxStreamLanes = 64;
 
 struct PhaseStamp {
   uint64_t n, h0, h1, h2, g_seen, g_done;  // bytes; host CLOCK_MONOTONIC ns; s_memrealtime ticks
@@ -249,6 +269,40 @@ int get_state(DevState** out) {
 hipStream_t pick_stream(DevState* st, void* stream) {
   (void)st;
   return static_cast<hipStream_t>(stream);
+}
+
+// A zeroed long-block lane scratch, ordered before the first use on stream s.
+int alloc_lane(hipStream_t s, uint8_t** out) {
+  void* d = nullptr;
+  hipError_t e = hipMalloc(&d, long_scratch_bytes());
+  if (e != hipSuccess) return fail(PDB_ENOMEM, std::string("hipMalloc(long-block lane): ") + hipGetErrorString(e));
+  if ((e = hipMemsetAsync(d, 0, kLongHdrBytes, s)) != hipSuccess) {
+    (void)hipFree(d);
+    return hip_fail(e, "hipMemsetAsync(long-block lane)");
+  }
+  *out = static_cast<uint8_t*>(d);
+  return PDB_OK;
+}
+
+// The long-block lane for device-resident calls on `s` (crc32c_internal.h): the stream's own scratch,
+// made at its first call.  Inside a stream capture nothing is allocated: a stream that was never
+// prepared (pdb_crc32c_prepare_stream) then runs without the lane -- long blocks are hashed by the
+// batch kernel's one-wave path, with identical results.  Past kMaxStreamLanes streams, likewise.
+const LongLane* stream_lane(DevState* st, hipStream_t s, LongLane* ll, bool may_alloc = true) {
+  std::lock_guard<std::mutex> lk(st->lane_mu);
+  for (const auto& x : st->lanes)
+    if (x.first == s) {
+      *ll = long_lane_at(x.second, st->d_pow2);
+      return ll;
+    }
+  if (!may_alloc || st->lanes.size() >= kMaxStreamLanes) return nullptr;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+  uint8_t* d = nullptr;
+  if (alloc_lane(s, &d)) return nullptr;
+  st->lanes.emplace_back(s, d);
+  *ll = long_lane_at(d, st->d_pow2);
+  return ll;
 }
 
 int ensure_ws(HostCtx* c, size_t bytes) {
@@ -663,9 +717,11 @@ int host_desc(const uint8_t* base, uint64_t base_len, const pdb_blk* blk, uint64
   std::vector<HostGroup> groups;
   HostGroup g{0, 0, UINT64_MAX, 0};
   uint64_t n1k = 0, n4k = 0, n256 = 0, n512 = 0, n1023 = 0;  // size classes of the sized kernels
+  uint32_t max_len = 0;
   for (uint64_t i = 0; i < nblk; ++i) {
     if (blk[i].off > base_len || blk[i].len > base_len - blk[i].off)
       return fail(PDB_ERANGE, "block " + std::to_string(i) + " exceeds base_len");
+    max_len = std::max(max_len, blk[i].len);
     n1k += blk[i].len - 1024u <= 128u;
     n4k += blk[i].len - 4096u <= 256u;
     n256 += blk[i].len - 1u <= 255u;
@@ -720,6 +776,10 @@ int host_desc(const uint8_t* base, uint64_t base_len, const pdb_blk* blk, uint64
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
   if ((rc = ensure_ws(st, nslots * slot_bytes + 256))) return rc;
   hipStream_t s = st->stream, cs = st->copy_stream;
+  // blocks of >= 16 KiB: the long-block lane on this context's stream (crc32c_internal.h)
+  if (max_len >= kLongMinBytes && !st->d_lane && (rc = alloc_lane(s, &st->d_lane))) return rc;
+  LongLane lane_v = long_lane_at(max_len >= kLongMinBytes ? st->d_lane : nullptr, dev->d_pow2);
+  const LongLane* lane = lane_v.hdr ? &lane_v : nullptr;
   uint32_t* d_nbad = reinterpret_cast<uint32_t*>(st->d_ws + nslots * slot_bytes);
   std::vector<std::vector<pdb_blk>> rbs(groups.size());  // async H2D sources, alive until the drain
   uint32_t nb = 0;
@@ -745,7 +805,7 @@ int host_desc(const uint8_t* base, uint64_t base_len, const pdb_blk* blk, uint64
       if ((e = pipe.end_copies(k)) != hipSuccess) return hip_fail(e, "hipEventRecord(staged)");
       e = launch_desc(hgeom, dev->d_tables, ws, reinterpret_cast<const pdb_blk*>(ws + off_desc), x.count, flags,
                       mode, reinterpret_cast<const uint32_t*>(ws + off_exp), reinterpret_cast<uint32_t*>(ws + off_out),
-                      ws + off_ok, d_nbad, s);
+                      ws + off_ok, d_nbad, s, lane);
       if (e != hipSuccess) return hip_fail(e, "launch_desc");
       if (mode == kModeOut) {
         if ((e = hipMemcpyAsync(out + x.first, ws + off_out, x.count * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
@@ -1287,6 +1347,20 @@ int pdb_crc32c_init(int device) {
   return get_state(&st);
 }
 
+int pdb_crc32c_prepare_stream(void* stream) {
+  DevState* st;
+  int rc = get_state(&st);
+  if (rc) return rc;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  hipError_t e = hipStreamIsCapturing(s, &cs);
+  if (e != hipSuccess) return hip_fail(e, "hipStreamIsCapturing");
+  if (cs != hipStreamCaptureStatusNone) return fail(PDB_EINVAL, "pdb_crc32c_prepare_stream: the stream is capturing");
+  LongLane ll;
+  if (!stream_lane(st, s, &ll)) return fail(PDB_ENOMEM, "no long-block lane for this stream (" + g_err + ")");
+  return PDB_OK;
+}
+
 const char* pdb_last_error(void) { return g_err.c_str(); }
 
 int pdb_crc32c_current_device(void) {
@@ -1354,8 +1428,10 @@ int pdb_crc32c_batch_device(const void* d_base, const pdb_blk* d_blk, uint64_t n
   int rc = get_state(&st);
   if (rc) return rc;
   if ((rc = quiesce(st))) return rc;
+  const hipStream_t s = pick_stream(st, stream);
+  LongLane ll;
   hipError_t e = launch_desc(st->geom, st->d_tables, static_cast<const uint8_t*>(d_base), d_blk, nblk,
-                             flags, kModeOut, nullptr, d_out, nullptr, nullptr, pick_stream(st, stream));
+                             flags, kModeOut, nullptr, d_out, nullptr, nullptr, s, stream_lane(st, s, &ll));
   return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_desc");
 }
 
@@ -1368,8 +1444,10 @@ int pdb_crc32c_verify_device(const void* d_base, const pdb_blk* d_blk, uint64_t 
   int rc = get_state(&st);
   if (rc) return rc;
   if ((rc = quiesce(st))) return rc;
+  const hipStream_t s = pick_stream(st, stream);
+  LongLane ll;
   hipError_t e = launch_desc(st->geom, st->d_tables, static_cast<const uint8_t*>(d_base), d_blk, nblk,
-                             flags, kModeVerify, d_expected, nullptr, d_ok, d_nbad, pick_stream(st, stream));
+                             flags, kModeVerify, d_expected, nullptr, d_ok, d_nbad, s, stream_lane(st, s, &ll));
   return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_desc(verify)");
 }
 
@@ -1400,8 +1478,10 @@ int pdb_sst_seal_device(void* d_buf, uint64_t buf_len, const pdb_block_handle* d
   int rc = get_state(&st);
   if (rc) return rc;
   if ((rc = quiesce(st))) return rc;
+  const hipStream_t s = pick_stream(st, stream);
+  LongLane ll;
   hipError_t e = launch_sst(st->geom, st->d_tables, static_cast<uint8_t*>(d_buf), buf_len, d_h, n, true,
-                            nullptr, nullptr, pick_stream(st, stream));
+                            nullptr, nullptr, s, stream_lane(st, s, &ll));
   return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_sst(seal)");
 }
 
@@ -1416,8 +1496,10 @@ int pdb_sst_verify_device(const void* d_buf, uint64_t buf_len, const pdb_block_h
   int rc = get_state(&st);
   if (rc) return rc;
   if ((rc = quiesce(st))) return rc;
+  const hipStream_t s = pick_stream(st, stream);
+  LongLane ll;
   hipError_t e = launch_sst(st->geom, st->d_tables, static_cast<uint8_t*>(const_cast<void*>(d_buf)),
-                            buf_len, d_h, n, false, d_ok, d_nbad, pick_stream(st, stream));
+                            buf_len, d_h, n, false, d_ok, d_nbad, s, stream_lane(st, s, &ll));
   return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_sst(verify)");
 }
 
@@ -1430,8 +1512,10 @@ int pdb_sst_crc_device(const void* d_buf, uint64_t buf_len, const pdb_block_hand
   int rc = get_state(&st);
   if (rc) return rc;
   if ((rc = quiesce(st))) return rc;
+  const hipStream_t s = pick_stream(st, stream);
+  LongLane ll;
   hipError_t e = launch_sst_masked(st->geom, st->d_tables, static_cast<uint8_t*>(const_cast<void*>(d_buf)), buf_len,
-                                   d_h, n, d_out, pick_stream(st, stream));
+                                   d_h, n, d_out, s, stream_lane(st, s, &ll));
   return e == hipSuccess ? PDB_OK : hip_fail(e, "launch_sst_masked");
 }
 

@@ -600,6 +600,8 @@ struct FixedSrc {
   __device__ __forceinline__ BlkDesc finish(Raw i) const { return {base + i * stride, len, init_raw}; }
   __device__ __forceinline__ BlkDesc get(uint64_t i) const { return finish(i); }
   __device__ __forceinline__ BlkDesc lane(Raw i) const { return finish(i); }  // per-lane fields
+  // (a fixed stride's length is known to the host: no long-block lane)
+  __device__ __forceinline__ bool long_export(uint64_t, const BlkDesc&, uint32_t, uint32_t) const { return false; }
 };
 
 // Descriptor fields are loaded by every lane from one address, so the compiler sees per-lane
@@ -611,10 +613,50 @@ __device__ __forceinline__ uint64_t uniform64(uint32_t lo, uint32_t hi) {
   return (static_cast<uint64_t>(h) << 32) | l;
 }
 
+// The long-block lane (crc32c_internal.h): export block i (p, n bytes, seed init_raw; wave-uniform
+// arguments, every lane calling) when it has at least min_bytes and the scratch at `lane` has room:
+// lane 0 reserves a record and np = ceil(n / 4096) pieces with one compare-and-swap loop (no
+// reservation is ever left half-made, so every reserved piece is written), then the wave writes the
+// record and the piece list.  False: the caller hashes the block itself.  (A batch kernel carries
+// the scratch base alone: the layout is fixed, and every SGPR counts in these kernels.)
+__device__ __forceinline__ bool long_export(uint8_t* lane, uint32_t min_bytes, uint64_t i, uintptr_t p, uint32_t n,
+                                            uint32_t init_raw, uint32_t u) {
+  if (!lane || n < min_bytes) return false;
+  unsigned long long* hdr = reinterpret_cast<unsigned long long*>(lane);
+  const uint32_t m = (n - 1u) >> 12, np = m + 1u, h = n - (m << 12);
+  unsigned long long got = ~0ull;
+  if (u == 0) {
+    unsigned long long old = __hip_atomic_load(hdr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (;;) {
+      if ((old >> 40) >= kLongRecCap || (old & kLongPieceMask) + np > kLongPieceCap) break;
+      if (__hip_atomic_compare_exchange_strong(hdr, &old, old + ((1ull << 40) | np), __ATOMIC_RELAXED,
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        got = old;
+        break;
+      }
+    }
+  }
+  got = uniform64(__builtin_amdgcn_readlane(static_cast<uint32_t>(got), 0),
+                  __builtin_amdgcn_readlane(static_cast<uint32_t>(got >> 32), 0));
+  if (got == ~0ull) return false;
+  const uint32_t slot = static_cast<uint32_t>(got >> 40), q0 = static_cast<uint32_t>(got & kLongPieceMask);
+  LongRec* rec = reinterpret_cast<LongRec*>(lane + kLongRecOff);
+  LongPiece* piece = reinterpret_cast<LongPiece*>(lane + kLongPieceOff);
+  if (u == 0) rec[slot] = LongRec{i, static_cast<uint64_t>(p), n, init_raw, q0, np};
+  for (uint32_t k = u; k < np; k += 64u)
+    piece[q0 + k] = k ? LongPiece{static_cast<uint64_t>(p) + h + 4096ull * (k - 1u), 4096u, 0u}
+                      : LongPiece{static_cast<uint64_t>(p), h, 1u};
+  return true;
+}
+
 struct DescSrc {
   const uint8_t* base;
   const pdb_blk* blk;
   uint32_t flags;
+  uint8_t* long_lane = nullptr;  // the long-block lane's scratch (null: off)
+  __device__ __forceinline__ bool long_export(uint64_t i, const BlkDesc& d, uint32_t u, uint32_t min_bytes) const {
+    return pdb::long_export(long_lane, min_bytes, i, reinterpret_cast<uintptr_t>(d.p), d.n, d.init_raw, u);
+  }
   using Raw = u32x4;  // pdb_blk {off lo, off hi, len, init}
   __device__ __forceinline__ Raw load(uint64_t i) const {
     // 8-B alignment is all pdb_blk guarantees: a 4-B-aligned 16-B load
@@ -689,6 +731,10 @@ struct SstSrc {
   uint8_t* buf;
   const pdb_block_handle* h;
   uint64_t len;  // image bytes
+  uint8_t* long_lane = nullptr;
+  __device__ __forceinline__ bool long_export(uint64_t i, const BlkDesc& d, uint32_t u, uint32_t min_bytes) const {
+    return pdb::long_export(long_lane, min_bytes, i, reinterpret_cast<uintptr_t>(d.p), d.n, d.init_raw, u);
+  }
   using Raw = u32x4;  // pdb_block_handle {offset lo, hi, size lo, hi}
   __device__ __forceinline__ Raw load(uint64_t i) const {
     return __builtin_nontemporal_load(reinterpret_cast<const u32x4a4*>(h + i));
@@ -702,6 +748,38 @@ struct SstSrc {
   __device__ __forceinline__ BlkDesc lane(const Raw& r) const {  // per-lane fields (no readfirstlane)
     return make((static_cast<uint64_t>(r.y) << 32) | r.x, (static_cast<uint64_t>(r.w) << 32) | r.z);
   }
+};
+
+// The long-block lane's pieces (crc_longpiece_kernel): piece q = {p, n, seeded}; init_raw carries the
+// seed the sstable-sized kernel starts a 4096-B piece from (SrcSeeds): 0xFFFFFFFF for a head
+// (Value()), 0 for a full piece (raw state 0).  A head of another length takes the kernel's slow path,
+// which is Value()-seeded.
+struct PieceSrc {
+  const LongPiece* piece;
+  using Raw = u32x4;  // {p lo, p hi, n, seeded}
+  __device__ __forceinline__ Raw load(uint64_t i) const {
+    return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(piece + i));
+  }
+  __device__ __forceinline__ BlkDesc lane(const Raw& r) const {
+    return {reinterpret_cast<const uint8_t*>((static_cast<uint64_t>(r.y) << 32) | r.x), r.z, r.w ? 0xFFFFFFFFu : 0u};
+  }
+  __device__ __forceinline__ bool long_export(uint64_t, const BlkDesc&, uint32_t, uint32_t) const { return false; }
+};
+
+// Start state of a 4096-B block in the sstable-sized kernel: Value()'s seed, or the piece's own.
+template <class Src>
+struct SrcSeeds {
+  static constexpr bool kOn = false;
+};
+template <>
+struct SrcSeeds<PieceSrc> {
+  static constexpr bool kOn = true;
+};
+
+// The pieces' raw states (leaves of the long-block combine)
+struct LeafSink {
+  uint32_t* leaf;
+  __device__ __forceinline__ void put(uint64_t i, uint32_t raw, const BlkDesc&) const { leaf[i] = raw; }
 };
 
 struct OutSink {
@@ -1295,11 +1373,30 @@ __global__ __launch_bounds__(kThreads) void crc_stream16_kernel(const uint32_t* 
     } else if (m.v && ia < nend) {
       r = Meta{src.finish(ra), ia, 0, true};
       ia = next_block(ia);
+      // a block past 64 KiB goes to the long-block lane, and the wave takes the one after it (rare:
+      // that descriptor is loaded when needed)
+      while (src.long_export(r.i, r.d, u, kLongMinStream)) {
+        if (ia >= nend) {
+          r.v = false;
+          break;
+        }
+        r = Meta{src.get(ia), ia, 0, true};
+        ia = next_block(ia);
+      }
     }
     ra = src.load(ia < nend ? ia : nend - 1);
     return r;
   };
   Meta mB{src.get(i), i, 0, true};
+  while (src.long_export(mB.i, mB.d, u, kLongMinStream)) {  // (the wave's first block)
+    if (ia >= nend) {
+      mB.v = false;
+      break;
+    }
+    mB = Meta{src.finish(ra), ia, 0, true};
+    ia = next_block(ia);
+    ra = src.load(ia < nend ? ia : nend - 1);
+  }
   Buf16 B{};
   issue(B, mB.d, 0);
   uint32_t acc = 0;
@@ -1861,8 +1958,12 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
     const uint32_t L = emax <= 1 ? 0u : (emax <= 2 ? 1u : (emax <= 4 ? 2u : (emax <= 8 ? 3u : 4u)));
     const uint32_t pref = row_suffix_tree(lds, u, hash_masked(lds, lt, pf, masked_start(pf, ureg)), L, tops());
 #pragma unroll
-    for (int r = 0; r < kBlk; ++r)
-      P[r] = (kRows && G.n[r] == kMin) ? 0xFFFFFFFFu : __builtin_amdgcn_readlane(pref, kRowLanes * r + kRowLanes - 1);
+    for (int r = 0; r < kBlk; ++r) {
+      // a block of exactly kBody bytes has no prefix: its start state is the seed itself
+      // (Value()'s, or a long-block piece's own: SrcSeeds)
+      const uint32_t seed = SrcSeeds<Src>::kOn ? __builtin_amdgcn_readlane(G.ld.init_raw, r) : 0xFFFFFFFFu;
+      P[r] = (kRows && G.n[r] == kMin) ? seed : __builtin_amdgcn_readlane(pref, kRowLanes * r + kRowLanes - 1);
+    }
   };
   // one body's lane partial: chains j (16-B pieces at bs + 16u + 1024j) with the DPP neighbour
   // dword, Horner-folded with shift 1024, P injected as lane 0's start
@@ -2142,8 +2243,13 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
         Slow nxt;
         stage(nxt, idx(k + 1), rn);  // past the end: re-stages the last block (unconditional)
         rn = src.load(idx(k + 2));
-        const uint32_t raw_state = slow_finish(lds, lt, u, ureg, cur.sf, cur.p, cur.n);
-        if (u == 0) SinkOps<Sink>::put(sink, cur.i, raw_state, cur.d, cur.pre);
+        // a long block (index / filter: up to MiBs) goes to the long-block lane instead of this wave
+        const BlkDesc ud{reinterpret_cast<const uint8_t*>(cur.p), cur.n,
+                          static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(cur.d.init_raw))};
+        if (!src.long_export(cur.i, ud, u, kLongMinBytes)) {
+          const uint32_t raw_state = slow_finish(lds, lt, u, ureg, cur.sf, cur.p, cur.n);
+          if (u == 0) SinkOps<Sink>::put(sink, cur.i, raw_state, cur.d, cur.pre);
+        }
         cur = nxt;
       }
       nslow = 0;

@@ -27,20 +27,70 @@ struct LaunchGeom {
   uint32_t block;  // threads per workgroup
 };
 
-// crc32c_kernels.hip -- all launches are asynchronous on `s`.
+// ---- the long-block lane (device-resident batches) ----------------------------------------------
+// A batch kernel hashes each block on one wave (~2 GB/s), so one index or filter block of a few MiB
+// inside a batch of 4-KiB blocks would set the launch's length (a 4 MiB block: ~2 ms against ~3 us
+// for 16 MiB of data blocks).  Instead the wave that meets a block of >= its kernel's threshold
+// EXPORTS it: one atomic reserves a record and the block's pieces in a per-stream scratch, and the
+// wave writes the piece list -- a head of h = n - 4096 m bytes (1..4096, Value() seed) followed by m
+// pieces of exactly 4096 B (hashed from state 0) -- and goes on.  After the batch kernel, on the same
+// stream, crc_longpiece_kernel hashes every exported piece on the whole GPU (the sstable-sized
+// kernel's 4-KiB body path: ~HBM rate), and long_combine_kernel folds each record's leaves with the
+// power-of-two operators (R(H || S_1 .. S_m) = sum_j shift(leaf_j, 4096 (m - j)), zero leaves padded
+// in front) and hands the raw state to the batch's own sink, exactly where the batch kernel would
+// have.  A full scratch (or no scratch) leaves the block to the batch kernel's one-wave path: the
+// results never depend on the lane, only the time does.  The combine kernel's last workgroup resets
+// the counters, so the lane is allocation-free and capturable per call.
+struct LongRec {     // 32 B
+  uint64_t i;        // block index in the batch
+  uint64_t p;        // block address
+  uint32_t n;        // bytes under the CRC
+  uint32_t init_raw; // ~Extend seed (0xFFFFFFFF: Value)
+  uint32_t q0, np;   // its pieces (= leaves) q0 .. q0 + np - 1, the head first
+};
+struct LongPiece {   // 16 B
+  uint64_t p;
+  uint32_t n;        // 4096, or the head's 1..4096
+  uint32_t seeded;   // 1: the head (Value() seed), 0: a full piece (state 0)
+};
+struct LongLane {
+  unsigned long long* hdr;  // [0] = records << 40 | pieces reserved; [1] = combine workgroups done
+  LongRec* rec;
+  LongPiece* piece;
+  uint32_t* leaf;           // raw state of piece q
+  const uint32_t* pow2;     // the 64 power-of-two shift operators (1024 u32 each)
+  uint32_t rec_cap, piece_cap;
+};
+constexpr uint32_t kLongRecCap = 1u << 16;
+constexpr uint32_t kLongPieceCap = 1u << 21;  // 8 GiB of long blocks per call
+constexpr unsigned long long kLongPieceMask = (1ull << 40) - 1;
+constexpr uint32_t kLongMinBytes = 16u << 10;         // sstable-sized and record kernels
+constexpr uint32_t kLongMinStream = (64u << 10) + 1;  // the any-length stream kernel (C3's 1..64 KiB stay)
+// scratch layout: [hdr 256 B][records][pieces][leaves] (a batch kernel carries only the base)
+constexpr size_t kLongHdrBytes = 256;
+constexpr size_t kLongRecOff = kLongHdrBytes;
+constexpr size_t kLongPieceOff = kLongRecOff + size_t(kLongRecCap) * sizeof(LongRec);
+constexpr size_t kLongLeafOff = kLongPieceOff + size_t(kLongPieceCap) * sizeof(LongPiece);
+constexpr size_t long_scratch_bytes() { return kLongLeafOff + size_t(kLongPieceCap) * 4; }
+// The lane over a zeroed scratch of long_scratch_bytes() at d (null d: no lane).
+LongLane long_lane_at(uint8_t* d, const uint32_t* d_pow2);
+
+// crc32c_kernels.hip -- all launches are asynchronous on `s`.  `ll`: the long-block lane (null: none;
+// every block is then hashed by the batch kernel itself).
 hipError_t launch_fixed(const LaunchGeom& g, const uint32_t* d_tables, const uint8_t* base,
                         uint64_t stride, uint32_t len, uint64_t nblk, uint32_t flags, uint32_t init,
                         uint32_t* out, hipStream_t s);
 hipError_t launch_desc(const LaunchGeom& g, const uint32_t* d_tables, const uint8_t* base,
                        const pdb_blk* blk, uint64_t nblk, uint32_t flags, int mode,
                        const uint32_t* expected, uint32_t* out, uint8_t* ok, uint32_t* nbad,
-                       hipStream_t s);
+                       hipStream_t s, const LongLane* ll = nullptr);
 hipError_t launch_sst(const LaunchGeom& g, const uint32_t* d_tables, uint8_t* buf, uint64_t buf_len,
                       const pdb_block_handle* h, uint64_t n, bool seal, uint8_t* ok, uint32_t* nbad,
-                      hipStream_t s);
+                      hipStream_t s, const LongLane* ll = nullptr);
 // out[i] = Mask(crc32c(contents_i || type_i)) -- the trailer word a seal writes, as an array.
 hipError_t launch_sst_masked(const LaunchGeom& g, const uint32_t* d_tables, uint8_t* buf, uint64_t buf_len,
-                             const pdb_block_handle* h, uint64_t n, uint32_t* out, hipStream_t s);
+                             const pdb_block_handle* h, uint64_t n, uint32_t* out, hipStream_t s,
+                             const LongLane* ll = nullptr);
 // Long span: raw CRCs of `nseg` segments of 2^seg_log2 bytes (+ the tail) in parallel, then a
 // one-workgroup tree combine with the power-of-two operators.  `scratch` holds
 // span_scratch_words(n) u32.  *out = Extend(init, data[0..n)).  Segments of at least

@@ -112,6 +112,96 @@ __global__ __launch_bounds__(1024) void span_combine_many_kernel(const uint32_t*
   if (threadIdx.x == 0) out[blockIdx.x] = ~sw[0];
 }
 
+// ---- the long-block lane (crc32c_internal.h): pieces, then one combine per record ----------------
+// Every piece the batch kernel exported, hashed by the sstable-sized kernel over a piece list (a full
+// piece: exactly its 4-KiB body path, started from state 0; a head: Value()'s seed -- the fast path
+// at 4096 B, the slow path below), one raw state per piece.  The count is read on the device: the
+// launch is made whether or not anything was exported, and returns at once when nothing was.
+__global__ __launch_bounds__(kThreads) void crc_longpiece_kernel(const uint32_t* __restrict__ tabs, LongLane ll) {
+  const uint64_t np = ll.hdr[0] & kLongPieceMask;
+  if (np == 0) return;
+  sized_kernel_body<PieceSrc, LeafSink, true, 4>(tabs, PieceSrc{ll.piece}, np, LeafSink{ll.leaf});
+}
+
+// op_k(c) through a power-of-two operator (4 x 256 entries) in LDS or global memory
+__device__ __forceinline__ uint32_t apply_op(const uint32_t* op, uint32_t c) {
+  return op[c & 0xffu] ^ op[256u + ((c >> 8) & 0xffu)] ^ op[512u + ((c >> 16) & 0xffu)] ^ op[768u + (c >> 24)];
+}
+
+constexpr uint32_t kCombLog2 = 13;  // leaves folded in LDS at once (2^13 = 32 MiB of block)
+constexpr uint32_t kComb = 1u << kCombLog2;
+
+// Workgroup r folds record r's leaves (front-padded with zero leaves to a power of two, or to a
+// multiple of 2^13 in chunks, each chunk's root shifted on by 2^13 pieces = 32 MiB), corrects an
+// Extend seed (R_s(B) = R_FFFFFFFF(B) ^ shift(s ^ 0xFFFFFFFF, n)), and hands the raw state to the
+// batch's sink.  The last workgroup to finish resets the lane's counters for the next call.
+template <class Sink>
+__global__ __launch_bounds__(1024) void long_combine_kernel(LongLane ll, Sink sink) {
+  __shared__ uint32_t sw[kComb];
+  __shared__ uint32_t ops[kCombLog2][1024];  // level k: shift 4096 << k (power-of-two operator 12 + k)
+  const unsigned long long hw = ll.hdr[0];
+  const uint32_t nrec = static_cast<uint32_t>(hw >> 40);
+  if (nrec == 0) return;  // (grid-uniform: nothing exported, nothing to reset)
+  const uint32_t t = threadIdx.x;
+  if (blockIdx.x < nrec) {
+    for (uint32_t i = t; i < kCombLog2 * 1024u; i += blockDim.x) ops[i >> 10][i & 1023u] = ll.pow2[12u * 1024u + i];
+    for (uint32_t r = blockIdx.x; r < nrec; r += gridDim.x) {
+      const LongRec R = ll.rec[r];
+      uint32_t ml = 0;
+      while ((1u << ml) < R.np && ml < kCombLog2) ++ml;
+      const uint32_t M = 1u << ml, nc = (R.np + M - 1u) / M;
+      const uint32_t pad = nc * M - R.np;
+      uint32_t acc = 0;  // (thread 0)
+      for (uint32_t c = 0; c < nc; ++c) {
+        __syncthreads();  // the previous fold's root has been read
+        for (uint32_t j = t; j < M; j += blockDim.x) {
+          const uint32_t v = c * M + j;
+          sw[j] = v < pad ? 0u : ll.leaf[R.q0 + (v - pad)];
+        }
+        __syncthreads();
+        for (uint32_t k = 0; k < ml; ++k) {
+          const uint32_t half = 1u << k, pairs = M >> (k + 1);
+          for (uint32_t j = t; j < pairs; j += blockDim.x) {
+            const uint32_t i = j << (k + 1);
+            sw[i] = apply_op(ops[k], sw[i]) ^ sw[i + half];
+          }
+          __syncthreads();
+        }
+        if (t == 0) acc = c ? apply_op(ll.pow2 + (12u + kCombLog2) * 1024u, acc) ^ sw[0] : sw[0];
+      }
+      if (t == 0) {
+        uint32_t raw = acc;
+        if (R.init_raw != 0xFFFFFFFFu) {  // an Extend seed (descriptor batches with PDB_CRC_USE_INIT)
+          uint32_t x = R.init_raw ^ 0xFFFFFFFFu;
+          for (uint32_t k = 0; k < 32u; ++k)
+            if ((R.n >> k) & 1u) x = apply_op(ll.pow2 + k * 1024u, x);
+          raw ^= x;
+        }
+        const BlkDesc d{reinterpret_cast<const uint8_t*>(R.p), R.n, R.init_raw};
+        SinkOps<Sink>::put(sink, R.i, raw, d, SinkOps<Sink>::pre(sink, R.i, d));
+      }
+    }
+  }
+  __syncthreads();
+  if (t == 0) {
+    __threadfence();
+    if (atomicAdd(ll.hdr + 1, 1ull) + 1ull == gridDim.x) {
+      ll.hdr[0] = 0ull;
+      ll.hdr[1] = 0ull;
+    }
+  }
+}
+
+// The lane's two launches after a batch kernel with sink `sink` (same stream)
+template <class Sink>
+hipError_t launch_long(const LaunchGeom& g, const uint32_t* d_tables, const LongLane* ll, const Sink& sink, hipStream_t s) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || !ll || !ll->hdr) return e;
+  hipLaunchKernelGGL(crc_longpiece_kernel, dim3(g.grid), dim3(kThreads), 0, s, d_tables, *ll);
+  hipLaunchKernelGGL((long_combine_kernel<Sink>), dim3(g.grid), dim3(1024), 0, s, *ll, sink);
+  return hipGetLastError();
+}
+
 }  // namespace
 
 hipError_t launch_span_many(const LaunchGeom& g, const uint32_t* d_tables, const uint32_t* d_pow2, const uint8_t* base,
@@ -228,47 +318,57 @@ hipError_t launch_desc_sink(const LaunchGeom& g, const uint32_t* d_tables, const
 hipError_t launch_desc(const LaunchGeom& g, const uint32_t* d_tables, const uint8_t* base,
                        const pdb_blk* blk, uint64_t nblk, uint32_t flags, int mode,
                        const uint32_t* expected, uint32_t* out, uint8_t* ok, uint32_t* nbad,
-                       hipStream_t s) {
+                       hipStream_t s, const LongLane* ll) {
   if (nblk == 0) return hipSuccess;
-  const DescSrc src{base, blk, flags};
-  if (mode == kModeOut) return launch_desc_sink(g, d_tables, src, nblk, flags, OutSink{out, flags}, s);
-  return launch_desc_sink(g, d_tables, src, nblk, flags, VerifySink{expected, ok, nbad, flags}, s);
+  DescSrc src{base, blk, flags};
+  if (ll) src.long_lane = reinterpret_cast<uint8_t*>(ll->hdr);
+  if (mode == kModeOut) {
+    const OutSink sink{out, flags};
+    (void)launch_desc_sink(g, d_tables, src, nblk, flags, sink, s);
+    return launch_long(g, d_tables, ll, sink, s);
+  }
+  const VerifySink sink{expected, ok, nbad, flags};
+  (void)launch_desc_sink(g, d_tables, src, nblk, flags, sink, s);
+  return launch_long(g, d_tables, ll, sink, s);
 }
 
 hipError_t launch_sst(const LaunchGeom& g, const uint32_t* d_tables, uint8_t* buf, uint64_t buf_len,
                       const pdb_block_handle* h, uint64_t n, bool seal, uint8_t* ok, uint32_t* nbad,
-                      hipStream_t s) {
+                      hipStream_t s, const LongLane* ll) {
   if (n == 0) return hipSuccess;
   const dim3 grid(grid_for(g, n)), block(kThreads);
   // exact 4-KiB body + batched prefix for the 4096..4352-B blocks (every data block TableBuilder
-  // emits: contents + type), the slow path in the same launch for the rest
+  // emits: contents + type), the slow path in the same launch for the rest, and the long-block lane
+  // for blocks of >= 16 KiB (a table's index and filter blocks)
   // (profiles/r01_ab_sst4k.json: verify +45 %, seal +27 % over crc_stream16_kernel)
-  const SstSrc src{buf, h, buf_len};  // handles outside the image are reported, never followed
+  SstSrc src{buf, h, buf_len};  // handles outside the image are reported, never followed
+  if (ll) src.long_lane = reinterpret_cast<uint8_t*>(ll->hdr);
   // seal: each wave parks its trailers (4 per lane) and writes them 64 groups later or when it is
   // done -- writing a trailer soon after its line was read costs more (DESIGN.md §6.0, f2:
   // +4.8 % over writing each group's trailers when hashed; diagnostics variant 72 is that form)
-  if (seal)
+  if (seal) {
     hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ParkSealSink<64>, true>), grid, block, 0, s, d_tables, src, n,
                        ParkSealSink<64>{});
-  else  // verify: 12 waves (168 VGPRs a lane: 32 B of spills instead of 124 at 16 waves), +1.2-1.7 % in
-        // A/B both orders (profiles/r03_waves/; diagnostics 127 / 128 / 129 = 12 / 8 / 16 waves)
-    hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstVerifySink, true, 4, QuadTabs, false, true, 12>), grid, dim3(768), 0,
-                       s, d_tables, src, n, SstVerifySink{ok, nbad});
-  return hipGetLastError();
+    return launch_long(g, d_tables, ll, ParkSealSink<64>{}, s);
+  }
+  // verify: 12 waves (168 VGPRs a lane: 32 B of spills instead of 124 at 16 waves), +1.2-1.7 % in
+  // A/B both orders (profiles/r03_waves/; diagnostics 127 / 128 / 129 = 12 / 8 / 16 waves)
+  hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstVerifySink, true, 4, QuadTabs, false, true, 12>), grid, dim3(768), 0,
+                     s, d_tables, src, n, SstVerifySink{ok, nbad});
+  return launch_long(g, d_tables, ll, SstVerifySink{ok, nbad}, s);
 }
 
 hipError_t launch_sst_masked(const LaunchGeom& g, const uint32_t* d_tables, uint8_t* buf, uint64_t buf_len,
-                             const pdb_block_handle* h, uint64_t n, uint32_t* out, hipStream_t s) {
+                             const pdb_block_handle* h, uint64_t n, uint32_t* out, hipStream_t s, const LongLane* ll) {
   if (n == 0) return hipSuccess;
   // the seal's masked CRCs into a compact array (pdb_sst_crc_device; the host seal brings back 4 B
   // per block across PCIe, not the span)
-  const SstSrc src{buf, h, buf_len};
+  SstSrc src{buf, h, buf_len};
+  if (ll) src.long_lane = reinterpret_cast<uint8_t*>(ll->hdr);
   // (12 waves: fewer spills, +0.7 % in A/B, profiles/r03_waves/ab_waves2.log; diagnostics 131 / 132)
   hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, SstCrcSink, true, 4, QuadTabs, false, true, 12>), dim3(grid_for(g, n)),
                      dim3(768), 0, s, d_tables, src, n, SstCrcSink{out});
-  return hipGetLastError();
+  return launch_long(g, d_tables, ll, SstCrcSink{out}, s);
 }
-
-
 
 }  // namespace pdb

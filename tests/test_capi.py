@@ -90,7 +90,7 @@ def test_library_is_gfx950_code(lib):
 
 
 def test_abi_version_and_pure_helpers(lib):
-    assert lib.pdb_crc32c_abi_version() == 1
+    assert lib.pdb_crc32c_abi_version() == 2
     assert crc32c.mask(0) == 0xA282EAD8
     for c in (0, 1, 0x8A9136AA, 0xFFFFFFFF, 0x12345678):
         assert crc32c.unmask(crc32c.mask(c)) == c
