@@ -26,10 +26,11 @@
  *     caller stream, made at the stream's first call outside a capture or by
  *     pdb_crc32c_prepare_stream, kept for the process).  Host entry points stage through a cached
  *     per-device workspace that only grows.
- *   - Long blocks (the long-block lane): a block of >= 16 KiB in a descriptor or sstable batch
- *     (> 64 KiB in a descriptor batch without a size hint) is not hashed by the wave that meets it;
- *     it is split into 4-KiB pieces hashed on the whole GPU after the batch kernel and folded with
- *     shift operators, on the same stream.  Results are identical either way: a stream without a
+ *   - Long blocks (the long-block lane): a block of >= 16 KiB in an sstable batch or a
+ *     PDB_CRC_SIZE_4K descriptor batch (> 64 KiB in a descriptor batch without a size hint) is not
+ *     hashed by the wave that meets it; it is split into 4-KiB pieces hashed on the whole GPU after
+ *     the batch kernel and folded with shift operators, on the same stream.  (Descriptor batches
+ *     with a WAL-record hint -- _256 / _512 / _1023 / _1K -- take no lane: log records are <= 32 KiB.)  Results are identical either way: a stream without a
  *     lane (captured before it was prepared), or a call whose long blocks exceed the scratch (8 GiB
  *     of them, or 65536 blocks), hashes them on one wave each -- only the time differs.
  *   - Per-block length in batches is < 2^32 bytes (the reference narrows to uint32_t:

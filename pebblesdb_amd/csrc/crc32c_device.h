@@ -602,6 +602,7 @@ struct FixedSrc {
   __device__ __forceinline__ BlkDesc lane(Raw i) const { return finish(i); }  // per-lane fields
   // (a fixed stride's length is known to the host: no long-block lane)
   __device__ __forceinline__ bool long_export(uint64_t, const BlkDesc&, uint32_t, uint32_t) const { return false; }
+  __device__ __forceinline__ bool long_export_cold(uint64_t, const BlkDesc&, uint32_t, uint32_t) const { return false; }
 };
 
 // Descriptor fields are loaded by every lane from one address, so the compiler sees per-lane
@@ -649,13 +650,29 @@ __device__ __forceinline__ bool long_export(uint8_t* lane, uint32_t min_bytes, u
   return true;
 }
 
+// The same as a real call, made only for a block already known to be long (the caller tests the
+// length inline): inlined into the sstable-sized kernel's drain, the export changes the register
+// allocation of the whole kernel (more spills: verify -1 %, in-place seal -0.4 % on one box,
+// tools/ab_lane.sh, profiles/r06/ab_lane/); as a call on that cold path it costs nothing.  (In the
+// stream kernel's block loop any call site costs C3 6-7 %: it keeps the inline form.)
+__device__ __attribute__((noinline)) bool long_export_call(uint8_t* lane, uint32_t min_bytes, uint64_t i, uintptr_t p,
+                                                           uint32_t n, uint32_t init_raw, uint32_t u) {
+  return long_export(lane, min_bytes, i, p, n, init_raw, u);
+}
+
 struct DescSrc {
   const uint8_t* base;
   const pdb_blk* blk;
   uint32_t flags;
   uint8_t* long_lane = nullptr;  // the long-block lane's scratch (null: off)
+  // inline (the stream kernel's block loop: a call site there costs C3 6-7 %, tools/ab_lane.sh)
   __device__ __forceinline__ bool long_export(uint64_t i, const BlkDesc& d, uint32_t u, uint32_t min_bytes) const {
     return pdb::long_export(long_lane, min_bytes, i, reinterpret_cast<uintptr_t>(d.p), d.n, d.init_raw, u);
+  }
+  // as a call, for a block already known to be deferred (the sstable-sized kernel's drain)
+  __device__ __forceinline__ bool long_export_cold(uint64_t i, const BlkDesc& d, uint32_t u, uint32_t min_bytes) const {
+    return long_lane && d.n >= min_bytes &&
+           pdb::long_export_call(long_lane, min_bytes, i, reinterpret_cast<uintptr_t>(d.p), d.n, d.init_raw, u);
   }
   using Raw = u32x4;  // pdb_blk {off lo, off hi, len, init}
   __device__ __forceinline__ Raw load(uint64_t i) const {
@@ -732,8 +749,14 @@ struct SstSrc {
   const pdb_block_handle* h;
   uint64_t len;  // image bytes
   uint8_t* long_lane = nullptr;
+  // inline (the stream kernel's block loop: a call site there costs C3 6-7 %, tools/ab_lane.sh)
   __device__ __forceinline__ bool long_export(uint64_t i, const BlkDesc& d, uint32_t u, uint32_t min_bytes) const {
     return pdb::long_export(long_lane, min_bytes, i, reinterpret_cast<uintptr_t>(d.p), d.n, d.init_raw, u);
+  }
+  // as a call, for a block already known to be deferred (the sstable-sized kernel's drain)
+  __device__ __forceinline__ bool long_export_cold(uint64_t i, const BlkDesc& d, uint32_t u, uint32_t min_bytes) const {
+    return long_lane && d.n >= min_bytes &&
+           pdb::long_export_call(long_lane, min_bytes, i, reinterpret_cast<uintptr_t>(d.p), d.n, d.init_raw, u);
   }
   using Raw = u32x4;  // pdb_block_handle {offset lo, hi, size lo, hi}
   __device__ __forceinline__ Raw load(uint64_t i) const {
@@ -764,6 +787,7 @@ struct PieceSrc {
     return {reinterpret_cast<const uint8_t*>((static_cast<uint64_t>(r.y) << 32) | r.x), r.z, r.w ? 0xFFFFFFFFu : 0u};
   }
   __device__ __forceinline__ bool long_export(uint64_t, const BlkDesc&, uint32_t, uint32_t) const { return false; }
+  __device__ __forceinline__ bool long_export_cold(uint64_t, const BlkDesc&, uint32_t, uint32_t) const { return false; }
 };
 
 // Start state of a 4096-B block in the sstable-sized kernel: Value()'s seed, or the piece's own.
@@ -2246,7 +2270,7 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
         // a long block (index / filter: up to MiBs) goes to the long-block lane instead of this wave
         const BlkDesc ud{reinterpret_cast<const uint8_t*>(cur.p), cur.n,
                           static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(cur.d.init_raw))};
-        if (!src.long_export(cur.i, ud, u, kLongMinBytes)) {
+        if (!src.long_export_cold(cur.i, ud, u, kLongMinBytes)) {
           const uint32_t raw_state = slow_finish(lds, lt, u, ureg, cur.sf, cur.p, cur.n);
           if (u == 0) SinkOps<Sink>::put(sink, cur.i, raw_state, cur.d, cur.pre);
         }

@@ -136,7 +136,7 @@ constexpr uint32_t kComb = 1u << kCombLog2;
 // Extend seed (R_s(B) = R_FFFFFFFF(B) ^ shift(s ^ 0xFFFFFFFF, n)), and hands the raw state to the
 // batch's sink.  The last workgroup to finish resets the lane's counters for the next call.
 template <class Sink>
-__global__ __launch_bounds__(1024) void long_combine_kernel(LongLane ll, Sink sink) {
+__global__ __launch_bounds__(256) void long_combine_kernel(LongLane ll, Sink sink) {
   __shared__ uint32_t sw[kComb];
   __shared__ uint32_t ops[kCombLog2][1024];  // level k: shift 4096 << k (power-of-two operator 12 + k)
   const unsigned long long hw = ll.hdr[0];
@@ -198,7 +198,7 @@ hipError_t launch_long(const LaunchGeom& g, const uint32_t* d_tables, const Long
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !ll || !ll->hdr) return e;
   hipLaunchKernelGGL(crc_longpiece_kernel, dim3(g.grid), dim3(kThreads), 0, s, d_tables, *ll);
-  hipLaunchKernelGGL((long_combine_kernel<Sink>), dim3(g.grid), dim3(1024), 0, s, *ll, sink);
+  hipLaunchKernelGGL((long_combine_kernel<Sink>), dim3(g.grid), dim3(256), 0, s, *ll, sink);  // (4 waves: a cheap empty launch)
   return hipGetLastError();
 }
 
@@ -320,6 +320,12 @@ hipError_t launch_desc(const LaunchGeom& g, const uint32_t* d_tables, const uint
                        const uint32_t* expected, uint32_t* out, uint8_t* ok, uint32_t* nbad,
                        hipStream_t s, const LongLane* ll) {
   if (nblk == 0) return hipSuccess;
+  // small-record hints (WAL / MANIFEST records: physical records are <= 32 KiB, log_format.h:24-33)
+  // take no long-block lane: its two launches would cost those batches 1-2 % (tools/ab_lane.sh), and
+  // a record outside the class is hashed by the record kernel's whole-wave path
+  const bool small = (flags & (PDB_CRC_SIZE_1K | PDB_CRC_SIZE_256 | PDB_CRC_SIZE_512 | PDB_CRC_SIZE_1023)) &&
+                     !(flags & (PDB_CRC_USE_INIT | PDB_CRC_SIZE_4K));
+  if (small) ll = nullptr;
   DescSrc src{base, blk, flags};
   if (ll) src.long_lane = reinterpret_cast<uint8_t*>(ll->hdr);
   if (mode == kModeOut) {

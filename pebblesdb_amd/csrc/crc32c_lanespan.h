@@ -483,9 +483,6 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
       sb &= sb - 1;
       const uintptr_t sp = static_cast<uintptr_t>(uniform64(__builtin_amdgcn_readlane(plo, k), __builtin_amdgcn_readlane(phi, k)));
       const uint32_t sn = __builtin_amdgcn_readlane(bn, k);
-      // a long record goes to the long-block lane (crc32c_internal.h) instead of this wave
-      if (src.long_export(b_r0 + k, BlkDesc{reinterpret_cast<const uint8_t*>(sp), sn, 0xFFFFFFFFu}, u, kLongMinBytes))
-        continue;
       const uint32_t rs = span_slow_record<TP>(lds, lt, u, ureg, sp, sn);
       if (u == 0)
         SinkOps<Sink>::put(sink, b_r0 + k, rs, BlkDesc{reinterpret_cast<const uint8_t*>(sp), sn, 0xFFFFFFFFu},

@@ -3,7 +3,8 @@ descriptor batches hand every block of >= 16 KiB (> 64 KiB without a size hint) 
 hashed on the whole GPU and folded with shift operators, instead of one wave.  Every trailer, CRC,
 ok byte and mismatch count below is checked against the oracle (oracle/crc32c_oracle.c, pinned by
 tests/golden): 64 KiB / 1.3 MiB / 4 MiB blocks inside 16 MiB of 4-KiB blocks for seal, verify, crc
-and descriptor batches (every size hint, Extend seeds), the thresholds +-1, a 40 MiB block (two LDS
+and descriptor batches (no hint and the 4K hint with the lane; Extend seeds; the WAL-record hints,
+which take no lane, exact on the one-wave path), the thresholds +-1, a 40 MiB block (two LDS
 chunks in the combine), the scratch overflowing (more long blocks than records), host batches, and
 a captured hipGraph on a prepared and on an unprepared stream.
 
@@ -137,9 +138,9 @@ def test_long_lane_overflow(crc, oracle_lib):
     one-wave path in the same launch, and every trailer is still exact."""
     from pebblesdb_amd import table as T
 
-    n = 70000
+    n = 72000
     rng = np.random.Generator(np.random.PCG64(23))
-    sizes = np.where(rng.random(n) < 0.9, 16384 + rng.integers(0, 64, size=n), 4170).astype(np.int64)
+    sizes = np.where(np.arange(n) % 20 != 7, 16384 + rng.integers(0, 64, size=n), 4170).astype(np.int64)
     offs = np.concatenate([[0], np.cumsum(sizes + 5)[:-1]]).astype(np.int64)
     total = int(offs[-1] + sizes[-1] + 5)
     d = torch.empty(total, dtype=torch.uint8, device="cuda")
