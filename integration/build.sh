@@ -19,6 +19,8 @@
 #   pdb_verify_gpu         integration/pdb_verify.cc: the same tool with every checksum of a file
 #                          checked in one GPU batch (data blocks / pdb::log::ReplayLog), over the
 #                          engine with pdb_format.cc (a damaged table's walk checks on the GPU too)
+#   pdb_tablegen          integration/pdb_tablegen.cc: one real sstable (data, filter, metaindex, index
+#                          blocks) from the reference TableBuilder as shipped (bench.py sst_tables)
 #   table_scan_ref / _gpu  integration/pdb_table_scan.cc: one verified scan of a table through the
 #                          reference's table reader / pdb_table.cc (parity of what a reader sees)
 set -euo pipefail
@@ -75,6 +77,7 @@ $CXX $DEFS $HOOKI -DPDB_HOOKS=0 -c "$HERE/pdb_dbbench.cc" -o "$B/obj_hooks/dbben
 $CXX $DEFS $HOOKI -DPDB_HOOKS=1 -c "$HERE/pdb_dbbench.cc" -o "$B/obj_hooks/dbbench_hooks.o"
 $CXX $DEFS $HOOKI -c "$ROOT/oracle/ref_sstwriter.cc" -o "$B/obj_hooks/sstwriter.o"
 $CXX $DEFS $HOOKI -c "$HERE/pdb_verify.cc" -o "$B/obj_hooks/pdb_verify.o"
+$CXX $DEFS $HOOKI -c "$HERE/pdb_tablegen.cc" -o "$B/obj_hooks/pdb_tablegen.o"
 $CXX $DEFS $HOOKI -DPDB_HOOKS=0 -c "$HERE/pdb_table_scan.cc" -o "$B/obj_hooks/table_scan_ref.o"
 $CXX $DEFS $HOOKI -DPDB_HOOKS=1 -c "$HERE/pdb_table_scan.cc" -o "$B/obj_hooks/table_scan_gpu.o"
 
@@ -97,6 +100,8 @@ $CXX -o "$B/sstwriter_gpu" "$B/obj_hooks/sstwriter.o" $HOOKS $(objs "$B/obj_ref"
 $CXX -o "$B/leveldb_verify_ref" $(objs "$B/obj_ref" leveldb-verify.cc $ENGINE $TABLE_REF util/crc32c.cc)
 $CXX -o "$B/pdb_verify_gpu" "$B/obj_hooks/pdb_verify.o" "$B/obj_hooks/pdb_format.o" \
   $(objs "$B/obj_ref" $ENGINE table/table_builder.cc table/table.cc util/crc32c.cc) $GPU
+# real tables for bench.py --workload sst_tables: the reference TableBuilder as shipped (CPU CRC)
+$CXX -o "$B/pdb_tablegen" "$B/obj_hooks/pdb_tablegen.o" $(objs "$B/obj_ref" $ENGINE $TABLE_REF util/crc32c.cc)
 $CXX -o "$B/table_scan_ref" "$B/obj_hooks/table_scan_ref.o" $(objs "$B/obj_ref" $ENGINE $TABLE_REF util/crc32c.cc)
 $CXX -o "$B/table_scan_gpu" "$B/obj_hooks/table_scan_gpu.o" $HOOKS $(objs "$B/obj_ref" $ENGINE util/crc32c.cc) $GPU
-echo "built $B/{table_scan_ref,table_scan_gpu,pdb_dbbench_cpu,pdb_dbbench_gpu_table,pdb_dbbench_gpu_table_noscan,pdb_dbbench_gpu_all,pdb_dbbench_buffered_cpu,sstwriter_gpu,leveldb_verify_ref,pdb_verify_gpu}"
+echo "built $B/{pdb_tablegen,table_scan_ref,table_scan_gpu,pdb_dbbench_cpu,pdb_dbbench_gpu_table,pdb_dbbench_gpu_table_noscan,pdb_dbbench_gpu_all,pdb_dbbench_buffered_cpu,sstwriter_gpu,leveldb_verify_ref,pdb_verify_gpu}"

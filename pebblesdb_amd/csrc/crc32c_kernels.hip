@@ -342,7 +342,7 @@ hipError_t launch_sst(const LaunchGeom& g, const uint32_t* d_tables, uint8_t* bu
                       const pdb_block_handle* h, uint64_t n, bool seal, uint8_t* ok, uint32_t* nbad,
                       hipStream_t s, const LongLane* ll) {
   if (n == 0) return hipSuccess;
-  const dim3 grid(grid_for(g, n)), block(kThreads);
+  const dim3 grid(grid_for(g, n));
   // exact 4-KiB body + batched prefix for the 4096..4352-B blocks (every data block TableBuilder
   // emits: contents + type), the slow path in the same launch for the rest, and the long-block lane
   // for blocks of >= 16 KiB (a table's index and filter blocks)
@@ -351,10 +351,12 @@ hipError_t launch_sst(const LaunchGeom& g, const uint32_t* d_tables, uint8_t* bu
   if (ll) src.long_lane = reinterpret_cast<uint8_t*>(ll->hdr);
   // seal: each wave parks its trailers (4 per lane) and writes them 64 groups later or when it is
   // done -- writing a trailer soon after its line was read costs more (DESIGN.md §6.0, f2:
-  // +4.8 % over writing each group's trailers when hashed; diagnostics variant 72 is that form)
+  // +4.8 % over writing each group's trailers when hashed; diagnostics variant 72 is that form).
+  // 12 waves (168 VGPRs a lane: 10 spills instead of 44-53 at 16 waves): +2.5 % over round 5's
+  // 16-wave seal, both orders on one box (tools/ab_lane.sh, profiles/r06/ab_lane/ab_seal.log)
   if (seal) {
-    hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ParkSealSink<64>, true>), grid, block, 0, s, d_tables, src, n,
-                       ParkSealSink<64>{});
+    hipLaunchKernelGGL((crc_sst4k_kernel<SstSrc, ParkSealSink<64>, true, 4, QuadTabs, false, true, 12>), grid, dim3(768), 0,
+                       s, d_tables, src, n, ParkSealSink<64>{});
     return launch_long(g, d_tables, ll, ParkSealSink<64>{}, s);
   }
   // verify: 12 waves (168 VGPRs a lane: 32 B of spills instead of 124 at 16 waves), +1.2-1.7 % in
