@@ -47,10 +47,14 @@ def parse():
     ap.add_argument("--settle", type=int, default=300,
                     help="untimed launches after the timed region before the steady-state re-timing (0: skip)")
     ap.add_argument("--workload", default="c2", choices=["c2", "c3", "sstable", "sst_verify", "sst_seal", "sst_crc",
-                                                        "wal", "wal100", "wal400", "wal1000"],
+                                                        "sst_tables", "wal", "wal100", "wal400", "wal1000"],
                     help="c2 (default, the headline) / c3: BASELINE configs; sstable: the C2 blocks in "
                          "sstable layout; sst_verify / sst_seal: SURVEY §8(f) rows 1-2 on a device sstable "
-                         "image of ~4.17-KiB blocks; wal: row 3, the log record CRC over 32-KiB log blocks")
+                         "image of ~4.17-KiB blocks; sst_tables: pdb_sst_verify_device over REAL tables (data, "
+                         "filter, metaindex and index blocks) written by the reference TableBuilder; wal: row 3, "
+                         "the log record CRC over 32-KiB log blocks")
+    ap.add_argument("--tables", type=int, default=4, help="sst_tables: tables per GPU")
+    ap.add_argument("--table-keys", type=int, default=1000000, help="sst_tables: keys per table (1 KiB values)")
     ap.add_argument("--nblk", type=int, default=None,
                     help="blocks per GPU (c2/sstable); default 1M (C2) on one GPU and, for c2 with --gpus N > 1, "
                          "BASELINE config 4's 4 194 304 (16 GiB per GPU: 128 GiB over 8 GPUs)")
@@ -202,6 +206,52 @@ def wal_layout(total_bytes: int, payload: int, block: int = 32768):
         if pos == end:
             end += block
     return np.asarray(offs, dtype=np.int64), np.asarray(lens, dtype=np.int64)
+
+
+def real_tables(ntables: int, nkeys: int, value_size: int, seed: int):
+    """`ntables` real sstables written by the reference engine's TableBuilder as shipped
+    (integration/_build/pdb_tablegen, built by integration/build.sh from the reference sources in
+    place; CPU CRC trailers), in parallel, into a temporary directory on this host, concatenated.
+    Returns (image bytes, handles of every block -- data blocks from each index block, then the
+    filter block from the metaindex, the metaindex and the index (table/table.cc:70-170) -- rebased
+    on the image, per-table facts)."""
+    import shutil
+    import subprocess
+    import tempfile
+
+    from pebblesdb_amd import crc32c
+    from pebblesdb_amd import table as T
+
+    exe = os.path.join(ROOT, "integration", "_build", "pdb_tablegen")
+    if not os.path.exists(exe):
+        raise SystemExit(f"bench.py: {exe} missing (integration/build.sh builds it)")
+    tmp = tempfile.mkdtemp(prefix="pdb_tables_")
+    try:
+        paths = [os.path.join(tmp, f"t{i}.sst") for i in range(ntables)]
+        procs = [subprocess.Popen([exe, p, str(nkeys), str(value_size), str(seed + i)], stdout=subprocess.PIPE)
+                 for i, p in enumerate(paths)]
+        for pr in procs:
+            if pr.wait() != 0:
+                raise SystemExit("bench.py: pdb_tablegen failed")
+        parts, hs, info, base = [], [], [], 0
+        for p in paths:
+            im = np.fromfile(p, dtype=np.uint8)
+            f = T.Footer.decode(im[-T.K_FOOTER_ENCODED_LENGTH:].tobytes())
+            idx = im[f.index.offset: f.index.offset + f.index.size].tobytes()
+            data = [T.BlockHandle.decode(v)[0] for _, v in T.block_entries(idx)]
+            mi = im[f.metaindex.offset: f.metaindex.offset + f.metaindex.size].tobytes()
+            meta = [T.BlockHandle.decode(v)[0] for _, v in T.block_entries(mi)]
+            h = np.zeros(len(data) + len(meta) + 2, dtype=crc32c.HANDLE_DTYPE)
+            h["offset"] = [x.offset + base for x in data + meta + [f.metaindex, f.index]]
+            h["size"] = [x.size for x in data + meta + [f.metaindex, f.index]]
+            hs.append(h)
+            parts.append(im)
+            info.append({"bytes": int(len(im)), "data_blocks": len(data), "filter_bytes": int(meta[0].size) if meta else 0,
+                         "index_bytes": int(f.index.size)})
+            base += len(im)
+        return np.concatenate(parts), np.concatenate(hs), info
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
 
 
 def zipf_kib_sizes(n: int, seed: int, kmax: int = 64) -> np.ndarray:
@@ -362,6 +412,45 @@ def main():
                                 "5-B trailer, " + {"sst_verify": "pdb_sst_verify_device", "sst_seal": "pdb_sst_seal_device",
                                                    "sst_crc": "pdb_sst_crc_device"}[args.workload],
                     "blocks_per_gpu": nblk, "bytes_per_gpu": hashed}
+    elif args.workload == "sst_tables":
+        # real tables: the reference engine's TableBuilder as shipped writes them (CPU CRC trailers),
+        # the image goes to HBM, and every block -- ~4.1-KiB data blocks, the MiB-sized filter and
+        # index blocks (the long-block lane), the metaindex -- is checked in one device verify
+        from pebblesdb_amd import table as T
+        from pebblesdb_amd._native import check, lib
+
+        img, hs, tinfo = real_tables(args.tables, args.table_keys, 1024, 401 + 16 * rank)
+        total = len(img)
+        data = torch.from_numpy(img).to(dev)
+        nblk = len(hs)
+        sizes, offs = hs["size"].astype(np.int64), hs["offset"].astype(np.int64)
+        d_h = T.handles_to_device(hs, dev)
+        cpu_blk = crc32c.make_blocks(offs, sizes + 1)
+        ok = torch.empty(nblk, dtype=torch.uint8, device=dev)
+        nbad = torch.zeros(1, dtype=torch.int32, device=dev)
+        L = stride = None
+        hashed = int((sizes + 1).sum())
+        sp = int(stream.cuda_stream)
+
+        def step():
+            check(lib().pdb_sst_verify_device(data.data_ptr(), total, d_h.data_ptr(), nblk, ok.data_ptr(),
+                                              nbad.data_ptr(), sp))
+
+        # the seal's trailer words, once (untimed), against the reference's own trailers in the files
+        out = T.crc_device(data, d_h)
+        stored = np.frombuffer(img.tobytes(), dtype=np.uint8)
+        t = offs + sizes + 1
+        words = (stored[t].astype(np.uint32) | (stored[t + 1].astype(np.uint32) << 8) |
+                 (stored[t + 2].astype(np.uint32) << 16) | (stored[t + 3].astype(np.uint32) << 24))
+        same = int(np.count_nonzero(out.cpu().numpy().view(np.uint32) == words))
+        long_m = sizes + 1 >= 16384
+        workload = {"workload": f"sst_tables: {args.tables} real sstables per GPU ({args.table_keys} keys x 1 KiB values, "
+                                "bloom 10 bits/key, kNoCompression) written by the reference TableBuilder "
+                                "(integration/_build/pdb_tablegen), every block verified by pdb_sst_verify_device",
+                    "blocks_per_gpu": nblk, "bytes_per_gpu": hashed, "tables": tinfo,
+                    "long_blocks": {"count": int(long_m.sum()), "bytes": int((sizes[long_m] + 1).sum()),
+                                    "max_bytes": int(sizes.max() + 1)},
+                    "gpu_trailers_equal_reference": f"{same}/{nblk}"}
     elif args.workload in ("wal", "wal100", "wal400", "wal1000"):
         # log file image: 32-KiB log blocks of physical records [crc 4][len 2][type 1][payload]
         # (db/log_format.h:27-30); fillseq-like 1055-B logical records (1 KiB value + key + batch
@@ -414,7 +503,7 @@ def main():
         workload = {"workload": "c3: Zipf 1-64 KiB blocks, packed, descriptor list (byte-balanced rank ranges)",
                     "blocks_per_gpu": nblk, "bytes_per_gpu": hashed}
     algo_bytes = hashed + 4 * nblk + (16 * nblk if args.workload in ("c3", "wal", "wal100", "wal400", "wal1000") else 0)
-    if args.workload == "sst_verify":  # + the 4-B stored trailer read, 16-B handle, 1-B ok written
+    if args.workload in ("sst_verify", "sst_tables"):  # + the 4-B stored trailer read, 16-B handle, 1-B ok written
         algo_bytes = hashed + nblk * (4 + 16 + 1)
     elif args.workload in ("sst_seal", "sst_crc"):  # + 4-B trailer / CRC written, 16-B handle
         algo_bytes = hashed + nblk * (4 + 16)
@@ -505,7 +594,7 @@ def main():
     if rank == 0:
         if args.diag:
             extra["diag"] = read_ceiling(torch, dev, data, stream)
-        if world == 1 and not args.no_ceiling:
+        if world == 1 and not args.no_ceiling and args.workload != "sst_tables":
             ceil = pattern_ceiling(torch, args.workload, data, stream, algo_bytes, nblk,
                                    d_h=d_h if args.workload.startswith("sst_") else None,
                                    d_blk=d_blk if args.workload.startswith("wal") or args.workload == "c3" else None,
@@ -521,10 +610,12 @@ def main():
             if args.workload in ("c2", "sstable", "c3", "wal", "wal100", "wal400", "wal1000"):
                 cpu = cpu_baseline(data, L, stride, nblk, args,
                                    d_blk if args.workload in ("c3", "wal", "wal100", "wal400", "wal1000") else None)
-            else:  # sst_verify / sst_seal: the reference's CRC over each block's contents || type
+            else:  # sst_verify / sst_seal / sst_tables: the reference's CRC over each block's contents || type
                 cpu = cpu_baseline(data, L, stride, nblk, args, cpu_blk)
         if wants_c4_shard(args, world, c4):
             extra["c4_shard"] = c4_shard(torch, crc32c, diag, dev, stream, args)
+        if args.workload == "sst_tables":  # every launch verified every block of the reference's tables
+            extra["verify"] = {"nbad_over_all_launches": int(nbad.item()), "ok_all": bool(ok.cpu().numpy().all())}
 
     if rank == 0:
         traffic = pmc_traffic(args.workload)
@@ -566,7 +657,9 @@ def main():
                            "wal1000": "crc_lanespan_kernel<DescSrc,OutSink,1023>",
                            "sst_verify": "crc_sst4k_kernel<SstSrc,SstVerifySink,nt,QuadTabs>",
                            "sst_seal": "crc_sst4k_kernel<SstSrc,ParkSealSink<64>,nt,QuadTabs>",
-                           "sst_crc": "crc_sst4k_kernel<SstSrc,SstCrcSink,nt,QuadTabs>"}[args.workload],
+                           "sst_crc": "crc_sst4k_kernel<SstSrc,SstCrcSink,nt,QuadTabs>",
+                           "sst_tables": "crc_sst4k_kernel<SstSrc,SstVerifySink,nt,QuadTabs> + the long-block lane "
+                                         "(crc_longpiece_kernel, long_combine_kernel)"}[args.workload],
                 "algorithmic_bytes_per_launch": algo_bytes,
                 "kernel_avg_ms": round(kern_avg_ms, 4),
                 "kernel_min_ms": round(float(np.min(kern_ms)), 4),
