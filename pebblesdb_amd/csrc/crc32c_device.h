@@ -1807,7 +1807,8 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
   // - 16 waits for it (its blocks are all taken, by waves that never wait on a later line: no cycle).
   // A deferred (slow-path) block marks its byte 0xFF, which the line store skips: it is stored
   // directly when hashed.
-  constexpr bool kOkRing = SinkRing<Sink>::kOn && kRows == 4 && kBlk == 4;
+  // (slot 6 is free only in the lane-quarter image: the 32-replica image keeps shift 1024 there)
+  constexpr bool kOkRing = SinkRing<Sink>::kOn && kRows == 4 && kBlk == 4 && __is_same(LT, QuadTabs);
   uint8_t* ok_ring = reinterpret_cast<uint8_t*>(lds + PDB_MAIN_BYTES + 6 * 4096u);
   uint32_t* ok_cnt = reinterpret_cast<uint32_t*>(lds + PDB_MAIN_BYTES + 6 * 4096u + 2048u);
   uint32_t* ok_tag = reinterpret_cast<uint32_t*>(lds + PDB_MAIN_BYTES + 6 * 4096u + 2112u);
