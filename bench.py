@@ -182,6 +182,9 @@ def dry_run_main(args, world: int, rank: int) -> None:
                 "region_s_max": float(t.item())}
         if wants_c4_shard(args, world, c4):
             line["c4_shard"] = {"blocks": C4_BLOCKS_PER_GPU, "bytes": C4_BLOCKS_PER_GPU * 4096, "dry_run": True}
+        if not args.no_copy_inclusive and args.workload in ("c2", "sstable"):
+            line["copy_inclusive"] = {"GiB/s": None, "dry_run": True, "concurrent_ranks": world,
+                                      "ranks_GiB/s": [None] * world, "entry": "pdb_crc32c_batch_host"}
         print(json.dumps(line), flush=True)
     if distributed:
         dist.destroy_process_group()
@@ -585,6 +588,12 @@ def main():
                                     "GiB_s_total_at_slowest": round(sum(b for b, _ in per) / (max(ms for _, ms in per) * 1e-3)
                                                                     / GIB, 3)}
 
+    # the copy-inclusive rate (host-resident blocks, H2D + kernel + D2H): at N > 1 every rank runs it on
+    # its own host sample at the same time (each GPU has its own PCIe link), outside `value`
+    ci = None
+    if not args.no_copy_inclusive and args.workload in ("c2", "sstable"):
+        ci = copy_inclusive(crc32c, data, L, stride, min(nblk, 1 << 18), world, cdev, dist if distributed else None)
+
     total_bytes = sum(r[3] for r in rows) * args.steps  # weak scaling: every rank hashes its own shard
     value = total_bytes / wall_max / GIB
     ms_per_step = wall_max / args.steps * 1e3
@@ -601,10 +610,6 @@ def main():
                                    hint=hint if args.workload.startswith("wal") else None, reseal=step)
             if ceil:
                 extra["pattern_ceiling"] = ceil
-        # the copy-inclusive rate is a one-GPU figure (like the CPU baseline): multi-rank runs skip it,
-        # so no rank sits in the process-group teardown while rank 0 copies for seconds
-        if not args.no_copy_inclusive and world == 1 and args.workload in ("c2", "sstable"):
-            extra["copy_inclusive"] = copy_inclusive(crc32c, data, L, stride, min(nblk, 1 << 18))
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             if args.workload in ("c2", "sstable", "c3", "wal", "wal100", "wal400", "wal1000"):
@@ -614,6 +619,8 @@ def main():
                 cpu = cpu_baseline(data, L, stride, nblk, args, cpu_blk)
         if wants_c4_shard(args, world, c4):
             extra["c4_shard"] = c4_shard(torch, crc32c, diag, dev, stream, args)
+        if ci is not None:
+            extra["copy_inclusive"] = ci
         if args.workload == "sst_tables":  # every launch verified every block of the reference's tables
             extra["verify"] = {"nbad_over_all_launches": int(nbad.item()), "ok_all": bool(ok.cpu().numpy().all())}
 
@@ -826,18 +833,34 @@ def read_ceiling(torch, dev, data, stream):
     return res
 
 
-def copy_inclusive(crc32c, data, L, stride, nblk):
-    """Host-resident blocks -> pdb_crc32c_batch_host (H2D + kernel + D2H), pageable memory."""
+def copy_inclusive(crc32c, data, L, stride, nblk, world: int = 1, cdev=None, dist=None):
+    """Host-resident blocks -> pdb_crc32c_batch_host (H2D + kernel + D2H), pageable memory: `nblk`
+    blocks of this rank's shard copied to host memory, 3 timed calls.  With N ranks every rank runs it
+    at once between barriers (each GPU hashes its own host sample over its own PCIe link): the line
+    gives each rank's rate and the aggregate, all ranks' bytes / the slowest rank's time."""
+    import torch
+
     host = data[: nblk * stride].cpu().numpy()
     blk = crc32c.make_blocks(np.arange(nblk) * stride, np.full(nblk, L))
     crc32c.batch_host(host, blk)  # warm (workspace growth)
     reps = 3
+    if dist is not None:
+        dist.barrier()
     t0 = time.perf_counter()
     for _ in range(reps):
         crc32c.batch_host(host, blk)
     dt = (time.perf_counter() - t0) / reps
-    return {"GiB/s": round(nblk * L / dt / GIB, 3), "blocks": nblk, "host_memory": "pageable",
-            "entry": "pdb_crc32c_batch_host"}
+    rate = nblk * L / dt / GIB
+    res = {"GiB/s": round(rate, 3), "blocks": nblk, "host_memory": "pageable", "entry": "pdb_crc32c_batch_host"}
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=cdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        rows = gather_rank_rows([int(rate * 1000)], world, cdev, dist)
+        res.update({"GiB/s": round(world * nblk * L / float(t.item()) / GIB, 3), "blocks_per_rank": nblk,
+                    "ranks_GiB/s": [r[0] / 1000 for r in rows], "concurrent_ranks": world,
+                    "aggregate": "all ranks' bytes / the slowest rank's time (each rank its own GPU and PCIe link)"})
+        del res["blocks"]
+    return res
 
 
 def cpu_baseline(data, L, stride, nblk, args, d_blk):

@@ -144,11 +144,15 @@ __global__ __launch_bounds__(256) void long_combine_kernel(LongLane ll, Sink sin
   if (nrec == 0) return;  // (grid-uniform: nothing exported, nothing to reset)
   const uint32_t t = threadIdx.x;
   if (blockIdx.x < nrec) {
-    for (uint32_t i = t; i < kCombLog2 * 1024u; i += blockDim.x) ops[i >> 10][i & 1023u] = ll.pow2[12u * 1024u + i];
+    uint32_t staged = 0;  // level operators staged so far (grown as records need them: a 64-KiB block needs 5)
     for (uint32_t r = blockIdx.x; r < nrec; r += gridDim.x) {
       const LongRec R = ll.rec[r];
       uint32_t ml = 0;
       while ((1u << ml) < R.np && ml < kCombLog2) ++ml;
+      if (ml > staged) {  // (workgroup-uniform; the first barrier below orders it)
+        for (uint32_t i = staged * 1024u + t; i < ml * 1024u; i += blockDim.x) ops[i >> 10][i & 1023u] = ll.pow2[12u * 1024u + i];
+        staged = ml;
+      }
       const uint32_t M = 1u << ml, nc = (R.np + M - 1u) / M;
       const uint32_t pad = nc * M - R.np;
       uint32_t acc = 0;  // (thread 0)

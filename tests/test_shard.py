@@ -192,6 +192,9 @@ def test_bench_dry_run_curve_keys():
         assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
         line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith('{"metric"')][-1])
         assert [set(x) >= {"rank", "blocks", "steady_kernel_avg_ms"} for x in line["ranks"]] == [True] * gpus
+        # the copy-inclusive leg runs on every rank at once (its own PCIe link), N = 1 included
+        ci = line["copy_inclusive"]
+        assert ci["concurrent_ranks"] == gpus and len(ci["ranks_GiB/s"]) == gpus and ci["entry"] == "pdb_crc32c_batch_host"
         if gpus == 1:
             assert line["c4_shard"]["blocks"] == 4194304 and line["c4_shard"]["bytes"] == 16 << 30
             assert line["steady_state"] is None
