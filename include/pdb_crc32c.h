@@ -35,7 +35,8 @@
  *     of them, or 65536 blocks), hashes them on one wave each -- only the time differs.
  *   - Per-block length in batches is < 2^32 bytes (the reference narrows to uint32_t:
  *     util/crc32c.cc:19-23,589); a single span (pdb_crc32c_extend*) may be longer.
- *   - Thread-safe: host entry points serialise per device; device entry points are pure launches.
+ *   - Thread-safe: host entry points take one of 4 staging contexts per device; device entry points
+ *     are pure launches.
  *     The library has no mutable global switches: every result depends only on the arguments.
  *   - Device-resident batches may read a few bytes outside a block: up to 15 bytes before its first
  *     byte and up to 3 bytes past its last one, never outside the 4-B-aligned dwords and 16-B lines
@@ -61,7 +62,8 @@
 extern "C" {
 #endif
 
-/* 2: pdb_crc32c_prepare_stream added; pdb_sst_seal_device_scratch (version 1) removed */
+/* 2: pdb_crc32c_prepare_stream, pdb_crc32c_init_mask and pdb_host_stripe_plan added;
+ *    pdb_sst_seal_device_scratch (version 1) removed */
 #define PDB_CRC32C_ABI_VERSION 2
 
 /* One block of a batch: bytes [base+off, base+off+len), optional Extend seed. 16 bytes. */
@@ -108,6 +110,21 @@ int pdb_crc32c_abi_version(void);
  * stream.  Called implicitly by every entry point; explicit calls are idempotent. */
 int pdb_crc32c_init(int device);
 const char* pdb_last_error(void); /* thread-local message of the last failure */
+/* The devices host batches stripe over (SURVEY §8(b) init(device_mask); bit d = HIP device d):
+ * pdb_crc32c_batch_host / _verify_host and the staging (DMA) route of pdb_sst_seal_host /
+ * _verify_host split a batch into contiguous runs of staging groups, ~1/N of the bytes per device,
+ * and stage every run through its own device's PCIe link at once (a batch of less than 8 MiB per
+ * device uses fewer devices).  Device-resident entry points and the zero-copy route keep the
+ * calling thread's device.  0 (the default) = the calling thread's current device.  Makes every
+ * masked device's state now; returns the number of devices, or a negative error (PDB_EINVAL: a
+ * device that is not visible). */
+int pdb_crc32c_init_mask(uint64_t device_mask);
+/* The staging plan a host descriptor batch of these blocks gets over `ndev` devices (groups of at
+ * most `chunk_bytes` of span, 0 = the library's 256 MiB): group k starts at block group_first[k] and
+ * runs on device index group_dev[k].  Fills at most `cap` groups; returns the number of groups.  Pure
+ * host code (no device needed): the planning half of pdb_crc32c_init_mask's striping, for tests. */
+int64_t pdb_host_stripe_plan(const pdb_blk* blk, uint64_t nblk, uint32_t ndev, uint64_t chunk_bytes,
+                             uint64_t* group_first, uint32_t* group_dev, uint64_t cap);
 /* Make the long-block lane's scratch for device-resident calls on `stream` now (it is otherwise made
  * at the stream's first call): call it before capturing device entry points on a stream into a
  * hipGraph.  PDB_EINVAL while the stream is capturing. */

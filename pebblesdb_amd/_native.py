@@ -45,6 +45,8 @@ SIGNATURES = {
     "pdb_host_free": (_I, [_V]),
     "pdb_crc32c_init": (_I, [_I]),
     "pdb_crc32c_prepare_stream": (_I, [_V]),
+    "pdb_crc32c_init_mask": (_I, [_U64]),
+    "pdb_host_stripe_plan": (ctypes.c_int64, [_V, _U64, _U32, _U64, _V, _V, _U64]),
     "pdb_last_error": (ctypes.c_char_p, []),
     "pdb_crc32c_current_device": (_I, []),
     "pdb_crc32c_extend": (_U32, [_U32, _V, ctypes.c_size_t]),

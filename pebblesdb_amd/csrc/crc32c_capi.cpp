@@ -677,9 +677,69 @@ static bool small_records_prefer_512(const pdb_blk* blk, uint64_t nblk) {
   return c512 < 0.95 * c256;
 }
 
+// ---- host batches: staging plan, striped over the devices of pdb_crc32c_init_mask ------------------
+// A group is a run of consecutive blocks staged by one copy: its span [lo, hi) (lo 16-B aligned down,
+// keeping the source's phase so the kernels' fast loads stay aligned) is at most host_chunk_bytes() (a
+// longer block forms its own group).  With several devices (pdb_crc32c_init_mask), device d takes a
+// contiguous run of groups holding ~1/N of the batch's bytes -- every device stages from its own PCIe
+// link at once -- and a batch of less than kStripeMinBytes per device uses fewer devices.
 struct HostGroup {
   uint64_t first, count, lo, hi;
+  uint32_t dev;  // index into the call's device list
 };
+
+std::atomic<uint64_t> g_host_mask{0};  // pdb_crc32c_init_mask (0: the calling thread's device)
+constexpr uint64_t kStripeMinBytes = 8ull << 20;
+
+std::vector<int> host_devices() {
+  const uint64_t m = g_host_mask.load(std::memory_order_acquire);
+  std::vector<int> d;
+  for (int i = 0; i < 64; ++i)
+    if ((m >> i) & 1u) d.push_back(i);
+  if (d.empty()) {
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess) cur = 0;
+    d.push_back(cur);
+  }
+  return d;
+}
+
+// span(i) = {lo, hi} of block i ({UINT64_MAX, 0}: an empty block, part of the group, no bytes)
+template <class Span>
+std::vector<HostGroup> plan_groups(uint64_t n, uint32_t ndev, uint64_t chunk, const Span& span) {
+  uint64_t total = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    const std::pair<uint64_t, uint64_t> sp = span(i);
+    if (sp.second > sp.first) total += sp.second - sp.first;
+  }
+  const uint64_t nd = std::max<uint64_t>(1, std::min<uint64_t>(ndev, total / kStripeMinBytes));
+  std::vector<HostGroup> groups;
+  HostGroup g{0, 0, UINT64_MAX, 0, 0};
+  uint64_t acc = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    if (g.count && g.dev + 1 < nd && acc >= (g.dev + 1) * (total / nd)) {  // the next device's share
+      groups.push_back(g);
+      g = HostGroup{i, 0, UINT64_MAX, 0, g.dev + 1};
+    }
+    const std::pair<uint64_t, uint64_t> sp = span(i);
+    if (sp.second > sp.first) {
+      const uint64_t lo = std::min(g.lo, sp.first), hi = std::max(g.hi, sp.second);
+      if (g.count && g.lo != UINT64_MAX && hi - lo > chunk) {
+        groups.push_back(g);
+        g = HostGroup{i, 0, sp.first, sp.second, g.dev};
+      } else {
+        g.lo = lo;
+        g.hi = hi;
+      }
+      acc += sp.second - sp.first;
+    }
+    ++g.count;
+  }
+  groups.push_back(g);
+  for (auto& x : groups)
+    if (x.lo == UINT64_MAX) x.lo = x.hi = 0;
+  return groups;
+}
 
 // Two-slot staging pipeline over copy_stream (H2D) and stream (kernel + D2H).  The destructor drains
 // both streams, so an early error return never leaves a copy in flight from host memory that is
@@ -704,6 +764,70 @@ struct SlotPipe {
   hipError_t end_group(size_t k) const { return hipEventRecord(st->drained[k & 1], st->stream); }
 };
 
+// One device's share of a host batch: a locked host context of that device, its contiguous run of
+// plan groups (blocks [first, first + count)) and their staging pipe.  (Members destroyed in reverse:
+// the pipe drains its streams before the context is unlocked.)
+struct HostLane {
+  int device = -1;
+  DevState* dev = nullptr;
+  std::unique_ptr<CtxLock> cl;
+  HostCtx* c = nullptr;
+  std::vector<size_t> gi;
+  uint64_t first = 0, count = 0;
+  std::unique_ptr<SlotPipe> pipe;
+};
+
+struct DeviceRestore {  // the caller's current device, put back on every return
+  int d = -1;
+  DeviceRestore() { (void)hipGetDevice(&d); }
+  ~DeviceRestore() {
+    if (d >= 0) (void)hipSetDevice(d);
+  }
+};
+
+// A host context on every device the plan uses, locked in ascending device order (two multi-device
+// batches never wait on each other in a cycle).
+int open_lanes(const std::vector<HostGroup>& groups, const std::vector<int>& devs, std::vector<HostLane>& lanes) {
+  int nvis = 0;
+  if (hipGetDeviceCount(&nvis) != hipSuccess || nvis <= 0)
+    return fail(PDB_ENODEV, "no HIP device visible (pdb_crc32c has no CPU fallback)");
+  lanes.clear();
+  lanes.resize(devs.size());
+  for (size_t k = 0; k < groups.size(); ++k) lanes[groups[k].dev].gi.push_back(k);
+  for (size_t d = 0; d < devs.size(); ++d) {
+    HostLane& L = lanes[d];
+    if (L.gi.empty()) continue;
+    L.device = devs[d];
+    hipError_t e = hipSetDevice(L.device);
+    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+    int rc = get_state(&L.dev);
+    if (rc) return rc;
+    L.cl.reset(new CtxLock(L.dev));
+    L.c = L.cl->c;
+    L.first = groups[L.gi.front()].first;
+    for (size_t k : L.gi) L.count += groups[k].count;
+  }
+  return PDB_OK;
+}
+
+// Issue every lane's groups round-robin (group j of each device, then j + 1, ...), so all devices'
+// copies start at once; issue(L, j) runs with L's device current.
+template <class Issue>
+int issue_lanes(std::vector<HostLane>& lanes, const Issue& issue) {
+  for (size_t j = 0;; ++j) {
+    bool any = false;
+    for (HostLane& L : lanes) {
+      if (j >= L.gi.size()) continue;
+      any = true;
+      hipError_t e = hipSetDevice(L.device);
+      if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+      int rc = issue(L, j);
+      if (rc) return rc;
+    }
+    if (!any) return PDB_OK;
+  }
+}
+
 // Host batch over descriptors: per group, stage [lo, hi) of the host span, the rebased
 // descriptors (and expected CRCs) in the workspace; H2D span + descriptors, kernel, D2H results.
 int host_desc(const uint8_t* base, uint64_t base_len, const pdb_blk* blk, uint64_t nblk,
@@ -714,8 +838,6 @@ int host_desc(const uint8_t* base, uint64_t base_len, const pdb_blk* blk, uint64
     return PDB_OK;
   }
   if (!base || !blk) return fail(PDB_EINVAL, "null argument");
-  std::vector<HostGroup> groups;
-  HostGroup g{0, 0, UINT64_MAX, 0};
   uint64_t n1k = 0, n4k = 0, n256 = 0, n512 = 0, n1023 = 0;  // size classes of the sized kernels
   uint32_t max_len = 0;
   for (uint64_t i = 0; i < nblk; ++i) {
@@ -727,20 +849,12 @@ int host_desc(const uint8_t* base, uint64_t base_len, const pdb_blk* blk, uint64
     n256 += blk[i].len - 1u <= 255u;
     n512 += blk[i].len - 257u <= 255u;
     n1023 += blk[i].len - 513u <= 510u;
-    if (blk[i].len) {
-      const uint64_t lo = std::min(g.lo, blk[i].off & ~static_cast<uint64_t>(15));
-      const uint64_t hi = std::max(g.hi, blk[i].off + blk[i].len);
-      if (g.count && g.lo != UINT64_MAX && hi - lo > host_chunk_bytes()) {
-        groups.push_back(g);
-        g = HostGroup{i, 0, blk[i].off & ~static_cast<uint64_t>(15), blk[i].off + blk[i].len};
-      } else {
-        g.lo = lo;
-        g.hi = hi;
-      }
-    }
-    ++g.count;
   }
-  groups.push_back(g);
+  const std::vector<int> devs = host_devices();
+  const std::vector<HostGroup> groups = plan_groups(nblk, static_cast<uint32_t>(devs.size()), host_chunk_bytes(), [&](uint64_t i) {
+    return blk[i].len ? std::make_pair(blk[i].off & ~static_cast<uint64_t>(15), blk[i].off + blk[i].len)
+                      : std::make_pair(UINT64_MAX, uint64_t{0});
+  });
   // host-visible lengths pick the kernel: mostly WAL-record or sstable-block sized -> the sized
   // kernels (same results; the hint only changes speed)
   if (!(flags & (PDB_CRC_USE_INIT | PDB_CRC_SIZE_1K | PDB_CRC_SIZE_4K | PDB_CRC_SIZE_256 | PDB_CRC_SIZE_512 | PDB_CRC_SIZE_1023))) {
@@ -752,73 +866,90 @@ int host_desc(const uint8_t* base, uint64_t base_len, const pdb_blk* blk, uint64
     if ((flags & (PDB_CRC_SIZE_512 | PDB_CRC_SIZE_1023)) && mixed_lengths(blk, nblk, (flags & PDB_CRC_SIZE_512) ? 512u : 1023u))
       flags |= PDB_CRC_SIZE_MIXED;
   }
-  // lo keeps the source's 16-B phase so the kernels' fast loads stay aligned
-  size_t need = 0;
-  uint64_t max_count = 0;
-  for (auto& x : groups) {
-    if (x.lo == UINT64_MAX) x.lo = x.hi = 0;
-    need = std::max<size_t>(need, x.hi - x.lo);
-    max_count = std::max(max_count, x.count);
-  }
-  const size_t off_desc = align_up(need + 16, 256);
-  const size_t off_out = align_up(off_desc + max_count * sizeof(pdb_blk), 256);
-  const size_t off_exp = align_up(off_out + max_count * sizeof(uint32_t), 256);
-  const size_t off_ok = align_up(off_exp + (mode == kModeVerify ? max_count * 4 : 0), 256);
-  const size_t slot_bytes = align_up(off_ok + (mode == kModeVerify ? max_count : 0), 256);
-  const size_t nslots = groups.size() > 1 ? 2 : 1;
-  DevState* dev;
-  int rc = get_state(&dev);
+  DeviceRestore restore;
+  std::vector<HostLane> lanes;
+  int rc = open_lanes(groups, devs, lanes);
   if (rc) return rc;
-  CtxLock cl(dev);
-  HostCtx* st = cl.c;
-  LaunchGeom hgeom = dev->hgeom;
-  hipError_t e = hipSetDevice(dev->device);
-  if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
-  if ((rc = ensure_ws(st, nslots * slot_bytes + 256))) return rc;
-  hipStream_t s = st->stream, cs = st->copy_stream;
-  // blocks of >= 16 KiB: the long-block lane on this context's stream (crc32c_internal.h)
-  if (max_len >= kLongMinBytes && !st->d_lane && (rc = alloc_lane(s, &st->d_lane))) return rc;
-  LongLane lane_v = long_lane_at(max_len >= kLongMinBytes ? st->d_lane : nullptr, dev->d_pow2);
-  const LongLane* lane = lane_v.hdr ? &lane_v : nullptr;
-  uint32_t* d_nbad = reinterpret_cast<uint32_t*>(st->d_ws + nslots * slot_bytes);
-  std::vector<std::vector<pdb_blk>> rbs(groups.size());  // async H2D sources, alive until the drain
-  uint32_t nb = 0;
-  {
-    SlotPipe pipe(st);
-    if (mode == kModeVerify && (e = hipMemsetAsync(d_nbad, 0, 4, s)) != hipSuccess)
-      return hip_fail(e, "hipMemsetAsync");
-    for (size_t k = 0; k < groups.size(); ++k) {
-      const HostGroup& x = groups[k];
-      uint8_t* ws = st->d_ws + (k % nslots) * slot_bytes;
-      std::vector<pdb_blk>& rb = rbs[k];
-      rb.assign(blk + x.first, blk + x.first + x.count);
-      for (auto& b : rb) b.off = b.len ? b.off - x.lo : 0;
-      if ((e = pipe.begin_copies(k)) != hipSuccess) return hip_fail(e, "hipStreamWaitEvent");
-      if (x.hi > x.lo && (e = hipMemcpyAsync(ws, base + x.lo, x.hi - x.lo, hipMemcpyHostToDevice, cs)) != hipSuccess)
-        return hip_fail(e, "hipMemcpyAsync(span)");
-      if ((e = hipMemcpyAsync(ws + off_desc, rb.data(), x.count * sizeof(pdb_blk), hipMemcpyHostToDevice, cs)) !=
-          hipSuccess)
-        return hip_fail(e, "hipMemcpyAsync(desc)");
-      if (mode == kModeVerify &&
-          (e = hipMemcpyAsync(ws + off_exp, expected + x.first, x.count * 4, hipMemcpyHostToDevice, cs)) != hipSuccess)
-        return hip_fail(e, "hipMemcpyAsync(expected)");
-      if ((e = pipe.end_copies(k)) != hipSuccess) return hip_fail(e, "hipEventRecord(staged)");
-      e = launch_desc(hgeom, dev->d_tables, ws, reinterpret_cast<const pdb_blk*>(ws + off_desc), x.count, flags,
-                      mode, reinterpret_cast<const uint32_t*>(ws + off_exp), reinterpret_cast<uint32_t*>(ws + off_out),
-                      ws + off_ok, d_nbad, s, lane);
-      if (e != hipSuccess) return hip_fail(e, "launch_desc");
-      if (mode == kModeOut) {
-        if ((e = hipMemcpyAsync(out + x.first, ws + off_out, x.count * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
-          return hip_fail(e, "hipMemcpyAsync(out)");
-      } else if (ok && (e = hipMemcpyAsync(ok + x.first, ws + off_ok, x.count, hipMemcpyDeviceToHost, s)) !=
-                           hipSuccess) {
-        return hip_fail(e, "hipMemcpyAsync(ok)");
-      }
-      if ((e = pipe.end_group(k)) != hipSuccess) return hip_fail(e, "hipEventRecord(drained)");
+  struct Geo {
+    size_t off_desc = 0, off_out = 0, off_exp = 0, off_ok = 0, slot_bytes = 0, nslots = 1;
+    uint32_t* d_nbad = nullptr;
+    LongLane ll{};
+    uint32_t nb = 0;
+  };
+  std::vector<Geo> geo(lanes.size());
+  hipError_t e;
+  for (size_t d = 0; d < lanes.size(); ++d) {
+    HostLane& L = lanes[d];
+    if (L.gi.empty()) continue;
+    Geo& G = geo[d];
+    if ((e = hipSetDevice(L.device)) != hipSuccess) return hip_fail(e, "hipSetDevice");
+    size_t need = 0;
+    uint64_t max_count = 0;
+    for (size_t k : L.gi) {
+      need = std::max<size_t>(need, groups[k].hi - groups[k].lo);
+      max_count = std::max(max_count, groups[k].count);
     }
-    if (mode == kModeVerify && (e = hipMemcpyAsync(&nb, d_nbad, 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
+    G.off_desc = align_up(need + 16, 256);
+    G.off_out = align_up(G.off_desc + max_count * sizeof(pdb_blk), 256);
+    G.off_exp = align_up(G.off_out + max_count * sizeof(uint32_t), 256);
+    G.off_ok = align_up(G.off_exp + (mode == kModeVerify ? max_count * 4 : 0), 256);
+    G.slot_bytes = align_up(G.off_ok + (mode == kModeVerify ? max_count : 0), 256);
+    G.nslots = L.gi.size() > 1 ? 2 : 1;
+    if ((rc = ensure_ws(L.c, G.nslots * G.slot_bytes + 256))) return rc;
+    // blocks of >= 16 KiB: the long-block lane on this context's stream (crc32c_internal.h)
+    if (max_len >= kLongMinBytes && !L.c->d_lane && (rc = alloc_lane(L.c->stream, &L.c->d_lane))) return rc;
+    G.ll = long_lane_at(max_len >= kLongMinBytes ? L.c->d_lane : nullptr, L.dev->d_pow2);
+    G.d_nbad = reinterpret_cast<uint32_t*>(L.c->d_ws + G.nslots * G.slot_bytes);
+    L.pipe.reset(new SlotPipe(L.c));
+    if (mode == kModeVerify && (e = hipMemsetAsync(G.d_nbad, 0, 4, L.c->stream)) != hipSuccess)
+      return hip_fail(e, "hipMemsetAsync");
+  }
+  std::vector<std::vector<pdb_blk>> rbs(groups.size());  // async H2D sources, alive until the drain
+  rc = issue_lanes(lanes, [&](HostLane& L, size_t k) -> int {
+    const Geo& G = geo[&L - lanes.data()];
+    const HostGroup& x = groups[L.gi[k]];
+    HostCtx* st = L.c;
+    hipStream_t s = st->stream, cs = st->copy_stream;
+    uint8_t* ws = st->d_ws + (k % G.nslots) * G.slot_bytes;
+    std::vector<pdb_blk>& rb = rbs[L.gi[k]];
+    rb.assign(blk + x.first, blk + x.first + x.count);
+    for (auto& b : rb) b.off = b.len ? b.off - x.lo : 0;
+    hipError_t e2;
+    if ((e2 = L.pipe->begin_copies(k)) != hipSuccess) return hip_fail(e2, "hipStreamWaitEvent");
+    if (x.hi > x.lo && (e2 = hipMemcpyAsync(ws, base + x.lo, x.hi - x.lo, hipMemcpyHostToDevice, cs)) != hipSuccess)
+      return hip_fail(e2, "hipMemcpyAsync(span)");
+    if ((e2 = hipMemcpyAsync(ws + G.off_desc, rb.data(), x.count * sizeof(pdb_blk), hipMemcpyHostToDevice, cs)) != hipSuccess)
+      return hip_fail(e2, "hipMemcpyAsync(desc)");
+    if (mode == kModeVerify &&
+        (e2 = hipMemcpyAsync(ws + G.off_exp, expected + x.first, x.count * 4, hipMemcpyHostToDevice, cs)) != hipSuccess)
+      return hip_fail(e2, "hipMemcpyAsync(expected)");
+    if ((e2 = L.pipe->end_copies(k)) != hipSuccess) return hip_fail(e2, "hipEventRecord(staged)");
+    e2 = launch_desc(L.dev->hgeom, L.dev->d_tables, ws, reinterpret_cast<const pdb_blk*>(ws + G.off_desc), x.count, flags,
+                     mode, reinterpret_cast<const uint32_t*>(ws + G.off_exp), reinterpret_cast<uint32_t*>(ws + G.off_out),
+                     ws + G.off_ok, G.d_nbad, s, G.ll.hdr ? &G.ll : nullptr);
+    if (e2 != hipSuccess) return hip_fail(e2, "launch_desc");
+    if (mode == kModeOut) {
+      if ((e2 = hipMemcpyAsync(out + x.first, ws + G.off_out, x.count * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
+        return hip_fail(e2, "hipMemcpyAsync(out)");
+    } else if (ok && (e2 = hipMemcpyAsync(ok + x.first, ws + G.off_ok, x.count, hipMemcpyDeviceToHost, s)) != hipSuccess) {
+      return hip_fail(e2, "hipMemcpyAsync(ok)");
+    }
+    if ((e2 = L.pipe->end_group(k)) != hipSuccess) return hip_fail(e2, "hipEventRecord(drained)");
+    return PDB_OK;
+  });
+  if (rc) return rc;
+  uint64_t nb = 0;
+  for (size_t d = 0; d < lanes.size(); ++d) {
+    HostLane& L = lanes[d];
+    if (L.gi.empty()) continue;
+    if ((e = hipSetDevice(L.device)) != hipSuccess) return hip_fail(e, "hipSetDevice");
+    if (mode == kModeVerify && (e = hipMemcpyAsync(&geo[d].nb, geo[d].d_nbad, 4, hipMemcpyDeviceToHost, L.c->stream)) != hipSuccess)
       return hip_fail(e, "hipMemcpyAsync(nbad)");
-    if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+  }
+  for (size_t d = 0; d < lanes.size(); ++d) {
+    if (lanes[d].gi.empty()) continue;
+    if ((e = hipStreamSynchronize(lanes[d].c->stream)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+    nb += geo[d].nb;
   }
   if (nbad_out) *nbad_out = nb;
   return PDB_OK;
@@ -1103,27 +1234,13 @@ int host_sst(uint8_t* buf, uint64_t buf_len, const pdb_block_handle* h, uint64_t
     return PDB_OK;
   }
   if (!buf || !h) return fail(PDB_EINVAL, "null argument");
-  // staging groups of at most host_chunk_bytes() of span (block + trailer), as for host_desc
-  std::vector<HostGroup> groups;
-  HostGroup g{0, 0, UINT64_MAX, 0};
   for (uint64_t i = 0; i < n; ++i) {
     // block + 5-byte trailer must lie inside the buffer (table/format.cc:84-87 "truncated")
     if (h[i].offset > buf_len || h[i].size > buf_len - h[i].offset ||
         buf_len - h[i].offset - h[i].size < 5)
       return fail(PDB_ERANGE, "block handle " + std::to_string(i) + " (+trailer) exceeds buffer");
     if (h[i].size + 1 > 0xFFFFFFFFull) return fail(PDB_ERANGE, "block larger than 4 GiB");
-    const uint64_t blo = h[i].offset & ~static_cast<uint64_t>(15), bhi = h[i].offset + h[i].size + 5;
-    const uint64_t lo = std::min(g.lo, blo), hi = std::max(g.hi, bhi);
-    if (g.count && hi - lo > host_chunk_bytes()) {
-      groups.push_back(g);
-      g = HostGroup{i, 1, blo, bhi};
-    } else {
-      g.lo = lo;
-      g.hi = hi;
-      ++g.count;
-    }
   }
-  groups.push_back(g);
   // PDB_HOST_MAPPED=0 (read once per process): pinned buffers take the DMA route below as well
   // (experiments: the engine's seals by DMA against zero-copy, profiles/r05/engine/)
   static const bool mapped = [] {
@@ -1132,16 +1249,11 @@ int host_sst(uint8_t* buf, uint64_t buf_len, const pdb_block_handle* h, uint64_t
   }();
   if (mapped)
     if (uint8_t* d_buf = pin_mapping(buf, buf_len)) return host_sst_mapped(buf, d_buf, buf_len, h, n, seal, ok, nbad_out);
-  size_t need = 0;
-  uint64_t max_count = 0;
-  for (const auto& x : groups) {
-    need = std::max<size_t>(need, x.hi - x.lo);
-    max_count = std::max(max_count, x.count);
-  }
-  const size_t off_h = align_up(need + 16, 256);
-  const size_t off_ok = align_up(off_h + max_count * sizeof(pdb_block_handle), 256);
-  const size_t slot_bytes = align_up(off_ok + 4 * max_count, 256);  // ok bytes (verify) or masked CRCs (seal)
-  const size_t nslots = groups.size() > 1 ? 2 : 1;
+  // staging groups of at most host_chunk_bytes() of span (block + trailer), striped over the devices
+  const std::vector<int> devs = host_devices();
+  const std::vector<HostGroup> groups = plan_groups(n, static_cast<uint32_t>(devs.size()), host_chunk_bytes(), [&](uint64_t i) {
+    return std::make_pair(h[i].offset & ~static_cast<uint64_t>(15), h[i].offset + h[i].size + 5);
+  });
   // Long blocks (as in host_sst_mapped, up to 2^14 pieces of 4 KiB): the sst kernel gets a 0-byte
   // stand-in at the block's offset (its type byte alone: cheap, and nothing it writes lands in the
   // image) and launch_span_many hashes the block from the group's staged copy; the host then puts
@@ -1152,135 +1264,186 @@ int host_sst(uint8_t* buf, uint64_t buf_len, const pdb_block_handle* h, uint64_t
   auto is_long = [&](const pdb_block_handle& b) {
     return b.size >= long_block && (b.size + 1 + kPiece - 1) / kPiece <= kMaxPieces;
   };
-  std::vector<uint64_t> longs;  // handle indices, ascending (so by group)
-  uint64_t npieces = 0, max_gpieces = 0;
-  for (const auto& x : groups) {
-    uint64_t gp = 0;
-    for (uint64_t i = x.first; i < x.first + x.count; ++i)
-      if (is_long(h[i])) {
-        longs.push_back(i);
-        gp += (h[i].size + 1 + kPiece - 1) / kPiece;
-      }
-    npieces += gp;
-    max_gpieces = std::max(max_gpieces, gp);
-  }
-  const uint64_t nl = longs.size();
-  DevState* dev;
-  int rc = get_state(&dev);
+  DeviceRestore restore;
+  std::vector<HostLane> lanes;
+  int rc = open_lanes(groups, devs, lanes);
   if (rc) return rc;
-  CtxLock cl(dev);
-  HostCtx* st = cl.c;
-  LaunchGeom hgeom = dev->hgeom;
-  hipError_t e = hipSetDevice(dev->device);
-  if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
-  // device: the slots, nbad, then the long blocks' leaves (one group's at a time: stream s)
-  const size_t ws_leaves = nslots * slot_bytes + 256;
-  if ((rc = ensure_ws(st, ws_leaves + align_up(4 * max_gpieces, 256)))) return rc;
-  // pinned: every group's rebased handles, then the trailer words (seal) or ok bytes (verify), then
-  // nbad, then the long blocks' CRCs, pieces and parts (every group's, side by side)
-  const size_t pin_crc = align_up(n * sizeof(pdb_block_handle), 64);
-  const size_t pin_lcrc = pin_crc + align_up(4 * n, 64) + 64;
-  const size_t pin_pieces = pin_lcrc + align_up(4 * nl, 64), pin_parts = pin_pieces + npieces * sizeof(pdb_blk);
-  if ((rc = ensure_pin(st, pin_parts + nl * sizeof(SpanPart)))) return rc;
-  if (nl && !st->d_pin) return fail(PDB_EHIP, "pinned scratch has no device mapping");
-  hipStream_t s = st->stream, cs = st->copy_stream;
-  uint32_t* d_nbad = reinterpret_cast<uint32_t*>(st->d_ws + nslots * slot_bytes);
-  uint32_t* h_lcrc = reinterpret_cast<uint32_t*>(st->h_pin + pin_lcrc);
-  uint64_t lq = 0, lp = 0;  // the next long block / piece (across groups)
+  // per lane: its slots; its pinned scratch holds, for ITS blocks (index - first): the rebased handles,
+  // the trailer words (seal) or ok bytes (verify), nbad, then its long blocks' CRCs, pieces and parts
+  struct Geo {
+    size_t off_h = 0, off_ok = 0, slot_bytes = 0, nslots = 1, ws_leaves = 0;
+    size_t pin_crc = 0, pin_lcrc = 0, pin_pieces = 0, pin_parts = 0;
+    std::vector<uint64_t> longs;  // its long blocks (handle indices, ascending)
+    uint64_t lq = 0, lp = 0;      // the next long block / piece (across its groups)
+    uint32_t* d_nbad = nullptr;
+  };
+  std::vector<Geo> geo(lanes.size());
+  hipError_t e;
+  for (size_t d = 0; d < lanes.size(); ++d) {
+    HostLane& L = lanes[d];
+    if (L.gi.empty()) continue;
+    Geo& G = geo[d];
+    if ((e = hipSetDevice(L.device)) != hipSuccess) return hip_fail(e, "hipSetDevice");
+    size_t need = 0;
+    uint64_t max_count = 0, npieces = 0, max_gpieces = 0;
+    for (size_t k : L.gi) {
+      const HostGroup& x = groups[k];
+      need = std::max<size_t>(need, x.hi - x.lo);
+      max_count = std::max(max_count, x.count);
+      uint64_t gp = 0;
+      for (uint64_t i = x.first; i < x.first + x.count; ++i)
+        if (is_long(h[i])) {
+          G.longs.push_back(i);
+          gp += (h[i].size + 1 + kPiece - 1) / kPiece;
+        }
+      npieces += gp;
+      max_gpieces = std::max(max_gpieces, gp);
+    }
+    G.off_h = align_up(need + 16, 256);
+    G.off_ok = align_up(G.off_h + max_count * sizeof(pdb_block_handle), 256);
+    G.slot_bytes = align_up(G.off_ok + 4 * max_count, 256);  // ok bytes (verify) or masked CRCs (seal)
+    G.nslots = L.gi.size() > 1 ? 2 : 1;
+    // device: the slots, nbad, then the long blocks' leaves (one group's at a time: stream s)
+    G.ws_leaves = G.nslots * G.slot_bytes + 256;
+    if ((rc = ensure_ws(L.c, G.ws_leaves + align_up(4 * max_gpieces, 256)))) return rc;
+    const uint64_t nl = G.longs.size();
+    G.pin_crc = align_up(L.count * sizeof(pdb_block_handle), 64);
+    G.pin_lcrc = G.pin_crc + align_up(4 * L.count, 64) + 64;
+    G.pin_pieces = G.pin_lcrc + align_up(4 * nl, 64);
+    G.pin_parts = G.pin_pieces + npieces * sizeof(pdb_blk);
+    if ((rc = ensure_pin(L.c, G.pin_parts + nl * sizeof(SpanPart)))) return rc;
+    if (nl && !L.c->d_pin) return fail(PDB_EHIP, "pinned scratch has no device mapping");
+    *reinterpret_cast<uint32_t*>(L.c->h_pin + G.pin_crc + align_up(4 * L.count, 64)) = 0;
+    G.d_nbad = reinterpret_cast<uint32_t*>(L.c->d_ws + G.nslots * G.slot_bytes);
+    L.pipe.reset(new SlotPipe(L.c));
+    if (!seal && (e = hipMemsetAsync(G.d_nbad, 0, 4, L.c->stream)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
+  }
   // Seal: only the 4 CRC bytes of every trailer change, so the kernel writes the masked CRCs into
   // a compact array, 4 B per block come back across PCIe (not the span), and the host encodes
   // them little-endian at offset + size + 1 (table_builder.cc:199-200).
-  pdb_block_handle* h_rh = reinterpret_cast<pdb_block_handle*>(st->h_pin);  // async H2D sources
-  uint32_t* crc = reinterpret_cast<uint32_t*>(st->h_pin + pin_crc);
-  uint8_t* h_ok = st->h_pin + pin_crc;
-  uint32_t* h_nb = reinterpret_cast<uint32_t*>(st->h_pin + pin_crc + align_up(4 * n, 64));
-  *h_nb = 0;
-  {
-    SlotPipe pipe(st);
-    if (!seal && (e = hipMemsetAsync(d_nbad, 0, 4, s)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
-    for (size_t k = 0; k < groups.size(); ++k) {
-      const HostGroup& x = groups[k];
-      uint8_t* ws = st->d_ws + (k % nslots) * slot_bytes;
-      pdb_block_handle* rh = h_rh + x.first;
-      for (uint64_t i = 0; i < x.count; ++i)
-        rh[i] = pdb_block_handle{h[x.first + i].offset - x.lo, is_long(h[x.first + i]) ? 0u : h[x.first + i].size};
-      if ((e = pipe.begin_copies(k)) != hipSuccess) return hip_fail(e, "hipStreamWaitEvent");
-      if ((e = hipMemcpyAsync(ws, buf + x.lo, x.hi - x.lo, hipMemcpyHostToDevice, cs)) != hipSuccess)
-        return hip_fail(e, "hipMemcpyAsync(span)");
-      if ((e = hipMemcpyAsync(ws + off_h, rh, x.count * sizeof(pdb_block_handle), hipMemcpyHostToDevice,
-                              cs)) != hipSuccess)
-        return hip_fail(e, "hipMemcpyAsync(handles)");
-      if ((e = pipe.end_copies(k)) != hipSuccess) return hip_fail(e, "hipEventRecord(staged)");
-      const pdb_block_handle* d_h = reinterpret_cast<const pdb_block_handle*>(ws + off_h);
-      if (seal) {
-        uint32_t* d_crc = reinterpret_cast<uint32_t*>(ws + off_ok);
-        if ((e = launch_sst_masked(hgeom, dev->d_tables, ws, x.hi - x.lo, d_h, x.count, d_crc, s)) != hipSuccess)
-          return hip_fail(e, "launch_sst_masked");
-        if ((e = hipMemcpyAsync(crc + x.first, d_crc, x.count * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
-          return hip_fail(e, "hipMemcpyAsync(crcs)");
-      } else {
-        if ((e = launch_sst(hgeom, dev->d_tables, ws, x.hi - x.lo, d_h, x.count, false, ws + off_ok, d_nbad, s)) !=
-            hipSuccess)
-          return hip_fail(e, "launch_sst");
-        if ((ok || nl) && (e = hipMemcpyAsync(h_ok + x.first, ws + off_ok, x.count, hipMemcpyDeviceToHost, s)) != hipSuccess)
-          return hip_fail(e, "hipMemcpyAsync(ok)");
-      }
-      // the group's long blocks: their pieces (offsets in the staged copy) and parts, pinned and
-      // mapped; CRCs to h_lcrc[lq0, lq)
-      const uint64_t lq0 = lq, lp0 = lp;
-      pdb_blk* pc = reinterpret_cast<pdb_blk*>(st->h_pin + pin_pieces);
-      SpanPart* parts = reinterpret_cast<SpanPart*>(st->h_pin + pin_parts);
-      for (; lq < nl && longs[lq] < x.first + x.count; ++lq) {
-        const pdb_block_handle& hb = h[longs[lq]];
-        const uint64_t L = hb.size + 1, pieces = (L + kPiece - 1) / kPiece, first = L - (pieces - 1) * kPiece;
-        uint32_t ml = 0;
-        while ((1ull << ml) < pieces) ++ml;
-        parts[lq] = SpanPart{static_cast<uint32_t>(lp - lp0), static_cast<uint32_t>(pieces), ml, 0u};
-        const uint64_t o = hb.offset - x.lo;
-        pc[lp++] = pdb_blk{o, static_cast<uint32_t>(first), 0u};
-        for (uint64_t j = 1; j < pieces; ++j)
-          pc[lp++] = pdb_blk{o + first + (j - 1) * kPiece, static_cast<uint32_t>(kPiece), 0xFFFFFFFFu};
-      }
-      if (lq > lq0) {
-        uint32_t* d_lcrc = reinterpret_cast<uint32_t*>(st->d_pin + pin_lcrc) + lq0;  // (written across PCIe)
-        e = launch_span_many(hgeom, dev->d_tables, dev->d_pow2, ws, reinterpret_cast<const pdb_blk*>(st->d_pin + pin_pieces) + lp0,
-                             lp - lp0, reinterpret_cast<const SpanPart*>(st->d_pin + pin_parts) + lq0,
-                             static_cast<uint32_t>(lq - lq0), 12, reinterpret_cast<uint32_t*>(st->d_ws + ws_leaves), d_lcrc, s);
-        if (e != hipSuccess) return hip_fail(e, "launch_span_many(long blocks)");
-      }
-      if ((e = pipe.end_group(k)) != hipSuccess) return hip_fail(e, "hipEventRecord(drained)");
-    }
-    if (!seal && (e = hipMemcpyAsync(h_nb, d_nbad, 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
-      return hip_fail(e, "hipMemcpyAsync(nbad)");
-    if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
-  }
-  int64_t nbad = seal ? 0 : static_cast<int64_t>(*h_nb);
-  for (uint64_t q = 0; q < nl; ++q) {  // the long blocks in place of their stand-ins
-    const uint64_t i = longs[q];
+  rc = issue_lanes(lanes, [&](HostLane& L, size_t k) -> int {
+    Geo& G = geo[&L - lanes.data()];
+    const HostGroup& x = groups[L.gi[k]];
+    HostCtx* st = L.c;
+    hipStream_t s = st->stream, cs = st->copy_stream;
+    const LaunchGeom& hgeom = L.dev->hgeom;
+    uint8_t* ws = st->d_ws + (k % G.nslots) * G.slot_bytes;
+    const uint64_t li = x.first - L.first;  // the group's first block in the lane's arrays
+    pdb_block_handle* rh = reinterpret_cast<pdb_block_handle*>(st->h_pin) + li;  // async H2D sources
+    for (uint64_t i = 0; i < x.count; ++i)
+      rh[i] = pdb_block_handle{h[x.first + i].offset - x.lo, is_long(h[x.first + i]) ? 0u : h[x.first + i].size};
+    hipError_t e2;
+    if ((e2 = L.pipe->begin_copies(k)) != hipSuccess) return hip_fail(e2, "hipStreamWaitEvent");
+    if ((e2 = hipMemcpyAsync(ws, buf + x.lo, x.hi - x.lo, hipMemcpyHostToDevice, cs)) != hipSuccess)
+      return hip_fail(e2, "hipMemcpyAsync(span)");
+    if ((e2 = hipMemcpyAsync(ws + G.off_h, rh, x.count * sizeof(pdb_block_handle), hipMemcpyHostToDevice, cs)) != hipSuccess)
+      return hip_fail(e2, "hipMemcpyAsync(handles)");
+    if ((e2 = L.pipe->end_copies(k)) != hipSuccess) return hip_fail(e2, "hipEventRecord(staged)");
+    const pdb_block_handle* d_h = reinterpret_cast<const pdb_block_handle*>(ws + G.off_h);
+    uint8_t* pin_res = st->h_pin + G.pin_crc;
     if (seal) {
-      crc[i] = pdb_mask(h_lcrc[q]);
+      uint32_t* d_crc = reinterpret_cast<uint32_t*>(ws + G.off_ok);
+      if ((e2 = launch_sst_masked(hgeom, L.dev->d_tables, ws, x.hi - x.lo, d_h, x.count, d_crc, s)) != hipSuccess)
+        return hip_fail(e2, "launch_sst_masked");
+      if ((e2 = hipMemcpyAsync(reinterpret_cast<uint32_t*>(pin_res) + li, d_crc, x.count * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
+        return hip_fail(e2, "hipMemcpyAsync(crcs)");
     } else {
-      const uint8_t* tr = buf + h[i].offset + h[i].size + 1;
-      const uint32_t w = static_cast<uint32_t>(tr[0]) | (static_cast<uint32_t>(tr[1]) << 8) |
-                         (static_cast<uint32_t>(tr[2]) << 16) | (static_cast<uint32_t>(tr[3]) << 24);
-      const uint8_t good = pdb_unmask(w) == h_lcrc[q] ? 1u : 0u;
-      nbad += (h_ok[i] ? 0 : -1) + (good ? 0 : 1);
-      h_ok[i] = good;
+      if ((e2 = launch_sst(hgeom, L.dev->d_tables, ws, x.hi - x.lo, d_h, x.count, false, ws + G.off_ok, G.d_nbad, s)) !=
+          hipSuccess)
+        return hip_fail(e2, "launch_sst");
+      if ((ok || !G.longs.empty()) &&
+          (e2 = hipMemcpyAsync(pin_res + li, ws + G.off_ok, x.count, hipMemcpyDeviceToHost, s)) != hipSuccess)
+        return hip_fail(e2, "hipMemcpyAsync(ok)");
     }
+    // the group's long blocks: their pieces (offsets in the staged copy) and parts, pinned and
+    // mapped; CRCs to the lane's long-CRC words [lq0, lq)
+    const uint64_t nl = G.longs.size(), lq0 = G.lq, lp0 = G.lp;
+    pdb_blk* pc = reinterpret_cast<pdb_blk*>(st->h_pin + G.pin_pieces);
+    SpanPart* parts = reinterpret_cast<SpanPart*>(st->h_pin + G.pin_parts);
+    for (; G.lq < nl && G.longs[G.lq] < x.first + x.count; ++G.lq) {
+      const pdb_block_handle& hb = h[G.longs[G.lq]];
+      const uint64_t Lb = hb.size + 1, pieces = (Lb + kPiece - 1) / kPiece, first = Lb - (pieces - 1) * kPiece;
+      uint32_t ml = 0;
+      while ((1ull << ml) < pieces) ++ml;
+      parts[G.lq] = SpanPart{static_cast<uint32_t>(G.lp - lp0), static_cast<uint32_t>(pieces), ml, 0u};
+      const uint64_t o = hb.offset - x.lo;
+      pc[G.lp++] = pdb_blk{o, static_cast<uint32_t>(first), 0u};
+      for (uint64_t j = 1; j < pieces; ++j)
+        pc[G.lp++] = pdb_blk{o + first + (j - 1) * kPiece, static_cast<uint32_t>(kPiece), 0xFFFFFFFFu};
+    }
+    if (G.lq > lq0) {
+      uint32_t* d_lcrc = reinterpret_cast<uint32_t*>(st->d_pin + G.pin_lcrc) + lq0;  // (written across PCIe)
+      e2 = launch_span_many(hgeom, L.dev->d_tables, L.dev->d_pow2, ws, reinterpret_cast<const pdb_blk*>(st->d_pin + G.pin_pieces) + lp0,
+                            G.lp - lp0, reinterpret_cast<const SpanPart*>(st->d_pin + G.pin_parts) + lq0,
+                            static_cast<uint32_t>(G.lq - lq0), 12, reinterpret_cast<uint32_t*>(st->d_ws + G.ws_leaves), d_lcrc, s);
+      if (e2 != hipSuccess) return hip_fail(e2, "launch_span_many(long blocks)");
+    }
+    if ((e2 = L.pipe->end_group(k)) != hipSuccess) return hip_fail(e2, "hipEventRecord(drained)");
+    return PDB_OK;
+  });
+  if (rc) return rc;
+  for (size_t d = 0; d < lanes.size(); ++d) {
+    HostLane& L = lanes[d];
+    if (L.gi.empty() || seal) continue;
+    if ((e = hipSetDevice(L.device)) != hipSuccess) return hip_fail(e, "hipSetDevice");
+    uint32_t* h_nb = reinterpret_cast<uint32_t*>(L.c->h_pin + geo[d].pin_crc + align_up(4 * L.count, 64));
+    if ((e = hipMemcpyAsync(h_nb, geo[d].d_nbad, 4, hipMemcpyDeviceToHost, L.c->stream)) != hipSuccess)
+      return hip_fail(e, "hipMemcpyAsync(nbad)");
   }
-  if (seal) {
-    for (uint64_t i = 0; i < n; ++i) {
-      uint8_t* tr = buf + h[i].offset + h[i].size + 1;
-      tr[0] = static_cast<uint8_t>(crc[i]);
-      tr[1] = static_cast<uint8_t>(crc[i] >> 8);
-      tr[2] = static_cast<uint8_t>(crc[i] >> 16);
-      tr[3] = static_cast<uint8_t>(crc[i] >> 24);
+  for (HostLane& L : lanes)
+    if (!L.gi.empty() && (e = hipStreamSynchronize(L.c->stream)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+  int64_t nbad = 0;
+  for (size_t d = 0; d < lanes.size(); ++d) {
+    HostLane& L = lanes[d];
+    if (L.gi.empty()) continue;
+    const Geo& G = geo[d];
+    uint32_t* crc = reinterpret_cast<uint32_t*>(L.c->h_pin + G.pin_crc);  // (seal) lane-local
+    uint8_t* h_ok = L.c->h_pin + G.pin_crc;                                  // (verify) lane-local
+    const uint32_t* h_lcrc = reinterpret_cast<const uint32_t*>(L.c->h_pin + G.pin_lcrc);
+    if (!seal) nbad += *reinterpret_cast<const uint32_t*>(L.c->h_pin + G.pin_crc + align_up(4 * L.count, 64));
+    for (uint64_t q = 0; q < G.longs.size(); ++q) {  // the long blocks in place of their stand-ins
+      const uint64_t i = G.longs[q], li = i - L.first;
+      if (seal) {
+        crc[li] = pdb_mask(h_lcrc[q]);
+      } else {
+        const uint8_t* tr = buf + h[i].offset + h[i].size + 1;
+        const uint32_t w = static_cast<uint32_t>(tr[0]) | (static_cast<uint32_t>(tr[1]) << 8) |
+                           (static_cast<uint32_t>(tr[2]) << 16) | (static_cast<uint32_t>(tr[3]) << 24);
+        const uint8_t good = pdb_unmask(w) == h_lcrc[q] ? 1u : 0u;
+        nbad += (h_ok[li] ? 0 : -1) + (good ? 0 : 1);
+        h_ok[li] = good;
+      }
     }
-  } else if (ok) {
-    memcpy(ok, h_ok, n);
+    if (seal) {
+      for (uint64_t li = 0; li < L.count; ++li) {
+        const pdb_block_handle& b = h[L.first + li];
+        uint8_t* tr = buf + b.offset + b.size + 1;
+        tr[0] = static_cast<uint8_t>(crc[li]);
+        tr[1] = static_cast<uint8_t>(crc[li] >> 8);
+        tr[2] = static_cast<uint8_t>(crc[li] >> 16);
+        tr[3] = static_cast<uint8_t>(crc[li] >> 24);
+      }
+    } else if (ok) {
+      memcpy(ok + L.first, h_ok, L.count);
+    }
   }
   if (nbad_out) *nbad_out = nbad;
   return PDB_OK;
+}
+
+// The striping plan of a host descriptor batch over `ndev` devices, for tests (pdb_host_stripe_plan)
+int64_t stripe_plan(const pdb_blk* blk, uint64_t nblk, uint32_t ndev, uint64_t chunk, uint64_t* first, uint32_t* dev,
+                    uint64_t cap) {
+  if (!ndev || ndev > 64) return fail(PDB_EINVAL, "ndev must be 1..64");
+  const std::vector<HostGroup> g = plan_groups(nblk, ndev, chunk ? chunk : host_chunk_bytes(), [&](uint64_t i) {
+    return blk[i].len ? std::make_pair(blk[i].off & ~static_cast<uint64_t>(15), blk[i].off + blk[i].len)
+                      : std::make_pair(UINT64_MAX, uint64_t{0});
+  });
+  for (size_t k = 0; k < g.size() && k < cap; ++k) {
+    if (first) first[k] = g[k].first;
+    if (dev) dev[k] = g[k].dev;
+  }
+  return static_cast<int64_t>(g.size());
 }
 
 }  // namespace
@@ -1345,6 +1508,35 @@ int pdb_crc32c_init(int device) {
   }
   DevState* st;
   return get_state(&st);
+}
+
+int pdb_crc32c_init_mask(uint64_t device_mask) {
+  if (device_mask == 0) {
+    g_host_mask.store(0, std::memory_order_release);
+    return 1;
+  }
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess || ndev <= 0) return fail(PDB_ENODEV, "no HIP device visible (pdb_crc32c has no CPU fallback)");
+  if (ndev < 64 && (device_mask >> ndev) != 0) return fail(PDB_EINVAL, "device_mask names a device that is not visible");
+  DeviceRestore restore;
+  int n = 0;
+  for (int d = 0; d < 64; ++d) {
+    if (!((device_mask >> d) & 1u)) continue;
+    if ((e = hipSetDevice(d)) != hipSuccess) return hip_fail(e, "hipSetDevice");
+    DevState* st;
+    int rc = get_state(&st);  // the device's tables and contexts, made now
+    if (rc) return rc;
+    ++n;
+  }
+  g_host_mask.store(device_mask, std::memory_order_release);
+  return n;
+}
+
+int64_t pdb_host_stripe_plan(const pdb_blk* blk, uint64_t nblk, uint32_t ndev, uint64_t chunk_bytes, uint64_t* group_first,
+                             uint32_t* group_dev, uint64_t cap) {
+  if (nblk && !blk) return fail(PDB_EINVAL, "null blocks");
+  return stripe_plan(blk, nblk, ndev, chunk_bytes, group_first, group_dev, cap);
 }
 
 int pdb_crc32c_prepare_stream(void* stream) {

@@ -100,7 +100,12 @@ def long_blocks():
 
 if __name__ == "__main__":
     crc.init_device(0)
+    if "--mask" in sys.argv:  # the striped route (pdb_crc32c_init_mask) over device 0 alone
+        from pebblesdb_amd._native import check, lib
+
+        assert check(lib().pdb_crc32c_init_mask(1)) == 1
     golden_batches()
     reference_tables()
     long_blocks()
-    print("host staging ok (PDB_HOST_CHUNK_BYTES=%s)" % os.environ.get("PDB_HOST_CHUNK_BYTES"))
+    print("host staging ok (PDB_HOST_CHUNK_BYTES=%s%s)" % (os.environ.get("PDB_HOST_CHUNK_BYTES"),
+                                                         ", device mask 1" if "--mask" in sys.argv else ""))

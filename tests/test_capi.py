@@ -119,3 +119,68 @@ def test_argument_validation(lib):
     assert crc32c.extend(0x1234, b"") == 0x1234  # Extend over nothing is the identity
     with pytest.raises(ValueError):
         crc32c.make_blocks([0], [1 << 32])
+
+
+def _legacy_groups(offs, lens, chunk):
+    """Round 5's single-device grouping (crc32c_capi.cpp host_desc): the plan over one device must
+    reproduce it exactly."""
+    firsts, g_first, lo, hi, count = [], 0, None, 0, 0
+    for i, (o, n) in enumerate(zip(offs, lens)):
+        if n:
+            blo, bhi = o & ~15, o + n
+            nlo, nhi = (blo, bhi) if lo is None else (min(lo, blo), max(hi, bhi))
+            if count and lo is not None and nhi - nlo > chunk:
+                firsts.append(g_first)
+                g_first, lo, hi, count = i, blo, bhi, 0
+            else:
+                lo, hi = nlo, nhi
+        count += 1
+    firsts.append(g_first)
+    return firsts
+
+
+def _plan(lib, blk, ndev, chunk):
+    import numpy as np
+
+    cap = len(blk) + 8
+    first = np.zeros(cap, dtype=np.uint64)
+    dev = np.zeros(cap, dtype=np.uint32)
+    ng = lib.pdb_host_stripe_plan(blk.ctypes.data, len(blk), ndev, chunk, first.ctypes.data, dev.ctypes.data, cap)
+    assert ng > 0
+    return first[:ng].astype(np.int64), dev[:ng].astype(np.int64)
+
+
+def test_stripe_plan(lib):
+    """pdb_crc32c_init_mask's striping plan (pure host code, no device): groups are contiguous runs
+    covering every block in order, each at most `chunk` bytes of span unless one block is longer;
+    device indices are non-decreasing and each device's share of the bytes is within one group of 1/N;
+    a batch of < 8 MiB per device uses fewer devices; one device reproduces round 5's grouping."""
+    import numpy as np
+
+    rng = np.random.Generator(np.random.PCG64(3))
+    lens = rng.integers(1, 70000, size=6000).astype(np.int64)
+    lens[::97] = 0  # empty blocks ride along in whatever group they fall in
+    lens[1234] = 9 << 20  # longer than a chunk: a group of its own
+    offs = np.concatenate([[5], 5 + np.cumsum(lens + 3)[:-1]]).astype(np.int64)
+    blk = crc32c.make_blocks(offs, lens)
+    total = int(lens.sum())
+    chunk = 4 << 20
+    for ndev in (1, 2, 3, 8):
+        first, dev = _plan(lib, blk, ndev, chunk)
+        assert first[0] == 0 and (np.diff(first) > 0).all() and first[-1] < len(blk)
+        assert (np.diff(dev) >= 0).all() and dev[0] == 0
+        nd = int(dev[-1]) + 1
+        assert nd == min(ndev, total // (8 << 20))
+        ends = np.append(first[1:], len(blk))
+        share = np.zeros(nd)
+        for f, e, d in zip(first, ends, dev):
+            lo = min(int(o) & ~15 for o, n in zip(offs[f:e], lens[f:e]) if n) if lens[f:e].any() else 0
+            hi = max(int(o + n) for o, n in zip(offs[f:e], lens[f:e]) if n) if lens[f:e].any() else 0
+            assert hi - lo <= chunk or (e - f == 1) or lens[f:e].max() > chunk
+            share[d] += lens[f:e].sum()
+        assert np.abs(share - total / nd).max() <= chunk + lens.max()
+        if ndev == 1:
+            assert first.tolist() == _legacy_groups(offs.tolist(), lens.tolist(), chunk)
+    # a small batch stays on one device
+    first, dev = _plan(lib, blk[:100], 8, 0)
+    assert dev.max() == 0 and len(first) == 1

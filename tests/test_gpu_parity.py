@@ -383,19 +383,21 @@ def test_host_batches_grouped_and_verify_host(crc, golden, oracle_lib):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("chunk", [8192, 3 << 20])
-def test_host_staging_small_groups_subprocess(crc, chunk):
+@pytest.mark.parametrize("chunk,mask", [(8192, False), (3 << 20, False), (3 << 20, True)])
+def test_host_staging_small_groups_subprocess(crc, chunk, mask):
     """The host batch / seal / verify entry points with the staging group span forced small (most
     groups hold one or two blocks, big blocks their own group), in a child process that sets
-    PDB_HOST_CHUNK_BYTES before loading the library (tests/host_staging_check.py)."""
+    PDB_HOST_CHUNK_BYTES before loading the library (tests/host_staging_check.py); with `mask`, through
+    pdb_crc32c_init_mask({0}) -- the striped host route on the one device this box has (the plan over
+    more devices: tests/test_capi.py::test_stripe_plan)."""
     import os
     import subprocess
     import sys
 
     here = os.path.dirname(os.path.abspath(__file__))
     env = dict(os.environ, PDB_HOST_CHUNK_BYTES=str(chunk))
-    r = subprocess.run([sys.executable, os.path.join(here, "host_staging_check.py")], env=env, capture_output=True,
-                       text=True, timeout=300)
+    r = subprocess.run([sys.executable, os.path.join(here, "host_staging_check.py")] + (["--mask"] if mask else []), env=env,
+                       capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "host staging ok" in r.stdout
 
