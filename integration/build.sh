@@ -10,6 +10,9 @@
 #                          replaced by pdb_table.cc (scans with verify_checksums: ~1-MiB read-ahead
 #                          windows checked in one pdb_sst_verify_host batch)
 #   pdb_dbbench_gpu_table_noscan  as gpu_table over the reference's own table.cc (A/B: no read-ahead)
+#   (gpu_table and gpu_all read the WAL / MANIFEST at recovery through integration/pdb_log_reader.cc:
+#    one GPU verify batch per log file instead of db/log_reader.cc's CRC per record)
+#   logreader_gpu          oracle/ref_logreader.cc's harness over pdb_log_reader.cc (corrupted-log parity)
 #   pdb_dbbench_gpu_all    as gpu_table, and util/crc32c.h -> include/pebblesdb_amd/crc32c.h for every
 #                          other call site (log_writer/log_reader records on the scalar GPU service)
 #   pdb_dbbench_buffered_cpu  as gpu_table (buffered emission, read-ahead windows) with every CRC on
@@ -44,6 +47,8 @@ ENGINE="db/builder.cc db/db_impl.cc db/db_iter.cc db/dbformat.cc db/filename.cc 
         util/env.cc util/env_posix.cc util/filter_policy.cc util/hash.cc util/histogram.cc
         util/logging.cc util/options.cc util/status.cc util/testutil.cc port/port_posix.cc"
 TABLE_REF="table/table_builder.cc table/format.cc table/table.cc"
+# the engine without db/log_reader.cc (the GPU builds link integration/pdb_log_reader.cc instead)
+ENGINE_NOLOG="$(echo $ENGINE | tr ' ' '\n' | grep -v '^db/log_reader.cc$' | tr '\n' ' ')"
 DEFS="-DLEVELDB_PLATFORM_POSIX -DOS_LINUX -DHAVE_FFLUSH_UNLOCKED -DHAVE_FREAD_UNLOCKED"
 DEFS="$DEFS -DHAVE_FWRITE_UNLOCKED -DHAVE_FDATASYNC -DHAVE_DECL_FDATASYNC=1 -DNDEBUG"
 CXX="g++ -O2 -std=c++11 -w -pthread"
@@ -78,6 +83,8 @@ $CXX $DEFS $HOOKI -DPDB_HOOKS=1 -c "$HERE/pdb_dbbench.cc" -o "$B/obj_hooks/dbben
 $CXX $DEFS $HOOKI -c "$ROOT/oracle/ref_sstwriter.cc" -o "$B/obj_hooks/sstwriter.o"
 $CXX $DEFS $HOOKI -c "$HERE/pdb_verify.cc" -o "$B/obj_hooks/pdb_verify.o"
 $CXX $DEFS $HOOKI -c "$HERE/pdb_tablegen.cc" -o "$B/obj_hooks/pdb_tablegen.o"
+$CXX $DEFS $HOOKI -c "$HERE/pdb_log_reader.cc" -o "$B/obj_hooks/pdb_log_reader.o"
+$CXX $DEFS $HOOKI -c "$ROOT/oracle/ref_logreader.cc" -o "$B/obj_hooks/logreader.o"
 $CXX $DEFS $HOOKI -DPDB_HOOKS=0 -c "$HERE/pdb_table_scan.cc" -o "$B/obj_hooks/table_scan_ref.o"
 $CXX $DEFS $HOOKI -DPDB_HOOKS=1 -c "$HERE/pdb_table_scan.cc" -o "$B/obj_hooks/table_scan_gpu.o"
 
@@ -87,11 +94,16 @@ HOOKS="$B/obj_hooks/pdb_table_builder.o $B/obj_hooks/pdb_format.o $B/obj_hooks/p
 # (A/B: the same hooks over the reference's own table reader, i.e. without the scan read-ahead)
 HOOKS_NOSCAN="$B/obj_hooks/pdb_table_builder.o $B/obj_hooks/pdb_format.o $B/obj_ref/table_table.cc.o"
 $CXX -o "$B/pdb_dbbench_cpu" "$B/obj_hooks/dbbench_cpu.o" $(objs "$B/obj_ref" $ENGINE $TABLE_REF util/crc32c.cc)
-$CXX -o "$B/pdb_dbbench_gpu_table" "$B/obj_hooks/dbbench_hooks.o" $HOOKS \
-  $(objs "$B/obj_ref" $ENGINE util/crc32c.cc) $GPU
+# (the WAL / MANIFEST readers of recovery: one GPU batch per log file, integration/pdb_log_reader.cc)
+LOGRD="$B/obj_hooks/pdb_log_reader.o"
+$CXX -o "$B/pdb_dbbench_gpu_table" "$B/obj_hooks/dbbench_hooks.o" $HOOKS $LOGRD \
+  $(objs "$B/obj_ref" $ENGINE_NOLOG util/crc32c.cc) $GPU
 $CXX -o "$B/pdb_dbbench_gpu_table_noscan" "$B/obj_hooks/dbbench_hooks.o" $HOOKS_NOSCAN \
   $(objs "$B/obj_ref" $ENGINE util/crc32c.cc) $GPU
-$CXX -o "$B/pdb_dbbench_gpu_all" "$B/obj_hooks/dbbench_hooks.o" $HOOKS $(objs "$B/obj_shim" $ENGINE) $GPU
+$CXX -o "$B/pdb_dbbench_gpu_all" "$B/obj_hooks/dbbench_hooks.o" $HOOKS $LOGRD $(objs "$B/obj_shim" $ENGINE_NOLOG) $GPU
+# the engine's log::Reader (pdb_log_reader.cc) under the reference reader's harness: the corrupted-log
+# fixtures through the engine path (tests/test_log.py)
+$CXX -o "$B/logreader_gpu" "$B/obj_hooks/logreader.o" $LOGRD $(objs "$B/obj_ref" $ENGINE_NOLOG $TABLE_REF util/crc32c.cc) $GPU
 # attribution A/B: buffered emission + read-ahead windows, every CRC on the CPU
 # (the reference's crc32c.cc); no GPU library linked
 HOOKS_CPU="$B/obj_hooks_cpu/pdb_table_builder.o $B/obj_hooks_cpu/pdb_format.o $B/obj_hooks_cpu/pdb_table.o"
@@ -104,4 +116,4 @@ $CXX -o "$B/pdb_verify_gpu" "$B/obj_hooks/pdb_verify.o" "$B/obj_hooks/pdb_format
 $CXX -o "$B/pdb_tablegen" "$B/obj_hooks/pdb_tablegen.o" $(objs "$B/obj_ref" $ENGINE $TABLE_REF util/crc32c.cc)
 $CXX -o "$B/table_scan_ref" "$B/obj_hooks/table_scan_ref.o" $(objs "$B/obj_ref" $ENGINE $TABLE_REF util/crc32c.cc)
 $CXX -o "$B/table_scan_gpu" "$B/obj_hooks/table_scan_gpu.o" $HOOKS $(objs "$B/obj_ref" $ENGINE util/crc32c.cc) $GPU
-echo "built $B/{pdb_tablegen,table_scan_ref,table_scan_gpu,pdb_dbbench_cpu,pdb_dbbench_gpu_table,pdb_dbbench_gpu_table_noscan,pdb_dbbench_gpu_all,pdb_dbbench_buffered_cpu,sstwriter_gpu,leveldb_verify_ref,pdb_verify_gpu}"
+echo "built $B/{logreader_gpu,pdb_tablegen,table_scan_ref,table_scan_gpu,pdb_dbbench_cpu,pdb_dbbench_gpu_table,pdb_dbbench_gpu_table_noscan,pdb_dbbench_gpu_all,pdb_dbbench_buffered_cpu,sstwriter_gpu,leveldb_verify_ref,pdb_verify_gpu}"

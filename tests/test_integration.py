@@ -324,3 +324,36 @@ def test_repairdb_paranoid_gpu_matches_reference(gpu, tmp_path):
     assert any("entries repaired" in l for l in ref_log), ref_log
     assert my_log == ref_log and my_seq == ref_seq
     assert hook["scan_batches"] > 0 and hook["seal_blocks"] > 0 and hook["verify_failed"] > 0
+
+
+def test_reopen_recovers_wal_through_batched_reader(gpu, tmp_path):
+    """DB::Open's recovery through the engine's batched log::Reader (integration/pdb_log_reader.cc:
+    one GPU verify per WAL / MANIFEST file, db/db_impl.cc:516-600, db/version_set.cc:2450): a
+    fillrandom with a 512 MiB memtable leaves every write in the WAL (nothing flushed; the harness
+    exits without closing, as a crash would); each build reopens its own database and a verified
+    readseq must deliver the same keys and values (FNV hash) on the GPU build and the reference CPU
+    build, and the GPU build must reopen the CPU build's database to the same content.  The reopen
+    ("open") times of both builds are printed beside each other."""
+    num = 100000
+    dbs = {}
+    for variant in ("gpu_table", "cpu"):
+        exe = _exe(f"pdb_dbbench_{variant}")
+        db = str(tmp_path / variant)
+        rc, out, err = _run([exe, "--benchmarks=fillrandom", f"--num={num}", "--value_size=1024",
+                             "--write_buffer_size=536870912", f"--db={db}", "--quiesce_ms=0"])
+        assert rc == 0, out + err
+        dbs[variant] = db
+    assert not [f for f in os.listdir(dbs["gpu_table"]) if f.endswith((".ldb", ".sst"))]  # all of it in the WAL
+    res = {}
+    for variant, db in (("gpu_table", dbs["gpu_table"]), ("cpu", dbs["cpu"]), ("gpu_table_on_cpu_db", dbs["cpu"])):
+        exe = _exe("pdb_dbbench_" + variant.replace("_on_cpu_db", ""))
+        rc, out, err = _run([exe, "--benchmarks=readseq", "--use_existing_db=1", "--verify_checksums=1", "--hash=1",
+                             f"--num={num}", f"--db={db}", "--quiesce_ms=0"])
+        assert rc == 0, out + err
+        import re
+
+        res[variant] = dict(_bench_json(out), hash=re.search(r"\(hash ([0-9a-f]{16})\)", out).group(1))
+    print(json.dumps({v: {"open_s": r["open"]["seconds"], "readseq_ops": r["readseq"]["ops"]} for v, r in res.items()}))
+    h = {v: (r["readseq"]["ops"], r["hash"]) for v, r in res.items()}
+    assert h["gpu_table"] == h["cpu"] == h["gpu_table_on_cpu_db"], h
+    assert h["cpu"][0] > 0.6 * num  # fillrandom's distinct keys
