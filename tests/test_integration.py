@@ -340,7 +340,7 @@ def test_reopen_recovers_wal_through_batched_reader(gpu, tmp_path):
         exe = _exe(f"pdb_dbbench_{variant}")
         db = str(tmp_path / variant)
         rc, out, err = _run([exe, "--benchmarks=fillrandom", f"--num={num}", "--value_size=1024",
-                             "--write_buffer_size=536870912", f"--db={db}", "--quiesce_ms=0"])
+                             "--write_buffer_size=536870912", f"--db={db}"])
         assert rc == 0, out + err
         dbs[variant] = db
     assert not [f for f in os.listdir(dbs["gpu_table"]) if f.endswith((".ldb", ".sst"))]  # all of it in the WAL
@@ -348,7 +348,7 @@ def test_reopen_recovers_wal_through_batched_reader(gpu, tmp_path):
     for variant, db in (("gpu_table", dbs["gpu_table"]), ("cpu", dbs["cpu"]), ("gpu_table_on_cpu_db", dbs["cpu"])):
         exe = _exe("pdb_dbbench_" + variant.replace("_on_cpu_db", ""))
         rc, out, err = _run([exe, "--benchmarks=readseq", "--use_existing_db=1", "--verify_checksums=1", "--hash=1",
-                             f"--num={num}", f"--db={db}", "--quiesce_ms=0"])
+                             f"--num={num}", f"--db={db}"])
         assert rc == 0, out + err
         import re
 
