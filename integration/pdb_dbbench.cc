@@ -24,6 +24,7 @@
 #include <dirent.h>
 #include <execinfo.h>
 #include <pthread.h>
+#include <sys/resource.h>
 #include <sys/stat.h>
 #include <signal.h>
 #include <unistd.h>
@@ -64,6 +65,15 @@ struct Flags {
   bool hash = false;  // readseq: FNV-1a-64 of every key and value (parity checks between builds)
   std::string db = "/tmp/pdb_dbbench";
 } F;
+
+// process CPU time (user + system) at the start of the running benchmark: Report prints the delta,
+// so a run states the host CPU it spent per operation beside its rate (point reads: DESIGN.md §8)
+double g_cpu0 = 0;
+double CpuSec() {
+  rusage ru;
+  getrusage(RUSAGE_SELF, &ru);
+  return ru.ru_utime.tv_sec + 1e-6 * ru.ru_utime.tv_usec + ru.ru_stime.tv_sec + 1e-6 * ru.ru_stime.tv_usec;
+}
 
 double NowSec() {
   timespec ts;
@@ -111,10 +121,11 @@ void Report(const Result& r) {
     printf("%-12s : %11.3f micros/op; %s\n", r.name, us, r.note.c_str());
   const double wall = r.wall > 0 ? r.wall : r.seconds;
   printf("{\"bench\": \"%s\", \"ops\": %ld, \"seconds\": %.4f, \"micros_per_op\": %.4f, \"MB_s\": %.2f, "
-         "\"verify_checksums\": %s, \"threads\": %d, \"wall_s\": %.4f, \"ops_per_s\": %.1f",
+         "\"verify_checksums\": %s, \"threads\": %d, \"wall_s\": %.4f, \"ops_per_s\": %.1f, \"cpu_s\": %.4f, "
+         "\"cpu_us_per_op\": %.3f",
          r.name, r.ops, r.seconds, us, r.bytes > 0 ? mbs : 0.0, F.verify_checksums ? "true" : "false",
          r.threads > 0 ? r.threads : 1, wall,
-         r.ops / wall);
+         r.ops / wall, CpuSec() - g_cpu0, (CpuSec() - g_cpu0) * 1e6 / (r.ops ? r.ops : 1));
 #if PDB_HOOKS
   pdb_hook_stats s;
   pdb_hook_stats_get(&s);
@@ -404,6 +415,7 @@ int main(int argc, char** argv) {
   // DB::Open: with --use_existing_db, the recovery of the MANIFEST and of every WAL not yet in a table
   // (db_impl.cc:516-600, version_set.cc:2450) -- through the batched reader in the GPU builds
   const double t_open = NowSec();
+  g_cpu0 = CpuSec();
   leveldb::DB* db = Open(fp, cache);
   Report(Result{"open", 1, NowSec() - t_open, 0, F.use_existing_db ? "(recovery)" : "(new database)"});
   size_t pos = 0;
@@ -416,6 +428,7 @@ int main(int argc, char** argv) {
 #if PDB_HOOKS
     pdb_hook_stats_reset();
 #endif
+    g_cpu0 = CpuSec();
     if (name == "fillseq") Report(Write(db, true));
     else if (name == "fillrandom") Report(Write(db, false));
     else if (name == "readrandom") Report(ReadRandom(db));
