@@ -37,7 +37,17 @@
  *     util/crc32c.cc:19-23,589); a single span (pdb_crc32c_extend*) may be longer.
  *   - Thread-safe: host entry points take one of 4 staging contexts per device; device entry points
  *     are pure launches.
- *     The library has no mutable global switches: every result depends only on the arguments.
+ *   - Every result depends only on the arguments.  The ROUTE (never the result) also depends on
+ *     pdb_crc32c_init_mask (which devices host batches stage through) and on these environment
+ *     variables, each read once per process, for experiments and diagnostics:
+ *       PDB_HOST_CHUNK_BYTES  host staging group span (default 256 MiB)
+ *       PDB_HOST_MAPPED=0     sstable host batches in pdb_host_alloc memory take the DMA route,
+ *                             not zero-copy
+ *       PDB_LONG_BLOCK=<n>    host sstable batches: the split threshold of long blocks (16 KiB)
+ *       PDB_SCALAR_WAIT=poll|sync  scalar Extend launches per call instead of the persistent server
+ *       PDB_SERVER_BOX=host   the scalar server's request area in pinned host memory, not in
+ *                             device memory through the large BAR
+ *       PDB_SEAL_STAMPS=<path>, PDB_SERVER_STAMPS=<path>  per-call timestamps written at exit
  *   - Device-resident batches may read a few bytes outside a block: up to 15 bytes before its first
  *     byte and up to 3 bytes past its last one, never outside the 4-B-aligned dwords and 16-B lines
  *     that hold the block's bytes.  A buffer handed to a device entry point must therefore stay

@@ -562,6 +562,31 @@ uint32_t my_slot() {
   return slot;
 }
 
+// Scalar waiters of this process (server_call's wait loop) and the CPUs it may run on: the affinity
+// mask, capped by a cgroup v2 CPU quota when one is set (a container's nproc shows the host's CPUs).
+std::atomic<uint32_t> g_waiters{0};
+struct WaitGuard {
+  WaitGuard() { g_waiters.fetch_add(1, std::memory_order_relaxed); }
+  ~WaitGuard() { g_waiters.fetch_sub(1, std::memory_order_relaxed); }
+};
+uint32_t wait_cpus() {
+  static const uint32_t v = [] {
+    cpu_set_t set;
+    uint32_t n = sched_getaffinity(0, sizeof(set), &set) == 0 ? static_cast<uint32_t>(CPU_COUNT(&set)) : 1u;
+    if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+      char quota[32];
+      unsigned long long period = 0;
+      if (fscanf(f, "%31s %llu", quota, &period) == 2 && strcmp(quota, "max") != 0 && period) {
+        const unsigned long long c = (strtoull(quota, nullptr, 10) + period - 1) / period;
+        if (c && c < n) n = static_cast<uint32_t>(c);
+      }
+      fclose(f);
+    }
+    return n ? n : 1u;
+  }();
+  return v;
+}
+
 // One request (n <= kServerCap) in this thread's slot: stage the bytes, post the request word,
 // spin on the slot's response word.  No device-wide lock: other threads' requests proceed in
 // their own slots.  An instance that left without answering (idle / lifetime exit racing the
@@ -580,13 +605,15 @@ int server_call(DevState* st, uint32_t init, const uint8_t* data, uint64_t n, ui
   const uint64_t h1 = st->stamps ? mono_ns() : 0;
   const uint64_t* resp = srv_resp(st, slot);
   double t0 = 0;
-  // Wait: spin (pause) for kSpinNs, then give the CPU back between polls (sched_yield): a verified
-  // point read waits ~5 us for its answer, and with more reader threads than the process's CPUs
-  // the spinning waiters took the CPU the others needed (16 threads: 411 k/s against 534 at 8;
-  // DESIGN.md §8, INTEGRATION.md §3, the host CPU per read measured by pdb_dbbench's cpu_us_per_op)
-  constexpr uint64_t kSpinNs = 2000;
-  const uint64_t w0 = mono_ns();
-  bool yielding = false;
+  // Wait: spin (pause) while this process has no more waiters than CPUs, else give the CPU back between
+  // polls (sched_yield).  A verified point read waits ~5 us for its answer; spinning is the cheapest
+  // wait while every waiter has a CPU (8 / 16 reader threads on a 16-CPU box: 560 k / 612 k reads/s
+  // spinning against 369 k / 393 k yielding after 2 us), and only with more waiters than CPUs do the
+  // spinners take the CPU the others need (32 threads: 246 k spinning, 369 k yielding).  This form, on
+  // one box: 551 / 684 / 498 / 404 k reads/s at 8 / 16 / 24 / 32 threads against 453 / 506 / 407 / 286
+  // k always spinning -- profiles/r06/point_reads, DESIGN.md §8, INTEGRATION.md §3.
+  WaitGuard wg;
+  const uint32_t cpus = wait_cpus();
   for (uint32_t spin = 1;; ++spin) {
     const uint64_t r = __atomic_load_n(resp, __ATOMIC_ACQUIRE);
     if (static_cast<uint32_t>(r >> 32) == seq) {
@@ -605,12 +632,8 @@ int server_call(DevState* st, uint32_t init, const uint8_t* data, uint64_t n, ui
       if (static_cast<uint32_t>(__atomic_load_n(resp, __ATOMIC_ACQUIRE) >> 32) == seq) continue;
       if ((rc = server_ensure(st, true, ep))) return rc;
     }
-    if (yielding) {
-      sched_yield();
-    } else {
-      __builtin_ia32_pause();
-      if ((spin & 7u) == 0 && mono_ns() - w0 > kSpinNs) yielding = true;
-    }
+    if (g_waiters.load(std::memory_order_relaxed) > cpus) sched_yield();
+    else __builtin_ia32_pause();
     if ((spin & 0xFFFFu) == 0) {
       const double t = now_s();
       if (t0 == 0) t0 = t;

@@ -763,13 +763,11 @@ struct SstSrc {
     return __builtin_nontemporal_load(reinterpret_cast<const u32x4a4*>(h + i));
   }
   __device__ __forceinline__ BlkDesc make(uint64_t off, uint64_t size) const {
-    // (len >= 5: every launcher's image holds at least one trailer -- the C-ABI refuses a smaller
-    // buffer -- so the kernel keeps no "len >= 5" flag live across its loops: it was one of the two
-    // VGPRs the 12-wave verify spilled, 1.5 MB of scratch writes per 1 M-block launch)
-    // (off + size <= lim, not size <= lim - off: the subtraction made the compiler keep a VGPR copy
-    // of lim's high half live, the other spill; off <= lim and size < 2^32 rule out an overflow)
-    const uint64_t lim = len - 5;
-    const bool ok = size < 0xFFFFFFFFull && off <= lim && off + size <= lim;
+    // (the 12-wave verify spills 2 VGPRs in its prologue, ~1.5 MB of scratch writes per 1 M-block
+    // launch: uniform values the compiler keeps as VGPR copies.  Writing this check as off + size <=
+    // len - 5 without the len >= 5 term took them to 1 and cost the 12-wave seal 1.2 %, both orders on
+    // one box (tools/ab_lane.sh, profiles/r06/ab_lane/ab_spill.log): not kept.)
+    const bool ok = len >= 5 && off <= len - 5 && size <= len - 5 - off && size < 0xFFFFFFFFull;
     return ok ? BlkDesc{buf + off, static_cast<uint32_t>(size) + 1u, 0xFFFFFFFFu} : BlkDesc{buf, 0u, 0u};
   }
   __device__ __forceinline__ BlkDesc finish(const Raw& r) const { return make(uniform64(r.x, r.y), uniform64(r.z, r.w)); }

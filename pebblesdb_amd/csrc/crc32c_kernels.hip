@@ -119,7 +119,8 @@ __global__ __launch_bounds__(1024) void span_combine_many_kernel(const uint32_t*
 // launch is made whether or not anything was exported, and returns at once when nothing was.
 __global__ __launch_bounds__(kThreads) void crc_longpiece_kernel(const uint32_t* __restrict__ tabs, LongLane ll) {
   const uint64_t np = ll.hdr[0] & kLongPieceMask;
-  if (np == 0) return;
+  // (a workgroup whose share of the pieces is empty leaves before staging its 160 KiB of tables)
+  if (np * blockIdx.x / gridDim.x == np * (blockIdx.x + 1u) / gridDim.x) return;
   sized_kernel_body<PieceSrc, LeafSink, true, 4>(tabs, PieceSrc{ll.piece}, np, LeafSink{ll.leaf});
 }
 
@@ -141,9 +142,12 @@ __global__ __launch_bounds__(256) void long_combine_kernel(LongLane ll, Sink sin
   __shared__ uint32_t ops[kCombLog2][1024];  // level k: shift 4096 << k (power-of-two operator 12 + k)
   const unsigned long long hw = ll.hdr[0];
   const uint32_t nrec = static_cast<uint32_t>(hw >> 40);
-  if (nrec == 0) return;  // (grid-uniform: nothing exported, nothing to reset)
+  // Only the min(records, grid) workgroups with a record take part (and count themselves out below):
+  // the others leave at once.  One that starts after the reset reads 0 records and leaves too -- every
+  // workgroup with a record has counted itself before the reset.
+  if (blockIdx.x >= nrec) return;
   const uint32_t t = threadIdx.x;
-  if (blockIdx.x < nrec) {
+  {
     uint32_t staged = 0;  // level operators staged so far (grown as records need them: a 64-KiB block needs 5)
     for (uint32_t r = blockIdx.x; r < nrec; r += gridDim.x) {
       const LongRec R = ll.rec[r];
@@ -189,7 +193,7 @@ __global__ __launch_bounds__(256) void long_combine_kernel(LongLane ll, Sink sin
   __syncthreads();
   if (t == 0) {
     __threadfence();
-    if (atomicAdd(ll.hdr + 1, 1ull) + 1ull == gridDim.x) {
+    if (atomicAdd(ll.hdr + 1, 1ull) + 1ull == (nrec < gridDim.x ? nrec : gridDim.x)) {
       ll.hdr[0] = 0ull;
       ll.hdr[1] = 0ull;
     }

@@ -35,7 +35,7 @@ for s in "$@"; do
     counters_span) step counters_span 900 bash tools/counters_span.sh ${TAG}_span wal100 wal400 wal1000 wal ;;
     prof_wal) for w in wal100 wal400 wal1000 wal; do step prof_$w 500 bash tools/profile.sh ${TAG}_prof_$w $w || exit 1; done ;;
     # every §8(f) row and C3, 50-step bench lines and rocprof evidence
-    bench_rows) for w in c3 sstable sst_verify sst_seal sst_crc wal wal100 wal400 wal1000; do step bench_$w 300 python bench.py --workload $w --no-copy-inclusive --steps 50 || exit 1; done ;;
+    bench_rows) for w in c3 sstable sst_verify sst_seal sst_crc sst_tables wal wal100 wal400 wal1000; do step bench_$w 300 python bench.py --workload $w --no-copy-inclusive --steps 50 || exit 1; done ;;
     prof_c2) step prof_c2 700 bash tools/profile.sh ${TAG}_prof_c2 c2 ;;
     prof_list) for w in ${PROF_WL:-c2}; do step prof_$w 700 bash tools/profile.sh ${TAG}_prof_$w $w || exit 1; done ;;
     copyinc) step copyinc 600 python tools/copy_inclusive.py ;;

@@ -6,7 +6,8 @@ seal / verify batch of 16 MiB of 4-KiB blocks, with and without one long block:
   * device route: pdb_sst_seal_device / _verify_device / _crc_device on the image in HBM (the
     long-block lane), kernel-side microseconds per call from HIP events around 50 back-to-back calls.
 One JSON line per route and long-block size; the device lines also give the cost per MiB of the
-batch relative to the batch without the long block."""
+batch relative to the batch without the long block.  --device-only skips the host routes (for a kernel
+trace of the device route: tools/long_lane_trace.sh)."""
 import ctypes
 import json
 import os
@@ -53,7 +54,8 @@ def main():
         pin[:] = img
         page = img.copy()
         ok = np.zeros(nblk, dtype=np.uint8)
-        for route, ptr in (("pageable", page.ctypes.data), ("pinned", p.value)):
+        routes = () if "--device-only" in sys.argv else (("pageable", page.ctypes.data), ("pinned", p.value))
+        for route, ptr in routes:
             seal = per_call(lambda: check(lib().pdb_sst_seal_host(ptr, total, h.ctypes.data, nblk)))
             ver = per_call(lambda: lib().pdb_sst_verify_host(ptr, total, h.ctypes.data, nblk, ok.ctypes.data))
             assert ok.all(), route

@@ -23,10 +23,11 @@ print(json.dumps({"build": sys.argv[2], "threads": int(sys.argv[3]), "ops_per_s"
                   "cpu_us_per_op": d["cpu_us_per_op"], "micros_per_op": d["micros_per_op"]}), flush=True)
 PY
 }
-for t in 1 8 16 32; do run cpu $B/pdb_dbbench_cpu $t; done
+run warm $B/pdb_dbbench_cpu 8   # page cache warm before anything is recorded
+for t in 1 8 16 24 32; do run cpu $B/pdb_dbbench_cpu $t; done
 for lib in "$@"; do
   cp "ab/$lib.so" pebblesdb_amd/_lib/libpdb_crc32c.so
-  for t in 1 8 16 32; do run "gpu_$lib" $B/pdb_dbbench_gpu_table $t; done
+  for t in 1 8 16 24 32; do run "gpu_$lib" $B/pdb_dbbench_gpu_table $t; done
 done
 for t in 8 16; do run cpu_again $B/pdb_dbbench_cpu $t; done
 cp "$OUT/orig.so" pebblesdb_amd/_lib/libpdb_crc32c.so
