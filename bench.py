@@ -54,6 +54,8 @@ def parse():
                          "filter, metaindex and index blocks) written by the reference TableBuilder; wal: row 3, "
                          "the log record CRC over 32-KiB log blocks")
     ap.add_argument("--tables", type=int, default=4, help="sst_tables: tables per GPU")
+    ap.add_argument("--tables-dir", default=None,
+                    help="sst_tables: keep the generated tables in this directory and reuse them")
     ap.add_argument("--table-keys", type=int, default=1000000, help="sst_tables: keys per table (1 KiB values)")
     ap.add_argument("--nblk", type=int, default=None,
                     help="blocks per GPU (c2/sstable); default 1M (C2) on one GPU and, for c2 with --gpus N > 1, "
@@ -211,13 +213,14 @@ def wal_layout(total_bytes: int, payload: int, block: int = 32768):
     return np.asarray(offs, dtype=np.int64), np.asarray(lens, dtype=np.int64)
 
 
-def real_tables(ntables: int, nkeys: int, value_size: int, seed: int):
+def real_tables(ntables: int, nkeys: int, value_size: int, seed: int, keep_dir: str = None):
     """`ntables` real sstables written by the reference engine's TableBuilder as shipped
     (integration/_build/pdb_tablegen, built by integration/build.sh from the reference sources in
     place; CPU CRC trailers), in parallel, into a temporary directory on this host, concatenated.
     Returns (image bytes, handles of every block -- data blocks from each index block, then the
     filter block from the metaindex, the metaindex and the index (table/table.cc:70-170) -- rebased
-    on the image, per-table facts)."""
+    on the image, per-table facts).  With `keep_dir` the tables are kept there and reused by the next
+    call with the same arguments (tools/profile.sh makes them before the profiled run)."""
     import shutil
     import subprocess
     import tempfile
@@ -228,11 +231,12 @@ def real_tables(ntables: int, nkeys: int, value_size: int, seed: int):
     exe = os.path.join(ROOT, "integration", "_build", "pdb_tablegen")
     if not os.path.exists(exe):
         raise SystemExit(f"bench.py: {exe} missing (integration/build.sh builds it)")
-    tmp = tempfile.mkdtemp(prefix="pdb_tables_")
+    tmp = keep_dir or tempfile.mkdtemp(prefix="pdb_tables_")
+    os.makedirs(tmp, exist_ok=True)
     try:
-        paths = [os.path.join(tmp, f"t{i}.sst") for i in range(ntables)]
+        paths = [os.path.join(tmp, f"t{i}_{nkeys}_{value_size}_{seed + i}.sst") for i in range(ntables)]
         procs = [subprocess.Popen([exe, p, str(nkeys), str(value_size), str(seed + i)], stdout=subprocess.PIPE)
-                 for i, p in enumerate(paths)]
+                 for i, p in enumerate(paths) if not os.path.exists(p)]
         for pr in procs:
             if pr.wait() != 0:
                 raise SystemExit("bench.py: pdb_tablegen failed")
@@ -254,7 +258,8 @@ def real_tables(ntables: int, nkeys: int, value_size: int, seed: int):
             base += len(im)
         return np.concatenate(parts), np.concatenate(hs), info
     finally:
-        shutil.rmtree(tmp, ignore_errors=True)
+        if not keep_dir:
+            shutil.rmtree(tmp, ignore_errors=True)
 
 
 def zipf_kib_sizes(n: int, seed: int, kmax: int = 64) -> np.ndarray:
@@ -422,7 +427,7 @@ def main():
         from pebblesdb_amd import table as T
         from pebblesdb_amd._native import check, lib
 
-        img, hs, tinfo = real_tables(args.tables, args.table_keys, 1024, 401 + 16 * rank)
+        img, hs, tinfo = real_tables(args.tables, args.table_keys, 1024, 401 + 16 * rank, args.tables_dir)
         total = len(img)
         data = torch.from_numpy(img).to(dev)
         nblk = len(hs)

@@ -178,7 +178,8 @@ int pdb_crc32c_verify_device(const void* d_base, const pdb_blk* d_blk, uint64_t 
  * blocks (and a seal writes the trailers) through the mapping, one launch, no DMA; the other host
  * entry points DMA from it without the runtime's pageable bounce copies.  Any host memory stays
  * valid for every entry point; this only changes the rate.  Freed allocations are kept for reuse
- * (a few), so staging per table does not page-lock anew.  *out = NULL for bytes == 0.  Free with
+ * (at most 8 and 256 MiB in all, the largest released first), so staging per table does not
+ * page-lock anew.  *out = NULL for bytes == 0.  Free with
  * pdb_host_free (NULL is a no-op; any other pointer not from pdb_host_alloc: PDB_EINVAL). */
 int pdb_host_alloc(uint64_t bytes, void** out);
 int pdb_host_free(void* p);

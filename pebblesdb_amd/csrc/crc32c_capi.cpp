@@ -342,7 +342,8 @@ int ensure_pin(HostCtx* c, size_t bytes) {
 
 // pdb_host_alloc's allocations: page-locked, with their device mappings.  A freed one is kept for
 // reuse (a TableBuilder stages every table in a fresh buffer; page-locking megabytes per table costs
-// more than the seal), up to kPinKeep of them.
+// more than the seal), at most kPinKeep of them and kPinKeepBytes in all: past either, the largest
+// kept ones are released first.
 struct PinAlloc {
   uint8_t* h;
   uint8_t* d;  // device mapping (null: none)
@@ -352,6 +353,7 @@ struct PinAlloc {
 std::mutex g_pin_mu;
 std::vector<PinAlloc> g_pins;
 constexpr size_t kPinKeep = 8;
+constexpr size_t kPinKeepBytes = size_t(256) << 20;
 
 // The device mapping of [p, p + len) when it lies inside one live pdb_host_alloc allocation, else null.
 uint8_t* pin_mapping(const void* p, uint64_t len) {
@@ -1522,19 +1524,26 @@ int pdb_host_alloc(uint64_t bytes, void** out) {
 int pdb_host_free(void* p) {
   if (!p) return PDB_OK;
   std::lock_guard<std::mutex> lk(g_pin_mu);
-  size_t kept = 0, at = g_pins.size();
-  for (size_t i = 0; i < g_pins.size(); ++i) {
+  size_t at = g_pins.size();
+  for (size_t i = 0; i < g_pins.size(); ++i)
     if (g_pins[i].h == p && g_pins[i].used) at = i;
-    kept += !g_pins[i].used;
-  }
   if (at == g_pins.size()) return fail(PDB_EINVAL, "pdb_host_free: not a live pdb_host_alloc allocation");
-  if (kept < kPinKeep) {
-    g_pins[at].used = false;
-    return PDB_OK;
+  g_pins[at].used = false;
+  hipError_t err = hipSuccess;
+  for (;;) {  // release the largest kept allocations while the cache is over either cap
+    size_t kept = 0, bytes = 0, big = g_pins.size();
+    for (size_t i = 0; i < g_pins.size(); ++i)
+      if (!g_pins[i].used) {
+        ++kept;
+        bytes += g_pins[i].cap;
+        if (big == g_pins.size() || g_pins[i].cap > g_pins[big].cap) big = i;
+      }
+    if (kept <= kPinKeep && bytes <= kPinKeepBytes) break;
+    const hipError_t e = hipHostFree(g_pins[big].h);
+    if (e != hipSuccess && err == hipSuccess) err = e;
+    g_pins.erase(g_pins.begin() + static_cast<std::ptrdiff_t>(big));
   }
-  g_pins.erase(g_pins.begin() + static_cast<std::ptrdiff_t>(at));
-  hipError_t e = hipHostFree(p);
-  return e == hipSuccess ? PDB_OK : hip_fail(e, "hipHostFree");
+  return err == hipSuccess ? PDB_OK : hip_fail(err, "hipHostFree");
 }
 
 int pdb_crc32c_init(int device) {

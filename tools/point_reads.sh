@@ -10,6 +10,8 @@ mkdir -p "$OUT"
 B=integration/_build
 DB=/tmp/pdb_point_reads
 cp pebblesdb_amd/_lib/libpdb_crc32c.so "$OUT/orig.so"
+# what the scalar wait sees as this process's CPUs (server_call: the affinity mask, capped by the quota)
+echo "{\"affinity_cpus\": $(python3 -c 'import os; print(len(os.sched_getaffinity(0)))'), \"cpu_max\": \"$(cat /sys/fs/cgroup/cpu.max 2>/dev/null)\"}"
 timeout -k 10 300 $B/pdb_dbbench_cpu --benchmarks=fillrandom --num=2000000 --value_size=1024 --db=$DB \
   > "$OUT/fill.log" 2>&1 || { echo "FAIL fill"; exit 1; }
 echo "fill done"
