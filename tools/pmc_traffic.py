@@ -17,8 +17,10 @@ out_dir, workload = sys.argv[1], (sys.argv[2] if len(sys.argv) > 2 else "c2")
 KERNELS = {"c2": "crc_pack4k_kernel", "sstable": "crc_sst4k_kernel", "c3": "crc_stream16_kernel",
            "wal": "crc_lanespan_kernel", "wal100": "crc_lanespan_kernel", "wal400": "crc_lanespan_kernel",
            "wal1000": "crc_lanespan_kernel", "sst_verify": "crc_sst4k_kernel", "sst_seal": "crc_sst4k_kernel",
-           "sst_crc": "crc_sst4k_kernel"}
+           "sst_crc": "crc_sst4k_kernel", "sst_tables": "crc_sst4k_kernel"}
 target = KERNELS[workload]
+# the launches that follow the batch kernel on the same stream (the long-block lane), reported beside it
+LANE = ("crc_longpiece_kernel", "long_combine_kernel") if workload == "sst_tables" else ()
 
 
 def rows(pattern):
@@ -86,5 +88,11 @@ entry = {
 }
 if fetch and write:
     entry["hbm_bytes_per_launch"] = int(statistics.median(fetch) * 1024 * factor + statistics.median(write) * 1024)
+for k in LANE:
+    d, f, w = durations(k), counter("FETCH_SIZE", k), counter("WRITE_SIZE", k)
+    entry[k] = {"launches_traced": len(d), "avg_ms_timed_launches": round(statistics.mean(d[-steps:]), 4) if d and steps else None,
+                "hbm_bytes_per_launch": int(statistics.median(f) * 1024 * factor + statistics.median(w) * 1024) if f and w else None}
+if LANE and all(entry.get(k, {}).get("hbm_bytes_per_launch") is not None for k in LANE) and "hbm_bytes_per_launch" in entry:
+    entry["hbm_bytes_per_call"] = entry["hbm_bytes_per_launch"] + sum(entry[k]["hbm_bytes_per_launch"] for k in LANE)
 res[workload] = entry
 print(json.dumps(res, indent=1))
