@@ -15,7 +15,8 @@ for lib in "${ORDER[@]}"; do
   n=$((n+1))
   cp "ab/$lib.so" pebblesdb_amd/_lib/libpdb_crc32c.so
   for w in ${AB_WORKLOADS:-sst_seal sst_verify sst_crc c3}; do
-    timeout -k 10 240 python bench.py --workload "$w" --steps 50 --no-cpu-baseline --no-ceiling --settle 100 \
+    extra=""; [ "$w" = sst_tables ] && extra="--tables-dir /tmp/pdb_tables_ab"  # (made once, reused)
+    timeout -k 10 240 python bench.py --workload "$w" --steps 50 --no-cpu-baseline --no-ceiling --settle 100 $extra \
       > "$OUT/${lib}_${n}_$w.json" 2> "$OUT/${lib}_${n}_$w.err" || { echo "FAIL $lib $w"; exit 1; }
     python - "$OUT/${lib}_${n}_$w.json" "$lib" "$w" <<'PY'
 import json, sys
