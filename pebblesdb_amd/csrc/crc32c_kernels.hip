@@ -136,10 +136,11 @@ constexpr uint32_t kComb = 1u << kCombLog2;
 // multiple of 2^13 in chunks, each chunk's root shifted on by 2^13 pieces = 32 MiB), corrects an
 // Extend seed (R_s(B) = R_FFFFFFFF(B) ^ shift(s ^ 0xFFFFFFFF, n)), and hands the raw state to the
 // batch's sink.  The last workgroup to finish resets the lane's counters for the next call.
+constexpr uint32_t kCombThreads = 1024;  // (256: the operators' staging and the first folds 4x longer)
 template <class Sink>
-__global__ __launch_bounds__(256) void long_combine_kernel(LongLane ll, Sink sink) {
+__global__ __launch_bounds__(kCombThreads) void long_combine_kernel(LongLane ll, Sink sink) {
   __shared__ uint32_t sw[kComb];
-  __shared__ uint32_t ops[kCombLog2][1024];  // level k: shift 4096 << k (power-of-two operator 12 + k)
+  __shared__ __attribute__((aligned(16))) uint32_t ops[kCombLog2][1024];  // level k: shift 4096 << k (power-of-two operator 12 + k)
   const unsigned long long hw = ll.hdr[0];
   const uint32_t nrec = static_cast<uint32_t>(hw >> 40);
   // Only the min(records, grid) workgroups with a record take part (and count themselves out below):
@@ -154,7 +155,10 @@ __global__ __launch_bounds__(256) void long_combine_kernel(LongLane ll, Sink sin
       uint32_t ml = 0;
       while ((1u << ml) < R.np && ml < kCombLog2) ++ml;
       if (ml > staged) {  // (workgroup-uniform; the first barrier below orders it)
-        for (uint32_t i = staged * 1024u + t; i < ml * 1024u; i += blockDim.x) ops[i >> 10][i & 1023u] = ll.pow2[12u * 1024u + i];
+        // (16-B loads: levels are 4 KiB, 16-B aligned in the operator table)
+        const uint4* src = reinterpret_cast<const uint4*>(ll.pow2 + 12u * 1024u);
+        uint4* dst = reinterpret_cast<uint4*>(&ops[0][0]);
+        for (uint32_t i = staged * 256u + t; i < ml * 256u; i += blockDim.x) dst[i] = src[i];
         staged = ml;
       }
       const uint32_t M = 1u << ml, nc = (R.np + M - 1u) / M;
@@ -206,7 +210,7 @@ hipError_t launch_long(const LaunchGeom& g, const uint32_t* d_tables, const Long
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !ll || !ll->hdr) return e;
   hipLaunchKernelGGL(crc_longpiece_kernel, dim3(g.grid), dim3(kThreads), 0, s, d_tables, *ll);
-  hipLaunchKernelGGL((long_combine_kernel<Sink>), dim3(g.grid), dim3(256), 0, s, *ll, sink);  // (4 waves: a cheap empty launch)
+  hipLaunchKernelGGL((long_combine_kernel<Sink>), dim3(g.grid), dim3(kCombThreads), 0, s, *ll, sink);
   return hipGetLastError();
 }
 
