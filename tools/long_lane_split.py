@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """tools/long_lane_split.py <trace dir> -- split tools/long_block_cost.py --device-only's kernel trace
-(rocprofv3 --kernel-trace -f csv) into the long-block lane's parts.  Every device call is three
-dispatches on one stream: the batch kernel (crc_sst4k_kernel), the piece kernel and the combine
-kernel; the script walks them in dispatch order (5 long-block sizes x seal / verify / crc x 55 calls)
+(rocprofv3 --kernel-trace -f csv) into the long-block lane's parts.  Every device call is two or
+three dispatches on one stream: the batch kernel (crc_sst4k_kernel), the piece kernel and (before
+the combine was fused into the piece kernel) the combine kernel; the script walks them in dispatch order (5 long-block sizes x seal / verify / crc x 55 calls)
 and prints, per size and entry, the median duration of each kernel, the gaps between them and the
 call-to-call cadence, in microseconds."""
 import csv
@@ -28,8 +28,17 @@ def main():
                 if kind:
                     rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), kind))
     rows.sort()
-    calls = [rows[i:i + 3] for i in range(0, len(rows) - 2, 3)]
-    assert all([k for _, _, k in c] == ["batch", "piece", "combine"] for c in calls), "unexpected dispatch order"
+    # a call = its batch kernel and what follows it up to the next batch kernel: the piece kernel and
+    # (before the fused form) the combine kernel
+    calls = []
+    for r in rows:
+        if r[2] == "batch":
+            calls.append([r])
+        else:
+            calls[-1].append(r)
+    assert all([k for _, _, k in c] in (["batch", "piece", "combine"], ["batch", "piece"]) for c in calls), \
+        "unexpected dispatch order"
+    calls = [c if len(c) == 3 else c + [(c[1][1], c[1][1], "combine")] for c in calls]  # (fused: a 0-us combine)
     assert len(calls) == len(SIZES) * len(OPS) * CALLS, len(calls)
     out = []
     for si, kib in enumerate(SIZES):

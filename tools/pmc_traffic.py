@@ -88,11 +88,13 @@ entry = {
 }
 if fetch and write:
     entry["hbm_bytes_per_launch"] = int(statistics.median(fetch) * 1024 * factor + statistics.median(write) * 1024)
-for k in LANE:
+for k in LANE:  # (the combine kernel exists only in builds before the fused piece kernel)
     d, f, w = durations(k), counter("FETCH_SIZE", k), counter("WRITE_SIZE", k)
-    entry[k] = {"launches_traced": len(d), "avg_ms_timed_launches": round(statistics.mean(d[-steps:]), 4) if d and steps else None,
-                "hbm_bytes_per_launch": int(statistics.median(f) * 1024 * factor + statistics.median(w) * 1024) if f and w else None}
-if LANE and all(entry.get(k, {}).get("hbm_bytes_per_launch") is not None for k in LANE) and "hbm_bytes_per_launch" in entry:
-    entry["hbm_bytes_per_call"] = entry["hbm_bytes_per_launch"] + sum(entry[k]["hbm_bytes_per_launch"] for k in LANE)
+    if d:
+        entry[k] = {"launches_traced": len(d), "avg_ms_timed_launches": round(statistics.mean(d[-steps:]), 4) if steps else None,
+                    "hbm_bytes_per_launch": int(statistics.median(f) * 1024 * factor + statistics.median(w) * 1024) if f and w else None}
+lane = [entry[k] for k in LANE if k in entry]
+if lane and all(x["hbm_bytes_per_launch"] is not None for x in lane) and "hbm_bytes_per_launch" in entry:
+    entry["hbm_bytes_per_call"] = entry["hbm_bytes_per_launch"] + sum(x["hbm_bytes_per_launch"] for x in lane)
 res[workload] = entry
 print(json.dumps(res, indent=1))
