@@ -117,11 +117,13 @@ __global__ __launch_bounds__(1024) void span_combine_many_kernel(const uint32_t*
 // piece: exactly its 4-KiB body path, started from state 0; a head: Value()'s seed -- the fast path
 // at 4096 B, the slow path below), one raw state per piece.  The count is read on the device: the
 // launch is made whether or not anything was exported, and returns at once when nothing was.
-__global__ __launch_bounds__(kThreads) void crc_longpiece_kernel(const uint32_t* __restrict__ tabs, LongLane ll) {
+constexpr uint32_t kPieceWaves = 12;  // (16 waves: 128 VGPRs, 24 of them spilled; 12 as the sstable kernels: 5)
+__global__ __launch_bounds__(kPieceWaves * 64) void crc_longpiece_kernel(const uint32_t* __restrict__ tabs, LongLane ll) {
   const uint64_t np = ll.hdr[0] & kLongPieceMask;
   // (a workgroup whose share of the pieces is empty leaves before staging its 160 KiB of tables)
   if (np * blockIdx.x / gridDim.x == np * (blockIdx.x + 1u) / gridDim.x) return;
-  sized_kernel_body<PieceSrc, LeafSink, true, 4>(tabs, PieceSrc{ll.piece}, np, LeafSink{ll.leaf});
+  sized_kernel_body<PieceSrc, LeafSink, true, 4, false, 4, QuadTabs, false, true, kPieceWaves>(tabs, PieceSrc{ll.piece}, np,
+                                                                                              LeafSink{ll.leaf});
 }
 
 // op_k(c) through a power-of-two operator (4 x 256 entries) in LDS or global memory
@@ -209,7 +211,7 @@ template <class Sink>
 hipError_t launch_long(const LaunchGeom& g, const uint32_t* d_tables, const LongLane* ll, const Sink& sink, hipStream_t s) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !ll || !ll->hdr) return e;
-  hipLaunchKernelGGL(crc_longpiece_kernel, dim3(g.grid), dim3(kThreads), 0, s, d_tables, *ll);
+  hipLaunchKernelGGL(crc_longpiece_kernel, dim3(g.grid), dim3(kPieceWaves * 64), 0, s, d_tables, *ll);
   hipLaunchKernelGGL((long_combine_kernel<Sink>), dim3(g.grid), dim3(kCombThreads), 0, s, *ll, sink);
   return hipGetLastError();
 }
