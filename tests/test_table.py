@@ -218,3 +218,68 @@ def test_pinned_staging_long_blocks(dev, oracle_lib):
         assert sorted(np.flatnonzero(ok == 0).tolist()) == sorted([bad[0], bad[3]])
     finally:
         check(lib().pdb_host_free(p))
+
+
+@gpu
+def test_pinned_staging_block_over_64mib(dev, oracle_lib):
+    """a host batch with one block of more than 2^14 pieces of 4 KiB (64 MiB) beside
+    smaller long blocks.  Zero-copy, such a block leaves the shared descriptor launch for a span
+    launch of its own whose result is remapped into the handles' order (crc32c_capi.cpp
+    host_sst_mapped); from pageable memory it goes through the device long-block lane.  Every
+    trailer vs the oracle, ok bytes in the handles' order, corruptions of the huge block and of a
+    neighbour counted once each, on both routes."""
+    import ctypes
+
+    import oracle
+    from pebblesdb_amd import crc32c
+    from pebblesdb_amd._native import check, lib
+
+    rng = np.random.Generator(np.random.PCG64(53))
+    huge = (64 << 20) + 4096 * 3 + 11  # (huge + 1) / 4096 > 2^14 pieces
+    sizes = rng.integers(4166, 4175, size=40).tolist()
+    sizes[5] = 20000
+    sizes[17] = huge
+    sizes[18] = 1363149  # a long block right after it: the order remap
+    sizes[30] = 65536
+    sizes += [0, 9]
+    sizes = np.array(sizes, dtype=np.int64)
+    offs = np.concatenate([[3], 3 + np.cumsum(sizes + 5)[:-1]]).astype(np.int64)
+    total = int(offs[-1] + sizes[-1] + 5) + 1
+    img = oracle.splitmix_bytes(total, 97).copy()
+    img[offs + sizes] = rng.integers(0, 2, size=len(sizes))
+    h = np.zeros(len(sizes), dtype=crc32c.HANDLE_DTYPE)
+    h["offset"], h["size"] = offs, sizes
+    want = [oracle_lib.mask(oracle_lib.value(img[o : o + z + 1].tobytes())) for o, z in zip(offs.tolist(), sizes.tolist())]
+    bad = [17, 18, 2]
+
+    def check_image(buf):
+        for i, (o, z) in enumerate(zip(offs.tolist(), sizes.tolist())):
+            assert int.from_bytes(buf[o + z + 1 : o + z + 5].tobytes(), "little") == want[i], (i, z)
+
+    def corrupt(buf):
+        buf[offs[17] + (40 << 20) + 5] ^= 0x20
+        buf[offs[18] + sizes[18] + 3] ^= 0x01  # a trailer byte
+        buf[offs[2] + 7] ^= 0x80
+
+    p = ctypes.c_void_p()
+    check(lib().pdb_host_alloc(total, ctypes.byref(p)))
+    try:
+        pin = np.ctypeslib.as_array((ctypes.c_uint8 * total).from_address(p.value))
+        pin[:] = img
+        check(lib().pdb_sst_seal_host(p.value, total, h.ctypes.data, len(h)))
+        check_image(pin)
+        ok = np.zeros(len(h), dtype=np.uint8)
+        assert lib().pdb_sst_verify_host(p.value, total, h.ctypes.data, len(h), ok.ctypes.data) == 0 and ok.all()
+        corrupt(pin)
+        assert lib().pdb_sst_verify_host(p.value, total, h.ctypes.data, len(h), ok.ctypes.data) == 3
+        assert sorted(np.flatnonzero(ok == 0).tolist()) == sorted(bad)
+        page = img.copy()  # pageable: the DMA route and the device long-block lane
+        check(lib().pdb_sst_seal_host(page.ctypes.data, total, h.ctypes.data, len(h)))
+        check_image(page)
+        ok[:] = 0
+        assert lib().pdb_sst_verify_host(page.ctypes.data, total, h.ctypes.data, len(h), ok.ctypes.data) == 0 and ok.all()
+        corrupt(page)
+        assert lib().pdb_sst_verify_host(page.ctypes.data, total, h.ctypes.data, len(h), ok.ctypes.data) == 3
+        assert sorted(np.flatnonzero(ok == 0).tolist()) == sorted(bad)
+    finally:
+        check(lib().pdb_host_free(p))
