@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """tools/long_lane_split.py <trace dir> -- split tools/long_block_cost.py --device-only's kernel trace
 (rocprofv3 --kernel-trace -f csv) into the long-block lane's parts.  Every device call is two or
-three dispatches on one stream: the batch kernel (crc_sst4k_kernel), the piece kernel and (before
-the combine was fused into the piece kernel) the combine kernel; the script walks them in dispatch order (5 long-block sizes x seal / verify / crc x 55 calls)
+three dispatches on one stream: the batch kernel (crc_sst4k_kernel), the piece kernel
+(crc_longpiece_kernel; crc_longlane_kernel, which also folds the records, since round 6's fused
+lane) and, before the fused lane, the combine kernel; the script walks them in dispatch order (5 long-block sizes x seal / verify / crc x 55 calls)
 and prints, per size and entry, the median duration of each kernel, the gaps between them and the
 call-to-call cadence, in microseconds."""
 import csv
@@ -23,7 +24,7 @@ def main():
         with open(f) as fh:
             for r in csv.DictReader(fh):
                 name = r["Kernel_Name"]
-                kind = ("batch" if "crc_sst4k_kernel" in name else "piece" if "crc_longpiece_kernel" in name
+                kind = ("batch" if "crc_sst4k_kernel" in name else "piece" if ("crc_longpiece_kernel" in name or "crc_longlane_kernel" in name)
                         else "combine" if "long_combine_kernel" in name else None)
                 if kind:
                     rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), kind))

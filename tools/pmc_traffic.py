@@ -20,7 +20,7 @@ KERNELS = {"c2": "crc_pack4k_kernel", "sstable": "crc_sst4k_kernel", "c3": "crc_
            "sst_crc": "crc_sst4k_kernel", "sst_tables": "crc_sst4k_kernel"}
 target = KERNELS[workload]
 # the launches that follow the batch kernel on the same stream (the long-block lane), reported beside it
-LANE = ("crc_longpiece_kernel", "long_combine_kernel") if workload == "sst_tables" else ()
+LANE = ("crc_longpiece_kernel", "long_combine_kernel", "crc_longlane_kernel") if workload == "sst_tables" else ()
 
 
 def rows(pattern):
