@@ -29,7 +29,6 @@ LongLane long_lane_at(uint8_t* d, const uint32_t* d_pow2) {
   ll.rec = reinterpret_cast<LongRec*>(d + kLongRecOff);
   ll.piece = reinterpret_cast<LongPiece*>(d + kLongPieceOff);
   ll.leaf = reinterpret_cast<uint32_t*>(d + kLongLeafOff);
-  ll.done = reinterpret_cast<uint32_t*>(d + kLongDoneOff);
   ll.pow2 = d_pow2;
   ll.rec_cap = kLongRecCap;
   ll.piece_cap = kLongPieceCap;
@@ -278,8 +277,7 @@ int alloc_lane(hipStream_t s, uint8_t** out) {
   void* d = nullptr;
   hipError_t e = hipMalloc(&d, long_scratch_bytes());
   if (e != hipSuccess) return fail(PDB_ENOMEM, std::string("hipMalloc(long-block lane): ") + hipGetErrorString(e));
-  if ((e = hipMemsetAsync(d, 0, kLongHdrBytes, s)) != hipSuccess ||
-      (e = hipMemsetAsync(static_cast<uint8_t*>(d) + kLongDoneOff, 0, size_t(kLongRecCap) * 4, s)) != hipSuccess) {
+  if ((e = hipMemsetAsync(d, 0, kLongHdrBytes, s)) != hipSuccess) {
     (void)hipFree(d);
     return hip_fail(e, "hipMemsetAsync(long-block lane)");
   }

@@ -645,8 +645,8 @@ __device__ __forceinline__ bool long_export(uint8_t* lane, uint32_t min_bytes, u
   LongPiece* piece = reinterpret_cast<LongPiece*>(lane + kLongPieceOff);
   if (u == 0) rec[slot] = LongRec{i, static_cast<uint64_t>(p), n, init_raw, q0, np};
   for (uint32_t k = u; k < np; k += 64u)
-    piece[q0 + k] = k ? LongPiece{static_cast<uint64_t>(p) + h + 4096ull * (k - 1u), 4096u, slot << 1}
-                      : LongPiece{static_cast<uint64_t>(p), h, (slot << 1) | 1u};
+    piece[q0 + k] = k ? LongPiece{static_cast<uint64_t>(p) + h + 4096ull * (k - 1u), 4096u, 0u}
+                      : LongPiece{static_cast<uint64_t>(p), h, 1u};
   return true;
 }
 
@@ -788,7 +788,7 @@ struct PieceSrc {
     return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(piece + i));
   }
   __device__ __forceinline__ BlkDesc lane(const Raw& r) const {
-    return {reinterpret_cast<const uint8_t*>((static_cast<uint64_t>(r.y) << 32) | r.x), r.z, (r.w & 1u) ? 0xFFFFFFFFu : 0u};
+    return {reinterpret_cast<const uint8_t*>((static_cast<uint64_t>(r.y) << 32) | r.x), r.z, r.w ? 0xFFFFFFFFu : 0u};
   }
   __device__ __forceinline__ bool long_export(uint64_t, const BlkDesc&, uint32_t, uint32_t) const { return false; }
   __device__ __forceinline__ bool long_export_cold(uint64_t, const BlkDesc&, uint32_t, uint32_t) const { return false; }
@@ -804,15 +804,10 @@ struct SrcSeeds<PieceSrc> {
   static constexpr bool kOn = true;
 };
 
-// The pieces' raw states (leaves of the long-block fold), stored with agent scope: write-through
-// (`sc1`) stores, so that once the storing wave has drained them (vmcnt 0) the workgroup folding the
-// record on another XCD reads them with agent-scope loads -- no release fence, whose L2 write-back
-// per wave cost the fused lane of round 6's first try 12-14 points on sst_tables.
+// The pieces' raw states (leaves of the long-block combine)
 struct LeafSink {
   uint32_t* leaf;
-  __device__ __forceinline__ void put(uint64_t i, uint32_t raw, const BlkDesc&) const {
-    __hip_atomic_store(leaf + i, raw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  __device__ __forceinline__ void put(uint64_t i, uint32_t raw, const BlkDesc&) const { leaf[i] = raw; }
 };
 
 struct OutSink {
@@ -1790,7 +1785,7 @@ constexpr uint32_t kSlowList = 64u;
 template <class Src, class Sink, bool kNT, int kRows, bool kDiagNoFold = false, int kBlk = 4, class LT = QuadTabs,
           bool kUA = false, bool kDeferF = true, uint32_t kW = kWavesPerWg>
 __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ tabs, Src src, uint64_t nblk,
-                                                  Sink sink, char** lds_out = nullptr) {
+                                                  Sink sink) {
   static_assert(kRows == 0 || kRows == 1 || kRows == 4, "no body (records <= 256 B), 1-KiB or 4-KiB bodies");
   static_assert(kBlk == 4 || (kBlk == 8 && kRows >= 1), "4-block groups, or 8 with 1- or 4-KiB bodies");
   constexpr uint32_t kRowLanes = 64u / kBlk, kRowShift = kBlk == 4 ? 4u : 3u;
@@ -1798,7 +1793,6 @@ __device__ __forceinline__ void sized_kernel_body(const uint32_t* __restrict__ t
   constexpr uint32_t kBody = 1024u * kRows, kMin = kRows ? kBody : 1u, kMax = kBody + 16u * kRowLanes;
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[PDB_LDS_BYTES / 4];
   char* lds = reinterpret_cast<char*>(lds_words);
-  if (lds_out) *lds_out = lds;  // (the long-block lane folds records in it afterwards)
   // lane-quarter image: T0..T3 and shift 1024 conflict-free, slots 0..5 = 16..512
   if constexpr (__is_same(LT, QuadTabs))
     stage_tables_q4<PDB_CAT_TREE16, PDB_CAT_TREE16, PDB_CAT_TREE16 + 1>(lds, tabs);  // image 1: tree levels 0, 1

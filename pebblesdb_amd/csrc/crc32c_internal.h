@@ -34,15 +34,13 @@ struct LaunchGeom {
 // EXPORTS it: one atomic reserves a record and the block's pieces in a per-stream scratch, and the
 // wave writes the piece list -- a head of h = n - 4096 m bytes (1..4096, Value() seed) followed by m
 // pieces of exactly 4096 B (hashed from state 0) -- and goes on.  After the batch kernel, on the same
-// stream, ONE launch of crc_longlane_kernel hashes every exported piece on the whole GPU (the
-// sstable-sized kernel's 4-KiB body path: ~HBM rate) into a leaf written through to memory (agent-
-// scope stores), counts each workgroup's pieces into their records once it has drained its stores,
-// and the workgroup whose count completes a record folds that record's leaves with the power-of-two
-// operators (R(H || S_1 .. S_m) = sum_j shift(leaf_j, 4096 (m - j)), zero leaves padded in front) and
-// hands the raw state to the batch's own sink, exactly where the batch kernel would have.  A full
-// scratch (or no scratch) leaves the block to the batch kernel's one-wave path: the results never
-// depend on the lane, only the time does.  The last workgroup to have read the header resets it, and
-// a record's folder its count, so the lane is allocation-free and capturable per call.
+// stream, crc_longpiece_kernel hashes every exported piece on the whole GPU (the sstable-sized
+// kernel's 4-KiB body path: ~HBM rate), and long_combine_kernel folds each record's leaves with the
+// power-of-two operators (R(H || S_1 .. S_m) = sum_j shift(leaf_j, 4096 (m - j)), zero leaves padded
+// in front) and hands the raw state to the batch's own sink, exactly where the batch kernel would
+// have.  A full scratch (or no scratch) leaves the block to the batch kernel's one-wave path: the
+// results never depend on the lane, only the time does.  The combine kernel's last workgroup resets
+// the counters, so the lane is allocation-free and capturable per call.
 struct LongRec {     // 32 B
   uint64_t i;        // block index in the batch
   uint64_t p;        // block address
@@ -53,14 +51,13 @@ struct LongRec {     // 32 B
 struct LongPiece {   // 16 B
   uint64_t p;
   uint32_t n;        // 4096, or the head's 1..4096
-  uint32_t seeded;   // bit 0: the head (Value() seed) or a full piece (state 0); bits 1..: its record
+  uint32_t seeded;   // 1: the head (Value() seed), 0: a full piece (state 0)
 };
 struct LongLane {
-  unsigned long long* hdr;  // [0] = records << 40 | pieces reserved; [1] = workgroups that have read [0]
+  unsigned long long* hdr;  // [0] = records << 40 | pieces reserved; [1] = combine workgroups done
   LongRec* rec;
   LongPiece* piece;
   uint32_t* leaf;           // raw state of piece q
-  uint32_t* done;           // pieces of record r hashed and drained (0 between calls)
   const uint32_t* pow2;     // the 64 power-of-two shift operators (1024 u32 each)
   uint32_t rec_cap, piece_cap;
 };
@@ -69,13 +66,12 @@ constexpr uint32_t kLongPieceCap = 1u << 21;  // 8 GiB of long blocks per call
 constexpr unsigned long long kLongPieceMask = (1ull << 40) - 1;
 constexpr uint32_t kLongMinBytes = 16u << 10;         // sstable-sized and record kernels
 constexpr uint32_t kLongMinStream = (64u << 10) + 1;  // the any-length stream kernel (C3's 1..64 KiB stay)
-// scratch layout: [hdr 256 B][records][pieces][leaves][done] (a batch kernel carries only the base)
+// scratch layout: [hdr 256 B][records][pieces][leaves] (a batch kernel carries only the base)
 constexpr size_t kLongHdrBytes = 256;
 constexpr size_t kLongRecOff = kLongHdrBytes;
 constexpr size_t kLongPieceOff = kLongRecOff + size_t(kLongRecCap) * sizeof(LongRec);
 constexpr size_t kLongLeafOff = kLongPieceOff + size_t(kLongPieceCap) * sizeof(LongPiece);
-constexpr size_t kLongDoneOff = kLongLeafOff + size_t(kLongPieceCap) * 4;
-constexpr size_t long_scratch_bytes() { return kLongDoneOff + size_t(kLongRecCap) * 4; }
+constexpr size_t long_scratch_bytes() { return kLongLeafOff + size_t(kLongPieceCap) * 4; }
 // The lane over a zeroed scratch of long_scratch_bytes() at d (null d: no lane).
 LongLane long_lane_at(uint8_t* d, const uint32_t* d_pow2);
 

@@ -112,8 +112,19 @@ __global__ __launch_bounds__(1024) void span_combine_many_kernel(const uint32_t*
   if (threadIdx.x == 0) out[blockIdx.x] = ~sw[0];
 }
 
-// ---- the long-block lane (crc32c_internal.h): one launch, pieces then the records they complete ----
+// ---- the long-block lane (crc32c_internal.h): pieces, then one combine per record ----------------
+// Every piece the batch kernel exported, hashed by the sstable-sized kernel over a piece list (a full
+// piece: exactly its 4-KiB body path, started from state 0; a head: Value()'s seed -- the fast path
+// at 4096 B, the slow path below), one raw state per piece.  The count is read on the device: the
+// launch is made whether or not anything was exported, and returns at once when nothing was.
 constexpr uint32_t kPieceWaves = 12;  // (16 waves: 128 VGPRs, 24 of them spilled; 12 as the sstable kernels: 5)
+__global__ __launch_bounds__(kPieceWaves * 64) void crc_longpiece_kernel(const uint32_t* __restrict__ tabs, LongLane ll) {
+  const uint64_t np = ll.hdr[0] & kLongPieceMask;
+  // (a workgroup whose share of the pieces is empty leaves before staging its 160 KiB of tables)
+  if (np * blockIdx.x / gridDim.x == np * (blockIdx.x + 1u) / gridDim.x) return;
+  sized_kernel_body<PieceSrc, LeafSink, true, 4, false, 4, QuadTabs, false, true, kPieceWaves>(tabs, PieceSrc{ll.piece}, np,
+                                                                                              LeafSink{ll.leaf});
+}
 
 // op_k(c) through a power-of-two operator (4 x 256 entries) in LDS or global memory
 __device__ __forceinline__ uint32_t apply_op(const uint32_t* op, uint32_t c) {
@@ -123,136 +134,85 @@ __device__ __forceinline__ uint32_t apply_op(const uint32_t* op, uint32_t c) {
 constexpr uint32_t kCombLog2 = 13;  // leaves folded in LDS at once (2^13 = 32 MiB of block)
 constexpr uint32_t kComb = 1u << kCombLog2;
 
-// Fold record R's leaves in LDS (sw: kComb u32; ops: level k = shift 4096 << k, power-of-two operator
-// 12 + k, the first `staged` levels already in place): front-padded with zero leaves to a power of
-// two, or to a multiple of 2^13 in chunks, each chunk's root shifted on by 2^13 pieces = 32 MiB; an
-// Extend seed corrected (R_s(B) = R_FFFFFFFF(B) ^ shift(s ^ 0xFFFFFFFF, n)).  Every thread of the
-// workgroup calls it; thread 0 gets the raw state.  The leaves come from other workgroups, possibly
-// on other XCDs: agent-scope loads, after the counts that completed the record.
-__device__ uint32_t fold_record(const LongLane& ll, const LongRec& R, uint32_t* sw, uint32_t* ops, uint32_t& staged) {
-  const uint32_t t = threadIdx.x;
-  uint32_t ml = 0;
-  while ((1u << ml) < R.np && ml < kCombLog2) ++ml;
-  const uint32_t M = 1u << ml, nc = (R.np + M - 1u) / M;
-  const uint32_t pad = nc * M - R.np;
-  // the levels this record needs beyond those staged (16-B loads: a level is 4 KiB, 16-B aligned in
-  // the operator table), loaded together with the first chunk's leaves: one round trip for both
-  const uint32_t s0 = staged * 256u, s1 = ml > staged ? ml * 256u : s0;
-  staged = ml > staged ? ml : staged;  // (workgroup-uniform; the barrier after the loads orders it)
-  const uint4* osrc = reinterpret_cast<const uint4*>(ll.pow2 + 12u * 1024u);
-  uint4* odst = reinterpret_cast<uint4*>(ops);
-  uint32_t acc = 0;  // (thread 0)
-  for (uint32_t c = 0; c < nc; ++c) {
-    __syncthreads();  // the previous fold's root has been read
-    const uint32_t jn = c == 0 && s1 - s0 > M ? s1 - s0 : M;
-    for (uint32_t j = t; j < jn; j += blockDim.x) {
-      const uint32_t v = c * M + j;
-      const bool lf = j < M, op = c == 0 && s0 + j < s1;
-      uint4 o{};
-      uint32_t w = 0;
-      if (op) o = osrc[s0 + j];
-      if (lf && v >= pad) w = __hip_atomic_load(ll.leaf + R.q0 + (v - pad), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (op) odst[s0 + j] = o;
-      if (lf) sw[j] = w;
-    }
-    __syncthreads();
-    for (uint32_t k = 0; k < ml; ++k) {
-      const uint32_t half = 1u << k, pairs = M >> (k + 1);
-      for (uint32_t j = t; j < pairs; j += blockDim.x) {
-        const uint32_t i = j << (k + 1);
-        sw[i] = apply_op(ops + k * 1024u, sw[i]) ^ sw[i + half];
-      }
-      __syncthreads();
-    }
-    if (t == 0) acc = c ? apply_op(ll.pow2 + (12u + kCombLog2) * 1024u, acc) ^ sw[0] : sw[0];
-  }
-  if (t == 0 && R.init_raw != 0xFFFFFFFFu) {  // an Extend seed (descriptor batches with PDB_CRC_USE_INIT)
-    uint32_t x = R.init_raw ^ 0xFFFFFFFFu;
-    for (uint32_t k = 0; k < 32u; ++k)
-      if ((R.n >> k) & 1u) x = apply_op(ll.pow2 + k * 1024u, x);
-    acc ^= x;
-  }
-  return acc;
-}
-
-// Every piece the batch kernel exported, hashed by the sstable-sized kernel over a piece list (a full
-// piece: exactly its 4-KiB body path, started from state 0; a head: Value()'s seed -- the fast path at
-// 4096 B, the slow path below), one raw state per piece, stored write-through.  Then each workgroup
-// drains its stores, adds its pieces to their records' counts, and folds every record whose count it
-// completes, into the batch's sink.  The counts are read on the device: the launch is made whether or
-// not anything was exported and returns at once when nothing was.  (Round 6's first lane ran the fold
-// as a second launch, ~1.5-1.9 us of kernel boundary plus a 5-us combine per call; a fused form that
-// published the leaves with release fences lost 12-14 points on sst_tables to their L2 write-backs.)
+// Workgroup r folds record r's leaves (front-padded with zero leaves to a power of two, or to a
+// multiple of 2^13 in chunks, each chunk's root shifted on by 2^13 pieces = 32 MiB), corrects an
+// Extend seed (R_s(B) = R_FFFFFFFF(B) ^ shift(s ^ 0xFFFFFFFF, n)), and hands the raw state to the
+// batch's sink.  The last workgroup to finish resets the lane's counters for the next call.
+constexpr uint32_t kCombThreads = 1024;  // (256: the operators' staging and the first folds 4x longer)
 template <class Sink>
-__global__ __launch_bounds__(kPieceWaves * 64) void crc_longlane_kernel(const uint32_t* __restrict__ tabs, LongLane ll,
-                                                                         Sink sink) {
+__global__ __launch_bounds__(kCombThreads) void long_combine_kernel(LongLane ll, Sink sink) {
+  __shared__ uint32_t sw[kComb];
+  __shared__ __attribute__((aligned(16))) uint32_t ops[kCombLog2][1024];  // level k: shift 4096 << k (power-of-two operator 12 + k)
   const unsigned long long hw = ll.hdr[0];
-  const uint64_t np = hw & kLongPieceMask;
-  if (np == 0) return;  // nothing exported (nothing to reset either)
-  // every wave of this workgroup has read the header before the workgroup counts itself in; the last
-  // workgroup to do so resets the header for the next call (no one reads it after that)
-  __syncthreads();
-  if (threadIdx.x == 0 &&
-      __hip_atomic_fetch_add(ll.hdr + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1ull == gridDim.x) {
-    __hip_atomic_store(ll.hdr, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(ll.hdr + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  // (a workgroup whose share of the pieces is empty leaves before staging its 160 KiB of tables)
-  const uint64_t qlo = np * blockIdx.x / gridDim.x, qhi = np * (blockIdx.x + 1u) / gridDim.x;
-  if (qlo == qhi) return;
-  // this workgroup's pieces [qlo, qhi) belong to records r0 .. r1 (a record's pieces are contiguous);
-  // read now, so that the tail's first loads need no round trip of their own
-  const uint32_t r0 = __builtin_amdgcn_readfirstlane(ll.piece[qlo].seeded) >> 1;
-  const uint32_t r1 = __builtin_amdgcn_readfirstlane(ll.piece[qhi - 1u].seeded) >> 1;
-  char* lds = nullptr;
-  sized_kernel_body<PieceSrc, LeafSink, true, 4, false, 4, QuadTabs, false, true, kPieceWaves>(tabs, PieceSrc{ll.piece}, np,
-                                                                                              LeafSink{ll.leaf}, &lds);
-  // thread t's record of the first round (most workgroups have one or two), loaded before the drain
-  // so that the drain waits for it too
-  LongRec Rt{};
-  if (r0 + threadIdx.x <= r1) Rt = ll.rec[r0 + threadIdx.x];
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's leaves have landed in memory
-  __syncthreads();
-  // the body's LDS image is dead now: the fold's leaves, its operators and a list of the records this
-  // workgroup completes
-  uint32_t* sw = reinterpret_cast<uint32_t*>(lds);
-  uint32_t* ops = sw + kComb;
-  uint32_t* list = ops + kCombLog2 * 1024u;  // [0] = count, then record indices
-  static_assert((kComb + kCombLog2 * 1024u + 1u + kPieceWaves * 64u) * 4u <= PDB_LDS_BYTES, "fits the body's LDS");
-  uint32_t staged = 0;
-  for (uint32_t rb = r0; rb <= r1; rb += blockDim.x) {
-    if (threadIdx.x == 0) list[0] = 0;
-    __syncthreads();
-    const uint32_t r = rb + threadIdx.x;
-    if (r <= r1) {
-      const LongRec R = rb == r0 ? Rt : ll.rec[r];
-      const uint64_t a = R.q0 > qlo ? R.q0 : qlo, e = R.q0 + R.np < qhi ? R.q0 + R.np : qhi;
-      const uint32_t cnt = static_cast<uint32_t>(e - a);
-      if (__hip_atomic_fetch_add(ll.done + r, cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + cnt == R.np)
-        list[1u + atomicAdd(list, 1u)] = r;  // (LDS)
-    }
-    __syncthreads();
-    const uint32_t nl = list[0];
-    for (uint32_t k = 0; k < nl; ++k) {
-      const uint32_t rr = list[1u + k];
-      const LongRec R = ll.rec[rr];
-      const uint32_t raw = fold_record(ll, R, sw, ops, staged);
-      if (threadIdx.x == 0) {
+  const uint32_t nrec = static_cast<uint32_t>(hw >> 40);
+  // Only the min(records, grid) workgroups with a record take part (and count themselves out below):
+  // the others leave at once.  One that starts after the reset reads 0 records and leaves too -- every
+  // workgroup with a record has counted itself before the reset.
+  if (blockIdx.x >= nrec) return;
+  const uint32_t t = threadIdx.x;
+  {
+    uint32_t staged = 0;  // level operators staged so far (grown as records need them: a 64-KiB block needs 5)
+    for (uint32_t r = blockIdx.x; r < nrec; r += gridDim.x) {
+      const LongRec R = ll.rec[r];
+      uint32_t ml = 0;
+      while ((1u << ml) < R.np && ml < kCombLog2) ++ml;
+      if (ml > staged) {  // (workgroup-uniform; the first barrier below orders it)
+        // (16-B loads: levels are 4 KiB, 16-B aligned in the operator table)
+        const uint4* src = reinterpret_cast<const uint4*>(ll.pow2 + 12u * 1024u);
+        uint4* dst = reinterpret_cast<uint4*>(&ops[0][0]);
+        for (uint32_t i = staged * 256u + t; i < ml * 256u; i += blockDim.x) dst[i] = src[i];
+        staged = ml;
+      }
+      const uint32_t M = 1u << ml, nc = (R.np + M - 1u) / M;
+      const uint32_t pad = nc * M - R.np;
+      uint32_t acc = 0;  // (thread 0)
+      for (uint32_t c = 0; c < nc; ++c) {
+        __syncthreads();  // the previous fold's root has been read
+        for (uint32_t j = t; j < M; j += blockDim.x) {
+          const uint32_t v = c * M + j;
+          sw[j] = v < pad ? 0u : ll.leaf[R.q0 + (v - pad)];
+        }
+        __syncthreads();
+        for (uint32_t k = 0; k < ml; ++k) {
+          const uint32_t half = 1u << k, pairs = M >> (k + 1);
+          for (uint32_t j = t; j < pairs; j += blockDim.x) {
+            const uint32_t i = j << (k + 1);
+            sw[i] = apply_op(ops[k], sw[i]) ^ sw[i + half];
+          }
+          __syncthreads();
+        }
+        if (t == 0) acc = c ? apply_op(ll.pow2 + (12u + kCombLog2) * 1024u, acc) ^ sw[0] : sw[0];
+      }
+      if (t == 0) {
+        uint32_t raw = acc;
+        if (R.init_raw != 0xFFFFFFFFu) {  // an Extend seed (descriptor batches with PDB_CRC_USE_INIT)
+          uint32_t x = R.init_raw ^ 0xFFFFFFFFu;
+          for (uint32_t k = 0; k < 32u; ++k)
+            if ((R.n >> k) & 1u) x = apply_op(ll.pow2 + k * 1024u, x);
+          raw ^= x;
+        }
         const BlkDesc d{reinterpret_cast<const uint8_t*>(R.p), R.n, R.init_raw};
         SinkOps<Sink>::put(sink, R.i, raw, d, SinkOps<Sink>::pre(sink, R.i, d));
-        ll.done[rr] = 0u;  // (only this workgroup touches it until the next call)
       }
     }
-    __syncthreads();  // the list is read before the next round rewrites it
+  }
+  __syncthreads();
+  if (t == 0) {
+    __threadfence();
+    if (atomicAdd(ll.hdr + 1, 1ull) + 1ull == (nrec < gridDim.x ? nrec : gridDim.x)) {
+      ll.hdr[0] = 0ull;
+      ll.hdr[1] = 0ull;
+    }
   }
 }
 
-// The lane's launch after a batch kernel with sink `sink` (same stream)
+// The lane's two launches after a batch kernel with sink `sink` (same stream)
 template <class Sink>
 hipError_t launch_long(const LaunchGeom& g, const uint32_t* d_tables, const LongLane* ll, const Sink& sink, hipStream_t s) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !ll || !ll->hdr) return e;
-  hipLaunchKernelGGL((crc_longlane_kernel<Sink>), dim3(g.grid), dim3(kPieceWaves * 64), 0, s, d_tables, *ll, sink);
+  hipLaunchKernelGGL(crc_longpiece_kernel, dim3(g.grid), dim3(kPieceWaves * 64), 0, s, d_tables, *ll);
+  hipLaunchKernelGGL((long_combine_kernel<Sink>), dim3(g.grid), dim3(kCombThreads), 0, s, *ll, sink);
   return hipGetLastError();
 }
 
