@@ -91,11 +91,16 @@ __global__ __launch_bounds__(kThreads) void read_pattern4k_kernel(const uint8_t*
 // offset + size + 5) read as 1-KiB-contiguous 16-B nt loads by the wave owning its 4-block group,
 // groups in workgroup lock-step over the workgroup's contiguous range (the sst kernel's
 // scheduling), handles a group ahead -- with kWrite 0: no stores (the pattern's read ceiling);
-// 1: each group's 4 trailers stored (4 byte stores, like SealSink) once its loads returned.
+// 1: each group's 4 trailers stored (4 byte stores, like SealSink) once its loads returned;
+// 2 / 3 (variants 142 / 143): instead of the 4 trailer bytes, the whole aligned 64-B / 128-B line
+// holding them, as 16-B stores (what a seal that rewrote the trailer's line with the bytes it read
+// would write: full-line writes, no partial-line merge at the memory side; lines past the image's
+// end are skipped).
 template <int kWrite>
 __global__ __launch_bounds__(kThreads) void seal_pattern_kernel(uint8_t* __restrict__ buf,
                                                                 const pdb_block_handle* __restrict__ h,
-                                                                uint64_t n, uint32_t* __restrict__ out) {
+                                                                uint64_t n, uint32_t* __restrict__ out,
+                                                                uint64_t len = 0) {
   typedef __attribute__((address_space(1))) uint8_t g_u8;
   const uint32_t u = threadIdx.x & 63u;
   const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -139,6 +144,14 @@ __global__ __launch_bounds__(kThreads) void seal_pattern_kernel(uint8_t* __restr
         for (int k = 0; k < 4; ++k) tr[k] = static_cast<uint8_t>(m >> (8 * k));
       }
     }
+    if constexpr (kWrite >= 2) {
+      constexpr uint32_t kLine = kWrite == 2 ? 64u : 128u, kPer = kLine / 16u;
+      const uint32_t r = u / kPer, k = u % kPer;
+      const uint32_t tl = __shfl(static_cast<uint32_t>(ta), r & 3u, 64), th = __shfl(static_cast<uint32_t>(ta >> 32), r & 3u, 64);
+      const uintptr_t base = ((static_cast<uintptr_t>(th) << 32) | tl) & ~static_cast<uintptr_t>(kLine - 1u);
+      if (r < 4u && b0 + r < hi && base + kLine <= reinterpret_cast<uintptr_t>(buf) + len)
+        *reinterpret_cast<u32x4*>(base + 16u * k) = x;
+    }
   }
   for (int k = 32; k; k >>= 1) acc ^= __shfl_xor(acc, k, 64);
   if (u == 0 && out) atomicXor(out, acc);
@@ -158,9 +171,13 @@ hipError_t launch_sst_variant(int v, const LaunchGeom& g, const uint32_t* d_tabl
   switch (v) {
     case 140:  // the seal's loads alone / loads + its in-place trailer stores (pattern ceilings;
     case 141:  // wrong trailers by design; nbad = XOR of what was read)
+    case 142:  // loads + the 64-B / 128-B line holding each trailer stored whole (wrong bytes there too)
+    case 143:
       if (!seal) return hipErrorInvalidValue;
-      if (v == 140) hipLaunchKernelGGL(seal_pattern_kernel<0>, grid, block, 0, s, buf, h, n, nbad);
-      else hipLaunchKernelGGL(seal_pattern_kernel<1>, grid, block, 0, s, buf, h, n, nbad);
+      if (v == 140) hipLaunchKernelGGL(seal_pattern_kernel<0>, grid, block, 0, s, buf, h, n, nbad, buf_len);
+      else if (v == 141) hipLaunchKernelGGL(seal_pattern_kernel<1>, grid, block, 0, s, buf, h, n, nbad, buf_len);
+      else if (v == 142) hipLaunchKernelGGL(seal_pattern_kernel<2>, grid, block, 0, s, buf, h, n, nbad, buf_len);
+      else hipLaunchKernelGGL(seal_pattern_kernel<3>, grid, block, 0, s, buf, h, n, nbad, buf_len);
       return hipGetLastError();
     case 72:  // the seal with each group's trailers written when hashed (no parking): the reference
               // image of the parked-trailer product seal (tests/test_sst4k.py)
