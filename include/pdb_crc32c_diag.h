@@ -35,7 +35,7 @@ int pdb_diag_read_stream(const void* d_base, uint64_t nbytes, uint32_t* d_out, v
 int pdb_diag_read_pattern4k(const void* d_base, uint64_t nblk, int variant, uint32_t* d_out, void* stream);
 
 /* Variants of the batch entry points (same arguments as the product's; ids in diag_variants.hip:
- * fixed 0 / 16, desc 0 / 16 / 161 / 63 / 64 / 67 / 125 / 126 / 127-133 / 180-182, sst 0 / 18 / 72 / 140 / 141 / 142 / 143). */
+ * fixed 0 / 16, desc 0 / 16 / 161 / 63 / 64 / 67 / 125 / 126 / 127-134 / 180-182, sst 0 / 18 / 72 / 140 / 141 / 142 / 143). */
 int pdb_diag_batch_fixed(int variant, const void* d_base, uint64_t stride, uint32_t len, uint64_t nblk,
                          uint32_t flags, uint32_t init, uint32_t* d_out, void* stream);
 int pdb_diag_batch_desc(int variant, const void* d_base, const pdb_blk* d_blk, uint64_t nblk, uint32_t flags,

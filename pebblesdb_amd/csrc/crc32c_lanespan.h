@@ -28,8 +28,8 @@
 // consecutive records whose span fits a region, each record on k lanes: see "items" below).  The
 // next item's loads are in flight while one is hashed.  Per lane, a record part is a run of the
 // region's dwords counted from the record's last one (whose bytes past the record are masked; the
-// finishing step then shifts by the record bytes it holds) and hashed as four interleaved slice-by-4
-// chains; the dword holding the record's first byte p is masked below p and injects U[z] (z masked
+// finishing step then shifts by the record bytes it holds) and hashed as two interleaved slice-by-4
+// chains (four until round 5); the dword holding the record's first byte p is masked below p and injects U[z] (z masked
 // bytes: the state entering the record is Value()'s 0xFFFFFFFF), and it REPLACES the state of its
 // chain, so no word before it needs masking.  Records outside the class (0 B, > MAXN)
 // are hashed by the whole wave when their batch is opened (slow path: global loads, the same
@@ -159,6 +159,19 @@ struct TabsS4 {
 #pragma unroll
     for (uint32_t c = 0; c < 3; ++c) x[c] = xor3(xor3(v[4 * c], v[4 * c + 1], v[4 * c + 2]), v[4 * c + 3], w[c]);
   }
+  // two chains stepped together (diagnostics MODE 51: a part as two chains): 8 lookups issued together
+  __device__ static __forceinline__ void step2(const char* lds, const LT& lt, uint32_t (&x)[2], const uint32_t (&w)[2]) {
+    uint32_t a[8], v[8];
+#pragma unroll
+    for (uint32_t c = 0; c < 2; ++c)
+#pragma unroll
+      for (uint32_t i = 0; i < 4; ++i) a[4 * c + i] = __builtin_amdgcn_perm(lt.t[i], x[c], lt.s[i]);
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) v[j] = lds_u32(lds, a[j]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (uint32_t c = 0; c < 2; ++c) x[c] = xor3(xor3(v[4 * c], v[4 * c + 1], v[4 * c + 2]), v[4 * c + 3], w[c]);
+  }
   __device__ static __forceinline__ void stage(char* lds, const uint32_t* __restrict__ tabs) {
     // T0..T3 x 8 replicas: 256 entries x 4 tables x 2 quads of 16 B; quad i at b<<8 | k<<5 | h<<4
     for (uint32_t i = threadIdx.x; i < 2048u; i += blockDim.x) {
@@ -250,16 +263,17 @@ __device__ __forceinline__ uint32_t span_slow_record(const char* lds, const type
 // A batch is 64 consecutive records (lane r of the batch registers: record 64 * batch + r).  Its
 // in-class records are hashed by items: runs of up to G = floor(64 / k) consecutive records, each
 // record on k consecutive lanes (lane u: record slot u / k, part c = u % k).  Counted from the
-// record's END, part c covers P = kPart words ending 4 P c bytes before the end, as four chains:
-// A its last LC = 8 words, B and C the 8 before each, D the LD before those; part k - 1's chain D
-// (the head) also runs on to the record's start.  Odd parts put the k lanes of a record on k
-// different LDS banks at every step (128-B parts would put them all on one).  The chains of an
-// item run in lock step: the head chain alone for lim = max(0, nw - P (k - 1) - 3 LC - LD) steps,
-// then NI = max(LC, LD) steps in which chain X works from step NI - len(X) on (the first word of A,
-// B, C is just loaded: their states start at 0).  Folds: per lane Q = shift(shift(D, 32) ^ C, 64)
-// ^ shift(B, 32) ^ A (D ends where C starts, whatever its length), then across the k lanes of a
-// record shift(Q[c + m], 4 P m) ^ Q[c] for m = 1, 2, 4.  k per batch minimises steps per batch for
-// its longest in-class record.
+// record's END, part c covers P = kPart words ending 4 P c bytes before the end, as two chains:
+// upper its last 2 LC = 16 words, lower the LC + LD before them; part k - 1's lower chain (the head)
+// also runs on to the record's start.  Odd parts put the k lanes of a record on k different LDS
+// banks at every step (128-B parts would put them all on one).  The chains of an item run in lock
+// step: the head chain alone for lim = max(0, nw - P (k - 1) - 3 LC - LD) steps, then N2 =
+// max(2 LC, LC + LD) steps in which a chain works from step N2 - len on (the upper chain's first
+// word is just loaded: its state starts at 0).  Folds: per lane Q = shift(lower, 64) ^ upper, then
+// across the k lanes of a record shift(Q[c + m], 4 P m) ^ Q[c] for m = 1, 2, 4.  (Round 5 hashed a
+// part as four chains A, B, C of LC words and D of LD, folded as shift(shift(D, 32) ^ C, 64) ^
+// shift(B, 32) ^ A: three operator applications per lane instead of one; MODE 52 keeps that form.)
+// k per batch minimises steps per batch for its longest in-class record.
 constexpr uint32_t kNoRec = 0x3FFFFFFFu;
 
 struct LaneSpanGeom {
@@ -305,19 +319,19 @@ __device__ __forceinline__ uint32_t wave_incl_add_u32(uint32_t v, uint32_t u) {
 // k for a batch whose longest in-class record has nw words: the fewest chain steps per batch,
 // items per batch x steps per item, with the records an item can hold: G = floor(64 / k), and
 // what fits a staging region at ~4 nw + 8 bytes a record
-template <uint32_t KMAX, class ST>
+template <uint32_t KMAX, class ST, uint32_t kNIx = ST::kNI>
 __device__ __forceinline__ LaneSpanGeom span_pick(uint32_t nw) {
   const float fit = static_cast<float>(ST::kUsable) * __builtin_amdgcn_rcpf(static_cast<float>(4u * nw + 8u));
   uint32_t gfit = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(fit)));
   gfit = gfit ? gfit : 1u;
-  LaneSpanGeom best{1u, 64u, 65536u, ST::kNI};
+  LaneSpanGeom best{1u, 64u, 65536u, kNIx};
   uint32_t best_cost = ~0u;
 #pragma unroll
   for (uint32_t k = 1; k <= KMAX; ++k) {
     const uint32_t g = 64u / k;
     const uint32_t geff = g < gfit ? g : gfit;
     const int32_t h = static_cast<int32_t>(nw) - static_cast<int32_t>((k - 1u) * ST::kPart + 3u * ST::kLC + ST::kLD);
-    const uint32_t it = ST::kNI + (h > 0 ? static_cast<uint32_t>(h) : 0u);  // lim + NI
+    const uint32_t it = kNIx + (h > 0 ? static_cast<uint32_t>(h) : 0u);  // lim + NI
     const uint32_t items = (64u + geff - 1u) / geff;
     if (items * it < best_cost) {
       best = LaneSpanGeom{k, g, (65536u + k - 1u) / k, it};
@@ -346,7 +360,7 @@ struct SpanItem {
 // bookkeeping alone); 17 the batch-uniform k only (no per-record lanes for mixed sizes); 18 the
 // item geometry instead of the CRC (first record << 24 | records << 16 | lane << 8 | lanes << 4 |
 // per-record mode); 40 / 41 / 42 = 0 / 1 / 2 with per-wave clock stamps (a Sink with a `stamps`
-// array).  The
+// array); 52 the four-chain parts of round 5 (exact), also the form the pricing modes 43-48 price.  The
 // round-2..4 A/B forms that lost are recorded in DESIGN.md's appendix and were removed in round 5.
 // TP: the table scheme.
 // kDyn: false = static batches wv + k W (diagnostics).
@@ -358,6 +372,16 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
   constexpr uint32_t kSpanRegion = SpanStage<MAXN>::kRegion, kSpanUsable = SpanStage<MAXN>::kUsable;
   typedef SpanStage<MAXN> ST;
   constexpr uint32_t LC = ST::kLC, LD = ST::kLD, NI = ST::kNI, PART = ST::kPart;
+  // A part as TWO chains (round 6): upper = its last 2 LC words, lower = the LC + LD before them (the
+  // head chain), folded by ONE shift-64 operator instead of the three of four chains (A..D: S32, S32,
+  // S64 -- value-dependent, bank-conflicted single-copy operator lookups), in N2 lock-step steps
+  // instead of NI with 8 lookups in flight per step instead of 16: +0.3 / +0.8 / +1.9 / +0.3 % on
+  // wal100 / wal400 / wal1000 / wal, +0.5 / +1.3 % on random 300-500- / 64-1000-B records, both orders
+  // (tools/ab_span.py, profiles/r06/two_chains/).  MODE 52 (diagnostics, exact) keeps the four-chain
+  // form; the pricing modes 43-48 price that form.
+  constexpr bool k2 = MODE != 52 && !(MODE >= 43 && MODE <= 48);
+  constexpr uint32_t N2 = 2u * LC > LC + LD ? 2u * LC : LC + LD;
+  constexpr uint32_t NIH = k2 ? N2 : NI;  // lock-step steps of a part in this mode
   static_assert(MAXN + 32u <= kSpanUsable, "a record of the class must fit a region");
   // k parts cover MAXN: 2, 5, 8 (a longer class -- diagnostics 1152 -- stays at 8 lanes and runs
   // the head chain alone for the rest)
@@ -458,9 +482,9 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
   bool bvar = false;     // mixed sizes: record r on bkr lanes (not the batch-uniform k)
   uint32_t bkw = 0;      // per lane: the record's lanes kr = ceil(words / PART) <= KMAX (bits 0-3; 0: not in
                          // the class) | the inclusive prefix sum of kr over the batch (bits 4..)
-  uint32_t bkmax = 1, biters_v = NI;
+  uint32_t bkmax = 1, biters_v = NIH;
   uint32_t bcursor = 64;
-  LaneSpanGeom bg{1u, 64u, 65536u, NI};
+  LaneSpanGeom bg{1u, 64u, 65536u, NIH};
 
   // make the prefetched batch current; records outside the class are hashed here by the whole
   // wave (rare: their loads wait behind the items in flight)
@@ -500,7 +524,7 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
     // either way): nw = dwords of [p, p + n) on the grid - 1 <= ceil(n / 4)
     const uint32_t nwl = ((plo & 3u) + bn + 3u) >> 2;
     const uint32_t nw = wave_max_u32(bfast ? (nwl > 1u ? nwl - 1u : 1u) : 0u);
-    bg = span_pick<KMAX, ST>(nw ? nw : 1u);
+    bg = span_pick<KMAX, ST, NIH>(nw ? nw : 1u);
     bcursor = 0;
     // Mixed sizes: the batch-uniform k is set by the longest record, so a short record's lanes
     // would hash padding.  Per-record lanes instead: record r on kr = ceil(words / PART) lanes
@@ -524,7 +548,7 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
         bkw = bkr | (bks << 4);
         const uint32_t sumk = __builtin_amdgcn_readlane(bks, 63);
         const uint32_t limr = bfast && nwr > bkr * PART ? nwr - bkr * PART : 0u;
-        const uint32_t iv = NI + wave_max_u32(limr);
+        const uint32_t iv = NIH + wave_max_u32(limr);
         const uint32_t f0 = static_cast<uint32_t>(__builtin_ctzll(bfastm)), f1 = 63u - static_cast<uint32_t>(__builtin_clzll(bfastm));
         const uint32_t span = (__builtin_amdgcn_readlane(plo, f1) + __builtin_amdgcn_readlane(bn, f1)) -
                               (__builtin_amdgcn_readlane(plo, f0) & ~15u);
@@ -723,7 +747,7 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
     // chain X (A, B, C, D = 0..3) works from lock-step step F[X] on; its word at step t is the one
     // ending 4 (NI - t) bytes before the chain's end
     constexpr int32_t FABC = static_cast<int32_t>(NI - LC), FD = static_cast<int32_t>(NI - LD);
-    const uint32_t k = it.k, lim = it.iters - NI;
+    const uint32_t k = it.k, lim = it.iters - NIH;
     const int32_t e = static_cast<int32_t>(it.e_loc);
     const int32_t pl = static_cast<int32_t>(it.p_loc);
     const bool act = it.p_loc != kNoRec;
@@ -748,102 +772,7 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
     const uint32_t pw = (lds_u32(region + sp, 0) & (0xFFFFFFFFu << (8u * zp)) & (sp == eg - 4 ? endm : 0xFFFFFFFFu)) ^ uz;
     // the last word of chain A on part 0 (the record's last dword) keeps the record's bytes only
     const uint32_t lastm = pc == 0 ? endm : 0xFFFFFFFFu;
-    // the p-word's lock-step step in chain A's numbering; T + LC X in chain X's
-    const int32_t T = static_cast<int32_t>(NI) - ((eA - sp) >> 2);
-    // base of the chains' words: chain X's dword i at q3 + 4 LC (3 - X) + 4 i (word at step t =
-    // dword t); below the region for short records (words never used)
-    const int32_t qd = (eA - static_cast<int32_t>(4u * NI + 12u * LC)) >> 2;  // q3's dword (region-relative)
-    const char* q3 = region + 4 * qd;
-    // the chains' reads are addressed as lds + qo + constant with qo opaque to the compiler, so every
-    // read takes its constant in the instruction's offset field (left to itself the compiler re-bases
-    // them on the highest address and computes each negative offset with a VALU; +1.9-2.1 % on
-    // wal400 / wal1000 / wal in A/B, profiles/r04/ab_variants_r04d.log)
-    uint32_t qo = static_cast<uint32_t>(region - lds) + static_cast<uint32_t>(4 * qd);
-    asm volatile("" : "+v"(qo));
-    auto sread = [&](uint32_t off) -> uint32_t { return lds_u32(lds, qo + off); };
-    // The p-word may also be the dword just before the head lane's first word (the lanes cover the
-    // record's dwords after its p-word: span_pick counts those): the head chain then starts from it.
-    uint32_t xd = 0;
-    uint32_t xa = 0, xb = 0, xc = 0;
-    if (lim > 0) {  // the head chain alone (junk on the other lanes, dropped)
-      const int32_t tD = T + static_cast<int32_t>(3u * LC + lim) - FD;  // the p-word's step in it
-      const char* q = q3 + 4 * (FD - static_cast<int32_t>(lim));
-      xd = tD == -1 ? pw : 0u;
-      for (int32_t t = 0; t < static_cast<int32_t>(lim); ++t, q += 4) {
-        const uint32_t w = lds_u32(q, 0);
-        xd = t == tD ? pw : TP::step(lds, lt, xd, w);
-      }
-      xd = head ? xd : 0u;
-    } else {
-      xd = head && T + static_cast<int32_t>(3u * LC) == FD - 1 ? pw : 0u;
-    }
-    // The chains' words: one ds_read_b32 per word and chain.  (Aligned ds_read_b64 pairs measured
-    // 2.5-9 % slower on every WAL row, profiles/r04/ab_pairs.log: the extra live pair registers and
-    // selects.)
-    // (diagnostics, wrong CRCs by design: MODE 48 prices the chains' words as 16-B reads, one per
-    // four words of a chain, at the 16-B-aligned addresses below them)
-    const uint32_t qo16 = qo & ~15u;
-    u32x4 qa4{}, qb4{}, qc4{}, qd4{};
-    auto sread4 = [&](uint32_t off) -> u32x4 { return *reinterpret_cast<const u32x4*>(lds + qo16 + off); };
-#pragma unroll
-    for (int32_t t = 0; t < static_cast<int32_t>(NI); ++t) {
-      const bool abc = t >= FABC, dd = t >= FD;  // compile time
-      uint32_t wa = 0, wb = 0, wc = 0, wd = 0;
-      if constexpr (MODE == 48) {
-        if (abc) {
-          const uint32_t r = static_cast<uint32_t>(t - FABC);
-          if ((r & 3u) == 0) qa4 = sread4(12u * LC + 4u * r), qb4 = sread4(8u * LC + 4u * r), qc4 = sread4(4u * LC + 4u * r);
-          wa = qa4[r & 3u], wb = qb4[r & 3u], wc = qc4[r & 3u];
-        }
-        if (dd) {
-          const uint32_t r = static_cast<uint32_t>(t - FD);
-          if ((r & 3u) == 0) qd4 = sread4(4u * r);
-          wd = qd4[r & 3u];
-        }
-      } else {
-        if (abc) {
-          wa = sread(12u * LC + 4u * t), wb = sread(8u * LC + 4u * t), wc = sread(4u * LC + 4u * t);
-          if (t == static_cast<int32_t>(NI) - 1) wa &= lastm;
-        }
-        if (dd) wd = sread(4u * t);
-      }
-      if (abc && t == FABC) {  // the first word: the state is 0
-        xa = wa, xb = wb, xc = wc;
-        if (dd) xd = TP::step(lds, lt, xd, wd);
-      } else if (abc && dd) {
-        uint32_t x4[4] = {xa, xb, xc, xd};
-        const uint32_t w4[4] = {wa, wb, wc, wd};
-        TP::step4(lds, lt, x4, w4);
-        xa = x4[0], xb = x4[1], xc = x4[2], xd = x4[3];
-      } else if (abc) {
-        uint32_t x3[3] = {xa, xb, xc};
-        const uint32_t w3[3] = {wa, wb, wc};
-        TP::step3(lds, lt, x3, w3);
-        xa = x3[0], xb = x3[1], xc = x3[2];
-      } else if (dd) {
-        xd = TP::step(lds, lt, xd, wd);
-      }
-      // the p-word replaces its chain's state: branch-free selects on every step (+0.1-3 % over
-      // selects bounded by the item's last replacement step, profiles/r04/ab/ab_nog.log)
-      if (abc) {
-        xa = T == t ? pw : xa;
-        xb = T + static_cast<int32_t>(LC) == t ? pw : xb;
-        xc = T + static_cast<int32_t>(2u * LC) == t ? pw : xc;
-      }
-      if (dd) xd = T + static_cast<int32_t>(3u * LC) == t ? pw : xd;
-    }
-    // Finish.  Chain X's state still holds its last word unshifted, and its bytes end 32 X bytes
-    // before the part's end, so the part's raw CRC is F(xA) ^ S32 F(xB) ^ S64 F(xC) ^ S96 F(xD)
-    // with F = the table step (shift 4) and S_n = shift n; these maps commute, so it is
-    // F(S64(S32(xD) ^ xC) ^ (S32(xB) ^ xA)), and across the k parts of a record
-    // F(sum_c S_{4 PART c}(R_c)): ONE table step after the cross-lane fold.
-    // A chain whose end is at or before the p-word's start holds no byte of the record.
-    const int32_t L = static_cast<int32_t>(NI);
-    const uint32_t ca = T < L ? xa : 0u;
-    const uint32_t cb = T + static_cast<int32_t>(LC) < L ? xb : 0u;
-    const uint32_t cc = T + static_cast<int32_t>(2u * LC) < L ? xc : 0u;
-    const uint32_t cd = T + static_cast<int32_t>(3u * LC) < L ? xd : 0u;
-    static_assert(LC == 8, "the in-part folds use the 32- and 64-B operators");
+    uint32_t P = 0, ca = 0, cb = 0, cc = 0, cd = 0;
     // (diagnostics, wrong CRCs by design: MODE 43 prices the folds' operator lookups as free, MODE 44
     // as 8 conflict-free lookups each, MODE 45 with no dependence between them (each indexed by
     // chain states, `alt`), MODE 46 the cross-lane operators alone as free)
@@ -854,9 +783,158 @@ __global__ __launch_bounds__((SpanStage<MAXN>::kWaves * 64)) void crc_lanespan_k
       if constexpr (MODE == 46) if (slot != kOp32 && slot != kOp64) return c ^ y;
       return span_op_x(lds, slot, c, y);
     };
-    const uint32_t lo2 = fold_op(kOp32, cb, ca, cb);  // S32(B) ^ A
-    const uint32_t hi2 = fold_op(kOp32, cd, cc, cd);  // S32(D) ^ C
-    uint32_t P = fold_op(kOp64, hi2, lo2, ca ^ cc);  // S64(hi2) ^ lo2
+    if constexpr (k2) {
+      // two chains: lower word t at dword qd2 + t (t >= FL: C and D, the head chain), upper word t at
+      // qd2 + 2 LC + t (t >= FU: B and A), the upper ending at the part's end eA
+      constexpr int32_t FU = static_cast<int32_t>(N2 - 2u * LC), FL = static_cast<int32_t>(N2 - LC - LD);
+      const int32_t Tu = static_cast<int32_t>(N2) - ((eA - sp) >> 2);  // the p-word's step, upper numbering
+      const int32_t Tl = Tu + static_cast<int32_t>(2u * LC);             // and lower numbering
+      const int32_t qd2 = (eA - static_cast<int32_t>(4u * N2 + 8u * LC)) >> 2;
+      uint32_t qo2 = static_cast<uint32_t>(region - lds) + static_cast<uint32_t>(4 * qd2);
+      asm volatile("" : "+v"(qo2));
+      auto sread2 = [&](uint32_t off) -> uint32_t { return lds_u32(lds, qo2 + off); };
+      uint32_t xl = 0, xu = 0;
+      if (lim > 0) {  // the head chain alone (junk on the other lanes, dropped)
+        const int32_t tL = Tl - FL + static_cast<int32_t>(lim);  // the p-word's step in it
+        const char* q = region + 4 * (qd2 + FL - static_cast<int32_t>(lim));
+        xl = tL == -1 ? pw : 0u;
+        for (int32_t t = 0; t < static_cast<int32_t>(lim); ++t, q += 4) {
+          const uint32_t w = lds_u32(q, 0);
+          xl = t == tL ? pw : TP::step(lds, lt, xl, w);
+        }
+        xl = head ? xl : 0u;
+      } else {
+        xl = head && Tl == FL - 1 ? pw : 0u;
+      }
+#pragma unroll
+      for (int32_t t = 0; t < static_cast<int32_t>(N2); ++t) {
+        const bool uu = t >= FU, ll = t >= FL;  // compile time
+        uint32_t wu = 0, wl = 0;
+        if (uu) {
+          wu = sread2(8u * LC + 4u * t);
+          if (t == static_cast<int32_t>(N2) - 1) wu &= lastm;
+        }
+        if (ll) wl = sread2(4u * t);
+        if (uu && t == FU) {  // the upper chain's first word: the state is 0
+          xu = wu;
+          if (ll) xl = TP::step(lds, lt, xl, wl);
+        } else if (uu && ll) {
+          uint32_t x2[2] = {xu, xl};
+          const uint32_t w2[2] = {wu, wl};
+          TP::step2(lds, lt, x2, w2);
+          xu = x2[0], xl = x2[1];
+        } else if (uu) {
+          xu = TP::step(lds, lt, xu, wu);
+        } else if (ll) {
+          xl = TP::step(lds, lt, xl, wl);
+        }
+        if (uu) xu = Tu == t ? pw : xu;
+        if (ll) xl = Tl == t ? pw : xl;
+      }
+      const uint32_t cu = Tu < static_cast<int32_t>(N2) ? xu : 0u;
+      const uint32_t cl = Tl < static_cast<int32_t>(N2) ? xl : 0u;
+      P = span_op_x(lds, kOp64, cl, cu);  // S64(lower) ^ upper
+    } else {
+      // the p-word's lock-step step in chain A's numbering; T + LC X in chain X's
+      const int32_t T = static_cast<int32_t>(NI) - ((eA - sp) >> 2);
+      // base of the chains' words: chain X's dword i at q3 + 4 LC (3 - X) + 4 i (word at step t =
+      // dword t); below the region for short records (words never used)
+      const int32_t qd = (eA - static_cast<int32_t>(4u * NI + 12u * LC)) >> 2;  // q3's dword (region-relative)
+      const char* q3 = region + 4 * qd;
+      // the chains' reads are addressed as lds + qo + constant with qo opaque to the compiler, so every
+      // read takes its constant in the instruction's offset field (left to itself the compiler re-bases
+      // them on the highest address and computes each negative offset with a VALU; +1.9-2.1 % on
+      // wal400 / wal1000 / wal in A/B, profiles/r04/ab_variants_r04d.log)
+      uint32_t qo = static_cast<uint32_t>(region - lds) + static_cast<uint32_t>(4 * qd);
+      asm volatile("" : "+v"(qo));
+      auto sread = [&](uint32_t off) -> uint32_t { return lds_u32(lds, qo + off); };
+      // The p-word may also be the dword just before the head lane's first word (the lanes cover the
+      // record's dwords after its p-word: span_pick counts those): the head chain then starts from it.
+      uint32_t xd = 0;
+      uint32_t xa = 0, xb = 0, xc = 0;
+      if (lim > 0) {  // the head chain alone (junk on the other lanes, dropped)
+        const int32_t tD = T + static_cast<int32_t>(3u * LC + lim) - FD;  // the p-word's step in it
+        const char* q = q3 + 4 * (FD - static_cast<int32_t>(lim));
+        xd = tD == -1 ? pw : 0u;
+        for (int32_t t = 0; t < static_cast<int32_t>(lim); ++t, q += 4) {
+          const uint32_t w = lds_u32(q, 0);
+          xd = t == tD ? pw : TP::step(lds, lt, xd, w);
+        }
+        xd = head ? xd : 0u;
+      } else {
+        xd = head && T + static_cast<int32_t>(3u * LC) == FD - 1 ? pw : 0u;
+      }
+      // The chains' words: one ds_read_b32 per word and chain.  (Aligned ds_read_b64 pairs measured
+      // 2.5-9 % slower on every WAL row, profiles/r04/ab_pairs.log: the extra live pair registers and
+      // selects.)
+      // (diagnostics, wrong CRCs by design: MODE 48 prices the chains' words as 16-B reads, one per
+      // four words of a chain, at the 16-B-aligned addresses below them)
+      const uint32_t qo16 = qo & ~15u;
+      u32x4 qa4{}, qb4{}, qc4{}, qd4{};
+      auto sread4 = [&](uint32_t off) -> u32x4 { return *reinterpret_cast<const u32x4*>(lds + qo16 + off); };
+  #pragma unroll
+      for (int32_t t = 0; t < static_cast<int32_t>(NI); ++t) {
+        const bool abc = t >= FABC, dd = t >= FD;  // compile time
+        uint32_t wa = 0, wb = 0, wc = 0, wd = 0;
+        if constexpr (MODE == 48) {
+          if (abc) {
+            const uint32_t r = static_cast<uint32_t>(t - FABC);
+            if ((r & 3u) == 0) qa4 = sread4(12u * LC + 4u * r), qb4 = sread4(8u * LC + 4u * r), qc4 = sread4(4u * LC + 4u * r);
+            wa = qa4[r & 3u], wb = qb4[r & 3u], wc = qc4[r & 3u];
+          }
+          if (dd) {
+            const uint32_t r = static_cast<uint32_t>(t - FD);
+            if ((r & 3u) == 0) qd4 = sread4(4u * r);
+            wd = qd4[r & 3u];
+          }
+        } else {
+          if (abc) {
+            wa = sread(12u * LC + 4u * t), wb = sread(8u * LC + 4u * t), wc = sread(4u * LC + 4u * t);
+            if (t == static_cast<int32_t>(NI) - 1) wa &= lastm;
+          }
+          if (dd) wd = sread(4u * t);
+        }
+        if (abc && t == FABC) {  // the first word: the state is 0
+          xa = wa, xb = wb, xc = wc;
+          if (dd) xd = TP::step(lds, lt, xd, wd);
+        } else if (abc && dd) {
+          uint32_t x4[4] = {xa, xb, xc, xd};
+          const uint32_t w4[4] = {wa, wb, wc, wd};
+          TP::step4(lds, lt, x4, w4);
+          xa = x4[0], xb = x4[1], xc = x4[2], xd = x4[3];
+        } else if (abc) {
+          uint32_t x3[3] = {xa, xb, xc};
+          const uint32_t w3[3] = {wa, wb, wc};
+          TP::step3(lds, lt, x3, w3);
+          xa = x3[0], xb = x3[1], xc = x3[2];
+        } else if (dd) {
+          xd = TP::step(lds, lt, xd, wd);
+        }
+        // the p-word replaces its chain's state: branch-free selects on every step (+0.1-3 % over
+        // selects bounded by the item's last replacement step, profiles/r04/ab/ab_nog.log)
+        if (abc) {
+          xa = T == t ? pw : xa;
+          xb = T + static_cast<int32_t>(LC) == t ? pw : xb;
+          xc = T + static_cast<int32_t>(2u * LC) == t ? pw : xc;
+        }
+        if (dd) xd = T + static_cast<int32_t>(3u * LC) == t ? pw : xd;
+      }
+      // Finish.  Chain X's state still holds its last word unshifted, and its bytes end 32 X bytes
+      // before the part's end, so the part's raw CRC is F(xA) ^ S32 F(xB) ^ S64 F(xC) ^ S96 F(xD)
+      // with F = the table step (shift 4) and S_n = shift n; these maps commute, so it is
+      // F(S64(S32(xD) ^ xC) ^ (S32(xB) ^ xA)), and across the k parts of a record
+      // F(sum_c S_{4 PART c}(R_c)): ONE table step after the cross-lane fold.
+      // A chain whose end is at or before the p-word's start holds no byte of the record.
+      const int32_t L = static_cast<int32_t>(NI);
+      ca = T < L ? xa : 0u;
+      cb = T + static_cast<int32_t>(LC) < L ? xb : 0u;
+      cc = T + static_cast<int32_t>(2u * LC) < L ? xc : 0u;
+      cd = T + static_cast<int32_t>(3u * LC) < L ? xd : 0u;
+      static_assert(LC == 8, "the in-part folds use the 32- and 64-B operators");
+      const uint32_t lo2 = fold_op(kOp32, cb, ca, cb);  // S32(B) ^ A
+      const uint32_t hi2 = fold_op(kOp32, cd, cc, cd);  // S32(D) ^ C
+      P = fold_op(kOp64, hi2, lo2, ca ^ cc);  // S64(hi2) ^ lo2
+    }
     if (k > 1u) {
       // the cross-lane fold, pre-shifted per lane: lane c applies shift(R_c, 4 PART (c mod 4)) (slots
       // P1, P2, P3 chosen per lane), the record's quad XOR-reduces, and a record of > 4 parts adds

@@ -254,6 +254,8 @@ hipError_t launch_desc_variant(int v, const LaunchGeom& g, const uint32_t* d_tab
       return launch_lanespan<DescSrc, OutSink, 48>(g, d_tables, src, nblk, record_class(flags), sink, s, mixed);
     case 133:  // exact: the cross-lane pre-shift's lookups on the lanes that use them only (EXEC-masked)
       return launch_lanespan<DescSrc, OutSink, 49>(g, d_tables, src, nblk, record_class(flags), sink, s, mixed);
+    case 134:  // exact: each part hashed as four chains (three in-part folds: the round-5 form, MODE 52)
+      return launch_lanespan<DescSrc, OutSink, 52>(g, d_tables, src, nblk, record_class(flags), sink, s, mixed);
     case 125:  // exact: the batch-uniform k only (no per-record lanes for mixed sizes)
       return launch_lanespan<DescSrc, OutSink, 17>(g, d_tables, src, nblk, record_class(flags), sink, s, mixed);
     case 126:  // the item geometry per record instead of its CRC (MODE 18; tests/test_lanespan.py)

@@ -183,8 +183,10 @@ def test_mixed_geometry_items():
 
 
 # 125: the batch-uniform lane count only (no per-record lanes for mixed sizes); 133: the cross-lane
-# pre-shift's lookups EXEC-masked to the lanes that use them (profiles/r05/ab/ab_slot_lookups_masked.log)
-RECORD_VARIANTS = [125, 133]
+# pre-shift's lookups EXEC-masked to the lanes that use them (profiles/r05/ab/ab_slot_lookups_masked.log);
+# 134: each part hashed as four chains with three in-part folds (round 5's form, MODE 52; the product hashes
+# two chains since round 6)
+RECORD_VARIANTS = [125, 133, 134]
 
 
 @pytest.mark.parametrize("hint", ["256", "512", "512m", "1023", "1023m", "1k"])
